@@ -1,0 +1,153 @@
+/*
+ * sfhe.h -- C ABI of the MI355X CKKS rank-sort engine (drop-in boundary).
+ *
+ * The reference (oksuman/sorting-fhe) is C++ calling OpenFHE 1.1.4; it has
+ * no FFI of its own.  Its hot path is DirectSort<N>::sort and the lbcrypto
+ * calls beneath it.  Every entry point below replaces
+ * one of those reference interfaces (cited per function), with plain
+ * pointers, sizes and int status codes so any FFI (ctypes, cgo, JNI, N-API)
+ * can bind it.  C++ callers can instead use the lbcrypto-compatible headers
+ * in sorting-fhe_amd/csrc/core and csrc/algo, which wrap the same engine.
+ *
+ * Conventions: functions return SFHE_OK (0) or a negative SFHE_E* code;
+ * sfhe_last_error() gives the message (thread-local).  Objects returned
+ * through out-pointers are owned by the caller and released with the
+ * matching *_free / *_destroy.  A context and everything created from it
+ * must be used from one thread at a time (calls are internally serialised).
+ */
+#ifndef SFHE_H
+#define SFHE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SFHE_ABI_VERSION 1
+
+#define SFHE_OK 0
+#define SFHE_EINVAL (-1)   /* bad argument */
+#define SFHE_ESCHEME (-2)  /* CKKS error: depth exhausted, missing key, ... */
+#define SFHE_EDEVICE (-3)  /* device / backend failure */
+#define SFHE_ENOTIMPL (-4) /* valid request, not implemented */
+
+typedef struct sfhe_ctx sfhe_ctx;
+typedef struct sfhe_ct sfhe_ct;
+typedef struct sfhe_sorter sfhe_sorter;
+
+/* Security levels (lbcrypto::SecurityLevel). */
+#define SFHE_HESTD_128_CLASSIC 0
+#define SFHE_HESTD_NOTSET 3
+
+/* CCParams<CryptoContextCKKSRNS> (GenCryptoContext inputs; reference
+ * tests/DirectSortTest.cpp:29-37, sort_algo.h:87-201). */
+typedef struct {
+    uint32_t mult_depth;
+    uint32_t scaling_mod_size;  /* bits of the scaling primes (e.g. 40) */
+    uint32_t first_mod_size;    /* bits of q_0 (default 60) */
+    uint32_t batch_size;        /* default slot count; 0 = n/2 */
+    uint32_t ring_dim;          /* 0 = smallest secure */
+    int32_t security_level;     /* SFHE_HESTD_* */
+    uint32_t num_large_digits;  /* HYBRID dnum; 0 = default (3) */
+    int32_t device;             /* HIP device ordinal */
+    uint64_t seed;              /* deterministic key / noise sampling */
+} sfhe_params;
+
+int sfhe_abi_version(void);
+const char* sfhe_last_error(void);
+/* "hip-gfx950" for the product library. */
+const char* sfhe_backend(void);
+void sfhe_params_default(sfhe_params* p);
+
+/* ---- context and keys ---------------------------------------------------
+ * Replaces GenCryptoContext + Enable(...) + KeyGen + EvalMultKeyGen
+ * (DirectSortTest.cpp:39-54) and EvalRotateKeyGen (:52). */
+int sfhe_context_create(const sfhe_params* p, sfhe_ctx** out);
+void sfhe_context_destroy(sfhe_ctx* c);
+int sfhe_keygen(sfhe_ctx* c);
+int sfhe_rotate_keygen(sfhe_ctx* c, const int32_t* idx, size_t count);
+/* ring_dim, mult_depth, #Q primes, #P primes, dnum (any pointer may be NULL) */
+int sfhe_context_info(sfhe_ctx* c, uint32_t* ring_dim, uint32_t* mult_depth, uint32_t* num_q,
+                      uint32_t* num_p, uint32_t* dnum);
+/* prime table [q_0..q_L, p_0..p_{K-1}] */
+int sfhe_context_primes(sfhe_ctx* c, uint64_t* out, size_t cap, size_t* count);
+/* Cache of encoded constant plaintexts (sort masks) across calls; default on. */
+int sfhe_set_plaintext_cache(sfhe_ctx* c, int on);
+/* Suppress the reference's stdout prints inside sort() (default off). */
+int sfhe_set_quiet(sfhe_ctx* c, int quiet);
+/* Block until queued device work is done; reports asynchronous errors. */
+int sfhe_sync(sfhe_ctx* c);
+/* counts[9]: keyswitch, rescale, tensor, ptmult, constmult, add, automorph,
+ * ntt_limbs, wsum_terms; bytes: algorithmic HBM bytes (SURVEY §8(d) model). */
+int sfhe_op_stats(sfhe_ctx* c, uint64_t* counts, double* bytes, int reset);
+
+/* ---- encryption ------------------------------------------------------------
+ * Replaces Encryption::encryptInput (encryption.cpp:5-12, MakeCKKSPacked-
+ * Plaintext + Encrypt) and DebugEncryption::getPlaintext / Decrypt
+ * (:14-33).  slots = 0 uses the batch size; level > 0 encrypts lower. */
+int sfhe_encrypt(sfhe_ctx* c, const double* values, size_t len, uint32_t slots, uint32_t level,
+                 sfhe_ct** out);
+/* writes min(cap, slots) real parts; *len = slots */
+int sfhe_decrypt(sfhe_ctx* c, const sfhe_ct* ct, double* out, size_t cap, size_t* len);
+void sfhe_ct_free(sfhe_ct* ct);
+int sfhe_ct_clone(const sfhe_ct* ct, sfhe_ct** out);
+/* Ciphertext::GetLevel / GetSlots / limb count */
+int sfhe_ct_info(const sfhe_ct* ct, uint32_t* level, uint32_t* slots, uint32_t* limbs);
+/* Ciphertext::SetSlots (metadata only) */
+int sfhe_ct_set_slots(sfhe_ct* ct, uint32_t slots);
+/* raw residues [c0 limbs][c1 limbs] (evaluation domain), 2*limbs*n words */
+int sfhe_ct_download(sfhe_ctx* c, const sfhe_ct* ct, uint64_t* out, size_t cap_words);
+
+/* ---- evaluation (CryptoContextImpl::Eval*, as called on the hot path) ---- */
+int sfhe_eval_add(sfhe_ctx* c, const sfhe_ct* a, const sfhe_ct* b, sfhe_ct** out);
+int sfhe_eval_sub(sfhe_ctx* c, const sfhe_ct* a, const sfhe_ct* b, sfhe_ct** out);
+int sfhe_eval_add_const(sfhe_ctx* c, const sfhe_ct* a, double k, sfhe_ct** out);
+int sfhe_eval_mult_const(sfhe_ctx* c, const sfhe_ct* a, double k, sfhe_ct** out);
+/* EvalMult(ct, pt): pt = encode(values, slots) at a's level */
+int sfhe_eval_mult_plain(sfhe_ctx* c, const sfhe_ct* a, const double* values, size_t len,
+                         uint32_t slots, sfhe_ct** out);
+/* EvalMultAndRelinearize / EvalMult(ct, ct) (sign.cpp:23-33) */
+int sfhe_eval_mult(sfhe_ctx* c, const sfhe_ct* a, const sfhe_ct* b, sfhe_ct** out);
+/* EvalRotate (rotation.h:224) */
+int sfhe_eval_rotate(sfhe_ctx* c, const sfhe_ct* a, int32_t r, sfhe_ct** out);
+/* EvalChebyshevSeriesPS (sort_algo.h:727-728, sign.cpp:76); c0/2 convention */
+int sfhe_eval_chebyshev(sfhe_ctx* c, const sfhe_ct* x, const double* coeffs, size_t count,
+                        double a, double b, sfhe_ct** out);
+
+/* ---- hot path ----------------------------------------------------------------
+ * sign(x, cc, CompositeSign, SignConfig(CompositeSignConfig(n, dg, df)))
+ * (sign.cpp:635-651; n in {3, 4}). */
+int sfhe_sign(sfhe_ctx* c, const sfhe_ct* x, int n, int dg, int df, sfhe_ct** out);
+/* Comparison::compare (comparison.cpp:4-22): (sign(a-b)+1)/2 */
+int sfhe_compare(sfhe_ctx* c, const sfhe_ct* a, const sfhe_ct* b, int n, int dg, int df,
+                 sfhe_ct** out);
+/* DirectSort<N>::getSizeParameters (sort_algo.h:87-201): depth and rotation
+ * keys for N in {4, 8, ..., 1024}. */
+int sfhe_direct_sort_params(uint32_t N, uint32_t* mult_depth, int32_t* rotations, size_t cap,
+                            size_t* count);
+/* Doubled-sinc Chebyshev table (generated_doubled_sinc_coeffs.h). */
+int sfhe_doubled_sinc_coeffs(uint32_t N, double* out, size_t cap, size_t* count);
+/* DirectSort<N> construction (sort_algo.h:74-81; encrypts the zero cache).
+ * debug != 0 uses DebugEncryption, so sort() runs the reference's three
+ * PRINT_PT decrypts ("as-test" timing); 0 = plain Encryption ("pure"). */
+int sfhe_sorter_create(sfhe_ctx* c, uint32_t N, int debug, sfhe_sorter** out);
+void sfhe_sorter_destroy(sfhe_sorter* s);
+/* DirectSort<N>::sort (sort_algo.h:752-774).  Sets the input's slots to
+ * the partition size as the reference does (sort_algo.h:711). */
+int sfhe_sorter_sort(sfhe_sorter* s, sfhe_ct* in, int n, int dg, int df, sfhe_ct** out);
+/* DirectSort<N>::constructRank (sort_algo.h:368-506) */
+int sfhe_sorter_rank(sfhe_sorter* s, const sfhe_ct* in, int n, int dg, int df, sfhe_ct** out);
+/* DirectSort<N>::rotationIndexCheckN (sort_algo.h:658-750) */
+int sfhe_sorter_place(sfhe_sorter* s, const sfhe_ct* rank, sfhe_ct* in, sfhe_ct** out);
+
+/* Decomposer<N>::decompose (rotation.h:54-102); algo 0 NAF, 1 BNAF, 2 BINARY.
+ * N in {4..1024}; writes (value, stepSize) pairs. */
+int sfhe_decompose(uint32_t N, const int32_t* keys, size_t nkeys, int32_t rotation, int32_t wrapN,
+                   int algo, int32_t* values, int32_t* steps, size_t cap, size_t* count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SFHE_H */

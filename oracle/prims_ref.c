@@ -1,0 +1,403 @@
+/*
+ * ORACLE -- test infrastructure only.  Never linked into the product.
+ *
+ * Plain-C restatement of the RNS-CKKS polynomial primitives of
+ * sorting-fhe_amd/csrc/prims.h.  The reference (oksuman/sorting-fhe) takes
+ * these from OpenFHE 1.1.4, which is an external dependency absent from
+ * /root/reference; the algorithms restated here are the
+ * published ones OpenFHE implements:
+ *   - negacyclic NTT, Cooley-Tukey forward / Gentleman-Sande inverse with
+ *     bit-reversed psi powers (Longa-Naehrig 2016, Alg. 1/2);
+ *   - automorphism X -> X^g as an index permutation of evaluation points;
+ *   - HYBRID key switching (Han-Ki 2020): ModUp by fast base conversion,
+ *     digit inner product, ModDown by P;
+ *   - rescale by the last prime with rounding.
+ * Modular products use exact 128-bit '%' (independent of the product's
+ * Barrett/Shoup code), so a bit-exact match with the HIP backend is a real
+ * cross-check.  Limb loops are OpenMP-parallel (the CPU baseline).
+ *
+ * The host CKKS layer (csrc/core) compiled against this file gives the
+ * oracle library oracle/_build/libsfhe_oracle.so (see oracle/Makefile).
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../sorting-fhe_amd/csrc/prims.h"
+
+typedef uint64_t u64;
+typedef unsigned __int128 u128;
+
+struct sfp_dev {
+    uint32_t n, logn, np;
+    u64* q;
+    u64 *psi, *psiS, *ipsi, *ipsiS;
+    u64 *ninv, *ninvS;
+};
+
+struct sfp_conv {
+    uint32_t ns, nt;
+    uint32_t *src, *dst;
+    u64 *inv, *mod;
+};
+
+static inline u64 mm(u64 a, u64 b, u64 q) { return (u64)(((u128)a * b) % q); }
+static inline u64 ad(u64 a, u64 b, u64 q) { u64 r = a + b; return r >= q ? r - q : r; }
+static inline u64 sb(u64 a, u64 b, u64 q) { return a >= b ? a - b : a + q - b; }
+static inline u64 shoup(u64 a, u64 w, u64 wp, u64 q) {
+    u64 hi = (u64)(((u128)a * wp) >> 64);
+    u64 r = a * w - hi * q;
+    return r >= q ? r - q : r;
+}
+static inline uint32_t brev(uint32_t x, uint32_t bits) {
+    uint32_t r = 0;
+    for (uint32_t i = 0; i < bits; ++i) r |= ((x >> i) & 1u) << (bits - 1 - i);
+    return r;
+}
+static inline uint32_t pidx(sfp_limbs m, uint32_t i) { return i < m.split ? i : m.pbase + (i - m.split); }
+
+const char* sfp_backend_name(void) { return "oracle-c"; }
+
+sfp_dev* sfp_create(int device, const sfp_tables* t) {
+    (void)device;
+    sfp_dev* d = (sfp_dev*)calloc(1, sizeof(sfp_dev));
+    d->logn = t->logn;
+    d->n = 1u << t->logn;
+    d->np = t->nprimes;
+    size_t tn = (size_t)d->np * d->n;
+    d->q = (u64*)malloc(d->np * 8);
+    memcpy(d->q, t->primes, d->np * 8);
+    d->psi = (u64*)malloc(tn * 8);
+    d->ipsi = (u64*)malloc(tn * 8);
+    memcpy(d->psi, t->psi_rev, tn * 8);
+    memcpy(d->ipsi, t->ipsi_rev, tn * 8);
+    /* recompute the Shoup companions independently */
+    d->psiS = (u64*)malloc(tn * 8);
+    d->ipsiS = (u64*)malloc(tn * 8);
+    d->ninv = (u64*)malloc(d->np * 8);
+    d->ninvS = (u64*)malloc(d->np * 8);
+    for (uint32_t p = 0; p < d->np; ++p) {
+        u64 q = d->q[p];
+        for (uint32_t k = 0; k < d->n; ++k) {
+            size_t o = (size_t)p * d->n + k;
+            d->psiS[o] = (u64)(((u128)d->psi[o] << 64) / q);
+            d->ipsiS[o] = (u64)(((u128)d->ipsi[o] << 64) / q);
+        }
+        /* n^{-1} by Fermat */
+        u64 r = 1, a = d->n % q, e = q - 2;
+        while (e) { if (e & 1) r = mm(r, a, q); a = mm(a, a, q); e >>= 1; }
+        d->ninv[p] = r;
+        d->ninvS[p] = (u64)(((u128)r << 64) / q);
+    }
+    return d;
+}
+
+void sfp_destroy(sfp_dev* d) {
+    if (!d) return;
+    free(d->q); free(d->psi); free(d->ipsi); free(d->psiS); free(d->ipsiS);
+    free(d->ninv); free(d->ninvS);
+    free(d);
+}
+
+void* sfp_alloc(sfp_dev* d, size_t bytes) { (void)d; return malloc(bytes ? bytes : 8); }
+void sfp_free(sfp_dev* d, void* p) { (void)d; free(p); }
+void sfp_h2d(sfp_dev* d, void* dst, const void* src, size_t b) { (void)d; memcpy(dst, src, b); }
+void sfp_d2h(sfp_dev* d, void* dst, const void* src, size_t b) { (void)d; memcpy(dst, src, b); }
+void sfp_d2d(sfp_dev* d, void* dst, const void* src, size_t b) { (void)d; memmove(dst, src, b); }
+void sfp_zero(sfp_dev* d, void* dst, size_t b) { (void)d; memset(dst, 0, b); }
+void sfp_sync(sfp_dev* d) { (void)d; }
+const char* sfp_last_error(sfp_dev* d) { (void)d; return NULL; }
+
+/* ---- NTT ---- */
+static void ntt_fwd(const sfp_dev* d, u64* a, uint32_t p) {
+    const uint32_t n = d->n;
+    const u64 q = d->q[p];
+    const u64* w = d->psi + (size_t)p * n;
+    const u64* wp = d->psiS + (size_t)p * n;
+    uint32_t t = n;
+    for (uint32_t m = 1; m < n; m <<= 1) {
+        t >>= 1;
+        for (uint32_t i = 0; i < m; ++i) {
+            uint32_t j1 = 2 * i * t;
+            u64 S = w[m + i], Sp = wp[m + i];
+            for (uint32_t j = j1; j < j1 + t; ++j) {
+                u64 U = a[j], V = shoup(a[j + t], S, Sp, q);
+                a[j] = ad(U, V, q);
+                a[j + t] = sb(U, V, q);
+            }
+        }
+    }
+}
+static void ntt_inv(const sfp_dev* d, u64* a, uint32_t p) {
+    const uint32_t n = d->n;
+    const u64 q = d->q[p];
+    const u64* w = d->ipsi + (size_t)p * n;
+    const u64* wp = d->ipsiS + (size_t)p * n;
+    uint32_t t = 1;
+    for (uint32_t m = n; m > 1; m >>= 1) {
+        uint32_t j1 = 0, h = m >> 1;
+        for (uint32_t i = 0; i < h; ++i) {
+            u64 S = w[h + i], Sp = wp[h + i];
+            for (uint32_t j = j1; j < j1 + t; ++j) {
+                u64 U = a[j], V = a[j + t];
+                a[j] = ad(U, V, q);
+                a[j + t] = shoup(sb(U, V, q), S, Sp, q);
+            }
+            j1 += 2 * t;
+        }
+        t <<= 1;
+    }
+    for (uint32_t j = 0; j < n; ++j) a[j] = shoup(a[j], d->ninv[p], d->ninvS[p], q);
+}
+
+void sfp_ntt(sfp_dev* d, uint64_t* p, sfp_limbs m, int inverse) {
+#pragma omp parallel for schedule(static)
+    for (uint32_t i = 0; i < m.count; ++i) {
+        if (inverse) ntt_inv(d, p + (size_t)i * d->n, pidx(m, i));
+        else ntt_fwd(d, p + (size_t)i * d->n, pidx(m, i));
+    }
+}
+
+/* ---- elementwise ---- */
+#define LOOP_LIMBS(...)                                                \
+    _Pragma("omp parallel for schedule(static)")                       \
+    for (uint32_t i = 0; i < m.count; ++i) {                            \
+        const u64 q = d->q[pidx(m, i)];                                 \
+        const size_t o = (size_t)i * d->n;                              \
+        (void)q;                                                        \
+        for (uint32_t x = 0; x < d->n; ++x) { __VA_ARGS__; }            \
+    }
+
+void sfp_add(sfp_dev* d, uint64_t* out, const uint64_t* a, const uint64_t* b, sfp_limbs m) {
+    LOOP_LIMBS(out[o + x] = ad(a[o + x], b[o + x], q))
+}
+void sfp_sub(sfp_dev* d, uint64_t* out, const uint64_t* a, const uint64_t* b, sfp_limbs m) {
+    LOOP_LIMBS(out[o + x] = sb(a[o + x], b[o + x], q))
+}
+void sfp_neg(sfp_dev* d, uint64_t* out, const uint64_t* a, sfp_limbs m) {
+    LOOP_LIMBS(out[o + x] = a[o + x] ? q - a[o + x] : 0)
+}
+void sfp_mul(sfp_dev* d, uint64_t* out, const uint64_t* a, const uint64_t* b, sfp_limbs m) {
+    LOOP_LIMBS(out[o + x] = mm(a[o + x], b[o + x], q))
+}
+void sfp_mul_add(sfp_dev* d, uint64_t* out, const uint64_t* a, const uint64_t* b,
+                 const uint64_t* c, sfp_limbs m) {
+    LOOP_LIMBS(out[o + x] = ad(mm(a[o + x], b[o + x], q), c[o + x], q))
+}
+void sfp_mul_const(sfp_dev* d, uint64_t* out, const uint64_t* a, const uint64_t* k, sfp_limbs m) {
+    LOOP_LIMBS(out[o + x] = mm(a[o + x], k[i], q))
+}
+void sfp_add_const(sfp_dev* d, uint64_t* out, const uint64_t* a, const uint64_t* k, sfp_limbs m) {
+    LOOP_LIMBS(out[o + x] = ad(a[o + x], k[i], q))
+}
+void sfp_tensor(sfp_dev* d, uint64_t* d0, uint64_t* d1, uint64_t* d2, const uint64_t* a0,
+                const uint64_t* a1, const uint64_t* b0, const uint64_t* b1, sfp_limbs m) {
+    LOOP_LIMBS({
+        u64 x0 = a0[o + x], x1 = a1[o + x], y0 = b0[o + x], y1 = b1[o + x];
+        u64 r0 = mm(x0, y0, q), r1 = ad(mm(x0, y1, q), mm(x1, y0, q), q), r2 = mm(x1, y1, q);
+        d0[o + x] = r0; d1[o + x] = r1; d2[o + x] = r2;
+    })
+}
+void sfp_lin_wsum(sfp_dev* d, uint64_t* out, const uint64_t* const* ins, const uint64_t* k,
+                  uint32_t nin, sfp_limbs m) {
+    LOOP_LIMBS({
+        u128 acc = 0;
+        for (uint32_t j = 0; j < nin; ++j) acc += (u128)ins[j][o + x] * k[(size_t)j * m.count + i];
+        out[o + x] = (u64)(acc % q);
+    })
+}
+
+void sfp_mac_plain(sfp_dev* d, uint64_t* out, const uint64_t* const* a, const uint64_t* const* b,
+                   uint32_t nin, sfp_limbs m) {
+    LOOP_LIMBS({
+        u128 acc = 0;
+        for (uint32_t j = 0; j < nin; ++j) acc += (u128)a[j][o + x] * b[j][o + x];
+        out[o + x] = (u64)(acc % q);
+    })
+}
+
+/* ---- automorphism ---- */
+void sfp_automorph(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t g, sfp_limbs m) {
+    const uint32_t n = d->n, logn = d->logn;
+    const u64 twoN = 2ull * n;
+    uint32_t* perm = (uint32_t*)malloc(n * 4);
+    for (uint32_t k = 0; k < n; ++k) {
+        u64 e = 2ull * brev(k, logn) + 1;
+        u64 ge = (e * g) % twoN;
+        perm[k] = brev((uint32_t)((ge - 1) / 2), logn);
+    }
+#pragma omp parallel for schedule(static)
+    for (uint32_t i = 0; i < m.count; ++i) {
+        const size_t o = (size_t)i * n;
+        for (uint32_t k = 0; k < n; ++k) out[o + k] = in[o + perm[k]];
+    }
+    free(perm);
+}
+
+/* ---- rescale ---- */
+void sfp_rescale(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t ell, const uint64_t* qlinv,
+                 uint32_t npoly, size_t in_stride, size_t out_stride) {
+    const uint32_t n = d->n;
+    const u64 ql = d->q[ell - 1];
+    u64* last = (u64*)malloc((size_t)n * 8);
+    for (uint32_t p = 0; p < npoly; ++p) {
+        const u64* src = in + p * in_stride;
+        u64* dst = out + p * out_stride;
+        memcpy(last, src + (size_t)(ell - 1) * n, (size_t)n * 8);
+        ntt_inv(d, last, ell - 1);
+#pragma omp parallel for schedule(static)
+        for (uint32_t i = 0; i < ell - 1; ++i) {
+            const u64 q = d->q[i];
+            u64* row = (u64*)malloc((size_t)n * 8);
+            const u64 qlmod = ql % q;
+            for (uint32_t x = 0; x < n; ++x) {
+                u64 v = last[x];
+                u64 r = v % q;
+                if (v > (ql >> 1)) r = sb(r, qlmod, q); /* centred: v - q_l */
+                row[x] = r;
+            }
+            ntt_fwd(d, row, i);
+            const size_t o = (size_t)i * n;
+            for (uint32_t x = 0; x < n; ++x) dst[o + x] = mm(sb(src[o + x], row[x], q), qlinv[i], q);
+            free(row);
+        }
+    }
+    free(last);
+}
+
+/* ---- base conversion / key switching ---- */
+sfp_conv* sfp_upload_conv(sfp_dev* d, uint32_t ns, const uint32_t* src, uint32_t nt,
+                          const uint32_t* dst, const uint64_t* inv, const uint64_t* mod) {
+    (void)d;
+    sfp_conv* c = (sfp_conv*)calloc(1, sizeof(sfp_conv));
+    c->ns = ns; c->nt = nt;
+    c->src = (uint32_t*)malloc(ns * 4); memcpy(c->src, src, ns * 4);
+    c->dst = (uint32_t*)malloc(nt * 4); memcpy(c->dst, dst, nt * 4);
+    c->inv = (u64*)malloc(ns * 8); memcpy(c->inv, inv, ns * 8);
+    c->mod = (u64*)malloc((size_t)ns * nt * 8); memcpy(c->mod, mod, (size_t)ns * nt * 8);
+    return c;
+}
+void sfp_free_conv(sfp_dev* d, sfp_conv* c) {
+    (void)d;
+    if (!c) return;
+    free(c->src); free(c->dst); free(c->inv); free(c->mod); free(c);
+}
+
+/* dst row t (prime c->dst[t]) = sum_i [src_i * inv_i]_{s_i} * mod[i][t]  (coefficient domain) */
+static void conv_rows(const sfp_dev* d, const sfp_conv* c, const u64* src, u64* const* dstRows,
+                      uint32_t ntUse) {
+    const uint32_t n = d->n;
+#pragma omp parallel for schedule(static)
+    for (uint32_t x = 0; x < n; ++x) {
+        u64 y[SFP_MAX_LIMBS];
+        for (uint32_t i = 0; i < c->ns; ++i) {
+            u64 qi = d->q[c->src[i]];
+            y[i] = mm(src[(size_t)i * n + x], c->inv[i], qi);
+        }
+        for (uint32_t t = 0; t < ntUse; ++t) {
+            u64 pt = d->q[c->dst[t]];
+            u128 acc = 0;
+            for (uint32_t i = 0; i < c->ns; ++i) acc += (u128)y[i] * c->mod[(size_t)i * c->nt + t];
+            dstRows[t][x] = (u64)(acc % pt);
+        }
+    }
+}
+
+void sfp_conv_apply(sfp_dev* d, uint64_t* dst, const uint64_t* src, const sfp_conv* c) {
+    u64** rows = (u64**)malloc(c->nt * sizeof(u64*));
+    for (uint32_t t = 0; t < c->nt; ++t) rows[t] = dst + (size_t)t * d->n;
+    conv_rows(d, c, src, rows, c->nt);
+    free(rows);
+}
+
+void sfp_modup(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t ell, uint32_t K,
+               uint32_t Lq, uint32_t lo, uint32_t hi, const sfp_conv* c, uint64_t* scratch) {
+    const uint32_t n = d->n, ns = hi - lo;
+    (void)K;
+    memcpy(scratch, in + (size_t)lo * n, (size_t)ns * n * 8);
+    for (uint32_t i = 0; i < ns; ++i) ntt_inv(d, scratch + (size_t)i * n, lo + i);
+    u64** rows = (u64**)malloc(c->nt * sizeof(u64*));
+    for (uint32_t t = 0; t < c->nt; ++t) {
+        uint32_t pr = c->dst[t];
+        uint32_t pos = pr < Lq ? pr : ell + (pr - Lq);
+        rows[t] = out + (size_t)pos * n;
+    }
+    conv_rows(d, c, scratch, rows, c->nt);
+#pragma omp parallel for schedule(static)
+    for (uint32_t t = 0; t < c->nt; ++t) ntt_fwd(d, rows[t], c->dst[t]);
+    free(rows);
+    memcpy(out + (size_t)lo * n, in + (size_t)lo * n, (size_t)ns * n * 8);
+}
+
+void sfp_ks_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
+                  size_t ext_stride, const uint64_t* key, uint32_t beta, uint32_t ell, uint32_t K,
+                  uint32_t Lq) {
+    const uint32_t n = d->n, rows = ell + K, NP = Lq + K;
+#pragma omp parallel for schedule(static)
+    for (uint32_t t = 0; t < rows; ++t) {
+        const uint32_t kr = t < ell ? t : Lq + (t - ell);
+        const u64 q = d->q[kr];
+        for (uint32_t x = 0; x < n; ++x) {
+            u128 s0 = 0, s1 = 0;
+            for (uint32_t j = 0; j < beta; ++j) {
+                u64 e = ext[j * ext_stride + (size_t)t * n + x];
+                const u64* kb = key + (size_t)j * 2 * NP * n;
+                const u64* ka = kb + (size_t)NP * n;
+                s0 += (u128)e * kb[(size_t)kr * n + x];
+                s1 += (u128)e * ka[(size_t)kr * n + x];
+            }
+            acc0[(size_t)t * n + x] = (u64)(s0 % q);
+            acc1[(size_t)t * n + x] = (u64)(s1 % q);
+        }
+    }
+}
+
+void sfp_moddown(sfp_dev* d, uint64_t* out, uint64_t* acc, uint32_t ell, uint32_t K, uint32_t Lq,
+                 const sfp_conv* c, const uint64_t* pinv, int add, uint64_t* scratch) {
+    const uint32_t n = d->n;
+    u64* pRows = acc + (size_t)ell * n;
+    for (uint32_t k = 0; k < K; ++k) ntt_inv(d, pRows + (size_t)k * n, Lq + k);
+    u64** rows = (u64**)malloc(ell * sizeof(u64*));
+    for (uint32_t i = 0; i < ell; ++i) rows[i] = scratch + (size_t)i * n;
+    conv_rows(d, c, pRows, rows, ell);
+#pragma omp parallel for schedule(static)
+    for (uint32_t i = 0; i < ell; ++i) {
+        const u64 q = d->q[i];
+        ntt_fwd(d, rows[i], i);
+        const size_t o = (size_t)i * n;
+        for (uint32_t x = 0; x < n; ++x) {
+            u64 v = mm(sb(acc[o + x], rows[i][x], q), pinv[i], q);
+            out[o + x] = add ? ad(out[o + x], v, q) : v;
+        }
+    }
+    free(rows);
+}
+
+/* ---- sampling / loading ---- */
+static inline u64 smix(u64 x) {
+    x += 0x9E3779B97F4A7C15ULL;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    return x ^ (x >> 31);
+}
+void sfp_sample_uniform(sfp_dev* d, uint64_t* p, sfp_limbs m, uint64_t seed) {
+#pragma omp parallel for schedule(static)
+    for (uint32_t i = 0; i < m.count; ++i) {
+        const uint32_t pi = pidx(m, i);
+        const u64 q = d->q[pi];
+        const u64 base = smix(seed ^ (0xD1B54A32D192ED03ULL * (u64)(pi + 1)));
+        for (uint32_t x = 0; x < d->n; ++x) {
+            u64 r0 = smix(base + 2ull * x), r1 = smix(base + 2ull * x + 1);
+            p[(size_t)i * d->n + x] = (u64)((((u128)r1 << 64) | r0) % q);
+        }
+    }
+}
+void sfp_load_i64(sfp_dev* d, uint64_t* p, const int64_t* c, sfp_limbs m) {
+    LOOP_LIMBS({
+        int64_t v = c[x];
+        u64 a = v < 0 ? (u64)(-(v + 1)) + 1 : (u64)v;
+        u64 r = a % q;
+        p[o + x] = (v < 0 && r) ? q - r : r;
+    })
+}

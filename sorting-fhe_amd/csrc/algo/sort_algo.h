@@ -1,0 +1,331 @@
+// Encrypted rank sort ("Optimized Rank Sort") on the device engine.
+//
+// Public surface of the reference's src/sort_algo.h: SortAlgo :22,
+// SortBase<N> :36-59, DirectSort<N> :61-774 (getSizeParameters :87-201,
+// slot-vector generators :206-306, vecRotsOpt :326-366, constructRank
+// :368-506, blindRotationOptN :561-584, rotationIndexCheckN :658-750,
+// sort :752-774) and BitonicSort<N> :1393-1487 (link-only here).
+//
+// Slot-level semantics, with P = min(N, n/2/N)
+// partitions, B = N/P batches and S = N*P slots:
+//   rank_r = sum_d step(x_r - x_{(r+d) mod N}) - 1/2  = #{j : x_j < x_r}
+//   out[rank_r] = x_r, via the doubled-sinc indicator D((r - rank_r - c)/2N)
+//   and per-partition masked rotations by c = (b*P + p) mod N.
+//
+// Engine-specific scheduling (identical slot values, fewer key switches):
+//   * baby-step rotations of one ciphertext share one hoisted ModUp;
+//   * each giant step's sum of np plaintext-mask products is accumulated
+//     before a single rescale (MultAddPlain), instead of np rescales.
+#pragma once
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <iostream>
+#include <string>
+#include <vector>
+
+#include "ciphertext-fwd.h"
+#include "coefficients.h"
+#include "comparison.h"
+#include "encryption.h"
+#include "lattice/hal/lat-backend.h"
+#include "mehp24/mehp24_utils.h"
+#include "openfhe.h"
+#include "rotation.h"
+
+using namespace lbcrypto;
+
+enum class SortAlgo { DirectSort, BitonicSort };
+
+inline void printElapsedTime(const std::string& what,
+                             const std::chrono::high_resolution_clock::time_point& start) {
+    auto ms = std::chrono::duration_cast<std::chrono::milliseconds>(
+                  std::chrono::high_resolution_clock::now() - start)
+                  .count();
+    std::cout << what << ": " << ms << " ms" << std::endl;
+}
+
+namespace sfhe {
+
+inline int ilog2(long v) {
+    int r = 0;
+    while ((1L << (r + 1)) <= v) ++r;
+    return r;
+}
+
+// Per-N metadata shared by constructRank and rotationIndexCheckN.
+struct RankLayout {
+    int N, P, B, S, npRank, npPlace;
+    RankLayout(int N, int maxBatch) : N(N) {
+        P = std::min(N, maxBatch / N);
+        B = N / P;
+        S = N * P;
+        // baby-step counts: 2^floor(log2(N)/2), as the reference's tables
+        // (sort_algo.h:383-416, :670-703)
+        npRank = std::min(1 << (ilog2(N) / 2), P);
+        npPlace = N <= 256 ? (1 << (ilog2(N) / 2)) : (N <= 1024 ? 8 : 4);
+    }
+};
+
+// Sign configuration DirectSortTest uses for each N (DirectSortTest.cpp:113-121).
+inline CompositeSignConfig defaultSignConfig(int N) {
+    if (N <= 16) return CompositeSignConfig(3, 2, 2);
+    if (N <= 128) return CompositeSignConfig(3, 3, 2);
+    if (N <= 512) return CompositeSignConfig(3, 4, 2);
+    return CompositeSignConfig(3, 5, 2);
+}
+
+// Levels consumed by DirectSort::sort with sign config `c`:
+//   rank: 1 (mask) + 3 * (max(dg,1) + df) (n = 3) + 1 (x 1/2)
+//   placement: 1 (x 1/2N) + PS depth of the doubled sinc + 1 (x input) + 1 (mask)
+inline int directSortDepth(int N, const CompositeSignConfig& c) {
+    const int perPoly = c.n == 3 ? 3 : 0;
+    int sign = perPoly * (std::max(c.dg, 1) + c.df);
+    if (c.n == 4) sign = 5 * std::max(c.dg, 1) + 4 * c.df;
+    const int ps = (int)lbcrypto::ChebyshevPSDepth(
+        (uint32_t)sfhe::doubledSincCoefficients(N).size() - 1);
+    return 1 + sign + 1 + 1 + ps + 1 + 1;
+}
+
+// Every rotation amount DirectSort<N>::sort issues, for rings 2^15 .. 2^18.
+inline std::vector<int> directSortRotations(int N) {
+    std::set<int> r;
+    for (int logn = 15; logn <= 18; ++logn) {
+        const int maxBatch = 1 << (logn - 1);
+        if (maxBatch < N) continue;
+        RankLayout L(N, maxBatch);
+        for (int i = 1; i < L.npRank; ++i) r.insert(i);
+        for (int i = 1; i < L.npPlace; ++i) r.insert(i);
+        for (int b = 0; b < L.B; ++b) {
+            for (int j = 0; j < L.P / L.npRank; ++j) r.insert(b * L.P + j * L.npRank);
+            for (int i = 0; i < L.P / L.npPlace; ++i) r.insert(b * L.P + i * L.npPlace);
+        }
+        for (int s = L.S / 2; s >= N; s /= 2) r.insert(s);
+    }
+    r.erase(0);
+    return std::vector<int>(r.begin(), r.end());
+}
+
+}  // namespace sfhe
+
+// ---------------------------------------------------------------------------
+template <int N>
+class SortBase {
+  protected:
+    std::shared_ptr<Encryption> m_enc;
+    const Ciphertext<DCRTPoly> m_zeroCache;
+
+    // fresh encryption of N zeros: the accumulator seed of every sum
+    virtual Ciphertext<DCRTPoly> createZeroCache() {
+        return m_enc->encryptInput(std::vector<double>(N, 0.0));
+    }
+
+  public:
+    SortBase(std::shared_ptr<Encryption> enc) : m_enc(enc), m_zeroCache(createZeroCache()) {}
+    virtual ~SortBase() = default;
+
+    virtual Ciphertext<DCRTPoly> sort(const Ciphertext<DCRTPoly>& input_array, SignFunc SignFunc,
+                                      SignConfig& Cfg) = 0;
+
+    virtual const Ciphertext<DCRTPoly>& getZero() const { return m_zeroCache; }
+    constexpr size_t getArraySize() const { return N; }
+};
+
+template <int N>
+class DirectSort : public SortBase<N> {
+  private:
+    CryptoContext<DCRTPoly> m_cc;
+    PublicKey<DCRTPoly> m_PublicKey;
+    Comparison comp;
+    RotationComposer<N> rot;
+    int max_batch;  // n/2
+
+  public:
+    std::shared_ptr<Encryption> m_enc;
+
+    DirectSort(CryptoContext<DCRTPoly> cc, PublicKey<DCRTPoly> publicKey,
+               std::vector<int> rotIndices, std::shared_ptr<Encryption> enc)
+        : SortBase<N>(enc), m_cc(cc), m_PublicKey(publicKey), comp(enc),
+          rot(m_cc, enc, rotIndices), max_batch((int)cc->GetRingDimension() / 2), m_enc(enc) {}
+
+    const std::set<int>& getRotationCalls() const { return rot.getRotationCalls(); }
+
+    // Batch size, depth and rotation keys for this N (reference :87-201).
+    // The depth is derived, not tabulated: it reproduces the reference's
+    // table 23,24,25,28,29,30,34,35,39 for N = 4..1024.
+    static void getSizeParameters(CCParams<CryptoContextCKKSRNS>& parameters,
+                                  std::vector<int>& rotations) {
+        parameters.SetBatchSize(N);
+        parameters.SetScalingModSize(40);
+        parameters.SetMultiplicativeDepth(
+            (uint32_t)sfhe::directSortDepth(N, sfhe::defaultSignConfig(N)));
+        rotations = sfhe::directSortRotations(N);
+    }
+
+    // ---- slot-vector generators (reference :206-306) ----
+    // 1 on partition k = slots [kN, (k+1)N)
+    std::vector<double> generateMaskVector(int num_slots, int k) {
+        std::vector<double> v(num_slots, 0.0);
+        std::fill(v.begin() + (size_t)k * N, v.begin() + (size_t)(k + 1) * N, 1.0);
+        return v;
+    }
+    std::vector<double> generateMaskVectorN(int num_slots, int k) {
+        return generateMaskVector(num_slots, k);
+    }
+    std::vector<double> generateMaskVector2N(int num_slots, int k) {
+        std::vector<double> v(num_slots, 0.0);
+        std::fill(v.begin() + (size_t)2 * k * N, v.begin() + (size_t)2 * (k + 1) * N, 1.0);
+        return v;
+    }
+    // [0, 1, ..., N-1]
+    std::vector<double> generateIndexVector() {
+        std::vector<double> v(N);
+        for (int i = 0; i < N; ++i) v[i] = i;
+        return v;
+    }
+    // partition p holds (k + p) mod N
+    std::vector<double> generateCheckingVectorN(int num_slots, int k) {
+        std::vector<double> v(num_slots);
+        for (int s = 0; s < num_slots; ++s) v[s] = (k + s / N) % N;
+        return v;
+    }
+    // blocks of 2N: N copies of c then N copies of c - N, c = (k + block) mod N
+    std::vector<double> generateCheckingVector2N(int num_slots, int k) {
+        std::vector<double> v(num_slots);
+        for (int s = 0; s < num_slots; ++s) {
+            int c = (k + s / (2 * N)) % N;
+            v[s] = (s % (2 * N)) < N ? c : c - N;
+        }
+        return v;
+    }
+    // left rotation for r > 0, right rotation for r < 0
+    std::vector<double> vectorRotate(const std::vector<double>& v, int r) {
+        if (v.empty()) return {};
+        const long n = (long)v.size();
+        long s = ((r % n) + n) % n;
+        std::vector<double> out(v.size());
+        for (long i = 0; i < n; ++i) out[i] = v[(i + s) % n];
+        return out;
+    }
+
+    // shifted[pN + r] = x[(r + is*P + p) mod N]: baby steps pre_i = Rot(x, i),
+    // giant steps j: Rot(sum_i pre_i * RotR(mask_{np j + i}, is*P + j np), is*P + j np)
+    Ciphertext<DCRTPoly> vecRotsOpt(const std::vector<Ciphertext<DCRTPoly>>& pre,
+                                    int num_partition, int num_slots, int np, int is) {
+        std::vector<Ciphertext<DCRTPoly>> giants;
+        for (int j = 0; j < num_partition / np; ++j) {
+            const int shift = is * num_partition + j * np;
+            std::vector<Plaintext> masks;
+            for (int i = 0; i < np; ++i)
+                masks.push_back(m_cc->MakeCKKSPackedPlaintext(
+                    vectorRotate(generateMaskVector(num_slots, np * j + i), -shift), 1,
+                    pre[i]->GetLevel(), nullptr, num_slots));
+            auto T = m_cc->EvalMultAddPlain(pre, masks);
+            T->SetSlots(num_slots);
+            giants.push_back(rot.rotate(T, shift));
+        }
+        return m_cc->EvalAddMany(giants);
+    }
+
+    Ciphertext<DCRTPoly> constructRank(const Ciphertext<DCRTPoly>& input_array, SignFunc SignFunc,
+                                       SignConfig& Cfg) {
+        const sfhe::RankLayout L(N, max_batch);
+        std::vector<int> amounts(L.npRank);
+        for (int i = 0; i < L.npRank; ++i) amounts[i] = i;
+        auto pre = rot.rotateMany(input_array, amounts);
+        for (auto& p : pre) p->SetSlots(L.S);
+
+        auto rank = this->getZero()->Clone();
+        rank->SetSlots(L.S);
+        for (int b = 0; b < L.B; ++b) {
+            auto shifted = vecRotsOpt(pre, L.P, L.S, L.npRank, b);
+            auto dup = input_array->Clone();
+            dup->SetSlots(L.S);
+            m_cc->EvalAddInPlace(rank, comp.compare(m_cc, dup, shifted, SignFunc, Cfg));
+        }
+        // sum the P partitions (period N inside S slots)
+        for (int s = L.S / 2; s >= N; s /= 2) m_cc->EvalAddInPlace(rank, rot.rotate(rank, s));
+        rank->SetSlots(N);
+        // remove the self comparison step(0) = 1/2
+        return m_cc->EvalSub(rank, 0.5);
+    }
+
+    // Rotates partition k = np*i + j of the masked inputs left by ib*P + k.
+    Ciphertext<DCRTPoly> blindRotationOptN(const std::vector<Ciphertext<DCRTPoly>>& masked_inputs,
+                                           int num_slots, int np, int ib, int num_partition) {
+        std::vector<Ciphertext<DCRTPoly>> giants;
+        for (int i = 0; i < (num_slots / N) / np; ++i) {
+            std::vector<Plaintext> masks;
+            for (int j = 0; j < np; ++j)
+                masks.push_back(m_cc->MakeCKKSPackedPlaintext(
+                    vectorRotate(generateMaskVectorN(num_slots, np * i + j), j), 1,
+                    masked_inputs[j]->GetLevel(), nullptr, num_slots));
+            auto tmp = m_cc->EvalMultAddPlain(masked_inputs, masks);
+            giants.push_back(rot.rotate(tmp, ib * num_partition + i * np));
+        }
+        auto result = this->getZero()->Clone();
+        m_cc->EvalAddInPlace(result, m_cc->EvalAddMany(giants));
+        return result;
+    }
+
+    Ciphertext<DCRTPoly> rotationIndexCheckN(const Ciphertext<DCRTPoly>& ctx_Rank,
+                                             const Ciphertext<DCRTPoly>& input_array) {
+        const sfhe::RankLayout L(N, max_batch);
+        auto output = this->getZero()->Clone();
+        Plaintext idx =
+            m_cc->MakeCKKSPackedPlaintext(generateIndexVector(), 1, ctx_Rank->GetLevel(), nullptr, N);
+        auto indexMinusRank = m_cc->EvalSub(idx, ctx_Rank);
+        indexMinusRank->SetSlots(L.S);
+        input_array->SetSlots(L.S);  // reference side effect (sort_algo.h:711)
+
+        const auto& sincCoeffs = selectDoubledSincCoefficients<N>();
+        for (int b = 0; b < L.B; ++b) {
+            Plaintext chk = m_cc->MakeCKKSPackedPlaintext(
+                generateCheckingVectorN(L.S, b * L.P), 1, indexMinusRank->GetLevel(), nullptr, L.S);
+            // (r - rank_r - c) / 2N  in (-1, 1/2)
+            auto z = m_cc->EvalMult(m_cc->EvalSub(indexMinusRank, chk), 1.0 / N / 2);
+            auto hit = m_cc->EvalChebyshevSeriesPS(z, sincCoeffs, -1, 1);
+            auto masked = m_cc->EvalMult(hit, input_array);
+            std::vector<int> amounts(L.npPlace);
+            for (int i = 0; i < L.npPlace; ++i) amounts[i] = i;
+            auto maskedRot = rot.rotateMany(masked, amounts);
+            m_cc->EvalAddInPlace(output, blindRotationOptN(maskedRot, L.S, L.npPlace, b, L.P));
+        }
+        for (int s = L.S / 2; s >= N; s /= 2) m_cc->EvalAddInPlace(output, rot.rotate(output, s));
+        output->SetSlots(N);
+        return output;
+    }
+
+    Ciphertext<DCRTPoly> sort(const Ciphertext<DCRTPoly>& input_array, SignFunc SignFunc,
+                              SignConfig& Cfg) override {
+        std::cout << "\n===== Direct Sort Input Array: \n";
+        PRINT_PT(m_enc, input_array);
+        auto ctx_Rank = constructRank(input_array, SignFunc, Cfg);
+        std::cout << "\n===== Constructed Rank: \n";
+        PRINT_PT(m_enc, ctx_Rank);
+        auto output_array = rotationIndexCheckN(ctx_Rank, input_array);
+        std::cout << "\n===== Final Output: \n";
+        PRINT_PT(m_enc, output_array);
+        std::cout << "Final Level: " << output_array->GetLevel() << std::endl;
+        return output_array;
+    }
+};
+
+// Compare-and-swap network (reference :1393-1487).  It bootstraps, which is
+// the SURVEY §8(f) rank-2/3 "next" row: linkable, throws until then.
+template <int N>
+class BitonicSort : public SortBase<N> {
+  public:
+    BitonicSort(CryptoContext<DCRTPoly> cc, PublicKey<DCRTPoly> publicKey,
+                std::vector<int> rotIndices, std::shared_ptr<Encryption> enc)
+        : SortBase<N>(enc), m_cc(cc), m_PublicKey(publicKey), m_rot(rotIndices) {}
+    Ciphertext<DCRTPoly> sort(const Ciphertext<DCRTPoly>&, SignFunc, SignConfig&) override {
+        throw OpenFHEException("BitonicSort needs CKKS bootstrapping (not implemented yet)");
+    }
+
+  private:
+    CryptoContext<DCRTPoly> m_cc;
+    PublicKey<DCRTPoly> m_PublicKey;
+    std::vector<int> m_rot;
+};

@@ -1,0 +1,421 @@
+// extern "C" boundary (include/sfhe.h) over the lbcrypto-compatible engine.
+#include <cstring>
+#include <iostream>
+#include <memory>
+#include <sstream>
+#include <streambuf>
+#include <string>
+
+#include "../../include/sfhe.h"
+#include "algo/coefficients.h"
+#include "algo/comparison.h"
+#include "algo/encryption.h"
+#include "algo/rotation.h"
+#include "algo/sign.h"
+#include "algo/sort_algo.h"
+#include "core/openfhe.h"
+#include "core/state.h"
+
+using namespace lbcrypto;
+using Ct = Ciphertext<DCRTPoly>;
+
+struct sfhe_ctx {
+    CryptoContext<DCRTPoly> cc;
+    KeyPair<DCRTPoly> keys;
+    bool quiet = false;
+};
+struct sfhe_ct {
+    Ct ct;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+struct NullBuf : std::streambuf {
+    int overflow(int c) override { return c; }
+};
+
+// silences std::cout while alive (reference prints inside sort())
+struct Quiet {
+    std::streambuf* old = nullptr;
+    NullBuf nb;
+    explicit Quiet(bool on) {
+        if (on) old = std::cout.rdbuf(&nb);
+    }
+    ~Quiet() {
+        if (old) std::cout.rdbuf(old);
+    }
+};
+
+template <class F>
+int guard(F&& f) {
+    try {
+        f();
+        return SFHE_OK;
+    } catch (const OpenFHEException& e) {
+        g_err = e.what();
+        return std::string(e.what()).find("device") != std::string::npos ? SFHE_EDEVICE
+                                                                          : SFHE_ESCHEME;
+    } catch (const std::invalid_argument& e) {
+        g_err = e.what();
+        return SFHE_EINVAL;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return SFHE_ESCHEME;
+    }
+}
+
+#define REQUIRE(cond, msg)                    \
+    do {                                      \
+        if (!(cond)) {                        \
+            g_err = msg;                      \
+            return SFHE_EINVAL;               \
+        }                                     \
+    } while (0)
+
+sfhe_ct* wrap(Ct c) { return new sfhe_ct{std::move(c)}; }
+
+SignConfig cfgOf(int n, int dg, int df) { return SignConfig(CompositeSignConfig(n, dg, df)); }
+
+struct SorterBase {
+    virtual ~SorterBase() = default;
+    virtual Ct sort(const Ct& in, SignConfig& cfg) = 0;
+    virtual Ct rank(const Ct& in, SignConfig& cfg) = 0;
+    virtual Ct place(const Ct& rank, const Ct& in) = 0;
+};
+
+template <int N>
+struct Sorter : SorterBase {
+    DirectSort<N> ds;
+    Sorter(CryptoContext<DCRTPoly> cc, PublicKey<DCRTPoly> pk, std::vector<int> rot,
+           std::shared_ptr<Encryption> enc)
+        : ds(cc, pk, rot, enc) {}
+    Ct sort(const Ct& in, SignConfig& cfg) override { return ds.sort(in, SignFunc::CompositeSign, cfg); }
+    Ct rank(const Ct& in, SignConfig& cfg) override {
+        return ds.constructRank(in, SignFunc::CompositeSign, cfg);
+    }
+    Ct place(const Ct& r, const Ct& in) override { return ds.rotationIndexCheckN(r, in); }
+};
+
+template <int N>
+int decomposeN(const std::vector<int>& keys, int r, int wrap, int algo, int32_t* v, int32_t* s,
+               size_t cap, size_t* count) {
+    Decomposer<N> d(keys);
+    auto steps = d.decompose(r, wrap, algo == 0 ? DecomposeAlgo::NAF
+                                      : algo == 1 ? DecomposeAlgo::BNAF
+                                                  : DecomposeAlgo::BINARY);
+    if (count) *count = steps.size();
+    for (size_t i = 0; i < steps.size() && i < cap; ++i) {
+        v[i] = steps[i].value;
+        s[i] = steps[i].stepSize;
+    }
+    return SFHE_OK;
+}
+
+bool validN(uint32_t N) {
+    return N >= 4 && N <= 1024 && (N & (N - 1)) == 0;
+}
+
+}  // namespace
+
+struct sfhe_sorter {
+    sfhe_ctx* ctx;
+    std::unique_ptr<SorterBase> impl;
+};
+
+extern "C" {
+
+int sfhe_abi_version(void) { return SFHE_ABI_VERSION; }
+const char* sfhe_last_error(void) { return g_err.c_str(); }
+const char* sfhe_backend(void) { return sfp_backend_name(); }
+
+void sfhe_params_default(sfhe_params* p) {
+    if (!p) return;
+    std::memset(p, 0, sizeof *p);
+    p->mult_depth = 1;
+    p->scaling_mod_size = 40;
+    p->first_mod_size = 60;
+    p->security_level = SFHE_HESTD_128_CLASSIC;
+    p->seed = 0x5eed5eed2025ULL;
+}
+
+int sfhe_context_create(const sfhe_params* p, sfhe_ctx** out) {
+    REQUIRE(p && out, "null argument");
+    return guard([&] {
+        CCParams<CryptoContextCKKSRNS> P;
+        P.SetMultiplicativeDepth(p->mult_depth);
+        P.SetScalingModSize(p->scaling_mod_size);
+        P.SetFirstModSize(p->first_mod_size ? p->first_mod_size : 60);
+        P.SetBatchSize(p->batch_size);
+        P.SetRingDim(p->ring_dim);
+        P.SetSecurityLevel(p->security_level == SFHE_HESTD_NOTSET ? HEStd_NotSet : HEStd_128_classic);
+        P.SetNumLargeDigits(p->num_large_digits);
+        P.SetDevice(p->device);
+        P.SetSeed(p->seed);
+        auto c = std::make_unique<sfhe_ctx>();
+        c->cc = GenCryptoContext(P);
+        c->cc->Enable(PKE);
+        c->cc->Enable(KEYSWITCH);
+        c->cc->Enable(LEVELEDSHE);
+        c->cc->Enable(ADVANCEDSHE);
+        *out = c.release();
+    });
+}
+
+void sfhe_context_destroy(sfhe_ctx* c) { delete c; }
+
+int sfhe_keygen(sfhe_ctx* c) {
+    REQUIRE(c, "null context");
+    return guard([&] {
+        c->keys = c->cc->KeyGen();
+        c->cc->EvalMultKeyGen(c->keys.secretKey);
+    });
+}
+
+int sfhe_rotate_keygen(sfhe_ctx* c, const int32_t* idx, size_t count) {
+    REQUIRE(c && (idx || !count), "null argument");
+    REQUIRE(c->keys.secretKey, "sfhe_keygen must be called first");
+    return guard([&] { c->cc->EvalRotateKeyGen(c->keys.secretKey, std::vector<int32_t>(idx, idx + count)); });
+}
+
+int sfhe_context_info(sfhe_ctx* c, uint32_t* n, uint32_t* depth, uint32_t* nq, uint32_t* np,
+                      uint32_t* dnum) {
+    REQUIRE(c, "null context");
+    const SfheContextState* s = c->cc->state();
+    if (n) *n = s->n;
+    if (depth) *depth = s->L;
+    if (nq) *nq = s->Lq;
+    if (np) *np = s->K;
+    if (dnum) *dnum = s->dnum;
+    return SFHE_OK;
+}
+
+int sfhe_set_plaintext_cache(sfhe_ctx* c, int on) {
+    REQUIRE(c, "null context");
+    return guard([&] { c->cc->SetPlaintextCache(on != 0); });
+}
+
+int sfhe_set_quiet(sfhe_ctx* c, int q) {
+    REQUIRE(c, "null context");
+    c->quiet = q != 0;
+    return SFHE_OK;
+}
+
+int sfhe_sync(sfhe_ctx* c) {
+    REQUIRE(c, "null context");
+    return guard([&] { c->cc->Synchronize(); });
+}
+
+int sfhe_op_stats(sfhe_ctx* c, uint64_t* counts, double* bytes, int reset) {
+    REQUIRE(c, "null context");
+    auto s = c->cc->GetOpStats();
+    if (counts) {
+        uint64_t v[9] = {s.keyswitch, s.rescale, s.tensor,  s.ptmult,    s.constmult,
+                         s.add,       s.automorph, s.ntt_limbs, s.wsum_terms};
+        std::memcpy(counts, v, sizeof v);
+    }
+    if (bytes) *bytes = s.algo_bytes;
+    if (reset) c->cc->ResetOpStats();
+    return SFHE_OK;
+}
+
+int sfhe_encrypt(sfhe_ctx* c, const double* v, size_t len, uint32_t slots, uint32_t level,
+                 sfhe_ct** out) {
+    REQUIRE(c && out && (v || !len), "null argument");
+    REQUIRE(c->keys.publicKey, "sfhe_keygen must be called first");
+    return guard([&] {
+        auto pt = c->cc->MakeCKKSPackedPlaintext(std::vector<double>(v, v + len), 1, level, nullptr, slots);
+        *out = wrap(c->cc->Encrypt(c->keys.publicKey, pt));
+    });
+}
+
+int sfhe_decrypt(sfhe_ctx* c, const sfhe_ct* ct, double* out, size_t cap, size_t* len) {
+    REQUIRE(c && ct, "null argument");
+    REQUIRE(c->keys.secretKey, "no secret key");
+    return guard([&] {
+        Plaintext pt;
+        c->cc->Decrypt(c->keys.secretKey, ct->ct, &pt);
+        const auto& v = pt->GetRealPackedValue();
+        if (len) *len = v.size();
+        for (size_t i = 0; i < v.size() && i < cap; ++i) out[i] = v[i];
+    });
+}
+
+void sfhe_ct_free(sfhe_ct* ct) { delete ct; }
+
+int sfhe_ct_clone(const sfhe_ct* ct, sfhe_ct** out) {
+    REQUIRE(ct && out, "null argument");
+    return guard([&] { *out = wrap(ct->ct->Clone()); });
+}
+
+int sfhe_ct_info(const sfhe_ct* ct, uint32_t* level, uint32_t* slots, uint32_t* limbs) {
+    REQUIRE(ct, "null ciphertext");
+    if (level) *level = ct->ct->GetLevel();
+    if (slots) *slots = ct->ct->GetSlots();
+    if (limbs) *limbs = ct->ct->GetNumLimbs();
+    return SFHE_OK;
+}
+
+int sfhe_ct_set_slots(sfhe_ct* ct, uint32_t slots) {
+    REQUIRE(ct && slots && !(slots & (slots - 1)), "slots must be a power of two");
+    ct->ct->SetSlots(slots);
+    return SFHE_OK;
+}
+
+int sfhe_ct_download(sfhe_ctx* c, const sfhe_ct* ct, uint64_t* out, size_t cap) {
+    REQUIRE(c && ct && out, "null argument");
+    const size_t n = c->cc->GetRingDimension();
+    const size_t L = ct->ct->GetNumLimbs();
+    REQUIRE(cap >= 2 * L * n, "output buffer too small");
+    return guard([&] {
+        auto* s = c->cc->state();
+        sfp_d2h(s->dev, out, ct->ct->c0, L * n * 8);
+        sfp_d2h(s->dev, out + L * n, ct->ct->c1, L * n * 8);
+        const char* e = sfp_last_error(s->dev);
+        if (e) throw OpenFHEException(std::string("device error: ") + e);
+    });
+}
+
+#define BINOP(name, expr)                                                           \
+    int name(sfhe_ctx* c, const sfhe_ct* a, const sfhe_ct* b, sfhe_ct** out) {       \
+        REQUIRE(c && a && b && out, "null argument");                               \
+        return guard([&] { *out = wrap(expr); });                                   \
+    }
+BINOP(sfhe_eval_add, c->cc->EvalAdd(a->ct, b->ct))
+BINOP(sfhe_eval_sub, c->cc->EvalSub(a->ct, b->ct))
+BINOP(sfhe_eval_mult, c->cc->EvalMult(a->ct, b->ct))
+
+int sfhe_eval_add_const(sfhe_ctx* c, const sfhe_ct* a, double k, sfhe_ct** out) {
+    REQUIRE(c && a && out, "null argument");
+    return guard([&] { *out = wrap(c->cc->EvalAdd(a->ct, k)); });
+}
+int sfhe_eval_mult_const(sfhe_ctx* c, const sfhe_ct* a, double k, sfhe_ct** out) {
+    REQUIRE(c && a && out, "null argument");
+    return guard([&] { *out = wrap(c->cc->EvalMult(a->ct, k)); });
+}
+int sfhe_eval_mult_plain(sfhe_ctx* c, const sfhe_ct* a, const double* v, size_t len,
+                         uint32_t slots, sfhe_ct** out) {
+    REQUIRE(c && a && out && (v || !len), "null argument");
+    return guard([&] {
+        auto pt = c->cc->MakeCKKSPackedPlaintext(std::vector<double>(v, v + len), 1,
+                                                 a->ct->GetLevel(), nullptr, slots);
+        *out = wrap(c->cc->EvalMult(a->ct, pt));
+    });
+}
+int sfhe_eval_rotate(sfhe_ctx* c, const sfhe_ct* a, int32_t r, sfhe_ct** out) {
+    REQUIRE(c && a && out, "null argument");
+    return guard([&] { *out = wrap(c->cc->EvalRotate(a->ct, r)); });
+}
+int sfhe_eval_chebyshev(sfhe_ctx* c, const sfhe_ct* x, const double* coeffs, size_t count,
+                        double a, double b, sfhe_ct** out) {
+    REQUIRE(c && x && coeffs && count && out, "null argument");
+    return guard([&] {
+        *out = wrap(c->cc->EvalChebyshevSeriesPS(x->ct, std::vector<double>(coeffs, coeffs + count), a, b));
+    });
+}
+
+int sfhe_sign(sfhe_ctx* c, const sfhe_ct* x, int n, int dg, int df, sfhe_ct** out) {
+    REQUIRE(c && x && out, "null argument");
+    REQUIRE(n == 3 || n == 4, "composite sign degree n must be 3 or 4");
+    return guard([&] { *out = wrap(sign(x->ct, c->cc, SignFunc::CompositeSign, cfgOf(n, dg, df))); });
+}
+
+int sfhe_compare(sfhe_ctx* c, const sfhe_ct* a, const sfhe_ct* b, int n, int dg, int df,
+                 sfhe_ct** out) {
+    REQUIRE(c && a && b && out, "null argument");
+    REQUIRE(n == 3 || n == 4, "composite sign degree n must be 3 or 4");
+    return guard([&] {
+        Comparison cmp;
+        auto cfg = cfgOf(n, dg, df);
+        *out = wrap(cmp.compare(c->cc, a->ct, b->ct, SignFunc::CompositeSign, cfg));
+    });
+}
+
+int sfhe_direct_sort_params(uint32_t N, uint32_t* depth, int32_t* rot, size_t cap, size_t* count) {
+    REQUIRE(validN(N), "N must be a power of two in [4, 1024]");
+    return guard([&] {
+        auto r = sfhe::directSortRotations((int)N);
+        if (depth) *depth = (uint32_t)sfhe::directSortDepth((int)N, sfhe::defaultSignConfig((int)N));
+        if (count) *count = r.size();
+        for (size_t i = 0; i < r.size() && i < cap && rot; ++i) rot[i] = r[i];
+    });
+}
+
+int sfhe_doubled_sinc_coeffs(uint32_t N, double* out, size_t cap, size_t* count) {
+    REQUIRE(validN(N), "N must be a power of two in [4, 1024]");
+    return guard([&] {
+        const auto& v = sfhe::doubledSincCoefficients((int)N);
+        if (count) *count = v.size();
+        for (size_t i = 0; i < v.size() && i < cap && out; ++i) out[i] = v[i];
+    });
+}
+
+int sfhe_sorter_create(sfhe_ctx* c, uint32_t N, int debug, sfhe_sorter** out) {
+    REQUIRE(c && out, "null argument");
+    REQUIRE(validN(N), "N must be a power of two in [4, 1024]");
+    REQUIRE(c->keys.publicKey, "sfhe_keygen must be called first");
+    return guard([&] {
+        std::shared_ptr<Encryption> enc =
+            debug ? std::shared_ptr<Encryption>(std::make_shared<DebugEncryption>(c->cc, c->keys))
+                  : std::make_shared<Encryption>(c->cc, c->keys.publicKey);
+        auto rot = sfhe::directSortRotations((int)N);
+        auto s = std::make_unique<sfhe_sorter>();
+        s->ctx = c;
+        switch (N) {
+#define CASE(K) \
+    case K: s->impl.reset(new Sorter<K>(c->cc, c->keys.publicKey, rot, enc)); break;
+            CASE(4) CASE(8) CASE(16) CASE(32) CASE(64) CASE(128) CASE(256) CASE(512) CASE(1024)
+#undef CASE
+        }
+        *out = s.release();
+    });
+}
+
+void sfhe_sorter_destroy(sfhe_sorter* s) { delete s; }
+
+int sfhe_sorter_sort(sfhe_sorter* s, sfhe_ct* in, int n, int dg, int df, sfhe_ct** out) {
+    REQUIRE(s && in && out, "null argument");
+    return guard([&] {
+        Quiet q(s->ctx->quiet);
+        auto cfg = cfgOf(n, dg, df);
+        *out = wrap(s->impl->sort(in->ct, cfg));
+    });
+}
+
+int sfhe_sorter_rank(sfhe_sorter* s, const sfhe_ct* in, int n, int dg, int df, sfhe_ct** out) {
+    REQUIRE(s && in && out, "null argument");
+    return guard([&] {
+        auto cfg = cfgOf(n, dg, df);
+        *out = wrap(s->impl->rank(in->ct, cfg));
+    });
+}
+
+int sfhe_sorter_place(sfhe_sorter* s, const sfhe_ct* rank, sfhe_ct* in, sfhe_ct** out) {
+    REQUIRE(s && rank && in && out, "null argument");
+    return guard([&] { *out = wrap(s->impl->place(rank->ct, in->ct)); });
+}
+
+int sfhe_decompose(uint32_t N, const int32_t* keys, size_t nkeys, int32_t rotation, int32_t wrapN,
+                   int algo, int32_t* values, int32_t* steps, size_t cap, size_t* count) {
+    REQUIRE(validN(N) && keys && nkeys && wrapN > 0, "bad argument");
+    std::vector<int> k(keys, keys + nkeys);
+    return guard([&] {
+        switch (N) {
+#define CASE(K) \
+    case K: decomposeN<K>(k, rotation, wrapN, algo, values, steps, cap, count); break;
+            CASE(4) CASE(8) CASE(16) CASE(32) CASE(64) CASE(128) CASE(256) CASE(512) CASE(1024)
+#undef CASE
+        }
+    });
+}
+
+int sfhe_context_primes(sfhe_ctx* c, uint64_t* out, size_t cap, size_t* count) {
+    REQUIRE(c, "null context");
+    const auto& p = c->cc->state()->primes;
+    if (count) *count = p.size();
+    for (size_t i = 0; i < p.size() && i < cap && out; ++i) out[i] = p[i];
+    return SFHE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,258 @@
+// Chebyshev-series evaluation for the sinc placement and g_4 sign polynomial.
+//
+// Reference call sites: src/sort_algo.h:727-728 (doubled-sinc, degree 1662
+// at N=256) and src/sign.cpp:76 (g_4, degree 27); both go to OpenFHE's
+// EvalChebyshevSeriesPS with coefficients in the c0/2 convention
+// (tests/SincTest.cpp:17-39).
+//
+// Algorithm (this engine's own, depth-exact):
+//   baby steps  T_1..T_k, k = 2^l        (T_j at depth ceil(log2 j))
+//   giant steps T_{2^i}, i = l+1..D-1    (T_{2^i} at depth i)
+//   p = q * T_M + r  (Chebyshev division, M a power of two) recursively;
+//   leaves sum_j a_j T_j (j <= k) are ONE fused weighted-sum kernel plus a
+//   rescale.  With depth budget D this reaches degree 2^D - 2^l, which is
+//   exactly OpenFHE's published depth table (≤5:3, ≤13:4, ≤27:5, ≤59:6,
+//   ≤119:7, ≤247:8, ≤495:9, ≤1007:10, ≤2031:11, ≤4031:12, ≤8127:13).
+//   l is chosen to minimise ciphertext products inside the budget; if the
+//   evaluation lands shallower than OpenFHE's depth the result is level-
+//   adjusted so the per-N multDepth tables (src/sort_algo.h:94-198) are
+//   consumed exactly.
+#include <algorithm>
+#include <cmath>
+#include <map>
+
+#include "state.h"
+
+namespace lbcrypto {
+
+uint32_t ChebyshevPSDepth(uint32_t d) {
+    if (d <= 1) return 1;
+    if (d == 2) return 2;
+    static const uint32_t ub[] = {5, 13, 27, 59, 119, 247, 495, 1007, 2031, 4031, 8127, 16255, 32511, 65023};
+    for (uint32_t i = 0; i < sizeof(ub) / sizeof(ub[0]); ++i)
+        if (d <= ub[i]) return 3 + i;
+    SFHE_THROW("Chebyshev degree too large");
+}
+
+std::vector<double> EvalChebyshevCoefficients(std::function<double(double)> func, double a,
+                                              double b, uint32_t degree) {
+    if (!degree) SFHE_THROW("degree must be positive");
+    const double bMinusA = 0.5 * (b - a), bPlusA = 0.5 * (b + a);
+    const double piByDeg = M_PI / (double)degree;
+    std::vector<double> fx(degree);
+    for (uint32_t j = 0; j < degree; ++j) fx[j] = func(std::cos(piByDeg * (j + 0.5)) * bMinusA + bPlusA);
+    // cos(pi * i * (2j+1) / (2 d)) depends only on i*(2j+1) mod 4d
+    const uint64_t P = 4ull * degree;
+    std::vector<double> ctab(P);
+    for (uint64_t m = 0; m < P; ++m) ctab[m] = std::cos(M_PI * (double)m / (2.0 * degree));
+    std::vector<double> c(degree, 0.0);
+    const double mult = 2.0 / (double)degree;
+    for (uint32_t i = 0; i < degree; ++i) {
+        double acc = 0.0;
+        uint64_t step = (2ull * i) % P, idx = i % P;
+        for (uint32_t j = 0; j < degree; ++j) {
+            acc += fx[j] * ctab[idx];
+            idx += step;
+            if (idx >= P) idx -= P;
+        }
+        c[i] = acc * mult;
+    }
+    return c;
+}
+
+namespace {
+
+using Ct = Ciphertext<DCRTPoly>;
+
+struct Val {
+    bool isConst = true;
+    double c = 0.0;
+    Ct ct;
+};
+
+class PSEvaluator {
+  public:
+    PSEvaluator(CryptoContextImpl<DCRTPoly>* cc, const Ct& y, uint32_t l, uint32_t D)
+        : cc(cc), l(l), k(1u << l), D(D) {
+        T.resize(k + 1);
+        T[1] = y;
+        for (uint32_t j = 2; j <= k; ++j) {
+            Ct prod;
+            if (j % 2 == 0)
+                prod = cc->EvalSquare(T[j / 2]);
+            else
+                prod = cc->EvalMult(T[j / 2], T[j / 2 + 1]);
+            Ct two = cc->EvalAdd(prod, prod);
+            T[j] = (j % 2 == 0) ? cc->EvalAdd(two, -1.0) : cc->EvalSub(two, atLevel(1, two->GetLevel()));
+        }
+        giant[l] = T[k];
+    }
+
+    Val eval(std::vector<double> p, uint32_t depth) {
+        trim(p);
+        if (p.empty()) return Val{true, 0.0, nullptr};
+        const uint32_t deg = (uint32_t)p.size() - 1;
+        if (deg == 0) return Val{true, p[0], nullptr};
+        if (deg <= k) return leaf(p);
+        if (depth >= 1 && deg + (1u << l) <= (1u << (depth - 1))) return eval(p, depth - 1);
+        const uint32_t M = deg >= (1u << (depth - 1)) ? (1u << (depth - 1)) : (1u << (depth - 2));
+        std::vector<double> q(deg - M + 1, 0.0), r(p.begin(), p.begin() + M);
+        for (uint32_t j = M; j <= deg; ++j) {
+            if (j == M) {
+                q[0] += p[j];
+            } else {
+                q[j - M] += 2.0 * p[j];
+                r[2 * M - j] -= p[j];
+            }
+        }
+        Val qv = eval(q, depth - 1);
+        Val rv = eval(r, depth);
+        const Ct& TM = power(M);
+        Val out;
+        out.isConst = false;
+        if (qv.isConst)
+            out.ct = cc->EvalMult(TM, qv.c);
+        else
+            out.ct = cc->EvalMult(qv.ct, TM);
+        if (rv.isConst) {
+            if (rv.c != 0.0) out.ct = cc->EvalAdd(out.ct, rv.c);
+        } else {
+            out.ct = cc->EvalAdd(out.ct, rv.ct);
+        }
+        return out;
+    }
+
+  private:
+    static void trim(std::vector<double>& p) {
+        while (!p.empty() && p.back() == 0.0) p.pop_back();
+    }
+
+    // T_M for a power of two M (giant steps built lazily: T_2M = 2 T_M^2 - 1)
+    const Ct& power(uint32_t M) {
+        if (M <= k) return T[M];
+        uint32_t i = (uint32_t)__builtin_ctz(M);
+        auto it = giant.find(i);
+        if (it != giant.end()) return it->second;
+        const Ct& half = power(M / 2);
+        Ct sq = cc->EvalSquare(half);
+        return giant[i] = cc->EvalAdd(cc->EvalAdd(sq, sq), -1.0);
+    }
+
+    const Ct& atLevel(uint32_t j, uint32_t level) {
+        auto key = std::make_pair(j, level);
+        auto it = aligned.find(key);
+        if (it != aligned.end()) return it->second;
+        return aligned[key] = (T[j]->GetLevel() == level ? T[j] : cc->AdjustLevel(T[j], level));
+    }
+
+    Val leaf(const std::vector<double>& p) {
+        const uint32_t deg = (uint32_t)p.size() - 1;
+        uint32_t lev = 0;
+        bool any = false;
+        for (uint32_t j = 1; j <= deg; ++j)
+            if (p[j] != 0.0) {
+                lev = std::max(lev, T[j]->GetLevel());
+                any = true;
+            }
+        if (!any) return Val{true, p[0], nullptr};
+        std::vector<const uint64_t*> ins0, ins1;
+        std::vector<double> w;
+        for (uint32_t j = 1; j <= deg; ++j) {
+            if (p[j] == 0.0) continue;
+            const Ct& t = atLevel(j, lev);
+            ins0.push_back(t->c0);
+            ins1.push_back(t->c1);
+            w.push_back(p[j]);
+        }
+        Val out;
+        out.isConst = false;
+        out.ct = cc->LinearWSumRescale(ins0, ins1, w, lev, T[1]->GetSlots());
+        if (p[0] != 0.0) out.ct = cc->EvalAdd(out.ct, p[0]);
+        return out;
+    }
+
+    CryptoContextImpl<DCRTPoly>* cc;
+    uint32_t l, k, D;
+    std::vector<Ct> T;
+    std::map<uint32_t, Ct> giant;
+    std::map<std::pair<uint32_t, uint32_t>, Ct> aligned;
+};
+
+}  // namespace
+
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalChebyshevSeriesPS(
+    const Ciphertext<DCRTPoly>& x, const std::vector<double>& coeffs, double a, double b) {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    std::vector<double> p(coeffs);
+    while (!p.empty() && p.back() == 0.0) p.pop_back();
+    if (p.empty()) SFHE_THROW("empty Chebyshev series");
+    p[0] *= 0.5;  // c0/2 convention -> true constant term
+    Ciphertext<DCRTPoly> y = x;
+    if (a != -1.0 || b != 1.0) {
+        y = EvalMult(x, 2.0 / (b - a));
+        y = EvalAdd(y, -(a + b) / (b - a));
+    }
+    const uint32_t d = (uint32_t)p.size() - 1;
+    if (d == 0) return EvalAdd(EvalMult(y, 0.0), p[0]);
+    const uint32_t D = ChebyshevPSDepth(d);
+    // choose the baby-step exponent l: reach degree d within depth D with the
+    // fewest ciphertext products (k-1 baby, D-1-l giant, ~d/k recursion nodes)
+    uint32_t bestL = 1;
+    double bestCost = 1e300;
+    for (uint32_t l = 1; l + 1 <= D && l <= 6; ++l) {
+        if ((1ull << D) - (1ull << l) < d) continue;
+        double cost = (double)((1u << l) - 1) + (double)(D - 1 - l) + std::ceil((double)d / (1u << l));
+        if (cost < bestCost) {
+            bestCost = cost;
+            bestL = l;
+        }
+    }
+    const uint32_t l = std::min(bestL, (uint32_t)(31 - __builtin_clz(std::max<uint32_t>(d, 2))));
+    PSEvaluator ps(this, y, l, D);
+    auto v = ps.eval(p, D);
+    Ciphertext<DCRTPoly> out = v.isConst ? EvalAdd(EvalMult(y, 0.0), v.c) : v.ct;
+    const uint32_t target = y->GetLevel() + D;
+    if (out->GetLevel() > target)
+        SFHE_THROW("internal: Chebyshev evaluation exceeded OpenFHE depth");
+    if (out->GetLevel() < target) out = AdjustLevel(out, target);
+    return out;
+}
+
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalChebyshevFunction(
+    std::function<double(double)> f, const Ciphertext<DCRTPoly>& x, double a, double b,
+    uint32_t degree) {
+    auto c = EvalChebyshevCoefficients(f, a, b, degree + 1);
+    return EvalChebyshevSeriesPS(x, c, a, b);
+}
+
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalPolyLinear(
+    const Ciphertext<DCRTPoly>& x, const std::vector<double>& coeffs) {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    std::vector<double> p(coeffs);
+    while (!p.empty() && p.back() == 0.0) p.pop_back();
+    if (p.size() < 2) SFHE_THROW("EvalPolyLinear needs degree >= 1");
+    const uint32_t d = (uint32_t)p.size() - 1;
+    std::vector<Ciphertext<DCRTPoly>> pw(d + 1);
+    pw[1] = x;
+    for (uint32_t j = 2; j <= d; ++j)
+        pw[j] = (j % 2 == 0) ? EvalSquare(pw[j / 2]) : EvalMult(pw[j / 2], pw[j / 2 + 1]);
+    uint32_t lev = 0;
+    for (uint32_t j = 1; j <= d; ++j)
+        if (p[j] != 0.0) lev = std::max(lev, pw[j]->GetLevel());
+    std::vector<const uint64_t*> i0, i1;
+    std::vector<double> w;
+    std::vector<Ciphertext<DCRTPoly>> keep;
+    for (uint32_t j = 1; j <= d; ++j) {
+        if (p[j] == 0.0) continue;
+        auto t = pw[j]->GetLevel() == lev ? pw[j] : AdjustLevel(pw[j], lev);
+        keep.push_back(t);
+        i0.push_back(t->c0);
+        i1.push_back(t->c1);
+        w.push_back(p[j]);
+    }
+    auto out = LinearWSumRescale(i0, i1, w, lev, x->GetSlots());
+    if (p[0] != 0.0) out = EvalAdd(out, p[0]);
+    return out;
+}
+
+}  // namespace lbcrypto

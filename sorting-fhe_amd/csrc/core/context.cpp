@@ -1,0 +1,1251 @@
+// RNS-CKKS context: parameters, primes, keys, encryption and the evaluator.
+//
+// Scheme: RNS-CKKS with HYBRID key switching (dnum digits, K special primes)
+// and scale-exact automatic rescaling (FLEXIBLEAUTO-style): every ciphertext
+// at level l carries the canonical scale Delta_l, with Delta_0 = 2^s and
+// Delta_{l+1} = Delta_l^2 / q_{L-l}; the scaling primes are picked greedily
+// so that Delta_l stays within ~2^-19 of 2^s.  Operands at different levels
+// are aligned by multiplying with the integer round(Delta_t q / Delta_l) and
+// rescaling, which costs no depth on the result (OpenFHE does the same).
+//
+// All polynomial work is enqueued through csrc/prims.h.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "state.h"
+
+namespace lbcrypto {
+
+// ============================================================================
+// number theory helpers (host)
+namespace {
+
+u64 mulmod(u64 a, u64 b, u64 m) { return (u64)((u128)a * b % m); }
+u64 powmod(u64 a, u64 e, u64 m) {
+    u64 r = 1 % m;
+    a %= m;
+    while (e) {
+        if (e & 1) r = mulmod(r, a, m);
+        a = mulmod(a, a, m);
+        e >>= 1;
+    }
+    return r;
+}
+u64 invmod(u64 a, u64 m) { return powmod(a % m, m - 2, m); }  // m prime
+
+bool isPrime(u64 n) {
+    if (n < 2) return false;
+    static const u64 small[] = {2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37};
+    for (u64 p : small) {
+        if (n % p == 0) return n == p;
+    }
+    u64 d = n - 1;
+    int s = 0;
+    while ((d & 1) == 0) {
+        d >>= 1;
+        ++s;
+    }
+    for (u64 a : small) {
+        u64 x = powmod(a, d, n);
+        if (x == 1 || x == n - 1) continue;
+        bool comp = true;
+        for (int r = 1; r < s; ++r) {
+            x = mulmod(x, x, n);
+            if (x == n - 1) {
+                comp = false;
+                break;
+            }
+        }
+        if (comp) return false;
+    }
+    return true;
+}
+
+// largest prime p < bound with p = 1 mod m, not in used
+u64 primeBelow(u64 bound, u64 m, const std::set<u64>& used) {
+    u64 c = ((bound - 1) / m) * m + 1;
+    if (c >= bound) c -= m;
+    for (; c > m; c -= m)
+        if (!used.count(c) && isPrime(c)) return c;
+    SFHE_THROW("no NTT-friendly prime found");
+}
+
+// prime p = 1 mod m closest to target, not in used
+u64 primeNear(double target, u64 m, const std::set<u64>& used) {
+    u64 base = (u64)std::llround((target - 1.0) / (double)m) * m + 1;
+    for (u64 k = 0; k < (1u << 22); ++k) {
+        u64 c1 = base + k * m;
+        if (!used.count(c1) && isPrime(c1)) {
+            // also look below at the same distance
+            u64 c2 = base - k * m;
+            if (k && c2 > m && !used.count(c2) && isPrime(c2) &&
+                std::fabs((double)c2 - target) < std::fabs((double)c1 - target))
+                return c2;
+            return c1;
+        }
+        if (k) {
+            u64 c2 = base - k * m;
+            if (c2 > m && !used.count(c2) && isPrime(c2)) return c2;
+        }
+    }
+    SFHE_THROW("no NTT-friendly prime near target");
+}
+
+u64 findPsi(u64 q, uint32_t n) {
+    const u64 twoN = 2ull * n;
+    for (u64 x = 2; x < q; ++x) {
+        u64 psi = powmod(x, (q - 1) / twoN, q);
+        if (powmod(psi, n, q) == q - 1) return psi;
+    }
+    SFHE_THROW("no primitive 2n-th root");
+}
+
+// HE-standard bound on log2(PQ) for 128-bit classical security (uniform
+// ternary secret), as OpenFHE's StdLatticeParm table.
+uint32_t maxLogQ128(uint32_t logn) {
+    switch (logn) {
+        case 10: return 27;
+        case 11: return 54;
+        case 12: return 109;
+        case 13: return 218;
+        case 14: return 438;
+        case 15: return 881;
+        case 16: return 1772;
+        case 17: return 3524;
+        default: return logn > 17 ? 7050u << (logn - 18) : 0;
+    }
+}
+
+// residue of round(x) (|x| < 2^126) modulo q
+u64 residueOf(double x, u64 q) {
+    double r = std::nearbyint(x);
+    bool neg = r < 0;
+    double a = std::fabs(r);
+    u128 v;
+    if (a < 1.8e19) {
+        v = (u128)(u64)a;
+    } else {
+        // split: a = hi * 2^64 + lo (exact for doubles)
+        double hi = std::floor(std::ldexp(a, -64));
+        double lo = a - std::ldexp(hi, 64);
+        v = ((u128)(u64)hi << 64) + (u128)(u64)lo;
+    }
+    u64 m = (u64)(v % q);
+    return neg ? (m ? q - m : 0) : m;
+}
+
+}  // namespace
+
+// ============================================================================
+// device buffers
+
+DeviceBuffer::~DeviceBuffer() {
+    if (!ptr) return;
+    std::lock_guard<std::mutex> g(st->poolMu);
+    st->freeList[words].push_back(ptr);
+}
+
+DeviceBufferPtr SfheContextState::alloc(size_t words) {
+    uint64_t* p = nullptr;
+    {
+        std::lock_guard<std::mutex> g(poolMu);
+        auto it = freeList.find(words);
+        if (it != freeList.end() && !it->second.empty()) {
+            p = it->second.back();
+            it->second.pop_back();
+        }
+    }
+    if (!p) {
+        p = (uint64_t*)sfp_alloc(dev, words * 8);
+        if (!p) {
+            // drop cached blocks and retry once
+            releaseAll();
+            p = (uint64_t*)sfp_alloc(dev, words * 8);
+            if (!p) SFHE_THROW("device allocation failed (" + std::to_string(words * 8) + " bytes)");
+        }
+        poolBytes += words * 8;
+    }
+    return std::make_shared<DeviceBuffer>(this, p, words);
+}
+
+void SfheContextState::releaseAll() {
+    std::lock_guard<std::mutex> g(poolMu);
+    sfp_sync(dev);
+    for (auto& kv : freeList)
+        for (auto* p : kv.second) {
+            sfp_free(dev, p);
+            poolBytes -= kv.first * 8;
+        }
+    freeList.clear();
+}
+
+// ============================================================================
+// internal helpers (friend of the context)
+
+class SfheInternal {
+  public:
+    using CC = CryptoContextImpl<DCRTPoly>;
+    using Ct = Ciphertext<DCRTPoly>;
+
+    static sfp_limbs Q(uint32_t ell) { return sfp_limbs{ell, ell, 0}; }
+    static sfp_limbs Range(uint32_t lo, uint32_t cnt) { return sfp_limbs{cnt, 0, lo}; }
+
+    static Ct newCt(CC* cc, uint32_t level, uint32_t slots) {
+        SfheContextState* s = cc->st.get();
+        auto ct = std::make_shared<CiphertextImpl<DCRTPoly>>();
+        uint32_t ell = s->ellOf(level);
+        ct->cc = cc->shared_from_this();
+        ct->buf = s->alloc((size_t)2 * ell * s->n);
+        ct->c0 = ct->buf->ptr;
+        ct->c1 = ct->c0 + (size_t)ell * s->n;
+        ct->level = level;
+        ct->slots = slots;
+        ct->scale = s->scale[level];
+        return ct;
+    }
+
+    static std::vector<u64> constResidues(SfheContextState* s, double v, uint32_t ell) {
+        std::vector<u64> k(ell);
+        for (uint32_t i = 0; i < ell; ++i) k[i] = residueOf(v, s->primes[i]);
+        return k;
+    }
+
+    // (c0,c1) at level l, ell limbs, any scale -> new ct at level l+1
+    static Ct rescale(CC* cc, const uint64_t* c0, const uint64_t* c1, uint32_t level,
+                      uint32_t slots) {
+        SfheContextState* s = cc->st.get();
+        uint32_t ell = s->ellOf(level);
+        if (ell < 2) SFHE_THROW("no levels left to rescale (multiplicative depth exhausted)");
+        Ct out = newCt(cc, level + 1, slots);
+        if (c1 - c0 < 0) SFHE_THROW("internal: layout");
+        sfp_rescale(s->dev, out->c0, c0, ell, s->qInvTable[ell].data(), 2, (size_t)(c1 - c0),
+                    (size_t)(out->c1 - out->c0));
+        s->stats.rescale++;
+        s->countBytes(4.0 * ell * s->n * 8 * 2 / 2);  // 4 l B per poly pair
+        return out;
+    }
+
+    // Align ct to targetLevel (>= its level) with a scale-exact adjustment.
+    static Ct adjust(CC* cc, const Ct& ct, uint32_t target) {
+        SfheContextState* s = cc->st.get();
+        if (target == ct->level) return ct;
+        if (target < ct->level) SFHE_THROW("cannot raise a ciphertext's level");
+        if (target > s->L) SFHE_THROW("target level beyond multiplicative depth");
+        uint32_t mid = target - 1;  // drop limbs (free), then one scaled rescale
+        uint32_t ell = s->ellOf(mid);
+        // result scale = scale_ct * K / q_{ell-1} = Delta_target
+        double K = s->scale[target] * (double)s->primes[ell - 1] / ct->scale;
+        auto k = constResidues(s, K, ell);
+        auto tmp = s->alloc((size_t)2 * ell * s->n);
+        uint64_t* t0 = tmp->ptr;
+        uint64_t* t1 = t0 + (size_t)ell * s->n;
+        sfp_mul_const(s->dev, t0, ct->c0, k.data(), Q(ell));
+        sfp_mul_const(s->dev, t1, ct->c1, k.data(), Q(ell));
+        s->stats.constmult++;
+        s->countBytes(4.0 * ell * s->n * 8);
+        return rescale(cc, t0, t1, mid, ct->slots);
+    }
+
+    static void align(CC* cc, Ct& a, Ct& b) {
+        uint32_t l = std::max(a->level, b->level);
+        a = adjust(cc, a, l);
+        b = adjust(cc, b, l);
+    }
+
+    // Hybrid key switch of d (ell limbs, evaluation domain) with `key`;
+    // adds the result into (out0, out1) (ell limbs each).
+    static void keySwitchAdd(CC* cc, const uint64_t* d, uint32_t ell, const DeviceBufferPtr& key,
+                             uint64_t* out0, uint64_t* out1) {
+        SfheContextState* s = cc->st.get();
+        const uint32_t n = s->n, K = s->K;
+        const uint32_t beta = (ell + s->alpha - 1) / s->alpha;
+        const size_t stride = (size_t)(ell + K) * n;
+        auto ext = s->alloc(stride * beta);
+        auto scratch = s->alloc((size_t)s->alpha * n);
+        auto& convs = modupConv(cc, ell);
+        for (uint32_t j = 0; j < beta; ++j) {
+            uint32_t lo = j * s->alpha, hi = std::min(lo + s->alpha, ell);
+            sfp_modup(s->dev, ext->ptr + j * stride, d, ell, K, s->Lq, lo, hi, convs[j],
+                      scratch->ptr);
+        }
+        innerAndModDown(cc, ext->ptr, stride, beta, ell, key, out0, out1);
+        s->stats.keyswitch++;
+        // (3 l + 2 beta (l+K)) B
+        s->countBytes((3.0 * ell + 2.0 * beta * (ell + K)) * n * 8);
+    }
+
+    static void innerAndModDown(CC* cc, const uint64_t* ext, size_t stride, uint32_t beta,
+                                uint32_t ell, const DeviceBufferPtr& key, uint64_t* out0,
+                                uint64_t* out1) {
+        SfheContextState* s = cc->st.get();
+        const uint32_t n = s->n, K = s->K;
+        auto acc = s->alloc((size_t)2 * (ell + K) * n);
+        uint64_t* acc0 = acc->ptr;
+        uint64_t* acc1 = acc0 + (size_t)(ell + K) * n;
+        sfp_ks_inner(s->dev, acc0, acc1, ext, stride, key->ptr, beta, ell, K, s->Lq);
+        auto scratch = s->alloc((size_t)(ell + K) * n);
+        sfp_moddown(s->dev, out0, acc0, ell, K, s->Lq, s->moddownConv, s->pInvModQ.data(), 1,
+                    scratch->ptr);
+        sfp_moddown(s->dev, out1, acc1, ell, K, s->Lq, s->moddownConv, s->pInvModQ.data(), 1,
+                    scratch->ptr);
+    }
+
+    static std::vector<sfp_conv*>& modupConv(CC* cc, uint32_t ell) {
+        SfheContextState* s = cc->st.get();
+        auto it = s->modupConv.find(ell);
+        if (it != s->modupConv.end()) return it->second;
+        std::vector<sfp_conv*> v;
+        uint32_t beta = (ell + s->alpha - 1) / s->alpha;
+        for (uint32_t j = 0; j < beta; ++j) {
+            uint32_t lo = j * s->alpha, hi = std::min(lo + s->alpha, ell);
+            std::vector<uint32_t> src, dst;
+            for (uint32_t i = lo; i < hi; ++i) src.push_back(i);
+            for (uint32_t i = 0; i < ell; ++i)
+                if (i < lo || i >= hi) dst.push_back(i);
+            for (uint32_t k = 0; k < s->K; ++k) dst.push_back(s->Lq + k);
+            v.push_back(makeConv(s, src, dst));
+        }
+        return s->modupConv[ell] = v;
+    }
+
+    static sfp_conv* makeConv(SfheContextState* s, const std::vector<uint32_t>& src,
+                              const std::vector<uint32_t>& dst) {
+        const uint32_t ns = (uint32_t)src.size(), nt = (uint32_t)dst.size();
+        std::vector<u64> inv(ns), mod((size_t)ns * nt);
+        for (uint32_t i = 0; i < ns; ++i) {
+            u64 qi = s->primes[src[i]];
+            u64 prod = 1;
+            for (uint32_t k = 0; k < ns; ++k)
+                if (k != i) prod = mulmod(prod, s->primes[src[k]] % qi, qi);
+            inv[i] = invmod(prod, qi);
+            for (uint32_t t = 0; t < nt; ++t) {
+                u64 pt = s->primes[dst[t]];
+                u64 pr = 1;
+                for (uint32_t k = 0; k < ns; ++k)
+                    if (k != i) pr = mulmod(pr, s->primes[src[k]] % pt, pt);
+                mod[(size_t)i * nt + t] = pr;
+            }
+        }
+        return sfp_upload_conv(s->dev, ns, src.data(), nt, dst.data(), inv.data(), mod.data());
+    }
+
+    // switching key from s' (device, Lq+K limbs, eval domain) to s
+    static DeviceBufferPtr genSwitchKey(CC* cc, const uint64_t* sPrime, const uint64_t* sk) {
+        SfheContextState* s = cc->st.get();
+        const uint32_t n = s->n, NP = s->Lq + s->K;
+        const sfp_limbs all{NP, NP, 0};
+        auto key = s->alloc((size_t)s->dnum * 2 * NP * n);
+        auto tmp = s->alloc((size_t)NP * n);
+        std::vector<int64_t> e(n);
+        for (uint32_t j = 0; j < s->dnum; ++j) {
+            uint64_t* b = key->ptr + (size_t)j * 2 * NP * n;
+            uint64_t* a = b + (size_t)NP * n;
+            sfp_sample_uniform(s->dev, a, all, s->nextSeed());
+            sampleCBD(s, e);
+            sfp_load_i64(s->dev, tmp->ptr, e.data(), all);
+            sfp_ntt(s->dev, tmp->ptr, all, 0);
+            // b = e - a s
+            sfp_mul(s->dev, b, a, sk, all);
+            sfp_sub(s->dev, b, tmp->ptr, b, all);
+            // + P * s' on the digit's q-limbs
+            uint32_t lo = j * s->alpha, hi = std::min(lo + s->alpha, s->Lq);
+            if (lo >= hi) continue;
+            std::vector<u64> pk(s->pModQ.begin() + lo, s->pModQ.begin() + hi);
+            sfp_mul_const(s->dev, tmp->ptr, sPrime + (size_t)lo * n, pk.data(),
+                          Range(lo, hi - lo));
+            sfp_add(s->dev, b + (size_t)lo * n, b + (size_t)lo * n, tmp->ptr, Range(lo, hi - lo));
+        }
+        return key;
+    }
+
+    static void sampleCBD(SfheContextState* s, std::vector<int64_t>& e) {
+        uint64_t seed = s->nextSeed();
+        for (size_t i = 0; i < e.size(); ++i) {
+            uint64_t r = sf_splitmix64(seed + i);
+            e[i] = (int64_t)__builtin_popcountll(r & 0xFFFFFull) -
+                   (int64_t)__builtin_popcountll((r >> 20) & 0xFFFFFull);
+        }
+    }
+    static void sampleTernary(SfheContextState* s, std::vector<int64_t>& v) {
+        uint64_t seed = s->nextSeed();
+        for (size_t i = 0; i < v.size(); ++i) {
+            uint64_t r = sf_splitmix64(seed + i);
+            v[i] = (int64_t)(r % 3) - 1;
+        }
+    }
+
+    // device encoding of a plaintext at `level` with scale Delta_level
+    static const uint64_t* encoded(CC* cc, const Plaintext& pt, uint32_t level) {
+        SfheContextState* s = cc->st.get();
+        std::lock_guard<std::mutex> g(pt->encMutex);
+        auto it = pt->encoded.find(level);
+        if (it != pt->encoded.end()) return it->second->ptr;
+        uint32_t ell = s->ellOf(level);
+        // context-level cache: identical (values, slots, level) encode identically
+        uint64_t h = 1469598103934665603ull;
+        if (s->ptCacheOn) {
+            auto mix = [&](uint64_t x) { h = (h ^ x) * 1099511628211ull; };
+            for (auto& c : pt->values) {
+                uint64_t b[2];
+                double re = c.real(), im = c.imag();
+                std::memcpy(&b[0], &re, 8);
+                std::memcpy(&b[1], &im, 8);
+                mix(b[0]);
+                mix(b[1]);
+            }
+            mix(pt->slots);
+            mix(level);
+            mix(pt->values.size());
+            auto ci = s->ptCache.find(h);
+            if (ci != s->ptCache.end())
+                for (auto& e : ci->second)
+                    if (e.slots == pt->slots && e.values == pt->values) {
+                        pt->encoded[level] = e.buf;
+                        return e.buf->ptr;
+                    }
+        }
+        std::vector<int64_t> coeffs;
+        ckks_encode(pt->values, pt->slots, s->n, s->scale[level], coeffs);
+        auto buf = s->alloc((size_t)ell * s->n);
+        sfp_load_i64(s->dev, buf->ptr, coeffs.data(), Q(ell));
+        sfp_ntt(s->dev, buf->ptr, Q(ell), 0);
+        pt->encoded[level] = buf;
+        if (s->ptCacheOn && s->ptCacheBytes + (size_t)ell * s->n * 8 <= s->ptCacheLimit) {
+            s->ptCache[h].push_back(PtCacheEntry{pt->values, pt->slots, buf});
+            s->ptCacheBytes += (size_t)ell * s->n * 8;
+        }
+        return buf->ptr;
+    }
+
+    static Ct copyOf(CC* cc, const Ct& a) {
+        SfheContextState* s = cc->st.get();
+        Ct out = newCt(cc, a->level, a->slots);
+        size_t bytes = (size_t)s->ellOf(a->level) * s->n * 8;
+        sfp_d2d(s->dev, out->c0, a->c0, bytes);
+        sfp_d2d(s->dev, out->c1, a->c1, bytes);
+        return out;
+    }
+    // make `a` exclusively owned before an in-place update
+    static void own(CC* cc, Ct& a) {
+        if (a->buf.use_count() > 1) {
+            Ct c = copyOf(cc, a);
+            a->buf = c->buf;
+            a->c0 = c->c0;
+            a->c1 = c->c1;
+        }
+    }
+};
+
+// ============================================================================
+// context construction
+
+CryptoContextImpl<DCRTPoly>::CryptoContextImpl(const CCParams<CryptoContextCKKSRNS>& p)
+    : st(new SfheContextState) {
+    SfheContextState& s = *st;
+    s.params = p;
+    s.L = p.GetMultiplicativeDepth();
+    s.Lq = s.L + 1;
+    s.seed = p.GetSeed();
+    const uint32_t sbits = p.GetScalingModSize();
+    const uint32_t fbits = p.GetFirstModSize();
+    if (sbits < 20 || sbits > 60) SFHE_THROW("scaling mod size must be in [20, 60]");
+    if (fbits < sbits || fbits > 60) SFHE_THROW("first mod size must be in [scale bits, 60]");
+    s.dnum = p.GetNumLargeDigits();
+    if (s.dnum == 0) s.dnum = s.Lq > 3 ? 3 : std::max<uint32_t>(1, s.Lq);
+    s.dnum = std::min(s.dnum, s.Lq);
+    s.alpha = (s.Lq + s.dnum - 1) / s.dnum;
+    s.dnum = (s.Lq + s.alpha - 1) / s.alpha;
+
+    uint32_t n = p.GetRingDim();
+    uint32_t batch = p.GetBatchSize();
+    bool secure = p.GetSecurityLevel() != HEStd_NotSet;
+    uint32_t logn_lo = 10;
+    if (n) {
+        if (n & (n - 1)) SFHE_THROW("ring dimension must be a power of two");
+        logn_lo = (uint32_t)__builtin_ctz(n);
+    } else if (batch) {
+        while ((1u << logn_lo) < 2 * batch) ++logn_lo;
+    }
+    for (uint32_t logn = logn_lo;; ++logn) {
+        if (logn > 17 && !n) SFHE_THROW("no ring dimension <= 2^17 satisfies the parameters");
+        const uint32_t N = 1u << logn;
+        const u64 m = 2ull * N;
+        std::set<u64> used;
+        std::vector<u64> q(s.Lq);
+        q[0] = primeBelow(1ull << fbits, m, used);
+        used.insert(q[0]);
+        std::vector<double> sc(s.Lq);
+        sc[0] = std::ldexp(1.0, (int)sbits);
+        for (uint32_t l = 0; l < s.L; ++l) {
+            double target = sc[l] * sc[l] / std::ldexp(1.0, (int)sbits);
+            u64 pr = primeNear(target, m, used);
+            used.insert(pr);
+            q[s.L - l] = pr;
+            sc[l + 1] = sc[l] * sc[l] / (double)pr;
+        }
+        // special primes: enough bits to cover the largest digit
+        double maxDigitBits = 0;
+        for (uint32_t j = 0; j < s.dnum; ++j) {
+            double b = 0;
+            for (uint32_t i = j * s.alpha; i < std::min((j + 1) * s.alpha, s.Lq); ++i)
+                b += std::log2((double)q[i]);
+            maxDigitBits = std::max(maxDigitBits, b);
+        }
+        uint32_t K = (uint32_t)std::ceil(maxDigitBits / 60.0);
+        std::vector<u64> P;
+        u64 bound = 1ull << 60;
+        for (uint32_t k = 0; k < K; ++k) {
+            u64 pr = primeBelow(bound, m, used);
+            used.insert(pr);
+            P.push_back(pr);
+            bound = pr;
+        }
+        double logQP = 0;
+        for (u64 x : q) logQP += std::log2((double)x);
+        for (u64 x : P) logQP += std::log2((double)x);
+        if (secure && logQP > maxLogQ128(logn)) {
+            if (n)
+                SFHE_THROW("The specified ring dimension (" + std::to_string(n) +
+                           ") does not comply with the HE standard recommendation (log2 QP = " +
+                           std::to_string(logQP) + " > " + std::to_string(maxLogQ128(logn)) +
+                           "); use HEStd_NotSet or a larger ring");
+            continue;
+        }
+        s.n = N;
+        s.logn = logn;
+        s.K = K;
+        s.primes = q;
+        s.primes.insert(s.primes.end(), P.begin(), P.end());
+        s.scale = sc;
+        break;
+    }
+    s.batch = batch ? batch : s.n / 2;
+    if (s.batch > s.n / 2) SFHE_THROW("batch size exceeds n/2");
+
+    const uint32_t NP = s.Lq + s.K;
+    for (u64 x : s.primes) s.bar.push_back(sf_make_barrett(x));
+
+    // NTT tables
+    std::vector<u64> psi((size_t)NP * s.n), psiS((size_t)NP * s.n), ipsi((size_t)NP * s.n),
+        ipsiS((size_t)NP * s.n), ninv(NP), ninvS(NP);
+    for (uint32_t i = 0; i < NP; ++i) {
+        u64 q = s.primes[i];
+        u64 w = findPsi(q, s.n);
+        u64 wi = invmod(w, q);
+        std::vector<u64> pw(s.n), ipw(s.n);
+        pw[0] = ipw[0] = 1;
+        for (uint32_t k = 1; k < s.n; ++k) {
+            pw[k] = mulmod(pw[k - 1], w, q);
+            ipw[k] = mulmod(ipw[k - 1], wi, q);
+        }
+        for (uint32_t k = 0; k < s.n; ++k) {
+            uint32_t r = sf_brev(k, s.logn);
+            size_t o = (size_t)i * s.n + k;
+            psi[o] = pw[r];
+            psiS[o] = sf_shoup_precomp(pw[r], q);
+            ipsi[o] = ipw[r];
+            ipsiS[o] = sf_shoup_precomp(ipw[r], q);
+        }
+        ninv[i] = invmod(s.n % q, q);
+        ninvS[i] = sf_shoup_precomp(ninv[i], q);
+    }
+    sfp_tables t;
+    t.logn = s.logn;
+    t.nprimes = NP;
+    t.primes = s.primes.data();
+    t.psi_rev = psi.data();
+    t.psi_rev_shoup = psiS.data();
+    t.ipsi_rev = ipsi.data();
+    t.ipsi_rev_shoup = ipsiS.data();
+    t.n_inv = ninv.data();
+    t.n_inv_shoup = ninvS.data();
+    s.dev = sfp_create(p.GetDevice(), &t);
+    if (!s.dev) SFHE_THROW(std::string("device backend '") + sfp_backend_name() + "' failed to initialise");
+
+    // P mod q_i, P^{-1} mod q_i
+    s.pModQ.resize(s.Lq);
+    s.pInvModQ.resize(s.Lq);
+    for (uint32_t i = 0; i < s.Lq; ++i) {
+        u64 qi = s.primes[i], pr = 1;
+        for (uint32_t k = 0; k < s.K; ++k) pr = mulmod(pr, s.primes[s.Lq + k] % qi, qi);
+        s.pModQ[i] = pr;
+        s.pInvModQ[i] = invmod(pr, qi);
+    }
+    {
+        std::vector<uint32_t> src, dst;
+        for (uint32_t k = 0; k < s.K; ++k) src.push_back(s.Lq + k);
+        for (uint32_t i = 0; i < s.Lq; ++i) dst.push_back(i);
+        s.moddownConv = SfheInternal::makeConv(&s, src, dst);
+    }
+    s.qInvTable.resize(s.Lq + 1);
+    for (uint32_t ell = 2; ell <= s.Lq; ++ell) {
+        u64 ql = s.primes[ell - 1];
+        for (uint32_t i = 0; i + 1 < ell; ++i)
+            s.qInvTable[ell].push_back(invmod(ql % s.primes[i], s.primes[i]));
+    }
+}
+
+CryptoContextImpl<DCRTPoly>::~CryptoContextImpl() {
+    if (!st) return;
+    st->relinKey.reset();
+    st->rotKeys.clear();
+    st->ptCache.clear();
+    for (auto& kv : st->modupConv)
+        for (auto* c : kv.second) sfp_free_conv(st->dev, c);
+    if (st->moddownConv) sfp_free_conv(st->dev, st->moddownConv);
+    st->releaseAll();
+    sfp_destroy(st->dev);
+}
+
+uint32_t CryptoContextImpl<DCRTPoly>::GetRingDimension() const { return st->n; }
+uint32_t CryptoContextImpl<DCRTPoly>::GetMultiplicativeDepth() const { return st->L; }
+EncodingParams CryptoContextImpl<DCRTPoly>::GetEncodingParams() const {
+    return std::make_shared<EncodingParamsImpl>(st->batch);
+}
+
+uint32_t CryptoContextImpl<DCRTPoly>::GaloisForRotation(int32_t r) const {
+    const int64_t half = st->n / 2;
+    int64_t rr = ((int64_t)r % half + half) % half;
+    return (uint32_t)powmod(5, (u64)rr, 2ull * st->n);
+}
+
+bool CryptoContextImpl<DCRTPoly>::HasRotationKey(int32_t r) const {
+    return st->rotKeys.count(GaloisForRotation(r)) > 0;
+}
+
+void CryptoContextImpl<DCRTPoly>::Synchronize() {
+    sfp_sync(st->dev);
+    const char* e = sfp_last_error(st->dev);
+    if (e) SFHE_THROW(std::string("device error: ") + e);
+}
+
+void CryptoContextImpl<DCRTPoly>::SetPlaintextCache(bool on) {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    st->ptCacheOn = on;
+    if (!on) {
+        st->ptCache.clear();
+        st->ptCacheBytes = 0;
+    }
+}
+
+CryptoContextImpl<DCRTPoly>::OpStats CryptoContextImpl<DCRTPoly>::GetOpStats() const {
+    return st->stats;
+}
+void CryptoContextImpl<DCRTPoly>::ResetOpStats() { st->stats = OpStats(); }
+
+// ============================================================================
+// keys
+
+KeyPair<DCRTPoly> CryptoContextImpl<DCRTPoly>::KeyGen() {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheContextState* s = st.get();
+    const uint32_t NP = s->Lq + s->K;
+    KeyPair<DCRTPoly> kp;
+    auto sk = std::make_shared<PrivateKeyImpl<DCRTPoly>>();
+    sk->cc = shared_from_this();
+    std::vector<int64_t> tern(s->n);
+    SfheInternal::sampleTernary(s, tern);
+    sk->ternary.assign(tern.begin(), tern.end());
+    sk->s = s->alloc((size_t)NP * s->n);
+    const sfp_limbs all{NP, NP, 0};
+    sfp_load_i64(s->dev, sk->s->ptr, tern.data(), all);
+    sfp_ntt(s->dev, sk->s->ptr, all, 0);
+
+    auto pk = std::make_shared<PublicKeyImpl<DCRTPoly>>();
+    pk->cc = shared_from_this();
+    const sfp_limbs q = SfheInternal::Q(s->Lq);
+    pk->a = s->alloc((size_t)s->Lq * s->n);
+    pk->b = s->alloc((size_t)s->Lq * s->n);
+    sfp_sample_uniform(s->dev, pk->a->ptr, q, s->nextSeed());
+    std::vector<int64_t> e(s->n);
+    SfheInternal::sampleCBD(s, e);
+    sfp_load_i64(s->dev, pk->b->ptr, e.data(), q);
+    sfp_ntt(s->dev, pk->b->ptr, q, 0);
+    auto t = s->alloc((size_t)s->Lq * s->n);
+    sfp_mul(s->dev, t->ptr, pk->a->ptr, sk->s->ptr, q);
+    sfp_sub(s->dev, pk->b->ptr, pk->b->ptr, t->ptr, q);
+    kp.publicKey = pk;
+    kp.secretKey = sk;
+    return kp;
+}
+
+void CryptoContextImpl<DCRTPoly>::EvalMultKeyGen(const PrivateKey<DCRTPoly>& sk) {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheContextState* s = st.get();
+    const uint32_t NP = s->Lq + s->K;
+    auto s2 = s->alloc((size_t)NP * s->n);
+    sfp_mul(s->dev, s2->ptr, sk->s->ptr, sk->s->ptr, sfp_limbs{NP, NP, 0});
+    s->relinKey = SfheInternal::genSwitchKey(this, s2->ptr, sk->s->ptr);
+}
+
+void CryptoContextImpl<DCRTPoly>::EvalRotateKeyGen(const PrivateKey<DCRTPoly>& sk,
+                                                   const std::vector<int32_t>& idx,
+                                                   const PublicKey<DCRTPoly>&) {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheContextState* s = st.get();
+    const uint32_t NP = s->Lq + s->K;
+    auto sg = s->alloc((size_t)NP * s->n);
+    for (int32_t r : idx) {
+        s->rotIndices.insert(r);
+        uint32_t gal = GaloisForRotation(r);
+        if (gal == 1 || s->rotKeys.count(gal)) continue;
+        sfp_automorph(s->dev, sg->ptr, sk->s->ptr, gal, sfp_limbs{NP, NP, 0});
+        s->rotKeys[gal] = SfheInternal::genSwitchKey(this, sg->ptr, sk->s->ptr);
+    }
+}
+
+void CryptoContextImpl<DCRTPoly>::ClearEvalMultKeys() {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    st->relinKey.reset();
+}
+void CryptoContextImpl<DCRTPoly>::ClearEvalAutomorphismKeys() {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    st->rotKeys.clear();
+    st->rotIndices.clear();
+}
+
+// ============================================================================
+// plaintexts, encryption, decryption
+
+Plaintext CryptoContextImpl<DCRTPoly>::MakeCKKSPackedPlaintext(const std::vector<double>& v,
+                                                               uint32_t scaleDeg, uint32_t level,
+                                                               const void* params,
+                                                               uint32_t slots) const {
+    std::vector<std::complex<double>> c(v.begin(), v.end());
+    return MakeCKKSPackedPlaintext(c, scaleDeg, level, params, slots);
+}
+
+Plaintext CryptoContextImpl<DCRTPoly>::MakeCKKSPackedPlaintext(
+    const std::vector<std::complex<double>>& v, uint32_t scaleDeg, uint32_t level, const void*,
+    uint32_t slots) const {
+    if (scaleDeg != 1) SFHE_THROW("only scale degree 1 plaintexts are supported");
+    if (!slots) slots = st->batch;
+    if (slots & (slots - 1)) SFHE_THROW("slot count must be a power of two");
+    if (slots > st->n / 2) SFHE_THROW("slot count exceeds n/2");
+    if (v.size() > slots)
+        SFHE_THROW("The size [" + std::to_string(v.size()) +
+                   "] of the vector with values should not be greater than slots [" +
+                   std::to_string(slots) + "]");
+    if (level > st->L) SFHE_THROW("plaintext level exceeds multiplicative depth");
+    return std::make_shared<PlaintextImpl>(v, slots, level);
+}
+
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::Encrypt(const PublicKey<DCRTPoly>& pk,
+                                                         const Plaintext& pt) {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheContextState* s = st.get();
+    if (!pk) SFHE_THROW("null public key");
+    const uint32_t level = pt->level, ell = s->ellOf(level);
+    const sfp_limbs q = SfheInternal::Q(ell);
+    const uint64_t* m = SfheInternal::encoded(this, pt, level);
+    auto ct = SfheInternal::newCt(this, level, pt->slots);
+    auto tmp = s->alloc((size_t)3 * ell * s->n);
+    uint64_t* v = tmp->ptr;
+    uint64_t* e0 = v + (size_t)ell * s->n;
+    uint64_t* e1 = e0 + (size_t)ell * s->n;
+    std::vector<int64_t> h(s->n);
+    SfheInternal::sampleTernary(s, h);
+    sfp_load_i64(s->dev, v, h.data(), q);
+    sfp_ntt(s->dev, v, q, 0);
+    SfheInternal::sampleCBD(s, h);
+    sfp_load_i64(s->dev, e0, h.data(), q);
+    sfp_ntt(s->dev, e0, q, 0);
+    SfheInternal::sampleCBD(s, h);
+    sfp_load_i64(s->dev, e1, h.data(), q);
+    sfp_ntt(s->dev, e1, q, 0);
+    sfp_mul_add(s->dev, ct->c0, v, pk->b->ptr, e0, q);
+    sfp_add(s->dev, ct->c0, ct->c0, m, q);
+    sfp_mul_add(s->dev, ct->c1, v, pk->a->ptr, e1, q);
+    return ct;
+}
+
+void CryptoContextImpl<DCRTPoly>::Decrypt(const PrivateKey<DCRTPoly>& sk,
+                                          const Ciphertext<DCRTPoly>& ct, Plaintext* out) {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheContextState* s = st.get();
+    if (!sk) SFHE_THROW("null secret key");
+    const uint32_t ell = s->ellOf(ct->level);
+    const uint32_t nl = std::min<uint32_t>(2, ell);
+    const sfp_limbs q = SfheInternal::Q(nl);
+    auto t = s->alloc((size_t)nl * s->n);
+    sfp_mul_add(s->dev, t->ptr, ct->c1, sk->s->ptr, ct->c0, q);
+    sfp_ntt(s->dev, t->ptr, q, 1);
+    std::vector<u64> h((size_t)nl * s->n);
+    sfp_d2h(s->dev, h.data(), t->ptr, h.size() * 8);
+    const char* err = sfp_last_error(s->dev);
+    if (err) SFHE_THROW(std::string("device error: ") + err);
+    std::vector<double> c(s->n);
+    const u64 q0 = s->primes[0];
+    if (nl == 1) {
+        for (uint32_t i = 0; i < s->n; ++i) {
+            u64 x = h[i];
+            double v = x > q0 / 2 ? -(double)(q0 - x) : (double)x;
+            c[i] = v / ct->scale;
+        }
+    } else {
+        const u64 q1 = s->primes[1];
+        const u64 q0inv = invmod(q0 % q1, q1);
+        const u128 Q = (u128)q0 * q1;
+        for (uint32_t i = 0; i < s->n; ++i) {
+            u64 a0 = h[i], a1 = h[s->n + i];
+            u64 d = (a1 + q1 - a0 % q1) % q1;
+            u128 x = (u128)a0 + (u128)q0 * mulmod(d, q0inv, q1);
+            double v = x > Q / 2 ? -(double)(Q - x) : (double)x;
+            c[i] = v / ct->scale;
+        }
+    }
+    std::vector<std::complex<double>> vals;
+    ckks_decode(c, ct->slots, s->n, vals);
+    auto pt = std::make_shared<PlaintextImpl>(vals, ct->slots, ct->level);
+    // precision estimate from the imaginary parts (inputs are real)
+    double var = 0;
+    for (auto& z : vals) var += z.imag() * z.imag();
+    double sd = std::sqrt(var / std::max<size_t>(1, vals.size()));
+    pt->logError = sd > 0 ? std::log2(sd) : -60.0;
+    pt->logPrecision = -pt->logError;
+    *out = pt;
+}
+
+const std::vector<double>& PlaintextImpl::GetRealPackedValue() const {
+    realCache.resize(std::min(length, values.size()));
+    for (size_t i = 0; i < realCache.size(); ++i) realCache[i] = values[i].real();
+    return realCache;
+}
+
+std::ostream& operator<<(std::ostream& os, const Plaintext& pt) {
+    const auto& v = pt->GetRealPackedValue();
+    os << "(";
+    for (size_t i = 0; i < v.size(); ++i) os << v[i] << (i + 1 < v.size() ? ", " : "");
+    return os << " ... )";
+}
+
+Ciphertext<DCRTPoly> CiphertextImpl<DCRTPoly>::Clone() const {
+    std::lock_guard<std::recursive_mutex> g(cc->state()->opMu);
+    auto self = std::make_shared<CiphertextImpl<DCRTPoly>>(*this);
+    return SfheInternal::copyOf(cc.get(), self);
+}
+
+uint32_t CiphertextImpl<DCRTPoly>::GetNumLimbs() const { return cc->state()->ellOf(level); }
+
+// ============================================================================
+// evaluator: additive
+
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalAdd(const Ciphertext<DCRTPoly>& a0,
+                                                         const Ciphertext<DCRTPoly>& b0) {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    auto a = a0, b = b0;
+    SfheInternal::align(this, a, b);
+    auto out = SfheInternal::newCt(this, a->level, std::max(a->slots, b->slots));
+    const uint32_t ell = st->ellOf(a->level);
+    sfp_add(st->dev, out->c0, a->c0, b->c0, SfheInternal::Q(ell));
+    sfp_add(st->dev, out->c1, a->c1, b->c1, SfheInternal::Q(ell));
+    st->stats.add++;
+    st->countBytes(6.0 * ell * st->n * 8);
+    return out;
+}
+
+void CryptoContextImpl<DCRTPoly>::EvalAddInPlace(Ciphertext<DCRTPoly>& a,
+                                                 const Ciphertext<DCRTPoly>& b0) {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    auto b = b0;
+    if (a->level != b->level || a->buf.use_count() > 1 || a->c1 - a->c0 != (ptrdiff_t)(st->ellOf(a->level) * st->n)) {
+        a = EvalAdd(a, b);
+        return;
+    }
+    const uint32_t ell = st->ellOf(a->level);
+    sfp_add(st->dev, a->c0, a->c0, b->c0, SfheInternal::Q(ell));
+    sfp_add(st->dev, a->c1, a->c1, b->c1, SfheInternal::Q(ell));
+    a->slots = std::max(a->slots, b->slots);
+    st->stats.add++;
+    st->countBytes(6.0 * ell * st->n * 8);
+}
+
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalAdd(const Ciphertext<DCRTPoly>& a,
+                                                         double c) {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    const uint32_t ell = st->ellOf(a->level);
+    auto out = SfheInternal::newCt(this, a->level, a->slots);
+    auto k = SfheInternal::constResidues(st.get(), c * a->scale, ell);
+    sfp_add_const(st->dev, out->c0, a->c0, k.data(), SfheInternal::Q(ell));
+    sfp_d2d(st->dev, out->c1, a->c1, (size_t)ell * st->n * 8);
+    st->stats.add++;
+    st->countBytes(4.0 * ell * st->n * 8);
+    return out;
+}
+
+void CryptoContextImpl<DCRTPoly>::EvalAddInPlace(Ciphertext<DCRTPoly>& a, double c) {
+    a = EvalAdd(a, c);
+}
+
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalAdd(const Ciphertext<DCRTPoly>& a,
+                                                         const Plaintext& p) {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    const uint32_t ell = st->ellOf(a->level);
+    const uint64_t* m = SfheInternal::encoded(this, p, a->level);
+    auto out = SfheInternal::newCt(this, a->level, std::max(a->slots, p->slots));
+    sfp_add(st->dev, out->c0, a->c0, m, SfheInternal::Q(ell));
+    sfp_d2d(st->dev, out->c1, a->c1, (size_t)ell * st->n * 8);
+    st->stats.add++;
+    st->countBytes(5.0 * ell * st->n * 8);
+    return out;
+}
+
+void CryptoContextImpl<DCRTPoly>::EvalAddInPlace(Ciphertext<DCRTPoly>& a, const Plaintext& p) {
+    a = EvalAdd(a, p);
+}
+
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalSub(const Ciphertext<DCRTPoly>& a0,
+                                                         const Ciphertext<DCRTPoly>& b0) {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    auto a = a0, b = b0;
+    SfheInternal::align(this, a, b);
+    auto out = SfheInternal::newCt(this, a->level, std::max(a->slots, b->slots));
+    const uint32_t ell = st->ellOf(a->level);
+    sfp_sub(st->dev, out->c0, a->c0, b->c0, SfheInternal::Q(ell));
+    sfp_sub(st->dev, out->c1, a->c1, b->c1, SfheInternal::Q(ell));
+    st->stats.add++;
+    st->countBytes(6.0 * ell * st->n * 8);
+    return out;
+}
+
+void CryptoContextImpl<DCRTPoly>::EvalSubInPlace(Ciphertext<DCRTPoly>& a,
+                                                 const Ciphertext<DCRTPoly>& b) {
+    a = EvalSub(a, b);
+}
+
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalNegate(const Ciphertext<DCRTPoly>& a) {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    const uint32_t ell = st->ellOf(a->level);
+    auto out = SfheInternal::newCt(this, a->level, a->slots);
+    sfp_neg(st->dev, out->c0, a->c0, SfheInternal::Q(ell));
+    sfp_neg(st->dev, out->c1, a->c1, SfheInternal::Q(ell));
+    st->countBytes(4.0 * ell * st->n * 8);
+    return out;
+}
+
+void CryptoContextImpl<DCRTPoly>::EvalNegateInPlace(Ciphertext<DCRTPoly>& a) { a = EvalNegate(a); }
+
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalSub(double c, const Ciphertext<DCRTPoly>& a) {
+    return EvalAdd(EvalNegate(a), c);
+}
+
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalSub(const Ciphertext<DCRTPoly>& a,
+                                                         const Plaintext& p) {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    const uint32_t ell = st->ellOf(a->level);
+    const uint64_t* m = SfheInternal::encoded(this, p, a->level);
+    auto out = SfheInternal::newCt(this, a->level, std::max(a->slots, p->slots));
+    sfp_sub(st->dev, out->c0, a->c0, m, SfheInternal::Q(ell));
+    sfp_d2d(st->dev, out->c1, a->c1, (size_t)ell * st->n * 8);
+    st->stats.add++;
+    st->countBytes(5.0 * ell * st->n * 8);
+    return out;
+}
+
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalSub(const Plaintext& p,
+                                                         const Ciphertext<DCRTPoly>& a) {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    const uint32_t ell = st->ellOf(a->level);
+    const uint64_t* m = SfheInternal::encoded(this, p, a->level);
+    auto out = SfheInternal::newCt(this, a->level, std::max(a->slots, p->slots));
+    sfp_sub(st->dev, out->c0, m, a->c0, SfheInternal::Q(ell));
+    sfp_neg(st->dev, out->c1, a->c1, SfheInternal::Q(ell));
+    st->stats.add++;
+    st->countBytes(5.0 * ell * st->n * 8);
+    return out;
+}
+
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalAddMany(
+    const std::vector<Ciphertext<DCRTPoly>>& v) {
+    if (v.empty()) SFHE_THROW("EvalAddMany of an empty vector");
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    std::vector<Ciphertext<DCRTPoly>> cur(v.begin(), v.end());
+    while (cur.size() > 1) {
+        std::vector<Ciphertext<DCRTPoly>> nxt;
+        for (size_t i = 0; i + 1 < cur.size(); i += 2) nxt.push_back(EvalAdd(cur[i], cur[i + 1]));
+        if (cur.size() & 1) nxt.push_back(cur.back());
+        cur.swap(nxt);
+    }
+    return cur[0]->buf.use_count() > 1 && cur[0] == v[0] ? cur[0]->Clone() : cur[0];
+}
+
+// ============================================================================
+// evaluator: multiplicative
+
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMult(const Ciphertext<DCRTPoly>& a,
+                                                          double c) {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheContextState* s = st.get();
+    const uint32_t ell = s->ellOf(a->level);
+    if (ell < 2) SFHE_THROW("no levels left (multiplicative depth exhausted)");
+    // integer K with scale_a * K / q_last = Delta_{l+1} * c
+    double K = c * s->scale[a->level + 1] * (double)s->primes[ell - 1] / a->scale;
+    auto k = SfheInternal::constResidues(s, K, ell);
+    auto tmp = s->alloc((size_t)2 * ell * s->n);
+    uint64_t* t0 = tmp->ptr;
+    uint64_t* t1 = t0 + (size_t)ell * s->n;
+    sfp_mul_const(s->dev, t0, a->c0, k.data(), SfheInternal::Q(ell));
+    sfp_mul_const(s->dev, t1, a->c1, k.data(), SfheInternal::Q(ell));
+    s->stats.constmult++;
+    s->countBytes(4.0 * ell * s->n * 8);
+    return SfheInternal::rescale(this, t0, t1, a->level, a->slots);
+}
+
+void CryptoContextImpl<DCRTPoly>::EvalMultInPlace(Ciphertext<DCRTPoly>& a, double c) {
+    a = EvalMult(a, c);
+}
+
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMult(const Ciphertext<DCRTPoly>& a,
+                                                          const Plaintext& p) {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheContextState* s = st.get();
+    const uint32_t ell = s->ellOf(a->level);
+    if (ell < 2) SFHE_THROW("no levels left (multiplicative depth exhausted)");
+    const uint64_t* m = SfheInternal::encoded(this, p, a->level);
+    auto tmp = s->alloc((size_t)2 * ell * s->n);
+    uint64_t* t0 = tmp->ptr;
+    uint64_t* t1 = t0 + (size_t)ell * s->n;
+    sfp_mul(s->dev, t0, a->c0, m, SfheInternal::Q(ell));
+    sfp_mul(s->dev, t1, a->c1, m, SfheInternal::Q(ell));
+    s->stats.ptmult++;
+    s->countBytes(5.0 * ell * s->n * 8);
+    return SfheInternal::rescale(this, t0, t1, a->level, std::max(a->slots, p->slots));
+}
+
+void CryptoContextImpl<DCRTPoly>::EvalMultInPlace(Ciphertext<DCRTPoly>& a, const Plaintext& p) {
+    a = EvalMult(a, p);
+}
+
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMult(const Ciphertext<DCRTPoly>& a0,
+                                                          const Ciphertext<DCRTPoly>& b0) {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheContextState* s = st.get();
+    if (!s->relinKey) SFHE_THROW("EvalMultKeyGen must be called before EvalMult");
+    auto a = a0, b = b0;
+    SfheInternal::align(this, a, b);
+    const uint32_t ell = s->ellOf(a->level);
+    if (ell < 2) SFHE_THROW("no levels left (multiplicative depth exhausted)");
+    auto t = s->alloc((size_t)3 * ell * s->n);
+    uint64_t* d0 = t->ptr;
+    uint64_t* d1 = d0 + (size_t)ell * s->n;
+    uint64_t* d2 = d1 + (size_t)ell * s->n;
+    sfp_tensor(s->dev, d0, d1, d2, a->c0, a->c1, b->c0, b->c1, SfheInternal::Q(ell));
+    s->stats.tensor++;
+    s->countBytes(7.0 * ell * s->n * 8);
+    SfheInternal::keySwitchAdd(this, d2, ell, s->relinKey, d0, d1);
+    return SfheInternal::rescale(this, d0, d1, a->level, std::max(a->slots, b->slots));
+}
+
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalSquare(const Ciphertext<DCRTPoly>& a) {
+    return EvalMult(a, a);
+}
+
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMultAddPlain(
+    const std::vector<Ciphertext<DCRTPoly>>& a, const std::vector<Plaintext>& p) {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheContextState* s = st.get();
+    if (a.empty() || a.size() != p.size()) SFHE_THROW("operand count mismatch");
+    uint32_t level = 0, slots = 0;
+    for (size_t i = 0; i < a.size(); ++i) {
+        level = std::max(level, a[i]->level);
+        slots = std::max(slots, std::max(a[i]->slots, p[i]->slots));
+    }
+    const uint32_t ell = s->ellOf(level);
+    if (ell < 2) SFHE_THROW("no levels left (multiplicative depth exhausted)");
+    std::vector<Ciphertext<DCRTPoly>> al(a.size());
+    std::vector<const uint64_t*> x0, x1, m;
+    for (size_t i = 0; i < a.size(); ++i) {
+        al[i] = SfheInternal::adjust(this, a[i], level);
+        x0.push_back(al[i]->c0);
+        x1.push_back(al[i]->c1);
+        m.push_back(SfheInternal::encoded(this, p[i], level));
+    }
+    auto tmp = s->alloc((size_t)2 * ell * s->n);
+    uint64_t* t0 = tmp->ptr;
+    uint64_t* t1 = t0 + (size_t)ell * s->n;
+    for (size_t done = 0; done < a.size(); done += SFP_MAX_WSUM) {
+        uint32_t take = (uint32_t)std::min<size_t>(SFP_MAX_WSUM, a.size() - done);
+        if (done == 0) {
+            sfp_mac_plain(s->dev, t0, x0.data(), m.data(), take, SfheInternal::Q(ell));
+            sfp_mac_plain(s->dev, t1, x1.data(), m.data(), take, SfheInternal::Q(ell));
+        } else {
+            auto part = s->alloc((size_t)2 * ell * s->n);
+            sfp_mac_plain(s->dev, part->ptr, x0.data() + done, m.data() + done, take, SfheInternal::Q(ell));
+            sfp_mac_plain(s->dev, part->ptr + (size_t)ell * s->n, x1.data() + done, m.data() + done, take,
+                          SfheInternal::Q(ell));
+            sfp_add(s->dev, t0, t0, part->ptr, SfheInternal::Q(ell));
+            sfp_add(s->dev, t1, t1, part->ptr + (size_t)ell * s->n, SfheInternal::Q(ell));
+        }
+    }
+    s->stats.ptmult += a.size();
+    s->countBytes((3.0 * a.size() + 2.0) * ell * s->n * 8);
+    return SfheInternal::rescale(this, t0, t1, level, slots);
+}
+
+// ============================================================================
+// rotations
+
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotate(const Ciphertext<DCRTPoly>& a,
+                                                            int32_t r) {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheContextState* s = st.get();
+    uint32_t gal = GaloisForRotation(r);
+    if (gal == 1) return a->Clone();
+    auto it = s->rotKeys.find(gal);
+    if (it == s->rotKeys.end())
+        SFHE_THROW("EvalKey for index [" + std::to_string(gal) + "] (rotation " +
+                   std::to_string(r) + ") is not found");
+    const uint32_t ell = s->ellOf(a->level);
+    auto out = SfheInternal::newCt(this, a->level, a->slots);
+    auto t = s->alloc((size_t)ell * s->n);
+    sfp_automorph(s->dev, out->c0, a->c0, gal, SfheInternal::Q(ell));
+    sfp_automorph(s->dev, t->ptr, a->c1, gal, SfheInternal::Q(ell));
+    sfp_zero(s->dev, out->c1, (size_t)ell * s->n * 8);
+    s->stats.automorph++;
+    s->countBytes(3.0 * ell * s->n * 8);
+    SfheInternal::keySwitchAdd(this, t->ptr, ell, it->second, out->c0, out->c1);
+    return out;
+}
+
+std::shared_ptr<FastRotationPrecomp> CryptoContextImpl<DCRTPoly>::EvalFastRotationPrecompute(
+    const Ciphertext<DCRTPoly>& a) {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheContextState* s = st.get();
+    auto pre = std::make_shared<FastRotationPrecomp>();
+    const uint32_t ell = s->ellOf(a->level);
+    pre->level = a->level;
+    pre->beta = (ell + s->alpha - 1) / s->alpha;
+    pre->stride = (size_t)(ell + s->K) * s->n;
+    pre->ext = s->alloc(pre->stride * pre->beta);
+    auto scratch = s->alloc((size_t)s->alpha * s->n);
+    auto& convs = SfheInternal::modupConv(this, ell);
+    for (uint32_t j = 0; j < pre->beta; ++j) {
+        uint32_t lo = j * s->alpha, hi = std::min(lo + s->alpha, ell);
+        sfp_modup(s->dev, pre->ext->ptr + j * pre->stride, a->c1, ell, s->K, s->Lq, lo, hi,
+                  convs[j], scratch->ptr);
+    }
+    return pre;
+}
+
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalFastRotation(
+    const Ciphertext<DCRTPoly>& a, int32_t r, uint32_t, const std::shared_ptr<FastRotationPrecomp>& pre) {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheContextState* s = st.get();
+    uint32_t gal = GaloisForRotation(r);
+    if (gal == 1) return a->Clone();
+    if (!pre || pre->level != a->level) SFHE_THROW("fast-rotation precomputation does not match");
+    auto it = s->rotKeys.find(gal);
+    if (it == s->rotKeys.end())
+        SFHE_THROW("EvalKey for rotation " + std::to_string(r) + " is not found");
+    const uint32_t ell = s->ellOf(a->level);
+    // sigma commutes with the (coefficient-wise) base extension, so rotating
+    // the extended digits equals extending the rotated c1.
+    auto ext = s->alloc(pre->stride * pre->beta);
+    const sfp_limbs em{ell + s->K, ell, s->Lq};
+    for (uint32_t j = 0; j < pre->beta; ++j)
+        sfp_automorph(s->dev, ext->ptr + j * pre->stride, pre->ext->ptr + j * pre->stride, gal, em);
+    auto out = SfheInternal::newCt(this, a->level, a->slots);
+    sfp_automorph(s->dev, out->c0, a->c0, gal, SfheInternal::Q(ell));
+    sfp_zero(s->dev, out->c1, (size_t)ell * s->n * 8);
+    SfheInternal::innerAndModDown(this, ext->ptr, pre->stride, pre->beta, ell, it->second,
+                                  out->c0, out->c1);
+    s->stats.keyswitch++;
+    s->stats.automorph++;
+    s->countBytes((3.0 * ell + 2.0 * pre->beta * (ell + s->K)) * s->n * 8);
+    return out;
+}
+
+// ============================================================================
+// fused weighted sum (Chebyshev leaves, EvalPolyLinear)
+
+// sum_j w_j * (c0_j, c1_j) at `level` (canonical scale), then one rescale
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::LinearWSumRescale(
+    const std::vector<const uint64_t*>& in0, const std::vector<const uint64_t*>& in1,
+    const std::vector<double>& w, uint32_t level, uint32_t slots) {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheContextState* s = st.get();
+    const uint32_t ell = s->ellOf(level);
+    if (ell < 2) SFHE_THROW("no levels left (multiplicative depth exhausted)");
+    auto tmp = s->alloc((size_t)2 * ell * s->n);
+    uint64_t* t0 = tmp->ptr;
+    uint64_t* t1 = t0 + (size_t)ell * s->n;
+    const sfp_limbs q{ell, ell, 0};
+    // chunks of SFP_MAX_WSUM terms accumulate through the extra "previous sum" input
+    size_t done = 0;
+    bool first = true;
+    while (done < w.size()) {
+        size_t take = std::min<size_t>(w.size() - done, SFP_MAX_WSUM - (first ? 0 : 1));
+        std::vector<const uint64_t*> a0, a1;
+        std::vector<uint64_t> kk;
+        if (!first) {
+            a0.push_back(t0);
+            a1.push_back(t1);
+            for (uint32_t i = 0; i < ell; ++i) kk.push_back(1);
+        }
+        for (size_t j = done; j < done + take; ++j) {
+            a0.push_back(in0[j]);
+            a1.push_back(in1[j]);
+            double K = w[j] * s->scale[level];  // product scale Delta_l^2 -> rescale -> Delta_{l+1}
+            for (uint32_t i = 0; i < ell; ++i) {
+                u64 q = s->primes[i];
+                double r = std::nearbyint(K);
+                bool neg = r < 0;
+                double a = std::fabs(r);
+                u128 v;
+                if (a < 1.8e19) v = (u128)(u64)a;
+                else {
+                    double hi = std::floor(std::ldexp(a, -64));
+                    v = ((u128)(u64)hi << 64) + (u128)(u64)(a - std::ldexp(hi, 64));
+                }
+                u64 m = (u64)(v % q);
+                kk.push_back(neg ? (m ? q - m : 0) : m);
+            }
+        }
+        sfp_lin_wsum(s->dev, t0, a0.data(), kk.data(), (uint32_t)a0.size(), q);
+        sfp_lin_wsum(s->dev, t1, a1.data(), kk.data(), (uint32_t)a1.size(), q);
+        s->stats.wsum_terms += take;
+        s->countBytes((double)(a0.size() + 1) * 2.0 * ell * s->n * 8);
+        done += take;
+        first = false;
+    }
+    return SfheInternal::rescale(this, t0, t1, level, slots);
+}
+
+
+// ============================================================================
+// level management
+
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::Rescale(const Ciphertext<DCRTPoly>& a) {
+    return a->Clone();  // automatic rescaling: nothing pending
+}
+
+void CryptoContextImpl<DCRTPoly>::LevelReduceInPlace(Ciphertext<DCRTPoly>& a, std::nullptr_t,
+                                                     size_t levels) {
+    a = AdjustLevel(a, a->level + (uint32_t)levels);
+}
+
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::AdjustLevel(const Ciphertext<DCRTPoly>& a,
+                                                             uint32_t targetLevel) {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    auto r = SfheInternal::adjust(this, a, targetLevel);
+    return r == a ? a->Clone() : r;
+}
+
+// ============================================================================
+// bootstrapping: the k-way / bitonic rows are next;
+// link-compatible entry points throw until then.
+
+void CryptoContextImpl<DCRTPoly>::EvalBootstrapSetup(std::vector<uint32_t>, std::vector<uint32_t>,
+                                                     uint32_t, uint32_t) {
+    SFHE_THROW("CKKS bootstrapping is not implemented in this engine yet (SURVEY §8(f) rank 2)");
+}
+void CryptoContextImpl<DCRTPoly>::EvalBootstrapKeyGen(const PrivateKey<DCRTPoly>&, uint32_t) {
+    SFHE_THROW("CKKS bootstrapping is not implemented in this engine yet (SURVEY §8(f) rank 2)");
+}
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalBootstrap(const Ciphertext<DCRTPoly>&,
+                                                               uint32_t, uint32_t) {
+    SFHE_THROW("CKKS bootstrapping is not implemented in this engine yet (SURVEY §8(f) rank 2)");
+}
+
+}  // namespace lbcrypto

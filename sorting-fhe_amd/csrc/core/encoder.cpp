@@ -1,0 +1,129 @@
+// CKKS canonical-embedding encoder (host).
+//
+// Slot j of a plaintext m(X) is m(zeta^(5^j)), zeta = exp(i*pi/n), so the
+// automorphism X -> X^(5^r) is a left rotation by r (OpenFHE convention,
+// SURVEY.md §8(a) a-12(ii)).  A vector of `slots` < n/2 values is packed
+// sparsely: m(X) = sum_t u_t X^(t*gap), gap = n/(2*slots), which replicates
+// the vector with period `slots` across all n/2 slots (a-12(i)).
+// The transform is the standard O(S log S) "special FFT" over the rotation
+// group <5> mod 2n (Cheon-Kim-Kim-Song).
+#include <cmath>
+#include <complex>
+#include <vector>
+
+#include "state.h"
+
+namespace lbcrypto {
+
+namespace {
+
+struct FFTTables {
+    uint32_t n = 0;
+    std::vector<uint64_t> rot;                  // 5^j mod 2n, j < n/2
+    std::vector<std::complex<double>> ksi;      // exp(2 pi i k / 2n), k <= 2n
+};
+
+const FFTTables& tables(uint32_t n) {
+    static std::mutex mu;
+    static std::map<uint32_t, std::unique_ptr<FFTTables>> cache;
+    std::lock_guard<std::mutex> g(mu);
+    auto& t = cache[n];
+    if (!t) {
+        t.reset(new FFTTables);
+        t->n = n;
+        const uint64_t M = 2ull * n;
+        t->rot.resize(n / 2);
+        uint64_t g5 = 1;
+        for (uint32_t j = 0; j < n / 2; ++j) {
+            t->rot[j] = g5;
+            g5 = (g5 * 5) % M;
+        }
+        t->ksi.resize(M + 1);
+        for (uint64_t k = 0; k <= M; ++k) {
+            double a = 2.0 * M_PI * (double)k / (double)M;
+            t->ksi[k] = std::complex<double>(std::cos(a), std::sin(a));
+        }
+    }
+    return *t;
+}
+
+void bitReverse(std::complex<double>* v, uint32_t size) {
+    for (uint32_t i = 1, j = 0; i < size; ++i) {
+        uint32_t bit = size >> 1;
+        for (; j >= bit; bit >>= 1) j -= bit;
+        j += bit;
+        if (i < j) std::swap(v[i], v[j]);
+    }
+}
+
+// slots -> coefficient pairs
+void fftSpecialInv(std::complex<double>* v, uint32_t size, const FFTTables& t) {
+    const uint64_t M = 2ull * t.n;
+    for (uint32_t len = size; len >= 1; len >>= 1) {
+        for (uint32_t i = 0; i < size; i += len) {
+            uint32_t lenh = len >> 1;
+            uint64_t lenq = (uint64_t)len << 2;
+            for (uint32_t j = 0; j < lenh; ++j) {
+                uint64_t idx = (lenq - (t.rot[j] % lenq)) * M / lenq;
+                std::complex<double> u = v[i + j] + v[i + j + lenh];
+                std::complex<double> w = (v[i + j] - v[i + j + lenh]) * t.ksi[idx];
+                v[i + j] = u;
+                v[i + j + lenh] = w;
+            }
+        }
+    }
+    bitReverse(v, size);
+    for (uint32_t i = 0; i < size; ++i) v[i] /= (double)size;
+}
+
+// coefficient pairs -> slots
+void fftSpecial(std::complex<double>* v, uint32_t size, const FFTTables& t) {
+    const uint64_t M = 2ull * t.n;
+    bitReverse(v, size);
+    for (uint32_t len = 2; len <= size; len <<= 1) {
+        for (uint32_t i = 0; i < size; i += len) {
+            uint32_t lenh = len >> 1;
+            uint64_t lenq = (uint64_t)len << 2;
+            for (uint32_t j = 0; j < lenh; ++j) {
+                uint64_t idx = (t.rot[j] % lenq) * M / lenq;
+                std::complex<double> u = v[i + j];
+                std::complex<double> w = v[i + j + lenh] * t.ksi[idx];
+                v[i + j] = u + w;
+                v[i + j + lenh] = u - w;
+            }
+        }
+    }
+}
+
+}  // namespace
+
+void ckks_encode(const std::vector<std::complex<double>>& vals, uint32_t slots, uint32_t n,
+                 double scale, std::vector<int64_t>& coeffs) {
+    const FFTTables& t = tables(n);
+    std::vector<std::complex<double>> u(slots, 0.0);
+    for (size_t i = 0; i < vals.size() && i < slots; ++i) u[i] = vals[i];
+    fftSpecialInv(u.data(), slots, t);
+    coeffs.assign(n, 0);
+    const uint32_t gap = (n / 2) / slots;
+    const double lim = 9.0e18;
+    for (uint32_t i = 0; i < slots; ++i) {
+        double re = std::nearbyint(u[i].real() * scale);
+        double im = std::nearbyint(u[i].imag() * scale);
+        if (std::fabs(re) > lim || std::fabs(im) > lim)
+            SFHE_THROW("encoded value exceeds 63 bits (|value * scale| too large)");
+        coeffs[(size_t)i * gap] = (int64_t)re;
+        coeffs[(size_t)n / 2 + (size_t)i * gap] = (int64_t)im;
+    }
+}
+
+void ckks_decode(const std::vector<double>& c, uint32_t slots, uint32_t n,
+                 std::vector<std::complex<double>>& out) {
+    const FFTTables& t = tables(n);
+    const uint32_t gap = (n / 2) / slots;
+    out.assign(slots, 0.0);
+    for (uint32_t i = 0; i < slots; ++i)
+        out[i] = std::complex<double>(c[(size_t)i * gap], c[(size_t)n / 2 + (size_t)i * gap]);
+    fftSpecial(out.data(), slots, t);
+}
+
+}  // namespace lbcrypto

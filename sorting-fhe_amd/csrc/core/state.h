@@ -1,0 +1,96 @@
+// Internal state of a CKKS context (not part of the public API).
+#pragma once
+#include <atomic>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <unordered_map>
+#include <vector>
+
+#include "../modarith.h"
+#include "openfhe.h"
+
+namespace lbcrypto {
+
+class DeviceBuffer {
+  public:
+    DeviceBuffer(SfheContextState* s, uint64_t* p, size_t w) : st(s), ptr(p), words(w) {}
+    ~DeviceBuffer();
+    SfheContextState* st;
+    uint64_t* ptr;
+    size_t words;
+};
+
+struct PtCacheEntry {
+    std::vector<std::complex<double>> values;
+    uint32_t slots;
+    DeviceBufferPtr buf;
+};
+
+struct SfheContextState {
+    CCParams<CryptoContextCKKSRNS> params;
+    uint32_t n = 0, logn = 0;
+    uint32_t L = 0;   // multiplicative depth
+    uint32_t Lq = 0;  // number of Q primes = L+1
+    uint32_t K = 0;   // number of P primes
+    uint32_t dnum = 0, alpha = 0;
+    uint32_t batch = 0;
+    std::vector<uint64_t> primes;  // [q_0..q_L, p_0..p_{K-1}]
+    std::vector<sf_barrett> bar;
+    std::vector<double> scale;  // canonical scale of each level 0..L
+    sfp_dev* dev = nullptr;
+
+    // base-conversion tables
+    std::map<uint32_t, std::vector<sfp_conv*>> modupConv;  // ell -> per digit
+    sfp_conv* moddownConv = nullptr;                        // P -> Q (all Lq targets)
+    std::vector<uint64_t> pInvModQ;                         // P^{-1} mod q_i
+    std::vector<uint64_t> pModQ;                            // P mod q_i
+    std::vector<std::vector<uint64_t>> qInvTable;  // [ell][i] = q_{ell-1}^{-1} mod q_i
+
+    // keys
+    DeviceBufferPtr relinKey;
+    std::map<uint32_t, DeviceBufferPtr> rotKeys;  // galois -> key
+    std::set<int32_t> rotIndices;
+
+    // memory pool (device words -> free list)
+    std::mutex poolMu;
+    std::map<size_t, std::vector<uint64_t*>> freeList;
+    size_t poolBytes = 0;
+
+    // serialises host-side use of the device from OpenMP callers
+    std::recursive_mutex opMu;
+
+    // plaintext encode cache (content -> device polynomial per level)
+    bool ptCacheOn = true;
+    size_t ptCacheBytes = 0;
+    size_t ptCacheLimit = (size_t)48 << 30;
+    std::unordered_map<uint64_t, std::vector<PtCacheEntry>> ptCache;  // key hash (incl. level)
+
+    std::atomic<uint64_t> seedCounter{1};
+    uint64_t seed = 0;
+    CryptoContextImpl<DCRTPoly>::OpStats stats;
+
+    // ---- helpers ----
+    uint32_t ellOf(uint32_t level) const { return Lq - level; }
+    uint64_t nextSeed() { return seed ^ (0x9E3779B97F4A7C15ULL * (seedCounter++)); }
+    DeviceBufferPtr alloc(size_t words);
+    void releaseAll();
+    void countBytes(double b) { stats.algo_bytes += b; }
+};
+
+// splitmix64 (used for deterministic host sampling; identical in the oracle)
+static inline uint64_t sf_splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ULL;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    return x ^ (x >> 31);
+}
+
+// CKKS special-FFT encoder (encoder.cpp)
+void ckks_encode(const std::vector<std::complex<double>>& v, uint32_t slots, uint32_t n,
+                 double scale, std::vector<int64_t>& coeffs);
+void ckks_decode(const std::vector<double>& coeffs, uint32_t slots, uint32_t n,
+                 std::vector<std::complex<double>>& out);
+
+}  // namespace lbcrypto

@@ -1,0 +1,158 @@
+// RNS polynomial primitive layer (L1 in SURVEY.md §1).
+//
+// Two implementations exist and are bit-for-bit interchangeable:
+//   * csrc/hip/prims_hip.hip  -- the product: hand-written gfx950 kernels;
+//   * oracle/prims_ref.c      -- the CPU oracle (test infrastructure only).
+// The host CKKS layer (csrc/core/*.cpp) is compiled against this interface
+// once per backend.  The product library never contains the oracle.
+//
+// Data layout (HBM): a polynomial with L limbs is L contiguous rows of n u64
+// residues, limb-major: limb i at base + i*n.  A ciphertext is two such
+// polynomials back to back (c0 rows, then c1 rows).  Limb i of a polynomial
+// uses prime index  i < split ? i : pbase + (i - split)  in the context's
+// prime table [q_0 .. q_L, p_0 .. p_{K-1}] (the "limb map").
+//
+// Every primitive is enqueued on the backend's stream; the host observes
+// results only through sfp_d2h (which synchronises).
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SFP_MAX_LIMBS 96
+#define SFP_MAX_WSUM 80
+
+typedef struct sfp_dev sfp_dev;
+
+typedef struct {
+    uint32_t count;  // number of limbs
+    uint32_t split;  // limbs [0, split) -> primes [0, split)
+    uint32_t pbase;  // limbs [split, count) -> primes [pbase, ...)
+} sfp_limbs;
+
+// Tables the host computes once per context (identical for both backends).
+typedef struct {
+    uint32_t logn;
+    uint32_t nprimes;       // L+1+K
+    const uint64_t* primes; // nprimes
+    // per prime, n entries each (bit-reversed psi powers, OpenFHE/SEAL layout)
+    const uint64_t* psi_rev;        // [nprimes][n]
+    const uint64_t* psi_rev_shoup;  // [nprimes][n]
+    const uint64_t* ipsi_rev;       // [nprimes][n]
+    const uint64_t* ipsi_rev_shoup; // [nprimes][n]
+    const uint64_t* n_inv;          // [nprimes]
+    const uint64_t* n_inv_shoup;    // [nprimes]
+} sfp_tables;
+
+// Base-conversion table for fast basis extension from a source set S of
+// primes to a target set T (Halevi-Polyakov-Shoup / OpenFHE "PartQlHat"):
+//   y_i  = x_i * shat_inv[i] mod s_i                 (i in S)
+//   out_t = sum_i y_i * shat_mod[i][t] mod t          (t in T)
+// where shat = prod(S) / s_i.  Lives in backend memory (sfp_upload_conv).
+typedef struct sfp_conv sfp_conv;
+
+// ---- lifetime / memory --------------------------------------------------
+sfp_dev* sfp_create(int device, const sfp_tables* t);
+void sfp_destroy(sfp_dev* d);
+const char* sfp_backend_name(void);
+void* sfp_alloc(sfp_dev* d, size_t bytes);
+void sfp_free(sfp_dev* d, void* p);
+void sfp_h2d(sfp_dev* d, void* dst, const void* src, size_t bytes);
+void sfp_d2h(sfp_dev* d, void* dst, const void* src, size_t bytes);
+void sfp_d2d(sfp_dev* d, void* dst, const void* src, size_t bytes);
+void sfp_zero(sfp_dev* d, void* dst, size_t bytes);
+void sfp_sync(sfp_dev* d);
+// Returns 0 if no asynchronous error is pending; otherwise an error string.
+const char* sfp_last_error(sfp_dev* d);
+
+// ---- NTT ----------------------------------------------------------------
+// In-place negacyclic NTT of every limb (forward: coefficient -> evaluation
+// at psi^(2*brev(k)+1); inverse includes the 1/n factor).
+void sfp_ntt(sfp_dev* d, uint64_t* p, sfp_limbs m, int inverse);
+
+// ---- elementwise ----------------------------------------------------------
+void sfp_add(sfp_dev* d, uint64_t* out, const uint64_t* a, const uint64_t* b, sfp_limbs m);
+void sfp_sub(sfp_dev* d, uint64_t* out, const uint64_t* a, const uint64_t* b, sfp_limbs m);
+void sfp_neg(sfp_dev* d, uint64_t* out, const uint64_t* a, sfp_limbs m);
+void sfp_mul(sfp_dev* d, uint64_t* out, const uint64_t* a, const uint64_t* b, sfp_limbs m);
+// out = a * b + c  (pointwise)
+void sfp_mul_add(sfp_dev* d, uint64_t* out, const uint64_t* a, const uint64_t* b,
+                 const uint64_t* c, sfp_limbs m);
+// out[i] = a[i] * k[limb] (k: host array of m.count residues)
+void sfp_mul_const(sfp_dev* d, uint64_t* out, const uint64_t* a, const uint64_t* k,
+                   sfp_limbs m);
+// out[i] = a[i] + k[limb]
+void sfp_add_const(sfp_dev* d, uint64_t* out, const uint64_t* a, const uint64_t* k,
+                   sfp_limbs m);
+// Ciphertext tensor: d0 = a0 b0, d1 = a0 b1 + a1 b0, d2 = a1 b1
+void sfp_tensor(sfp_dev* d, uint64_t* d0, uint64_t* d1, uint64_t* d2, const uint64_t* a0,
+                const uint64_t* a1, const uint64_t* b0, const uint64_t* b1, sfp_limbs m);
+// out = sum_j ins[j] * k[j][limb]  (+ k0[limb] if k0 != NULL), j < nin <= SFP_MAX_WSUM.
+// ins: host array of device pointers; k: host array nin x m.count.
+void sfp_lin_wsum(sfp_dev* d, uint64_t* out, const uint64_t* const* ins, const uint64_t* k,
+                  uint32_t nin, sfp_limbs m);
+
+// out = sum_j a[j] * b[j]  (pointwise products summed, nin <= SFP_MAX_WSUM).
+// a, b: host arrays of device pointers.
+void sfp_mac_plain(sfp_dev* d, uint64_t* out, const uint64_t* const* a, const uint64_t* const* b,
+                   uint32_t nin, sfp_limbs m);
+
+// ---- automorphism ----------------------------------------------------------
+// out = sigma_g(in) in the evaluation domain (g odd, < 2n); out != in.
+void sfp_automorph(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t galois, sfp_limbs m);
+
+// ---- rescale ------------------------------------------------------------------
+// in: ell limbs (evaluation domain, limb map identity); out: ell-1 limbs,
+//   out_i = (in_i - [in_last]_{q_i}) * q_last^{-1} mod q_i   (in_last taken in
+//   coefficient domain with the rounding offset floor(q_last/2)).
+// qlinv: host array ell-1 of q_last^{-1} mod q_i.  npoly polynomials (stride
+// in_stride / out_stride u64) are processed.
+void sfp_rescale(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t ell, const uint64_t* qlinv,
+                 uint32_t npoly, size_t in_stride, size_t out_stride);
+
+// ---- basis conversion / key switching ----------------------------------------
+// Upload a conversion table: ns source primes (prime indices src_idx), nt
+// target primes (dst_idx); shat_inv[ns], shat_mod[ns][nt].
+sfp_conv* sfp_upload_conv(sfp_dev* d, uint32_t ns, const uint32_t* src_idx, uint32_t nt,
+                          const uint32_t* dst_idx, const uint64_t* shat_inv,
+                          const uint64_t* shat_mod);
+void sfp_free_conv(sfp_dev* d, sfp_conv* c);
+// Fast base conversion in the COEFFICIENT domain: src has ns rows, dst nt rows.
+void sfp_conv_apply(sfp_dev* d, uint64_t* dst, const uint64_t* src, const sfp_conv* c);
+
+// Hybrid key-switch ModUp for one digit (evaluation domain in and out).
+//   in   : ell limbs (limb map identity), evaluation domain.
+//   out  : ell+K limbs (limb map split=ell, pbase=L+1).  Limbs of the digit
+//          [lo, hi) are copied; all others are Conv(INTT(in[lo,hi))) then NTT.
+//   scratch: at least (hi-lo) * n words.
+void sfp_modup(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t ell, uint32_t K,
+               uint32_t Lq, uint32_t lo, uint32_t hi, const sfp_conv* c, uint64_t* scratch);
+
+// Key inner product:  acc0 = sum_j ext_j * kb_j,  acc1 = sum_j ext_j * ka_j
+//   ext  : beta extended polys, each (ell+K) limbs, stride ext_stride.
+//   key  : beta digits, each [b rows (Lq+K)][a rows (Lq+K)]; ext limb t maps to
+//          key row t (t < ell) or Lq + (t - ell).
+void sfp_ks_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
+                  size_t ext_stride, const uint64_t* key, uint32_t beta, uint32_t ell, uint32_t K,
+                  uint32_t Lq);
+
+// ModDown:  out_i (+)= (acc_i - NTT(Conv_{P->Q}(INTT(acc_P)))_i) * pinv_i
+//   acc : ell+K limbs (split=ell, pbase=Lq), evaluation domain; destroyed.
+//   out : ell limbs.  If add != 0 the result is added into out.
+//   pinv: host array ell of P^{-1} mod q_i.  scratch: (ell+K)*n words.
+void sfp_moddown(sfp_dev* d, uint64_t* out, uint64_t* acc, uint32_t ell, uint32_t K, uint32_t Lq,
+                 const sfp_conv* c, const uint64_t* pinv, int add, uint64_t* scratch);
+
+// ---- sampling (counter-based, deterministic) ------------------------------------
+// Uniform residues mod each limb's prime: value for (limb, i) is derived from
+// splitmix64(seed, stream-id = prime index, i); identical on every backend.
+void sfp_sample_uniform(sfp_dev* d, uint64_t* p, sfp_limbs m, uint64_t seed);
+// Load signed coefficients (same for every limb) reduced mod each prime.
+void sfp_load_i64(sfp_dev* d, uint64_t* p, const int64_t* coeffs, sfp_limbs m);
+
+#ifdef __cplusplus
+}
+#endif

@@ -1,0 +1,373 @@
+"""ctypes binding of the C ABI in include/sfhe.h.
+
+The product library is ``sorting-fhe_amd/build/libsfhe.so`` (HIP, gfx950).
+``load("oracle")`` loads ``oracle/_build/libsfhe_oracle.so``, the CPU oracle
+build -- test infrastructure only (tests/, __graft_entry__.smoke and the
+bench's cpu_baseline leg); product code paths call ``load()`` and fail
+loudly when the HIP library is missing.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Sequence
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(_HERE)
+REPO_ROOT = os.path.dirname(PKG_ROOT)
+PRODUCT_LIB = os.path.join(PKG_ROOT, "build", "libsfhe.so")
+ORACLE_LIB = os.path.join(REPO_ROOT, "oracle", "_build", "libsfhe_oracle.so")
+
+SFHE_OK = 0
+HESTD_128_CLASSIC = 0
+HESTD_NOTSET = 3
+
+# every symbol include/sfhe.h declares (checked by tests/test_abi.py)
+ABI_SYMBOLS = [
+    "sfhe_abi_version", "sfhe_last_error", "sfhe_backend", "sfhe_params_default",
+    "sfhe_context_create", "sfhe_context_destroy", "sfhe_keygen", "sfhe_rotate_keygen",
+    "sfhe_context_info", "sfhe_context_primes", "sfhe_set_plaintext_cache", "sfhe_set_quiet",
+    "sfhe_sync", "sfhe_op_stats", "sfhe_encrypt", "sfhe_decrypt", "sfhe_ct_free",
+    "sfhe_ct_clone", "sfhe_ct_info", "sfhe_ct_set_slots", "sfhe_ct_download", "sfhe_eval_add",
+    "sfhe_eval_sub", "sfhe_eval_add_const", "sfhe_eval_mult_const", "sfhe_eval_mult_plain",
+    "sfhe_eval_mult", "sfhe_eval_rotate", "sfhe_eval_chebyshev", "sfhe_sign", "sfhe_compare",
+    "sfhe_direct_sort_params", "sfhe_doubled_sinc_coeffs", "sfhe_sorter_create",
+    "sfhe_sorter_destroy", "sfhe_sorter_sort", "sfhe_sorter_rank", "sfhe_sorter_place",
+    "sfhe_decompose",
+]
+
+
+class SfheError(RuntimeError):
+    pass
+
+
+class Params(C.Structure):
+    _fields_ = [
+        ("mult_depth", C.c_uint32),
+        ("scaling_mod_size", C.c_uint32),
+        ("first_mod_size", C.c_uint32),
+        ("batch_size", C.c_uint32),
+        ("ring_dim", C.c_uint32),
+        ("security_level", C.c_int32),
+        ("num_large_digits", C.c_uint32),
+        ("device", C.c_int32),
+        ("seed", C.c_uint64),
+    ]
+
+
+_VP = C.c_void_p
+_PVP = C.POINTER(C.c_void_p)
+_U32 = C.c_uint32
+_PU32 = C.POINTER(C.c_uint32)
+_SZ = C.c_size_t
+_PSZ = C.POINTER(C.c_size_t)
+_PD = C.POINTER(C.c_double)
+_PI32 = C.POINTER(C.c_int32)
+_PU64 = C.POINTER(C.c_uint64)
+
+_SIGS = {
+    "sfhe_abi_version": (C.c_int, []),
+    "sfhe_last_error": (C.c_char_p, []),
+    "sfhe_backend": (C.c_char_p, []),
+    "sfhe_params_default": (None, [C.POINTER(Params)]),
+    "sfhe_context_create": (C.c_int, [C.POINTER(Params), _PVP]),
+    "sfhe_context_destroy": (None, [_VP]),
+    "sfhe_keygen": (C.c_int, [_VP]),
+    "sfhe_rotate_keygen": (C.c_int, [_VP, _PI32, _SZ]),
+    "sfhe_context_info": (C.c_int, [_VP, _PU32, _PU32, _PU32, _PU32, _PU32]),
+    "sfhe_context_primes": (C.c_int, [_VP, _PU64, _SZ, _PSZ]),
+    "sfhe_set_plaintext_cache": (C.c_int, [_VP, C.c_int]),
+    "sfhe_set_quiet": (C.c_int, [_VP, C.c_int]),
+    "sfhe_sync": (C.c_int, [_VP]),
+    "sfhe_op_stats": (C.c_int, [_VP, _PU64, _PD, C.c_int]),
+    "sfhe_encrypt": (C.c_int, [_VP, _PD, _SZ, _U32, _U32, _PVP]),
+    "sfhe_decrypt": (C.c_int, [_VP, _VP, _PD, _SZ, _PSZ]),
+    "sfhe_ct_free": (None, [_VP]),
+    "sfhe_ct_clone": (C.c_int, [_VP, _PVP]),
+    "sfhe_ct_info": (C.c_int, [_VP, _PU32, _PU32, _PU32]),
+    "sfhe_ct_set_slots": (C.c_int, [_VP, _U32]),
+    "sfhe_ct_download": (C.c_int, [_VP, _VP, _PU64, _SZ]),
+    "sfhe_eval_add": (C.c_int, [_VP, _VP, _VP, _PVP]),
+    "sfhe_eval_sub": (C.c_int, [_VP, _VP, _VP, _PVP]),
+    "sfhe_eval_add_const": (C.c_int, [_VP, _VP, C.c_double, _PVP]),
+    "sfhe_eval_mult_const": (C.c_int, [_VP, _VP, C.c_double, _PVP]),
+    "sfhe_eval_mult_plain": (C.c_int, [_VP, _VP, _PD, _SZ, _U32, _PVP]),
+    "sfhe_eval_mult": (C.c_int, [_VP, _VP, _VP, _PVP]),
+    "sfhe_eval_rotate": (C.c_int, [_VP, _VP, C.c_int32, _PVP]),
+    "sfhe_eval_chebyshev": (C.c_int, [_VP, _VP, _PD, _SZ, C.c_double, C.c_double, _PVP]),
+    "sfhe_sign": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_int, _PVP]),
+    "sfhe_compare": (C.c_int, [_VP, _VP, _VP, C.c_int, C.c_int, C.c_int, _PVP]),
+    "sfhe_direct_sort_params": (C.c_int, [_U32, _PU32, _PI32, _SZ, _PSZ]),
+    "sfhe_doubled_sinc_coeffs": (C.c_int, [_U32, _PD, _SZ, _PSZ]),
+    "sfhe_sorter_create": (C.c_int, [_VP, _U32, C.c_int, _PVP]),
+    "sfhe_sorter_destroy": (None, [_VP]),
+    "sfhe_sorter_sort": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_int, _PVP]),
+    "sfhe_sorter_rank": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_int, _PVP]),
+    "sfhe_sorter_place": (C.c_int, [_VP, _VP, _VP, _PVP]),
+    "sfhe_decompose": (C.c_int, [_U32, _PI32, _SZ, C.c_int32, C.c_int32, C.c_int, _PI32, _PI32, _SZ, _PSZ]),
+}
+
+_libs: dict = {}
+
+
+def lib_path(backend: str = "hip") -> str:
+    return PRODUCT_LIB if backend == "hip" else ORACLE_LIB
+
+
+def load(backend: str = "hip"):
+    """Load the engine library.  backend='hip' is the product (raises if the
+    HIP build is absent); backend='oracle' is the CPU oracle (tests only)."""
+    if backend in _libs:
+        return _libs[backend]
+    path = lib_path(backend)
+    if not os.path.exists(path):
+        raise SfheError(
+            f"{backend} library not built: {path} is missing "
+            f"(run `make -C sorting-fhe_amd` for the HIP product, `make -C oracle` for the oracle)")
+    lib = C.CDLL(path)
+    for name, (res, args) in _SIGS.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    _libs[backend] = lib
+    return lib
+
+
+def _darr(v: Sequence[float]):
+    a = (C.c_double * len(v))(*[float(x) for x in v])
+    return a
+
+
+class Engine:
+    """Thin object wrapper; one CKKS context + key pair."""
+
+    def __init__(self, backend: str = "hip", *, mult_depth: int, ring_dim: int = 0,
+                 batch_size: int = 0, scaling_mod_size: int = 40, first_mod_size: int = 60,
+                 secure: bool = False, num_large_digits: int = 0, seed: int = 0x5EED5EED2025,
+                 device: int = 0, rotations: Sequence[int] = (), keygen: bool = True):
+        self.lib = load(backend)
+        self.backend = backend
+        p = Params()
+        self.lib.sfhe_params_default(C.byref(p))
+        p.mult_depth = mult_depth
+        p.ring_dim = ring_dim
+        p.batch_size = batch_size
+        p.scaling_mod_size = scaling_mod_size
+        p.first_mod_size = first_mod_size
+        p.security_level = HESTD_128_CLASSIC if secure else HESTD_NOTSET
+        p.num_large_digits = num_large_digits
+        p.seed = seed
+        p.device = device
+        self.ctx = C.c_void_p()
+        self._chk(self.lib.sfhe_context_create(C.byref(p), C.byref(self.ctx)))
+        if keygen:
+            self._chk(self.lib.sfhe_keygen(self.ctx))
+            if rotations:
+                self.rotate_keygen(rotations)
+
+    # -- plumbing --
+    def _chk(self, rc: int):
+        if rc != SFHE_OK:
+            raise SfheError(f"sfhe error {rc}: {self.lib.sfhe_last_error().decode()}")
+
+    def close(self):
+        if self.ctx:
+            self.lib.sfhe_context_destroy(self.ctx)
+            self.ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _new(self, fn, *args) -> "Ct":
+        out = C.c_void_p()
+        self._chk(fn(*args, C.byref(out)))
+        return Ct(self, out)
+
+    # -- context --
+    def rotate_keygen(self, idx: Sequence[int]):
+        a = (C.c_int32 * len(idx))(*idx)
+        self._chk(self.lib.sfhe_rotate_keygen(self.ctx, a, len(idx)))
+
+    def info(self) -> dict:
+        v = [C.c_uint32() for _ in range(5)]
+        self._chk(self.lib.sfhe_context_info(self.ctx, *[C.byref(x) for x in v]))
+        return dict(ring_dim=v[0].value, mult_depth=v[1].value, num_q=v[2].value,
+                    num_p=v[3].value, dnum=v[4].value)
+
+    def primes(self) -> list:
+        cnt = C.c_size_t()
+        self._chk(self.lib.sfhe_context_primes(self.ctx, None, 0, C.byref(cnt)))
+        buf = (C.c_uint64 * cnt.value)()
+        self._chk(self.lib.sfhe_context_primes(self.ctx, buf, cnt.value, None))
+        return list(buf)
+
+    def sync(self):
+        self._chk(self.lib.sfhe_sync(self.ctx))
+
+    def set_quiet(self, q: bool = True):
+        self._chk(self.lib.sfhe_set_quiet(self.ctx, int(q)))
+
+    def set_plaintext_cache(self, on: bool):
+        self._chk(self.lib.sfhe_set_plaintext_cache(self.ctx, int(on)))
+
+    def op_stats(self, reset: bool = False) -> dict:
+        c = (C.c_uint64 * 9)()
+        b = C.c_double()
+        self._chk(self.lib.sfhe_op_stats(self.ctx, c, C.byref(b), int(reset)))
+        keys = ["keyswitch", "rescale", "tensor", "ptmult", "constmult", "add", "automorph",
+                "ntt_limbs", "wsum_terms"]
+        d = dict(zip(keys, list(c)))
+        d["algo_bytes"] = b.value
+        return d
+
+    # -- data --
+    def encrypt(self, values: Sequence[float], slots: int = 0, level: int = 0) -> "Ct":
+        a = _darr(values)
+        return self._new(self.lib.sfhe_encrypt, self.ctx, a, len(values), slots, level)
+
+    def decrypt(self, ct: "Ct") -> list:
+        n = C.c_size_t()
+        self._chk(self.lib.sfhe_decrypt(self.ctx, ct.h, None, 0, C.byref(n)))
+        buf = (C.c_double * n.value)()
+        self._chk(self.lib.sfhe_decrypt(self.ctx, ct.h, buf, n.value, None))
+        return list(buf)
+
+    # -- eval --
+    def add(self, a, b):
+        return self._new(self.lib.sfhe_eval_add, self.ctx, a.h, b.h)
+
+    def sub(self, a, b):
+        return self._new(self.lib.sfhe_eval_sub, self.ctx, a.h, b.h)
+
+    def add_const(self, a, k: float):
+        return self._new(self.lib.sfhe_eval_add_const, self.ctx, a.h, float(k))
+
+    def mult_const(self, a, k: float):
+        return self._new(self.lib.sfhe_eval_mult_const, self.ctx, a.h, float(k))
+
+    def mult_plain(self, a, values: Sequence[float], slots: int = 0):
+        return self._new(self.lib.sfhe_eval_mult_plain, self.ctx, a.h, _darr(values), len(values), slots)
+
+    def mult(self, a, b):
+        return self._new(self.lib.sfhe_eval_mult, self.ctx, a.h, b.h)
+
+    def rotate(self, a, r: int):
+        return self._new(self.lib.sfhe_eval_rotate, self.ctx, a.h, int(r))
+
+    def chebyshev(self, x, coeffs: Sequence[float], a: float = -1.0, b: float = 1.0):
+        return self._new(self.lib.sfhe_eval_chebyshev, self.ctx, x.h, _darr(coeffs), len(coeffs),
+                         float(a), float(b))
+
+    def sign(self, x, n: int, dg: int, df: int):
+        return self._new(self.lib.sfhe_sign, self.ctx, x.h, n, dg, df)
+
+    def compare(self, a, b, n: int, dg: int, df: int):
+        return self._new(self.lib.sfhe_compare, self.ctx, a.h, b.h, n, dg, df)
+
+    def sorter(self, N: int, debug: bool = False) -> "Sorter":
+        h = C.c_void_p()
+        self._chk(self.lib.sfhe_sorter_create(self.ctx, N, int(debug), C.byref(h)))
+        return Sorter(self, h, N)
+
+
+class Ct:
+    def __init__(self, eng: Engine, h):
+        self.eng = eng
+        self.h = h
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.eng.lib.sfhe_ct_free(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    def info(self) -> dict:
+        v = [C.c_uint32() for _ in range(3)]
+        self.eng._chk(self.eng.lib.sfhe_ct_info(self.h, *[C.byref(x) for x in v]))
+        return dict(level=v[0].value, slots=v[1].value, limbs=v[2].value)
+
+    @property
+    def level(self) -> int:
+        return self.info()["level"]
+
+    @property
+    def slots(self) -> int:
+        return self.info()["slots"]
+
+    def set_slots(self, s: int):
+        self.eng._chk(self.eng.lib.sfhe_ct_set_slots(self.h, s))
+
+    def clone(self) -> "Ct":
+        return self.eng._new(self.eng.lib.sfhe_ct_clone, self.h)
+
+    def download(self):
+        import numpy as np
+        n = self.eng.info()["ring_dim"]
+        words = 2 * self.info()["limbs"] * n
+        buf = np.empty(words, dtype=np.uint64)
+        self.eng._chk(self.eng.lib.sfhe_ct_download(
+            self.eng.ctx, self.h, buf.ctypes.data_as(_PU64), words))
+        return buf
+
+
+class Sorter:
+    def __init__(self, eng: Engine, h, N: int):
+        self.eng, self.h, self.N = eng, h, N
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.eng.lib.sfhe_sorter_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    def sort(self, ct: Ct, n: int = 3, dg: int = 2, df: int = 2) -> Ct:
+        return self.eng._new(self.eng.lib.sfhe_sorter_sort, self.h, ct.h, n, dg, df)
+
+    def rank(self, ct: Ct, n: int = 3, dg: int = 2, df: int = 2) -> Ct:
+        return self.eng._new(self.eng.lib.sfhe_sorter_rank, self.h, ct.h, n, dg, df)
+
+    def place(self, rank: Ct, ct: Ct) -> Ct:
+        return self.eng._new(self.eng.lib.sfhe_sorter_place, self.h, rank.h, ct.h)
+
+
+def direct_sort_params(N: int, backend: str = "hip"):
+    lib = load(backend)
+    depth = C.c_uint32()
+    cnt = C.c_size_t()
+    rc = lib.sfhe_direct_sort_params(N, C.byref(depth), None, 0, C.byref(cnt))
+    if rc != SFHE_OK:
+        raise SfheError(lib.sfhe_last_error().decode())
+    buf = (C.c_int32 * cnt.value)()
+    lib.sfhe_direct_sort_params(N, None, buf, cnt.value, None)
+    return depth.value, list(buf)
+
+
+def doubled_sinc_coeffs(N: int, backend: str = "hip"):
+    lib = load(backend)
+    cnt = C.c_size_t()
+    rc = lib.sfhe_doubled_sinc_coeffs(N, None, 0, C.byref(cnt))
+    if rc != SFHE_OK:
+        raise SfheError(lib.sfhe_last_error().decode())
+    buf = (C.c_double * cnt.value)()
+    lib.sfhe_doubled_sinc_coeffs(N, buf, cnt.value, None)
+    return list(buf)
+
+
+def decompose(N: int, keys: Sequence[int], rotation: int, wrapN: int, algo: int, backend: str = "hip"):
+    lib = load(backend)
+    k = (C.c_int32 * len(keys))(*keys)
+    cap = 64
+    v = (C.c_int32 * cap)()
+    s = (C.c_int32 * cap)()
+    cnt = C.c_size_t()
+    rc = lib.sfhe_decompose(N, k, len(keys), rotation, wrapN, algo, v, s, cap, C.byref(cnt))
+    if rc != SFHE_OK:
+        raise SfheError(lib.sfhe_last_error().decode())
+    return [(v[i], s[i]) for i in range(min(cnt.value, cap))]
