@@ -37,6 +37,13 @@ typedef struct sfhe_ctx sfhe_ctx;
 typedef struct sfhe_ct sfhe_ct;
 typedef struct sfhe_sorter sfhe_sorter;
 
+/* Scaling techniques (lbcrypto::ScalingTechnique values).  FLEXIBLEAUTOEXT,
+ * OpenFHE's default and therefore the reference's (it never calls
+ * SetScalingTechnique), forms fresh encryptions modulo Q*q_ext and rescales
+ * by q_ext; FLEXIBLEAUTO encrypts directly modulo Q. */
+#define SFHE_FLEXIBLEAUTO 2
+#define SFHE_FLEXIBLEAUTOEXT 3
+
 /* Security levels (lbcrypto::SecurityLevel). */
 #define SFHE_HESTD_128_CLASSIC 0
 #define SFHE_HESTD_NOTSET 3
@@ -53,6 +60,7 @@ typedef struct {
     uint32_t num_large_digits;  /* HYBRID dnum; 0 = default (3) */
     int32_t device;             /* HIP device ordinal */
     uint64_t seed;              /* deterministic key / noise sampling */
+    int32_t scaling_technique;  /* SFHE_FLEXIBLEAUTO[EXT]; 0 = FLEXIBLEAUTOEXT */
 } sfhe_params;
 
 int sfhe_abi_version(void);
@@ -71,7 +79,7 @@ int sfhe_rotate_keygen(sfhe_ctx* c, const int32_t* idx, size_t count);
 /* ring_dim, mult_depth, #Q primes, #P primes, dnum (any pointer may be NULL) */
 int sfhe_context_info(sfhe_ctx* c, uint32_t* ring_dim, uint32_t* mult_depth, uint32_t* num_q,
                       uint32_t* num_p, uint32_t* dnum);
-/* prime table [q_0..q_L, p_0..p_{K-1}] */
+/* prime table [q_0..q_L, p_0..p_{K-1}] (+ q_ext under FLEXIBLEAUTOEXT) */
 int sfhe_context_primes(sfhe_ctx* c, uint64_t* out, size_t cap, size_t* count);
 /* Cache of encoded constant plaintexts (sort masks) across calls; default on. */
 int sfhe_set_plaintext_cache(sfhe_ctx* c, int on);

@@ -40,6 +40,7 @@ struct sfp_conv {
     uint32_t ns, nt;
     uint32_t *src, *dst;
     u64 *inv, *mod;
+    u64 *sprod; /* prod(S) mod dst_t */
 };
 
 static inline u64 mm(u64 a, u64 b, u64 q) { return (u64)(((u128)a * b) % q); }
@@ -55,7 +56,7 @@ static inline uint32_t brev(uint32_t x, uint32_t bits) {
     for (uint32_t i = 0; i < bits; ++i) r |= ((x >> i) & 1u) << (bits - 1 - i);
     return r;
 }
-static inline uint32_t pidx(sfp_limbs m, uint32_t i) { return i < m.split ? i : m.pbase + (i - m.split); }
+static inline uint32_t pidx(sfp_limbs m, uint32_t i) { return (i < m.split ? m.base + i : m.pbase + (i - m.split)); }
 
 const char* sfp_backend_name(void) { return "oracle-c"; }
 
@@ -238,14 +239,19 @@ void sfp_automorph(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t g, sf
 /* ---- rescale ---- */
 void sfp_rescale(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t ell, const uint64_t* qlinv,
                  uint32_t npoly, size_t in_stride, size_t out_stride) {
+    sfp_rescale_ext(d, out, in, ell, ell - 1, qlinv, npoly, in_stride, out_stride);
+}
+
+void sfp_rescale_ext(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t ell, uint32_t drop_prime,
+                     const uint64_t* qlinv, uint32_t npoly, size_t in_stride, size_t out_stride) {
     const uint32_t n = d->n;
-    const u64 ql = d->q[ell - 1];
+    const u64 ql = d->q[drop_prime];
     u64* last = (u64*)malloc((size_t)n * 8);
     for (uint32_t p = 0; p < npoly; ++p) {
         const u64* src = in + p * in_stride;
         u64* dst = out + p * out_stride;
         memcpy(last, src + (size_t)(ell - 1) * n, (size_t)n * 8);
-        ntt_inv(d, last, ell - 1);
+        ntt_inv(d, last, drop_prime);
 #pragma omp parallel for schedule(static)
         for (uint32_t i = 0; i < ell - 1; ++i) {
             const u64 q = d->q[i];
@@ -269,37 +275,49 @@ void sfp_rescale(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t ell, co
 /* ---- base conversion / key switching ---- */
 sfp_conv* sfp_upload_conv(sfp_dev* d, uint32_t ns, const uint32_t* src, uint32_t nt,
                           const uint32_t* dst, const uint64_t* inv, const uint64_t* mod) {
-    (void)d;
     sfp_conv* c = (sfp_conv*)calloc(1, sizeof(sfp_conv));
     c->ns = ns; c->nt = nt;
     c->src = (uint32_t*)malloc(ns * 4); memcpy(c->src, src, ns * 4);
     c->dst = (uint32_t*)malloc(nt * 4); memcpy(c->dst, dst, nt * 4);
     c->inv = (u64*)malloc(ns * 8); memcpy(c->inv, inv, ns * 8);
     c->mod = (u64*)malloc((size_t)ns * nt * 8); memcpy(c->mod, mod, (size_t)ns * nt * 8);
+    c->sprod = (u64*)malloc(nt * 8);
+    for (uint32_t t = 0; t < nt; ++t) {
+        u64 pt = d->q[dst[t]], r = 1;
+        for (uint32_t i = 0; i < ns; ++i) r = mm(r, d->q[src[i]] % pt, pt);
+        c->sprod[t] = r;
+    }
     return c;
 }
 void sfp_free_conv(sfp_dev* d, sfp_conv* c) {
     (void)d;
     if (!c) return;
-    free(c->src); free(c->dst); free(c->inv); free(c->mod); free(c);
+    free(c->src); free(c->dst); free(c->inv); free(c->mod); free(c->sprod); free(c);
 }
 
-/* dst row t (prime c->dst[t]) = sum_i [src_i * inv_i]_{s_i} * mod[i][t]  (coefficient domain) */
+/* dst row t (prime c->dst[t]) = sum_i [src_i * inv_i]_{s_i} * mod[i][t]  (coefficient domain).
+ * centered: each y_i is taken in (-s_i/2, s_i/2], i.e. y_i - s_i when y_i > s_i/2, which
+ * subtracts prod(S) mod t once per such i; the conversion error sum_i y_i/s_i is then
+ * zero-mean (ModDown rounds instead of flooring with a +K/2 bias). */
 static void conv_rows(const sfp_dev* d, const sfp_conv* c, const u64* src, u64* const* dstRows,
-                      uint32_t ntUse) {
+                      uint32_t ntUse, int centered) {
     const uint32_t n = d->n;
 #pragma omp parallel for schedule(static)
     for (uint32_t x = 0; x < n; ++x) {
         u64 y[SFP_MAX_LIMBS];
+        u64 neg = 0;
         for (uint32_t i = 0; i < c->ns; ++i) {
             u64 qi = d->q[c->src[i]];
             y[i] = mm(src[(size_t)i * n + x], c->inv[i], qi);
+            if (centered && y[i] > (qi >> 1)) ++neg;
         }
         for (uint32_t t = 0; t < ntUse; ++t) {
             u64 pt = d->q[c->dst[t]];
             u128 acc = 0;
             for (uint32_t i = 0; i < c->ns; ++i) acc += (u128)y[i] * c->mod[(size_t)i * c->nt + t];
-            dstRows[t][x] = (u64)(acc % pt);
+            u64 v = (u64)(acc % pt);
+            if (neg) v = sb(v, mm(neg, c->sprod[t], pt), pt);
+            dstRows[t][x] = v;
         }
     }
 }
@@ -307,7 +325,7 @@ static void conv_rows(const sfp_dev* d, const sfp_conv* c, const u64* src, u64* 
 void sfp_conv_apply(sfp_dev* d, uint64_t* dst, const uint64_t* src, const sfp_conv* c) {
     u64** rows = (u64**)malloc(c->nt * sizeof(u64*));
     for (uint32_t t = 0; t < c->nt; ++t) rows[t] = dst + (size_t)t * d->n;
-    conv_rows(d, c, src, rows, c->nt);
+    conv_rows(d, c, src, rows, c->nt, 0);
     free(rows);
 }
 
@@ -323,7 +341,7 @@ void sfp_modup(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t ell, uint
         uint32_t pos = pr < Lq ? pr : ell + (pr - Lq);
         rows[t] = out + (size_t)pos * n;
     }
-    conv_rows(d, c, scratch, rows, c->nt);
+    conv_rows(d, c, scratch, rows, c->nt, 0);
 #pragma omp parallel for schedule(static)
     for (uint32_t t = 0; t < c->nt; ++t) ntt_fwd(d, rows[t], c->dst[t]);
     free(rows);
@@ -360,7 +378,7 @@ void sfp_moddown(sfp_dev* d, uint64_t* out, uint64_t* acc, uint32_t ell, uint32_
     for (uint32_t k = 0; k < K; ++k) ntt_inv(d, pRows + (size_t)k * n, Lq + k);
     u64** rows = (u64**)malloc(ell * sizeof(u64*));
     for (uint32_t i = 0; i < ell; ++i) rows[i] = scratch + (size_t)i * n;
-    conv_rows(d, c, pRows, rows, ell);
+    conv_rows(d, c, pRows, rows, ell, 1);
 #pragma omp parallel for schedule(static)
     for (uint32_t i = 0; i < ell; ++i) {
         const u64 q = d->q[i];

@@ -5,6 +5,7 @@
 #pragma once
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdint>
 #include <iostream>
 #include <map>
@@ -148,7 +149,8 @@ class RotationComposer {
     std::vector<Ciphertext<DCRTPoly>> rotateMany(const Ciphertext<DCRTPoly>& in,
                                                  const std::vector<int>& amounts) {
         std::vector<Ciphertext<DCRTPoly>> out(amounts.size());
-        bool hoist = true;
+        static const bool noHoist = std::getenv("SFHE_NO_HOIST") != nullptr;
+        bool hoist = !noHoist;
         for (int a : amounts)
             if (a % (int)in->GetSlots() != 0 && !m_keys.count(a)) hoist = false;
         if (!hoist) {

@@ -138,6 +138,7 @@ void sfhe_params_default(sfhe_params* p) {
     p->first_mod_size = 60;
     p->security_level = SFHE_HESTD_128_CLASSIC;
     p->seed = 0x5eed5eed2025ULL;
+    p->scaling_technique = SFHE_FLEXIBLEAUTOEXT;
 }
 
 int sfhe_context_create(const sfhe_params* p, sfhe_ctx** out) {
@@ -153,6 +154,11 @@ int sfhe_context_create(const sfhe_params* p, sfhe_ctx** out) {
         P.SetNumLargeDigits(p->num_large_digits);
         P.SetDevice(p->device);
         P.SetSeed(p->seed);
+        if (p->scaling_technique != 0 && p->scaling_technique != SFHE_FLEXIBLEAUTO &&
+            p->scaling_technique != SFHE_FLEXIBLEAUTOEXT)
+            throw std::invalid_argument("scaling_technique must be FLEXIBLEAUTO or FLEXIBLEAUTOEXT");
+        P.SetScalingTechnique(p->scaling_technique == SFHE_FLEXIBLEAUTO ? FLEXIBLEAUTO
+                                                                         : FLEXIBLEAUTOEXT);
         auto c = std::make_unique<sfhe_ctx>();
         c->cc = GenCryptoContext(P);
         c->cc->Enable(PKE);
@@ -407,6 +413,24 @@ int sfhe_decompose(uint32_t N, const int32_t* keys, size_t nkeys, int32_t rotati
             CASE(4) CASE(8) CASE(16) CASE(32) CASE(64) CASE(128) CASE(256) CASE(512) CASE(1024)
 #undef CASE
         }
+    });
+}
+
+int sfhe_debug_decrypt_coeffs(sfhe_ctx* c, const sfhe_ct* ct, double* out, size_t cap) {
+    REQUIRE(c && ct && out, "null argument");
+    REQUIRE(c->keys.secretKey, "no secret key");
+    const size_t n = c->cc->GetRingDimension();
+    REQUIRE(cap >= n, "output buffer too small");
+    return guard([&] {
+        auto* s = c->cc->state();
+        auto t = s->alloc(n);
+        const sfp_limbs q{1, 1, 0, 0};
+        sfp_mul_add(s->dev, t->ptr, ct->ct->c1, c->keys.secretKey->s->ptr, ct->ct->c0, q);
+        sfp_ntt(s->dev, t->ptr, q, 1);
+        std::vector<uint64_t> h(n);
+        sfp_d2h(s->dev, h.data(), t->ptr, n * 8);
+        const uint64_t q0 = s->primes[0];
+        for (size_t i = 0; i < n; ++i) out[i] = h[i] > q0 / 2 ? -(double)(q0 - h[i]) : (double)h[i];
     });
 }
 

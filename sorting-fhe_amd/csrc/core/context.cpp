@@ -11,6 +11,8 @@
 // All polynomial work is enqueued through csrc/prims.h.
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "state.h"
@@ -187,6 +189,24 @@ class SfheInternal {
   public:
     using CC = CryptoContextImpl<DCRTPoly>;
     using Ct = Ciphertext<DCRTPoly>;
+
+    // Debug: SFHE_TRACE=1 prints a hash of every op result (stderr), so the
+    // traces of two backends can be diffed to find the first divergent op.
+    static Ct traced(CC* cc, Ct ct, const char* what) {
+        static const bool on = std::getenv("SFHE_TRACE") != nullptr;
+        if (!on) return ct;
+        static uint64_t counter = 0;
+        SfheContextState* s = cc->st.get();
+        const size_t words = (size_t)s->ellOf(ct->level) * s->n;
+        std::vector<u64> h(words * 2);
+        sfp_d2h(s->dev, h.data(), ct->c0, words * 8);
+        sfp_d2h(s->dev, h.data() + words, ct->c1, words * 8);
+        uint64_t f = 1469598103934665603ull;
+        for (u64 v : h) f = (f ^ v) * 1099511628211ull;
+        std::fprintf(stderr, "TRACE %llu %s L%u %016llx\n", (unsigned long long)counter++, what,
+                     ct->level, (unsigned long long)f);
+        return ct;
+    }
 
     static sfp_limbs Q(uint32_t ell) { return sfp_limbs{ell, ell, 0}; }
     static sfp_limbs Range(uint32_t lo, uint32_t cnt) { return sfp_limbs{cnt, 0, lo}; }
@@ -409,6 +429,16 @@ class SfheInternal {
         ckks_encode(pt->values, pt->slots, s->n, s->scale[level], coeffs);
         auto buf = s->alloc((size_t)ell * s->n);
         sfp_load_i64(s->dev, buf->ptr, coeffs.data(), Q(ell));
+        if (std::getenv("SFHE_TRACE")) {
+            uint64_t f = 1469598103934665603ull;
+            for (int64_t v : coeffs) f = (f ^ (uint64_t)v) * 1099511628211ull;
+            std::vector<u64> h((size_t)ell * s->n);
+            sfp_d2h(s->dev, h.data(), buf->ptr, h.size() * 8);
+            uint64_t g = 1469598103934665603ull;
+            for (u64 v : h) g = (g ^ v) * 1099511628211ull;
+            std::fprintf(stderr, "ENCODE slots=%u level=%u coeffs=%016llx loaded=%016llx\n", pt->slots,
+                         level, (unsigned long long)f, (unsigned long long)g);
+        }
         sfp_ntt(s->dev, buf->ptr, Q(ell), 0);
         pt->encoded[level] = buf;
         if (s->ptCacheOn && s->ptCacheBytes + (size_t)ell * s->n * 8 <= s->ptCacheLimit) {
@@ -447,6 +477,11 @@ CryptoContextImpl<DCRTPoly>::CryptoContextImpl(const CCParams<CryptoContextCKKSR
     s.L = p.GetMultiplicativeDepth();
     s.Lq = s.L + 1;
     s.seed = p.GetSeed();
+    switch (p.GetScalingTechnique()) {
+        case FLEXIBLEAUTO: s.ext = false; break;
+        case FLEXIBLEAUTOEXT: s.ext = true; break;
+        default: SFHE_THROW("only FLEXIBLEAUTO and FLEXIBLEAUTOEXT scaling are supported");
+    }
     const uint32_t sbits = p.GetScalingModSize();
     const uint32_t fbits = p.GetFirstModSize();
     if (sbits < 20 || sbits > 60) SFHE_THROW("scaling mod size must be in [20, 60]");
@@ -492,7 +527,10 @@ CryptoContextImpl<DCRTPoly>::CryptoContextImpl(const CCParams<CryptoContextCKKSR
                 b += std::log2((double)q[i]);
             maxDigitBits = std::max(maxDigitBits, b);
         }
-        uint32_t K = (uint32_t)std::ceil(maxDigitBits / 60.0);
+        // P must exceed every digit modulus with margin, or the key-switch
+        // noise (digit * error / P) is not negligible (special primes are
+        // just below 2^60)
+        uint32_t K = (uint32_t)std::ceil((maxDigitBits + 20.0) / 59.9);
         std::vector<u64> P;
         u64 bound = 1ull << 60;
         for (uint32_t k = 0; k < K; ++k) {
@@ -501,7 +539,12 @@ CryptoContextImpl<DCRTPoly>::CryptoContextImpl(const CCParams<CryptoContextCKKSR
             P.push_back(pr);
             bound = pr;
         }
-        double logQP = 0;
+        u64 qext = 0;
+        if (s.ext) {
+            qext = primeNear(std::ldexp(1.0, (int)sbits), m, used);
+            used.insert(qext);
+        }
+        double logQP = qext ? std::log2((double)qext) : 0.0;
         for (u64 x : q) logQP += std::log2((double)x);
         for (u64 x : P) logQP += std::log2((double)x);
         if (secure && logQP > maxLogQ128(logn)) {
@@ -517,13 +560,15 @@ CryptoContextImpl<DCRTPoly>::CryptoContextImpl(const CCParams<CryptoContextCKKSR
         s.K = K;
         s.primes = q;
         s.primes.insert(s.primes.end(), P.begin(), P.end());
+        if (s.ext) s.primes.push_back(qext);
         s.scale = sc;
         break;
     }
     s.batch = batch ? batch : s.n / 2;
+    if (std::getenv("SFHE_NO_PTCACHE")) s.ptCacheOn = false;
     if (s.batch > s.n / 2) SFHE_THROW("batch size exceeds n/2");
 
-    const uint32_t NP = s.Lq + s.K;
+    const uint32_t NP = s.tablePrimes();
     for (u64 x : s.primes) s.bar.push_back(sf_make_barrett(x));
 
     // NTT tables
@@ -563,6 +608,14 @@ CryptoContextImpl<DCRTPoly>::CryptoContextImpl(const CCParams<CryptoContextCKKSR
     s.dev = sfp_create(p.GetDevice(), &t);
     if (!s.dev) SFHE_THROW(std::string("device backend '") + sfp_backend_name() + "' failed to initialise");
 
+    if (s.ext) {
+        s.extIdx = s.Lq + s.K;
+        const u64 qe = s.primes[s.extIdx];
+        for (uint32_t i = 0; i < s.Lq; ++i) {
+            s.extModQ.push_back(qe % s.primes[i]);
+            s.extInvModQ.push_back(invmod(qe % s.primes[i], s.primes[i]));
+        }
+    }
     // P mod q_i, P^{-1} mod q_i
     s.pModQ.resize(s.Lq);
     s.pInvModQ.resize(s.Lq);
@@ -647,23 +700,30 @@ KeyPair<DCRTPoly> CryptoContextImpl<DCRTPoly>::KeyGen() {
     std::vector<int64_t> tern(s->n);
     SfheInternal::sampleTernary(s, tern);
     sk->ternary.assign(tern.begin(), tern.end());
-    sk->s = s->alloc((size_t)NP * s->n);
-    const sfp_limbs all{NP, NP, 0};
+    const uint32_t NT = s->tablePrimes();
+    sk->s = s->alloc((size_t)NT * s->n);
+    const sfp_limbs all{NT, NT, 0};
     sfp_load_i64(s->dev, sk->s->ptr, tern.data(), all);
     sfp_ntt(s->dev, sk->s->ptr, all, 0);
+    (void)NP;
 
     auto pk = std::make_shared<PublicKeyImpl<DCRTPoly>>();
     pk->cc = shared_from_this();
-    const sfp_limbs q = SfheInternal::Q(s->Lq);
-    pk->a = s->alloc((size_t)s->Lq * s->n);
-    pk->b = s->alloc((size_t)s->Lq * s->n);
+    // rows [q_0..q_L] (+ the q_ext row, prime index extIdx, when ext)
+    const uint32_t R = s->Lq + (s->ext ? 1 : 0);
+    const sfp_limbs q{R, s->Lq, s->extIdx, 0};
+    pk->a = s->alloc((size_t)R * s->n);
+    pk->b = s->alloc((size_t)R * s->n);
     sfp_sample_uniform(s->dev, pk->a->ptr, q, s->nextSeed());
     std::vector<int64_t> e(s->n);
     SfheInternal::sampleCBD(s, e);
     sfp_load_i64(s->dev, pk->b->ptr, e.data(), q);
     sfp_ntt(s->dev, pk->b->ptr, q, 0);
-    auto t = s->alloc((size_t)s->Lq * s->n);
-    sfp_mul(s->dev, t->ptr, pk->a->ptr, sk->s->ptr, q);
+    auto t = s->alloc((size_t)R * s->n);
+    sfp_mul(s->dev, t->ptr, pk->a->ptr, sk->s->ptr, SfheInternal::Q(s->Lq));
+    if (s->ext)
+        sfp_mul(s->dev, t->ptr + (size_t)s->Lq * s->n, pk->a->ptr + (size_t)s->Lq * s->n,
+                sk->s->ptr + (size_t)s->extIdx * s->n, sfp_limbs{1, 0, s->extIdx, 0});
     sfp_sub(s->dev, pk->b->ptr, pk->b->ptr, t->ptr, q);
     kp.publicKey = pk;
     kp.secretKey = sk;
@@ -740,24 +800,46 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::Encrypt(const PublicKey<DCRTPo
     const sfp_limbs q = SfheInternal::Q(ell);
     const uint64_t* m = SfheInternal::encoded(this, pt, level);
     auto ct = SfheInternal::newCt(this, level, pt->slots);
-    auto tmp = s->alloc((size_t)3 * ell * s->n);
+    // FLEXIBLEAUTOEXT: one extra row modulo q_ext (prime index extIdx)
+    const uint32_t R = ell + (s->ext ? 1 : 0);
+    const sfp_limbs qr{R, ell, s->extIdx, 0};
+    const size_t rw = (size_t)R * s->n;
+    auto tmp = s->alloc((s->ext ? 5 : 3) * rw);
     uint64_t* v = tmp->ptr;
-    uint64_t* e0 = v + (size_t)ell * s->n;
-    uint64_t* e1 = e0 + (size_t)ell * s->n;
+    uint64_t* e0 = v + rw;
+    uint64_t* e1 = e0 + rw;
     std::vector<int64_t> h(s->n);
     SfheInternal::sampleTernary(s, h);
-    sfp_load_i64(s->dev, v, h.data(), q);
-    sfp_ntt(s->dev, v, q, 0);
+    sfp_load_i64(s->dev, v, h.data(), qr);
+    sfp_ntt(s->dev, v, qr, 0);
     SfheInternal::sampleCBD(s, h);
-    sfp_load_i64(s->dev, e0, h.data(), q);
-    sfp_ntt(s->dev, e0, q, 0);
+    sfp_load_i64(s->dev, e0, h.data(), qr);
+    sfp_ntt(s->dev, e0, qr, 0);
     SfheInternal::sampleCBD(s, h);
-    sfp_load_i64(s->dev, e1, h.data(), q);
-    sfp_ntt(s->dev, e1, q, 0);
-    sfp_mul_add(s->dev, ct->c0, v, pk->b->ptr, e0, q);
-    sfp_add(s->dev, ct->c0, ct->c0, m, q);
-    sfp_mul_add(s->dev, ct->c1, v, pk->a->ptr, e1, q);
-    return ct;
+    sfp_load_i64(s->dev, e1, h.data(), qr);
+    sfp_ntt(s->dev, e1, qr, 0);
+    if (!s->ext) {
+        sfp_mul_add(s->dev, ct->c0, v, pk->b->ptr, e0, q);
+        sfp_add(s->dev, ct->c0, ct->c0, m, q);
+        sfp_mul_add(s->dev, ct->c1, v, pk->a->ptr, e1, q);
+        return SfheInternal::traced(this, ct, "Encrypt");
+    }
+    // (v*pk + (e0 + q_ext*m, e1)) mod Q*q_ext; the q_ext row of q_ext*m is 0.
+    // Dividing by q_ext leaves m at scale Delta_level with the encryption
+    // noise shrunk by q_ext (only the rounding of the division remains).
+    uint64_t* c0x = e1 + rw;
+    uint64_t* c1x = c0x + rw;
+    const size_t qw = (size_t)ell * s->n, pkExt = (size_t)s->Lq * s->n;
+    const sfp_limbs x1{1, 0, s->extIdx, 0};
+    sfp_mul_add(s->dev, c0x, v, pk->b->ptr, e0, q);
+    sfp_mul_const(s->dev, c1x, m, s->extModQ.data(), q);
+    sfp_add(s->dev, c0x, c0x, c1x, q);
+    sfp_mul_add(s->dev, c1x, v, pk->a->ptr, e1, q);
+    sfp_mul_add(s->dev, c0x + qw, v + qw, pk->b->ptr + pkExt, e0 + qw, x1);
+    sfp_mul_add(s->dev, c1x + qw, v + qw, pk->a->ptr + pkExt, e1 + qw, x1);
+    sfp_rescale_ext(s->dev, ct->c0, c0x, R, s->extIdx, s->extInvModQ.data(), 2, rw,
+                    (size_t)(ct->c1 - ct->c0));
+    return SfheInternal::traced(this, ct, "Encrypt");
 }
 
 void CryptoContextImpl<DCRTPoly>::Decrypt(const PrivateKey<DCRTPoly>& sk,
@@ -842,7 +924,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalAdd(const Ciphertext<DCRTP
     sfp_add(st->dev, out->c1, a->c1, b->c1, SfheInternal::Q(ell));
     st->stats.add++;
     st->countBytes(6.0 * ell * st->n * 8);
-    return out;
+    return SfheInternal::traced(this, out, "EvalAdd");
 }
 
 void CryptoContextImpl<DCRTPoly>::EvalAddInPlace(Ciphertext<DCRTPoly>& a,
@@ -871,7 +953,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalAdd(const Ciphertext<DCRTP
     sfp_d2d(st->dev, out->c1, a->c1, (size_t)ell * st->n * 8);
     st->stats.add++;
     st->countBytes(4.0 * ell * st->n * 8);
-    return out;
+    return SfheInternal::traced(this, out, "EvalAdd");
 }
 
 void CryptoContextImpl<DCRTPoly>::EvalAddInPlace(Ciphertext<DCRTPoly>& a, double c) {
@@ -888,7 +970,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalAdd(const Ciphertext<DCRTP
     sfp_d2d(st->dev, out->c1, a->c1, (size_t)ell * st->n * 8);
     st->stats.add++;
     st->countBytes(5.0 * ell * st->n * 8);
-    return out;
+    return SfheInternal::traced(this, out, "EvalAdd");
 }
 
 void CryptoContextImpl<DCRTPoly>::EvalAddInPlace(Ciphertext<DCRTPoly>& a, const Plaintext& p) {
@@ -906,7 +988,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalSub(const Ciphertext<DCRTP
     sfp_sub(st->dev, out->c1, a->c1, b->c1, SfheInternal::Q(ell));
     st->stats.add++;
     st->countBytes(6.0 * ell * st->n * 8);
-    return out;
+    return SfheInternal::traced(this, out, "EvalSub");
 }
 
 void CryptoContextImpl<DCRTPoly>::EvalSubInPlace(Ciphertext<DCRTPoly>& a,
@@ -921,7 +1003,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalNegate(const Ciphertext<DC
     sfp_neg(st->dev, out->c0, a->c0, SfheInternal::Q(ell));
     sfp_neg(st->dev, out->c1, a->c1, SfheInternal::Q(ell));
     st->countBytes(4.0 * ell * st->n * 8);
-    return out;
+    return SfheInternal::traced(this, out, "EvalNegate");
 }
 
 void CryptoContextImpl<DCRTPoly>::EvalNegateInPlace(Ciphertext<DCRTPoly>& a) { a = EvalNegate(a); }
@@ -940,7 +1022,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalSub(const Ciphertext<DCRTP
     sfp_d2d(st->dev, out->c1, a->c1, (size_t)ell * st->n * 8);
     st->stats.add++;
     st->countBytes(5.0 * ell * st->n * 8);
-    return out;
+    return SfheInternal::traced(this, out, "EvalSub");
 }
 
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalSub(const Plaintext& p,
@@ -953,7 +1035,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalSub(const Plaintext& p,
     sfp_neg(st->dev, out->c1, a->c1, SfheInternal::Q(ell));
     st->stats.add++;
     st->countBytes(5.0 * ell * st->n * 8);
-    return out;
+    return SfheInternal::traced(this, out, "EvalSub");
 }
 
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalAddMany(
@@ -989,7 +1071,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMult(const Ciphertext<DCRT
     sfp_mul_const(s->dev, t1, a->c1, k.data(), SfheInternal::Q(ell));
     s->stats.constmult++;
     s->countBytes(4.0 * ell * s->n * 8);
-    return SfheInternal::rescale(this, t0, t1, a->level, a->slots);
+    return SfheInternal::traced(this, SfheInternal::rescale(this, t0, t1, a->level, a->slots), "EvalMult");
 }
 
 void CryptoContextImpl<DCRTPoly>::EvalMultInPlace(Ciphertext<DCRTPoly>& a, double c) {
@@ -1010,7 +1092,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMult(const Ciphertext<DCRT
     sfp_mul(s->dev, t1, a->c1, m, SfheInternal::Q(ell));
     s->stats.ptmult++;
     s->countBytes(5.0 * ell * s->n * 8);
-    return SfheInternal::rescale(this, t0, t1, a->level, std::max(a->slots, p->slots));
+    return SfheInternal::traced(this, SfheInternal::rescale(this, t0, t1, a->level, std::max(a->slots, p->slots)), "EvalMult");
 }
 
 void CryptoContextImpl<DCRTPoly>::EvalMultInPlace(Ciphertext<DCRTPoly>& a, const Plaintext& p) {
@@ -1034,7 +1116,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMult(const Ciphertext<DCRT
     s->stats.tensor++;
     s->countBytes(7.0 * ell * s->n * 8);
     SfheInternal::keySwitchAdd(this, d2, ell, s->relinKey, d0, d1);
-    return SfheInternal::rescale(this, d0, d1, a->level, std::max(a->slots, b->slots));
+    return SfheInternal::traced(this, SfheInternal::rescale(this, d0, d1, a->level, std::max(a->slots, b->slots)), "EvalMult");
 }
 
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalSquare(const Ciphertext<DCRTPoly>& a) {
@@ -1080,7 +1162,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMultAddPlain(
     }
     s->stats.ptmult += a.size();
     s->countBytes((3.0 * a.size() + 2.0) * ell * s->n * 8);
-    return SfheInternal::rescale(this, t0, t1, level, slots);
+    return SfheInternal::traced(this, SfheInternal::rescale(this, t0, t1, level, slots), "EvalMultAddPlain");
 }
 
 // ============================================================================
@@ -1105,7 +1187,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotate(const Ciphertext<DC
     s->stats.automorph++;
     s->countBytes(3.0 * ell * s->n * 8);
     SfheInternal::keySwitchAdd(this, t->ptr, ell, it->second, out->c0, out->c1);
-    return out;
+    return SfheInternal::traced(this, out, "EvalRotate");
 }
 
 std::shared_ptr<FastRotationPrecomp> CryptoContextImpl<DCRTPoly>::EvalFastRotationPrecompute(
@@ -1153,7 +1235,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalFastRotation(
     s->stats.keyswitch++;
     s->stats.automorph++;
     s->countBytes((3.0 * ell + 2.0 * pre->beta * (ell + s->K)) * s->n * 8);
-    return out;
+    return SfheInternal::traced(this, out, "EvalFastRotation");
 }
 
 // ============================================================================
@@ -1209,7 +1291,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::LinearWSumRescale(
         done += take;
         first = false;
     }
-    return SfheInternal::rescale(this, t0, t1, level, slots);
+    return SfheInternal::traced(this, SfheInternal::rescale(this, t0, t1, level, slots), "LinearWSumRescale");
 }
 
 

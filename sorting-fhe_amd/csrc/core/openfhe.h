@@ -101,7 +101,7 @@ class CCParams<CryptoContextCKKSRNS> {
     uint32_t ringDim = 0;
     SecurityLevel securityLevel = HEStd_128_classic;
     uint32_t numLargeDigits = 0;
-    ScalingTechnique scalingTechnique = FLEXIBLEAUTO;
+    ScalingTechnique scalingTechnique = FLEXIBLEAUTOEXT;  // OpenFHE default
     KeySwitchTechnique ksTech = HYBRID;
     int device = 0;
     uint64_t seed = 0x5eed5eed2025ULL;

@@ -36,7 +36,13 @@ struct SfheContextState {
     uint32_t K = 0;   // number of P primes
     uint32_t dnum = 0, alpha = 0;
     uint32_t batch = 0;
-    std::vector<uint64_t> primes;  // [q_0..q_L, p_0..p_{K-1}]
+    std::vector<uint64_t> primes;  // [q_0..q_L, p_0..p_{K-1}] (+ q_ext when ext)
+    // FLEXIBLEAUTOEXT: fresh encryptions are formed modulo Q*q_ext and
+    // rescaled by q_ext, so their noise is divided away (extIdx = Lq+K)
+    bool ext = false;
+    uint32_t extIdx = 0;
+    std::vector<uint64_t> extInvModQ;  // q_ext^{-1} mod q_i
+    std::vector<uint64_t> extModQ;     // q_ext mod q_i
     std::vector<sf_barrett> bar;
     std::vector<double> scale;  // canonical scale of each level 0..L
     sfp_dev* dev = nullptr;
@@ -47,6 +53,7 @@ struct SfheContextState {
     std::vector<uint64_t> pInvModQ;                         // P^{-1} mod q_i
     std::vector<uint64_t> pModQ;                            // P mod q_i
     std::vector<std::vector<uint64_t>> qInvTable;  // [ell][i] = q_{ell-1}^{-1} mod q_i
+    uint32_t tablePrimes() const { return Lq + K + (ext ? 1 : 0); }
 
     // keys
     DeviceBufferPtr relinKey;

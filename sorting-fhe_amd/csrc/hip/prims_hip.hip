@@ -1,0 +1,996 @@
+// gfx950 (MI355X, CDNA4) implementation of the RNS primitive layer
+// (csrc/prims.h).  All work is integer modular arithmetic on 64-bit
+// residues of <= 60-bit primes: HBM-bound streaming kernels, no MFMA.
+//
+// Layout: a polynomial is `count` rows of n u64 (limb-major).  Every kernel
+// maps (row, coefficient) -> thread with 16-byte per-lane accesses where the
+// access is contiguous, so a wave moves 1 KiB per instruction.
+//
+// NTT: n = R * 256 is processed in two LDS-staged passes per limb:
+//   column pass  - the first log2(R) Cooley-Tukey stages (strides >= 256)
+//                  on tiles of R rows x (4096/R) columns;
+//   row pass     - the last 8 stages (strides 128..1) on tiles of 16 rows
+//                  of 256 contiguous words.
+// Each pass reads and writes the limb once (2 HBM round trips per NTT).
+// The inverse runs the mirrored Gentleman-Sande passes and folds 1/n into
+// its last pass.  Twiddles are the bit-reversed psi tables (Shoup form).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../modarith.h"
+#include "../prims.h"
+
+#define SFP_CHECK(call)                                                     \
+    do {                                                                    \
+        hipError_t e_ = (call);                                             \
+        if (e_ != hipSuccess) record(d, #call, e_);                          \
+    } while (0)
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kTile = 4096;  // words per NTT tile (32 KiB of LDS)
+
+struct Bar {
+    u64 q, mu, r64;
+    uint32_t b, pad;
+};
+static_assert(sizeof(Bar) == sizeof(sf_barrett), "layout");
+
+__device__ __forceinline__ uint32_t primeOf(const sfp_limbs& m, uint32_t i) {
+    return i < m.split ? m.base + i : m.pbase + (i - m.split);
+}
+
+__device__ __forceinline__ u64 bmul(u64 a, u64 b, const sf_barrett& m) { return sf_mul(a, b, &m); }
+
+__device__ __forceinline__ sf_barrett loadBar(const sf_barrett* t, uint32_t p) {
+    sf_barrett m;
+    m.q = t[p].q;
+    m.mu = t[p].mu;
+    m.r64 = t[p].r64;
+    m.b = t[p].b;
+    m.pad = 0;
+    return m;
+}
+
+// 128-bit accumulator helpers
+struct Acc {
+    u64 lo, hi;
+};
+__device__ __forceinline__ void macc(Acc& a, u64 x, u64 y) {
+    u64 l = x * y;
+    u64 h = __umul64hi(x, y);
+    u64 s = a.lo + l;
+    a.hi += h + (s < l ? 1 : 0);
+    a.lo = s;
+}
+
+}  // namespace
+
+struct sfp_dev {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint32_t n = 0, logn = 0, np = 0;
+    sf_barrett* bar = nullptr;  // device [np]
+    u64 *psi = nullptr, *psiS = nullptr, *ipsi = nullptr, *ipsiS = nullptr;
+    u64 *ninv = nullptr, *ninvS = nullptr;
+    std::vector<sf_barrett> hbar;
+    // pinned argument ring (host) mirrored on the device
+    char* hring = nullptr;
+    char* dring = nullptr;
+    size_t ringCap = 0, ringOff = 0;
+    // pinned, host-coherent bounce buffer for bulk host<->device transfers
+    // (read / written by kernels directly)
+    char* bounce = nullptr;
+    size_t bounceCap = 0;
+    std::mutex mu;
+    std::string err;
+};
+
+struct sfp_conv {
+    uint32_t ns = 0, nt = 0;
+    uint32_t* src = nullptr;  // device
+    uint32_t* dst = nullptr;  // device
+    u64* inv = nullptr;       // device [ns]
+    u64* mod = nullptr;       // device [ns][nt]
+    u64* sprod = nullptr;     // device [nt]: prod(S) mod dst_t (centred conversion)
+    std::vector<uint32_t> hsrc, hdst;
+};
+
+static void record(sfp_dev* d, const char* what, hipError_t e) {
+    std::lock_guard<std::mutex> g(d->mu);
+    if (d->err.empty()) d->err = std::string(what) + ": " + hipGetErrorString(e);
+}
+
+static bool debugSync() {
+    static const bool on = [] {
+        const char* v = std::getenv("SFHE_DEBUG_SYNC");
+        return v && *v && *v != '0';
+    }();
+    return on;
+}
+
+static void checkLaunch(sfp_dev* d, const char* k) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) record(d, k, e);
+    if (debugSync()) {
+        e = hipStreamSynchronize(d->stream);
+        if (e != hipSuccess) record(d, k, e);
+    }
+}
+
+static unsigned gridFor(size_t work, unsigned perBlock) {
+    size_t g = (work + perBlock - 1) / perBlock;
+    return (unsigned)(g ? g : 1);
+}
+
+// ============================================================================
+// NTT kernels
+
+// Column pass: first log2(R) stages; tile = R rows x CW columns of one limb.
+template <bool INV>
+__global__ __launch_bounds__(kThreads) void k_ntt_col(u64* __restrict__ data, sfp_limbs m,
+                                                      const sf_barrett* __restrict__ bar,
+                                                      const u64* __restrict__ tw,
+                                                      const u64* __restrict__ twS,
+                                                      const u64* __restrict__ ninv,
+                                                      const u64* __restrict__ ninvS, uint32_t logn) {
+    __shared__ u64 s[kTile];
+    const uint32_t n = 1u << logn;
+    const uint32_t R = n >> 8;                 // rows of the 256-wide matrix
+    const uint32_t tile = n < kTile ? n : kTile;
+    const uint32_t CW = tile / R;              // columns per tile
+    const uint32_t limb = blockIdx.y;
+    const uint32_t p = primeOf(m, limb);
+    const u64 q = bar[p].q;
+    u64* a = data + (size_t)limb * n;
+    const u64* w = tw + (size_t)p * n;
+    const u64* wS = twS + (size_t)p * n;
+    const uint32_t c0 = blockIdx.x * CW;
+    for (uint32_t e = threadIdx.x; e < tile; e += kThreads) {
+        uint32_t r = e / CW, c = e % CW;
+        s[e] = a[(size_t)r * 256 + c0 + c];
+    }
+    __syncthreads();
+    const uint32_t nb = tile / 2;  // butterflies per stage
+    if (!INV) {
+        for (uint32_t tp = R >> 1, mm = 1; tp >= 1; tp >>= 1, mm <<= 1) {
+            for (uint32_t b = threadIdx.x; b < nb; b += kThreads) {
+                uint32_t c = b % CW, pr = b / CW;
+                uint32_t r = (pr / tp) * 2 * tp + (pr % tp);
+                u64 W = w[mm + r / (2 * tp)], WS = wS[mm + r / (2 * tp)];
+                u64 U = s[r * CW + c];
+                u64 V = sf_mul_shoup(s[(r + tp) * CW + c], W, WS, q);
+                s[r * CW + c] = sf_add(U, V, q);
+                s[(r + tp) * CW + c] = sf_sub(U, V, q);
+            }
+            __syncthreads();
+        }
+    } else {
+        for (uint32_t tp = 1; tp < R; tp <<= 1) {
+            const uint32_t h = R / (2 * tp);  // = n/(2t) with t = 256 tp
+            for (uint32_t b = threadIdx.x; b < nb; b += kThreads) {
+                uint32_t c = b % CW, pr = b / CW;
+                uint32_t r = (pr / tp) * 2 * tp + (pr % tp);
+                u64 W = w[h + r / (2 * tp)], WS = wS[h + r / (2 * tp)];
+                u64 U = s[r * CW + c], V = s[(r + tp) * CW + c];
+                s[r * CW + c] = sf_add(U, V, q);
+                s[(r + tp) * CW + c] = sf_mul_shoup(sf_sub(U, V, q), W, WS, q);
+            }
+            __syncthreads();
+        }
+        const u64 ni = ninv[p], niS = ninvS[p];
+        for (uint32_t e = threadIdx.x; e < tile; e += kThreads) s[e] = sf_mul_shoup(s[e], ni, niS, q);
+        __syncthreads();
+    }
+    for (uint32_t e = threadIdx.x; e < tile; e += kThreads) {
+        uint32_t r = e / CW, c = e % CW;
+        a[(size_t)r * 256 + c0 + c] = s[e];
+    }
+}
+
+// Row pass: last 8 stages on 16 rows of 256 contiguous words.
+template <bool INV>
+__global__ __launch_bounds__(kThreads) void k_ntt_row(u64* __restrict__ data, sfp_limbs m,
+                                                      const sf_barrett* __restrict__ bar,
+                                                      const u64* __restrict__ tw,
+                                                      const u64* __restrict__ twS, uint32_t logn) {
+    __shared__ u64 s[kTile];
+    const uint32_t n = 1u << logn;
+    const uint32_t limb = blockIdx.y;
+    const uint32_t p = primeOf(m, limb);
+    const u64 q = bar[p].q;
+    const size_t base = (size_t)blockIdx.x * kTile;  // first word of the 16-row tile
+    u64* a = data + (size_t)limb * n + base;
+    const u64* w = tw + (size_t)p * n;
+    const u64* wS = twS + (size_t)p * n;
+    {
+        const ulonglong2* src = reinterpret_cast<const ulonglong2*>(a);
+        ulonglong2* dst = reinterpret_cast<ulonglong2*>(s);
+        for (uint32_t e = threadIdx.x; e < kTile / 2; e += kThreads) dst[e] = src[e];
+    }
+    __syncthreads();
+    if (!INV) {
+        for (uint32_t t = 128; t >= 1; t >>= 1) {
+            const uint32_t mm = n / (2 * t);
+            for (uint32_t b = threadIdx.x; b < kTile / 2; b += kThreads) {
+                uint32_t j = (b / t) * 2 * t + (b % t);  // local index of the upper element
+                uint32_t idx = mm + (uint32_t)((base + j) / (2 * t));
+                u64 W = w[idx], WS = wS[idx];
+                u64 U = s[j];
+                u64 V = sf_mul_shoup(s[j + t], W, WS, q);
+                s[j] = sf_add(U, V, q);
+                s[j + t] = sf_sub(U, V, q);
+            }
+            __syncthreads();
+        }
+    } else {
+        for (uint32_t t = 1; t <= 128; t <<= 1) {
+            const uint32_t h = n / (2 * t);
+            for (uint32_t b = threadIdx.x; b < kTile / 2; b += kThreads) {
+                uint32_t j = (b / t) * 2 * t + (b % t);
+                uint32_t idx = h + (uint32_t)((base + j) / (2 * t));
+                u64 W = w[idx], WS = wS[idx];
+                u64 U = s[j], V = s[j + t];
+                s[j] = sf_add(U, V, q);
+                s[j + t] = sf_mul_shoup(sf_sub(U, V, q), W, WS, q);
+            }
+            __syncthreads();
+        }
+    }
+    {
+        const ulonglong2* src = reinterpret_cast<const ulonglong2*>(s);
+        ulonglong2* dst = reinterpret_cast<ulonglong2*>(a);
+        for (uint32_t e = threadIdx.x; e < kTile / 2; e += kThreads) dst[e] = src[e];
+    }
+}
+
+// ============================================================================
+// elementwise kernels: one thread per pair of coefficients (16 B per lane)
+
+enum EwOp { EW_ADD, EW_SUB, EW_NEG, EW_MUL, EW_MULADD, EW_MULC, EW_ADDC };
+
+struct ConstArgs {
+    u64 k[SFP_MAX_LIMBS];
+};
+
+template <int OP>
+__global__ __launch_bounds__(kThreads) void k_ew(u64* __restrict__ out, const u64* __restrict__ a,
+                                                 const u64* __restrict__ b, const u64* __restrict__ c,
+                                                 sfp_limbs m, const sf_barrett* __restrict__ bar,
+                                                 uint32_t logn, ConstArgs k) {
+    const size_t pairs = ((size_t)m.count << logn) >> 1;
+    for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < pairs;
+         i += (size_t)gridDim.x * kThreads) {
+        const uint32_t limb = (uint32_t)((2 * i) >> logn);
+        const sf_barrett B = loadBar(bar, primeOf(m, limb));
+        const u64 q = B.q;
+        ulonglong2 x = reinterpret_cast<const ulonglong2*>(a)[i];
+        ulonglong2 r;
+        if (OP == EW_ADD || OP == EW_SUB || OP == EW_MUL || OP == EW_MULADD) {
+            ulonglong2 y = reinterpret_cast<const ulonglong2*>(b)[i];
+            if (OP == EW_ADD) {
+                r.x = sf_add(x.x, y.x, q);
+                r.y = sf_add(x.y, y.y, q);
+            } else if (OP == EW_SUB) {
+                r.x = sf_sub(x.x, y.x, q);
+                r.y = sf_sub(x.y, y.y, q);
+            } else {
+                r.x = bmul(x.x, y.x, B);
+                r.y = bmul(x.y, y.y, B);
+                if (OP == EW_MULADD) {
+                    ulonglong2 z = reinterpret_cast<const ulonglong2*>(c)[i];
+                    r.x = sf_add(r.x, z.x, q);
+                    r.y = sf_add(r.y, z.y, q);
+                }
+            }
+        } else if (OP == EW_NEG) {
+            r.x = sf_neg(x.x, q);
+            r.y = sf_neg(x.y, q);
+        } else if (OP == EW_MULC) {
+            r.x = bmul(x.x, k.k[limb], B);
+            r.y = bmul(x.y, k.k[limb], B);
+        } else {  // EW_ADDC
+            r.x = sf_add(x.x, k.k[limb], q);
+            r.y = sf_add(x.y, k.k[limb], q);
+        }
+        reinterpret_cast<ulonglong2*>(out)[i] = r;
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void k_tensor(u64* __restrict__ d0, u64* __restrict__ d1,
+                                                     u64* __restrict__ d2, const u64* __restrict__ a0,
+                                                     const u64* __restrict__ a1, const u64* __restrict__ b0,
+                                                     const u64* __restrict__ b1, sfp_limbs m,
+                                                     const sf_barrett* __restrict__ bar, uint32_t logn) {
+    const size_t total = (size_t)m.count << logn;
+    for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < total;
+         i += (size_t)gridDim.x * kThreads) {
+        const sf_barrett B = loadBar(bar, primeOf(m, (uint32_t)(i >> logn)));
+        u64 x0 = a0[i], x1 = a1[i], y0 = b0[i], y1 = b1[i];
+        Acc t{0, 0};
+        macc(t, x0, y1);
+        macc(t, x1, y0);
+        u64 r0 = bmul(x0, y0, B);
+        u64 r1 = sf_reduce128_acc(t.lo, t.hi, &B);
+        u64 r2 = bmul(x1, y1, B);
+        d0[i] = r0;
+        d1[i] = r1;
+        d2[i] = r2;
+    }
+}
+
+struct PtrList {
+    const u64* p[SFP_MAX_WSUM];
+};
+struct PtrList2 {
+    const u64* a[SFP_MAX_WSUM];
+    const u64* b[SFP_MAX_WSUM];
+};
+
+// out = sum_j ins[j] * k[j][limb]   (k: device array nin x count)
+__global__ __launch_bounds__(kThreads) void k_lin_wsum(u64* __restrict__ out, PtrList ins,
+                                                       const u64* __restrict__ k, uint32_t nin,
+                                                       sfp_limbs m, const sf_barrett* __restrict__ bar,
+                                                       uint32_t logn) {
+    const size_t total = (size_t)m.count << logn;
+    for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < total;
+         i += (size_t)gridDim.x * kThreads) {
+        const uint32_t limb = (uint32_t)(i >> logn);
+        const sf_barrett B = loadBar(bar, primeOf(m, limb));
+        Acc acc{0, 0};
+        for (uint32_t j = 0; j < nin; ++j) macc(acc, ins.p[j][i], k[(size_t)j * m.count + limb]);
+        out[i] = sf_reduce128_acc(acc.lo, acc.hi, &B);
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void k_mac_plain(u64* __restrict__ out, PtrList2 ab,
+                                                        uint32_t nin, sfp_limbs m,
+                                                        const sf_barrett* __restrict__ bar,
+                                                        uint32_t logn) {
+    const size_t total = (size_t)m.count << logn;
+    for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < total;
+         i += (size_t)gridDim.x * kThreads) {
+        const sf_barrett B = loadBar(bar, primeOf(m, (uint32_t)(i >> logn)));
+        Acc acc{0, 0};
+        for (uint32_t j = 0; j < nin; ++j) macc(acc, ab.a[j][i], ab.b[j][i]);
+        out[i] = sf_reduce128_acc(acc.lo, acc.hi, &B);
+    }
+}
+
+// out[k] = in[perm_g(k)] for every limb
+__global__ __launch_bounds__(kThreads) void k_automorph(u64* __restrict__ out, const u64* __restrict__ in,
+                                                        uint32_t g, uint32_t count, uint32_t logn) {
+    const uint32_t n = 1u << logn;
+    const size_t total = (size_t)count << logn;
+    const u64 mask = 2ull * n - 1;
+    for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < total;
+         i += (size_t)gridDim.x * kThreads) {
+        const uint32_t kk = (uint32_t)(i & (n - 1));
+        const size_t row = i - kk;
+        const u64 e = 2ull * sf_brev(kk, logn) + 1;
+        const u64 ge = (e * g) & mask;
+        const uint32_t src = sf_brev((uint32_t)((ge - 1) >> 1), logn);
+        out[i] = in[row + src];
+    }
+}
+
+// ============================================================================
+// rescale helpers
+
+// rows[i][x] = centred(v[x]) mod q_i   for i < cnt  (v in [0, q_last))
+__global__ __launch_bounds__(kThreads) void k_bcast_centered(u64* __restrict__ rows, const u64* __restrict__ v,
+                                                             uint32_t cnt, u64 ql,
+                                                             const sf_barrett* __restrict__ bar,
+                                                             uint32_t logn) {
+    const size_t total = (size_t)cnt << logn;
+    const u64 half = ql >> 1;
+    for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < total;
+         i += (size_t)gridDim.x * kThreads) {
+        const uint32_t r = (uint32_t)(i >> logn);
+        const sf_barrett B = loadBar(bar, r);
+        const u64 x = v[i & ((1ull << logn) - 1)];
+        u64 y = sf_reduce128(x, 0, &B);
+        if (x > half) y = sf_sub(y, sf_reduce128(ql, 0, &B), B.q);
+        rows[i] = y;
+    }
+}
+
+// out_i = (in_i - t_i) * k_i
+__global__ __launch_bounds__(kThreads) void k_sub_mulc(u64* __restrict__ out, const u64* __restrict__ in,
+                                                       const u64* __restrict__ t, uint32_t cnt, ConstArgs k,
+                                                       const sf_barrett* __restrict__ bar, uint32_t logn,
+                                                       int add) {
+    const size_t total = (size_t)cnt << logn;
+    for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < total;
+         i += (size_t)gridDim.x * kThreads) {
+        const uint32_t r = (uint32_t)(i >> logn);
+        const sf_barrett B = loadBar(bar, r);
+        u64 v = bmul(sf_sub(in[i], t[i], B.q), k.k[r], B);
+        out[i] = add ? sf_add(out[i], v, B.q) : v;
+    }
+}
+
+// ============================================================================
+// fast base conversion (coefficient domain)
+//   out row rowOf(t) = sum_i [x_i * inv_i]_{s_i} * mod[i][t]  mod prime dst[t]
+// rowOf(t) = dst[t] < Lq ? dst[t] : ell + (dst[t] - Lq)   (ext layout), or
+// rowOf(t) = t when ell == 0xffffffff (dense layout).
+constexpr int kMaxConvSrc = 32;
+
+// centered != 0: each y_i is taken in (-s_i/2, s_i/2] (subtracting prod(S)
+// mod t once per y_i > s_i/2), which makes the ModDown conversion error
+// sum_i y_i/s_i zero-mean: a rounding, not a floor with a +K/2 bias.
+__global__ __launch_bounds__(kThreads) void k_conv(u64* __restrict__ out, const u64* __restrict__ src,
+                                                   const uint32_t* __restrict__ sidx,
+                                                   const uint32_t* __restrict__ didx,
+                                                   const u64* __restrict__ inv, const u64* __restrict__ mod,
+                                                   const u64* __restrict__ sprod,
+                                                   uint32_t ns, uint32_t nt, uint32_t ntUse,
+                                                   const sf_barrett* __restrict__ bar, uint32_t logn,
+                                                   uint32_t ell, uint32_t Lq, int centered) {
+    extern __shared__ u64 smod[];  // ns * nt
+    for (uint32_t e = threadIdx.x; e < ns * nt; e += kThreads) smod[e] = mod[e];
+    __syncthreads();
+    const uint32_t n = 1u << logn;
+    for (uint32_t x = blockIdx.x * kThreads + threadIdx.x; x < n; x += gridDim.x * kThreads) {
+        u64 y[kMaxConvSrc];
+        u64 neg = 0;
+#pragma unroll
+        for (int i = 0; i < kMaxConvSrc; ++i) {
+            if ((uint32_t)i < ns) {
+                const sf_barrett B = loadBar(bar, sidx[i]);
+                y[i] = bmul(src[((size_t)i << logn) + x], inv[i], B);
+                if (centered && y[i] > (B.q >> 1)) ++neg;
+            }
+        }
+        for (uint32_t t = 0; t < ntUse; ++t) {
+            Acc acc{0, 0};
+#pragma unroll
+            for (int i = 0; i < kMaxConvSrc; ++i)
+                if ((uint32_t)i < ns) macc(acc, y[i], smod[i * nt + t]);
+            const uint32_t pt = didx[t];
+            const sf_barrett B = loadBar(bar, pt);
+            const uint32_t row = ell == 0xffffffffu ? t : (pt < Lq ? pt : ell + (pt - Lq));
+            u64 v = sf_reduce128_acc(acc.lo, acc.hi, &B);
+            if (neg) v = sf_sub(v, bmul(neg, sprod[t], B), B.q);
+            out[((size_t)row << logn) + x] = v;
+        }
+    }
+}
+
+// key inner product over ext rows t < ell+K
+__global__ __launch_bounds__(kThreads) void k_ks_inner(u64* __restrict__ acc0, u64* __restrict__ acc1,
+                                                       const u64* __restrict__ ext, size_t extStride,
+                                                       const u64* __restrict__ key, uint32_t beta,
+                                                       uint32_t ell, uint32_t K, uint32_t Lq,
+                                                       const sf_barrett* __restrict__ bar, uint32_t logn) {
+    const uint32_t rows = ell + K, NP = Lq + K;
+    const size_t total = (size_t)rows << logn;
+    const uint32_t n = 1u << logn;
+    for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < total;
+         i += (size_t)gridDim.x * kThreads) {
+        const uint32_t t = (uint32_t)(i >> logn);
+        const uint32_t x = (uint32_t)(i & (n - 1));
+        const uint32_t kr = t < ell ? t : Lq + (t - ell);
+        const sf_barrett B = loadBar(bar, kr);
+        Acc s0{0, 0}, s1{0, 0};
+        for (uint32_t j = 0; j < beta; ++j) {
+            const u64 e = ext[j * extStride + i];
+            const u64* kb = key + (size_t)j * 2 * NP * n;
+            const u64* ka = kb + (size_t)NP * n;
+            macc(s0, e, kb[((size_t)kr << logn) + x]);
+            macc(s1, e, ka[((size_t)kr << logn) + x]);
+        }
+        acc0[i] = sf_reduce128_acc(s0.lo, s0.hi, &B);
+        acc1[i] = sf_reduce128_acc(s1.lo, s1.hi, &B);
+    }
+}
+
+// ============================================================================
+// sampling / loading
+
+__device__ __forceinline__ u64 smix(u64 x) {
+    x += 0x9E3779B97F4A7C15ULL;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    return x ^ (x >> 31);
+}
+
+__global__ __launch_bounds__(kThreads) void k_uniform(u64* __restrict__ p, sfp_limbs m, u64 seed,
+                                                      const sf_barrett* __restrict__ bar, uint32_t logn) {
+    const size_t total = (size_t)m.count << logn;
+    const uint32_t n = 1u << logn;
+    for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < total;
+         i += (size_t)gridDim.x * kThreads) {
+        const uint32_t limb = (uint32_t)(i >> logn);
+        const uint32_t pi = primeOf(m, limb);
+        const sf_barrett B = loadBar(bar, pi);
+        const u64 base = smix(seed ^ (0xD1B54A32D192ED03ULL * (u64)(pi + 1)));
+        const u64 x = i & (n - 1);
+        const u64 r0 = smix(base + 2 * x), r1 = smix(base + 2 * x + 1);
+        p[i] = sf_reduce128_acc(r0, r1, &B);
+    }
+}
+
+// One thread per coefficient: the signed input (pinned host memory, read
+// once over the host link) is reduced into every limb.
+__global__ __launch_bounds__(kThreads) void k_load_i64(u64* __restrict__ p, const int64_t* __restrict__ c,
+                                                       sfp_limbs m, const sf_barrett* __restrict__ bar,
+                                                       uint32_t logn) {
+    const uint32_t n = 1u << logn;
+    for (uint32_t x = blockIdx.x * kThreads + threadIdx.x; x < n; x += gridDim.x * kThreads) {
+        const int64_t v = c[x];
+        const u64 a = v < 0 ? (u64)(-(v + 1)) + 1 : (u64)v;
+        for (uint32_t limb = 0; limb < m.count; ++limb) {
+            const sf_barrett B = loadBar(bar, primeOf(m, limb));
+            const u64 r = sf_reduce128(a, 0, &B);
+            p[((size_t)limb << logn) + x] = (v < 0 && r) ? B.q - r : r;
+        }
+    }
+}
+
+// Plain copies run as kernels on the compute stream (never on the DMA
+// engines), so every byte movement is ordered with the arithmetic around it.
+__global__ __launch_bounds__(kThreads) void k_copy16(ulonglong2* __restrict__ dst,
+                                                     const ulonglong2* __restrict__ src, size_t cnt) {
+    for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < cnt; i += (size_t)gridDim.x * kThreads)
+        dst[i] = src[i];
+}
+__global__ __launch_bounds__(kThreads) void k_copy1(unsigned char* __restrict__ dst,
+                                                    const unsigned char* __restrict__ src, size_t cnt) {
+    for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < cnt; i += (size_t)gridDim.x * kThreads)
+        dst[i] = src[i];
+}
+__global__ __launch_bounds__(kThreads) void k_fill16(ulonglong2* __restrict__ dst, size_t cnt) {
+    for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < cnt; i += (size_t)gridDim.x * kThreads)
+        dst[i] = make_ulonglong2(0, 0);
+}
+__global__ __launch_bounds__(kThreads) void k_fill1(unsigned char* __restrict__ dst, size_t cnt) {
+    for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < cnt; i += (size_t)gridDim.x * kThreads)
+        dst[i] = 0;
+}
+
+// ============================================================================
+// host side
+
+static unsigned ewGrid(size_t work) {
+    size_t g = (work + kThreads - 1) / kThreads;
+    if (g > 256 * 16) g = 256 * 16;
+    return (unsigned)(g ? g : 1);
+}
+
+// Device-side byte copy on the compute stream (either side may be pinned
+// host memory).  Never uses the DMA engines: see DESIGN.md "transfers".
+static void devCopy(sfp_dev* d, void* dst, const void* src, size_t b) {
+    if (!b) return;
+    if ((((uintptr_t)dst | (uintptr_t)src | b) & 15) == 0) {
+        const size_t cnt = b / 16;
+        hipLaunchKernelGGL(k_copy16, dim3(ewGrid(cnt)), dim3(kThreads), 0, d->stream, (ulonglong2*)dst,
+                           (const ulonglong2*)src, cnt);
+    } else {
+        hipLaunchKernelGGL(k_copy1, dim3(ewGrid(b)), dim3(kThreads), 0, d->stream, (unsigned char*)dst,
+                           (const unsigned char*)src, b);
+    }
+    checkLaunch(d, "copy");
+}
+
+static void devZero(sfp_dev* d, void* dst, size_t b) {
+    if (!b) return;
+    if ((((uintptr_t)dst | b) & 15) == 0) {
+        hipLaunchKernelGGL(k_fill16, dim3(ewGrid(b / 16)), dim3(kThreads), 0, d->stream, (ulonglong2*)dst,
+                           b / 16);
+    } else {
+        hipLaunchKernelGGL(k_fill1, dim3(ewGrid(b)), dim3(kThreads), 0, d->stream, (unsigned char*)dst, b);
+    }
+    checkLaunch(d, "zero");
+}
+
+// Small host array -> device memory, ordered on the stream: staged in the
+// pinned ring, pulled across by a copy kernel.  The ring region is reused
+// only after the stream has drained past every earlier pull.
+static void* ringPut(sfp_dev* d, const void* src, size_t bytes) {
+    bytes = (bytes + 255) & ~(size_t)255;
+    if (d->ringOff + bytes > d->ringCap) {
+        hipStreamSynchronize(d->stream);
+        d->ringOff = 0;
+    }
+    char* h = d->hring + d->ringOff;
+    char* dv = d->dring + d->ringOff;
+    std::memcpy(h, src, bytes);
+    devCopy(d, dv, h, bytes);
+    d->ringOff += bytes;
+    return dv;
+}
+
+// Bulk host -> device through the bounce buffer, chunk by chunk.
+static void hostToDev(sfp_dev* d, void* dst, const void* src, size_t b) {
+    SFP_CHECK(hipStreamSynchronize(d->stream));
+    for (size_t off = 0; off < b; off += d->bounceCap) {
+        const size_t c = b - off < d->bounceCap ? b - off : d->bounceCap;
+        std::memcpy(d->bounce, (const char*)src + off, c);
+        devCopy(d, (char*)dst + off, d->bounce, c);
+        SFP_CHECK(hipStreamSynchronize(d->stream));
+    }
+}
+
+static void devToHost(sfp_dev* d, void* dst, const void* src, size_t b) {
+    for (size_t off = 0; off < b; off += d->bounceCap) {
+        const size_t c = b - off < d->bounceCap ? b - off : d->bounceCap;
+        devCopy(d, d->bounce, (const char*)src + off, c);
+        SFP_CHECK(hipStreamSynchronize(d->stream));
+        std::memcpy((char*)dst + off, d->bounce, c);
+    }
+}
+
+// (C linkage comes from the declarations in prims.h)
+
+const char* sfp_backend_name(void) { return "hip-gfx950"; }
+
+sfp_dev* sfp_create(int device, const sfp_tables* t) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device) return nullptr;
+    if (hipSetDevice(device) != hipSuccess) return nullptr;
+    auto* d = new sfp_dev;
+    d->device = device;
+    d->logn = t->logn;
+    d->n = 1u << t->logn;
+    d->np = t->nprimes;
+    if (d->logn < 12) {
+        delete d;
+        return nullptr;  // kernels assume n >= 4096
+    }
+    if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete d;
+        return nullptr;
+    }
+    d->hbar.resize(d->np);
+    for (uint32_t i = 0; i < d->np; ++i) d->hbar[i] = sf_make_barrett(t->primes[i]);
+    const size_t tn = (size_t)d->np * d->n * 8;
+    bool ok = hipMalloc(&d->bar, d->np * sizeof(sf_barrett)) == hipSuccess &&
+              hipMalloc(&d->psi, tn) == hipSuccess && hipMalloc(&d->psiS, tn) == hipSuccess &&
+              hipMalloc(&d->ipsi, tn) == hipSuccess && hipMalloc(&d->ipsiS, tn) == hipSuccess &&
+              hipMalloc(&d->ninv, d->np * 8) == hipSuccess &&
+              hipMalloc(&d->ninvS, d->np * 8) == hipSuccess;
+    d->ringCap = (size_t)16 << 20;
+    d->bounceCap = (size_t)32 << 20;
+    ok = ok &&
+         hipHostMalloc((void**)&d->hring, d->ringCap, hipHostMallocMapped | hipHostMallocCoherent) ==
+             hipSuccess &&
+         hipMalloc((void**)&d->dring, d->ringCap) == hipSuccess &&
+         hipHostMalloc((void**)&d->bounce, d->bounceCap, hipHostMallocMapped | hipHostMallocCoherent) ==
+             hipSuccess;
+    if (!ok) {
+        delete d;
+        return nullptr;
+    }
+    hostToDev(d, d->bar, d->hbar.data(), d->np * sizeof(sf_barrett));
+    hostToDev(d, d->psi, t->psi_rev, tn);
+    hostToDev(d, d->psiS, t->psi_rev_shoup, tn);
+    hostToDev(d, d->ipsi, t->ipsi_rev, tn);
+    hostToDev(d, d->ipsiS, t->ipsi_rev_shoup, tn);
+    hostToDev(d, d->ninv, t->n_inv, d->np * 8);
+    hostToDev(d, d->ninvS, t->n_inv_shoup, d->np * 8);
+    if (!d->err.empty()) {
+        sfp_destroy(d);
+        return nullptr;
+    }
+    return d;
+}
+
+void sfp_destroy(sfp_dev* d) {
+    if (!d) return;
+    hipStreamSynchronize(d->stream);
+    hipFree(d->bar);
+    hipFree(d->psi);
+    hipFree(d->psiS);
+    hipFree(d->ipsi);
+    hipFree(d->ipsiS);
+    hipFree(d->ninv);
+    hipFree(d->ninvS);
+    hipFree(d->dring);
+    hipHostFree(d->hring);
+    hipHostFree(d->bounce);
+    hipStreamDestroy(d->stream);
+    delete d;
+}
+
+void* sfp_alloc(sfp_dev* d, size_t bytes) {
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes ? bytes : 8) != hipSuccess) {
+        hipGetLastError();
+        return nullptr;
+    }
+    return p;
+}
+void sfp_free(sfp_dev* d, void* p) {
+    (void)d;
+    hipFree(p);
+}
+void sfp_h2d(sfp_dev* d, void* dst, const void* src, size_t b) { hostToDev(d, dst, src, b); }
+void sfp_d2h(sfp_dev* d, void* dst, const void* src, size_t b) { devToHost(d, dst, src, b); }
+void sfp_d2d(sfp_dev* d, void* dst, const void* src, size_t b) { devCopy(d, dst, src, b); }
+void sfp_zero(sfp_dev* d, void* dst, size_t b) { devZero(d, dst, b); }
+void sfp_sync(sfp_dev* d) { SFP_CHECK(hipStreamSynchronize(d->stream)); }
+const char* sfp_last_error(sfp_dev* d) {
+    hipError_t e = hipStreamQuery(d->stream);
+    if (e != hipSuccess && e != hipErrorNotReady) record(d, "stream", e);
+    std::lock_guard<std::mutex> g(d->mu);
+    return d->err.empty() ? nullptr : d->err.c_str();
+}
+
+// ---- NTT ----
+void sfp_ntt(sfp_dev* d, uint64_t* p, sfp_limbs m, int inverse) {
+    if (!m.count) return;
+    const uint32_t n = d->n;
+    const uint32_t tile = n < (uint32_t)kTile ? n : (uint32_t)kTile;
+    dim3 gcol(n / tile, m.count), grow(n / kTile, m.count);
+    if (!inverse) {
+        hipLaunchKernelGGL(k_ntt_col<false>, gcol, dim3(kThreads), 0, d->stream, p, m, d->bar, d->psi,
+                           d->psiS, d->ninv, d->ninvS, d->logn);
+        hipLaunchKernelGGL(k_ntt_row<false>, grow, dim3(kThreads), 0, d->stream, p, m, d->bar, d->psi,
+                           d->psiS, d->logn);
+    } else {
+        hipLaunchKernelGGL(k_ntt_row<true>, grow, dim3(kThreads), 0, d->stream, p, m, d->bar, d->ipsi,
+                           d->ipsiS, d->logn);
+        hipLaunchKernelGGL(k_ntt_col<true>, gcol, dim3(kThreads), 0, d->stream, p, m, d->bar, d->ipsi,
+                           d->ipsiS, d->ninv, d->ninvS, d->logn);
+    }
+    checkLaunch(d, "ntt");
+}
+
+// ---- elementwise ----
+template <int OP>
+static void ew(sfp_dev* d, u64* out, const u64* a, const u64* b, const u64* c, sfp_limbs m,
+               const u64* k) {
+    if (!m.count) return;
+    ConstArgs ka;
+    if (k) std::memcpy(ka.k, k, m.count * 8);
+    const size_t pairs = ((size_t)m.count * d->n) / 2;
+    hipLaunchKernelGGL(k_ew<OP>, dim3(ewGrid(pairs)), dim3(kThreads), 0, d->stream, out, a, b, c, m,
+                       d->bar, d->logn, ka);
+    checkLaunch(d, "elementwise");
+}
+
+void sfp_add(sfp_dev* d, uint64_t* out, const uint64_t* a, const uint64_t* b, sfp_limbs m) {
+    ew<EW_ADD>(d, out, a, b, nullptr, m, nullptr);
+}
+void sfp_sub(sfp_dev* d, uint64_t* out, const uint64_t* a, const uint64_t* b, sfp_limbs m) {
+    ew<EW_SUB>(d, out, a, b, nullptr, m, nullptr);
+}
+void sfp_neg(sfp_dev* d, uint64_t* out, const uint64_t* a, sfp_limbs m) {
+    ew<EW_NEG>(d, out, a, nullptr, nullptr, m, nullptr);
+}
+void sfp_mul(sfp_dev* d, uint64_t* out, const uint64_t* a, const uint64_t* b, sfp_limbs m) {
+    ew<EW_MUL>(d, out, a, b, nullptr, m, nullptr);
+}
+void sfp_mul_add(sfp_dev* d, uint64_t* out, const uint64_t* a, const uint64_t* b,
+                 const uint64_t* c, sfp_limbs m) {
+    ew<EW_MULADD>(d, out, a, b, c, m, nullptr);
+}
+void sfp_mul_const(sfp_dev* d, uint64_t* out, const uint64_t* a, const uint64_t* k, sfp_limbs m) {
+    ew<EW_MULC>(d, out, a, nullptr, nullptr, m, k);
+}
+void sfp_add_const(sfp_dev* d, uint64_t* out, const uint64_t* a, const uint64_t* k, sfp_limbs m) {
+    ew<EW_ADDC>(d, out, a, nullptr, nullptr, m, k);
+}
+
+void sfp_tensor(sfp_dev* d, uint64_t* d0, uint64_t* d1, uint64_t* d2, const uint64_t* a0,
+                const uint64_t* a1, const uint64_t* b0, const uint64_t* b1, sfp_limbs m) {
+    const size_t total = (size_t)m.count * d->n;
+    hipLaunchKernelGGL(k_tensor, dim3(ewGrid(total)), dim3(kThreads), 0, d->stream, d0, d1, d2, a0, a1,
+                       b0, b1, m, d->bar, d->logn);
+    checkLaunch(d, "tensor");
+}
+
+void sfp_lin_wsum(sfp_dev* d, uint64_t* out, const uint64_t* const* ins, const uint64_t* k,
+                  uint32_t nin, sfp_limbs m) {
+    if (nin > SFP_MAX_WSUM) {
+        record(d, "lin_wsum", hipErrorInvalidValue);
+        return;
+    }
+    PtrList pl;
+    for (uint32_t j = 0; j < nin; ++j) pl.p[j] = ins[j];
+    const u64* dk = (const u64*)ringPut(d, k, (size_t)nin * m.count * 8);
+    const size_t total = (size_t)m.count * d->n;
+    hipLaunchKernelGGL(k_lin_wsum, dim3(ewGrid(total)), dim3(kThreads), 0, d->stream, out, pl, dk, nin,
+                       m, d->bar, d->logn);
+    checkLaunch(d, "lin_wsum");
+}
+
+void sfp_mac_plain(sfp_dev* d, uint64_t* out, const uint64_t* const* a, const uint64_t* const* b,
+                   uint32_t nin, sfp_limbs m) {
+    if (nin > SFP_MAX_WSUM) {
+        record(d, "mac_plain", hipErrorInvalidValue);
+        return;
+    }
+    PtrList2 pl;
+    for (uint32_t j = 0; j < nin; ++j) {
+        pl.a[j] = a[j];
+        pl.b[j] = b[j];
+    }
+    const size_t total = (size_t)m.count * d->n;
+    hipLaunchKernelGGL(k_mac_plain, dim3(ewGrid(total)), dim3(kThreads), 0, d->stream, out, pl, nin, m,
+                       d->bar, d->logn);
+    checkLaunch(d, "mac_plain");
+}
+
+void sfp_automorph(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t g, sfp_limbs m) {
+    const size_t total = (size_t)m.count * d->n;
+    hipLaunchKernelGGL(k_automorph, dim3(ewGrid(total)), dim3(kThreads), 0, d->stream, out, in, g,
+                       m.count, d->logn);
+    checkLaunch(d, "automorph");
+}
+
+// ---- scratch owned by the backend (grow-only) ----
+static u64* scratch(sfp_dev* d, size_t words) {
+    static thread_local sfp_dev* owner = nullptr;
+    struct S {
+        u64* p = nullptr;
+        size_t w = 0;
+    };
+    static std::mutex mu;
+    static std::vector<std::pair<sfp_dev*, S>> pool;
+    std::lock_guard<std::mutex> g(mu);
+    (void)owner;
+    for (auto& e : pool)
+        if (e.first == d) {
+            if (e.second.w < words) {
+                hipStreamSynchronize(d->stream);
+                hipFree(e.second.p);
+                hipMalloc(&e.second.p, words * 8);
+                e.second.w = words;
+            }
+            return e.second.p;
+        }
+    S s;
+    hipMalloc(&s.p, words * 8);
+    s.w = words;
+    pool.push_back({d, s});
+    return s.p;
+}
+
+void sfp_rescale(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t ell, const uint64_t* qlinv,
+                 uint32_t npoly, size_t inStride, size_t outStride) {
+    sfp_rescale_ext(d, out, in, ell, ell - 1, qlinv, npoly, inStride, outStride);
+}
+
+void sfp_rescale_ext(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t ell, uint32_t dropPrime,
+                     const uint64_t* qlinv, uint32_t npoly, size_t inStride, size_t outStride) {
+    const uint32_t n = d->n;
+    const uint32_t cnt = ell - 1;
+    u64* tmp = scratch(d, (size_t)(cnt + 1) * n);
+    u64* last = tmp + (size_t)cnt * n;
+    ConstArgs k;
+    std::memcpy(k.k, qlinv, cnt * 8);
+    const u64 ql = d->hbar[dropPrime].q;
+    for (uint32_t p = 0; p < npoly; ++p) {
+        const u64* src = in + p * inStride;
+        u64* dst = out + p * outStride;
+        devCopy(d, last, src + (size_t)cnt * n, (size_t)n * 8);
+        sfp_ntt(d, last, sfp_limbs{1, 0, dropPrime, 0}, 1);
+        hipLaunchKernelGGL(k_bcast_centered, dim3(ewGrid((size_t)cnt * n)), dim3(kThreads), 0, d->stream,
+                           tmp, last, cnt, ql, d->bar, d->logn);
+        sfp_ntt(d, tmp, sfp_limbs{cnt, cnt, 0, 0}, 0);
+        hipLaunchKernelGGL(k_sub_mulc, dim3(ewGrid((size_t)cnt * n)), dim3(kThreads), 0, d->stream, dst,
+                           src, tmp, cnt, k, d->bar, d->logn, 0);
+        checkLaunch(d, "rescale");
+    }
+}
+
+// ---- base conversion / key switching ----
+sfp_conv* sfp_upload_conv(sfp_dev* d, uint32_t ns, const uint32_t* src, uint32_t nt,
+                          const uint32_t* dst, const uint64_t* inv, const uint64_t* mod) {
+    if (ns > (uint32_t)kMaxConvSrc) {
+        record(d, "upload_conv (too many source primes)", hipErrorInvalidValue);
+        return nullptr;
+    }
+    auto* c = new sfp_conv;
+    c->ns = ns;
+    c->nt = nt;
+    c->hsrc.assign(src, src + ns);
+    c->hdst.assign(dst, dst + nt);
+    hipMalloc(&c->src, ns * 4);
+    hipMalloc(&c->dst, nt * 4);
+    hipMalloc(&c->inv, ns * 8);
+    hipMalloc(&c->mod, (size_t)ns * nt * 8);
+    hostToDev(d, c->src, src, ns * 4);
+    hostToDev(d, c->dst, dst, nt * 4);
+    hostToDev(d, c->inv, inv, ns * 8);
+    hostToDev(d, c->mod, mod, (size_t)ns * nt * 8);
+    std::vector<u64> sp(nt);
+    for (uint32_t t = 0; t < nt; ++t) {
+        const sf_barrett& B = d->hbar[dst[t]];
+        u64 r = 1;
+        for (uint32_t i = 0; i < ns; ++i) r = sf_mul(r, d->hbar[src[i]].q % B.q, &B);
+        sp[t] = r;
+    }
+    hipMalloc(&c->sprod, nt * 8);
+    hostToDev(d, c->sprod, sp.data(), nt * 8);
+    return c;
+}
+
+void sfp_free_conv(sfp_dev* d, sfp_conv* c) {
+    if (!c) return;
+    hipStreamSynchronize(d->stream);
+    hipFree(c->src);
+    hipFree(c->dst);
+    hipFree(c->inv);
+    hipFree(c->mod);
+    hipFree(c->sprod);
+    delete c;
+}
+
+static void convLaunch(sfp_dev* d, u64* out, const u64* src, const sfp_conv* c, uint32_t ntUse,
+                       uint32_t ell, uint32_t Lq, int centered) {
+    const size_t lds = (size_t)c->ns * c->nt * 8;
+    hipLaunchKernelGGL(k_conv, dim3(ewGrid(d->n)), dim3(kThreads), lds, d->stream, out, src, c->src,
+                       c->dst, c->inv, c->mod, c->sprod, c->ns, c->nt, ntUse, d->bar, d->logn, ell, Lq,
+                       centered);
+    checkLaunch(d, "conv");
+}
+
+void sfp_conv_apply(sfp_dev* d, uint64_t* dst, const uint64_t* src, const sfp_conv* c) {
+    convLaunch(d, dst, src, c, c->nt, 0xffffffffu, 0, 0);
+}
+
+void sfp_modup(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t ell, uint32_t K,
+               uint32_t Lq, uint32_t lo, uint32_t hi, const sfp_conv* c, uint64_t* scr) {
+    const uint32_t n = d->n, ns = hi - lo;
+    devCopy(d, scr, in + (size_t)lo * n, (size_t)ns * n * 8);
+    sfp_ntt(d, scr, sfp_limbs{ns, ns, 0, lo}, 1);
+    convLaunch(d, out, scr, c, c->nt, ell, Lq, 0);
+    // NTT every converted row: q rows [0, lo), q rows [hi, ell), then the K P rows
+    if (lo) sfp_ntt(d, out, sfp_limbs{lo, lo, 0, 0}, 0);
+    sfp_ntt(d, out + (size_t)hi * n, sfp_limbs{ell - hi + K, ell - hi, Lq, hi}, 0);
+    devCopy(d, out + (size_t)lo * n, in + (size_t)lo * n, (size_t)ns * n * 8);
+}
+
+void sfp_ks_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
+                  size_t extStride, const uint64_t* key, uint32_t beta, uint32_t ell, uint32_t K,
+                  uint32_t Lq) {
+    const size_t total = (size_t)(ell + K) * d->n;
+    hipLaunchKernelGGL(k_ks_inner, dim3(ewGrid(total)), dim3(kThreads), 0, d->stream, acc0, acc1, ext,
+                       extStride, key, beta, ell, K, Lq, d->bar, d->logn);
+    checkLaunch(d, "ks_inner");
+}
+
+void sfp_moddown(sfp_dev* d, uint64_t* out, uint64_t* acc, uint32_t ell, uint32_t K, uint32_t Lq,
+                 const sfp_conv* c, const uint64_t* pinv, int add, uint64_t* scr) {
+    const uint32_t n = d->n;
+    u64* pRows = acc + (size_t)ell * n;
+    sfp_ntt(d, pRows, sfp_limbs{K, 0, Lq, 0}, 1);
+    convLaunch(d, scr, pRows, c, ell, 0xffffffffu, Lq, 1);
+    sfp_ntt(d, scr, sfp_limbs{ell, ell, 0, 0}, 0);
+    ConstArgs k;
+    std::memcpy(k.k, pinv, ell * 8);
+    hipLaunchKernelGGL(k_sub_mulc, dim3(ewGrid((size_t)ell * n)), dim3(kThreads), 0, d->stream, out, acc,
+                       scr, ell, k, d->bar, d->logn, add);
+    checkLaunch(d, "moddown");
+}
+
+// ---- sampling ----
+void sfp_sample_uniform(sfp_dev* d, uint64_t* p, sfp_limbs m, uint64_t seed) {
+    const size_t total = (size_t)m.count * d->n;
+    hipLaunchKernelGGL(k_uniform, dim3(ewGrid(total)), dim3(kThreads), 0, d->stream, p, m, seed, d->bar,
+                       d->logn);
+    checkLaunch(d, "uniform");
+}
+
+void sfp_load_i64(sfp_dev* d, uint64_t* p, const int64_t* c, sfp_limbs m) {
+    // the bounce buffer is free once the stream has drained; the kernel
+    // reads the coefficients straight from it
+    SFP_CHECK(hipStreamSynchronize(d->stream));
+    std::memcpy(d->bounce, c, (size_t)d->n * 8);
+    hipLaunchKernelGGL(k_load_i64, dim3(ewGrid(d->n)), dim3(kThreads), 0, d->stream, p,
+                       (const int64_t*)d->bounce, m, d->bar, d->logn);
+    checkLaunch(d, "load_i64");
+}
+
+

@@ -29,9 +29,14 @@ typedef struct sfp_dev sfp_dev;
 
 typedef struct {
     uint32_t count;  // number of limbs
-    uint32_t split;  // limbs [0, split) -> primes [0, split)
+    uint32_t split;  // limbs [0, split) -> primes [base, base + split)
     uint32_t pbase;  // limbs [split, count) -> primes [pbase, ...)
+    uint32_t base;   // (0 unless addressing a run that starts mid-table)
 } sfp_limbs;
+
+static inline uint32_t sfp_prime_of(sfp_limbs m, uint32_t i) {
+    return i < m.split ? m.base + i : m.pbase + (i - m.split);
+}
 
 // Tables the host computes once per context (identical for both backends).
 typedef struct {
@@ -112,6 +117,12 @@ void sfp_automorph(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t galoi
 // in_stride / out_stride u64) are processed.
 void sfp_rescale(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t ell, const uint64_t* qlinv,
                  uint32_t npoly, size_t in_stride, size_t out_stride);
+// Same, but the dropped (last) row is modulo prime index drop_prime instead of
+// ell-1 (rows 0..ell-2 stay primes 0..ell-2): the extended-modulus
+// encryption's division by q_ext.
+void sfp_rescale_ext(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t ell,
+                     uint32_t drop_prime, const uint64_t* qlinv, uint32_t npoly, size_t in_stride,
+                     size_t out_stride);
 
 // ---- basis conversion / key switching ----------------------------------------
 // Upload a conversion table: ns source primes (prime indices src_idx), nt
@@ -139,7 +150,8 @@ void sfp_ks_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ex
                   size_t ext_stride, const uint64_t* key, uint32_t beta, uint32_t ell, uint32_t K,
                   uint32_t Lq);
 
-// ModDown:  out_i (+)= (acc_i - NTT(Conv_{P->Q}(INTT(acc_P)))_i) * pinv_i
+// ModDown:  out_i (+)= (acc_i - NTT(Conv_{P->Q}(INTT(acc_P)))_i) * pinv_i, with the
+//   P->Q conversion on centred residues (zero-mean rounding error).
 //   acc : ell+K limbs (split=ell, pbase=Lq), evaluation domain; destroyed.
 //   out : ell limbs.  If add != 0 the result is added into out.
 //   pinv: host array ell of P^{-1} mod q_i.  scratch: (ell+K)*n words.

@@ -52,6 +52,7 @@ class Params(C.Structure):
         ("num_large_digits", C.c_uint32),
         ("device", C.c_int32),
         ("seed", C.c_uint64),
+        ("scaling_technique", C.c_int32),
     ]
 
 
@@ -144,7 +145,8 @@ class Engine:
     def __init__(self, backend: str = "hip", *, mult_depth: int, ring_dim: int = 0,
                  batch_size: int = 0, scaling_mod_size: int = 40, first_mod_size: int = 60,
                  secure: bool = False, num_large_digits: int = 0, seed: int = 0x5EED5EED2025,
-                 device: int = 0, rotations: Sequence[int] = (), keygen: bool = True):
+                 device: int = 0, rotations: Sequence[int] = (), keygen: bool = True,
+                 scaling: str = "FLEXIBLEAUTOEXT"):
         self.lib = load(backend)
         self.backend = backend
         p = Params()
@@ -158,6 +160,7 @@ class Engine:
         p.num_large_digits = num_large_digits
         p.seed = seed
         p.device = device
+        p.scaling_technique = {"FLEXIBLEAUTO": 2, "FLEXIBLEAUTOEXT": 3}[scaling]
         self.ctx = C.c_void_p()
         self._chk(self.lib.sfhe_context_create(C.byref(p), C.byref(self.ctx)))
         if keygen:

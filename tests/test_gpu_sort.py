@@ -1,0 +1,88 @@
+"""GPU acceptance at the BASELINE.json configurations (DirectSortTest shape).
+
+Oracle: the float64 slot-level re-enactment (oracle/slotsim.py) and std::sort
+of the input.  Bars:
+  * the reference's own gate: max |out - sort(x)| < 0.01 and final level ==
+    multDepth (tests/DirectSortTest.cpp:140-141, :194) -- also applied to
+    |out - slotsim|;
+  * at the reference's 40-bit scale (sort_algo.h:92) the CKKS noise of the
+    first sign stages is amplified by the sign composition's gain (~N at
+    |d| = 1/N) and by the sinc slope at placement: N=256 lands near 2^-7.4.
+    The 50-bit-scale case shows that this is noise, not arithmetic error:
+    the same circuit then matches slotsim to 2^-14.
+"""
+import numpy as np
+import pytest
+
+import sfhe
+from oracle import slotsim
+
+pytestmark = pytest.mark.gpu
+
+
+def run_sort(N, logn, secure=False, debug=False, scale_bits=40):
+    depth, rots = sfhe.direct_sort_params(N, "hip")
+    e = sfhe.Engine("hip", mult_depth=depth, ring_dim=1 << logn, batch_size=N, secure=secure,
+                    rotations=rots, seed=20251205 + N, scaling_mod_size=scale_bits)
+    e.set_quiet(True)
+    x = slotsim.input_vector(N)
+    s = e.sorter(N, debug=debug)
+    out = s.sort(e.encrypt(x.tolist()), *slotsim.default_sign_config(N))
+    return e, x, out, depth
+
+
+@pytest.mark.parametrize("N,logn,secure,scale_bits,sim_tol", [
+    (8, 17, True, 40, 2 ** -12),     # config 1 (DirectSortTest N=8: ring 2^17, 128-bit)
+    (128, 16, False, 40, 0.01),      # config 3
+    (256, 16, False, 40, 0.01),      # metric config
+    (256, 16, False, 50, 2 ** -14),  # same circuit, 50-bit scale: noise-limited
+])
+def test_direct_sort(N, logn, secure, scale_bits, sim_tol):
+    e, x, out, depth = run_sort(N, logn, secure, scale_bits=scale_bits)
+    assert out.level == depth
+    got = np.array(e.decrypt(out))
+    exact = np.sort(x)
+    err = np.max(np.abs(got - exact))
+    sim, _ = slotsim.direct_sort(x, N, 1 << logn)
+    print(f"N={N} ring=2^{logn} max err {err:.3g} (log2 {np.log2(err):.2f}); vs slotsim "
+          f"{np.max(np.abs(got - sim)):.3g}")
+    assert err < 0.01
+    assert np.max(np.abs(got - sim)) < sim_tol
+
+
+def test_rank_matches_oracle():
+    N, logn = 64, 16
+    depth, rots = sfhe.direct_sort_params(N, "hip")
+    e = sfhe.Engine("hip", mult_depth=depth, ring_dim=1 << logn, batch_size=N, rotations=rots)
+    x = slotsim.input_vector(N)
+    s = e.sorter(N)
+    cfg = slotsim.default_sign_config(N)
+    rank = np.array(e.decrypt(s.rank(e.encrypt(x.tolist()), *cfg)))
+    sim = slotsim.construct_rank(x, N, 1 << logn, cfg)
+    assert np.max(np.abs(rank - np.argsort(np.argsort(x)))) < 1e-3
+    assert np.max(np.abs(rank - sim)) < 1e-4
+
+
+@pytest.mark.parametrize("cfg", [(4, 3, 3), (3, 4, 2)])
+def test_sign_config2(cfg):
+    """BASELINE config 2: sign() on one ciphertext at ring 2^15, depth 30, scale 50."""
+    e = sfhe.Engine("hip", mult_depth=30, ring_dim=1 << 15, batch_size=1 << 14, scaling_mod_size=50)
+    rng = np.random.default_rng(99)
+    mag = rng.uniform(2 ** -7, 1.0, 1 << 14)
+    x = mag * rng.choice([-1.0, 1.0], size=mag.size)
+    out = e.sign(e.encrypt(x.tolist()), *cfg)
+    got = np.array(e.decrypt(out))
+    ref = slotsim.composite_sign(x, *cfg)
+    assert out.level == slotsim.sign_depth(*cfg)
+    assert np.max(np.abs(got - ref)) < 1e-3
+    assert np.all(np.sign(got) == np.sign(x))
+
+
+def test_compare_reference_vectors():
+    """tests/CompareTest.cpp:13-63: depth 50, scale 59, ring 2^12;
+    compare({1,5,3,4},{2,4,3,3}) with CompositeSign(4,3,3) = {0,1,0.5,1} +- 0.1."""
+    e = sfhe.Engine("hip", mult_depth=50, ring_dim=1 << 12, batch_size=4, scaling_mod_size=59)
+    a = e.encrypt([1.0, 5.0, 3.0, 4.0])
+    b = e.encrypt([2.0, 4.0, 3.0, 3.0])
+    got = np.array(e.decrypt(e.compare(a, b, 4, 3, 3)))
+    assert np.max(np.abs(got - np.array([0, 1, 0.5, 1]))) < 0.1
