@@ -90,6 +90,17 @@ int sfhe_sync(sfhe_ctx* c);
 /* counts[9]: keyswitch, rescale, tensor, ptmult, constmult, add, automorph,
  * ntt_limbs, wsum_terms; bytes: algorithmic HBM bytes (SURVEY §8(d) model). */
 int sfhe_op_stats(sfhe_ctx* c, uint64_t* counts, double* bytes, int reset);
+/* Live kernel timing (bench roofline; no reference counterpart): kernel
+ * families SFHE_KFAM_*; every `period`-th launch of the family is bracketed
+ * by HIP events on the context's stream (period 0 = off; resets counters).
+ * _read synchronises and returns launches seen, launches timed, their summed
+ * duration (ms) and summed algorithmic bytes (prims.h defines the model). */
+#define SFHE_KFAM_NTT 0
+#define SFHE_KFAM_CONV 1
+#define SFHE_KFAM_KSINNER 2
+int sfhe_kernel_timing(sfhe_ctx* c, uint32_t family, uint32_t period);
+int sfhe_kernel_timing_read(sfhe_ctx* c, uint32_t family, uint64_t* launches, uint64_t* timed,
+                            double* ms, double* bytes);
 
 /* ---- encryption ------------------------------------------------------------
  * Replaces Encryption::encryptInput (encryption.cpp:5-12, MakeCKKSPacked-
@@ -132,7 +143,7 @@ int sfhe_sign(sfhe_ctx* c, const sfhe_ct* x, int n, int dg, int df, sfhe_ct** ou
 int sfhe_compare(sfhe_ctx* c, const sfhe_ct* a, const sfhe_ct* b, int n, int dg, int df,
                  sfhe_ct** out);
 /* DirectSort<N>::getSizeParameters (sort_algo.h:87-201): depth and rotation
- * keys for N in {4, 8, ..., 1024}. */
+ * keys: the reference table for N in {4, 8, ..., 2048} (sorters: N <= 1024). */
 int sfhe_direct_sort_params(uint32_t N, uint32_t* mult_depth, int32_t* rotations, size_t cap,
                             size_t* count);
 /* Doubled-sinc Chebyshev table (generated_doubled_sinc_coeffs.h). */

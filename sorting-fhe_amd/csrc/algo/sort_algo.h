@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cmath>
 #include <iostream>
 #include <string>
@@ -29,6 +30,7 @@
 #include "coefficients.h"
 #include "comparison.h"
 #include "encryption.h"
+#include "size_params.h"
 #include "lattice/hal/lat-backend.h"
 #include "mehp24/mehp24_utils.h"
 #include "openfhe.h"
@@ -88,23 +90,12 @@ inline int directSortDepth(int N, const CompositeSignConfig& c) {
     return 1 + sign + 1 + 1 + ps + 1 + 1;
 }
 
-// Every rotation amount DirectSort<N>::sort issues, for rings 2^15 .. 2^18.
-inline std::vector<int> directSortRotations(int N) {
-    std::set<int> r;
-    for (int logn = 15; logn <= 18; ++logn) {
-        const int maxBatch = 1 << (logn - 1);
-        if (maxBatch < N) continue;
-        RankLayout L(N, maxBatch);
-        for (int i = 1; i < L.npRank; ++i) r.insert(i);
-        for (int i = 1; i < L.npPlace; ++i) r.insert(i);
-        for (int b = 0; b < L.B; ++b) {
-            for (int j = 0; j < L.P / L.npRank; ++j) r.insert(b * L.P + j * L.npRank);
-            for (int i = 0; i < L.P / L.npPlace; ++i) r.insert(b * L.P + i * L.npPlace);
-        }
-        for (int s = L.S / 2; s >= N; s /= 2) r.insert(s);
-    }
-    r.erase(0);
-    return std::vector<int>(r.begin(), r.end());
+// getSizeParameters' (depth, rotation keys) for N (reference :87-201);
+// nullptr when the reference has no entry.
+inline const SizeParams* sizeParams(int N) {
+    for (const auto& e : sizeParamTable())
+        if (e.N == N) return &e;
+    return nullptr;
 }
 
 }  // namespace sfhe
@@ -151,16 +142,20 @@ class DirectSort : public SortBase<N> {
 
     const std::set<int>& getRotationCalls() const { return rot.getRotationCalls(); }
 
-    // Batch size, depth and rotation keys for this N (reference :87-201).
-    // The depth is derived, not tabulated: it reproduces the reference's
-    // table 23,24,25,28,29,30,34,35,39 for N = 4..1024.
+    // Batch size, scale, depth and rotation keys for this N (reference
+    // :87-201; the tables are the reference's, sfhe::directSortDepth
+    // re-derives the depths and tests/test_host.py checks they agree).
     static void getSizeParameters(CCParams<CryptoContextCKKSRNS>& parameters,
                                   std::vector<int>& rotations) {
         parameters.SetBatchSize(N);
+        const sfhe::SizeParams* p = sfhe::sizeParams(N);
+        if (!p) {
+            std::cerr << "Unsupported N" << std::endl;
+            std::exit(1);
+        }
         parameters.SetScalingModSize(40);
-        parameters.SetMultiplicativeDepth(
-            (uint32_t)sfhe::directSortDepth(N, sfhe::defaultSignConfig(N)));
-        rotations = sfhe::directSortRotations(N);
+        parameters.SetMultiplicativeDepth((uint32_t)p->multDepth);
+        rotations = p->rotations;
     }
 
     // ---- slot-vector generators (reference :206-306) ----

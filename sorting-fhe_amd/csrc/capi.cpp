@@ -339,10 +339,11 @@ int sfhe_compare(sfhe_ctx* c, const sfhe_ct* a, const sfhe_ct* b, int n, int dg,
 }
 
 int sfhe_direct_sort_params(uint32_t N, uint32_t* depth, int32_t* rot, size_t cap, size_t* count) {
-    REQUIRE(validN(N), "N must be a power of two in [4, 1024]");
+    const sfhe::SizeParams* p = sfhe::sizeParams((int)N);
+    REQUIRE(p, "N has no DirectSort size parameters (reference table: 4 .. 2048)");
     return guard([&] {
-        auto r = sfhe::directSortRotations((int)N);
-        if (depth) *depth = (uint32_t)sfhe::directSortDepth((int)N, sfhe::defaultSignConfig((int)N));
+        const auto& r = p->rotations;
+        if (depth) *depth = (uint32_t)p->multDepth;
         if (count) *count = r.size();
         for (size_t i = 0; i < r.size() && i < cap && rot; ++i) rot[i] = r[i];
     });
@@ -365,7 +366,7 @@ int sfhe_sorter_create(sfhe_ctx* c, uint32_t N, int debug, sfhe_sorter** out) {
         std::shared_ptr<Encryption> enc =
             debug ? std::shared_ptr<Encryption>(std::make_shared<DebugEncryption>(c->cc, c->keys))
                   : std::make_shared<Encryption>(c->cc, c->keys.publicKey);
-        auto rot = sfhe::directSortRotations((int)N);
+        const auto rot = sfhe::sizeParams((int)N)->rotations;
         auto s = std::make_unique<sfhe_sorter>();
         s->ctx = c;
         switch (N) {
@@ -431,6 +432,25 @@ int sfhe_debug_decrypt_coeffs(sfhe_ctx* c, const sfhe_ct* ct, double* out, size_
         sfp_d2h(s->dev, h.data(), t->ptr, n * 8);
         const uint64_t q0 = s->primes[0];
         for (size_t i = 0; i < n; ++i) out[i] = h[i] > q0 / 2 ? -(double)(q0 - h[i]) : (double)h[i];
+    });
+}
+
+int sfhe_kernel_timing(sfhe_ctx* c, uint32_t family, uint32_t period) {
+    REQUIRE(c, "null context");
+    REQUIRE(family < SFP_FAM_COUNT, "unknown kernel family");
+    return guard([&] {
+        std::lock_guard<std::recursive_mutex> g(c->cc->state()->opMu);
+        sfp_prof_set(c->cc->state()->dev, family, period);
+    });
+}
+
+int sfhe_kernel_timing_read(sfhe_ctx* c, uint32_t family, uint64_t* launches, uint64_t* timed,
+                            double* ms, double* bytes) {
+    REQUIRE(c, "null context");
+    REQUIRE(family < SFP_FAM_COUNT, "unknown kernel family");
+    return guard([&] {
+        std::lock_guard<std::recursive_mutex> g(c->cc->state()->opMu);
+        sfp_prof_read(c->cc->state()->dev, family, launches, timed, ms, bytes);
     });
 }
 

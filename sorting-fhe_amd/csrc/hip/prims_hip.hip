@@ -89,6 +89,14 @@ struct sfp_dev {
     // (read / written by kernels directly)
     char* bounce = nullptr;
     size_t bounceCap = 0;
+    // live kernel timing (sfp_prof_*)
+    struct ProfFam {
+        uint32_t period = 0;
+        uint64_t seen = 0, timed = 0;
+        double ms = 0, bytes = 0;
+        std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+    } prof[SFP_FAM_COUNT];
+    std::vector<hipEvent_t> evPool;
     std::mutex mu;
     std::string err;
 };
@@ -125,6 +133,49 @@ static void checkLaunch(sfp_dev* d, const char* k) {
     }
 }
 
+// ---- live kernel timing ----
+static hipEvent_t takeEvent(sfp_dev* d) {
+    if (!d->evPool.empty()) {
+        hipEvent_t e = d->evPool.back();
+        d->evPool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    SFP_CHECK(hipEventCreate(&e));
+    return e;
+}
+
+static void profFlush(sfp_dev* d, sfp_dev::ProfFam& f) {
+    if (f.pending.empty()) return;
+    SFP_CHECK(hipEventSynchronize(f.pending.back().second));
+    for (auto& pr : f.pending) {
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess) f.ms += ms;
+        d->evPool.push_back(pr.first);
+        d->evPool.push_back(pr.second);
+    }
+    f.pending.clear();
+}
+
+// Run `launch` (one kernel launch on d->stream); bracket it with events when
+// this family is being timed and this launch is a sampled one.
+template <class F>
+static void timedLaunch(sfp_dev* d, uint32_t fam, double bytes, F&& launch) {
+    sfp_dev::ProfFam& f = d->prof[fam];
+    if (!f.period || (f.seen++ % f.period) != 0) {
+        launch();
+        return;
+    }
+    hipEvent_t a = takeEvent(d), b = takeEvent(d);
+    SFP_CHECK(hipEventRecord(a, d->stream));
+    launch();
+    SFP_CHECK(hipEventRecord(b, d->stream));
+    f.pending.push_back({a, b});
+    f.timed++;
+    f.bytes += bytes;
+    if (f.pending.size() >= 8192) profFlush(d, f);
+}
+
 static unsigned gridFor(size_t work, unsigned perBlock) {
     size_t g = (work + perBlock - 1) / perBlock;
     return (unsigned)(g ? g : 1);
@@ -133,121 +184,173 @@ static unsigned gridFor(size_t work, unsigned perBlock) {
 // ============================================================================
 // NTT kernels
 
-// Column pass: first log2(R) stages; tile = R rows x CW columns of one limb.
-template <bool INV>
-__global__ __launch_bounds__(kThreads) void k_ntt_col(u64* __restrict__ data, sfp_limbs m,
-                                                      const sf_barrett* __restrict__ bar,
-                                                      const u64* __restrict__ tw,
-                                                      const u64* __restrict__ twS,
-                                                      const u64* __restrict__ ninv,
-                                                      const u64* __restrict__ ninvS, uint32_t logn) {
-    __shared__ u64 s[kTile];
+// One pass of the negacyclic NTT over 4096-word tiles.
+//
+// n = R * 256 is viewed as R rows of 256 words.  The forward transform is the
+// bit-reversed-twiddle Cooley-Tukey schedule: global stage S (0..logn-1) pairs
+// x with x + n/2^(S+1) and uses psi_rev[2^S + (x >> (logn - S))].
+//   COL pass: stages 0..logR-1; a tile is C = 4096/R whole columns (R x C).
+//   ROW pass: stages logR..logn-1; a tile is 16 whole rows (16 x 256).
+// The tile is staged in padded LDS (word e at e + e/16: conflict-free for the
+// unit-stride and stride-16 patterns below) and its stages are run in rounds
+// of up to four: every thread pulls 16 words into registers, runs the round's
+// radix-2 stages there, and writes them back -- one LDS round trip per four
+// stages.  The inverse runs the Gentleman-Sande stages in reverse order (ROW
+// pass first) and folds n^-1 into the COL pass's store.
+__device__ __forceinline__ uint32_t ldsPad(uint32_t e) { return e + (e >> 4); }
+
+struct NttTile {
+    uint32_t logn, d;     // d = stages in this pass (logR or 8)
+    uint32_t C;           // COL: columns per tile
+    uint32_t c0, r0;      // COL: first column; ROW: first row
+};
+
+// global index of tile-local sub-transform `st`, position u
+template <bool COL>
+__device__ __forceinline__ uint32_t nttGlobal(const NttTile& T, uint32_t st, uint32_t u) {
+    return COL ? u * 256u + T.c0 + st : (T.r0 + st) * 256u + u;
+}
+template <bool COL>
+__device__ __forceinline__ uint32_t nttLocal(const NttTile& T, uint32_t st, uint32_t u) {
+    return COL ? u * T.C + st : st * 256u + u;
+}
+
+// One round: stages k0..k0+B-1 of the pass (k relative to the pass's first
+// global stage S0).  16/2^B groups of 2^B words per thread.
+template <bool INV, bool COL, int B>
+__device__ __forceinline__ void nttRound(u64* s, const NttTile& T, uint32_t S0, uint32_t k0, u64 q,
+                                         const u64* __restrict__ w, const u64* __restrict__ wS) {
+    constexpr int M = 1 << B;
+    constexpr int GPT = 16 / M;  // groups per thread
+    const uint32_t D = 1u << T.d;
+    const uint32_t h = D >> (k0 + B);     // smallest stride of the round (in u)
+    const uint32_t span = D >> k0;        // hi step
+    const uint32_t nsub = COL ? T.C : 16u;
+#pragma unroll
+    for (int gi = 0; gi < GPT; ++gi) {
+        const uint32_t gid = threadIdx.x + gi * kThreads;
+        uint32_t st, lo, hi;
+        if (COL) {
+            st = gid % nsub;
+            const uint32_t rest = gid / nsub;
+            lo = rest % h;
+            hi = rest / h;
+        } else {
+            lo = gid % h;
+            const uint32_t rest = gid / h;
+            hi = rest & ((1u << k0) - 1);
+            st = rest >> k0;
+        }
+        const uint32_t ub = hi * span + lo;
+        u64 v[M];
+#pragma unroll
+        for (int j = 0; j < M; ++j) v[j] = s[ldsPad(nttLocal<COL>(T, st, ub + j * h))];
+        if (!INV) {
+#pragma unroll
+            for (int t = 0; t < B; ++t) {
+                const uint32_t S = S0 + k0 + t;
+                const int half = 1 << (B - 1 - t);
+#pragma unroll
+                for (int j = 0; j < M; ++j) {
+                    if (j & half) continue;
+                    const uint32_t x = nttGlobal<COL>(T, st, ub + j * h);
+                    const uint32_t ti = (1u << S) + (x >> (T.logn - S));
+                    const u64 W = w[ti], WS = wS[ti];
+                    const u64 U = v[j];
+                    const u64 V = sf_mul_shoup(v[j + half], W, WS, q);
+                    v[j] = sf_add(U, V, q);
+                    v[j + half] = sf_sub(U, V, q);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int t = B - 1; t >= 0; --t) {
+                const uint32_t S = S0 + k0 + t;
+                const int half = 1 << (B - 1 - t);
+#pragma unroll
+                for (int j = 0; j < M; ++j) {
+                    if (j & half) continue;
+                    const uint32_t x = nttGlobal<COL>(T, st, ub + j * h);
+                    const uint32_t ti = (1u << S) + (x >> (T.logn - S));
+                    const u64 W = w[ti], WS = wS[ti];
+                    const u64 U = v[j], V = v[j + half];
+                    v[j] = sf_add(U, V, q);
+                    v[j + half] = sf_mul_shoup(sf_sub(U, V, q), W, WS, q);
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < M; ++j) s[ldsPad(nttLocal<COL>(T, st, ub + j * h))] = v[j];
+    }
+}
+
+template <bool INV, bool COL>
+__device__ __forceinline__ void nttRoundDyn(int b, u64* s, const NttTile& T, uint32_t S0, uint32_t k0,
+                                            u64 q, const u64* w, const u64* wS) {
+    switch (b) {
+        case 4: nttRound<INV, COL, 4>(s, T, S0, k0, q, w, wS); break;
+        case 3: nttRound<INV, COL, 3>(s, T, S0, k0, q, w, wS); break;
+        case 2: nttRound<INV, COL, 2>(s, T, S0, k0, q, w, wS); break;
+        default: nttRound<INV, COL, 1>(s, T, S0, k0, q, w, wS); break;
+    }
+}
+
+template <bool INV, bool COL>
+__global__ __launch_bounds__(kThreads) void k_ntt(u64* __restrict__ data, sfp_limbs m,
+                                                  const sf_barrett* __restrict__ bar,
+                                                  const u64* __restrict__ tw, const u64* __restrict__ twS,
+                                                  const u64* __restrict__ ninv,
+                                                  const u64* __restrict__ ninvS, uint32_t logn) {
+    __shared__ u64 s[kTile + kTile / 16];
     const uint32_t n = 1u << logn;
-    const uint32_t R = n >> 8;                 // rows of the 256-wide matrix
-    const uint32_t tile = n < kTile ? n : kTile;
-    const uint32_t CW = tile / R;              // columns per tile
+    const uint32_t logR = logn - 8;
     const uint32_t limb = blockIdx.y;
     const uint32_t p = primeOf(m, limb);
     const u64 q = bar[p].q;
     u64* a = data + (size_t)limb * n;
     const u64* w = tw + (size_t)p * n;
     const u64* wS = twS + (size_t)p * n;
-    const uint32_t c0 = blockIdx.x * CW;
-    for (uint32_t e = threadIdx.x; e < tile; e += kThreads) {
-        uint32_t r = e / CW, c = e % CW;
-        s[e] = a[(size_t)r * 256 + c0 + c];
+    NttTile T;
+    T.logn = logn;
+    T.d = COL ? logR : 8u;
+    T.C = COL ? (kTile >> logR) : 0u;
+    T.c0 = COL ? blockIdx.x * T.C : 0u;
+    T.r0 = COL ? 0u : blockIdx.x * 16u;
+    const uint32_t S0 = COL ? 0u : logR;
+
+    // global -> LDS, 16 B per lane; tile-linear word e is row-major (u, st)
+#pragma unroll
+    for (int k = 0; k < kTile / 2 / kThreads; ++k) {
+        const uint32_t e = 2 * (threadIdx.x + k * kThreads);
+        const size_t g = COL ? (size_t)(e / T.C) * 256 + T.c0 + (e % T.C) : (size_t)T.r0 * 256 + e;
+        const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(a + g);
+        s[ldsPad(e)] = x.x;
+        s[ldsPad(e + 1)] = x.y;
     }
     __syncthreads();
-    const uint32_t nb = tile / 2;  // butterflies per stage
-    if (!INV) {
-        for (uint32_t tp = R >> 1, mm = 1; tp >= 1; tp >>= 1, mm <<= 1) {
-            for (uint32_t b = threadIdx.x; b < nb; b += kThreads) {
-                uint32_t c = b % CW, pr = b / CW;
-                uint32_t r = (pr / tp) * 2 * tp + (pr % tp);
-                u64 W = w[mm + r / (2 * tp)], WS = wS[mm + r / (2 * tp)];
-                u64 U = s[r * CW + c];
-                u64 V = sf_mul_shoup(s[(r + tp) * CW + c], W, WS, q);
-                s[r * CW + c] = sf_add(U, V, q);
-                s[(r + tp) * CW + c] = sf_sub(U, V, q);
-            }
-            __syncthreads();
-        }
-    } else {
-        for (uint32_t tp = 1; tp < R; tp <<= 1) {
-            const uint32_t h = R / (2 * tp);  // = n/(2t) with t = 256 tp
-            for (uint32_t b = threadIdx.x; b < nb; b += kThreads) {
-                uint32_t c = b % CW, pr = b / CW;
-                uint32_t r = (pr / tp) * 2 * tp + (pr % tp);
-                u64 W = w[h + r / (2 * tp)], WS = wS[h + r / (2 * tp)];
-                u64 U = s[r * CW + c], V = s[(r + tp) * CW + c];
-                s[r * CW + c] = sf_add(U, V, q);
-                s[(r + tp) * CW + c] = sf_mul_shoup(sf_sub(U, V, q), W, WS, q);
-            }
-            __syncthreads();
-        }
-        const u64 ni = ninv[p], niS = ninvS[p];
-        for (uint32_t e = threadIdx.x; e < tile; e += kThreads) s[e] = sf_mul_shoup(s[e], ni, niS, q);
+    // rounds of <= 4 stages: forward 4,4,..,rem ; inverse mirrored
+    const uint32_t nr = (T.d + 3) / 4;
+    for (uint32_t ri = 0; ri < nr; ++ri) {
+        const uint32_t r = INV ? nr - 1 - ri : ri;
+        const uint32_t k0 = 4 * r;
+        const int b = (int)min(4u, T.d - k0);
+        nttRoundDyn<INV, COL>(b, s, T, S0, k0, q, w, wS);
         __syncthreads();
     }
-    for (uint32_t e = threadIdx.x; e < tile; e += kThreads) {
-        uint32_t r = e / CW, c = e % CW;
-        a[(size_t)r * 256 + c0 + c] = s[e];
-    }
-}
-
-// Row pass: last 8 stages on 16 rows of 256 contiguous words.
-template <bool INV>
-__global__ __launch_bounds__(kThreads) void k_ntt_row(u64* __restrict__ data, sfp_limbs m,
-                                                      const sf_barrett* __restrict__ bar,
-                                                      const u64* __restrict__ tw,
-                                                      const u64* __restrict__ twS, uint32_t logn) {
-    __shared__ u64 s[kTile];
-    const uint32_t n = 1u << logn;
-    const uint32_t limb = blockIdx.y;
-    const uint32_t p = primeOf(m, limb);
-    const u64 q = bar[p].q;
-    const size_t base = (size_t)blockIdx.x * kTile;  // first word of the 16-row tile
-    u64* a = data + (size_t)limb * n + base;
-    const u64* w = tw + (size_t)p * n;
-    const u64* wS = twS + (size_t)p * n;
-    {
-        const ulonglong2* src = reinterpret_cast<const ulonglong2*>(a);
-        ulonglong2* dst = reinterpret_cast<ulonglong2*>(s);
-        for (uint32_t e = threadIdx.x; e < kTile / 2; e += kThreads) dst[e] = src[e];
-    }
-    __syncthreads();
-    if (!INV) {
-        for (uint32_t t = 128; t >= 1; t >>= 1) {
-            const uint32_t mm = n / (2 * t);
-            for (uint32_t b = threadIdx.x; b < kTile / 2; b += kThreads) {
-                uint32_t j = (b / t) * 2 * t + (b % t);  // local index of the upper element
-                uint32_t idx = mm + (uint32_t)((base + j) / (2 * t));
-                u64 W = w[idx], WS = wS[idx];
-                u64 U = s[j];
-                u64 V = sf_mul_shoup(s[j + t], W, WS, q);
-                s[j] = sf_add(U, V, q);
-                s[j + t] = sf_sub(U, V, q);
-            }
-            __syncthreads();
+    const bool scale = INV && COL;
+    const u64 ni = scale ? ninv[p] : 0, niS = scale ? ninvS[p] : 0;
+#pragma unroll
+    for (int k = 0; k < kTile / 2 / kThreads; ++k) {
+        const uint32_t e = 2 * (threadIdx.x + k * kThreads);
+        const size_t g = COL ? (size_t)(e / T.C) * 256 + T.c0 + (e % T.C) : (size_t)T.r0 * 256 + e;
+        ulonglong2 x;
+        x.x = s[ldsPad(e)];
+        x.y = s[ldsPad(e + 1)];
+        if (scale) {
+            x.x = sf_mul_shoup(x.x, ni, niS, q);
+            x.y = sf_mul_shoup(x.y, ni, niS, q);
         }
-    } else {
-        for (uint32_t t = 1; t <= 128; t <<= 1) {
-            const uint32_t h = n / (2 * t);
-            for (uint32_t b = threadIdx.x; b < kTile / 2; b += kThreads) {
-                uint32_t j = (b / t) * 2 * t + (b % t);
-                uint32_t idx = h + (uint32_t)((base + j) / (2 * t));
-                u64 W = w[idx], WS = wS[idx];
-                u64 U = s[j], V = s[j + t];
-                s[j] = sf_add(U, V, q);
-                s[j + t] = sf_mul_shoup(sf_sub(U, V, q), W, WS, q);
-            }
-            __syncthreads();
-        }
-    }
-    {
-        const ulonglong2* src = reinterpret_cast<const ulonglong2*>(s);
-        ulonglong2* dst = reinterpret_cast<ulonglong2*>(a);
-        for (uint32_t e = threadIdx.x; e < kTile / 2; e += kThreads) dst[e] = src[e];
+        *reinterpret_cast<ulonglong2*>(a + g) = x;
     }
 }
 
@@ -687,6 +790,8 @@ sfp_dev* sfp_create(int device, const sfp_tables* t) {
 void sfp_destroy(sfp_dev* d) {
     if (!d) return;
     hipStreamSynchronize(d->stream);
+    for (auto& f : d->prof) profFlush(d, f);
+    for (hipEvent_t e : d->evPool) hipEventDestroy(e);
     hipFree(d->bar);
     hipFree(d->psi);
     hipFree(d->psiS);
@@ -728,21 +833,45 @@ const char* sfp_last_error(sfp_dev* d) {
 // ---- NTT ----
 void sfp_ntt(sfp_dev* d, uint64_t* p, sfp_limbs m, int inverse) {
     if (!m.count) return;
-    const uint32_t n = d->n;
-    const uint32_t tile = n < (uint32_t)kTile ? n : (uint32_t)kTile;
-    dim3 gcol(n / tile, m.count), grow(n / kTile, m.count);
+    const uint32_t tiles = d->n / kTile;  // tiles per limb, both passes
+    const dim3 g(tiles, m.count);
+    const double bytes = 16.0 * m.count * d->n;
+    const u64* tw = inverse ? d->ipsi : d->psi;
+    const u64* twS = inverse ? d->ipsiS : d->psiS;
+    auto pass = [&](auto kern) {
+        timedLaunch(d, SFP_FAM_NTT, bytes, [&] {
+            hipLaunchKernelGGL(kern, g, dim3(kThreads), 0, d->stream, p, m, d->bar, tw, twS, d->ninv,
+                               d->ninvS, d->logn);
+        });
+    };
     if (!inverse) {
-        hipLaunchKernelGGL(k_ntt_col<false>, gcol, dim3(kThreads), 0, d->stream, p, m, d->bar, d->psi,
-                           d->psiS, d->ninv, d->ninvS, d->logn);
-        hipLaunchKernelGGL(k_ntt_row<false>, grow, dim3(kThreads), 0, d->stream, p, m, d->bar, d->psi,
-                           d->psiS, d->logn);
+        pass(k_ntt<false, true>);
+        pass(k_ntt<false, false>);
     } else {
-        hipLaunchKernelGGL(k_ntt_row<true>, grow, dim3(kThreads), 0, d->stream, p, m, d->bar, d->ipsi,
-                           d->ipsiS, d->logn);
-        hipLaunchKernelGGL(k_ntt_col<true>, gcol, dim3(kThreads), 0, d->stream, p, m, d->bar, d->ipsi,
-                           d->ipsiS, d->ninv, d->ninvS, d->logn);
+        pass(k_ntt<true, false>);
+        pass(k_ntt<true, true>);
     }
     checkLaunch(d, "ntt");
+}
+
+void sfp_prof_set(sfp_dev* d, uint32_t fam, uint32_t period) {
+    if (fam >= SFP_FAM_COUNT) return;
+    auto& f = d->prof[fam];
+    profFlush(d, f);
+    f = sfp_dev::ProfFam{};
+    f.period = period;
+}
+
+int sfp_prof_read(sfp_dev* d, uint32_t fam, uint64_t* launches, uint64_t* timed, double* ms,
+                  double* bytes) {
+    if (fam >= SFP_FAM_COUNT) return -1;
+    auto& f = d->prof[fam];
+    profFlush(d, f);
+    if (launches) *launches = f.seen;
+    if (timed) *timed = f.timed;
+    if (ms) *ms = f.ms;
+    if (bytes) *bytes = f.bytes;
+    return 0;
 }
 
 // ---- elementwise ----
@@ -930,9 +1059,11 @@ void sfp_free_conv(sfp_dev* d, sfp_conv* c) {
 static void convLaunch(sfp_dev* d, u64* out, const u64* src, const sfp_conv* c, uint32_t ntUse,
                        uint32_t ell, uint32_t Lq, int centered) {
     const size_t lds = (size_t)c->ns * c->nt * 8;
-    hipLaunchKernelGGL(k_conv, dim3(ewGrid(d->n)), dim3(kThreads), lds, d->stream, out, src, c->src,
-                       c->dst, c->inv, c->mod, c->sprod, c->ns, c->nt, ntUse, d->bar, d->logn, ell, Lq,
-                       centered);
+    timedLaunch(d, SFP_FAM_CONV, 8.0 * d->n * (c->ns + ntUse), [&] {
+        hipLaunchKernelGGL(k_conv, dim3(ewGrid(d->n)), dim3(kThreads), lds, d->stream, out, src, c->src,
+                           c->dst, c->inv, c->mod, c->sprod, c->ns, c->nt, ntUse, d->bar, d->logn, ell,
+                           Lq, centered);
+    });
     checkLaunch(d, "conv");
 }
 
@@ -956,8 +1087,11 @@ void sfp_ks_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ex
                   size_t extStride, const uint64_t* key, uint32_t beta, uint32_t ell, uint32_t K,
                   uint32_t Lq) {
     const size_t total = (size_t)(ell + K) * d->n;
-    hipLaunchKernelGGL(k_ks_inner, dim3(ewGrid(total)), dim3(kThreads), 0, d->stream, acc0, acc1, ext,
-                       extStride, key, beta, ell, K, Lq, d->bar, d->logn);
+    // reads beta ext rows + 2*beta key rows, writes 2 accumulator rows, per limb
+    timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + 2.0), [&] {
+        hipLaunchKernelGGL(k_ks_inner, dim3(ewGrid(total)), dim3(kThreads), 0, d->stream, acc0, acc1, ext,
+                           extStride, key, beta, ell, K, Lq, d->bar, d->logn);
+    });
     checkLaunch(d, "ks_inner");
 }
 

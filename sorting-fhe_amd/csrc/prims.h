@@ -165,6 +165,20 @@ void sfp_sample_uniform(sfp_dev* d, uint64_t* p, sfp_limbs m, uint64_t seed);
 // Load signed coefficients (same for every limb) reduced mod each prime.
 void sfp_load_i64(sfp_dev* d, uint64_t* p, const int64_t* coeffs, sfp_limbs m);
 
+// ---- live kernel timing ---------------------------------------------------------
+// Kernel families timed with events recorded on the backend's stream around
+// single launches.  Algorithmic bytes per launch (minimum HBM traffic):
+//   NTT pass     16 B per coefficient (read + write once; twiddles excluded)
+//   CONV         8 B per source coefficient read + 8 B per target written
+//   KSINNER      8 B per ext / key / accumulator word touched
+enum { SFP_FAM_NTT = 0, SFP_FAM_CONV = 1, SFP_FAM_KSINNER = 2, SFP_FAM_COUNT = 3 };
+// Time every `period`-th launch of `fam` (0 = off); resets its counters.
+void sfp_prof_set(sfp_dev* d, uint32_t fam, uint32_t period);
+// Since the last sfp_prof_set: launches seen, launches timed, their summed
+// duration (ms) and summed algorithmic bytes.  Synchronises the stream.
+int sfp_prof_read(sfp_dev* d, uint32_t fam, uint64_t* launches, uint64_t* timed, double* ms,
+                  double* bytes);
+
 #ifdef __cplusplus
 }
 #endif

@@ -33,7 +33,7 @@ ABI_SYMBOLS = [
     "sfhe_eval_mult", "sfhe_eval_rotate", "sfhe_eval_chebyshev", "sfhe_sign", "sfhe_compare",
     "sfhe_direct_sort_params", "sfhe_doubled_sinc_coeffs", "sfhe_sorter_create",
     "sfhe_sorter_destroy", "sfhe_sorter_sort", "sfhe_sorter_rank", "sfhe_sorter_place",
-    "sfhe_decompose",
+    "sfhe_decompose", "sfhe_kernel_timing", "sfhe_kernel_timing_read",
 ]
 
 
@@ -105,6 +105,8 @@ _SIGS = {
     "sfhe_sorter_sort": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_int, _PVP]),
     "sfhe_sorter_rank": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_int, _PVP]),
     "sfhe_sorter_place": (C.c_int, [_VP, _VP, _VP, _PVP]),
+    "sfhe_kernel_timing": (C.c_int, [_VP, _U32, _U32]),
+    "sfhe_kernel_timing_read": (C.c_int, [_VP, _U32, _PU64, _PU64, _PD, _PD]),
     "sfhe_decompose": (C.c_int, [_U32, _PI32, _SZ, C.c_int32, C.c_int32, C.c_int, _PI32, _PI32, _SZ, _PSZ]),
 }
 
@@ -225,6 +227,18 @@ class Engine:
         d = dict(zip(keys, list(c)))
         d["algo_bytes"] = b.value
         return d
+
+    KFAM = {"ntt": 0, "conv": 1, "ks_inner": 2}
+
+    def kernel_timing(self, family: str, period: int = 1):
+        self._chk(self.lib.sfhe_kernel_timing(self.ctx, self.KFAM[family], period))
+
+    def kernel_timing_read(self, family: str) -> dict:
+        la, ti = C.c_uint64(), C.c_uint64()
+        ms, by = C.c_double(), C.c_double()
+        self._chk(self.lib.sfhe_kernel_timing_read(self.ctx, self.KFAM[family], C.byref(la),
+                                                   C.byref(ti), C.byref(ms), C.byref(by)))
+        return {"launches": la.value, "timed": ti.value, "ms": ms.value, "bytes": by.value}
 
     # -- data --
     def encrypt(self, values: Sequence[float], slots: int = 0, level: int = 0) -> "Ct":

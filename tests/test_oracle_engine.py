@@ -1,0 +1,133 @@
+"""The CKKS engine's host layer on the CPU oracle backend (no GPU).
+
+These exercise the same host code the product runs (context, keys, encoder,
+key switching, Chebyshev PS, sign, DirectSort) with the C oracle prims, at
+ring sizes the oracle finishes in seconds.  Bars are the reference tests'
+own: CompareTest +-0.1, SignTest +-0.1 + sign agreement, RotationTest 1e-6,
+DirectSortTest < 0.01 and level == multDepth.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import sfhe
+from oracle import cheb, slotsim
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+REF = json.load(open(os.path.join(GOLD, "reference_params.json")))
+
+
+def test_encrypt_decrypt_and_ext_precision(oracle_lib):
+    x = np.linspace(-1, 1, 64)
+    errs = {}
+    for sc in ("FLEXIBLEAUTO", "FLEXIBLEAUTOEXT"):
+        e = sfhe.Engine("oracle", mult_depth=3, ring_dim=1 << 13, batch_size=64, scaling=sc)
+        ct = e.encrypt(x.tolist())
+        assert ct.level == 0 and ct.slots == 64
+        errs[sc] = np.max(np.abs(np.array(e.decrypt(ct)) - x))
+    assert errs["FLEXIBLEAUTO"] < 2 ** -20
+    assert errs["FLEXIBLEAUTOEXT"] < errs["FLEXIBLEAUTO"] / 4  # fresh noise divided by q_ext
+
+
+def test_arithmetic_and_levels(oracle_lib):
+    e = sfhe.Engine("oracle", mult_depth=6, ring_dim=1 << 12, batch_size=16)
+    rng = np.random.default_rng(3)
+    a, b = rng.uniform(-1, 1, 16), rng.uniform(-1, 1, 16)
+    ca, cb = e.encrypt(a.tolist()), e.encrypt(b.tolist())
+    chk = lambda ct, ref, tol=1e-5: np.testing.assert_allclose(e.decrypt(ct), ref, atol=tol)
+    chk(e.add(ca, cb), a + b)
+    chk(e.sub(ca, cb), a - b)
+    m = e.mult(ca, cb)
+    assert m.level == 1
+    chk(m, a * b)
+    chk(e.mult_const(ca, -2.5), -2.5 * a)
+    chk(e.add_const(ca, 0.25), a + 0.25)
+    chk(e.mult_plain(ca, list(range(16)), 16), a * np.arange(16), 1e-4)
+    # mixed levels align automatically
+    chk(e.add(m, ca), a * b + a)
+    sq = e.mult(e.mult(m, m), m)
+    assert sq.level == 3
+    chk(sq, (a * b) ** 3)
+
+
+@pytest.mark.parametrize("r", [1, 2, 3, 5, 8, -1, 15])
+def test_rotation(oracle_lib, r):
+    """RotationTest (tests/RotationTest.cpp:73-170): left rotation, 1e-6."""
+    e = sfhe.Engine("oracle", mult_depth=2, ring_dim=1 << 12, batch_size=16,
+                    scaling_mod_size=50, rotations=[1, 2, 3, 5, 8, -1, 15])
+    x = np.arange(16) / 16.0
+    got = np.array(e.decrypt(e.rotate(e.encrypt(x.tolist()), r)))
+    np.testing.assert_allclose(got, np.roll(x, -r), atol=1e-6)
+
+
+def test_compare_reference_vectors(oracle_lib):
+    """tests/CompareTest.cpp:13-63, verbatim parameters."""
+    t = REF["compare_test"]
+    e = sfhe.Engine("oracle", mult_depth=t["mult_depth"], ring_dim=1 << t["ring_dim_log2"],
+                    batch_size=len(t["a"]), scaling_mod_size=t["scaling_mod_size"])
+    out = e.compare(e.encrypt(t["a"]), e.encrypt(t["b"]), *t["composite_sign_config"])
+    np.testing.assert_allclose(e.decrypt(out), t["expected"], atol=t["tolerance"])
+
+
+@pytest.mark.parametrize("cfg", [(3, 2, 2), (4, 3, 3)])
+def test_sign_matches_slot_simulation(oracle_lib, cfg):
+    """SignTest shape (tests/SignTest.cpp:17-121) at ring 2^12, depth 30, scale 50."""
+    e = sfhe.Engine("oracle", mult_depth=30, ring_dim=1 << 12, batch_size=512, scaling_mod_size=50)
+    rng = np.random.default_rng(5)
+    x = rng.uniform(2 ** -5, 1, 512) * rng.choice([-1, 1], 512)
+    out = e.sign(e.encrypt(x.tolist()), *cfg)
+    got = np.array(e.decrypt(out))
+    assert out.level == slotsim.sign_depth(*cfg)
+    assert np.all(np.sign(got) == np.sign(x))
+    assert np.max(np.abs(got - slotsim.composite_sign(x, *cfg))) < 1e-4
+
+
+def test_chebyshev_ps(oracle_lib):
+    """EvalChebyshevSeriesPS on the doubled sinc of N=8 (degree 70, depth 7)."""
+    c = cheb.doubled_sinc_coeffs(8)
+    e = sfhe.Engine("oracle", mult_depth=9, ring_dim=1 << 12, batch_size=64, scaling_mod_size=50)
+    x = np.linspace(-0.99, 0.99, 64)
+    out = e.chebyshev(e.encrypt(x.tolist()), c.tolist())
+    assert out.level == cheb.ps_depth(len(c) - 1)
+    np.testing.assert_allclose(e.decrypt(out), cheb.cheb_eval(c, x), atol=1e-6)
+
+
+@pytest.mark.parametrize("N", [4, 8, 16])
+def test_direct_sort(oracle_lib, N):
+    """DirectSortTest (tests/DirectSortTest.cpp:96-210) on the oracle at ring 2^12."""
+    depth, rots = sfhe.direct_sort_params(N, "oracle")
+    e = sfhe.Engine("oracle", mult_depth=depth, ring_dim=1 << 12, batch_size=N, rotations=rots,
+                    seed=20251205 + N)
+    e.set_quiet(True)
+    x = slotsim.input_vector(N)
+    out = e.sorter(N).sort(e.encrypt(x.tolist()), *slotsim.default_sign_config(N))
+    assert out.level == depth
+    got = np.array(e.decrypt(out))
+    assert np.max(np.abs(got - np.sort(x))) < 0.01
+    sim, _ = slotsim.direct_sort(x, N, 1 << 12)
+    assert np.max(np.abs(got - sim)) < 2 ** -12
+
+
+def test_sort_rank_and_place_split(oracle_lib):
+    """constructRank then rotationIndexCheckN == sort (sort_algo.h:752-774)."""
+    N = 8
+    depth, rots = sfhe.direct_sort_params(N, "oracle")
+    e = sfhe.Engine("oracle", mult_depth=depth, ring_dim=1 << 12, batch_size=N, rotations=rots)
+    e.set_quiet(True)
+    x = slotsim.input_vector(N)
+    s = e.sorter(N)
+    ct = e.encrypt(x.tolist())
+    rank = s.rank(ct, *slotsim.default_sign_config(N))
+    np.testing.assert_allclose(e.decrypt(rank), np.argsort(np.argsort(x)), atol=1e-3)
+    out = s.place(rank, ct)
+    np.testing.assert_allclose(e.decrypt(out), np.sort(x), atol=0.01)
+
+
+def test_depth_exhaustion_is_an_error(oracle_lib):
+    e = sfhe.Engine("oracle", mult_depth=1, ring_dim=1 << 12, batch_size=4)
+    c = e.encrypt([0.5, 0.5, 0.5, 0.5])
+    c2 = e.mult(c, c)
+    with pytest.raises(sfhe.SfheError):
+        e.mult(c2, c2)

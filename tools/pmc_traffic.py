@@ -1,0 +1,95 @@
+#!/usr/bin/env python3
+"""HBM traffic per launch of the hot kernel families from two rocprofv3 PMC
+passes (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950):
+
+    rocprofv3 --pmc FETCH_SIZE --output-format csv -d F -o run -- python3 bench.py ...
+    rocprofv3 --pmc WRITE_SIZE --output-format csv -d W -o run -- python3 bench.py ...
+    python tools/pmc_traffic.py F/run_counter_collection.csv W/run_counter_collection.csv \
+        --n 65536 --out profiles/pmc_traffic.json
+
+Corrections (/opt/skills/guides/MI355X_MICROARCH.md, HBM section): counters
+are in KiB; FETCH_SIZE reports half the bytes of a 16-B-per-lane coalesced
+streaming read (x2); WRITE_SIZE is exact for 16-B-per-lane stores.  The NTT
+and k_conv / k_ks_inner read and write 16 B per lane where contiguous.
+
+Algorithmic bytes per launch (prims.h): NTT pass 16 B x coefficients of the
+launch (from the grid: 256 threads per 4096-word tile).
+"""
+import argparse
+import collections
+import csv
+import hashlib
+import json
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def family(name: str):
+    s = name.split("(")[0].replace("void ", "")
+    if s.startswith("k_ntt"):
+        return "ntt"
+    if s == "k_conv":
+        return "conv"
+    if s == "k_ks_inner":
+        return "ks_inner"
+    return None
+
+
+def load(path, counter):
+    per = {}
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if r["Counter_Name"] != counter:
+                continue
+            per[int(r["Dispatch_Id"])] = (r["Kernel_Name"], int(r["Grid_Size"]), float(r["Counter_Value"]))
+    return per
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch_csv")
+    ap.add_argument("write_csv")
+    ap.add_argument("--n", type=int, default=65536)
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    a = ap.parse_args()
+    fe = load(a.fetch_csv, "FETCH_SIZE")
+    wr = load(a.write_csv, "WRITE_SIZE")
+    acc = collections.defaultdict(lambda: {"launches": 0, "fetch": 0.0, "write": 0.0, "algo": 0.0})
+    # the two passes run the same deterministic program: pair dispatches by
+    # order within each family
+    fam_f = collections.defaultdict(list)
+    fam_w = collections.defaultdict(list)
+    for _, (name, grid, v) in sorted(fe.items()):
+        if family(name):
+            fam_f[family(name)].append((grid, v))
+    for _, (name, grid, v) in sorted(wr.items()):
+        if family(name):
+            fam_w[family(name)].append((grid, v))
+    out = {}
+    for fam in fam_f:
+        F, W = fam_f[fam], fam_w.get(fam, [])
+        k = min(len(F), len(W))
+        fetch = sum(v for _, v in F[:k]) * 1024 * 2
+        write = sum(v for _, v in W[:k]) * 1024
+        entry = {"launches": k, "hbm_bytes_per_launch": (fetch + write) / k,
+                 "fetch_bytes_per_launch": fetch / k, "write_bytes_per_launch": write / k}
+        if fam == "ntt":
+            tiles_threads = 256 * (a.n // 4096)
+            algo = sum(16.0 * (g // tiles_threads) * a.n for g, _ in F[:k])
+            entry["algorithmic_bytes_per_launch"] = algo / k
+            entry["traffic_over_algorithmic"] = (fetch + write) / algo
+        out[fam] = entry
+    src = os.path.join(ROOT, "sorting-fhe_amd", "csrc", "hip", "prims_hip.hip")
+    with open(src, "rb") as f:
+        sha = hashlib.sha256(f.read()).hexdigest()[:16]
+    j = {"kernel_source_sha": sha, "ring_dim": a.n,
+         "corrections": "KiB->B; FETCH_SIZE x2 (gfx950 16-B/lane streaming read); WRITE_SIZE x1",
+         "families": out}
+    with open(a.out, "w") as f:
+        json.dump(j, f, indent=1)
+    print(json.dumps(j, indent=1))
+
+
+if __name__ == "__main__":
+    main()
