@@ -46,6 +46,7 @@ struct sfp_conv {
     uint32_t *src, *dst;
     u64 *inv, *mod;
     u64 *sprod; /* prod(S) mod dst_t */
+    uint32_t *drow; /* output row of target t */
 };
 
 static inline u64 mm(u64 a, u64 b, u64 q) { return (u64)(((u128)a * b) % q); }
@@ -290,9 +291,12 @@ void sfp_rescale_ext(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t ell
 
 /* ---- base conversion / key switching ---- */
 sfp_conv* sfp_upload_conv(sfp_dev* d, uint32_t ns, const uint32_t* src, uint32_t nt,
-                          const uint32_t* dst, const uint64_t* inv, const uint64_t* mod) {
+                          const uint32_t* dst, const uint32_t* drow, const uint64_t* inv,
+                          const uint64_t* mod) {
     sfp_conv* c = (sfp_conv*)calloc(1, sizeof(sfp_conv));
     c->ns = ns; c->nt = nt;
+    c->drow = (uint32_t*)malloc(nt * 4);
+    for (uint32_t t = 0; t < nt; ++t) c->drow[t] = drow ? drow[t] : t;
     c->src = (uint32_t*)malloc(ns * 4); memcpy(c->src, src, ns * 4);
     c->dst = (uint32_t*)malloc(nt * 4); memcpy(c->dst, dst, nt * 4);
     c->inv = (u64*)malloc(ns * 8); memcpy(c->inv, inv, ns * 8);
@@ -308,7 +312,7 @@ sfp_conv* sfp_upload_conv(sfp_dev* d, uint32_t ns, const uint32_t* src, uint32_t
 void sfp_free_conv(sfp_dev* d, sfp_conv* c) {
     (void)d;
     if (!c) return;
-    free(c->src); free(c->dst); free(c->inv); free(c->mod); free(c->sprod); free(c);
+    free(c->src); free(c->dst); free(c->inv); free(c->mod); free(c->sprod); free(c->drow); free(c);
 }
 
 /* dst row t (prime c->dst[t]) = sum_i [src_i * inv_i]_{s_i} * mod[i][t]  (coefficient domain).
@@ -340,28 +344,33 @@ static void conv_rows(const sfp_dev* d, const sfp_conv* c, const u64* src, u64* 
 
 void sfp_conv_apply(sfp_dev* d, uint64_t* dst, const uint64_t* src, const sfp_conv* c) {
     u64** rows = (u64**)malloc(c->nt * sizeof(u64*));
-    for (uint32_t t = 0; t < c->nt; ++t) rows[t] = dst + (size_t)t * d->n;
+    for (uint32_t t = 0; t < c->nt; ++t) rows[t] = dst + (size_t)c->drow[t] * d->n;
     conv_rows(d, c, src, rows, c->nt, 0);
     free(rows);
 }
 
-void sfp_modup(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t ell, uint32_t K,
-               uint32_t Lq, uint32_t lo, uint32_t hi, const sfp_conv* c, uint64_t* scratch) {
-    const uint32_t n = d->n, ns = hi - lo;
-    (void)K;
-    memcpy(scratch, in + (size_t)lo * n, (size_t)ns * n * 8);
-    for (uint32_t i = 0; i < ns; ++i) ntt_inv(d, scratch + (size_t)i * n, lo + i);
-    u64** rows = (u64**)malloc(c->nt * sizeof(u64*));
-    for (uint32_t t = 0; t < c->nt; ++t) {
-        uint32_t pr = c->dst[t];
-        uint32_t pos = pr < Lq ? pr : ell + (pr - Lq);
-        rows[t] = out + (size_t)pos * n;
-    }
-    conv_rows(d, c, scratch, rows, c->nt, 0);
+/* every digit j: own rows copied, the others NTT(Conv_j(INTT(in[digit j]))) */
+void sfp_modup(sfp_dev* d, uint64_t* ext, const uint64_t* in, uint32_t ell, uint32_t K,
+               uint32_t Lq, uint32_t alpha, const sfp_conv* const* convs, uint64_t* scratch) {
+    const uint32_t n = d->n;
+    const uint32_t beta = (ell + alpha - 1) / alpha;
+    const size_t stride = (size_t)(ell + K) * n;
+    (void)Lq;
+    memcpy(scratch, in, (size_t)ell * n * 8);
 #pragma omp parallel for schedule(static)
-    for (uint32_t t = 0; t < c->nt; ++t) ntt_fwd(d, rows[t], c->dst[t]);
-    free(rows);
-    memcpy(out + (size_t)lo * n, in + (size_t)lo * n, (size_t)ns * n * 8);
+    for (uint32_t i = 0; i < ell; ++i) ntt_inv(d, scratch + (size_t)i * n, i);
+    for (uint32_t j = 0; j < beta; ++j) {
+        const sfp_conv* c = convs[j];
+        const uint32_t lo = j * alpha, hi = lo + alpha < ell ? lo + alpha : ell;
+        u64* out = ext + j * stride;
+        u64** rows = (u64**)malloc(c->nt * sizeof(u64*));
+        for (uint32_t t = 0; t < c->nt; ++t) rows[t] = out + (size_t)c->drow[t] * n;
+        conv_rows(d, c, scratch + (size_t)lo * n, rows, c->nt, 0);
+#pragma omp parallel for schedule(static)
+        for (uint32_t t = 0; t < c->nt; ++t) ntt_fwd(d, rows[t], c->dst[t]);
+        free(rows);
+        memcpy(out + (size_t)lo * n, in + (size_t)lo * n, (size_t)(hi - lo) * n * 8);
+    }
 }
 
 void sfp_ks_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
@@ -387,8 +396,9 @@ void sfp_ks_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ex
     }
 }
 
-void sfp_moddown(sfp_dev* d, uint64_t* out, uint64_t* acc, uint32_t ell, uint32_t K, uint32_t Lq,
-                 const sfp_conv* c, const uint64_t* pinv, int add, uint64_t* scratch) {
+static void moddown1(sfp_dev* d, uint64_t* out, uint64_t* acc, uint32_t ell, uint32_t K,
+                     uint32_t Lq, const sfp_conv* c, const uint64_t* pinv, int add,
+                     uint64_t* scratch) {
     const uint32_t n = d->n;
     u64* pRows = acc + (size_t)ell * n;
     for (uint32_t k = 0; k < K; ++k) ntt_inv(d, pRows + (size_t)k * n, Lq + k);
@@ -406,6 +416,13 @@ void sfp_moddown(sfp_dev* d, uint64_t* out, uint64_t* acc, uint32_t ell, uint32_
         }
     }
     free(rows);
+}
+
+void sfp_moddown2(sfp_dev* d, uint64_t* out0, uint64_t* out1, uint64_t* acc, size_t acc_stride,
+                  uint32_t ell, uint32_t K, uint32_t Lq, const sfp_conv* c, const uint64_t* pinv,
+                  int add0, int add1, uint64_t* scratch) {
+    moddown1(d, out0, acc, ell, K, Lq, c, pinv, add0, scratch);
+    moddown1(d, out1, acc + acc_stride, ell, K, Lq, c, pinv, add1, scratch + (size_t)ell * d->n);
 }
 
 /* ---- sampling / loading ---- */

@@ -273,23 +273,19 @@ class SfheInternal {
         b = adjust(cc, b, l);
     }
 
-    // Hybrid key switch of d (ell limbs, evaluation domain) with `key`;
-    // adds the result into (out0, out1) (ell limbs each).
-    static void keySwitchAdd(CC* cc, const uint64_t* d, uint32_t ell, const DeviceBufferPtr& key,
-                             uint64_t* out0, uint64_t* out1) {
+    // Hybrid key switch of d (ell limbs, evaluation domain) with `key`; the
+    // result goes to (out0, out1) (ell limbs each), added when add0 / add1.
+    static void keySwitch(CC* cc, const uint64_t* d, uint32_t ell, const DeviceBufferPtr& key,
+                          uint64_t* out0, uint64_t* out1, int add0, int add1) {
         SfheContextState* s = cc->st.get();
         const uint32_t n = s->n, K = s->K;
         const uint32_t beta = (ell + s->alpha - 1) / s->alpha;
         const size_t stride = (size_t)(ell + K) * n;
         auto ext = s->alloc(stride * beta);
-        auto scratch = s->alloc((size_t)s->alpha * n);
+        auto scratch = s->alloc((size_t)ell * n);
         auto& convs = modupConv(cc, ell);
-        for (uint32_t j = 0; j < beta; ++j) {
-            uint32_t lo = j * s->alpha, hi = std::min(lo + s->alpha, ell);
-            sfp_modup(s->dev, ext->ptr + j * stride, d, ell, K, s->Lq, lo, hi, convs[j],
-                      scratch->ptr);
-        }
-        innerAndModDown(cc, ext->ptr, stride, beta, ell, key, out0, out1);
+        sfp_modup(s->dev, ext->ptr, d, ell, K, s->Lq, s->alpha, convs.data(), scratch->ptr);
+        innerAndModDown(cc, ext->ptr, stride, beta, ell, key, out0, out1, add0, add1);
         s->stats.keyswitch++;
         // (3 l + 2 beta (l+K)) B
         s->countBytes((3.0 * ell + 2.0 * beta * (ell + K)) * n * 8);
@@ -297,18 +293,16 @@ class SfheInternal {
 
     static void innerAndModDown(CC* cc, const uint64_t* ext, size_t stride, uint32_t beta,
                                 uint32_t ell, const DeviceBufferPtr& key, uint64_t* out0,
-                                uint64_t* out1) {
+                                uint64_t* out1, int add0, int add1) {
         SfheContextState* s = cc->st.get();
         const uint32_t n = s->n, K = s->K;
-        auto acc = s->alloc((size_t)2 * (ell + K) * n);
-        uint64_t* acc0 = acc->ptr;
-        uint64_t* acc1 = acc0 + (size_t)(ell + K) * n;
-        sfp_ks_inner(s->dev, acc0, acc1, ext, stride, key->ptr, beta, ell, K, s->Lq);
-        auto scratch = s->alloc((size_t)(ell + K) * n);
-        sfp_moddown(s->dev, out0, acc0, ell, K, s->Lq, s->moddownConv, s->pInvModQ.data(), 1,
-                    scratch->ptr);
-        sfp_moddown(s->dev, out1, acc1, ell, K, s->Lq, s->moddownConv, s->pInvModQ.data(), 1,
-                    scratch->ptr);
+        const size_t accStride = (size_t)(ell + K) * n;
+        auto acc = s->alloc(2 * accStride);
+        sfp_ks_inner(s->dev, acc->ptr, acc->ptr + accStride, ext, stride, key->ptr, beta, ell, K,
+                     s->Lq);
+        auto scratch = s->alloc((size_t)2 * ell * n);
+        sfp_moddown2(s->dev, out0, out1, acc->ptr, accStride, ell, K, s->Lq, s->moddownConv,
+                     s->pInvModQ.data(), add0, add1, scratch->ptr);
     }
 
     static std::vector<sfp_conv*>& modupConv(CC* cc, uint32_t ell) {
@@ -319,18 +313,20 @@ class SfheInternal {
         uint32_t beta = (ell + s->alpha - 1) / s->alpha;
         for (uint32_t j = 0; j < beta; ++j) {
             uint32_t lo = j * s->alpha, hi = std::min(lo + s->alpha, ell);
-            std::vector<uint32_t> src, dst;
+            std::vector<uint32_t> src, dst, row;
             for (uint32_t i = lo; i < hi; ++i) src.push_back(i);
             for (uint32_t i = 0; i < ell; ++i)
                 if (i < lo || i >= hi) dst.push_back(i);
             for (uint32_t k = 0; k < s->K; ++k) dst.push_back(s->Lq + k);
-            v.push_back(makeConv(s, src, dst));
+            // extended layout: q rows at their index, P row k at ell + k
+            for (uint32_t p : dst) row.push_back(p < s->Lq ? p : ell + (p - s->Lq));
+            v.push_back(makeConv(s, src, dst, row.data()));
         }
         return s->modupConv[ell] = v;
     }
 
     static sfp_conv* makeConv(SfheContextState* s, const std::vector<uint32_t>& src,
-                              const std::vector<uint32_t>& dst) {
+                              const std::vector<uint32_t>& dst, const uint32_t* dstRow = nullptr) {
         const uint32_t ns = (uint32_t)src.size(), nt = (uint32_t)dst.size();
         std::vector<u64> inv(ns), mod((size_t)ns * nt);
         for (uint32_t i = 0; i < ns; ++i) {
@@ -347,7 +343,8 @@ class SfheInternal {
                 mod[(size_t)i * nt + t] = pr;
             }
         }
-        return sfp_upload_conv(s->dev, ns, src.data(), nt, dst.data(), inv.data(), mod.data());
+        return sfp_upload_conv(s->dev, ns, src.data(), nt, dst.data(), dstRow, inv.data(),
+                               mod.data());
     }
 
     // switching key from s' (device, Lq+K limbs, eval domain) to s
@@ -1115,7 +1112,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMult(const Ciphertext<DCRT
     sfp_tensor(s->dev, d0, d1, d2, a->c0, a->c1, b->c0, b->c1, SfheInternal::Q(ell));
     s->stats.tensor++;
     s->countBytes(7.0 * ell * s->n * 8);
-    SfheInternal::keySwitchAdd(this, d2, ell, s->relinKey, d0, d1);
+    SfheInternal::keySwitch(this, d2, ell, s->relinKey, d0, d1, 1, 1);
     return SfheInternal::traced(this, SfheInternal::rescale(this, d0, d1, a->level, std::max(a->slots, b->slots)), "EvalMult");
 }
 
@@ -1183,10 +1180,10 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotate(const Ciphertext<DC
     auto t = s->alloc((size_t)ell * s->n);
     sfp_automorph(s->dev, out->c0, a->c0, gal, SfheInternal::Q(ell));
     sfp_automorph(s->dev, t->ptr, a->c1, gal, SfheInternal::Q(ell));
-    sfp_zero(s->dev, out->c1, (size_t)ell * s->n * 8);
     s->stats.automorph++;
     s->countBytes(3.0 * ell * s->n * 8);
-    SfheInternal::keySwitchAdd(this, t->ptr, ell, it->second, out->c0, out->c1);
+    // c0' = sigma(c0) + ks0, c1' = ks1
+    SfheInternal::keySwitch(this, t->ptr, ell, it->second, out->c0, out->c1, 1, 0);
     return SfheInternal::traced(this, out, "EvalRotate");
 }
 
@@ -1200,13 +1197,10 @@ std::shared_ptr<FastRotationPrecomp> CryptoContextImpl<DCRTPoly>::EvalFastRotati
     pre->beta = (ell + s->alpha - 1) / s->alpha;
     pre->stride = (size_t)(ell + s->K) * s->n;
     pre->ext = s->alloc(pre->stride * pre->beta);
-    auto scratch = s->alloc((size_t)s->alpha * s->n);
+    auto scratch = s->alloc((size_t)ell * s->n);
     auto& convs = SfheInternal::modupConv(this, ell);
-    for (uint32_t j = 0; j < pre->beta; ++j) {
-        uint32_t lo = j * s->alpha, hi = std::min(lo + s->alpha, ell);
-        sfp_modup(s->dev, pre->ext->ptr + j * pre->stride, a->c1, ell, s->K, s->Lq, lo, hi,
-                  convs[j], scratch->ptr);
-    }
+    sfp_modup(s->dev, pre->ext->ptr, a->c1, ell, s->K, s->Lq, s->alpha, convs.data(),
+              scratch->ptr);
     return pre;
 }
 
@@ -1224,14 +1218,13 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalFastRotation(
     // sigma commutes with the (coefficient-wise) base extension, so rotating
     // the extended digits equals extending the rotated c1.
     auto ext = s->alloc(pre->stride * pre->beta);
-    const sfp_limbs em{ell + s->K, ell, s->Lq};
-    for (uint32_t j = 0; j < pre->beta; ++j)
-        sfp_automorph(s->dev, ext->ptr + j * pre->stride, pre->ext->ptr + j * pre->stride, gal, em);
+    // one permutation launch over every digit's rows (the map is prime-independent)
+    const uint32_t rows = pre->beta * (ell + s->K);
+    sfp_automorph(s->dev, ext->ptr, pre->ext->ptr, gal, sfp_limbs{rows, rows, 0, 0});
     auto out = SfheInternal::newCt(this, a->level, a->slots);
     sfp_automorph(s->dev, out->c0, a->c0, gal, SfheInternal::Q(ell));
-    sfp_zero(s->dev, out->c1, (size_t)ell * s->n * 8);
     SfheInternal::innerAndModDown(this, ext->ptr, pre->stride, pre->beta, ell, it->second,
-                                  out->c0, out->c1);
+                                  out->c0, out->c1, 1, 0);
     s->stats.keyswitch++;
     s->stats.automorph++;
     s->countBytes((3.0 * ell + 2.0 * pre->beta * (ell + s->K)) * s->n * 8);

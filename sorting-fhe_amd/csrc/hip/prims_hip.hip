@@ -16,6 +16,7 @@
 // its last pass.  Twiddles are the bit-reversed psi tables (Shoup form).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -108,6 +109,7 @@ struct sfp_conv {
     u64* inv = nullptr;       // device [ns]
     u64* mod = nullptr;       // device [ns][nt]
     u64* sprod = nullptr;     // device [nt]: prod(S) mod dst_t (centred conversion)
+    uint32_t* drow = nullptr; // device [nt]: output row of target t
     std::vector<uint32_t> hsrc, hdst;
 };
 
@@ -131,6 +133,20 @@ static void checkLaunch(sfp_dev* d, const char* k) {
         e = hipStreamSynchronize(d->stream);
         if (e != hipSuccess) record(d, k, e);
     }
+}
+
+// Every prime index a limb map can produce must exist: a kernel given an
+// out-of-table prime would read garbage reduction constants (and a zero
+// modulus never terminates a reduction loop), so reject the call on the host.
+static bool limbsOk(sfp_dev* d, const sfp_limbs& m, const char* what) {
+    if (!m.count) return true;
+    uint32_t hi = 0;
+    if (m.split) hi = m.base + m.split - 1;
+    if (m.count > m.split) hi = std::max(hi, m.pbase + (m.count - m.split) - 1);
+    if (hi < d->np && m.count <= (1u << 20)) return true;
+    std::lock_guard<std::mutex> g(d->mu);
+    if (d->err.empty()) d->err = std::string(what) + ": limb map indexes past the prime table";
+    return false;
 }
 
 // ---- live kernel timing ----
@@ -191,13 +207,25 @@ static unsigned gridFor(size_t work, unsigned perBlock) {
 // x with x + n/2^(S+1) and uses psi_rev[2^S + (x >> (logn - S))].
 //   COL pass: stages 0..logR-1; a tile is C = 4096/R whole columns (R x C).
 //   ROW pass: stages logR..logn-1; a tile is 16 whole rows (16 x 256).
-// The tile is staged in padded LDS (word e at e + e/16: conflict-free for the
-// unit-stride and stride-16 patterns below) and its stages are run in rounds
-// of up to four: every thread pulls 16 words into registers, runs the round's
-// radix-2 stages there, and writes them back -- one LDS round trip per four
-// stages.  The inverse runs the Gentleman-Sande stages in reverse order (ROW
-// pass first) and folds n^-1 into the COL pass's store.
-__device__ __forceinline__ uint32_t ldsPad(uint32_t e) { return e + (e >> 4); }
+// A 512-thread block stages the tile in LDS (XOR-swizzled: every round's
+// 32-lane access pattern hits distinct banks) and runs its stages in rounds
+// of up to three: each thread pulls 8 words into registers, runs the round's
+// radix-2 stages there and writes them back.  Butterflies are lazy (Harvey):
+// forward values live in [0, 4q), inverse values in [0, 2q); the pass that
+// finishes the transform reduces to [0, q).  The inverse runs the
+// Gentleman-Sande stages in reverse order (ROW pass first) and folds n^-1
+// into the COL pass's store.
+#ifndef SFHE_NTT_LOGE
+#define SFHE_NTT_LOGE 3
+#endif
+constexpr int kNttLogE = SFHE_NTT_LOGE;         // stages per register round
+constexpr int kNttE = 1 << kNttLogE;            // words per thread per round
+constexpr int kNttThreads = kTile / kNttE;      // threads per 4096-word tile
+
+__device__ __forceinline__ uint32_t ldsSw(uint32_t e) {
+    const uint32_t x = e >> 5;
+    return e ^ ((x ^ (x << 2)) & 31u);
+}
 
 struct NttTile {
     uint32_t logn, d;     // d = stages in this pass (logR or 8)
@@ -216,19 +244,20 @@ __device__ __forceinline__ uint32_t nttLocal(const NttTile& T, uint32_t st, uint
 }
 
 // One round: stages k0..k0+B-1 of the pass (k relative to the pass's first
-// global stage S0).  16/2^B groups of 2^B words per thread.
+// global stage S0).  8/2^B groups of 2^B words per thread.
 template <bool INV, bool COL, int B>
 __device__ __forceinline__ void nttRound(u64* s, const NttTile& T, uint32_t S0, uint32_t k0, u64 q,
                                          const u64* __restrict__ w, const u64* __restrict__ wS) {
     constexpr int M = 1 << B;
-    constexpr int GPT = 16 / M;  // groups per thread
+    constexpr int GPT = kNttE / M;  // groups per thread
     const uint32_t D = 1u << T.d;
     const uint32_t h = D >> (k0 + B);     // smallest stride of the round (in u)
     const uint32_t span = D >> k0;        // hi step
     const uint32_t nsub = COL ? T.C : 16u;
+    const u64 q2 = 2 * q;
 #pragma unroll
     for (int gi = 0; gi < GPT; ++gi) {
-        const uint32_t gid = threadIdx.x + gi * kThreads;
+        const uint32_t gid = threadIdx.x + gi * kNttThreads;
         uint32_t st, lo, hi;
         if (COL) {
             st = gid % nsub;
@@ -242,74 +271,114 @@ __device__ __forceinline__ void nttRound(u64* s, const NttTile& T, uint32_t S0, 
             st = rest >> k0;
         }
         const uint32_t ub = hi * span + lo;
+        // stage t of the round uses psi_rev[2^S + (x0 >> (logn-S)) + (j >> (B-t))]
+        // (x0 = member 0's global index): 2^t distinct twiddles, all loaded
+        // up front so the round waits on one memory latency, not B
+        const uint32_t x0 = nttGlobal<COL>(T, st, ub);
+        u64 W[M - 1], WS[M - 1];  // stage t's q-th twiddle at (1<<t)-1+q
+#pragma unroll
+        for (int t = 0; t < B; ++t) {
+            const uint32_t S = S0 + k0 + t;
+            const uint32_t tb = (1u << S) + (x0 >> (T.logn - S));
+#pragma unroll
+            for (int qd = 0; qd < (1 << t); ++qd) {
+                W[(1 << t) - 1 + qd] = w[tb + qd];
+                WS[(1 << t) - 1 + qd] = wS[tb + qd];
+            }
+        }
         u64 v[M];
 #pragma unroll
-        for (int j = 0; j < M; ++j) v[j] = s[ldsPad(nttLocal<COL>(T, st, ub + j * h))];
+        for (int j = 0; j < M; ++j) v[j] = s[ldsSw(nttLocal<COL>(T, st, ub + j * h))];
         if (!INV) {
+            // Harvey CT butterfly: in [0,4q) -> out [0,4q)
 #pragma unroll
             for (int t = 0; t < B; ++t) {
-                const uint32_t S = S0 + k0 + t;
                 const int half = 1 << (B - 1 - t);
 #pragma unroll
                 for (int j = 0; j < M; ++j) {
                     if (j & half) continue;
-                    const uint32_t x = nttGlobal<COL>(T, st, ub + j * h);
-                    const uint32_t ti = (1u << S) + (x >> (T.logn - S));
-                    const u64 W = w[ti], WS = wS[ti];
-                    const u64 U = v[j];
-                    const u64 V = sf_mul_shoup(v[j + half], W, WS, q);
-                    v[j] = sf_add(U, V, q);
-                    v[j + half] = sf_sub(U, V, q);
+                    const int ti = (1 << t) - 1 + (j >> (B - t));
+                    u64 X = v[j];
+                    X = X >= q2 ? X - q2 : X;
+                    const u64 Y = sf_mul_shoup_lazy(v[j + half], W[ti], WS[ti], q);
+                    v[j] = X + Y;
+                    v[j + half] = X - Y + q2;
                 }
             }
         } else {
+            // Harvey GS butterfly: in [0,2q) -> out [0,2q)
 #pragma unroll
             for (int t = B - 1; t >= 0; --t) {
-                const uint32_t S = S0 + k0 + t;
                 const int half = 1 << (B - 1 - t);
 #pragma unroll
                 for (int j = 0; j < M; ++j) {
                     if (j & half) continue;
-                    const uint32_t x = nttGlobal<COL>(T, st, ub + j * h);
-                    const uint32_t ti = (1u << S) + (x >> (T.logn - S));
-                    const u64 W = w[ti], WS = wS[ti];
-                    const u64 U = v[j], V = v[j + half];
-                    v[j] = sf_add(U, V, q);
-                    v[j + half] = sf_mul_shoup(sf_sub(U, V, q), W, WS, q);
+                    const int ti = (1 << t) - 1 + (j >> (B - t));
+                    const u64 X = v[j], Y = v[j + half];
+                    const u64 Sm = X + Y;
+                    v[j] = Sm >= q2 ? Sm - q2 : Sm;
+                    v[j + half] = sf_mul_shoup_lazy(X - Y + q2, W[ti], WS[ti], q);
                 }
             }
         }
 #pragma unroll
-        for (int j = 0; j < M; ++j) s[ldsPad(nttLocal<COL>(T, st, ub + j * h))] = v[j];
+        for (int j = 0; j < M; ++j) s[ldsSw(nttLocal<COL>(T, st, ub + j * h))] = v[j];
     }
 }
 
 template <bool INV, bool COL>
 __device__ __forceinline__ void nttRoundDyn(int b, u64* s, const NttTile& T, uint32_t S0, uint32_t k0,
                                             u64 q, const u64* w, const u64* wS) {
-    switch (b) {
-        case 4: nttRound<INV, COL, 4>(s, T, S0, k0, q, w, wS); break;
-        case 3: nttRound<INV, COL, 3>(s, T, S0, k0, q, w, wS); break;
-        case 2: nttRound<INV, COL, 2>(s, T, S0, k0, q, w, wS); break;
-        default: nttRound<INV, COL, 1>(s, T, S0, k0, q, w, wS); break;
+    if constexpr (kNttLogE >= 3) {
+        if (b == 3) return nttRound<INV, COL, 3>(s, T, S0, k0, q, w, wS);
     }
+    if (b == 2) return nttRound<INV, COL, 2>(s, T, S0, k0, q, w, wS);
+    nttRound<INV, COL, 1>(s, T, S0, k0, q, w, wS);
+}
+
+// A 2-D set of rows for one NTT launch, passed by value: row (p, i) for
+// p < P, i < R lives at base + p*ps + i*is (word offsets).  Prime of row i:
+// primeOf(pm, i).  The first pass reads `src` (optionally the centred lift of
+// a row modulo prime `liftPrime`; optionally also writing the raw words to
+// `copy`), the intermediate lands in `dst`, and the last pass writes `dst` --
+// or, with `epi`, eout = (ein - v) * k_i (+ eout when `add`).
+struct RowPtr {
+    const u64* base;
+    long long ps, is;  // word strides (may be negative: two unrelated buffers)
+};
+struct RowGroup {
+    uint32_t P, R;
+    sfp_limbs pm;
+    RowPtr src, dst, copy, ein, eout;
+    uint32_t copyByAlpha;  // copy row = copy.base + (i / alpha) * ps + i * is
+    uint32_t alpha;
+    uint32_t skipEll;      // >0: skip rows alpha*p <= i < min(alpha*(p+1), skipEll) (ModUp own digit)
+    uint32_t lift, liftPrime;
+    uint32_t epi, addMask;  // addMask bit p: accumulate into eout for polynomial p
+    u64 k[SFP_MAX_LIMBS], kS[SFP_MAX_LIMBS];  // epilogue constant per i (value, Shoup)
+    u64 liftSub[SFP_MAX_LIMBS];               // q_liftPrime mod q_i
+};
+
+__device__ __forceinline__ u64* rowAt(const RowPtr& r, uint32_t p, uint32_t i) {
+    return const_cast<u64*>(r.base) + p * r.ps + i * r.is;
 }
 
 template <bool INV, bool COL>
-__global__ __launch_bounds__(kThreads) void k_ntt(u64* __restrict__ data, sfp_limbs m,
-                                                  const sf_barrett* __restrict__ bar,
+__global__ __launch_bounds__(kNttThreads) void k_ntt(const RowGroup G, const sf_barrett* __restrict__ bar,
                                                   const u64* __restrict__ tw, const u64* __restrict__ twS,
                                                   const u64* __restrict__ ninv,
                                                   const u64* __restrict__ ninvS, uint32_t logn) {
-    __shared__ u64 s[kTile + kTile / 16];
+    __shared__ u64 s[kTile];
+    constexpr bool FIRST = (COL != INV);  // forward: COL first; inverse: ROW first
     const uint32_t n = 1u << logn;
     const uint32_t logR = logn - 8;
-    const uint32_t limb = blockIdx.y;
-    const uint32_t p = primeOf(m, limb);
-    const u64 q = bar[p].q;
-    u64* a = data + (size_t)limb * n;
-    const u64* w = tw + (size_t)p * n;
-    const u64* wS = twS + (size_t)p * n;
+    const uint32_t rid = blockIdx.y;
+    const uint32_t pp = rid / G.R, ii = rid % G.R;
+    if (G.skipEll && ii >= G.alpha * pp && ii < min(G.alpha * (pp + 1), G.skipEll)) return;
+    const uint32_t prime = primeOf(G.pm, ii);
+    const u64 q = bar[prime].q;
+    const u64* w = tw + (size_t)prime * n;
+    const u64* wS = twS + (size_t)prime * n;
     NttTile T;
     T.logn = logn;
     T.d = COL ? logR : 8u;
@@ -318,39 +387,82 @@ __global__ __launch_bounds__(kThreads) void k_ntt(u64* __restrict__ data, sfp_li
     T.r0 = COL ? 0u : blockIdx.x * 16u;
     const uint32_t S0 = COL ? 0u : logR;
 
+    const u64* in = FIRST ? rowAt(G.src, pp, ii) : rowAt(G.dst, pp, ii);
+    u64* cp = nullptr;
+    if (FIRST && G.copy.base)
+        cp = G.copyByAlpha ? const_cast<u64*>(G.copy.base) + (ii / G.alpha) * G.copy.ps + ii * G.copy.is
+                           : rowAt(G.copy, pp, ii);
+    sf_barrett LB{};
+    u64 lsub = 0;
+    if (FIRST && G.lift) {
+        LB = loadBar(bar, prime);
+        lsub = G.liftSub[ii];
+    }
+    const u64 lhalf = (FIRST && G.lift) ? (bar[G.liftPrime].q >> 1) : 0;
+
     // global -> LDS, 16 B per lane; tile-linear word e is row-major (u, st)
 #pragma unroll
-    for (int k = 0; k < kTile / 2 / kThreads; ++k) {
-        const uint32_t e = 2 * (threadIdx.x + k * kThreads);
+    for (int k = 0; k < kTile / 2 / kNttThreads; ++k) {
+        const uint32_t e = 2 * (threadIdx.x + k * kNttThreads);
         const size_t g = COL ? (size_t)(e / T.C) * 256 + T.c0 + (e % T.C) : (size_t)T.r0 * 256 + e;
-        const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(a + g);
-        s[ldsPad(e)] = x.x;
-        s[ldsPad(e + 1)] = x.y;
+        ulonglong2 x = *reinterpret_cast<const ulonglong2*>(in + g);
+        if (FIRST) {
+            if (cp) *reinterpret_cast<ulonglong2*>(cp + g) = x;
+            if (G.lift) {
+                u64 r0 = sf_reduce128(x.x, 0, &LB), r1 = sf_reduce128(x.y, 0, &LB);
+                if (x.x > lhalf) r0 = sf_sub(r0, lsub, q);
+                if (x.y > lhalf) r1 = sf_sub(r1, lsub, q);
+                x.x = r0;
+                x.y = r1;
+            }
+        }
+        s[ldsSw(e)] = x.x;
+        s[ldsSw(e + 1)] = x.y;
     }
     __syncthreads();
-    // rounds of <= 4 stages: forward 4,4,..,rem ; inverse mirrored
-    const uint32_t nr = (T.d + 3) / 4;
+    const uint32_t nr = (T.d + kNttLogE - 1) / kNttLogE;
     for (uint32_t ri = 0; ri < nr; ++ri) {
         const uint32_t r = INV ? nr - 1 - ri : ri;
-        const uint32_t k0 = 4 * r;
-        const int b = (int)min(4u, T.d - k0);
+        const uint32_t k0 = kNttLogE * r;
+        const int b = (int)min((uint32_t)kNttLogE, T.d - k0);
         nttRoundDyn<INV, COL>(b, s, T, S0, k0, q, w, wS);
         __syncthreads();
     }
     const bool scale = INV && COL;
-    const u64 ni = scale ? ninv[p] : 0, niS = scale ? ninvS[p] : 0;
+    const u64 ni = scale ? ninv[prime] : 0, niS = scale ? ninvS[prime] : 0;
+    const bool epi = !FIRST && G.epi;
+    u64* out = epi ? rowAt(G.eout, pp, ii) : rowAt(G.dst, pp, ii);
+    const u64* ein = epi ? rowAt(G.ein, pp, ii) : nullptr;
+    const u64 ek = epi ? G.k[ii] : 0, ekS = epi ? G.kS[ii] : 0;
 #pragma unroll
-    for (int k = 0; k < kTile / 2 / kThreads; ++k) {
-        const uint32_t e = 2 * (threadIdx.x + k * kThreads);
+    for (int k = 0; k < kTile / 2 / kNttThreads; ++k) {
+        const uint32_t e = 2 * (threadIdx.x + k * kNttThreads);
         const size_t g = COL ? (size_t)(e / T.C) * 256 + T.c0 + (e % T.C) : (size_t)T.r0 * 256 + e;
         ulonglong2 x;
-        x.x = s[ldsPad(e)];
-        x.y = s[ldsPad(e + 1)];
-        if (scale) {
-            x.x = sf_mul_shoup(x.x, ni, niS, q);
-            x.y = sf_mul_shoup(x.y, ni, niS, q);
+        x.x = s[ldsSw(e)];
+        x.y = s[ldsSw(e + 1)];
+        if (!FIRST) {  // finish the lazy ranges: forward [0,4q), inverse [0,2q) -> [0,q)
+            if (scale) {
+                x.x = sf_mul_shoup_lazy(x.x, ni, niS, q);
+                x.y = sf_mul_shoup_lazy(x.y, ni, niS, q);
+            } else {
+                x.x = x.x >= 2 * q ? x.x - 2 * q : x.x;
+                x.y = x.y >= 2 * q ? x.y - 2 * q : x.y;
+            }
+            x.x = x.x >= q ? x.x - q : x.x;
+            x.y = x.y >= q ? x.y - q : x.y;
         }
-        *reinterpret_cast<ulonglong2*>(a + g) = x;
+        if (epi) {
+            const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(ein + g);
+            x.x = sf_mul_shoup(sf_sub(a.x, x.x, q), ek, ekS, q);
+            x.y = sf_mul_shoup(sf_sub(a.y, x.y, q), ek, ekS, q);
+            if ((G.addMask >> pp) & 1u) {
+                const ulonglong2 o = *reinterpret_cast<const ulonglong2*>(out + g);
+                x.x = sf_add(x.x, o.x, q);
+                x.y = sf_add(x.y, o.y, q);
+            }
+        }
+        *reinterpret_cast<ulonglong2*>(out + g) = x;
     }
 }
 
@@ -488,37 +600,8 @@ __global__ __launch_bounds__(kThreads) void k_automorph(u64* __restrict__ out, c
 // rescale helpers
 
 // rows[i][x] = centred(v[x]) mod q_i   for i < cnt  (v in [0, q_last))
-__global__ __launch_bounds__(kThreads) void k_bcast_centered(u64* __restrict__ rows, const u64* __restrict__ v,
-                                                             uint32_t cnt, u64 ql,
-                                                             const sf_barrett* __restrict__ bar,
-                                                             uint32_t logn) {
-    const size_t total = (size_t)cnt << logn;
-    const u64 half = ql >> 1;
-    for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < total;
-         i += (size_t)gridDim.x * kThreads) {
-        const uint32_t r = (uint32_t)(i >> logn);
-        const sf_barrett B = loadBar(bar, r);
-        const u64 x = v[i & ((1ull << logn) - 1)];
-        u64 y = sf_reduce128(x, 0, &B);
-        if (x > half) y = sf_sub(y, sf_reduce128(ql, 0, &B), B.q);
-        rows[i] = y;
-    }
-}
 
 // out_i = (in_i - t_i) * k_i
-__global__ __launch_bounds__(kThreads) void k_sub_mulc(u64* __restrict__ out, const u64* __restrict__ in,
-                                                       const u64* __restrict__ t, uint32_t cnt, ConstArgs k,
-                                                       const sf_barrett* __restrict__ bar, uint32_t logn,
-                                                       int add) {
-    const size_t total = (size_t)cnt << logn;
-    for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < total;
-         i += (size_t)gridDim.x * kThreads) {
-        const uint32_t r = (uint32_t)(i >> logn);
-        const sf_barrett B = loadBar(bar, r);
-        u64 v = bmul(sf_sub(in[i], t[i], B.q), k.k[r], B);
-        out[i] = add ? sf_add(out[i], v, B.q) : v;
-    }
-}
 
 // ============================================================================
 // fast base conversion (coefficient domain)
@@ -530,41 +613,59 @@ constexpr int kMaxConvSrc = 32;
 // centered != 0: each y_i is taken in (-s_i/2, s_i/2] (subtracting prod(S)
 // mod t once per y_i > s_i/2), which makes the ModDown conversion error
 // sum_i y_i/s_i zero-mean: a rounding, not a floor with a +K/2 bias.
-__global__ __launch_bounds__(kThreads) void k_conv(u64* __restrict__ out, const u64* __restrict__ src,
-                                                   const uint32_t* __restrict__ sidx,
-                                                   const uint32_t* __restrict__ didx,
-                                                   const u64* __restrict__ inv, const u64* __restrict__ mod,
-                                                   const u64* __restrict__ sprod,
-                                                   uint32_t ns, uint32_t nt, uint32_t ntUse,
-                                                   const sf_barrett* __restrict__ bar, uint32_t logn,
-                                                   uint32_t ell, uint32_t Lq, int centered) {
-    extern __shared__ u64 smod[];  // ns * nt
-    for (uint32_t e = threadIdx.x; e < ns * nt; e += kThreads) smod[e] = mod[e];
+// Fast base conversion of several jobs in one launch (grid: x = coefficient
+// blocks, y = job, z = chunk of kConvChunk targets).  For source rows s_i
+// (coefficient domain) and targets t:
+//   y_i = [s_i * inv_i]_{q_i};  out_t = sum_i y_i * mod[i][t]  mod p_t
+// centred: subtract prod(q_i) mod p_t once per y_i > q_i/2 (value in
+// (-Q/2, Q/2] instead of [0, Q)).
+constexpr int kConvChunk = 12;
+constexpr int kMaxConvJobs = 16;
+struct ConvJob {
+    const u64* src;
+    u64* dst;
+    const uint32_t *sidx, *didx, *drow;
+    const u64 *inv, *mod, *sprod;
+    uint32_t ns, nt, ntUse, centered;
+};
+struct ConvJobs {
+    ConvJob j[kMaxConvJobs];
+};
+
+__global__ __launch_bounds__(kThreads) void k_conv(const ConvJobs J, const sf_barrett* __restrict__ bar,
+                                                   uint32_t logn) {
+    __shared__ u64 smod[kMaxConvSrc * kConvChunk];
+    const ConvJob& c = J.j[blockIdx.y];
+    const uint32_t t0 = blockIdx.z * kConvChunk;
+    if (t0 >= c.ntUse) return;
+    const uint32_t tc = min((uint32_t)kConvChunk, c.ntUse - t0);
+    for (uint32_t e = threadIdx.x; e < c.ns * tc; e += kThreads) {
+        const uint32_t i = e / tc, t = e % tc;
+        smod[i * kConvChunk + t] = c.mod[(size_t)i * c.nt + t0 + t];
+    }
     __syncthreads();
     const uint32_t n = 1u << logn;
-    for (uint32_t x = blockIdx.x * kThreads + threadIdx.x; x < n; x += gridDim.x * kThreads) {
-        u64 y[kMaxConvSrc];
-        u64 neg = 0;
+    const uint32_t x = blockIdx.x * kThreads + threadIdx.x;
+    if (x >= n) return;
+    u64 y[kMaxConvSrc];
+    u64 neg = 0;
 #pragma unroll
-        for (int i = 0; i < kMaxConvSrc; ++i) {
-            if ((uint32_t)i < ns) {
-                const sf_barrett B = loadBar(bar, sidx[i]);
-                y[i] = bmul(src[((size_t)i << logn) + x], inv[i], B);
-                if (centered && y[i] > (B.q >> 1)) ++neg;
-            }
+    for (int i = 0; i < kMaxConvSrc; ++i) {
+        if ((uint32_t)i < c.ns) {
+            const sf_barrett B = loadBar(bar, c.sidx[i]);
+            y[i] = bmul(c.src[((size_t)i << logn) + x], c.inv[i], B);
+            if (c.centered && y[i] > (B.q >> 1)) ++neg;
         }
-        for (uint32_t t = 0; t < ntUse; ++t) {
-            Acc acc{0, 0};
+    }
+    for (uint32_t t = 0; t < tc; ++t) {
+        Acc acc{0, 0};
 #pragma unroll
-            for (int i = 0; i < kMaxConvSrc; ++i)
-                if ((uint32_t)i < ns) macc(acc, y[i], smod[i * nt + t]);
-            const uint32_t pt = didx[t];
-            const sf_barrett B = loadBar(bar, pt);
-            const uint32_t row = ell == 0xffffffffu ? t : (pt < Lq ? pt : ell + (pt - Lq));
-            u64 v = sf_reduce128_acc(acc.lo, acc.hi, &B);
-            if (neg) v = sf_sub(v, bmul(neg, sprod[t], B), B.q);
-            out[((size_t)row << logn) + x] = v;
-        }
+        for (int i = 0; i < kMaxConvSrc; ++i)
+            if ((uint32_t)i < c.ns) macc(acc, y[i], smod[i * kConvChunk + t]);
+        const sf_barrett B = loadBar(bar, c.didx[t0 + t]);
+        u64 v = sf_reduce128_acc(acc.lo, acc.hi, &B);
+        if (neg) v = sf_sub(v, bmul(neg, c.sprod[t0 + t], B), B.q);
+        c.dst[((size_t)c.drow[t0 + t] << logn) + x] = v;
     }
 }
 
@@ -831,16 +932,27 @@ const char* sfp_last_error(sfp_dev* d) {
 }
 
 // ---- NTT ----
-void sfp_ntt(sfp_dev* d, uint64_t* p, sfp_limbs m, int inverse) {
-    if (!m.count) return;
-    const uint32_t tiles = d->n / kTile;  // tiles per limb, both passes
-    const dim3 g(tiles, m.count);
-    const double bytes = 16.0 * m.count * d->n;
+static RowGroup rowsOf(uint32_t P, uint32_t R, sfp_limbs pm) {
+    RowGroup G;
+    std::memset(&G, 0, sizeof G);
+    G.P = P;
+    G.R = R;
+    G.pm = pm;
+    return G;
+}
+
+// Both passes of a (batched) NTT over the rows of G.
+static void nttRows(sfp_dev* d, const RowGroup& G, int inverse) {
+    const uint32_t rows = G.P * G.R;
+    if (!rows || !limbsOk(d, G.pm, "ntt")) return;
+    if (G.lift && G.liftPrime >= d->np) return (void)limbsOk(d, sfp_limbs{1, 1, G.liftPrime, G.liftPrime}, "ntt lift");
+    const dim3 g(d->n / kTile, rows);
+    const double bytes = 16.0 * rows * d->n;
     const u64* tw = inverse ? d->ipsi : d->psi;
     const u64* twS = inverse ? d->ipsiS : d->psiS;
     auto pass = [&](auto kern) {
         timedLaunch(d, SFP_FAM_NTT, bytes, [&] {
-            hipLaunchKernelGGL(kern, g, dim3(kThreads), 0, d->stream, p, m, d->bar, tw, twS, d->ninv,
+            hipLaunchKernelGGL(kern, g, dim3(kNttThreads), 0, d->stream, G, d->bar, tw, twS, d->ninv,
                                d->ninvS, d->logn);
         });
     };
@@ -852,6 +964,12 @@ void sfp_ntt(sfp_dev* d, uint64_t* p, sfp_limbs m, int inverse) {
         pass(k_ntt<true, true>);
     }
     checkLaunch(d, "ntt");
+}
+
+void sfp_ntt(sfp_dev* d, uint64_t* p, sfp_limbs m, int inverse) {
+    RowGroup G = rowsOf(1, m.count, m);
+    G.src = G.dst = RowPtr{p, 0, (long long)d->n};
+    nttRows(d, G, inverse);
 }
 
 void sfp_prof_set(sfp_dev* d, uint32_t fam, uint32_t period) {
@@ -878,7 +996,7 @@ int sfp_prof_read(sfp_dev* d, uint32_t fam, uint64_t* launches, uint64_t* timed,
 template <int OP>
 static void ew(sfp_dev* d, u64* out, const u64* a, const u64* b, const u64* c, sfp_limbs m,
                const u64* k) {
-    if (!m.count) return;
+    if (!m.count || !limbsOk(d, m, "elementwise")) return;
     ConstArgs ka;
     if (k) std::memcpy(ka.k, k, m.count * 8);
     const size_t pairs = ((size_t)m.count * d->n) / 2;
@@ -912,6 +1030,7 @@ void sfp_add_const(sfp_dev* d, uint64_t* out, const uint64_t* a, const uint64_t*
 
 void sfp_tensor(sfp_dev* d, uint64_t* d0, uint64_t* d1, uint64_t* d2, const uint64_t* a0,
                 const uint64_t* a1, const uint64_t* b0, const uint64_t* b1, sfp_limbs m) {
+    if (!limbsOk(d, m, "tensor")) return;
     const size_t total = (size_t)m.count * d->n;
     hipLaunchKernelGGL(k_tensor, dim3(ewGrid(total)), dim3(kThreads), 0, d->stream, d0, d1, d2, a0, a1,
                        b0, b1, m, d->bar, d->logn);
@@ -920,6 +1039,7 @@ void sfp_tensor(sfp_dev* d, uint64_t* d0, uint64_t* d1, uint64_t* d2, const uint
 
 void sfp_lin_wsum(sfp_dev* d, uint64_t* out, const uint64_t* const* ins, const uint64_t* k,
                   uint32_t nin, sfp_limbs m) {
+    if (!limbsOk(d, m, "lin_wsum")) return;
     if (nin > SFP_MAX_WSUM) {
         record(d, "lin_wsum", hipErrorInvalidValue);
         return;
@@ -935,6 +1055,7 @@ void sfp_lin_wsum(sfp_dev* d, uint64_t* out, const uint64_t* const* ins, const u
 
 void sfp_mac_plain(sfp_dev* d, uint64_t* out, const uint64_t* const* a, const uint64_t* const* b,
                    uint32_t nin, sfp_limbs m) {
+    if (!limbsOk(d, m, "mac_plain")) return;
     if (nin > SFP_MAX_WSUM) {
         record(d, "mac_plain", hipErrorInvalidValue);
         return;
@@ -990,32 +1111,45 @@ void sfp_rescale(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t ell, co
     sfp_rescale_ext(d, out, in, ell, ell - 1, qlinv, npoly, inStride, outStride);
 }
 
+// (in_p,i - lift(INTT(in_p,last))) * qlinv_i for both polys: INTT of the two
+// dropped rows, then one NTT launch pair that lifts them to every remaining
+// prime and applies the subtract-multiply in its last pass.
 void sfp_rescale_ext(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t ell, uint32_t dropPrime,
                      const uint64_t* qlinv, uint32_t npoly, size_t inStride, size_t outStride) {
     const uint32_t n = d->n;
     const uint32_t cnt = ell - 1;
-    u64* tmp = scratch(d, (size_t)(cnt + 1) * n);
-    u64* last = tmp + (size_t)cnt * n;
-    ConstArgs k;
-    std::memcpy(k.k, qlinv, cnt * 8);
-    const u64 ql = d->hbar[dropPrime].q;
-    for (uint32_t p = 0; p < npoly; ++p) {
-        const u64* src = in + p * inStride;
-        u64* dst = out + p * outStride;
-        devCopy(d, last, src + (size_t)cnt * n, (size_t)n * 8);
-        sfp_ntt(d, last, sfp_limbs{1, 0, dropPrime, 0}, 1);
-        hipLaunchKernelGGL(k_bcast_centered, dim3(ewGrid((size_t)cnt * n)), dim3(kThreads), 0, d->stream,
-                           tmp, last, cnt, ql, d->bar, d->logn);
-        sfp_ntt(d, tmp, sfp_limbs{cnt, cnt, 0, 0}, 0);
-        hipLaunchKernelGGL(k_sub_mulc, dim3(ewGrid((size_t)cnt * n)), dim3(kThreads), 0, d->stream, dst,
-                           src, tmp, cnt, k, d->bar, d->logn, 0);
-        checkLaunch(d, "rescale");
+    if (cnt > SFP_MAX_LIMBS) {
+        record(d, "rescale (too many limbs)", hipErrorInvalidValue);
+        return;
     }
+    u64* last = scratch(d, (size_t)npoly * n + (size_t)npoly * cnt * n);
+    u64* tmp = last + (size_t)npoly * n;
+    RowGroup A = rowsOf(npoly, 1, sfp_limbs{1, 0, dropPrime, 0});
+    A.src = RowPtr{in + (size_t)cnt * n, (long long)inStride, 0};
+    A.dst = RowPtr{last, (long long)n, 0};
+    nttRows(d, A, 1);
+    RowGroup B = rowsOf(npoly, cnt, sfp_limbs{cnt, cnt, 0, 0});
+    B.src = RowPtr{last, (long long)n, 0};
+    B.lift = 1;
+    B.liftPrime = dropPrime;
+    B.dst = RowPtr{tmp, (long long)cnt * n, (long long)n};
+    B.epi = 1;
+    B.ein = RowPtr{in, (long long)inStride, (long long)n};
+    B.eout = RowPtr{out, (long long)outStride, (long long)n};
+    const u64 ql = d->hbar[dropPrime].q;
+    for (uint32_t i = 0; i < cnt; ++i) {
+        const u64 q = d->hbar[i].q;
+        B.k[i] = qlinv[i];
+        B.kS[i] = sf_shoup_precomp(qlinv[i], q);
+        B.liftSub[i] = ql % q;
+    }
+    nttRows(d, B, 0);
 }
 
 // ---- base conversion / key switching ----
 sfp_conv* sfp_upload_conv(sfp_dev* d, uint32_t ns, const uint32_t* src, uint32_t nt,
-                          const uint32_t* dst, const uint64_t* inv, const uint64_t* mod) {
+                          const uint32_t* dst, const uint32_t* drow, const uint64_t* inv,
+                          const uint64_t* mod) {
     if (ns > (uint32_t)kMaxConvSrc) {
         record(d, "upload_conv (too many source primes)", hipErrorInvalidValue);
         return nullptr;
@@ -1029,6 +1163,10 @@ sfp_conv* sfp_upload_conv(sfp_dev* d, uint32_t ns, const uint32_t* src, uint32_t
     hipMalloc(&c->dst, nt * 4);
     hipMalloc(&c->inv, ns * 8);
     hipMalloc(&c->mod, (size_t)ns * nt * 8);
+    hipMalloc(&c->drow, nt * 4);
+    std::vector<uint32_t> rows(nt);
+    for (uint32_t t = 0; t < nt; ++t) rows[t] = drow ? drow[t] : t;
+    hostToDev(d, c->drow, rows.data(), nt * 4);
     hostToDev(d, c->src, src, ns * 4);
     hostToDev(d, c->dst, dst, nt * 4);
     hostToDev(d, c->inv, inv, ns * 8);
@@ -1053,34 +1191,76 @@ void sfp_free_conv(sfp_dev* d, sfp_conv* c) {
     hipFree(c->inv);
     hipFree(c->mod);
     hipFree(c->sprod);
+    hipFree(c->drow);
     delete c;
 }
 
-static void convLaunch(sfp_dev* d, u64* out, const u64* src, const sfp_conv* c, uint32_t ntUse,
-                       uint32_t ell, uint32_t Lq, int centered) {
-    const size_t lds = (size_t)c->ns * c->nt * 8;
-    timedLaunch(d, SFP_FAM_CONV, 8.0 * d->n * (c->ns + ntUse), [&] {
-        hipLaunchKernelGGL(k_conv, dim3(ewGrid(d->n)), dim3(kThreads), lds, d->stream, out, src, c->src,
-                           c->dst, c->inv, c->mod, c->sprod, c->ns, c->nt, ntUse, d->bar, d->logn, ell,
-                           Lq, centered);
+static ConvJob convJob(const sfp_conv* c, u64* dst, const u64* src, uint32_t ntUse, int centered) {
+    ConvJob j;
+    j.src = src;
+    j.dst = dst;
+    j.sidx = c->src;
+    j.didx = c->dst;
+    j.drow = c->drow;
+    j.inv = c->inv;
+    j.mod = c->mod;
+    j.sprod = c->sprod;
+    j.ns = c->ns;
+    j.nt = c->nt;
+    j.ntUse = ntUse;
+    j.centered = (uint32_t)centered;
+    return j;
+}
+
+static void convLaunch(sfp_dev* d, const ConvJobs& J, uint32_t njobs) {
+    if (!njobs) return;
+    uint32_t maxT = 0;
+    double bytes = 0;
+    for (uint32_t k = 0; k < njobs; ++k) {
+        maxT = std::max(maxT, J.j[k].ntUse);
+        bytes += 8.0 * d->n * (J.j[k].ns + J.j[k].ntUse);
+    }
+    const dim3 g(d->n / kThreads, njobs, (maxT + kConvChunk - 1) / kConvChunk);
+    timedLaunch(d, SFP_FAM_CONV, bytes, [&] {
+        hipLaunchKernelGGL(k_conv, g, dim3(kThreads), 0, d->stream, J, d->bar, d->logn);
     });
     checkLaunch(d, "conv");
 }
 
 void sfp_conv_apply(sfp_dev* d, uint64_t* dst, const uint64_t* src, const sfp_conv* c) {
-    convLaunch(d, dst, src, c, c->nt, 0xffffffffu, 0, 0);
+    ConvJobs J;
+    J.j[0] = convJob(c, dst, src, c->nt, 0);
+    convLaunch(d, J, 1);
 }
 
-void sfp_modup(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t ell, uint32_t K,
-               uint32_t Lq, uint32_t lo, uint32_t hi, const sfp_conv* c, uint64_t* scr) {
-    const uint32_t n = d->n, ns = hi - lo;
-    devCopy(d, scr, in + (size_t)lo * n, (size_t)ns * n * 8);
-    sfp_ntt(d, scr, sfp_limbs{ns, ns, 0, lo}, 1);
-    convLaunch(d, out, scr, c, c->nt, ell, Lq, 0);
-    // NTT every converted row: q rows [0, lo), q rows [hi, ell), then the K P rows
-    if (lo) sfp_ntt(d, out, sfp_limbs{lo, lo, 0, 0}, 0);
-    sfp_ntt(d, out + (size_t)hi * n, sfp_limbs{ell - hi + K, ell - hi, Lq, hi}, 0);
-    devCopy(d, out + (size_t)lo * n, in + (size_t)lo * n, (size_t)ns * n * 8);
+void sfp_modup(sfp_dev* d, uint64_t* ext, const uint64_t* in, uint32_t ell, uint32_t K,
+               uint32_t Lq, uint32_t alpha, const sfp_conv* const* convs, uint64_t* scr) {
+    const uint32_t n = d->n;
+    const uint32_t beta = (ell + alpha - 1) / alpha;
+    const long long stride = (long long)(ell + K) * n;
+    if (beta > (uint32_t)kMaxConvJobs || ell + K > SFP_MAX_LIMBS) {
+        record(d, "modup (too many digits / limbs)", hipErrorInvalidValue);
+        return;
+    }
+    // INTT of every input row; the raw rows go to their digit's ext block
+    RowGroup A = rowsOf(1, ell, sfp_limbs{ell, ell, 0, 0});
+    A.src = RowPtr{in, 0, (long long)n};
+    A.dst = RowPtr{scr, 0, (long long)n};
+    A.copy = RowPtr{ext, stride, (long long)n};
+    A.copyByAlpha = 1;
+    A.alpha = alpha;
+    nttRows(d, A, 1);
+    // every digit's conversion in one launch
+    ConvJobs J;
+    for (uint32_t j = 0; j < beta; ++j)
+        J.j[j] = convJob(convs[j], ext + j * stride, scr + (size_t)j * alpha * n, convs[j]->nt, 0);
+    convLaunch(d, J, beta);
+    // NTT of every converted row (digit-own rows skipped)
+    RowGroup B = rowsOf(beta, ell + K, sfp_limbs{ell + K, ell, Lq, 0});
+    B.src = B.dst = RowPtr{ext, stride, (long long)n};
+    B.skipEll = ell;
+    B.alpha = alpha;
+    nttRows(d, B, 0);
 }
 
 void sfp_ks_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
@@ -1095,22 +1275,38 @@ void sfp_ks_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ex
     checkLaunch(d, "ks_inner");
 }
 
-void sfp_moddown(sfp_dev* d, uint64_t* out, uint64_t* acc, uint32_t ell, uint32_t K, uint32_t Lq,
-                 const sfp_conv* c, const uint64_t* pinv, int add, uint64_t* scr) {
+void sfp_moddown2(sfp_dev* d, uint64_t* out0, uint64_t* out1, uint64_t* acc, size_t accStride,
+                  uint32_t ell, uint32_t K, uint32_t Lq, const sfp_conv* c, const uint64_t* pinv,
+                  int add0, int add1, uint64_t* scr) {
     const uint32_t n = d->n;
+    if (ell > SFP_MAX_LIMBS) {
+        record(d, "moddown (too many limbs)", hipErrorInvalidValue);
+        return;
+    }
     u64* pRows = acc + (size_t)ell * n;
-    sfp_ntt(d, pRows, sfp_limbs{K, 0, Lq, 0}, 1);
-    convLaunch(d, scr, pRows, c, ell, 0xffffffffu, Lq, 1);
-    sfp_ntt(d, scr, sfp_limbs{ell, ell, 0, 0}, 0);
-    ConstArgs k;
-    std::memcpy(k.k, pinv, ell * 8);
-    hipLaunchKernelGGL(k_sub_mulc, dim3(ewGrid((size_t)ell * n)), dim3(kThreads), 0, d->stream, out, acc,
-                       scr, ell, k, d->bar, d->logn, add);
-    checkLaunch(d, "moddown");
+    RowGroup A = rowsOf(2, K, sfp_limbs{K, 0, Lq, 0});
+    A.src = A.dst = RowPtr{pRows, (long long)accStride, (long long)n};
+    nttRows(d, A, 1);
+    ConvJobs J;
+    J.j[0] = convJob(c, scr, pRows, ell, 1);
+    J.j[1] = convJob(c, scr + (size_t)ell * n, pRows + accStride, ell, 1);
+    convLaunch(d, J, 2);
+    RowGroup B = rowsOf(2, ell, sfp_limbs{ell, ell, 0, 0});
+    B.src = B.dst = RowPtr{scr, (long long)ell * n, (long long)n};
+    B.epi = 1;
+    B.addMask = (add0 ? 1u : 0u) | (add1 ? 2u : 0u);
+    B.ein = RowPtr{acc, (long long)accStride, (long long)n};
+    B.eout = RowPtr{out0, (long long)(out1 - out0), (long long)n};
+    for (uint32_t i = 0; i < ell; ++i) {
+        B.k[i] = pinv[i];
+        B.kS[i] = sf_shoup_precomp(pinv[i], d->hbar[i].q);
+    }
+    nttRows(d, B, 0);
 }
 
 // ---- sampling ----
 void sfp_sample_uniform(sfp_dev* d, uint64_t* p, sfp_limbs m, uint64_t seed) {
+    if (!limbsOk(d, m, "uniform")) return;
     const size_t total = (size_t)m.count * d->n;
     hipLaunchKernelGGL(k_uniform, dim3(ewGrid(total)), dim3(kThreads), 0, d->stream, p, m, seed, d->bar,
                        d->logn);
@@ -1118,6 +1314,7 @@ void sfp_sample_uniform(sfp_dev* d, uint64_t* p, sfp_limbs m, uint64_t seed) {
 }
 
 void sfp_load_i64(sfp_dev* d, uint64_t* p, const int64_t* c, sfp_limbs m) {
+    if (!limbsOk(d, m, "load_i64")) return;
     // the bounce buffer is free once the stream has drained; the kernel
     // reads the coefficients straight from it
     SFP_CHECK(hipStreamSynchronize(d->stream));

@@ -126,21 +126,26 @@ void sfp_rescale_ext(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t ell
 
 // ---- basis conversion / key switching ----------------------------------------
 // Upload a conversion table: ns source primes (prime indices src_idx), nt
-// target primes (dst_idx); shat_inv[ns], shat_mod[ns][nt].
+// target primes (dst_idx) written to output rows dst_row[t] (NULL: row t);
+// shat_inv[ns], shat_mod[ns][nt].
 sfp_conv* sfp_upload_conv(sfp_dev* d, uint32_t ns, const uint32_t* src_idx, uint32_t nt,
-                          const uint32_t* dst_idx, const uint64_t* shat_inv,
-                          const uint64_t* shat_mod);
+                          const uint32_t* dst_idx, const uint32_t* dst_row,
+                          const uint64_t* shat_inv, const uint64_t* shat_mod);
 void sfp_free_conv(sfp_dev* d, sfp_conv* c);
-// Fast base conversion in the COEFFICIENT domain: src has ns rows, dst nt rows.
+// Fast base conversion in the COEFFICIENT domain: src has ns rows; target t
+// is written to dst row dst_row[t].
 void sfp_conv_apply(sfp_dev* d, uint64_t* dst, const uint64_t* src, const sfp_conv* c);
 
-// Hybrid key-switch ModUp for one digit (evaluation domain in and out).
+// Hybrid key-switch ModUp of every digit (evaluation domain in and out).
 //   in   : ell limbs (limb map identity), evaluation domain.
-//   out  : ell+K limbs (limb map split=ell, pbase=L+1).  Limbs of the digit
-//          [lo, hi) are copied; all others are Conv(INTT(in[lo,hi))) then NTT.
-//   scratch: at least (hi-lo) * n words.
-void sfp_modup(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t ell, uint32_t K,
-               uint32_t Lq, uint32_t lo, uint32_t hi, const sfp_conv* c, uint64_t* scratch);
+//   ext  : beta = ceil(ell/alpha) extended polys of ell+K rows each (stride
+//          (ell+K)*n; row t < ell is prime t, row ell+k is prime Lq+k).  Rows
+//          of digit j's own range [j*alpha, min((j+1)*alpha, ell)) are copies
+//          of `in`; all others are NTT(Conv_j(INTT(in[digit j]))), with
+//          convs[j] writing rows by its dst_row table.
+//   scratch: ell*n words.
+void sfp_modup(sfp_dev* d, uint64_t* ext, const uint64_t* in, uint32_t ell, uint32_t K,
+               uint32_t Lq, uint32_t alpha, const sfp_conv* const* convs, uint64_t* scratch);
 
 // Key inner product:  acc0 = sum_j ext_j * kb_j,  acc1 = sum_j ext_j * ka_j
 //   ext  : beta extended polys, each (ell+K) limbs, stride ext_stride.
@@ -150,13 +155,16 @@ void sfp_ks_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ex
                   size_t ext_stride, const uint64_t* key, uint32_t beta, uint32_t ell, uint32_t K,
                   uint32_t Lq);
 
-// ModDown:  out_i (+)= (acc_i - NTT(Conv_{P->Q}(INTT(acc_P)))_i) * pinv_i, with the
-//   P->Q conversion on centred residues (zero-mean rounding error).
-//   acc : ell+K limbs (split=ell, pbase=Lq), evaluation domain; destroyed.
-//   out : ell limbs.  If add != 0 the result is added into out.
-//   pinv: host array ell of P^{-1} mod q_i.  scratch: (ell+K)*n words.
-void sfp_moddown(sfp_dev* d, uint64_t* out, uint64_t* acc, uint32_t ell, uint32_t K, uint32_t Lq,
-                 const sfp_conv* c, const uint64_t* pinv, int add, uint64_t* scratch);
+// ModDown of both key-switch accumulators:
+//   out_p,i (+)= (acc_p,i - NTT(Conv_{P->Q}(INTT(acc_p,P)))_i) * pinv_i,
+//   with the P->Q conversion on centred residues (zero-mean rounding error).
+//   acc : two polys of ell+K rows (q rows then P rows, evaluation domain),
+//         acc_1 = acc + acc_stride; their P rows are destroyed.
+//   add0/add1: accumulate into out0/out1 instead of overwriting.
+//   pinv: host array ell of P^{-1} mod q_i.  scratch: 2*ell*n words.
+void sfp_moddown2(sfp_dev* d, uint64_t* out0, uint64_t* out1, uint64_t* acc, size_t acc_stride,
+                  uint32_t ell, uint32_t K, uint32_t Lq, const sfp_conv* c, const uint64_t* pinv,
+                  int add0, int add1, uint64_t* scratch);
 
 // ---- sampling (counter-based, deterministic) ------------------------------------
 // Uniform residues mod each limb's prime: value for (limb, i) is derived from

@@ -1,0 +1,103 @@
+// Prim-level microbenchmark of the HIP backend (links libsfhe.so).
+//   make -C tools microbench && tools/build/microbench [logn]
+// Times sfp_ntt (forward / inverse) over a range of limb counts, and the
+// fused key-switch / rescale prims at the metric context's top level.
+// Reports average wall time per call (stream-synchronised batches) and the
+// algorithmic bandwidth (prims.h byte model).
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "openfhe.h"
+#include "prims.h"
+#include "state.h"
+
+using namespace lbcrypto;
+
+template <class F>
+static double timeIt(sfp_dev* d, int iters, F&& f) {
+    f();
+    sfp_sync(d);
+    auto t0 = std::chrono::high_resolution_clock::now();
+    for (int i = 0; i < iters; ++i) f();
+    sfp_sync(d);
+    auto t1 = std::chrono::high_resolution_clock::now();
+    return std::chrono::duration<double, std::micro>(t1 - t0).count() / iters;
+}
+
+int main(int argc, char** argv) {
+    const int logn = argc > 1 ? std::atoi(argv[1]) : 16;
+    CCParams<CryptoContextCKKSRNS> p;
+    p.SetMultiplicativeDepth(34);
+    p.SetScalingModSize(40);
+    p.SetRingDim(1u << logn);
+    p.SetBatchSize(256);
+    p.SetSecurityLevel(HEStd_NotSet);
+    auto cc = GenCryptoContext(p);
+    SfheContextState* s = cc->state();
+    sfp_dev* d = s->dev;
+    const uint32_t n = s->n;
+    const size_t maxRows = 160;
+    auto* buf = (uint64_t*)sfp_alloc(d, maxRows * n * 8);
+    const uint32_t NP = s->Lq + s->K;  // valid prime indices: [0, NP)
+    for (size_t r0 = 0; r0 < maxRows; r0 += NP) {
+        const uint32_t c = (uint32_t)std::min<size_t>(NP, maxRows - r0);
+        sfp_sample_uniform(d, buf + r0 * n, sfp_limbs{c, c, 0, 0}, 7 + r0);
+    }
+    setvbuf(stdout, nullptr, _IONBF, 0);
+    std::printf("n=2^%d Lq=%u K=%u dnum=%u alpha=%u\n", logn, s->Lq, s->K, s->dnum, s->alpha);
+    std::printf("%-10s %6s %10s %10s %10s %10s\n", "op", "rows", "fwd us", "fwd GB/s", "inv us",
+                "inv GB/s");
+    for (uint32_t rows : {1u, 2u, 4u, 8u, 16u, 24u, 35u, 47u}) {
+        if (rows > NP) continue;
+        const sfp_limbs m{rows, rows, 0, 0};
+        const double f = timeIt(d, 50, [&] { sfp_ntt(d, buf, m, 0); });
+        const double i = timeIt(d, 50, [&] { sfp_ntt(d, buf, m, 1); });
+        const double bytes = 32.0 * rows * n;  // two passes x 16 B per coefficient
+        std::printf("%-10s %6u %10.2f %10.1f %10.2f %10.1f\n", "ntt", rows, f, bytes / f / 1e3, i,
+                    bytes / i / 1e3);
+    }
+    // key switch pieces at the top level (ell = Lq)
+    const uint32_t ell = s->Lq, K = s->K, beta = (ell + s->alpha - 1) / s->alpha;
+    const size_t stride = (size_t)(ell + K) * n;
+    auto* ext = (uint64_t*)sfp_alloc(d, stride * beta * 8);
+    auto* scr = (uint64_t*)sfp_alloc(d, (size_t)2 * ell * n * 8);
+    auto* acc = (uint64_t*)sfp_alloc(d, 2 * stride * 8);
+    auto* out = (uint64_t*)sfp_alloc(d, (size_t)2 * ell * n * 8);
+    sfp_sample_uniform(d, acc, sfp_limbs{ell + K, ell, s->Lq, 0}, 9);
+    sfp_sample_uniform(d, acc + stride, sfp_limbs{ell + K, ell, s->Lq, 0}, 10);
+    // conversion tables as the engine builds them
+    std::vector<sfp_conv*> convs;
+    {
+        auto ct = cc->Encrypt(cc->KeyGen().publicKey, cc->MakeCKKSPackedPlaintext(std::vector<double>(256, 0.5)));
+        cc->EvalMultKeyGen(cc->KeyGen().secretKey);
+        auto sq = cc->EvalMult(ct, ct);  // builds the modup tables of the top level
+        (void)sq;
+        convs = s->modupConv.at(ell);
+    }
+    const double mu = timeIt(d, 30, [&] {
+        sfp_modup(d, ext, buf, ell, K, s->Lq, s->alpha, convs.data(), scr);
+    });
+    const double ki = timeIt(d, 30, [&] {
+        sfp_ks_inner(d, acc, acc + stride, ext, stride, s->relinKey->ptr, beta, ell, K, s->Lq);
+    });
+    const double md = timeIt(d, 30, [&] {
+        sfp_moddown2(d, out, out + (size_t)ell * n, acc, stride, ell, K, s->Lq, s->moddownConv,
+                     s->pInvModQ.data(), 1, 1, scr);
+    });
+    const double rs = timeIt(d, 30, [&] {
+        sfp_rescale(d, out, buf, ell, s->qInvTable[ell].data(), 2, (size_t)ell * n, (size_t)(ell - 1) * n);
+    });
+    const double B = 8.0 * n;
+    std::printf("modup   ell=%u beta=%u: %8.2f us  (%.1f GB/s on ell + beta(ell+K) rows)\n", ell, beta,
+                mu, (ell + beta * (ell + K)) * B / mu / 1e3);
+    std::printf("ks_inner            : %8.2f us  (%.1f GB/s)\n", ki, (3.0 * beta + 2) * (ell + K) * B / ki / 1e3);
+    std::printf("moddown2            : %8.2f us  (%.1f GB/s on 2(ell+K) + 2 ell rows)\n", md,
+                (2.0 * (ell + K) + 2.0 * ell) * B / md / 1e3);
+    std::printf("rescale x2 polys    : %8.2f us  (%.1f GB/s on 4 ell rows)\n", rs, 4.0 * ell * B / rs / 1e3);
+    const char* e = sfp_last_error(d);
+    if (e) std::printf("ERROR: %s\n", e);
+    return e ? 1 : 0;
+}
