@@ -114,6 +114,17 @@ void sfp_d2h(sfp_dev* d, void* dst, const void* src, size_t b) { (void)d; memcpy
 void sfp_d2d(sfp_dev* d, void* dst, const void* src, size_t b) { (void)d; memmove(dst, src, b); }
 void sfp_zero(sfp_dev* d, void* dst, size_t b) { (void)d; memset(dst, 0, b); }
 void sfp_sync(sfp_dev* d) { (void)d; }
+/* one synchronous lane: everything is already ordered */
+struct sfp_event { int lane; };
+static struct sfp_event g_oracle_event = {0};
+int sfp_lanes(sfp_dev* d) { (void)d; return SFP_MAX_LANES; }
+void sfp_set_lane(sfp_dev* d, int lane) { (void)d; (void)lane; }
+int sfp_get_lane(sfp_dev* d) { (void)d; return 0; }
+sfp_event* sfp_event_record(sfp_dev* d) { (void)d; return &g_oracle_event; }
+void sfp_event_wait(sfp_dev* d, const sfp_event* e) { (void)d; (void)e; }
+int sfp_event_done(sfp_dev* d, const sfp_event* e) { (void)d; (void)e; return 1; }
+void sfp_event_free(sfp_dev* d, sfp_event* e) { (void)d; (void)e; }
+void sfp_lane_wait(sfp_dev* d, int waiter, int waitee) { (void)d; (void)waiter; (void)waitee; }
 /* kernel timing is a device-backend feature; the oracle reports nothing */
 void sfp_prof_set(sfp_dev* d, uint32_t fam, uint32_t period) { (void)d; (void)fam; (void)period; }
 int sfp_prof_read(sfp_dev* d, uint32_t fam, uint64_t* launches, uint64_t* timed, double* ms,

@@ -19,7 +19,10 @@
 #pragma once
 
 #include <algorithm>
+#include <map>
+#include <array>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cmath>
 #include <iostream>
@@ -101,6 +104,35 @@ inline const SizeParams* sizeParams(int N) {
 }  // namespace sfhe
 
 // ---------------------------------------------------------------------------
+namespace sfhe {
+// SFHE_PHASES=1: device-synchronised wall time of each sort phase on stderr
+// (diagnostics only; adds synchronisation, so never on in benchmarks).
+class PhaseTimer {
+  public:
+    explicit PhaseTimer(CryptoContext<DCRTPoly> cc) : m_cc(std::move(cc)) {
+        static const bool on = std::getenv("SFHE_PHASES") != nullptr;
+        m_on = on;
+        if (m_on) {
+            m_cc->Synchronize();
+            m_t = std::chrono::steady_clock::now();
+        }
+    }
+    void mark(const char* what) {
+        if (!m_on) return;
+        m_cc->Synchronize();
+        auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "PHASE %-28s %8.3f ms\n", what,
+                     std::chrono::duration<double, std::milli>(now - m_t).count());
+        m_t = now;
+    }
+
+  private:
+    CryptoContext<DCRTPoly> m_cc;
+    bool m_on = false;
+    std::chrono::steady_clock::time_point m_t;
+};
+}  // namespace sfhe
+
 template <int N>
 class SortBase {
   protected:
@@ -206,16 +238,22 @@ class DirectSort : public SortBase<N> {
 
     // shifted[pN + r] = x[(r + is*P + p) mod N]: baby steps pre_i = Rot(x, i),
     // giant steps j: Rot(sum_i pre_i * RotR(mask_{np j + i}, is*P + j np), is*P + j np)
+    // The 0/1 masks depend only on (N, layout, batch, giant step, level), so
+    // their Plaintexts (and with them the device encodings) are kept across
+    // sorts: repeated sorts skip mask generation, rotation and re-encoding.
+    std::map<std::array<int, 5>, std::vector<Plaintext>> m_masks;
+
     Ciphertext<DCRTPoly> vecRotsOpt(const std::vector<Ciphertext<DCRTPoly>>& pre,
                                     int num_partition, int num_slots, int np, int is) {
         std::vector<Ciphertext<DCRTPoly>> giants;
         for (int j = 0; j < num_partition / np; ++j) {
             const int shift = is * num_partition + j * np;
-            std::vector<Plaintext> masks;
-            for (int i = 0; i < np; ++i)
-                masks.push_back(m_cc->MakeCKKSPackedPlaintext(
-                    vectorRotate(generateMaskVector(num_slots, np * j + i), -shift), 1,
-                    pre[i]->GetLevel(), nullptr, num_slots));
+            auto& masks = m_masks[{0, is, j, (int)pre[0]->GetLevel(), num_slots}];
+            if (masks.empty())
+                for (int i = 0; i < np; ++i)
+                    masks.push_back(m_cc->MakeCKKSPackedPlaintext(
+                        vectorRotate(generateMaskVector(num_slots, np * j + i), -shift), 1,
+                        pre[i]->GetLevel(), nullptr, num_slots));
             auto T = m_cc->EvalMultAddPlain(pre, masks);
             T->SetSlots(num_slots);
             giants.push_back(rot.rotate(T, shift));
@@ -226,21 +264,33 @@ class DirectSort : public SortBase<N> {
     Ciphertext<DCRTPoly> constructRank(const Ciphertext<DCRTPoly>& input_array, SignFunc SignFunc,
                                        SignConfig& Cfg) {
         const sfhe::RankLayout L(N, max_batch);
+        sfhe::PhaseTimer ph(m_cc);
         std::vector<int> amounts(L.npRank);
         for (int i = 0; i < L.npRank; ++i) amounts[i] = i;
         auto pre = rot.rotateMany(input_array, amounts);
         for (auto& p : pre) p->SetSlots(L.S);
+        ph.mark("rank: baby rotations");
 
         auto rank = this->getZero()->Clone();
         rank->SetSlots(L.S);
+        // the batches are independent: each runs on its own lane (stream)
+        std::vector<Ciphertext<DCRTPoly>> parts(L.B);
+        const int lanes = std::min(L.B, m_cc->LaneCount());
+        m_cc->ForkLanes(lanes);
         for (int b = 0; b < L.B; ++b) {
+            m_cc->SetLane(b % lanes);
             auto shifted = vecRotsOpt(pre, L.P, L.S, L.npRank, b);
             auto dup = input_array->Clone();
             dup->SetSlots(L.S);
-            m_cc->EvalAddInPlace(rank, comp.compare(m_cc, dup, shifted, SignFunc, Cfg));
+            parts[b] = comp.compare(m_cc, dup, shifted, SignFunc, Cfg);
         }
+        m_cc->SetLane(0);
+        m_cc->JoinLanes();
+        for (int b = 0; b < L.B; ++b) m_cc->EvalAddInPlace(rank, parts[b]);
+        ph.mark("rank: batches (vecRotsOpt+compare)");
         // sum the P partitions (period N inside S slots)
         for (int s = L.S / 2; s >= N; s /= 2) m_cc->EvalAddInPlace(rank, rot.rotate(rank, s));
+        ph.mark("rank: folds");
         rank->SetSlots(N);
         // remove the self comparison step(0) = 1/2
         return m_cc->EvalSub(rank, 0.5);
@@ -251,11 +301,12 @@ class DirectSort : public SortBase<N> {
                                            int num_slots, int np, int ib, int num_partition) {
         std::vector<Ciphertext<DCRTPoly>> giants;
         for (int i = 0; i < (num_slots / N) / np; ++i) {
-            std::vector<Plaintext> masks;
-            for (int j = 0; j < np; ++j)
-                masks.push_back(m_cc->MakeCKKSPackedPlaintext(
-                    vectorRotate(generateMaskVectorN(num_slots, np * i + j), j), 1,
-                    masked_inputs[j]->GetLevel(), nullptr, num_slots));
+            auto& masks = m_masks[{1, 0, i, (int)masked_inputs[0]->GetLevel(), num_slots}];
+            if (masks.empty())
+                for (int j = 0; j < np; ++j)
+                    masks.push_back(m_cc->MakeCKKSPackedPlaintext(
+                        vectorRotate(generateMaskVectorN(num_slots, np * i + j), j), 1,
+                        masked_inputs[j]->GetLevel(), nullptr, num_slots));
             auto tmp = m_cc->EvalMultAddPlain(masked_inputs, masks);
             giants.push_back(rot.rotate(tmp, ib * num_partition + i * np));
         }
@@ -267,17 +318,28 @@ class DirectSort : public SortBase<N> {
     Ciphertext<DCRTPoly> rotationIndexCheckN(const Ciphertext<DCRTPoly>& ctx_Rank,
                                              const Ciphertext<DCRTPoly>& input_array) {
         const sfhe::RankLayout L(N, max_batch);
+        sfhe::PhaseTimer ph(m_cc);
         auto output = this->getZero()->Clone();
-        Plaintext idx =
-            m_cc->MakeCKKSPackedPlaintext(generateIndexVector(), 1, ctx_Rank->GetLevel(), nullptr, N);
+        auto& idxMemo = m_masks[{2, 0, 0, (int)ctx_Rank->GetLevel(), N}];
+        if (idxMemo.empty())
+            idxMemo.push_back(m_cc->MakeCKKSPackedPlaintext(generateIndexVector(), 1, ctx_Rank->GetLevel(),
+                                                            nullptr, N));
+        Plaintext idx = idxMemo[0];
         auto indexMinusRank = m_cc->EvalSub(idx, ctx_Rank);
         indexMinusRank->SetSlots(L.S);
         input_array->SetSlots(L.S);  // reference side effect (sort_algo.h:711)
 
         const auto& sincCoeffs = selectDoubledSincCoefficients<N>();
+        std::vector<Ciphertext<DCRTPoly>> parts(L.B);
+        const int lanes = std::min(L.B, m_cc->LaneCount());
+        m_cc->ForkLanes(lanes);
         for (int b = 0; b < L.B; ++b) {
-            Plaintext chk = m_cc->MakeCKKSPackedPlaintext(
-                generateCheckingVectorN(L.S, b * L.P), 1, indexMinusRank->GetLevel(), nullptr, L.S);
+            m_cc->SetLane(b % lanes);
+            auto& chkMemo = m_masks[{3, b, 0, (int)indexMinusRank->GetLevel(), L.S}];
+            if (chkMemo.empty())
+                chkMemo.push_back(m_cc->MakeCKKSPackedPlaintext(generateCheckingVectorN(L.S, b * L.P), 1,
+                                                                indexMinusRank->GetLevel(), nullptr, L.S));
+            Plaintext chk = chkMemo[0];
             // (r - rank_r - c) / 2N  in (-1, 1/2)
             auto z = m_cc->EvalMult(m_cc->EvalSub(indexMinusRank, chk), 1.0 / N / 2);
             auto hit = m_cc->EvalChebyshevSeriesPS(z, sincCoeffs, -1, 1);
@@ -285,9 +347,14 @@ class DirectSort : public SortBase<N> {
             std::vector<int> amounts(L.npPlace);
             for (int i = 0; i < L.npPlace; ++i) amounts[i] = i;
             auto maskedRot = rot.rotateMany(masked, amounts);
-            m_cc->EvalAddInPlace(output, blindRotationOptN(maskedRot, L.S, L.npPlace, b, L.P));
+            parts[b] = blindRotationOptN(maskedRot, L.S, L.npPlace, b, L.P);
         }
+        m_cc->SetLane(0);
+        m_cc->JoinLanes();
+        for (int b = 0; b < L.B; ++b) m_cc->EvalAddInPlace(output, parts[b]);
+        ph.mark("place: batches (sinc PS+mask+blind rotation)");
         for (int s = L.S / 2; s >= N; s /= 2) m_cc->EvalAddInPlace(output, rot.rotate(output, s));
+        ph.mark("place: folds");
         output->SetSlots(N);
         return output;
     }

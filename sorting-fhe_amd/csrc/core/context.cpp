@@ -143,17 +143,24 @@ u64 residueOf(double x, u64 q) {
 // device buffers
 
 DeviceBuffer::~DeviceBuffer() {
+    if (ready) sfp_event_free(st->dev, ready);
     if (!ptr) return;
     std::lock_guard<std::mutex> g(st->poolMu);
-    st->freeList[words].push_back(ptr);
+    if (!st->forkedLanes)
+        st->freeList[0][words].push_back(ptr);  // everything is ordered behind lane 0 again
+    else if (region == st->region && lane == st->lane)
+        st->freeList[lane][words].push_back(ptr);  // private to this lane in this region
+    else
+        st->deferredFree.push_back({words, ptr});  // another lane may still use it: after the join
 }
 
 DeviceBufferPtr SfheContextState::alloc(size_t words) {
     uint64_t* p = nullptr;
     {
         std::lock_guard<std::mutex> g(poolMu);
-        auto it = freeList.find(words);
-        if (it != freeList.end() && !it->second.empty()) {
+        auto& fl = freeList[lane];
+        auto it = fl.find(words);
+        if (it != fl.end() && !it->second.empty()) {
             p = it->second.back();
             it->second.pop_back();
         }
@@ -168,18 +175,20 @@ DeviceBufferPtr SfheContextState::alloc(size_t words) {
         }
         poolBytes += words * 8;
     }
-    return std::make_shared<DeviceBuffer>(this, p, words);
+    return std::make_shared<DeviceBuffer>(this, p, words, lane, forkedLanes ? region : 0);
 }
 
 void SfheContextState::releaseAll() {
     std::lock_guard<std::mutex> g(poolMu);
     sfp_sync(dev);
-    for (auto& kv : freeList)
-        for (auto* p : kv.second) {
-            sfp_free(dev, p);
-            poolBytes -= kv.first * 8;
-        }
-    freeList.clear();
+    for (auto& fl : freeList) {
+        for (auto& kv : fl)
+            for (auto* p : kv.second) {
+                sfp_free(dev, p);
+                poolBytes -= kv.first * 8;
+            }
+        fl.clear();
+    }
 }
 
 // ============================================================================
@@ -393,11 +402,25 @@ class SfheInternal {
     }
 
     // device encoding of a plaintext at `level` with scale Delta_level
+    // An encoding produced on another lane that may still be in flight is
+    // waited for (device-side) before use.
+    static const uint64_t* ready(SfheContextState* s, DeviceBuffer* b) {
+        if (b->ready) {
+            if (sfp_event_done(s->dev, b->ready)) {
+                sfp_event_free(s->dev, b->ready);
+                b->ready = nullptr;
+            } else {
+                sfp_event_wait(s->dev, b->ready);
+            }
+        }
+        return b->ptr;
+    }
+
     static const uint64_t* encoded(CC* cc, const Plaintext& pt, uint32_t level) {
         SfheContextState* s = cc->st.get();
         std::lock_guard<std::mutex> g(pt->encMutex);
         auto it = pt->encoded.find(level);
-        if (it != pt->encoded.end()) return it->second->ptr;
+        if (it != pt->encoded.end()) return ready(s, it->second.get());
         uint32_t ell = s->ellOf(level);
         // context-level cache: identical (values, slots, level) encode identically
         uint64_t h = 1469598103934665603ull;
@@ -419,7 +442,7 @@ class SfheInternal {
                 for (auto& e : ci->second)
                     if (e.slots == pt->slots && e.values == pt->values) {
                         pt->encoded[level] = e.buf;
-                        return e.buf->ptr;
+                        return ready(s, e.buf.get());
                     }
         }
         std::vector<int64_t> coeffs;
@@ -437,6 +460,7 @@ class SfheInternal {
                          level, (unsigned long long)f, (unsigned long long)g);
         }
         sfp_ntt(s->dev, buf->ptr, Q(ell), 0);
+        buf->ready = sfp_event_record(s->dev);
         pt->encoded[level] = buf;
         if (s->ptCacheOn && s->ptCacheBytes + (size_t)ell * s->n * 8 <= s->ptCacheLimit) {
             s->ptCache[h].push_back(PtCacheEntry{pt->values, pt->slots, buf});
@@ -668,6 +692,48 @@ void CryptoContextImpl<DCRTPoly>::Synchronize() {
     sfp_sync(st->dev);
     const char* e = sfp_last_error(st->dev);
     if (e) SFHE_THROW(std::string("device error: ") + e);
+}
+
+int CryptoContextImpl<DCRTPoly>::LaneCount() const { return sfp_lanes(st->dev); }
+
+void CryptoContextImpl<DCRTPoly>::ForkLanes(int count) {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheContextState* s = st.get();
+    if (s->forkedLanes) SFHE_THROW("ForkLanes: a lane region is already open");
+    count = std::max(1, std::min(count, sfp_lanes(s->dev)));
+    sfp_set_lane(s->dev, 0);
+    s->lane = 0;
+    for (int i = 1; i < count; ++i) sfp_lane_wait(s->dev, i, 0);
+    s->forkedLanes = count;
+    s->region = ++s->regionCount;
+}
+
+void CryptoContextImpl<DCRTPoly>::SetLane(int lane) {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheContextState* s = st.get();
+    if (lane != 0 && (!s->forkedLanes || lane >= s->forkedLanes))
+        SFHE_THROW("SetLane: lane " + std::to_string(lane) + " outside the open region");
+    s->lane = lane;
+    sfp_set_lane(s->dev, lane);
+}
+
+void CryptoContextImpl<DCRTPoly>::JoinLanes() {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheContextState* s = st.get();
+    if (!s->forkedLanes) return;
+    for (int i = 1; i < s->forkedLanes; ++i) sfp_lane_wait(s->dev, 0, i);
+    sfp_set_lane(s->dev, 0);
+    std::lock_guard<std::mutex> pg(s->poolMu);
+    for (int i = 1; i < s->forkedLanes; ++i) {
+        for (auto& kv : s->freeList[i])
+            for (auto* p : kv.second) s->freeList[0][kv.first].push_back(p);
+        s->freeList[i].clear();
+    }
+    for (auto& e : s->deferredFree) s->freeList[0][e.first].push_back(e.second);
+    s->deferredFree.clear();
+    s->lane = 0;
+    s->forkedLanes = 0;
+    s->region = 0;
 }
 
 void CryptoContextImpl<DCRTPoly>::SetPlaintextCache(bool on) {

@@ -363,6 +363,15 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
                                            uint32_t slots);
     // Wait for all device work; throws on an asynchronous device error.
     void Synchronize();
+    // Engine extension: independent work on concurrent lanes (HIP streams).
+    // ForkLanes(k) orders lanes 1..k-1 after everything issued so far on lane
+    // 0; SetLane(i) routes the following operations to lane i; JoinLanes()
+    // orders lane 0 after all of them.  Objects created on a lane may be
+    // read on other lanes only after the join.
+    int LaneCount() const;
+    void ForkLanes(int count);
+    void SetLane(int lane);
+    void JoinLanes();
     // Plaintext-encoding cache across calls (default on); see DESIGN.md.
     void SetPlaintextCache(bool on);
     // Operation counters (for the roofline byte model).

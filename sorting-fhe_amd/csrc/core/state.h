@@ -15,11 +15,15 @@ namespace lbcrypto {
 
 class DeviceBuffer {
   public:
-    DeviceBuffer(SfheContextState* s, uint64_t* p, size_t w) : st(s), ptr(p), words(w) {}
+    DeviceBuffer(SfheContextState* s, uint64_t* p, size_t w, int l, uint64_t r)
+        : st(s), ptr(p), words(w), lane(l), region(r) {}
     ~DeviceBuffer();
     SfheContextState* st;
     uint64_t* ptr;
     size_t words;
+    int lane;                      // lane that allocated it
+    uint64_t region;               // fork/join region it was allocated in (0: none)
+    sfp_event* ready = nullptr;    // shared encodings: end of the producing work
 };
 
 struct PtCacheEntry {
@@ -62,7 +66,14 @@ struct SfheContextState {
 
     // memory pool (device words -> free list)
     std::mutex poolMu;
-    std::map<size_t, std::vector<uint64_t*>> freeList;
+    // free lists per lane: a block freed on one lane is reused only by work
+    // ordered after it (same lane, or any lane after a join)
+    std::map<size_t, std::vector<uint64_t*>> freeList[SFP_MAX_LANES];
+    std::vector<std::pair<size_t, uint64_t*>> deferredFree;  // cross-lane frees inside a region
+    int lane = 0;          // lane new work goes to
+    int forkedLanes = 0;   // > 0 while a fork/join region is open
+    uint64_t region = 0;   // id of the open region (0: none)
+    uint64_t regionCount = 0;
     size_t poolBytes = 0;
 
     // serialises host-side use of the device from OpenMP callers

@@ -21,6 +21,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <unordered_map>
 #include <string>
 #include <vector>
 
@@ -74,9 +75,18 @@ __device__ __forceinline__ void macc(Acc& a, u64 x, u64 y) {
 
 }  // namespace
 
+struct sfp_event {
+    hipEvent_t e = nullptr;
+    int lane = 0;
+};
+
 struct sfp_dev {
     int device = 0;
-    hipStream_t stream = nullptr;
+    // lanes: independent in-order streams; every launch goes to streams[cur]
+    hipStream_t streams[SFP_MAX_LANES] = {};
+    int nLanes = 1, cur = 0;
+    hipStream_t st() const { return streams[cur]; }
+    std::vector<sfp_event*> evFree;
     uint32_t n = 0, logn = 0, np = 0;
     sf_barrett* bar = nullptr;  // device [np]
     u64 *psi = nullptr, *psiS = nullptr, *ipsi = nullptr, *ipsiS = nullptr;
@@ -98,6 +108,11 @@ struct sfp_dev {
         std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
     } prof[SFP_FAM_COUNT];
     std::vector<hipEvent_t> evPool;
+    // content-addressed device copies of small constant arrays (kernel
+    // argument tables): bump-allocated in one buffer
+    u64* cpool = nullptr;
+    size_t cpoolCap = 0, cpoolOff = 0;
+    std::unordered_map<uint64_t, std::vector<std::pair<std::vector<u64>, size_t>>> cmap;
     std::mutex mu;
     std::string err;
 };
@@ -118,6 +133,14 @@ static void record(sfp_dev* d, const char* what, hipError_t e) {
     if (d->err.empty()) d->err = std::string(what) + ": " + hipGetErrorString(e);
 }
 
+// Drain every lane (shared host-visible resources: ring, bounce, constant pool).
+static void syncAll(sfp_dev* d) {
+    for (int i = 0; i < d->nLanes; ++i) {
+        hipError_t e = hipStreamSynchronize(d->streams[i]);
+        if (e != hipSuccess) record(d, "synchronize", e);
+    }
+}
+
 static bool debugSync() {
     static const bool on = [] {
         const char* v = std::getenv("SFHE_DEBUG_SYNC");
@@ -130,7 +153,7 @@ static void checkLaunch(sfp_dev* d, const char* k) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) record(d, k, e);
     if (debugSync()) {
-        e = hipStreamSynchronize(d->stream);
+        e = hipStreamSynchronize(d->st());
         if (e != hipSuccess) record(d, k, e);
     }
 }
@@ -173,7 +196,7 @@ static void profFlush(sfp_dev* d, sfp_dev::ProfFam& f) {
     f.pending.clear();
 }
 
-// Run `launch` (one kernel launch on d->stream); bracket it with events when
+// Run `launch` (one kernel launch on d->st()); bracket it with events when
 // this family is being timed and this launch is a sampled one.
 template <class F>
 static void timedLaunch(sfp_dev* d, uint32_t fam, double bytes, F&& launch) {
@@ -183,9 +206,9 @@ static void timedLaunch(sfp_dev* d, uint32_t fam, double bytes, F&& launch) {
         return;
     }
     hipEvent_t a = takeEvent(d), b = takeEvent(d);
-    SFP_CHECK(hipEventRecord(a, d->stream));
+    SFP_CHECK(hipEventRecord(a, d->st()));
     launch();
-    SFP_CHECK(hipEventRecord(b, d->stream));
+    SFP_CHECK(hipEventRecord(b, d->st()));
     f.pending.push_back({a, b});
     f.timed++;
     f.bytes += bytes;
@@ -215,12 +238,20 @@ static unsigned gridFor(size_t work, unsigned perBlock) {
 // finishes the transform reduces to [0, q).  The inverse runs the
 // Gentleman-Sande stages in reverse order (ROW pass first) and folds n^-1
 // into the COL pass's store.
+#ifndef SFHE_NTT_EXP
+#define SFHE_NTT_EXP 0  // experiments only: 1 no butterflies, 2 no twiddle loads, 3 no rounds
+#endif
 #ifndef SFHE_NTT_LOGE
 #define SFHE_NTT_LOGE 3
 #endif
 constexpr int kNttLogE = SFHE_NTT_LOGE;         // stages per register round
 constexpr int kNttE = 1 << kNttLogE;            // words per thread per round
-constexpr int kNttThreads = kTile / kNttE;      // threads per 4096-word tile
+#ifndef SFHE_NTT_TILE
+#define SFHE_NTT_TILE 4096
+#endif
+constexpr int kNttTile = SFHE_NTT_TILE;         // words per tile (one block)
+constexpr int kNttRows = kNttTile / 256;        // ROW pass: whole rows per tile
+constexpr int kNttThreads = kNttTile / kNttE;   // threads per tile
 
 __device__ __forceinline__ uint32_t ldsSw(uint32_t e) {
     const uint32_t x = e >> 5;
@@ -229,7 +260,7 @@ __device__ __forceinline__ uint32_t ldsSw(uint32_t e) {
 
 struct NttTile {
     uint32_t logn, d;     // d = stages in this pass (logR or 8)
-    uint32_t C;           // COL: columns per tile
+    uint32_t C, logC;     // COL: columns per tile (a power of two)
     uint32_t c0, r0;      // COL: first column; ROW: first row
 };
 
@@ -251,22 +282,22 @@ __device__ __forceinline__ void nttRound(u64* s, const NttTile& T, uint32_t S0, 
     constexpr int M = 1 << B;
     constexpr int GPT = kNttE / M;  // groups per thread
     const uint32_t D = 1u << T.d;
-    const uint32_t h = D >> (k0 + B);     // smallest stride of the round (in u)
+    const uint32_t logh = T.d - k0 - B;
+    const uint32_t h = 1u << logh;        // smallest stride of the round (in u)
     const uint32_t span = D >> k0;        // hi step
-    const uint32_t nsub = COL ? T.C : 16u;
     const u64 q2 = 2 * q;
 #pragma unroll
     for (int gi = 0; gi < GPT; ++gi) {
         const uint32_t gid = threadIdx.x + gi * kNttThreads;
         uint32_t st, lo, hi;
-        if (COL) {
-            st = gid % nsub;
-            const uint32_t rest = gid / nsub;
-            lo = rest % h;
-            hi = rest / h;
+        if (COL) {  // every extent is a power of two: shifts and masks only
+            st = gid & (T.C - 1);
+            const uint32_t rest = gid >> T.logC;
+            lo = rest & (h - 1);
+            hi = rest >> logh;
         } else {
-            lo = gid % h;
-            const uint32_t rest = gid / h;
+            lo = gid & (h - 1);
+            const uint32_t rest = gid >> logh;
             hi = rest & ((1u << k0) - 1);
             st = rest >> k0;
         }
@@ -282,13 +313,22 @@ __device__ __forceinline__ void nttRound(u64* s, const NttTile& T, uint32_t S0, 
             const uint32_t tb = (1u << S) + (x0 >> (T.logn - S));
 #pragma unroll
             for (int qd = 0; qd < (1 << t); ++qd) {
+#if SFHE_NTT_EXP >= 2
+                W[(1 << t) - 1 + qd] = tb + qd;
+                WS[(1 << t) - 1 + qd] = tb;
+#else
                 W[(1 << t) - 1 + qd] = w[tb + qd];
                 WS[(1 << t) - 1 + qd] = wS[tb + qd];
+#endif
             }
         }
         u64 v[M];
 #pragma unroll
         for (int j = 0; j < M; ++j) v[j] = s[ldsSw(nttLocal<COL>(T, st, ub + j * h))];
+#if SFHE_NTT_EXP >= 1
+        v[0] ^= W[0] ^ WS[0];
+        if (false)
+#endif
         if (!INV) {
             // Harvey CT butterfly: in [0,4q) -> out [0,4q)
 #pragma unroll
@@ -355,8 +395,9 @@ struct RowGroup {
     uint32_t skipEll;      // >0: skip rows alpha*p <= i < min(alpha*(p+1), skipEll) (ModUp own digit)
     uint32_t lift, liftPrime;
     uint32_t epi, addMask;  // addMask bit p: accumulate into eout for polynomial p
-    u64 k[SFP_MAX_LIMBS], kS[SFP_MAX_LIMBS];  // epilogue constant per i (value, Shoup)
-    u64 liftSub[SFP_MAX_LIMBS];               // q_liftPrime mod q_i
+    // device arrays (constant cache): epilogue constant per i (value, Shoup)
+    // and q_liftPrime mod q_i -- pointers keep the kernel arguments small
+    const u64 *k, *kS, *liftSub;
 };
 
 __device__ __forceinline__ u64* rowAt(const RowPtr& r, uint32_t p, uint32_t i) {
@@ -368,7 +409,7 @@ __global__ __launch_bounds__(kNttThreads) void k_ntt(const RowGroup G, const sf_
                                                   const u64* __restrict__ tw, const u64* __restrict__ twS,
                                                   const u64* __restrict__ ninv,
                                                   const u64* __restrict__ ninvS, uint32_t logn) {
-    __shared__ u64 s[kTile];
+    __shared__ u64 s[kNttTile];
     constexpr bool FIRST = (COL != INV);  // forward: COL first; inverse: ROW first
     const uint32_t n = 1u << logn;
     const uint32_t logR = logn - 8;
@@ -382,9 +423,10 @@ __global__ __launch_bounds__(kNttThreads) void k_ntt(const RowGroup G, const sf_
     NttTile T;
     T.logn = logn;
     T.d = COL ? logR : 8u;
-    T.C = COL ? (kTile >> logR) : 0u;
+    T.logC = COL ? (uint32_t)__builtin_ctz(kNttTile) - logR : 0u;
+    T.C = 1u << T.logC;
     T.c0 = COL ? blockIdx.x * T.C : 0u;
-    T.r0 = COL ? 0u : blockIdx.x * 16u;
+    T.r0 = COL ? 0u : blockIdx.x * kNttRows;
     const uint32_t S0 = COL ? 0u : logR;
 
     const u64* in = FIRST ? rowAt(G.src, pp, ii) : rowAt(G.dst, pp, ii);
@@ -402,9 +444,9 @@ __global__ __launch_bounds__(kNttThreads) void k_ntt(const RowGroup G, const sf_
 
     // global -> LDS, 16 B per lane; tile-linear word e is row-major (u, st)
 #pragma unroll
-    for (int k = 0; k < kTile / 2 / kNttThreads; ++k) {
+    for (int k = 0; k < kNttTile / 2 / kNttThreads; ++k) {
         const uint32_t e = 2 * (threadIdx.x + k * kNttThreads);
-        const size_t g = COL ? (size_t)(e / T.C) * 256 + T.c0 + (e % T.C) : (size_t)T.r0 * 256 + e;
+        const size_t g = COL ? (size_t)(e >> T.logC) * 256 + T.c0 + (e & (T.C - 1)) : (size_t)T.r0 * 256 + e;
         ulonglong2 x = *reinterpret_cast<const ulonglong2*>(in + g);
         if (FIRST) {
             if (cp) *reinterpret_cast<ulonglong2*>(cp + g) = x;
@@ -420,7 +462,11 @@ __global__ __launch_bounds__(kNttThreads) void k_ntt(const RowGroup G, const sf_
         s[ldsSw(e + 1)] = x.y;
     }
     __syncthreads();
+#if SFHE_NTT_EXP >= 3
+    const uint32_t nr = 0;
+#else
     const uint32_t nr = (T.d + kNttLogE - 1) / kNttLogE;
+#endif
     for (uint32_t ri = 0; ri < nr; ++ri) {
         const uint32_t r = INV ? nr - 1 - ri : ri;
         const uint32_t k0 = kNttLogE * r;
@@ -435,9 +481,9 @@ __global__ __launch_bounds__(kNttThreads) void k_ntt(const RowGroup G, const sf_
     const u64* ein = epi ? rowAt(G.ein, pp, ii) : nullptr;
     const u64 ek = epi ? G.k[ii] : 0, ekS = epi ? G.kS[ii] : 0;
 #pragma unroll
-    for (int k = 0; k < kTile / 2 / kNttThreads; ++k) {
+    for (int k = 0; k < kNttTile / 2 / kNttThreads; ++k) {
         const uint32_t e = 2 * (threadIdx.x + k * kNttThreads);
-        const size_t g = COL ? (size_t)(e / T.C) * 256 + T.c0 + (e % T.C) : (size_t)T.r0 * 256 + e;
+        const size_t g = COL ? (size_t)(e >> T.logC) * 256 + T.c0 + (e & (T.C - 1)) : (size_t)T.r0 * 256 + e;
         ulonglong2 x;
         x.x = s[ldsSw(e)];
         x.y = s[ldsSw(e + 1)];
@@ -776,10 +822,10 @@ static void devCopy(sfp_dev* d, void* dst, const void* src, size_t b) {
     if (!b) return;
     if ((((uintptr_t)dst | (uintptr_t)src | b) & 15) == 0) {
         const size_t cnt = b / 16;
-        hipLaunchKernelGGL(k_copy16, dim3(ewGrid(cnt)), dim3(kThreads), 0, d->stream, (ulonglong2*)dst,
+        hipLaunchKernelGGL(k_copy16, dim3(ewGrid(cnt)), dim3(kThreads), 0, d->st(), (ulonglong2*)dst,
                            (const ulonglong2*)src, cnt);
     } else {
-        hipLaunchKernelGGL(k_copy1, dim3(ewGrid(b)), dim3(kThreads), 0, d->stream, (unsigned char*)dst,
+        hipLaunchKernelGGL(k_copy1, dim3(ewGrid(b)), dim3(kThreads), 0, d->st(), (unsigned char*)dst,
                            (const unsigned char*)src, b);
     }
     checkLaunch(d, "copy");
@@ -788,10 +834,10 @@ static void devCopy(sfp_dev* d, void* dst, const void* src, size_t b) {
 static void devZero(sfp_dev* d, void* dst, size_t b) {
     if (!b) return;
     if ((((uintptr_t)dst | b) & 15) == 0) {
-        hipLaunchKernelGGL(k_fill16, dim3(ewGrid(b / 16)), dim3(kThreads), 0, d->stream, (ulonglong2*)dst,
+        hipLaunchKernelGGL(k_fill16, dim3(ewGrid(b / 16)), dim3(kThreads), 0, d->st(), (ulonglong2*)dst,
                            b / 16);
     } else {
-        hipLaunchKernelGGL(k_fill1, dim3(ewGrid(b)), dim3(kThreads), 0, d->stream, (unsigned char*)dst, b);
+        hipLaunchKernelGGL(k_fill1, dim3(ewGrid(b)), dim3(kThreads), 0, d->st(), (unsigned char*)dst, b);
     }
     checkLaunch(d, "zero");
 }
@@ -802,7 +848,7 @@ static void devZero(sfp_dev* d, void* dst, size_t b) {
 static void* ringPut(sfp_dev* d, const void* src, size_t bytes) {
     bytes = (bytes + 255) & ~(size_t)255;
     if (d->ringOff + bytes > d->ringCap) {
-        hipStreamSynchronize(d->stream);
+        syncAll(d);
         d->ringOff = 0;
     }
     char* h = d->hring + d->ringOff;
@@ -815,22 +861,48 @@ static void* ringPut(sfp_dev* d, const void* src, size_t bytes) {
 
 // Bulk host -> device through the bounce buffer, chunk by chunk.
 static void hostToDev(sfp_dev* d, void* dst, const void* src, size_t b) {
-    SFP_CHECK(hipStreamSynchronize(d->stream));
+    syncAll(d);  // the bounce buffer is shared by every lane
     for (size_t off = 0; off < b; off += d->bounceCap) {
         const size_t c = b - off < d->bounceCap ? b - off : d->bounceCap;
         std::memcpy(d->bounce, (const char*)src + off, c);
         devCopy(d, (char*)dst + off, d->bounce, c);
-        SFP_CHECK(hipStreamSynchronize(d->stream));
+        SFP_CHECK(hipStreamSynchronize(d->st()));
     }
 }
 
 static void devToHost(sfp_dev* d, void* dst, const void* src, size_t b) {
+    syncAll(d);
     for (size_t off = 0; off < b; off += d->bounceCap) {
         const size_t c = b - off < d->bounceCap ? b - off : d->bounceCap;
         devCopy(d, d->bounce, (const char*)src + off, c);
-        SFP_CHECK(hipStreamSynchronize(d->stream));
+        SFP_CHECK(hipStreamSynchronize(d->st()));
         std::memcpy((char*)dst + off, d->bounce, c);
     }
+}
+
+// Device copy of a small constant array, shared by every call with the same
+// contents (uploaded once; the stream is drained only on a miss).
+static const u64* devConst(sfp_dev* d, const u64* v, size_t count) {
+    uint64_t h = 1469598103934665603ull ^ count;
+    for (size_t i = 0; i < count; ++i) h = (h ^ v[i]) * 1099511628211ull;
+    auto& bucket = d->cmap[h];
+    for (auto& e : bucket)
+        if (e.first.size() == count && std::equal(v, v + count, e.first.begin())) return d->cpool + e.second;
+    const size_t words = (count + 1) & ~(size_t)1;  // keep 16-B alignment
+    if (!d->cpool || d->cpoolOff + words > d->cpoolCap) {
+        syncAll(d);  // no queued kernel may still read the old entries
+        if (!d->cpool) {
+            d->cpoolCap = (size_t)1 << 19;  // 4 MiB
+            SFP_CHECK(hipMalloc((void**)&d->cpool, d->cpoolCap * 8));
+        }
+        d->cmap.clear();
+        d->cpoolOff = 0;
+    }
+    const size_t off = d->cpoolOff;
+    d->cpoolOff += words;
+    hostToDev(d, d->cpool + off, v, count * 8);
+    d->cmap[h].push_back({std::vector<u64>(v, v + count), off});
+    return d->cpool + off;
 }
 
 // (C linkage comes from the declarations in prims.h)
@@ -850,10 +922,14 @@ sfp_dev* sfp_create(int device, const sfp_tables* t) {
         delete d;
         return nullptr;  // kernels assume n >= 4096
     }
-    if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) {
-        delete d;
-        return nullptr;
-    }
+    d->nLanes = 4;
+    if (const char* v = std::getenv("SFHE_LANES")) d->nLanes = std::max(1, std::min(SFP_MAX_LANES, std::atoi(v)));
+    for (int l = 0; l < d->nLanes; ++l)
+        if (hipStreamCreateWithFlags(&d->streams[l], hipStreamNonBlocking) != hipSuccess) {
+            for (int k = 0; k < l; ++k) hipStreamDestroy(d->streams[k]);
+            delete d;
+            return nullptr;
+        }
     d->hbar.resize(d->np);
     for (uint32_t i = 0; i < d->np; ++i) d->hbar[i] = sf_make_barrett(t->primes[i]);
     const size_t tn = (size_t)d->np * d->n * 8;
@@ -890,7 +966,11 @@ sfp_dev* sfp_create(int device, const sfp_tables* t) {
 
 void sfp_destroy(sfp_dev* d) {
     if (!d) return;
-    hipStreamSynchronize(d->stream);
+    syncAll(d);
+    for (sfp_event* e : d->evFree) {
+        hipEventDestroy(e->e);
+        delete e;
+    }
     for (auto& f : d->prof) profFlush(d, f);
     for (hipEvent_t e : d->evPool) hipEventDestroy(e);
     hipFree(d->bar);
@@ -903,7 +983,8 @@ void sfp_destroy(sfp_dev* d) {
     hipFree(d->dring);
     hipHostFree(d->hring);
     hipHostFree(d->bounce);
-    hipStreamDestroy(d->stream);
+    hipFree(d->cpool);
+    for (int l = 0; l < d->nLanes; ++l) hipStreamDestroy(d->streams[l]);
     delete d;
 }
 
@@ -923,9 +1004,53 @@ void sfp_h2d(sfp_dev* d, void* dst, const void* src, size_t b) { hostToDev(d, ds
 void sfp_d2h(sfp_dev* d, void* dst, const void* src, size_t b) { devToHost(d, dst, src, b); }
 void sfp_d2d(sfp_dev* d, void* dst, const void* src, size_t b) { devCopy(d, dst, src, b); }
 void sfp_zero(sfp_dev* d, void* dst, size_t b) { devZero(d, dst, b); }
-void sfp_sync(sfp_dev* d) { SFP_CHECK(hipStreamSynchronize(d->stream)); }
+void sfp_sync(sfp_dev* d) { syncAll(d); }
+
+int sfp_lanes(sfp_dev* d) { return d->nLanes; }
+void sfp_set_lane(sfp_dev* d, int lane) {
+    if (lane < 0 || lane >= d->nLanes) {
+        record(d, "set_lane", hipErrorInvalidValue);
+        return;
+    }
+    d->cur = lane;
+}
+int sfp_get_lane(sfp_dev* d) { return d->cur; }
+
+sfp_event* sfp_event_record(sfp_dev* d) {
+    sfp_event* e;
+    if (!d->evFree.empty()) {
+        e = d->evFree.back();
+        d->evFree.pop_back();
+    } else {
+        e = new sfp_event;
+        SFP_CHECK(hipEventCreateWithFlags(&e->e, hipEventDisableTiming));
+    }
+    e->lane = d->cur;
+    SFP_CHECK(hipEventRecord(e->e, d->st()));
+    return e;
+}
+void sfp_event_wait(sfp_dev* d, const sfp_event* e) {
+    if (e && e->lane != d->cur) SFP_CHECK(hipStreamWaitEvent(d->st(), e->e, 0));
+}
+int sfp_event_done(sfp_dev* d, const sfp_event* e) {
+    (void)d;
+    return !e || hipEventQuery(e->e) == hipSuccess;
+}
+void sfp_event_free(sfp_dev* d, sfp_event* e) {
+    if (e) d->evFree.push_back(e);  // re-recording later is safe: waits bind at enqueue time
+}
+void sfp_lane_wait(sfp_dev* d, int waiter, int waitee) {
+    if (waiter == waitee) return;
+    const int keep = d->cur;
+    d->cur = waitee;
+    sfp_event* e = sfp_event_record(d);
+    d->cur = waiter;
+    sfp_event_wait(d, e);
+    sfp_event_free(d, e);
+    d->cur = keep;
+}
 const char* sfp_last_error(sfp_dev* d) {
-    hipError_t e = hipStreamQuery(d->stream);
+    hipError_t e = hipStreamQuery(d->st());
     if (e != hipSuccess && e != hipErrorNotReady) record(d, "stream", e);
     std::lock_guard<std::mutex> g(d->mu);
     return d->err.empty() ? nullptr : d->err.c_str();
@@ -946,13 +1071,13 @@ static void nttRows(sfp_dev* d, const RowGroup& G, int inverse) {
     const uint32_t rows = G.P * G.R;
     if (!rows || !limbsOk(d, G.pm, "ntt")) return;
     if (G.lift && G.liftPrime >= d->np) return (void)limbsOk(d, sfp_limbs{1, 1, G.liftPrime, G.liftPrime}, "ntt lift");
-    const dim3 g(d->n / kTile, rows);
+    const dim3 g(d->n / kNttTile, rows);
     const double bytes = 16.0 * rows * d->n;
     const u64* tw = inverse ? d->ipsi : d->psi;
     const u64* twS = inverse ? d->ipsiS : d->psiS;
     auto pass = [&](auto kern) {
         timedLaunch(d, SFP_FAM_NTT, bytes, [&] {
-            hipLaunchKernelGGL(kern, g, dim3(kNttThreads), 0, d->stream, G, d->bar, tw, twS, d->ninv,
+            hipLaunchKernelGGL(kern, g, dim3(kNttThreads), 0, d->st(), G, d->bar, tw, twS, d->ninv,
                                d->ninvS, d->logn);
         });
     };
@@ -1000,7 +1125,7 @@ static void ew(sfp_dev* d, u64* out, const u64* a, const u64* b, const u64* c, s
     ConstArgs ka;
     if (k) std::memcpy(ka.k, k, m.count * 8);
     const size_t pairs = ((size_t)m.count * d->n) / 2;
-    hipLaunchKernelGGL(k_ew<OP>, dim3(ewGrid(pairs)), dim3(kThreads), 0, d->stream, out, a, b, c, m,
+    hipLaunchKernelGGL(k_ew<OP>, dim3(ewGrid(pairs)), dim3(kThreads), 0, d->st(), out, a, b, c, m,
                        d->bar, d->logn, ka);
     checkLaunch(d, "elementwise");
 }
@@ -1032,7 +1157,7 @@ void sfp_tensor(sfp_dev* d, uint64_t* d0, uint64_t* d1, uint64_t* d2, const uint
                 const uint64_t* a1, const uint64_t* b0, const uint64_t* b1, sfp_limbs m) {
     if (!limbsOk(d, m, "tensor")) return;
     const size_t total = (size_t)m.count * d->n;
-    hipLaunchKernelGGL(k_tensor, dim3(ewGrid(total)), dim3(kThreads), 0, d->stream, d0, d1, d2, a0, a1,
+    hipLaunchKernelGGL(k_tensor, dim3(ewGrid(total)), dim3(kThreads), 0, d->st(), d0, d1, d2, a0, a1,
                        b0, b1, m, d->bar, d->logn);
     checkLaunch(d, "tensor");
 }
@@ -1048,7 +1173,7 @@ void sfp_lin_wsum(sfp_dev* d, uint64_t* out, const uint64_t* const* ins, const u
     for (uint32_t j = 0; j < nin; ++j) pl.p[j] = ins[j];
     const u64* dk = (const u64*)ringPut(d, k, (size_t)nin * m.count * 8);
     const size_t total = (size_t)m.count * d->n;
-    hipLaunchKernelGGL(k_lin_wsum, dim3(ewGrid(total)), dim3(kThreads), 0, d->stream, out, pl, dk, nin,
+    hipLaunchKernelGGL(k_lin_wsum, dim3(ewGrid(total)), dim3(kThreads), 0, d->st(), out, pl, dk, nin,
                        m, d->bar, d->logn);
     checkLaunch(d, "lin_wsum");
 }
@@ -1066,14 +1191,14 @@ void sfp_mac_plain(sfp_dev* d, uint64_t* out, const uint64_t* const* a, const ui
         pl.b[j] = b[j];
     }
     const size_t total = (size_t)m.count * d->n;
-    hipLaunchKernelGGL(k_mac_plain, dim3(ewGrid(total)), dim3(kThreads), 0, d->stream, out, pl, nin, m,
+    hipLaunchKernelGGL(k_mac_plain, dim3(ewGrid(total)), dim3(kThreads), 0, d->st(), out, pl, nin, m,
                        d->bar, d->logn);
     checkLaunch(d, "mac_plain");
 }
 
 void sfp_automorph(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t g, sfp_limbs m) {
     const size_t total = (size_t)m.count * d->n;
-    hipLaunchKernelGGL(k_automorph, dim3(ewGrid(total)), dim3(kThreads), 0, d->stream, out, in, g,
+    hipLaunchKernelGGL(k_automorph, dim3(ewGrid(total)), dim3(kThreads), 0, d->st(), out, in, g,
                        m.count, d->logn);
     checkLaunch(d, "automorph");
 }
@@ -1086,13 +1211,14 @@ static u64* scratch(sfp_dev* d, size_t words) {
         size_t w = 0;
     };
     static std::mutex mu;
-    static std::vector<std::pair<sfp_dev*, S>> pool;
+    static std::vector<std::pair<const void*, S>> pool;
     std::lock_guard<std::mutex> g(mu);
     (void)owner;
+    const void* key = (const char*)d + d->cur;  // one scratch buffer per lane
     for (auto& e : pool)
-        if (e.first == d) {
+        if (e.first == key) {
             if (e.second.w < words) {
-                hipStreamSynchronize(d->stream);
+                syncAll(d);
                 hipFree(e.second.p);
                 hipMalloc(&e.second.p, words * 8);
                 e.second.w = words;
@@ -1102,7 +1228,7 @@ static u64* scratch(sfp_dev* d, size_t words) {
     S s;
     hipMalloc(&s.p, words * 8);
     s.w = words;
-    pool.push_back({d, s});
+    pool.push_back({key, s});
     return s.p;
 }
 
@@ -1137,12 +1263,15 @@ void sfp_rescale_ext(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t ell
     B.ein = RowPtr{in, (long long)inStride, (long long)n};
     B.eout = RowPtr{out, (long long)outStride, (long long)n};
     const u64 ql = d->hbar[dropPrime].q;
+    u64 kS[SFP_MAX_LIMBS], lsub[SFP_MAX_LIMBS];
     for (uint32_t i = 0; i < cnt; ++i) {
         const u64 q = d->hbar[i].q;
-        B.k[i] = qlinv[i];
-        B.kS[i] = sf_shoup_precomp(qlinv[i], q);
-        B.liftSub[i] = ql % q;
+        kS[i] = sf_shoup_precomp(qlinv[i], q);
+        lsub[i] = ql % q;
     }
+    B.k = devConst(d, qlinv, cnt);
+    B.kS = devConst(d, kS, cnt);
+    B.liftSub = devConst(d, lsub, cnt);
     nttRows(d, B, 0);
 }
 
@@ -1185,7 +1314,7 @@ sfp_conv* sfp_upload_conv(sfp_dev* d, uint32_t ns, const uint32_t* src, uint32_t
 
 void sfp_free_conv(sfp_dev* d, sfp_conv* c) {
     if (!c) return;
-    hipStreamSynchronize(d->stream);
+    syncAll(d);
     hipFree(c->src);
     hipFree(c->dst);
     hipFree(c->inv);
@@ -1222,7 +1351,7 @@ static void convLaunch(sfp_dev* d, const ConvJobs& J, uint32_t njobs) {
     }
     const dim3 g(d->n / kThreads, njobs, (maxT + kConvChunk - 1) / kConvChunk);
     timedLaunch(d, SFP_FAM_CONV, bytes, [&] {
-        hipLaunchKernelGGL(k_conv, g, dim3(kThreads), 0, d->stream, J, d->bar, d->logn);
+        hipLaunchKernelGGL(k_conv, g, dim3(kThreads), 0, d->st(), J, d->bar, d->logn);
     });
     checkLaunch(d, "conv");
 }
@@ -1269,7 +1398,7 @@ void sfp_ks_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ex
     const size_t total = (size_t)(ell + K) * d->n;
     // reads beta ext rows + 2*beta key rows, writes 2 accumulator rows, per limb
     timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + 2.0), [&] {
-        hipLaunchKernelGGL(k_ks_inner, dim3(ewGrid(total)), dim3(kThreads), 0, d->stream, acc0, acc1, ext,
+        hipLaunchKernelGGL(k_ks_inner, dim3(ewGrid(total)), dim3(kThreads), 0, d->st(), acc0, acc1, ext,
                            extStride, key, beta, ell, K, Lq, d->bar, d->logn);
     });
     checkLaunch(d, "ks_inner");
@@ -1297,10 +1426,10 @@ void sfp_moddown2(sfp_dev* d, uint64_t* out0, uint64_t* out1, uint64_t* acc, siz
     B.addMask = (add0 ? 1u : 0u) | (add1 ? 2u : 0u);
     B.ein = RowPtr{acc, (long long)accStride, (long long)n};
     B.eout = RowPtr{out0, (long long)(out1 - out0), (long long)n};
-    for (uint32_t i = 0; i < ell; ++i) {
-        B.k[i] = pinv[i];
-        B.kS[i] = sf_shoup_precomp(pinv[i], d->hbar[i].q);
-    }
+    u64 kS[SFP_MAX_LIMBS];
+    for (uint32_t i = 0; i < ell; ++i) kS[i] = sf_shoup_precomp(pinv[i], d->hbar[i].q);
+    B.k = devConst(d, pinv, ell);
+    B.kS = devConst(d, kS, ell);
     nttRows(d, B, 0);
 }
 
@@ -1308,18 +1437,18 @@ void sfp_moddown2(sfp_dev* d, uint64_t* out0, uint64_t* out1, uint64_t* acc, siz
 void sfp_sample_uniform(sfp_dev* d, uint64_t* p, sfp_limbs m, uint64_t seed) {
     if (!limbsOk(d, m, "uniform")) return;
     const size_t total = (size_t)m.count * d->n;
-    hipLaunchKernelGGL(k_uniform, dim3(ewGrid(total)), dim3(kThreads), 0, d->stream, p, m, seed, d->bar,
+    hipLaunchKernelGGL(k_uniform, dim3(ewGrid(total)), dim3(kThreads), 0, d->st(), p, m, seed, d->bar,
                        d->logn);
     checkLaunch(d, "uniform");
 }
 
 void sfp_load_i64(sfp_dev* d, uint64_t* p, const int64_t* c, sfp_limbs m) {
     if (!limbsOk(d, m, "load_i64")) return;
-    // the bounce buffer is free once the stream has drained; the kernel
+    // the bounce buffer is free once every lane has drained; the kernel
     // reads the coefficients straight from it
-    SFP_CHECK(hipStreamSynchronize(d->stream));
+    syncAll(d);
     std::memcpy(d->bounce, c, (size_t)d->n * 8);
-    hipLaunchKernelGGL(k_load_i64, dim3(ewGrid(d->n)), dim3(kThreads), 0, d->stream, p,
+    hipLaunchKernelGGL(k_load_i64, dim3(ewGrid(d->n)), dim3(kThreads), 0, d->st(), p,
                        (const int64_t*)d->bounce, m, d->bar, d->logn);
     checkLaunch(d, "load_i64");
 }

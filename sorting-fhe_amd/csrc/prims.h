@@ -173,6 +173,24 @@ void sfp_sample_uniform(sfp_dev* d, uint64_t* p, sfp_limbs m, uint64_t seed);
 // Load signed coefficients (same for every limb) reduced mod each prime.
 void sfp_load_i64(sfp_dev* d, uint64_t* p, const int64_t* coeffs, sfp_limbs m);
 
+// ---- lanes: independent in-order queues (HIP streams) ----------------------------
+// Every prim launches on the current lane.  Work on different lanes may run
+// concurrently; order it with events.  The oracle has one synchronous lane
+// and treats every call below as satisfied.
+#define SFP_MAX_LANES 8
+typedef struct sfp_event sfp_event;
+int sfp_lanes(sfp_dev* d);
+void sfp_set_lane(sfp_dev* d, int lane);
+int sfp_get_lane(sfp_dev* d);
+// Event at the current end of the current lane.
+sfp_event* sfp_event_record(sfp_dev* d);
+// The current lane waits (device-side) for `e`; no-op for an event of this lane.
+void sfp_event_wait(sfp_dev* d, const sfp_event* e);
+int sfp_event_done(sfp_dev* d, const sfp_event* e);
+void sfp_event_free(sfp_dev* d, sfp_event* e);
+// Lane `waiter` waits for everything enqueued so far on lane `waitee`.
+void sfp_lane_wait(sfp_dev* d, int waiter, int waitee);
+
 // ---- live kernel timing ---------------------------------------------------------
 // Kernel families timed with events recorded on the backend's stream around
 // single launches.  Algorithmic bytes per launch (minimum HBM traffic):
