@@ -264,6 +264,22 @@ void sfp_automorph(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t g, sf
     free(perm);
 }
 
+void sfp_lin_wsum_multi(sfp_dev* d, uint64_t* out, size_t out_stride, size_t poly_stride,
+                        const uint64_t* const* in0, const uint64_t* const* in1, uint32_t nin,
+                        const uint64_t* k, uint32_t nout, sfp_limbs m) {
+    const uint64_t** ins = (const uint64_t**)malloc(nin * sizeof(uint64_t*));
+    uint64_t* kk = (uint64_t*)malloc((size_t)nin * m.count * 8);
+    for (uint32_t o = 0; o < nout; ++o) {
+        memcpy(kk, k + (size_t)o * nin * m.count, (size_t)nin * m.count * 8);
+        for (int p = 0; p < 2; ++p) {
+            for (uint32_t j = 0; j < nin; ++j) ins[j] = p ? in1[j] : in0[j];
+            sfp_lin_wsum(d, out + o * out_stride + p * poly_stride, ins, kk, nin, m);
+        }
+    }
+    free(ins);
+    free(kk);
+}
+
 /* ---- rescale ---- */
 void sfp_rescale(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t ell, const uint64_t* qlinv,
                  uint32_t npoly, size_t in_stride, size_t out_stride) {

@@ -19,6 +19,7 @@
 //   consumed exactly.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <map>
 
 #include "state.h"
@@ -64,6 +65,15 @@ namespace {
 
 using Ct = Ciphertext<DCRTPoly>;
 
+// SFHE_PS_LANES (diagnostic): 0 no helper lanes, 1 baby steps, 2 + recursion
+int psMode() {
+    static const int m = [] {
+        const char* v = std::getenv("SFHE_PS_LANES");
+        return v ? std::atoi(v) : 0;
+    }();
+    return m;
+}
+
 struct Val {
     bool isConst = true;
     double c = 0.0;
@@ -72,11 +82,16 @@ struct Val {
 
 class PSEvaluator {
   public:
-    PSEvaluator(CryptoContextImpl<DCRTPoly>* cc, const Ct& y, uint32_t l, uint32_t D)
-        : cc(cc), l(l), k(1u << l), D(D) {
+    // lanes: {parent, helpers...} of a dataflow region; independent products
+    // are spread over them (inputs from other lanes are waited for device-side)
+    PSEvaluator(CryptoContextImpl<DCRTPoly>* cc, const Ct& y, uint32_t l, uint32_t D,
+                std::vector<int> lanes)
+        : cc(cc), l(l), k(1u << l), D(D), lanes(std::move(lanes)) {
         T.resize(k + 1);
         T[1] = y;
+        // T_j for 2^(t-1) < j <= 2^t only need T_i with i <= 2^(t-1): one wave
         for (uint32_t j = 2; j <= k; ++j) {
+            if (psMode() >= 1) cc->SetLane(this->lanes[j % this->lanes.size()]);
             Ct prod;
             if (j % 2 == 0)
                 prod = cc->EvalSquare(T[j / 2]);
@@ -86,6 +101,52 @@ class PSEvaluator {
             T[j] = (j % 2 == 0) ? cc->EvalAdd(two, -1.0) : cc->EvalSub(two, atLevel(1, two->GetLevel()));
         }
         giant[l] = T[k];
+        cc->SetLane(this->lanes[0]);
+    }
+
+    // Collect the leaves eval() will visit, in visiting order (same control
+    // flow, no ciphertext work), then compute them all: one multi-output
+    // weighted sum + one batched rescale per leaf level.
+    void precomputeLeaves(const std::vector<double>& p, uint32_t depth) {
+        std::vector<std::vector<double>> leaves;
+        plan(p, depth, leaves);
+        std::map<uint32_t, std::vector<size_t>> byLevel;
+        std::vector<uint32_t> lev(leaves.size());
+        for (size_t i = 0; i < leaves.size(); ++i) {
+            lev[i] = leafLevel(leaves[i]);
+            byLevel[lev[i]].push_back(i);
+        }
+        pre.assign(leaves.size(), nullptr);
+        for (auto& kv : byLevel) {
+            const uint32_t L = kv.first;
+            std::vector<uint32_t> js;  // inputs used by any leaf of this level
+            for (uint32_t j = 1; j <= k; ++j)
+                for (size_t i : kv.second)
+                    if (j < leaves[i].size() && leaves[i][j] != 0.0) {
+                        js.push_back(j);
+                        break;
+                    }
+            std::vector<const uint64_t*> ins0, ins1;
+            for (uint32_t j : js) {
+                const Ct& t = atLevel(j, L);
+                cc->state()->dep(t->buf.get());
+                ins0.push_back(t->c0);
+                ins1.push_back(t->c1);
+            }
+            for (size_t b0 = 0; b0 < kv.second.size(); b0 += 64) {
+                std::vector<std::vector<double>> w;
+                const size_t b1 = std::min(kv.second.size(), b0 + 64);
+                for (size_t t = b0; t < b1; ++t) {
+                    const auto& pl = leaves[kv.second[t]];
+                    std::vector<double> row;
+                    for (uint32_t j : js) row.push_back(j < pl.size() ? pl[j] : 0.0);
+                    w.push_back(std::move(row));
+                }
+                auto cts = cc->LinearWSumRescaleMulti(ins0, ins1, w, L, T[1]->GetSlots());
+                for (size_t t = b0; t < b1; ++t) pre[kv.second[t]] = cts[t - b0];
+            }
+        }
+        nextLeaf = 0;
     }
 
     Val eval(std::vector<double> p, uint32_t depth) {
@@ -105,7 +166,12 @@ class PSEvaluator {
                 r[2 * M - j] -= p[j];
             }
         }
+        // the quotient and remainder subtrees are independent: quotient on the
+        // next lane, remainder here; the product and sum run on this lane
+        const int here = cc->state()->lane;
+        if (psMode() >= 2) cc->SetLane(lanes[(nextLane++) % lanes.size()]);
         Val qv = eval(q, depth - 1);
+        cc->SetLane(here);
         Val rv = eval(r, depth);
         const Ct& TM = power(M);
         Val out;
@@ -123,6 +189,41 @@ class PSEvaluator {
     }
 
   private:
+    // eval()'s control flow without ciphertext work: the leaf polynomials
+    void plan(std::vector<double> p, uint32_t depth, std::vector<std::vector<double>>& leaves) {
+        trim(p);
+        if (p.size() <= 1) return;
+        const uint32_t deg = (uint32_t)p.size() - 1;
+        if (deg <= k) {
+            for (uint32_t j = 1; j <= deg; ++j)
+                if (p[j] != 0.0) {
+                    leaves.push_back(p);
+                    return;
+                }
+            return;
+        }
+        if (depth >= 1 && deg + (1u << l) <= (1u << (depth - 1))) return plan(p, depth - 1, leaves);
+        const uint32_t M = deg >= (1u << (depth - 1)) ? (1u << (depth - 1)) : (1u << (depth - 2));
+        std::vector<double> q(deg - M + 1, 0.0), r(p.begin(), p.begin() + M);
+        for (uint32_t j = M; j <= deg; ++j) {
+            if (j == M) {
+                q[0] += p[j];
+            } else {
+                q[j - M] += 2.0 * p[j];
+                r[2 * M - j] -= p[j];
+            }
+        }
+        plan(q, depth - 1, leaves);
+        plan(r, depth, leaves);
+    }
+
+    uint32_t leafLevel(const std::vector<double>& p) const {
+        uint32_t lev = 0;
+        for (uint32_t j = 1; j < p.size(); ++j)
+            if (p[j] != 0.0) lev = std::max(lev, T[j]->GetLevel());
+        return lev;
+    }
+
     static void trim(std::vector<double>& p) {
         while (!p.empty() && p.back() == 0.0) p.pop_back();
     }
@@ -146,6 +247,18 @@ class PSEvaluator {
     }
 
     Val leaf(const std::vector<double>& p) {
+        if (!pre.empty()) {  // precomputed (same visiting order as plan())
+            bool any = false;
+            for (uint32_t j = 1; j < p.size(); ++j) any = any || p[j] != 0.0;
+            if (!any) return Val{true, p[0], nullptr};
+            if (nextLeaf >= pre.size()) SFHE_THROW("internal: Chebyshev leaf plan mismatch");
+            Val out;
+            out.isConst = false;
+            out.ct = pre[nextLeaf];
+            pre[nextLeaf++] = nullptr;
+            if (p[0] != 0.0) out.ct = cc->EvalAdd(out.ct, p[0]);
+            return out;
+        }
         const uint32_t deg = (uint32_t)p.size() - 1;
         uint32_t lev = 0;
         bool any = false;
@@ -160,6 +273,7 @@ class PSEvaluator {
         for (uint32_t j = 1; j <= deg; ++j) {
             if (p[j] == 0.0) continue;
             const Ct& t = atLevel(j, lev);
+            cc->state()->dep(t->buf.get());  // raw pointers below: order after their writers
             ins0.push_back(t->c0);
             ins1.push_back(t->c1);
             w.push_back(p[j]);
@@ -173,6 +287,10 @@ class PSEvaluator {
 
     CryptoContextImpl<DCRTPoly>* cc;
     uint32_t l, k, D;
+    std::vector<int> lanes;
+    uint32_t nextLane = 1;
+    std::vector<Ct> pre;  // precomputed leaves in visiting order
+    size_t nextLeaf = 0;
     std::vector<Ct> T;
     std::map<uint32_t, Ct> giant;
     std::map<std::pair<uint32_t, uint32_t>, Ct> aligned;
@@ -208,9 +326,16 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalChebyshevSeriesPS(
         }
     }
     const uint32_t l = std::min(bestL, (uint32_t)(31 - __builtin_clz(std::max<uint32_t>(d, 2))));
-    PSEvaluator ps(this, y, l, D);
-    auto v = ps.eval(p, D);
-    Ciphertext<DCRTPoly> out = v.isConst ? EvalAdd(EvalMult(y, 0.0), v.c) : v.ct;
+    const auto lanes = psMode() ? ForkHelpers() : std::vector<int>{};
+    Ciphertext<DCRTPoly> out;
+    {
+        PSEvaluator ps(this, y, l, D, lanes.empty() ? std::vector<int>{st->lane} : lanes);
+        static const bool batched = std::getenv("SFHE_PS_UNBATCHED") == nullptr;
+        if (batched) ps.precomputeLeaves(p, D);
+        auto v = ps.eval(p, D);
+        out = v.isConst ? EvalAdd(EvalMult(y, 0.0), v.c) : v.ct;
+    }
+    if (!lanes.empty()) JoinHelpers(lanes);
     const uint32_t target = y->GetLevel() + D;
     if (out->GetLevel() > target)
         SFHE_THROW("internal: Chebyshev evaluation exceeded OpenFHE depth");

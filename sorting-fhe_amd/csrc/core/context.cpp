@@ -146,7 +146,9 @@ DeviceBuffer::~DeviceBuffer() {
     if (ready) sfp_event_free(st->dev, ready);
     if (!ptr) return;
     std::lock_guard<std::mutex> g(st->poolMu);
-    if (!st->forkedLanes)
+    if (st->dataflow)
+        st->dataflowFree.push_back({words, ptr});  // any lane may still read it: after the sub-join
+    else if (!st->forkedLanes)
         st->freeList[0][words].push_back(ptr);  // everything is ordered behind lane 0 again
     else if (region == st->region && lane == st->lane)
         st->freeList[lane][words].push_back(ptr);  // private to this lane in this region
@@ -175,7 +177,24 @@ DeviceBufferPtr SfheContextState::alloc(size_t words) {
         }
         poolBytes += words * 8;
     }
-    return std::make_shared<DeviceBuffer>(this, p, words, lane, forkedLanes ? region : 0);
+    auto b = std::make_shared<DeviceBuffer>(this, p, words, lane, forkedLanes ? region : 0);
+    b->seq = ++laneSeq[lane];
+    return b;
+}
+
+void SfheContextState::laneWait(int waiter, int waitee) {
+    if (waiter == waitee) return;
+    sfp_lane_wait(dev, waiter, waitee);
+    synced[waiter][waitee] = laneSeq[waitee];
+}
+
+void SfheContextState::dep(DeviceBuffer* b) {
+    if (b && b->lane != lane && synced[lane][b->lane] < b->seq) laneWait(lane, b->lane);
+}
+
+void SfheContextState::wrote(DeviceBuffer* b) {
+    b->lane = lane;
+    b->seq = ++laneSeq[lane];
 }
 
 void SfheContextState::releaseAll() {
@@ -215,6 +234,16 @@ class SfheInternal {
         std::fprintf(stderr, "TRACE %llu %s L%u %016llx\n", (unsigned long long)counter++, what,
                      ct->level, (unsigned long long)f);
         return ct;
+    }
+
+    // order the current lane after the writers of the inputs (lanes)
+    static void deps(SfheContextState* s, std::initializer_list<const Ct*> in) {
+        for (const Ct* c : in)
+            if (c && *c) s->dep((*c)->buf.get());
+    }
+    static void depsv(SfheContextState* s, const std::vector<Ct>& in) {
+        for (const Ct& c : in)
+            if (c) s->dep(c->buf.get());
     }
 
     static sfp_limbs Q(uint32_t ell) { return sfp_limbs{ell, ell, 0}; }
@@ -703,16 +732,49 @@ void CryptoContextImpl<DCRTPoly>::ForkLanes(int count) {
     count = std::max(1, std::min(count, sfp_lanes(s->dev)));
     sfp_set_lane(s->dev, 0);
     s->lane = 0;
-    for (int i = 1; i < count; ++i) sfp_lane_wait(s->dev, i, 0);
+    for (int i = 1; i < count; ++i) s->laneWait(i, 0);
     s->forkedLanes = count;
     s->region = ++s->regionCount;
+}
+
+std::vector<int> CryptoContextImpl<DCRTPoly>::ForkHelpers() {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheContextState* s = st.get();
+    std::vector<int> lanes{s->lane};
+    if (!s->dataflow) {
+        // helpers: lanes that are not primaries of an open batch region
+        const int first = s->forkedLanes ? s->forkedLanes : 0;
+        for (int l = first; l < sfp_lanes(s->dev); ++l)
+            if (l != s->lane) {
+                s->laneWait(l, s->lane);
+                lanes.push_back(l);
+            }
+    }
+    s->dataflow++;
+    return lanes;
+}
+
+void CryptoContextImpl<DCRTPoly>::JoinHelpers(const std::vector<int>& lanes) {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheContextState* s = st.get();
+    if (!s->dataflow) return;
+    const int parent = lanes.empty() ? s->lane : lanes[0];
+    s->lane = parent;
+    sfp_set_lane(s->dev, parent);
+    for (size_t i = 1; i < lanes.size(); ++i) s->laneWait(parent, lanes[i]);
+    if (--s->dataflow == 0) {
+        std::lock_guard<std::mutex> pg(s->poolMu);
+        for (auto& e : s->dataflowFree) s->freeList[parent][e.first].push_back(e.second);
+        s->dataflowFree.clear();
+    }
 }
 
 void CryptoContextImpl<DCRTPoly>::SetLane(int lane) {
     std::lock_guard<std::recursive_mutex> g(st->opMu);
     SfheContextState* s = st.get();
-    if (lane != 0 && (!s->forkedLanes || lane >= s->forkedLanes))
+    if (lane != 0 && !s->dataflow && (!s->forkedLanes || lane >= s->forkedLanes))
         SFHE_THROW("SetLane: lane " + std::to_string(lane) + " outside the open region");
+    if (lane < 0 || lane >= sfp_lanes(s->dev)) SFHE_THROW("SetLane: no lane " + std::to_string(lane));
     s->lane = lane;
     sfp_set_lane(s->dev, lane);
 }
@@ -721,7 +783,7 @@ void CryptoContextImpl<DCRTPoly>::JoinLanes() {
     std::lock_guard<std::recursive_mutex> g(st->opMu);
     SfheContextState* s = st.get();
     if (!s->forkedLanes) return;
-    for (int i = 1; i < s->forkedLanes; ++i) sfp_lane_wait(s->dev, 0, i);
+    for (int i = 1; i < s->forkedLanes; ++i) s->laneWait(0, i);
     sfp_set_lane(s->dev, 0);
     std::lock_guard<std::mutex> pg(s->poolMu);
     for (int i = 1; i < s->forkedLanes; ++i) {
@@ -908,6 +970,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::Encrypt(const PublicKey<DCRTPo
 void CryptoContextImpl<DCRTPoly>::Decrypt(const PrivateKey<DCRTPoly>& sk,
                                           const Ciphertext<DCRTPoly>& ct, Plaintext* out) {
     std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheInternal::deps(st.get(), {&ct});
     SfheContextState* s = st.get();
     if (!sk) SFHE_THROW("null secret key");
     const uint32_t ell = s->ellOf(ct->level);
@@ -967,6 +1030,7 @@ std::ostream& operator<<(std::ostream& os, const Plaintext& pt) {
 
 Ciphertext<DCRTPoly> CiphertextImpl<DCRTPoly>::Clone() const {
     std::lock_guard<std::recursive_mutex> g(cc->state()->opMu);
+    cc->state()->dep(buf.get());
     auto self = std::make_shared<CiphertextImpl<DCRTPoly>>(*this);
     return SfheInternal::copyOf(cc.get(), self);
 }
@@ -979,6 +1043,7 @@ uint32_t CiphertextImpl<DCRTPoly>::GetNumLimbs() const { return cc->state()->ell
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalAdd(const Ciphertext<DCRTPoly>& a0,
                                                          const Ciphertext<DCRTPoly>& b0) {
     std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheInternal::deps(st.get(), {&a0, &b0});
     auto a = a0, b = b0;
     SfheInternal::align(this, a, b);
     auto out = SfheInternal::newCt(this, a->level, std::max(a->slots, b->slots));
@@ -993,14 +1058,19 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalAdd(const Ciphertext<DCRTP
 void CryptoContextImpl<DCRTPoly>::EvalAddInPlace(Ciphertext<DCRTPoly>& a,
                                                  const Ciphertext<DCRTPoly>& b0) {
     std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheInternal::deps(st.get(), {&a, &b0});
     auto b = b0;
-    if (a->level != b->level || a->buf.use_count() > 1 || a->c1 - a->c0 != (ptrdiff_t)(st->ellOf(a->level) * st->n)) {
+    // in place only on an exclusively owned buffer outside dataflow regions
+    // (there another lane may still be reading the old value)
+    if (a->level != b->level || a->buf.use_count() > 1 || st->dataflow ||
+        a->c1 - a->c0 != (ptrdiff_t)(st->ellOf(a->level) * st->n)) {
         a = EvalAdd(a, b);
         return;
     }
     const uint32_t ell = st->ellOf(a->level);
     sfp_add(st->dev, a->c0, a->c0, b->c0, SfheInternal::Q(ell));
     sfp_add(st->dev, a->c1, a->c1, b->c1, SfheInternal::Q(ell));
+    st->wrote(a->buf.get());
     a->slots = std::max(a->slots, b->slots);
     st->stats.add++;
     st->countBytes(6.0 * ell * st->n * 8);
@@ -1009,6 +1079,7 @@ void CryptoContextImpl<DCRTPoly>::EvalAddInPlace(Ciphertext<DCRTPoly>& a,
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalAdd(const Ciphertext<DCRTPoly>& a,
                                                          double c) {
     std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheInternal::deps(st.get(), {&a});
     const uint32_t ell = st->ellOf(a->level);
     auto out = SfheInternal::newCt(this, a->level, a->slots);
     auto k = SfheInternal::constResidues(st.get(), c * a->scale, ell);
@@ -1026,6 +1097,7 @@ void CryptoContextImpl<DCRTPoly>::EvalAddInPlace(Ciphertext<DCRTPoly>& a, double
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalAdd(const Ciphertext<DCRTPoly>& a,
                                                          const Plaintext& p) {
     std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheInternal::deps(st.get(), {&a});
     const uint32_t ell = st->ellOf(a->level);
     const uint64_t* m = SfheInternal::encoded(this, p, a->level);
     auto out = SfheInternal::newCt(this, a->level, std::max(a->slots, p->slots));
@@ -1043,6 +1115,7 @@ void CryptoContextImpl<DCRTPoly>::EvalAddInPlace(Ciphertext<DCRTPoly>& a, const 
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalSub(const Ciphertext<DCRTPoly>& a0,
                                                          const Ciphertext<DCRTPoly>& b0) {
     std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheInternal::deps(st.get(), {&a0, &b0});
     auto a = a0, b = b0;
     SfheInternal::align(this, a, b);
     auto out = SfheInternal::newCt(this, a->level, std::max(a->slots, b->slots));
@@ -1061,6 +1134,7 @@ void CryptoContextImpl<DCRTPoly>::EvalSubInPlace(Ciphertext<DCRTPoly>& a,
 
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalNegate(const Ciphertext<DCRTPoly>& a) {
     std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheInternal::deps(st.get(), {&a});
     const uint32_t ell = st->ellOf(a->level);
     auto out = SfheInternal::newCt(this, a->level, a->slots);
     sfp_neg(st->dev, out->c0, a->c0, SfheInternal::Q(ell));
@@ -1078,6 +1152,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalSub(double c, const Cipher
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalSub(const Ciphertext<DCRTPoly>& a,
                                                          const Plaintext& p) {
     std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheInternal::deps(st.get(), {&a});
     const uint32_t ell = st->ellOf(a->level);
     const uint64_t* m = SfheInternal::encoded(this, p, a->level);
     auto out = SfheInternal::newCt(this, a->level, std::max(a->slots, p->slots));
@@ -1091,6 +1166,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalSub(const Ciphertext<DCRTP
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalSub(const Plaintext& p,
                                                          const Ciphertext<DCRTPoly>& a) {
     std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheInternal::deps(st.get(), {&a});
     const uint32_t ell = st->ellOf(a->level);
     const uint64_t* m = SfheInternal::encoded(this, p, a->level);
     auto out = SfheInternal::newCt(this, a->level, std::max(a->slots, p->slots));
@@ -1121,6 +1197,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalAddMany(
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMult(const Ciphertext<DCRTPoly>& a,
                                                           double c) {
     std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheInternal::deps(st.get(), {&a});
     SfheContextState* s = st.get();
     const uint32_t ell = s->ellOf(a->level);
     if (ell < 2) SFHE_THROW("no levels left (multiplicative depth exhausted)");
@@ -1144,6 +1221,7 @@ void CryptoContextImpl<DCRTPoly>::EvalMultInPlace(Ciphertext<DCRTPoly>& a, doubl
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMult(const Ciphertext<DCRTPoly>& a,
                                                           const Plaintext& p) {
     std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheInternal::deps(st.get(), {&a});
     SfheContextState* s = st.get();
     const uint32_t ell = s->ellOf(a->level);
     if (ell < 2) SFHE_THROW("no levels left (multiplicative depth exhausted)");
@@ -1165,6 +1243,7 @@ void CryptoContextImpl<DCRTPoly>::EvalMultInPlace(Ciphertext<DCRTPoly>& a, const
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMult(const Ciphertext<DCRTPoly>& a0,
                                                           const Ciphertext<DCRTPoly>& b0) {
     std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheInternal::deps(st.get(), {&a0, &b0});
     SfheContextState* s = st.get();
     if (!s->relinKey) SFHE_THROW("EvalMultKeyGen must be called before EvalMult");
     auto a = a0, b = b0;
@@ -1189,6 +1268,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalSquare(const Ciphertext<DC
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMultAddPlain(
     const std::vector<Ciphertext<DCRTPoly>>& a, const std::vector<Plaintext>& p) {
     std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheInternal::depsv(st.get(), a);
     SfheContextState* s = st.get();
     if (a.empty() || a.size() != p.size()) SFHE_THROW("operand count mismatch");
     uint32_t level = 0, slots = 0;
@@ -1234,6 +1314,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMultAddPlain(
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotate(const Ciphertext<DCRTPoly>& a,
                                                             int32_t r) {
     std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheInternal::deps(st.get(), {&a});
     SfheContextState* s = st.get();
     uint32_t gal = GaloisForRotation(r);
     if (gal == 1) return a->Clone();
@@ -1256,6 +1337,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotate(const Ciphertext<DC
 std::shared_ptr<FastRotationPrecomp> CryptoContextImpl<DCRTPoly>::EvalFastRotationPrecompute(
     const Ciphertext<DCRTPoly>& a) {
     std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheInternal::deps(st.get(), {&a});
     SfheContextState* s = st.get();
     auto pre = std::make_shared<FastRotationPrecomp>();
     const uint32_t ell = s->ellOf(a->level);
@@ -1273,6 +1355,7 @@ std::shared_ptr<FastRotationPrecomp> CryptoContextImpl<DCRTPoly>::EvalFastRotati
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalFastRotation(
     const Ciphertext<DCRTPoly>& a, int32_t r, uint32_t, const std::shared_ptr<FastRotationPrecomp>& pre) {
     std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheInternal::deps(st.get(), {&a});
     SfheContextState* s = st.get();
     uint32_t gal = GaloisForRotation(r);
     if (gal == 1) return a->Clone();
@@ -1301,6 +1384,71 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalFastRotation(
 // fused weighted sum (Chebyshev leaves, EvalPolyLinear)
 
 // sum_j w_j * (c0_j, c1_j) at `level` (canonical scale), then one rescale
+namespace {
+// residue of round(w * Delta_level) modulo each of the ell primes (weight of a
+// ciphertext at `level` whose product is rescaled to the next level)
+void weightResidues(const SfheContextState* s, double w, uint32_t level, uint32_t ell,
+                    std::vector<uint64_t>& kk) {
+    const double K = w * s->scale[level];
+    const double r = std::nearbyint(K);
+    const bool neg = r < 0;
+    const double a = std::fabs(r);
+    u128 v;
+    if (a < 1.8e19) {
+        v = (u128)(u64)a;
+    } else {
+        const double hi = std::floor(std::ldexp(a, -64));
+        v = ((u128)(u64)hi << 64) + (u128)(u64)(a - std::ldexp(hi, 64));
+    }
+    for (uint32_t i = 0; i < ell; ++i) {
+        const u64 q = s->primes[i];
+        const u64 m = (u64)(v % q);
+        kk.push_back(neg ? (m ? q - m : 0) : m);
+    }
+}
+}  // namespace
+
+std::vector<Ciphertext<DCRTPoly>> CryptoContextImpl<DCRTPoly>::LinearWSumRescaleMulti(
+    const std::vector<const uint64_t*>& in0, const std::vector<const uint64_t*>& in1,
+    const std::vector<std::vector<double>>& w, uint32_t level, uint32_t slots) {
+    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheContextState* s = st.get();
+    const uint32_t ell = s->ellOf(level), n = s->n;
+    const uint32_t nin = (uint32_t)in0.size(), nout = (uint32_t)w.size();
+    if (ell < 2) SFHE_THROW("no levels left (multiplicative depth exhausted)");
+    if (nin == 0 || nin > SFP_MAX_WSUM || nout == 0) SFHE_THROW("LinearWSumRescaleMulti: bad sizes");
+    std::vector<uint64_t> kk;
+    kk.reserve((size_t)nout * nin * ell);
+    for (const auto& row : w) {
+        if (row.size() != nin) SFHE_THROW("LinearWSumRescaleMulti: weight row size");
+        for (double x : row) weightResidues(s, x, level, ell, kk);
+    }
+    const size_t pw = (size_t)ell * n;  // words per polynomial
+    auto sums = s->alloc((size_t)nout * 2 * pw);
+    sfp_lin_wsum_multi(s->dev, sums->ptr, 2 * pw, pw, in0.data(), in1.data(), nin, kk.data(), nout,
+                       SfheInternal::Q(ell));
+    // one rescale of all 2 * nout polynomials; the results share one buffer
+    const size_t qw = (size_t)(ell - 1) * n;
+    auto res = s->alloc((size_t)nout * 2 * qw);
+    sfp_rescale(s->dev, res->ptr, sums->ptr, ell, s->qInvTable[ell].data(), 2 * nout, pw, qw);
+    std::vector<Ciphertext<DCRTPoly>> out(nout);
+    for (uint32_t o = 0; o < nout; ++o) {
+        auto ct = std::make_shared<CiphertextImpl<DCRTPoly>>();
+        ct->cc = shared_from_this();
+        ct->buf = res;
+        ct->c0 = res->ptr + (size_t)o * 2 * qw;
+        ct->c1 = ct->c0 + qw;
+        ct->level = level + 1;
+        ct->slots = slots;
+        ct->scale = s->scale[level + 1];
+        out[o] = ct;
+    }
+    s->stats.wsum_terms += (uint64_t)nin * nout;
+    s->stats.rescale += 2 * nout;
+    s->countBytes(((double)nin + nout) * 2.0 * pw * 8 + 4.0 * pw * 8 * nout);
+    return out;
+}
+
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::LinearWSumRescale(
     const std::vector<const uint64_t*>& in0, const std::vector<const uint64_t*>& in1,
     const std::vector<double>& w, uint32_t level, uint32_t slots) {
@@ -1369,6 +1517,7 @@ void CryptoContextImpl<DCRTPoly>::LevelReduceInPlace(Ciphertext<DCRTPoly>& a, st
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::AdjustLevel(const Ciphertext<DCRTPoly>& a,
                                                              uint32_t targetLevel) {
     std::lock_guard<std::recursive_mutex> g(st->opMu);
+    SfheInternal::deps(st.get(), {&a});
     auto r = SfheInternal::adjust(this, a, targetLevel);
     return r == a ? a->Clone() : r;
 }

@@ -361,6 +361,11 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
                                            const std::vector<const uint64_t*>& in1,
                                            const std::vector<double>& w, uint32_t level,
                                            uint32_t slots);
+    // Engine extension: nout weighted sums of the same inputs in one pass
+    // (one multi-output kernel + one batched rescale); w[o] has nin weights.
+    std::vector<Ciphertext<DCRTPoly>> LinearWSumRescaleMulti(
+        const std::vector<const uint64_t*>& in0, const std::vector<const uint64_t*>& in1,
+        const std::vector<std::vector<double>>& w, uint32_t level, uint32_t slots);
     // Wait for all device work; throws on an asynchronous device error.
     void Synchronize();
     // Engine extension: independent work on concurrent lanes (HIP streams).
@@ -372,6 +377,13 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
     void ForkLanes(int count);
     void SetLane(int lane);
     void JoinLanes();
+    // Dataflow sub-region on helper lanes (lanes that are not primaries of the
+    // open region): returns {current lane, helpers...}, all ordered after the
+    // current lane.  Inside, operations may read results of other lanes (they
+    // wait for them device-side) and frees are deferred to JoinHelpers, which
+    // orders the parent lane after every helper.
+    std::vector<int> ForkHelpers();
+    void JoinHelpers(const std::vector<int>& lanes);
     // Plaintext-encoding cache across calls (default on); see DESIGN.md.
     void SetPlaintextCache(bool on);
     // Operation counters (for the roofline byte model).

@@ -21,8 +21,9 @@ class DeviceBuffer {
     SfheContextState* st;
     uint64_t* ptr;
     size_t words;
-    int lane;                      // lane that allocated it
+    int lane;                      // lane of the last writer (allocating lane until an in-place write)
     uint64_t region;               // fork/join region it was allocated in (0: none)
+    uint64_t seq = 0;              // position of its last write in lane's sequence
     sfp_event* ready = nullptr;    // shared encodings: end of the producing work
 };
 
@@ -74,6 +75,17 @@ struct SfheContextState {
     int forkedLanes = 0;   // > 0 while a fork/join region is open
     uint64_t region = 0;   // id of the open region (0: none)
     uint64_t regionCount = 0;
+    // dataflow sub-regions (cross-lane reads allowed; every free is deferred
+    // to the sub-join, where the parent lane has waited for all helpers)
+    int dataflow = 0;
+    std::vector<std::pair<size_t, uint64_t*>> dataflowFree;
+    // cross-lane ordering: laneSeq[l] counts writes issued on lane l;
+    // synced[h][x] = laneSeq[x] at the last time lane h waited for lane x
+    uint64_t laneSeq[SFP_MAX_LANES] = {};
+    uint64_t synced[SFP_MAX_LANES][SFP_MAX_LANES] = {};
+    void laneWait(int waiter, int waitee);
+    void dep(DeviceBuffer* b);     // current lane waits for b's last writer if needed
+    void wrote(DeviceBuffer* b);   // b was just written on the current lane
     size_t poolBytes = 0;
 
     // serialises host-side use of the device from OpenMP callers

@@ -91,6 +91,10 @@ struct sfp_dev {
     sf_barrett* bar = nullptr;  // device [np]
     u64 *psi = nullptr, *psiS = nullptr, *ipsi = nullptr, *ipsiS = nullptr;
     u64 *ninv = nullptr, *ninvS = nullptr;
+    // FP64 twiddles for primes < 2^42 (exact doubles w and rounded w/q), and
+    // per-prime 1/q and n^-1 as doubles
+    double *psiD = nullptr, *psiQ = nullptr, *ipsiD = nullptr, *ipsiQ = nullptr;
+    double *qinvD = nullptr, *ninvD = nullptr, *ninvQ = nullptr;
     std::vector<sf_barrett> hbar;
     // pinned argument ring (host) mirrored on the device
     char* hring = nullptr;
@@ -238,6 +242,9 @@ static unsigned gridFor(size_t work, unsigned perBlock) {
 // finishes the transform reduces to [0, q).  The inverse runs the
 // Gentleman-Sande stages in reverse order (ROW pass first) and folds n^-1
 // into the COL pass's store.
+#ifndef SFHE_NTT_FP
+#define SFHE_NTT_FP 1  // FP64 butterflies for primes < 2^42
+#endif
 #ifndef SFHE_NTT_EXP
 #define SFHE_NTT_EXP 0  // experiments only: 1 no butterflies, 2 no twiddle loads, 3 no rounds
 #endif
@@ -376,6 +383,112 @@ __device__ __forceinline__ void nttRoundDyn(int b, u64* s, const NttTile& T, uin
     nttRound<INV, COL, 1>(s, T, S0, k0, q, w, wS);
 }
 
+// ---- FP64 butterflies (primes q < 2^42) ------------------------------------
+// Residues are held as exact doubles.  For |Y| < 2^52, W in [0, q):
+//   hi = Y*W, lo = fma(Y, W, -hi) (hi + lo == Y*W exactly),
+//   qq = rint(Y * (W/q))            (within 1 of the true quotient),
+//   r  = fma(-qq, q, hi) + lo       (exact: |hi - qq q| < 2^53)
+// gives r == Y*W (mod q) with |r| < 2q.  Within one pass (<= 9 stages from
+// [0, q)) forward values stay below 19q and inverse values below 2^9 q <
+// 2^51, so no intermediate reduction is needed.
+constexpr uint64_t kFpPrimeBound = 1ull << 42;
+
+__device__ __forceinline__ double fpMulMod(double y, double w, double wq, double q) {
+    const double hi = y * w;
+    const double lo = fma(y, w, -hi);
+    const double qq = rint(y * wq);
+    return fma(-qq, q, hi) + lo;
+}
+
+// |v| < 2^52 -> [0, q)
+__device__ __forceinline__ double fpReduce(double v, double q, double qinv) {
+    double r = fma(-rint(v * qinv), q, v);
+    return r < 0.0 ? r + q : r;
+}
+
+template <bool INV, bool COL, int B>
+__device__ __forceinline__ void nttRoundFP(double* s, const NttTile& T, uint32_t S0, uint32_t k0, double q,
+                                           const double* __restrict__ w, const double* __restrict__ wq) {
+    constexpr int M = 1 << B;
+    constexpr int GPT = kNttE / M;
+    const uint32_t D = 1u << T.d;
+    const uint32_t logh = T.d - k0 - B;
+    const uint32_t h = 1u << logh;
+    const uint32_t span = D >> k0;
+#pragma unroll
+    for (int gi = 0; gi < GPT; ++gi) {
+        const uint32_t gid = threadIdx.x + gi * kNttThreads;
+        uint32_t st, lo, hi;
+        if (COL) {
+            st = gid & (T.C - 1);
+            const uint32_t rest = gid >> T.logC;
+            lo = rest & (h - 1);
+            hi = rest >> logh;
+        } else {
+            lo = gid & (h - 1);
+            const uint32_t rest = gid >> logh;
+            hi = rest & ((1u << k0) - 1);
+            st = rest >> k0;
+        }
+        const uint32_t ub = hi * span + lo;
+        const uint32_t x0 = nttGlobal<COL>(T, st, ub);
+        double W[M - 1], WQ[M - 1];
+#pragma unroll
+        for (int t = 0; t < B; ++t) {
+            const uint32_t S = S0 + k0 + t;
+            const uint32_t tb = (1u << S) + (x0 >> (T.logn - S));
+#pragma unroll
+            for (int qd = 0; qd < (1 << t); ++qd) {
+                W[(1 << t) - 1 + qd] = w[tb + qd];
+                WQ[(1 << t) - 1 + qd] = wq[tb + qd];
+            }
+        }
+        double v[M];
+#pragma unroll
+        for (int j = 0; j < M; ++j) v[j] = s[ldsSw(nttLocal<COL>(T, st, ub + j * h))];
+        if (!INV) {
+#pragma unroll
+            for (int t = 0; t < B; ++t) {
+                const int half = 1 << (B - 1 - t);
+#pragma unroll
+                for (int j = 0; j < M; ++j) {
+                    if (j & half) continue;
+                    const int ti = (1 << t) - 1 + (j >> (B - t));
+                    const double X = v[j];
+                    const double Y = fpMulMod(v[j + half], W[ti], WQ[ti], q);
+                    v[j] = X + Y;
+                    v[j + half] = X - Y;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int t = B - 1; t >= 0; --t) {
+                const int half = 1 << (B - 1 - t);
+#pragma unroll
+                for (int j = 0; j < M; ++j) {
+                    if (j & half) continue;
+                    const int ti = (1 << t) - 1 + (j >> (B - t));
+                    const double X = v[j], Y = v[j + half];
+                    v[j] = X + Y;
+                    v[j + half] = fpMulMod(X - Y, W[ti], WQ[ti], q);
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < M; ++j) s[ldsSw(nttLocal<COL>(T, st, ub + j * h))] = v[j];
+    }
+}
+
+template <bool INV, bool COL>
+__device__ __forceinline__ void nttRoundDynFP(int b, double* s, const NttTile& T, uint32_t S0, uint32_t k0,
+                                              double q, const double* w, const double* wq) {
+    if constexpr (kNttLogE >= 3) {
+        if (b == 3) return nttRoundFP<INV, COL, 3>(s, T, S0, k0, q, w, wq);
+    }
+    if (b == 2) return nttRoundFP<INV, COL, 2>(s, T, S0, k0, q, w, wq);
+    nttRoundFP<INV, COL, 1>(s, T, S0, k0, q, w, wq);
+}
+
 // A 2-D set of rows for one NTT launch, passed by value: row (p, i) for
 // p < P, i < R lives at base + p*ps + i*is (word offsets).  Prime of row i:
 // primeOf(pm, i).  The first pass reads `src` (optionally the centred lift of
@@ -408,7 +521,12 @@ template <bool INV, bool COL>
 __global__ __launch_bounds__(kNttThreads) void k_ntt(const RowGroup G, const sf_barrett* __restrict__ bar,
                                                   const u64* __restrict__ tw, const u64* __restrict__ twS,
                                                   const u64* __restrict__ ninv,
-                                                  const u64* __restrict__ ninvS, uint32_t logn) {
+                                                  const u64* __restrict__ ninvS, uint32_t logn,
+                                                  const double* __restrict__ twD,
+                                                  const double* __restrict__ twQ,
+                                                  const double* __restrict__ qinvD,
+                                                  const double* __restrict__ ninvD,
+                                                  const double* __restrict__ ninvQ, int useFp) {
     __shared__ u64 s[kNttTile];
     constexpr bool FIRST = (COL != INV);  // forward: COL first; inverse: ROW first
     const uint32_t n = 1u << logn;
@@ -418,6 +536,7 @@ __global__ __launch_bounds__(kNttThreads) void k_ntt(const RowGroup G, const sf_
     if (G.skipEll && ii >= G.alpha * pp && ii < min(G.alpha * (pp + 1), G.skipEll)) return;
     const uint32_t prime = primeOf(G.pm, ii);
     const u64 q = bar[prime].q;
+    const bool fp = useFp && q < kFpPrimeBound;  // uniform per block
     const u64* w = tw + (size_t)prime * n;
     const u64* wS = twS + (size_t)prime * n;
     NttTile T;
@@ -458,8 +577,13 @@ __global__ __launch_bounds__(kNttThreads) void k_ntt(const RowGroup G, const sf_
                 x.y = r1;
             }
         }
-        s[ldsSw(e)] = x.x;
-        s[ldsSw(e + 1)] = x.y;
+        if (fp) {
+            s[ldsSw(e)] = __double_as_longlong((double)x.x);
+            s[ldsSw(e + 1)] = __double_as_longlong((double)x.y);
+        } else {
+            s[ldsSw(e)] = x.x;
+            s[ldsSw(e + 1)] = x.y;
+        }
     }
     __syncthreads();
 #if SFHE_NTT_EXP >= 3
@@ -471,7 +595,11 @@ __global__ __launch_bounds__(kNttThreads) void k_ntt(const RowGroup G, const sf_
         const uint32_t r = INV ? nr - 1 - ri : ri;
         const uint32_t k0 = kNttLogE * r;
         const int b = (int)min((uint32_t)kNttLogE, T.d - k0);
-        nttRoundDyn<INV, COL>(b, s, T, S0, k0, q, w, wS);
+        if (fp)
+            nttRoundDynFP<INV, COL>(b, reinterpret_cast<double*>(s), T, S0, k0, (double)q,
+                                    twD + (size_t)prime * n, twQ + (size_t)prime * n);
+        else
+            nttRoundDyn<INV, COL>(b, s, T, S0, k0, q, w, wS);
         __syncthreads();
     }
     const bool scale = INV && COL;
@@ -487,7 +615,16 @@ __global__ __launch_bounds__(kNttThreads) void k_ntt(const RowGroup G, const sf_
         ulonglong2 x;
         x.x = s[ldsSw(e)];
         x.y = s[ldsSw(e + 1)];
-        if (!FIRST) {  // finish the lazy ranges: forward [0,4q), inverse [0,2q) -> [0,q)
+        if (fp) {  // every FP pass ends canonical: [0, q) as u64
+            const double qd = (double)q, qi = qinvD[prime];
+            double a0 = __longlong_as_double(x.x), a1 = __longlong_as_double(x.y);
+            if (scale) {
+                a0 = fpMulMod(a0, ninvD[prime], ninvQ[prime], qd);
+                a1 = fpMulMod(a1, ninvD[prime], ninvQ[prime], qd);
+            }
+            x.x = (u64)fpReduce(a0, qd, qi);
+            x.y = (u64)fpReduce(a1, qd, qi);
+        } else if (!FIRST) {  // finish the lazy ranges: forward [0,4q), inverse [0,2q) -> [0,q)
             if (scale) {
                 x.x = sf_mul_shoup_lazy(x.x, ni, niS, q);
                 x.y = sf_mul_shoup_lazy(x.y, ni, niS, q);
@@ -608,6 +745,55 @@ __global__ __launch_bounds__(kThreads) void k_lin_wsum(u64* __restrict__ out, Pt
         Acc acc{0, 0};
         for (uint32_t j = 0; j < nin; ++j) macc(acc, ins.p[j][i], k[(size_t)j * m.count + limb]);
         out[i] = sf_reduce128_acc(acc.lo, acc.hi, &B);
+    }
+}
+
+// Multi-output weighted sum: grid (coefficient blocks, limb, chunk of
+// kWsumChunk outputs).  Each thread streams the nin inputs of its coefficient
+// once per chunk and keeps 2 x kWsumChunk 128-bit accumulators; the chunk's
+// weights for this limb sit in LDS.
+constexpr int kWsumChunk = 8;
+__global__ __launch_bounds__(kThreads) void k_lin_wsum_multi(u64* __restrict__ out, size_t outStride,
+                                                             size_t polyStride, PtrList2 ins,
+                                                             const u64* __restrict__ k, uint32_t nin,
+                                                             uint32_t nout, sfp_limbs m,
+                                                             const sf_barrett* __restrict__ bar,
+                                                             uint32_t logn) {
+    __shared__ u64 sk[kWsumChunk * SFP_MAX_WSUM];
+    const uint32_t limb = blockIdx.y;
+    const uint32_t o0 = blockIdx.z * kWsumChunk;
+    const uint32_t oc = min((uint32_t)kWsumChunk, nout - o0);
+    for (uint32_t e = threadIdx.x; e < oc * nin; e += kThreads) {
+        const uint32_t o = e / nin, j = e % nin;
+        sk[o * SFP_MAX_WSUM + j] = k[((size_t)(o0 + o) * nin + j) * m.count + limb];
+    }
+    __syncthreads();
+    const uint32_t n = 1u << logn;
+    const uint32_t x = blockIdx.x * kThreads + threadIdx.x;
+    if (x >= n) return;
+    const size_t off = ((size_t)limb << logn) + x;
+    Acc a0[kWsumChunk], a1[kWsumChunk];
+#pragma unroll
+    for (int o = 0; o < kWsumChunk; ++o) a0[o] = a1[o] = Acc{0, 0};
+    for (uint32_t j = 0; j < nin; ++j) {
+        const u64 v0 = ins.a[j][off], v1 = ins.b[j][off];
+#pragma unroll
+        for (int o = 0; o < kWsumChunk; ++o) {
+            if ((uint32_t)o < oc) {
+                const u64 w = sk[o * SFP_MAX_WSUM + j];
+                macc(a0[o], v0, w);
+                macc(a1[o], v1, w);
+            }
+        }
+    }
+    const sf_barrett B = loadBar(bar, primeOf(m, limb));
+#pragma unroll
+    for (int o = 0; o < kWsumChunk; ++o) {
+        if ((uint32_t)o < oc) {
+            u64* dst = out + (size_t)(o0 + o) * outStride + off;
+            dst[0] = sf_reduce128_acc(a0[o].lo, a0[o].hi, &B);
+            dst[polyStride] = sf_reduce128_acc(a1[o].lo, a1[o].hi, &B);
+        }
     }
 }
 
@@ -937,7 +1123,10 @@ sfp_dev* sfp_create(int device, const sfp_tables* t) {
               hipMalloc(&d->psi, tn) == hipSuccess && hipMalloc(&d->psiS, tn) == hipSuccess &&
               hipMalloc(&d->ipsi, tn) == hipSuccess && hipMalloc(&d->ipsiS, tn) == hipSuccess &&
               hipMalloc(&d->ninv, d->np * 8) == hipSuccess &&
-              hipMalloc(&d->ninvS, d->np * 8) == hipSuccess;
+              hipMalloc(&d->ninvS, d->np * 8) == hipSuccess && hipMalloc(&d->psiD, tn) == hipSuccess &&
+              hipMalloc(&d->psiQ, tn) == hipSuccess && hipMalloc(&d->ipsiD, tn) == hipSuccess &&
+              hipMalloc(&d->ipsiQ, tn) == hipSuccess && hipMalloc(&d->qinvD, d->np * 8) == hipSuccess &&
+              hipMalloc(&d->ninvD, d->np * 8) == hipSuccess && hipMalloc(&d->ninvQ, d->np * 8) == hipSuccess;
     d->ringCap = (size_t)16 << 20;
     d->bounceCap = (size_t)32 << 20;
     ok = ok &&
@@ -957,6 +1146,34 @@ sfp_dev* sfp_create(int device, const sfp_tables* t) {
     hostToDev(d, d->ipsiS, t->ipsi_rev_shoup, tn);
     hostToDev(d, d->ninv, t->n_inv, d->np * 8);
     hostToDev(d, d->ninvS, t->n_inv_shoup, d->np * 8);
+    {
+        std::vector<double> a((size_t)d->np * d->n), b((size_t)d->np * d->n), qi(d->np), ni(d->np), nq(d->np);
+        auto fill = [&](const uint64_t* tab, double* A, double* Bq) {
+            for (uint32_t p = 0; p < d->np; ++p) {
+                const double q = (double)d->hbar[p].q;
+                for (uint32_t k = 0; k < d->n; ++k) {
+                    const size_t o = (size_t)p * d->n + k;
+                    A[o] = (double)tab[o];
+                    Bq[o] = (double)tab[o] / q;
+                }
+            }
+        };
+        fill(t->psi_rev, a.data(), b.data());
+        hostToDev(d, d->psiD, a.data(), tn);
+        hostToDev(d, d->psiQ, b.data(), tn);
+        fill(t->ipsi_rev, a.data(), b.data());
+        hostToDev(d, d->ipsiD, a.data(), tn);
+        hostToDev(d, d->ipsiQ, b.data(), tn);
+        for (uint32_t p = 0; p < d->np; ++p) {
+            const double q = (double)d->hbar[p].q;
+            qi[p] = 1.0 / q;
+            ni[p] = (double)t->n_inv[p];
+            nq[p] = (double)t->n_inv[p] / q;
+        }
+        hostToDev(d, d->qinvD, qi.data(), d->np * 8);
+        hostToDev(d, d->ninvD, ni.data(), d->np * 8);
+        hostToDev(d, d->ninvQ, nq.data(), d->np * 8);
+    }
     if (!d->err.empty()) {
         sfp_destroy(d);
         return nullptr;
@@ -980,6 +1197,7 @@ void sfp_destroy(sfp_dev* d) {
     hipFree(d->ipsiS);
     hipFree(d->ninv);
     hipFree(d->ninvS);
+    for (double* x : {d->psiD, d->psiQ, d->ipsiD, d->ipsiQ, d->qinvD, d->ninvD, d->ninvQ}) hipFree(x);
     hipFree(d->dring);
     hipHostFree(d->hring);
     hipHostFree(d->bounce);
@@ -1057,6 +1275,15 @@ const char* sfp_last_error(sfp_dev* d) {
 }
 
 // ---- NTT ----
+// FP64 butterflies for primes < 2^42 (SFHE_NTT_FP=0 selects the integer path)
+static int nttFp() {
+    static const int on = [] {
+        const char* v = std::getenv("SFHE_NTT_FP");
+        return v ? std::atoi(v) : SFHE_NTT_FP;
+    }();
+    return on;
+}
+
 static RowGroup rowsOf(uint32_t P, uint32_t R, sfp_limbs pm) {
     RowGroup G;
     std::memset(&G, 0, sizeof G);
@@ -1075,10 +1302,12 @@ static void nttRows(sfp_dev* d, const RowGroup& G, int inverse) {
     const double bytes = 16.0 * rows * d->n;
     const u64* tw = inverse ? d->ipsi : d->psi;
     const u64* twS = inverse ? d->ipsiS : d->psiS;
+    const double* twD = inverse ? d->ipsiD : d->psiD;
+    const double* twQ = inverse ? d->ipsiQ : d->psiQ;
     auto pass = [&](auto kern) {
         timedLaunch(d, SFP_FAM_NTT, bytes, [&] {
             hipLaunchKernelGGL(kern, g, dim3(kNttThreads), 0, d->st(), G, d->bar, tw, twS, d->ninv,
-                               d->ninvS, d->logn);
+                               d->ninvS, d->logn, twD, twQ, d->qinvD, d->ninvD, d->ninvQ, nttFp());
         });
     };
     if (!inverse) {
@@ -1176,6 +1405,26 @@ void sfp_lin_wsum(sfp_dev* d, uint64_t* out, const uint64_t* const* ins, const u
     hipLaunchKernelGGL(k_lin_wsum, dim3(ewGrid(total)), dim3(kThreads), 0, d->st(), out, pl, dk, nin,
                        m, d->bar, d->logn);
     checkLaunch(d, "lin_wsum");
+}
+
+void sfp_lin_wsum_multi(sfp_dev* d, uint64_t* out, size_t outStride, size_t polyStride,
+                        const uint64_t* const* in0, const uint64_t* const* in1, uint32_t nin,
+                        const uint64_t* k, uint32_t nout, sfp_limbs m) {
+    if (!nout || !nin) return;
+    if (nin > SFP_MAX_WSUM || !limbsOk(d, m, "lin_wsum_multi")) {
+        record(d, "lin_wsum_multi", hipErrorInvalidValue);
+        return;
+    }
+    PtrList2 pl;
+    for (uint32_t j = 0; j < nin; ++j) {
+        pl.a[j] = in0[j];
+        pl.b[j] = in1[j];
+    }
+    const u64* dk = (const u64*)ringPut(d, k, (size_t)nout * nin * m.count * 8);
+    const dim3 g(d->n / kThreads, m.count, (nout + kWsumChunk - 1) / kWsumChunk);
+    hipLaunchKernelGGL(k_lin_wsum_multi, g, dim3(kThreads), 0, d->st(), out, outStride, polyStride, pl, dk,
+                       nin, nout, m, d->bar, d->logn);
+    checkLaunch(d, "lin_wsum_multi");
 }
 
 void sfp_mac_plain(sfp_dev* d, uint64_t* out, const uint64_t* const* a, const uint64_t* const* b,

@@ -99,6 +99,14 @@ void sfp_tensor(sfp_dev* d, uint64_t* d0, uint64_t* d1, uint64_t* d2, const uint
 // ins: host array of device pointers; k: host array nin x m.count.
 void sfp_lin_wsum(sfp_dev* d, uint64_t* out, const uint64_t* const* ins, const uint64_t* k,
                   uint32_t nin, sfp_limbs m);
+// Several weighted sums of the same ciphertext inputs in one pass (the
+// Chebyshev leaves): for o < nout, p in {0, 1}:
+//   out + o*out_stride + p*poly_stride  =  sum_j in_p[j] * k[o][j][limb]
+// in0/in1: host arrays of nin device pointers (c0 / c1 of each input),
+// nin <= SFP_MAX_WSUM; k: host array nout x nin x m.count.
+void sfp_lin_wsum_multi(sfp_dev* d, uint64_t* out, size_t out_stride, size_t poly_stride,
+                        const uint64_t* const* in0, const uint64_t* const* in1, uint32_t nin,
+                        const uint64_t* k, uint32_t nout, sfp_limbs m);
 
 // out = sum_j a[j] * b[j]  (pointwise products summed, nin <= SFP_MAX_WSUM).
 // a, b: host arrays of device pointers.
