@@ -19,6 +19,9 @@
 #pragma once
 
 #include <algorithm>
+#include <exception>
+#include <mutex>
+#include <thread>
 #include <map>
 #include <array>
 #include <chrono>
@@ -105,6 +108,48 @@ inline const SizeParams* sizeParams(int N) {
 
 // ---------------------------------------------------------------------------
 namespace sfhe {
+// Runs body(b) for b < count, batch b on lane b % lanes.  By default one host
+// thread issues the batches in order (the GPU already overlaps the lanes:
+// issuing is ~3x faster than the device work).  SFHE_HOST_THREADS=1 gives
+// each lane its own host thread (the reference's OpenMP batch loop); the
+// first exception is rethrown after all threads join.
+inline bool hostThreads() {
+    static const bool on = [] {
+        const char* v = std::getenv("SFHE_HOST_THREADS");
+        return v && *v && *v != '0';
+    }();
+    return on;
+}
+
+template <class F>
+void parallelLanes(const CryptoContext<DCRTPoly>& cc, int lanes, int count, F&& body) {
+    if (!hostThreads() || lanes <= 1) {
+        for (int b = 0; b < count; ++b) {
+            cc->SetLane(b % lanes);
+            body(b);
+        }
+        cc->SetLane(0);
+        return;
+    }
+    std::exception_ptr err;
+    std::mutex em;
+    auto run = [&](int t) {
+        try {
+            cc->SetLane(t);
+            for (int b = t; b < count; b += lanes) body(b);
+        } catch (...) {
+            std::lock_guard<std::mutex> g(em);
+            if (!err) err = std::current_exception();
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < lanes; ++t) th.emplace_back(run, t);
+    run(0);
+    for (auto& x : th) x.join();
+    cc->SetLane(0);
+    if (err) std::rethrow_exception(err);
+}
+
 // SFHE_PHASES=1: device-synchronised wall time of each sort phase on stderr
 // (diagnostics only; adds synchronisation, so never on in benchmarks).
 class PhaseTimer {
@@ -242,18 +287,28 @@ class DirectSort : public SortBase<N> {
     // their Plaintexts (and with them the device encodings) are kept across
     // sorts: repeated sorts skip mask generation, rotation and re-encoding.
     std::map<std::array<int, 5>, std::vector<Plaintext>> m_masks;
+    std::mutex m_masksMu;  // the batches' host threads share the memo
+    // Returns the memoised plaintexts for `key`, building them once with
+    // build(vec).  Filled under the lock; std::map references stay valid.
+    template <class F>
+    const std::vector<Plaintext>& maskMemo(const std::array<int, 5>& key, F&& build) {
+        std::lock_guard<std::mutex> g(m_masksMu);
+        auto& v = m_masks[key];
+        if (v.empty()) build(v);
+        return v;
+    }
 
     Ciphertext<DCRTPoly> vecRotsOpt(const std::vector<Ciphertext<DCRTPoly>>& pre,
                                     int num_partition, int num_slots, int np, int is) {
         std::vector<Ciphertext<DCRTPoly>> giants;
         for (int j = 0; j < num_partition / np; ++j) {
             const int shift = is * num_partition + j * np;
-            auto& masks = m_masks[{0, is, j, (int)pre[0]->GetLevel(), num_slots}];
-            if (masks.empty())
+            auto& masks = maskMemo({0, is, j, (int)pre[0]->GetLevel(), num_slots}, [&](auto& v) {
                 for (int i = 0; i < np; ++i)
-                    masks.push_back(m_cc->MakeCKKSPackedPlaintext(
+                    v.push_back(m_cc->MakeCKKSPackedPlaintext(
                         vectorRotate(generateMaskVector(num_slots, np * j + i), -shift), 1,
                         pre[i]->GetLevel(), nullptr, num_slots));
+            });
             auto T = m_cc->EvalMultAddPlain(pre, masks);
             T->SetSlots(num_slots);
             giants.push_back(rot.rotate(T, shift));
@@ -277,14 +332,12 @@ class DirectSort : public SortBase<N> {
         std::vector<Ciphertext<DCRTPoly>> parts(L.B);
         const int lanes = std::min(L.B, m_cc->LaneCount());
         m_cc->ForkLanes(lanes);
-        for (int b = 0; b < L.B; ++b) {
-            m_cc->SetLane(b % lanes);
+        sfhe::parallelLanes(m_cc, lanes, L.B, [&](int b) {
             auto shifted = vecRotsOpt(pre, L.P, L.S, L.npRank, b);
             auto dup = input_array->Clone();
             dup->SetSlots(L.S);
             parts[b] = comp.compare(m_cc, dup, shifted, SignFunc, Cfg);
-        }
-        m_cc->SetLane(0);
+        });
         m_cc->JoinLanes();
         for (int b = 0; b < L.B; ++b) m_cc->EvalAddInPlace(rank, parts[b]);
         ph.mark("rank: batches (vecRotsOpt+compare)");
@@ -301,12 +354,12 @@ class DirectSort : public SortBase<N> {
                                            int num_slots, int np, int ib, int num_partition) {
         std::vector<Ciphertext<DCRTPoly>> giants;
         for (int i = 0; i < (num_slots / N) / np; ++i) {
-            auto& masks = m_masks[{1, 0, i, (int)masked_inputs[0]->GetLevel(), num_slots}];
-            if (masks.empty())
+            auto& masks = maskMemo({1, 0, i, (int)masked_inputs[0]->GetLevel(), num_slots}, [&](auto& v) {
                 for (int j = 0; j < np; ++j)
-                    masks.push_back(m_cc->MakeCKKSPackedPlaintext(
+                    v.push_back(m_cc->MakeCKKSPackedPlaintext(
                         vectorRotate(generateMaskVectorN(num_slots, np * i + j), j), 1,
                         masked_inputs[j]->GetLevel(), nullptr, num_slots));
+            });
             auto tmp = m_cc->EvalMultAddPlain(masked_inputs, masks);
             giants.push_back(rot.rotate(tmp, ib * num_partition + i * np));
         }
@@ -320,11 +373,9 @@ class DirectSort : public SortBase<N> {
         const sfhe::RankLayout L(N, max_batch);
         sfhe::PhaseTimer ph(m_cc);
         auto output = this->getZero()->Clone();
-        auto& idxMemo = m_masks[{2, 0, 0, (int)ctx_Rank->GetLevel(), N}];
-        if (idxMemo.empty())
-            idxMemo.push_back(m_cc->MakeCKKSPackedPlaintext(generateIndexVector(), 1, ctx_Rank->GetLevel(),
-                                                            nullptr, N));
-        Plaintext idx = idxMemo[0];
+        Plaintext idx = maskMemo({2, 0, 0, (int)ctx_Rank->GetLevel(), N}, [&](auto& v) {
+            v.push_back(m_cc->MakeCKKSPackedPlaintext(generateIndexVector(), 1, ctx_Rank->GetLevel(), nullptr, N));
+        })[0];
         auto indexMinusRank = m_cc->EvalSub(idx, ctx_Rank);
         indexMinusRank->SetSlots(L.S);
         input_array->SetSlots(L.S);  // reference side effect (sort_algo.h:711)
@@ -333,13 +384,11 @@ class DirectSort : public SortBase<N> {
         std::vector<Ciphertext<DCRTPoly>> parts(L.B);
         const int lanes = std::min(L.B, m_cc->LaneCount());
         m_cc->ForkLanes(lanes);
-        for (int b = 0; b < L.B; ++b) {
-            m_cc->SetLane(b % lanes);
-            auto& chkMemo = m_masks[{3, b, 0, (int)indexMinusRank->GetLevel(), L.S}];
-            if (chkMemo.empty())
-                chkMemo.push_back(m_cc->MakeCKKSPackedPlaintext(generateCheckingVectorN(L.S, b * L.P), 1,
-                                                                indexMinusRank->GetLevel(), nullptr, L.S));
-            Plaintext chk = chkMemo[0];
+        sfhe::parallelLanes(m_cc, lanes, L.B, [&](int b) {
+            Plaintext chk = maskMemo({3, b, 0, (int)indexMinusRank->GetLevel(), L.S}, [&](auto& v) {
+                v.push_back(m_cc->MakeCKKSPackedPlaintext(generateCheckingVectorN(L.S, b * L.P), 1,
+                                                          indexMinusRank->GetLevel(), nullptr, L.S));
+            })[0];
             // (r - rank_r - c) / 2N  in (-1, 1/2)
             auto z = m_cc->EvalMult(m_cc->EvalSub(indexMinusRank, chk), 1.0 / N / 2);
             auto hit = m_cc->EvalChebyshevSeriesPS(z, sincCoeffs, -1, 1);
@@ -348,8 +397,7 @@ class DirectSort : public SortBase<N> {
             for (int i = 0; i < L.npPlace; ++i) amounts[i] = i;
             auto maskedRot = rot.rotateMany(masked, amounts);
             parts[b] = blindRotationOptN(maskedRot, L.S, L.npPlace, b, L.P);
-        }
-        m_cc->SetLane(0);
+        });
         m_cc->JoinLanes();
         for (int b = 0; b < L.B; ++b) m_cc->EvalAddInPlace(output, parts[b]);
         ph.mark("place: batches (sinc PS+mask+blind rotation)");

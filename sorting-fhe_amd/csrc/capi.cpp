@@ -439,7 +439,7 @@ int sfhe_kernel_timing(sfhe_ctx* c, uint32_t family, uint32_t period) {
     REQUIRE(c, "null context");
     REQUIRE(family < SFP_FAM_COUNT, "unknown kernel family");
     return guard([&] {
-        std::lock_guard<std::recursive_mutex> g(c->cc->state()->opMu);
+        OpLock g(c->cc->state());
         sfp_prof_set(c->cc->state()->dev, family, period);
     });
 }
@@ -449,7 +449,7 @@ int sfhe_kernel_timing_read(sfhe_ctx* c, uint32_t family, uint64_t* launches, ui
     REQUIRE(c, "null context");
     REQUIRE(family < SFP_FAM_COUNT, "unknown kernel family");
     return guard([&] {
-        std::lock_guard<std::recursive_mutex> g(c->cc->state()->opMu);
+        OpLock g(c->cc->state());
         sfp_prof_read(c->cc->state()->dev, family, launches, timed, ms, bytes);
     });
 }

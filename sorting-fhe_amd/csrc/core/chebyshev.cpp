@@ -300,7 +300,7 @@ class PSEvaluator {
 
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalChebyshevSeriesPS(
     const Ciphertext<DCRTPoly>& x, const std::vector<double>& coeffs, double a, double b) {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     std::vector<double> p(coeffs);
     while (!p.empty() && p.back() == 0.0) p.pop_back();
     if (p.empty()) SFHE_THROW("empty Chebyshev series");
@@ -352,7 +352,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalChebyshevFunction(
 
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalPolyLinear(
     const Ciphertext<DCRTPoly>& x, const std::vector<double>& coeffs) {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     std::vector<double> p(coeffs);
     while (!p.empty() && p.back() == 0.0) p.pop_back();
     if (p.size() < 2) SFHE_THROW("EvalPolyLinear needs degree >= 1");

@@ -150,7 +150,7 @@ DeviceBuffer::~DeviceBuffer() {
         st->dataflowFree.push_back({words, ptr});  // any lane may still read it: after the sub-join
     else if (!st->forkedLanes)
         st->freeList[0][words].push_back(ptr);  // everything is ordered behind lane 0 again
-    else if (region == st->region && lane == st->lane)
+    else if (region == st->region && lane == st->myLane())
         st->freeList[lane][words].push_back(ptr);  // private to this lane in this region
     else
         st->deferredFree.push_back({words, ptr});  // another lane may still use it: after the join
@@ -180,6 +180,17 @@ DeviceBufferPtr SfheContextState::alloc(size_t words) {
     auto b = std::make_shared<DeviceBuffer>(this, p, words, lane, forkedLanes ? region : 0);
     b->seq = ++laneSeq[lane];
     return b;
+}
+
+namespace {
+thread_local const SfheContextState* tCtx = nullptr;
+thread_local int tLane = 0;
+}  // namespace
+
+int SfheContextState::myLane() const { return tCtx == this ? tLane : 0; }
+void SfheContextState::setMyLane(int l) {
+    tCtx = this;
+    tLane = l;
 }
 
 void SfheContextState::laneWait(int waiter, int waitee) {
@@ -726,19 +737,20 @@ void CryptoContextImpl<DCRTPoly>::Synchronize() {
 int CryptoContextImpl<DCRTPoly>::LaneCount() const { return sfp_lanes(st->dev); }
 
 void CryptoContextImpl<DCRTPoly>::ForkLanes(int count) {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     SfheContextState* s = st.get();
     if (s->forkedLanes) SFHE_THROW("ForkLanes: a lane region is already open");
     count = std::max(1, std::min(count, sfp_lanes(s->dev)));
     sfp_set_lane(s->dev, 0);
     s->lane = 0;
+    s->setMyLane(0);
     for (int i = 1; i < count; ++i) s->laneWait(i, 0);
     s->forkedLanes = count;
     s->region = ++s->regionCount;
 }
 
 std::vector<int> CryptoContextImpl<DCRTPoly>::ForkHelpers() {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     SfheContextState* s = st.get();
     std::vector<int> lanes{s->lane};
     if (!s->dataflow) {
@@ -755,11 +767,12 @@ std::vector<int> CryptoContextImpl<DCRTPoly>::ForkHelpers() {
 }
 
 void CryptoContextImpl<DCRTPoly>::JoinHelpers(const std::vector<int>& lanes) {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     SfheContextState* s = st.get();
     if (!s->dataflow) return;
     const int parent = lanes.empty() ? s->lane : lanes[0];
     s->lane = parent;
+    s->setMyLane(parent);
     sfp_set_lane(s->dev, parent);
     for (size_t i = 1; i < lanes.size(); ++i) s->laneWait(parent, lanes[i]);
     if (--s->dataflow == 0) {
@@ -770,17 +783,18 @@ void CryptoContextImpl<DCRTPoly>::JoinHelpers(const std::vector<int>& lanes) {
 }
 
 void CryptoContextImpl<DCRTPoly>::SetLane(int lane) {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     SfheContextState* s = st.get();
     if (lane != 0 && !s->dataflow && (!s->forkedLanes || lane >= s->forkedLanes))
         SFHE_THROW("SetLane: lane " + std::to_string(lane) + " outside the open region");
     if (lane < 0 || lane >= sfp_lanes(s->dev)) SFHE_THROW("SetLane: no lane " + std::to_string(lane));
+    s->setMyLane(lane);
     s->lane = lane;
     sfp_set_lane(s->dev, lane);
 }
 
 void CryptoContextImpl<DCRTPoly>::JoinLanes() {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     SfheContextState* s = st.get();
     if (!s->forkedLanes) return;
     for (int i = 1; i < s->forkedLanes; ++i) s->laneWait(0, i);
@@ -794,12 +808,13 @@ void CryptoContextImpl<DCRTPoly>::JoinLanes() {
     for (auto& e : s->deferredFree) s->freeList[0][e.first].push_back(e.second);
     s->deferredFree.clear();
     s->lane = 0;
+    s->setMyLane(0);
     s->forkedLanes = 0;
     s->region = 0;
 }
 
 void CryptoContextImpl<DCRTPoly>::SetPlaintextCache(bool on) {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     st->ptCacheOn = on;
     if (!on) {
         st->ptCache.clear();
@@ -816,7 +831,7 @@ void CryptoContextImpl<DCRTPoly>::ResetOpStats() { st->stats = OpStats(); }
 // keys
 
 KeyPair<DCRTPoly> CryptoContextImpl<DCRTPoly>::KeyGen() {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     SfheContextState* s = st.get();
     const uint32_t NP = s->Lq + s->K;
     KeyPair<DCRTPoly> kp;
@@ -856,7 +871,7 @@ KeyPair<DCRTPoly> CryptoContextImpl<DCRTPoly>::KeyGen() {
 }
 
 void CryptoContextImpl<DCRTPoly>::EvalMultKeyGen(const PrivateKey<DCRTPoly>& sk) {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     SfheContextState* s = st.get();
     const uint32_t NP = s->Lq + s->K;
     auto s2 = s->alloc((size_t)NP * s->n);
@@ -867,7 +882,7 @@ void CryptoContextImpl<DCRTPoly>::EvalMultKeyGen(const PrivateKey<DCRTPoly>& sk)
 void CryptoContextImpl<DCRTPoly>::EvalRotateKeyGen(const PrivateKey<DCRTPoly>& sk,
                                                    const std::vector<int32_t>& idx,
                                                    const PublicKey<DCRTPoly>&) {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     SfheContextState* s = st.get();
     const uint32_t NP = s->Lq + s->K;
     auto sg = s->alloc((size_t)NP * s->n);
@@ -881,11 +896,11 @@ void CryptoContextImpl<DCRTPoly>::EvalRotateKeyGen(const PrivateKey<DCRTPoly>& s
 }
 
 void CryptoContextImpl<DCRTPoly>::ClearEvalMultKeys() {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     st->relinKey.reset();
 }
 void CryptoContextImpl<DCRTPoly>::ClearEvalAutomorphismKeys() {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     st->rotKeys.clear();
     st->rotIndices.clear();
 }
@@ -918,7 +933,7 @@ Plaintext CryptoContextImpl<DCRTPoly>::MakeCKKSPackedPlaintext(
 
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::Encrypt(const PublicKey<DCRTPoly>& pk,
                                                          const Plaintext& pt) {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     SfheContextState* s = st.get();
     if (!pk) SFHE_THROW("null public key");
     const uint32_t level = pt->level, ell = s->ellOf(level);
@@ -969,7 +984,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::Encrypt(const PublicKey<DCRTPo
 
 void CryptoContextImpl<DCRTPoly>::Decrypt(const PrivateKey<DCRTPoly>& sk,
                                           const Ciphertext<DCRTPoly>& ct, Plaintext* out) {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     SfheInternal::deps(st.get(), {&ct});
     SfheContextState* s = st.get();
     if (!sk) SFHE_THROW("null secret key");
@@ -1029,7 +1044,7 @@ std::ostream& operator<<(std::ostream& os, const Plaintext& pt) {
 }
 
 Ciphertext<DCRTPoly> CiphertextImpl<DCRTPoly>::Clone() const {
-    std::lock_guard<std::recursive_mutex> g(cc->state()->opMu);
+    OpLock g(cc->state());
     cc->state()->dep(buf.get());
     auto self = std::make_shared<CiphertextImpl<DCRTPoly>>(*this);
     return SfheInternal::copyOf(cc.get(), self);
@@ -1042,7 +1057,7 @@ uint32_t CiphertextImpl<DCRTPoly>::GetNumLimbs() const { return cc->state()->ell
 
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalAdd(const Ciphertext<DCRTPoly>& a0,
                                                          const Ciphertext<DCRTPoly>& b0) {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     SfheInternal::deps(st.get(), {&a0, &b0});
     auto a = a0, b = b0;
     SfheInternal::align(this, a, b);
@@ -1057,7 +1072,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalAdd(const Ciphertext<DCRTP
 
 void CryptoContextImpl<DCRTPoly>::EvalAddInPlace(Ciphertext<DCRTPoly>& a,
                                                  const Ciphertext<DCRTPoly>& b0) {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     SfheInternal::deps(st.get(), {&a, &b0});
     auto b = b0;
     // in place only on an exclusively owned buffer outside dataflow regions
@@ -1078,7 +1093,7 @@ void CryptoContextImpl<DCRTPoly>::EvalAddInPlace(Ciphertext<DCRTPoly>& a,
 
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalAdd(const Ciphertext<DCRTPoly>& a,
                                                          double c) {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     SfheInternal::deps(st.get(), {&a});
     const uint32_t ell = st->ellOf(a->level);
     auto out = SfheInternal::newCt(this, a->level, a->slots);
@@ -1096,7 +1111,7 @@ void CryptoContextImpl<DCRTPoly>::EvalAddInPlace(Ciphertext<DCRTPoly>& a, double
 
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalAdd(const Ciphertext<DCRTPoly>& a,
                                                          const Plaintext& p) {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     SfheInternal::deps(st.get(), {&a});
     const uint32_t ell = st->ellOf(a->level);
     const uint64_t* m = SfheInternal::encoded(this, p, a->level);
@@ -1114,7 +1129,7 @@ void CryptoContextImpl<DCRTPoly>::EvalAddInPlace(Ciphertext<DCRTPoly>& a, const 
 
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalSub(const Ciphertext<DCRTPoly>& a0,
                                                          const Ciphertext<DCRTPoly>& b0) {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     SfheInternal::deps(st.get(), {&a0, &b0});
     auto a = a0, b = b0;
     SfheInternal::align(this, a, b);
@@ -1133,7 +1148,7 @@ void CryptoContextImpl<DCRTPoly>::EvalSubInPlace(Ciphertext<DCRTPoly>& a,
 }
 
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalNegate(const Ciphertext<DCRTPoly>& a) {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     SfheInternal::deps(st.get(), {&a});
     const uint32_t ell = st->ellOf(a->level);
     auto out = SfheInternal::newCt(this, a->level, a->slots);
@@ -1151,7 +1166,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalSub(double c, const Cipher
 
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalSub(const Ciphertext<DCRTPoly>& a,
                                                          const Plaintext& p) {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     SfheInternal::deps(st.get(), {&a});
     const uint32_t ell = st->ellOf(a->level);
     const uint64_t* m = SfheInternal::encoded(this, p, a->level);
@@ -1165,7 +1180,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalSub(const Ciphertext<DCRTP
 
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalSub(const Plaintext& p,
                                                          const Ciphertext<DCRTPoly>& a) {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     SfheInternal::deps(st.get(), {&a});
     const uint32_t ell = st->ellOf(a->level);
     const uint64_t* m = SfheInternal::encoded(this, p, a->level);
@@ -1180,7 +1195,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalSub(const Plaintext& p,
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalAddMany(
     const std::vector<Ciphertext<DCRTPoly>>& v) {
     if (v.empty()) SFHE_THROW("EvalAddMany of an empty vector");
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     std::vector<Ciphertext<DCRTPoly>> cur(v.begin(), v.end());
     while (cur.size() > 1) {
         std::vector<Ciphertext<DCRTPoly>> nxt;
@@ -1196,7 +1211,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalAddMany(
 
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMult(const Ciphertext<DCRTPoly>& a,
                                                           double c) {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     SfheInternal::deps(st.get(), {&a});
     SfheContextState* s = st.get();
     const uint32_t ell = s->ellOf(a->level);
@@ -1220,7 +1235,7 @@ void CryptoContextImpl<DCRTPoly>::EvalMultInPlace(Ciphertext<DCRTPoly>& a, doubl
 
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMult(const Ciphertext<DCRTPoly>& a,
                                                           const Plaintext& p) {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     SfheInternal::deps(st.get(), {&a});
     SfheContextState* s = st.get();
     const uint32_t ell = s->ellOf(a->level);
@@ -1242,7 +1257,7 @@ void CryptoContextImpl<DCRTPoly>::EvalMultInPlace(Ciphertext<DCRTPoly>& a, const
 
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMult(const Ciphertext<DCRTPoly>& a0,
                                                           const Ciphertext<DCRTPoly>& b0) {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     SfheInternal::deps(st.get(), {&a0, &b0});
     SfheContextState* s = st.get();
     if (!s->relinKey) SFHE_THROW("EvalMultKeyGen must be called before EvalMult");
@@ -1267,7 +1282,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalSquare(const Ciphertext<DC
 
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMultAddPlain(
     const std::vector<Ciphertext<DCRTPoly>>& a, const std::vector<Plaintext>& p) {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     SfheInternal::depsv(st.get(), a);
     SfheContextState* s = st.get();
     if (a.empty() || a.size() != p.size()) SFHE_THROW("operand count mismatch");
@@ -1313,7 +1328,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMultAddPlain(
 
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotate(const Ciphertext<DCRTPoly>& a,
                                                             int32_t r) {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     SfheInternal::deps(st.get(), {&a});
     SfheContextState* s = st.get();
     uint32_t gal = GaloisForRotation(r);
@@ -1336,7 +1351,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotate(const Ciphertext<DC
 
 std::shared_ptr<FastRotationPrecomp> CryptoContextImpl<DCRTPoly>::EvalFastRotationPrecompute(
     const Ciphertext<DCRTPoly>& a) {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     SfheInternal::deps(st.get(), {&a});
     SfheContextState* s = st.get();
     auto pre = std::make_shared<FastRotationPrecomp>();
@@ -1354,7 +1369,7 @@ std::shared_ptr<FastRotationPrecomp> CryptoContextImpl<DCRTPoly>::EvalFastRotati
 
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalFastRotation(
     const Ciphertext<DCRTPoly>& a, int32_t r, uint32_t, const std::shared_ptr<FastRotationPrecomp>& pre) {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     SfheInternal::deps(st.get(), {&a});
     SfheContextState* s = st.get();
     uint32_t gal = GaloisForRotation(r);
@@ -1411,7 +1426,7 @@ void weightResidues(const SfheContextState* s, double w, uint32_t level, uint32_
 std::vector<Ciphertext<DCRTPoly>> CryptoContextImpl<DCRTPoly>::LinearWSumRescaleMulti(
     const std::vector<const uint64_t*>& in0, const std::vector<const uint64_t*>& in1,
     const std::vector<std::vector<double>>& w, uint32_t level, uint32_t slots) {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     SfheContextState* s = st.get();
     const uint32_t ell = s->ellOf(level), n = s->n;
     const uint32_t nin = (uint32_t)in0.size(), nout = (uint32_t)w.size();
@@ -1452,7 +1467,7 @@ std::vector<Ciphertext<DCRTPoly>> CryptoContextImpl<DCRTPoly>::LinearWSumRescale
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::LinearWSumRescale(
     const std::vector<const uint64_t*>& in0, const std::vector<const uint64_t*>& in1,
     const std::vector<double>& w, uint32_t level, uint32_t slots) {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     SfheContextState* s = st.get();
     const uint32_t ell = s->ellOf(level);
     if (ell < 2) SFHE_THROW("no levels left (multiplicative depth exhausted)");
@@ -1516,7 +1531,7 @@ void CryptoContextImpl<DCRTPoly>::LevelReduceInPlace(Ciphertext<DCRTPoly>& a, st
 
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::AdjustLevel(const Ciphertext<DCRTPoly>& a,
                                                              uint32_t targetLevel) {
-    std::lock_guard<std::recursive_mutex> g(st->opMu);
+    OpLock g(st.get());
     SfheInternal::deps(st.get(), {&a});
     auto r = SfheInternal::adjust(this, a, targetLevel);
     return r == a ? a->Clone() : r;

@@ -84,6 +84,8 @@ struct SfheContextState {
     uint64_t laneSeq[SFP_MAX_LANES] = {};
     uint64_t synced[SFP_MAX_LANES][SFP_MAX_LANES] = {};
     void laneWait(int waiter, int waitee);
+    int myLane() const;            // the calling thread's lane (0 unless SetLane)
+    void setMyLane(int l);
     void dep(DeviceBuffer* b);     // current lane waits for b's last writer if needed
     void wrote(DeviceBuffer* b);   // b was just written on the current lane
     size_t poolBytes = 0;
@@ -107,6 +109,20 @@ struct SfheContextState {
     DeviceBufferPtr alloc(size_t words);
     void releaseAll();
     void countBytes(double b) { stats.algo_bytes += b; }
+};
+
+// Serialises host-side use of a context and routes the calling thread's
+// operations to its lane (each host thread of a lane region has its own).
+class OpLock {
+  public:
+    explicit OpLock(SfheContextState* s) : s_(s), g_(s->opMu) {
+        s_->lane = s_->myLane();
+        sfp_set_lane(s_->dev, s_->lane);
+    }
+
+  private:
+    SfheContextState* s_;
+    std::lock_guard<std::recursive_mutex> g_;
 };
 
 // splitmix64 (used for deterministic host sampling; identical in the oracle)

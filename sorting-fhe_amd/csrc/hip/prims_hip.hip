@@ -87,6 +87,7 @@ struct sfp_dev {
     int nLanes = 1, cur = 0;
     hipStream_t st() const { return streams[cur]; }
     std::vector<sfp_event*> evFree;
+    std::mutex evMu;  // evFree: buffers release events from any host thread
     uint32_t n = 0, logn = 0, np = 0;
     sf_barrett* bar = nullptr;  // device [np]
     u64 *psi = nullptr, *psiS = nullptr, *ipsi = nullptr, *ipsiS = nullptr;
@@ -1231,15 +1232,26 @@ void sfp_set_lane(sfp_dev* d, int lane) {
         return;
     }
     d->cur = lane;
+    // HIP's current device is per host thread; a lane may be driven from a
+    // thread other than the one that created the device
+    thread_local int curDev = -1;
+    if (curDev != d->device) {
+        SFP_CHECK(hipSetDevice(d->device));
+        curDev = d->device;
+    }
 }
 int sfp_get_lane(sfp_dev* d) { return d->cur; }
 
 sfp_event* sfp_event_record(sfp_dev* d) {
-    sfp_event* e;
-    if (!d->evFree.empty()) {
-        e = d->evFree.back();
-        d->evFree.pop_back();
-    } else {
+    sfp_event* e = nullptr;
+    {
+        std::lock_guard<std::mutex> g(d->evMu);
+        if (!d->evFree.empty()) {
+            e = d->evFree.back();
+            d->evFree.pop_back();
+        }
+    }
+    if (!e) {
         e = new sfp_event;
         SFP_CHECK(hipEventCreateWithFlags(&e->e, hipEventDisableTiming));
     }
@@ -1255,7 +1267,9 @@ int sfp_event_done(sfp_dev* d, const sfp_event* e) {
     return !e || hipEventQuery(e->e) == hipSuccess;
 }
 void sfp_event_free(sfp_dev* d, sfp_event* e) {
-    if (e) d->evFree.push_back(e);  // re-recording later is safe: waits bind at enqueue time
+    if (!e) return;
+    std::lock_guard<std::mutex> g(d->evMu);
+    d->evFree.push_back(e);  // re-recording later is safe: waits bind at enqueue time
 }
 void sfp_lane_wait(sfp_dev* d, int waiter, int waitee) {
     if (waiter == waitee) return;
