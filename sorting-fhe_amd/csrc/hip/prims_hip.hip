@@ -228,17 +228,20 @@ static unsigned gridFor(size_t work, unsigned perBlock) {
 // ============================================================================
 // NTT kernels
 
-// One pass of the negacyclic NTT over 4096-word tiles.
+// One pass of the negacyclic NTT over 2048-word tiles.
 //
 // n = R * 256 is viewed as R rows of 256 words.  The forward transform is the
 // bit-reversed-twiddle Cooley-Tukey schedule: global stage S (0..logn-1) pairs
 // x with x + n/2^(S+1) and uses psi_rev[2^S + (x >> (logn - S))].
-//   COL pass: stages 0..logR-1; a tile is C = 4096/R whole columns (R x C).
-//   ROW pass: stages logR..logn-1; a tile is 16 whole rows (16 x 256).
-// A 512-thread block stages the tile in LDS (XOR-swizzled: every round's
-// 32-lane access pattern hits distinct banks) and runs its stages in rounds
-// of up to three: each thread pulls 8 words into registers, runs the round's
-// radix-2 stages there and writes them back.  Butterflies are lazy (Harvey):
+//   COL pass: stages 0..logR-1; a tile is C = 2048/R whole columns (R x C).
+//   ROW pass: stages logR..logn-1; a tile is 8 whole rows (8 x 256).
+// A block stages the tile in LDS (XOR-swizzled) with 16-byte coalesced loads
+// and runs its stages in register rounds of up to LE stages: each thread pulls
+// 2^LE words into registers, runs the round's radix-2 stages there and writes
+// them back.  The tile size and LE were chosen by measurement (tools/
+// microbench): a pass over few rows is latency-bound, so smaller tiles (more
+// CUs) and more threads per tile win; 4096-word tiles or direct-from-HBM
+// rounds were slower at every size.  Butterflies are lazy (Harvey):
 // forward values live in [0, 4q), inverse values in [0, 2q); the pass that
 // finishes the transform reduces to [0, q).  The inverse runs the
 // Gentleman-Sande stages in reverse order (ROW pass first) and folds n^-1
@@ -246,20 +249,15 @@ static unsigned gridFor(size_t work, unsigned perBlock) {
 #ifndef SFHE_NTT_FP
 #define SFHE_NTT_FP 1  // FP64 butterflies for primes < 2^42
 #endif
-#ifndef SFHE_NTT_EXP
-#define SFHE_NTT_EXP 0  // experiments only: 1 no butterflies, 2 no twiddle loads, 3 no rounds
-#endif
-#ifndef SFHE_NTT_LOGE
-#define SFHE_NTT_LOGE 3
-#endif
-constexpr int kNttLogE = SFHE_NTT_LOGE;         // stages per register round
-constexpr int kNttE = 1 << kNttLogE;            // words per thread per round
 #ifndef SFHE_NTT_TILE
-#define SFHE_NTT_TILE 4096
+#define SFHE_NTT_TILE 2048
 #endif
 constexpr int kNttTile = SFHE_NTT_TILE;         // words per tile (one block)
 constexpr int kNttRows = kNttTile / 256;        // ROW pass: whole rows per tile
-constexpr int kNttThreads = kNttTile / kNttE;   // threads per tile
+// LE = stages per register round (2^LE words per thread, kNttTile >> LE
+// threads).  Launches of few rows are latency-bound and run LE = 2 (twice the
+// waves per tile); larger ones run LE = 3 (fewer rounds and barriers).
+constexpr int kNttSmallRows = 12;
 
 __device__ __forceinline__ uint32_t ldsSw(uint32_t e) {
     const uint32_t x = e >> 5;
@@ -282,13 +280,28 @@ __device__ __forceinline__ uint32_t nttLocal(const NttTile& T, uint32_t st, uint
     return COL ? u * T.C + st : st * 256u + u;
 }
 
+// Stage k of the pass (global stage S = S0 + k) at global index x0 uses
+// psi_rev[2^S + (x0 >> (logn - S))].
+//   COL (S0 = 0): x0 >> (logn - k) < 2^k: the pass needs only the table's
+//       entries [1, 2^logR), shared by every tile -> staged in LDS once per
+//       block (LDS word (2^k - 1) + ...), so its rounds never wait on HBM;
+//   ROW (S0 = logR): 8 * 255 distinct entries per tile (twice the tile's own
+//       bytes); staging them cost more occupancy than it saved, so the ROW
+//       rounds read the table directly (index 2^S + (x0 >> (8 - k))).
+constexpr uint32_t kNttColTw = 512;  // 2^logR - 1 entries, logR <= 9
+template <bool COL>
+__device__ __forceinline__ uint32_t twIndex(const NttTile& T, uint32_t S0, uint32_t k, uint32_t x0) {
+    if (COL) return (1u << k) - 1 + (x0 >> (T.logn - k));
+    return (1u << (S0 + k)) + (x0 >> (8 - k));
+}
+
 // One round: stages k0..k0+B-1 of the pass (k relative to the pass's first
 // global stage S0).  8/2^B groups of 2^B words per thread.
-template <bool INV, bool COL, int B>
+template <bool INV, bool COL, int LE, int B>
 __device__ __forceinline__ void nttRound(u64* s, const NttTile& T, uint32_t S0, uint32_t k0, u64 q,
-                                         const u64* __restrict__ w, const u64* __restrict__ wS) {
+                                         const u64* w, const u64* wS) {
     constexpr int M = 1 << B;
-    constexpr int GPT = kNttE / M;  // groups per thread
+    constexpr int GPT = (1 << LE) / M;  // groups per thread
     const uint32_t D = 1u << T.d;
     const uint32_t logh = T.d - k0 - B;
     const uint32_t h = 1u << logh;        // smallest stride of the round (in u)
@@ -296,7 +309,7 @@ __device__ __forceinline__ void nttRound(u64* s, const NttTile& T, uint32_t S0, 
     const u64 q2 = 2 * q;
 #pragma unroll
     for (int gi = 0; gi < GPT; ++gi) {
-        const uint32_t gid = threadIdx.x + gi * kNttThreads;
+        const uint32_t gid = threadIdx.x + gi * (kNttTile >> LE);
         uint32_t st, lo, hi;
         if (COL) {  // every extent is a power of two: shifts and masks only
             st = gid & (T.C - 1);
@@ -311,32 +324,21 @@ __device__ __forceinline__ void nttRound(u64* s, const NttTile& T, uint32_t S0, 
         }
         const uint32_t ub = hi * span + lo;
         // stage t of the round uses psi_rev[2^S + (x0 >> (logn-S)) + (j >> (B-t))]
-        // (x0 = member 0's global index): 2^t distinct twiddles, all loaded
-        // up front so the round waits on one memory latency, not B
+        // (x0 = member 0's global index): 2^t distinct twiddles (LDS)
         const uint32_t x0 = nttGlobal<COL>(T, st, ub);
         u64 W[M - 1], WS[M - 1];  // stage t's q-th twiddle at (1<<t)-1+q
 #pragma unroll
         for (int t = 0; t < B; ++t) {
-            const uint32_t S = S0 + k0 + t;
-            const uint32_t tb = (1u << S) + (x0 >> (T.logn - S));
+            const uint32_t tb = twIndex<COL>(T, S0, k0 + t, x0);
 #pragma unroll
             for (int qd = 0; qd < (1 << t); ++qd) {
-#if SFHE_NTT_EXP >= 2
-                W[(1 << t) - 1 + qd] = tb + qd;
-                WS[(1 << t) - 1 + qd] = tb;
-#else
                 W[(1 << t) - 1 + qd] = w[tb + qd];
                 WS[(1 << t) - 1 + qd] = wS[tb + qd];
-#endif
             }
         }
         u64 v[M];
 #pragma unroll
         for (int j = 0; j < M; ++j) v[j] = s[ldsSw(nttLocal<COL>(T, st, ub + j * h))];
-#if SFHE_NTT_EXP >= 1
-        v[0] ^= W[0] ^ WS[0];
-        if (false)
-#endif
         if (!INV) {
             // Harvey CT butterfly: in [0,4q) -> out [0,4q)
 #pragma unroll
@@ -374,14 +376,14 @@ __device__ __forceinline__ void nttRound(u64* s, const NttTile& T, uint32_t S0, 
     }
 }
 
-template <bool INV, bool COL>
+template <bool INV, bool COL, int LE>
 __device__ __forceinline__ void nttRoundDyn(int b, u64* s, const NttTile& T, uint32_t S0, uint32_t k0,
                                             u64 q, const u64* w, const u64* wS) {
-    if constexpr (kNttLogE >= 3) {
-        if (b == 3) return nttRound<INV, COL, 3>(s, T, S0, k0, q, w, wS);
+    if constexpr (LE >= 3) {
+        if (b == 3) return nttRound<INV, COL, LE, 3>(s, T, S0, k0, q, w, wS);
     }
-    if (b == 2) return nttRound<INV, COL, 2>(s, T, S0, k0, q, w, wS);
-    nttRound<INV, COL, 1>(s, T, S0, k0, q, w, wS);
+    if (b == 2) return nttRound<INV, COL, LE, 2>(s, T, S0, k0, q, w, wS);
+    nttRound<INV, COL, LE, 1>(s, T, S0, k0, q, w, wS);
 }
 
 // ---- FP64 butterflies (primes q < 2^42) ------------------------------------
@@ -407,18 +409,18 @@ __device__ __forceinline__ double fpReduce(double v, double q, double qinv) {
     return r < 0.0 ? r + q : r;
 }
 
-template <bool INV, bool COL, int B>
+template <bool INV, bool COL, int LE, int B>
 __device__ __forceinline__ void nttRoundFP(double* s, const NttTile& T, uint32_t S0, uint32_t k0, double q,
-                                           const double* __restrict__ w, const double* __restrict__ wq) {
+                                           const double* w, const double* wq) {
     constexpr int M = 1 << B;
-    constexpr int GPT = kNttE / M;
+    constexpr int GPT = (1 << LE) / M;
     const uint32_t D = 1u << T.d;
     const uint32_t logh = T.d - k0 - B;
     const uint32_t h = 1u << logh;
     const uint32_t span = D >> k0;
 #pragma unroll
     for (int gi = 0; gi < GPT; ++gi) {
-        const uint32_t gid = threadIdx.x + gi * kNttThreads;
+        const uint32_t gid = threadIdx.x + gi * (kNttTile >> LE);
         uint32_t st, lo, hi;
         if (COL) {
             st = gid & (T.C - 1);
@@ -436,8 +438,7 @@ __device__ __forceinline__ void nttRoundFP(double* s, const NttTile& T, uint32_t
         double W[M - 1], WQ[M - 1];
 #pragma unroll
         for (int t = 0; t < B; ++t) {
-            const uint32_t S = S0 + k0 + t;
-            const uint32_t tb = (1u << S) + (x0 >> (T.logn - S));
+            const uint32_t tb = twIndex<COL>(T, S0, k0 + t, x0);
 #pragma unroll
             for (int qd = 0; qd < (1 << t); ++qd) {
                 W[(1 << t) - 1 + qd] = w[tb + qd];
@@ -480,14 +481,14 @@ __device__ __forceinline__ void nttRoundFP(double* s, const NttTile& T, uint32_t
     }
 }
 
-template <bool INV, bool COL>
+template <bool INV, bool COL, int LE>
 __device__ __forceinline__ void nttRoundDynFP(int b, double* s, const NttTile& T, uint32_t S0, uint32_t k0,
                                               double q, const double* w, const double* wq) {
-    if constexpr (kNttLogE >= 3) {
-        if (b == 3) return nttRoundFP<INV, COL, 3>(s, T, S0, k0, q, w, wq);
+    if constexpr (LE >= 3) {
+        if (b == 3) return nttRoundFP<INV, COL, LE, 3>(s, T, S0, k0, q, w, wq);
     }
-    if (b == 2) return nttRoundFP<INV, COL, 2>(s, T, S0, k0, q, w, wq);
-    nttRoundFP<INV, COL, 1>(s, T, S0, k0, q, w, wq);
+    if (b == 2) return nttRoundFP<INV, COL, LE, 2>(s, T, S0, k0, q, w, wq);
+    nttRoundFP<INV, COL, LE, 1>(s, T, S0, k0, q, w, wq);
 }
 
 // A 2-D set of rows for one NTT launch, passed by value: row (p, i) for
@@ -518,8 +519,22 @@ __device__ __forceinline__ u64* rowAt(const RowPtr& r, uint32_t p, uint32_t i) {
     return const_cast<u64*>(r.base) + p * r.ps + i * r.is;
 }
 
-template <bool INV, bool COL>
-__global__ __launch_bounds__(kNttThreads) void k_ntt(const RowGroup G, const sf_barrett* __restrict__ bar,
+// Developer build knob: SFHE_NTT_TRACE accumulates per-phase shader clocks
+// of every block (thread 0, after each barrier) for tools/microbench.
+#ifdef SFHE_NTT_TRACE
+__device__ unsigned long long g_nttTrace[4][8];
+#define NTT_MARK(i)                                                          \
+    if (threadIdx.x == 0) {                                                  \
+        const unsigned long long t_ = clock64();                             \
+        atomicAdd(&g_nttTrace[INV * 2 + COL][(i)], t_ - tprev);              \
+        tprev = t_;                                                          \
+    }
+#else
+#define NTT_MARK(i)
+#endif
+
+template <bool INV, bool COL, int LE>
+__global__ __launch_bounds__(kNttTile >> LE) void k_ntt(const RowGroup G, const sf_barrett* __restrict__ bar,
                                                   const u64* __restrict__ tw, const u64* __restrict__ twS,
                                                   const u64* __restrict__ ninv,
                                                   const u64* __restrict__ ninvS, uint32_t logn,
@@ -529,6 +544,10 @@ __global__ __launch_bounds__(kNttThreads) void k_ntt(const RowGroup G, const sf_
                                                   const double* __restrict__ ninvD,
                                                   const double* __restrict__ ninvQ, int useFp) {
     __shared__ u64 s[kNttTile];
+    __shared__ u64 tW[COL ? kNttColTw : 1], tX[COL ? kNttColTw : 1];  // COL twiddles (value, Shoup or W/q)
+#ifdef SFHE_NTT_TRACE
+    unsigned long long tprev = clock64();
+#endif
     constexpr bool FIRST = (COL != INV);  // forward: COL first; inverse: ROW first
     const uint32_t n = 1u << logn;
     const uint32_t logR = logn - 8;
@@ -538,8 +557,6 @@ __global__ __launch_bounds__(kNttThreads) void k_ntt(const RowGroup G, const sf_
     const uint32_t prime = primeOf(G.pm, ii);
     const u64 q = bar[prime].q;
     const bool fp = useFp && q < kFpPrimeBound;  // uniform per block
-    const u64* w = tw + (size_t)prime * n;
-    const u64* wS = twS + (size_t)prime * n;
     NttTile T;
     T.logn = logn;
     T.d = COL ? logR : 8u;
@@ -548,6 +565,18 @@ __global__ __launch_bounds__(kNttThreads) void k_ntt(const RowGroup G, const sf_
     T.c0 = COL ? blockIdx.x * T.C : 0u;
     T.r0 = COL ? 0u : blockIdx.x * kNttRows;
     const uint32_t S0 = COL ? 0u : logR;
+
+    // the pass's twiddle table (value, Shoup companion or W/q) for this prime
+    const u64* gw = fp ? reinterpret_cast<const u64*>(twD) + (size_t)prime * n : tw + (size_t)prime * n;
+    const u64* gx = fp ? reinterpret_cast<const u64*>(twQ) + (size_t)prime * n : twS + (size_t)prime * n;
+    if (COL) {  // entries [1, 2^logR) -> LDS
+        for (uint32_t e = threadIdx.x; e < (1u << logR) - 1; e += (kNttTile >> LE)) {
+            tW[e] = gw[e + 1];
+            tX[e] = gx[e + 1];
+        }
+    }
+    const u64* rw = COL ? tW : gw;
+    const u64* rx = COL ? tX : gx;
 
     const u64* in = FIRST ? rowAt(G.src, pp, ii) : rowAt(G.dst, pp, ii);
     u64* cp = nullptr;
@@ -564,8 +593,8 @@ __global__ __launch_bounds__(kNttThreads) void k_ntt(const RowGroup G, const sf_
 
     // global -> LDS, 16 B per lane; tile-linear word e is row-major (u, st)
 #pragma unroll
-    for (int k = 0; k < kNttTile / 2 / kNttThreads; ++k) {
-        const uint32_t e = 2 * (threadIdx.x + k * kNttThreads);
+    for (int k = 0; k < (1 << LE) / 2; ++k) {
+        const uint32_t e = 2 * (threadIdx.x + k * (kNttTile >> LE));
         const size_t g = COL ? (size_t)(e >> T.logC) * 256 + T.c0 + (e & (T.C - 1)) : (size_t)T.r0 * 256 + e;
         ulonglong2 x = *reinterpret_cast<const ulonglong2*>(in + g);
         if (FIRST) {
@@ -587,21 +616,19 @@ __global__ __launch_bounds__(kNttThreads) void k_ntt(const RowGroup G, const sf_
         }
     }
     __syncthreads();
-#if SFHE_NTT_EXP >= 3
-    const uint32_t nr = 0;
-#else
-    const uint32_t nr = (T.d + kNttLogE - 1) / kNttLogE;
-#endif
+    NTT_MARK(0);
+    const uint32_t nr = (T.d + LE - 1) / LE;
     for (uint32_t ri = 0; ri < nr; ++ri) {
         const uint32_t r = INV ? nr - 1 - ri : ri;
-        const uint32_t k0 = kNttLogE * r;
-        const int b = (int)min((uint32_t)kNttLogE, T.d - k0);
+        const uint32_t k0 = LE * r;
+        const int b = (int)min((uint32_t)LE, T.d - k0);
         if (fp)
-            nttRoundDynFP<INV, COL>(b, reinterpret_cast<double*>(s), T, S0, k0, (double)q,
-                                    twD + (size_t)prime * n, twQ + (size_t)prime * n);
+            nttRoundDynFP<INV, COL, LE>(b, reinterpret_cast<double*>(s), T, S0, k0, (double)q,
+                                        reinterpret_cast<const double*>(rw), reinterpret_cast<const double*>(rx));
         else
-            nttRoundDyn<INV, COL>(b, s, T, S0, k0, q, w, wS);
+            nttRoundDyn<INV, COL, LE>(b, s, T, S0, k0, q, rw, rx);
         __syncthreads();
+        NTT_MARK(1 + ri);
     }
     const bool scale = INV && COL;
     const u64 ni = scale ? ninv[prime] : 0, niS = scale ? ninvS[prime] : 0;
@@ -610,8 +637,8 @@ __global__ __launch_bounds__(kNttThreads) void k_ntt(const RowGroup G, const sf_
     const u64* ein = epi ? rowAt(G.ein, pp, ii) : nullptr;
     const u64 ek = epi ? G.k[ii] : 0, ekS = epi ? G.kS[ii] : 0;
 #pragma unroll
-    for (int k = 0; k < kNttTile / 2 / kNttThreads; ++k) {
-        const uint32_t e = 2 * (threadIdx.x + k * kNttThreads);
+    for (int k = 0; k < (1 << LE) / 2; ++k) {
+        const uint32_t e = 2 * (threadIdx.x + k * (kNttTile >> LE));
         const size_t g = COL ? (size_t)(e >> T.logC) * 256 + T.c0 + (e & (T.C - 1)) : (size_t)T.r0 * 256 + e;
         ulonglong2 x;
         x.x = s[ldsSw(e)];
@@ -648,6 +675,10 @@ __global__ __launch_bounds__(kNttThreads) void k_ntt(const RowGroup G, const sf_
         }
         *reinterpret_cast<ulonglong2*>(out + g) = x;
     }
+    NTT_MARK(5);
+#ifdef SFHE_NTT_TRACE
+    if (threadIdx.x == 0) atomicAdd(&g_nttTrace[INV * 2 + COL][7], 1ull);
+#endif
 }
 
 // ============================================================================
@@ -1318,18 +1349,29 @@ static void nttRows(sfp_dev* d, const RowGroup& G, int inverse) {
     const u64* twS = inverse ? d->ipsiS : d->psiS;
     const double* twD = inverse ? d->ipsiD : d->psiD;
     const double* twQ = inverse ? d->ipsiQ : d->psiQ;
-    auto pass = [&](auto kern) {
+    const bool small = rows < (uint32_t)kNttSmallRows;
+    auto pass = [&](auto kern, int le) {
         timedLaunch(d, SFP_FAM_NTT, bytes, [&] {
-            hipLaunchKernelGGL(kern, g, dim3(kNttThreads), 0, d->st(), G, d->bar, tw, twS, d->ninv,
+            hipLaunchKernelGGL(kern, g, dim3(kNttTile >> le), 0, d->st(), G, d->bar, tw, twS, d->ninv,
                                d->ninvS, d->logn, twD, twQ, d->qinvD, d->ninvD, d->ninvQ, nttFp());
         });
     };
     if (!inverse) {
-        pass(k_ntt<false, true>);
-        pass(k_ntt<false, false>);
+        if (small) {
+            pass(k_ntt<false, true, 2>, 2);
+            pass(k_ntt<false, false, 2>, 2);
+        } else {
+            pass(k_ntt<false, true, 3>, 3);
+            pass(k_ntt<false, false, 3>, 3);
+        }
     } else {
-        pass(k_ntt<true, false>);
-        pass(k_ntt<true, true>);
+        if (small) {
+            pass(k_ntt<true, false, 2>, 2);
+            pass(k_ntt<true, true, 2>, 2);
+        } else {
+            pass(k_ntt<true, false, 3>, 3);
+            pass(k_ntt<true, true, 3>, 3);
+        }
     }
     checkLaunch(d, "ntt");
 }
@@ -1338,6 +1380,22 @@ void sfp_ntt(sfp_dev* d, uint64_t* p, sfp_limbs m, int inverse) {
     RowGroup G = rowsOf(1, m.count, m);
     G.src = G.dst = RowPtr{p, 0, (long long)d->n};
     nttRows(d, G, inverse);
+}
+
+// Developer hook (SFHE_NTT_TRACE builds): per-kernel phase clocks since the
+// last call, [variant INV*2+COL][phase 0..5, 7 = blocks]; -1 otherwise.
+extern "C" int sfp_ntt_trace(sfp_dev* d, unsigned long long* out32) {
+#ifdef SFHE_NTT_TRACE
+    syncAll(d);
+    SFP_CHECK(hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_nttTrace), sizeof(unsigned long long) * 32));
+    static const unsigned long long zero[32] = {};
+    SFP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_nttTrace), zero, sizeof zero));
+    return 0;
+#else
+    (void)d;
+    (void)out32;
+    return -1;
+#endif
 }
 
 void sfp_prof_set(sfp_dev* d, uint32_t fam, uint32_t period) {

@@ -16,6 +16,22 @@
 
 using namespace lbcrypto;
 
+extern "C" int sfp_ntt_trace(sfp_dev* d, unsigned long long* out32);
+
+// per-block phase clocks of the last measured NTTs (SFHE_NTT_TRACE builds)
+static void printTrace(sfp_dev* d) {
+    unsigned long long t[32];
+    if (sfp_ntt_trace(d, t) != 0) return;
+    static const char* names[4] = {"fwd ROW", "fwd COL", "inv ROW", "inv COL"};
+    for (int v = 0; v < 4; ++v) {
+        const unsigned long long nb = t[v * 8 + 7];
+        if (!nb) continue;
+        std::printf("    %s blocks=%llu clk/block:", names[v], nb);
+        for (int p = 0; p < 6; ++p) std::printf(" %7.0f", (double)t[v * 8 + p] / nb);
+        std::printf("\n");
+    }
+}
+
 template <class F>
 static double timeIt(sfp_dev* d, int iters, F&& f) {
     f();
@@ -52,12 +68,17 @@ int main(int argc, char** argv) {
                 "inv GB/s");
     for (uint32_t rows : {1u, 2u, 4u, 8u, 16u, 24u, 35u, 47u}) {
         if (rows > NP) continue;
-        const sfp_limbs m{rows, rows, 0, 0};
+        static const uint32_t base = std::getenv("MB_BASE") ? std::atoi(std::getenv("MB_BASE")) : 0;
+        if (rows + base > NP) continue;
+        const sfp_limbs m{rows, rows, base, 0};
+        unsigned long long scratch[32];
+        sfp_ntt_trace(d, scratch);
         const double f = timeIt(d, 50, [&] { sfp_ntt(d, buf, m, 0); });
         const double i = timeIt(d, 50, [&] { sfp_ntt(d, buf, m, 1); });
         const double bytes = 32.0 * rows * n;  // two passes x 16 B per coefficient
         std::printf("%-10s %6u %10.2f %10.1f %10.2f %10.1f\n", "ntt", rows, f, bytes / f / 1e3, i,
                     bytes / i / 1e3);
+        printTrace(d);
     }
     // key switch pieces at the top level (ell = Lq)
     const uint32_t ell = s->Lq, K = s->K, beta = (ell + s->alpha - 1) / s->alpha;
