@@ -316,6 +316,27 @@ void sfp_rescale_ext(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t ell
     free(last);
 }
 
+/* fused product + rescale (prims.h), stated as the two steps */
+void sfp_mul_const_rescale(sfp_dev* d, uint64_t* out, const uint64_t* in, const uint64_t* k,
+                           uint32_t ell, const uint64_t* qlinv, uint32_t npoly, size_t in_stride,
+                           size_t out_stride) {
+    const size_t w = (size_t)ell * d->n;
+    u64* t = (u64*)malloc(w * npoly * 8);
+    for (uint32_t p = 0; p < npoly; ++p)
+        sfp_mul_const(d, t + p * w, in + p * in_stride, k, (sfp_limbs){ell, ell, 0, 0});
+    sfp_rescale(d, out, t, ell, qlinv, npoly, w, out_stride);
+    free(t);
+}
+void sfp_mul_rescale(sfp_dev* d, uint64_t* out, const uint64_t* in, const uint64_t* m, uint32_t ell,
+                     const uint64_t* qlinv, uint32_t npoly, size_t in_stride, size_t out_stride) {
+    const size_t w = (size_t)ell * d->n;
+    u64* t = (u64*)malloc(w * npoly * 8);
+    for (uint32_t p = 0; p < npoly; ++p)
+        sfp_mul(d, t + p * w, in + p * in_stride, m, (sfp_limbs){ell, ell, 0, 0});
+    sfp_rescale(d, out, t, ell, qlinv, npoly, w, out_stride);
+    free(t);
+}
+
 /* ---- base conversion / key switching ---- */
 sfp_conv* sfp_upload_conv(sfp_dev* d, uint32_t ns, const uint32_t* src, uint32_t nt,
                           const uint32_t* dst, const uint32_t* drow, const uint64_t* inv,
@@ -403,6 +424,13 @@ void sfp_modup(sfp_dev* d, uint64_t* ext, const uint64_t* in, uint32_t ell, uint
 void sfp_ks_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
                   size_t ext_stride, const uint64_t* key, uint32_t beta, uint32_t ell, uint32_t K,
                   uint32_t Lq) {
+    sfp_ks_inner_fold(d, acc0, acc1, ext, ext_stride, key, beta, ell, K, Lq, NULL, NULL, 0);
+}
+
+void sfp_ks_inner_fold(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
+                       size_t ext_stride, const uint64_t* key, uint32_t beta, uint32_t ell,
+                       uint32_t K, uint32_t Lq, const uint64_t* fold0, const uint64_t* fold1,
+                       uint64_t fold_k) {
     const uint32_t n = d->n, rows = ell + K, NP = Lq + K;
 #pragma omp parallel for schedule(static)
     for (uint32_t t = 0; t < rows; ++t) {
@@ -416,6 +444,10 @@ void sfp_ks_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ex
                 const u64* ka = kb + (size_t)NP * n;
                 s0 += (u128)e * kb[(size_t)kr * n + x];
                 s1 += (u128)e * ka[(size_t)kr * n + x];
+            }
+            if (fold0 && t == ell - 1) {
+                s0 += (u128)fold0[(size_t)t * n + x] * fold_k;
+                s1 += (u128)fold1[(size_t)t * n + x] * fold_k;
             }
             acc0[(size_t)t * n + x] = (u64)(s0 % q);
             acc1[(size_t)t * n + x] = (u64)(s1 % q);
@@ -450,6 +482,29 @@ void sfp_moddown2(sfp_dev* d, uint64_t* out0, uint64_t* out1, uint64_t* acc, siz
                   int add0, int add1, uint64_t* scratch) {
     moddown1(d, out0, acc, ell, K, Lq, c, pinv, add0, scratch);
     moddown1(d, out1, acc + acc_stride, ell, K, Lq, c, pinv, add1, scratch + (size_t)ell * d->n);
+}
+
+/* ModDown + add + rescale, stated as the two steps it fuses (prims.h):
+ * ModDown of the folded accumulators, add d on rows < l (row l already holds
+ * P d_l through the fold), then Rescale. */
+void sfp_moddown_rescale(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint64_t* d0,
+                         const uint64_t* d1, uint64_t* acc, size_t acc_stride, uint32_t ell,
+                         uint32_t K, uint32_t Lq, const sfp_conv* c, const uint64_t* pinv,
+                         const uint64_t* pmod, const uint64_t* qlinv, uint64_t* scratch) {
+    const uint32_t n = d->n, l = ell - 1;
+    (void)pmod;
+    u64* s = (u64*)malloc((size_t)ell * n * 8);
+    for (int p = 0; p < 2; ++p) {
+        const u64* dp = p ? d1 : d0;
+        u64* op = p ? out1 : out0;
+        moddown1(d, s, acc + (size_t)p * acc_stride, ell, K, Lq, c, pinv, 0, scratch);
+        for (uint32_t i = 0; i < l; ++i) {
+            const u64 q = d->q[i];
+            for (uint32_t x = 0; x < n; ++x) s[(size_t)i * n + x] = ad(s[(size_t)i * n + x], dp[(size_t)i * n + x], q);
+        }
+        sfp_rescale(d, op, s, ell, qlinv, 1, 0, 0);
+    }
+    free(s);
 }
 
 /* ---- sampling / loading ---- */

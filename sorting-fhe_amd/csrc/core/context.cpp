@@ -306,14 +306,52 @@ class SfheInternal {
         // result scale = scale_ct * K / q_{ell-1} = Delta_target
         double K = s->scale[target] * (double)s->primes[ell - 1] / ct->scale;
         auto k = constResidues(s, K, ell);
-        auto tmp = s->alloc((size_t)2 * ell * s->n);
-        uint64_t* t0 = tmp->ptr;
-        uint64_t* t1 = t0 + (size_t)ell * s->n;
-        sfp_mul_const(s->dev, t0, ct->c0, k.data(), Q(ell));
-        sfp_mul_const(s->dev, t1, ct->c1, k.data(), Q(ell));
         s->stats.constmult++;
         s->countBytes(4.0 * ell * s->n * 8);
-        return rescale(cc, t0, t1, mid, ct->slots);
+        return mulRescale(cc, ct, mid, k.data(), nullptr, ct->slots);
+    }
+
+    // SFHE_FUSED_RESCALE=0 selects the two-step paths (product, then rescale)
+    // the fused prims replace; tests check both agree bit for bit.
+    static bool fusedRescale() {
+        static const bool on = [] {
+            const char* v = std::getenv("SFHE_FUSED_RESCALE");
+            return !v || *v != '0';
+        }();
+        return on;
+    }
+
+    // Rescale(ct * k) (k: ell per-row residues) or Rescale(ct (.) m) (m: ell
+    // plaintext rows) in one fused prim; ct's first ellOf(level) rows are used.
+    static Ct mulRescale(CC* cc, const Ct& ct, uint32_t level, const u64* k, const uint64_t* m,
+                         uint32_t slots) {
+        SfheContextState* s = cc->st.get();
+        const uint32_t ell = s->ellOf(level);
+        if (ell < 2) SFHE_THROW("no levels left to rescale (multiplicative depth exhausted)");
+        if (!fusedRescale()) {
+            auto tmp = s->alloc((size_t)2 * ell * s->n);
+            uint64_t* t0 = tmp->ptr;
+            uint64_t* t1 = t0 + (size_t)ell * s->n;
+            if (k) {
+                sfp_mul_const(s->dev, t0, ct->c0, k, Q(ell));
+                sfp_mul_const(s->dev, t1, ct->c1, k, Q(ell));
+            } else {
+                sfp_mul(s->dev, t0, ct->c0, m, Q(ell));
+                sfp_mul(s->dev, t1, ct->c1, m, Q(ell));
+            }
+            return rescale(cc, t0, t1, level, slots);
+        }
+        Ct out = newCt(cc, level + 1, slots);
+        const size_t inStride = (size_t)(ct->c1 - ct->c0), outStride = (size_t)(out->c1 - out->c0);
+        if (k)
+            sfp_mul_const_rescale(s->dev, out->c0, ct->c0, k, ell, s->qInvTable[ell].data(), 2, inStride,
+                                  outStride);
+        else
+            sfp_mul_rescale(s->dev, out->c0, ct->c0, m, ell, s->qInvTable[ell].data(), 2, inStride,
+                            outStride);
+        s->stats.rescale++;
+        s->countBytes(4.0 * ell * s->n * 8 * 2 / 2);
+        return out;
     }
 
     static void align(CC* cc, Ct& a, Ct& b) {
@@ -338,6 +376,38 @@ class SfheInternal {
         s->stats.keyswitch++;
         // (3 l + 2 beta (l+K)) B
         s->countBytes((3.0 * ell + 2.0 * beta * (ell + K)) * n * 8);
+    }
+
+    // EvalMult's tail: relinearise (d0, d1, d2) at `level` and rescale, with the
+    // ModDown and the rescale fused (sfp_moddown_rescale): the same result as
+    // keySwitch(d2, +d0, +d1) followed by rescale(), four launches fewer.
+    static Ct relinRescale(CC* cc, uint64_t* d0, uint64_t* d1, const uint64_t* d2, uint32_t level,
+                           uint32_t slots) {
+        SfheContextState* s = cc->st.get();
+        const uint32_t ell = s->ellOf(level);
+        if (ell < 2) SFHE_THROW("no levels left to rescale (multiplicative depth exhausted)");
+        const uint32_t n = s->n, K = s->K;
+        const uint32_t beta = (ell + s->alpha - 1) / s->alpha;
+        const size_t stride = (size_t)(ell + K) * n;
+        auto ext = s->alloc(stride * beta);
+        {
+            auto scratch = s->alloc((size_t)ell * n);
+            auto& convs = modupConv(cc, ell);
+            sfp_modup(s->dev, ext->ptr, d2, ell, K, s->Lq, s->alpha, convs.data(), scratch->ptr);
+        }
+        auto acc = s->alloc(2 * stride);
+        sfp_ks_inner_fold(s->dev, acc->ptr, acc->ptr + stride, ext->ptr, stride, s->relinKey->ptr, beta,
+                          ell, K, s->Lq, d0, d1, s->pModQ[ell - 1]);
+        Ct out = newCt(cc, level + 1, slots);
+        auto scratch = s->alloc((size_t)2 * (ell - 1) * n);
+        sfp_moddown_rescale(s->dev, out->c0, out->c1, d0, d1, acc->ptr, stride, ell, K, s->Lq,
+                            s->moddownConv, s->pInvModQ.data(), s->pModQ.data(),
+                            s->qInvTable[ell].data(), scratch->ptr);
+        s->stats.keyswitch++;
+        s->stats.rescale++;
+        s->countBytes((3.0 * ell + 2.0 * beta * (ell + K)) * n * 8);
+        s->countBytes(4.0 * ell * n * 8);
+        return out;
     }
 
     static void innerAndModDown(CC* cc, const uint64_t* ext, size_t stride, uint32_t beta,
@@ -1219,14 +1289,10 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMult(const Ciphertext<DCRT
     // integer K with scale_a * K / q_last = Delta_{l+1} * c
     double K = c * s->scale[a->level + 1] * (double)s->primes[ell - 1] / a->scale;
     auto k = SfheInternal::constResidues(s, K, ell);
-    auto tmp = s->alloc((size_t)2 * ell * s->n);
-    uint64_t* t0 = tmp->ptr;
-    uint64_t* t1 = t0 + (size_t)ell * s->n;
-    sfp_mul_const(s->dev, t0, a->c0, k.data(), SfheInternal::Q(ell));
-    sfp_mul_const(s->dev, t1, a->c1, k.data(), SfheInternal::Q(ell));
     s->stats.constmult++;
     s->countBytes(4.0 * ell * s->n * 8);
-    return SfheInternal::traced(this, SfheInternal::rescale(this, t0, t1, a->level, a->slots), "EvalMult");
+    return SfheInternal::traced(this, SfheInternal::mulRescale(this, a, a->level, k.data(), nullptr, a->slots),
+                                "EvalMult");
 }
 
 void CryptoContextImpl<DCRTPoly>::EvalMultInPlace(Ciphertext<DCRTPoly>& a, double c) {
@@ -1241,14 +1307,10 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMult(const Ciphertext<DCRT
     const uint32_t ell = s->ellOf(a->level);
     if (ell < 2) SFHE_THROW("no levels left (multiplicative depth exhausted)");
     const uint64_t* m = SfheInternal::encoded(this, p, a->level);
-    auto tmp = s->alloc((size_t)2 * ell * s->n);
-    uint64_t* t0 = tmp->ptr;
-    uint64_t* t1 = t0 + (size_t)ell * s->n;
-    sfp_mul(s->dev, t0, a->c0, m, SfheInternal::Q(ell));
-    sfp_mul(s->dev, t1, a->c1, m, SfheInternal::Q(ell));
     s->stats.ptmult++;
     s->countBytes(5.0 * ell * s->n * 8);
-    return SfheInternal::traced(this, SfheInternal::rescale(this, t0, t1, a->level, std::max(a->slots, p->slots)), "EvalMult");
+    return SfheInternal::traced(
+        this, SfheInternal::mulRescale(this, a, a->level, nullptr, m, std::max(a->slots, p->slots)), "EvalMult");
 }
 
 void CryptoContextImpl<DCRTPoly>::EvalMultInPlace(Ciphertext<DCRTPoly>& a, const Plaintext& p) {
@@ -1272,8 +1334,12 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMult(const Ciphertext<DCRT
     sfp_tensor(s->dev, d0, d1, d2, a->c0, a->c1, b->c0, b->c1, SfheInternal::Q(ell));
     s->stats.tensor++;
     s->countBytes(7.0 * ell * s->n * 8);
+    const uint32_t slots = std::max(a->slots, b->slots);
+    if (SfheInternal::fusedRescale())
+        return SfheInternal::traced(this, SfheInternal::relinRescale(this, d0, d1, d2, a->level, slots),
+                                    "EvalMult");
     SfheInternal::keySwitch(this, d2, ell, s->relinKey, d0, d1, 1, 1);
-    return SfheInternal::traced(this, SfheInternal::rescale(this, d0, d1, a->level, std::max(a->slots, b->slots)), "EvalMult");
+    return SfheInternal::traced(this, SfheInternal::rescale(this, d0, d1, a->level, slots), "EvalMult");
 }
 
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalSquare(const Ciphertext<DCRTPoly>& a) {

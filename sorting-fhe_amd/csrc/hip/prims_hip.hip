@@ -116,6 +116,7 @@ struct sfp_dev {
     // content-addressed device copies of small constant arrays (kernel
     // argument tables): bump-allocated in one buffer
     u64* cpool = nullptr;
+    u64* cpoolOld = nullptr;  // the retired generation (devConst)
     size_t cpoolCap = 0, cpoolOff = 0;
     std::unordered_map<uint64_t, std::vector<std::pair<std::vector<u64>, size_t>>> cmap;
     std::mutex mu;
@@ -510,9 +511,14 @@ struct RowGroup {
     uint32_t skipEll;      // >0: skip rows alpha*p <= i < min(alpha*(p+1), skipEll) (ModUp own digit)
     uint32_t lift, liftPrime;
     uint32_t epi, addMask;  // addMask bit p: accumulate into eout for polynomial p
-    // device arrays (constant cache): epilogue constant per i (value, Shoup)
+    RowPtr eadd;            // epi with eadd.base: eout += eadd * k2_i
+    // multipliers (a rescale fused with the product before it):
+    //   pre / preK: the first pass reads src * pre (elementwise) or src * preK_i
+    //   emul / emK: the epilogue uses ein * emul or ein * emK_i in place of ein
+    RowPtr pre, emul;
+    // device arrays (constant cache): epilogue constants per i (value, Shoup)
     // and q_liftPrime mod q_i -- pointers keep the kernel arguments small
-    const u64 *k, *kS, *liftSub;
+    const u64 *k, *kS, *k2, *k2S, *liftSub, *preK, *preKS, *emK, *emKS;
 };
 
 __device__ __forceinline__ u64* rowAt(const RowPtr& r, uint32_t p, uint32_t i) {
@@ -585,10 +591,11 @@ __global__ __launch_bounds__(kNttTile >> LE) void k_ntt(const RowGroup G, const 
                            : rowAt(G.copy, pp, ii);
     sf_barrett LB{};
     u64 lsub = 0;
-    if (FIRST && G.lift) {
-        LB = loadBar(bar, prime);
-        lsub = G.liftSub[ii];
-    }
+    const u64* pre = FIRST && G.pre.base ? rowAt(G.pre, pp, ii) : nullptr;
+    const bool preK = FIRST && G.preK;
+    const u64 pk = preK ? G.preK[ii] : 0, pkS = preK ? G.preKS[ii] : 0;
+    if (FIRST && (G.lift || pre)) LB = loadBar(bar, prime);
+    if (FIRST && G.lift) lsub = G.liftSub[ii];
     const u64 lhalf = (FIRST && G.lift) ? (bar[G.liftPrime].q >> 1) : 0;
 
     // global -> LDS, 16 B per lane; tile-linear word e is row-major (u, st)
@@ -599,6 +606,15 @@ __global__ __launch_bounds__(kNttTile >> LE) void k_ntt(const RowGroup G, const 
         ulonglong2 x = *reinterpret_cast<const ulonglong2*>(in + g);
         if (FIRST) {
             if (cp) *reinterpret_cast<ulonglong2*>(cp + g) = x;
+            if (pre) {
+                const ulonglong2 m = *reinterpret_cast<const ulonglong2*>(pre + g);
+                x.x = bmul(x.x, m.x, LB);
+                x.y = bmul(x.y, m.y, LB);
+            }
+            if (preK) {
+                x.x = sf_mul_shoup(x.x, pk, pkS, q);
+                x.y = sf_mul_shoup(x.y, pk, pkS, q);
+            }
             if (G.lift) {
                 u64 r0 = sf_reduce128(x.x, 0, &LB), r1 = sf_reduce128(x.y, 0, &LB);
                 if (x.x > lhalf) r0 = sf_sub(r0, lsub, q);
@@ -636,6 +652,12 @@ __global__ __launch_bounds__(kNttTile >> LE) void k_ntt(const RowGroup G, const 
     u64* out = epi ? rowAt(G.eout, pp, ii) : rowAt(G.dst, pp, ii);
     const u64* ein = epi ? rowAt(G.ein, pp, ii) : nullptr;
     const u64 ek = epi ? G.k[ii] : 0, ekS = epi ? G.kS[ii] : 0;
+    const u64* ead = epi && G.eadd.base ? rowAt(G.eadd, pp, ii) : nullptr;
+    const u64 ek2 = ead ? G.k2[ii] : 0, ek2S = ead ? G.k2S[ii] : 0;
+    const u64* emul = epi && G.emul.base ? rowAt(G.emul, pp, ii) : nullptr;
+    const bool emK = epi && G.emK;
+    const u64 emk = emK ? G.emK[ii] : 0, emkS = emK ? G.emKS[ii] : 0;
+    const sf_barrett EB = emul ? loadBar(bar, prime) : sf_barrett{};
 #pragma unroll
     for (int k = 0; k < (1 << LE) / 2; ++k) {
         const uint32_t e = 2 * (threadIdx.x + k * (kNttTile >> LE));
@@ -664,13 +686,27 @@ __global__ __launch_bounds__(kNttTile >> LE) void k_ntt(const RowGroup G, const 
             x.y = x.y >= q ? x.y - q : x.y;
         }
         if (epi) {
-            const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(ein + g);
+            ulonglong2 a = *reinterpret_cast<const ulonglong2*>(ein + g);
+            if (emul) {
+                const ulonglong2 m = *reinterpret_cast<const ulonglong2*>(emul + g);
+                a.x = bmul(a.x, m.x, EB);
+                a.y = bmul(a.y, m.y, EB);
+            }
+            if (emK) {
+                a.x = sf_mul_shoup(a.x, emk, emkS, q);
+                a.y = sf_mul_shoup(a.y, emk, emkS, q);
+            }
             x.x = sf_mul_shoup(sf_sub(a.x, x.x, q), ek, ekS, q);
             x.y = sf_mul_shoup(sf_sub(a.y, x.y, q), ek, ekS, q);
             if ((G.addMask >> pp) & 1u) {
                 const ulonglong2 o = *reinterpret_cast<const ulonglong2*>(out + g);
                 x.x = sf_add(x.x, o.x, q);
                 x.y = sf_add(x.y, o.y, q);
+            }
+            if (ead) {
+                const ulonglong2 o = *reinterpret_cast<const ulonglong2*>(ead + g);
+                x.x = sf_add(x.x, sf_mul_shoup(o.x, ek2, ek2S, q), q);
+                x.y = sf_add(x.y, sf_mul_shoup(o.y, ek2, ek2S, q), q);
             }
         }
         *reinterpret_cast<ulonglong2*>(out + g) = x;
@@ -933,11 +969,89 @@ __global__ __launch_bounds__(kThreads) void k_conv(const ConvJobs J, const sf_ba
     }
 }
 
+// ModDown conversion fused with the following rescale (sfp_moddown_rescale).
+// Per coefficient x of each poly: the centred P->Q conversion conv_t of the K
+// P-rows (as k_conv), the dropped row's coefficient r = (a_l - conv_l) P^-1
+// mod q_l, and for every kept target t < l:  y_t = conv_t + P_t [r]_t, with
+// [r]_t the centred lift of r (r > q_l/2 stands for r - q_l).
+struct MdrsJob {
+    const u64* src;  // K P-rows, coefficient domain
+    const u64* al;   // accumulator row l, coefficient domain
+    u64* dst;        // l rows
+};
+struct MdrsArgs {
+    MdrsJob j[2];
+    const uint32_t* sidx;
+    const u64 *inv, *mod, *sprod;  // the ModDown conversion table (targets 0..)
+    const u64 *pmod, *lsub;        // P mod q_t, q_l mod q_t
+    u64 pinvl;                     // P^-1 mod q_l
+    uint32_t ns, nt, l;
+};
+
+__global__ __launch_bounds__(kThreads) void k_conv_mdrs(const MdrsArgs A, const sf_barrett* __restrict__ bar,
+                                                        uint32_t logn) {
+    constexpr int W = kConvChunk + 1;  // the chunk's targets + target l
+    __shared__ u64 smod[kMaxConvSrc * W];
+    const MdrsJob& J = A.j[blockIdx.y];
+    const uint32_t t0 = blockIdx.z * kConvChunk;
+    if (t0 >= A.l) return;
+    const uint32_t tc = min((uint32_t)kConvChunk, A.l - t0);
+    for (uint32_t e = threadIdx.x; e < A.ns * W; e += kThreads) {
+        const uint32_t i = e / W, t = e % W;
+        const uint32_t tt = t < tc ? t0 + t : A.l;
+        smod[e] = t < tc || t == (uint32_t)kConvChunk ? A.mod[(size_t)i * A.nt + tt] : 0;
+    }
+    __syncthreads();
+    const uint32_t n = 1u << logn;
+    const uint32_t x = blockIdx.x * kThreads + threadIdx.x;
+    if (x >= n) return;
+    u64 y[kMaxConvSrc];
+    u64 neg = 0;
+#pragma unroll
+    for (int i = 0; i < kMaxConvSrc; ++i) {
+        if ((uint32_t)i < A.ns) {
+            const sf_barrett B = loadBar(bar, A.sidx[i]);
+            y[i] = bmul(J.src[((size_t)i << logn) + x], A.inv[i], B);
+            if (y[i] > (B.q >> 1)) ++neg;
+        }
+    }
+    // the dropped row: r = (a_l - conv_l) * P^-1 mod q_l
+    u64 r;
+    bool rneg;
+    {
+        Acc acc{0, 0};
+#pragma unroll
+        for (int i = 0; i < kMaxConvSrc; ++i)
+            if ((uint32_t)i < A.ns) macc(acc, y[i], smod[i * W + kConvChunk]);
+        const sf_barrett B = loadBar(bar, A.l);
+        u64 c = sf_reduce128_acc(acc.lo, acc.hi, &B);
+        if (neg) c = sf_sub(c, bmul(neg, A.sprod[A.l], B), B.q);
+        r = bmul(sf_sub(J.al[((size_t)A.l << logn) + x], c, B.q), A.pinvl, B);
+        rneg = r > (B.q >> 1);
+    }
+    for (uint32_t t = 0; t < tc; ++t) {
+        const uint32_t tt = t0 + t;
+        Acc acc{0, 0};
+#pragma unroll
+        for (int i = 0; i < kMaxConvSrc; ++i)
+            if ((uint32_t)i < A.ns) macc(acc, y[i], smod[i * W + t]);
+        const sf_barrett B = loadBar(bar, tt);
+        u64 v = sf_reduce128_acc(acc.lo, acc.hi, &B);
+        if (neg) v = sf_sub(v, bmul(neg, A.sprod[tt], B), B.q);
+        u64 lift = sf_reduce128(r, 0, &B);
+        if (rneg) lift = sf_sub(lift, A.lsub[tt], B.q);
+        v = sf_add(v, bmul(lift, A.pmod[tt], B), B.q);
+        J.dst[((size_t)tt << logn) + x] = v;
+    }
+}
+
 // key inner product over ext rows t < ell+K
 __global__ __launch_bounds__(kThreads) void k_ks_inner(u64* __restrict__ acc0, u64* __restrict__ acc1,
                                                        const u64* __restrict__ ext, size_t extStride,
                                                        const u64* __restrict__ key, uint32_t beta,
                                                        uint32_t ell, uint32_t K, uint32_t Lq,
+                                                       const u64* __restrict__ fold0,
+                                                       const u64* __restrict__ fold1, u64 foldK,
                                                        const sf_barrett* __restrict__ bar, uint32_t logn) {
     const uint32_t rows = ell + K, NP = Lq + K;
     const size_t total = (size_t)rows << logn;
@@ -955,6 +1069,10 @@ __global__ __launch_bounds__(kThreads) void k_ks_inner(u64* __restrict__ acc0, u
             const u64* ka = kb + (size_t)NP * n;
             macc(s0, e, kb[((size_t)kr << logn) + x]);
             macc(s1, e, ka[((size_t)kr << logn) + x]);
+        }
+        if (fold0 && t == ell - 1) {  // + P * d_l (sfp_ks_inner_fold)
+            macc(s0, fold0[i], foldK);
+            macc(s1, fold1[i], foldK);
         }
         acc0[i] = sf_reduce128_acc(s0.lo, s0.hi, &B);
         acc1[i] = sf_reduce128_acc(s1.lo, s1.hi, &B);
@@ -1064,16 +1182,16 @@ static void devZero(sfp_dev* d, void* dst, size_t b) {
 // pinned ring, pulled across by a copy kernel.  The ring region is reused
 // only after the stream has drained past every earlier pull.
 static void* ringPut(sfp_dev* d, const void* src, size_t bytes) {
-    bytes = (bytes + 255) & ~(size_t)255;
-    if (d->ringOff + bytes > d->ringCap) {
+    const size_t span = (bytes + 255) & ~(size_t)255;  // keep entries 256-B aligned
+    if (d->ringOff + span > d->ringCap) {
         syncAll(d);
         d->ringOff = 0;
     }
     char* h = d->hring + d->ringOff;
     char* dv = d->dring + d->ringOff;
-    std::memcpy(h, src, bytes);
+    std::memcpy(h, src, bytes);  // only the caller's bytes: src may end right there
     devCopy(d, dv, h, bytes);
-    d->ringOff += bytes;
+    d->ringOff += span;
     return dv;
 }
 
@@ -1108,11 +1226,17 @@ static const u64* devConst(sfp_dev* d, const u64* v, size_t count) {
         if (e.first.size() == count && std::equal(v, v + count, e.first.begin())) return d->cpool + e.second;
     const size_t words = (count + 1) & ~(size_t)1;  // keep 16-B alignment
     if (!d->cpool || d->cpoolOff + words > d->cpoolCap) {
-        syncAll(d);  // no queued kernel may still read the old entries
-        if (!d->cpool) {
-            d->cpoolCap = (size_t)1 << 19;  // 4 MiB
-            SFP_CHECK(hipMalloc((void**)&d->cpool, d->cpoolCap * 8));
+        // Two generations: the full pool is retired, not overwritten, so
+        // pointers a prim obtained just before this call (for the same
+        // launch) stay valid; the generation before it is free once every
+        // queued kernel has drained.
+        syncAll(d);
+        if (!d->cpoolOld) {
+            d->cpoolCap = (size_t)1 << 19;  // 4 MiB per generation
+            SFP_CHECK(hipMalloc((void**)&d->cpoolOld, d->cpoolCap * 8));
         }
+        std::swap(d->cpool, d->cpoolOld);
+        if (!d->cpool) SFP_CHECK(hipMalloc((void**)&d->cpool, d->cpoolCap * 8));
         d->cmap.clear();
         d->cpoolOff = 0;
     }
@@ -1234,6 +1358,7 @@ void sfp_destroy(sfp_dev* d) {
     hipHostFree(d->hring);
     hipHostFree(d->bounce);
     hipFree(d->cpool);
+    hipFree(d->cpoolOld);
     for (int l = 0; l < d->nLanes; ++l) hipStreamDestroy(d->streams[l]);
     delete d;
 }
@@ -1561,12 +1686,16 @@ void sfp_rescale(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t ell, co
 // (in_p,i - lift(INTT(in_p,last))) * qlinv_i for both polys: INTT of the two
 // dropped rows, then one NTT launch pair that lifts them to every remaining
 // prime and applies the subtract-multiply in its last pass.
-void sfp_rescale_ext(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t ell, uint32_t dropPrime,
-                     const uint64_t* qlinv, uint32_t npoly, size_t inStride, size_t outStride) {
+// Rescale of in * w: w = mulRows (elementwise, ell rows shared by the polys),
+// w = mulK (host array of ell per-row residues) or w = 1.  The dropped row is
+// multiplied on its INTT's load, the kept rows in the epilogue.
+static void rescaleCore(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t ell, uint32_t dropPrime,
+                        const uint64_t* qlinv, uint32_t npoly, size_t inStride, size_t outStride,
+                        const uint64_t* mulRows, const uint64_t* mulK) {
     const uint32_t n = d->n;
     const uint32_t cnt = ell - 1;
-    if (cnt > SFP_MAX_LIMBS) {
-        record(d, "rescale (too many limbs)", hipErrorInvalidValue);
+    if (cnt > SFP_MAX_LIMBS || ell < 2) {
+        record(d, "rescale (limb count)", hipErrorInvalidValue);
         return;
     }
     u64* last = scratch(d, (size_t)npoly * n + (size_t)npoly * cnt * n);
@@ -1574,6 +1703,22 @@ void sfp_rescale_ext(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t ell
     RowGroup A = rowsOf(npoly, 1, sfp_limbs{1, 0, dropPrime, 0});
     A.src = RowPtr{in + (size_t)cnt * n, (long long)inStride, 0};
     A.dst = RowPtr{last, (long long)n, 0};
+    // per-call multipliers go through the upload ring (stream-ordered, not
+    // cached: a cached entry would need cross-lane ordering)
+    u64 mk[2 * SFP_MAX_LIMBS + 2];
+    const u64* dmk = nullptr;
+    if (mulRows) A.pre = RowPtr{mulRows + (size_t)cnt * n, 0, 0};
+    if (mulK) {
+        for (uint32_t i = 0; i < cnt; ++i) {
+            mk[i] = mulK[i];
+            mk[cnt + i] = sf_shoup_precomp(mulK[i], d->hbar[i].q);
+        }
+        mk[2 * cnt] = mulK[cnt];
+        mk[2 * cnt + 1] = sf_shoup_precomp(mulK[cnt], d->hbar[dropPrime].q);
+        dmk = (const u64*)ringPut(d, mk, (2 * cnt + 2) * 8);
+        A.preK = dmk + 2 * cnt;
+        A.preKS = dmk + 2 * cnt + 1;
+    }
     nttRows(d, A, 1);
     RowGroup B = rowsOf(npoly, cnt, sfp_limbs{cnt, cnt, 0, 0});
     B.src = RowPtr{last, (long long)n, 0};
@@ -1593,7 +1738,27 @@ void sfp_rescale_ext(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t ell
     B.k = devConst(d, qlinv, cnt);
     B.kS = devConst(d, kS, cnt);
     B.liftSub = devConst(d, lsub, cnt);
+    if (mulRows) B.emul = RowPtr{mulRows, 0, (long long)n};
+    if (mulK) {
+        B.emK = dmk;
+        B.emKS = dmk + cnt;
+    }
     nttRows(d, B, 0);
+}
+
+void sfp_rescale_ext(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t ell, uint32_t dropPrime,
+                     const uint64_t* qlinv, uint32_t npoly, size_t inStride, size_t outStride) {
+    rescaleCore(d, out, in, ell, dropPrime, qlinv, npoly, inStride, outStride, nullptr, nullptr);
+}
+
+void sfp_mul_const_rescale(sfp_dev* d, uint64_t* out, const uint64_t* in, const uint64_t* k, uint32_t ell,
+                           const uint64_t* qlinv, uint32_t npoly, size_t inStride, size_t outStride) {
+    rescaleCore(d, out, in, ell, ell - 1, qlinv, npoly, inStride, outStride, nullptr, k);
+}
+
+void sfp_mul_rescale(sfp_dev* d, uint64_t* out, const uint64_t* in, const uint64_t* m, uint32_t ell,
+                     const uint64_t* qlinv, uint32_t npoly, size_t inStride, size_t outStride) {
+    rescaleCore(d, out, in, ell, ell - 1, qlinv, npoly, inStride, outStride, m, nullptr);
 }
 
 // ---- base conversion / key switching ----
@@ -1716,11 +1881,22 @@ void sfp_modup(sfp_dev* d, uint64_t* ext, const uint64_t* in, uint32_t ell, uint
 void sfp_ks_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
                   size_t extStride, const uint64_t* key, uint32_t beta, uint32_t ell, uint32_t K,
                   uint32_t Lq) {
+    sfp_ks_inner_fold(d, acc0, acc1, ext, extStride, key, beta, ell, K, Lq, nullptr, nullptr, 0);
+}
+
+void sfp_ks_inner_fold(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
+                       size_t extStride, const uint64_t* key, uint32_t beta, uint32_t ell,
+                       uint32_t K, uint32_t Lq, const uint64_t* fold0, const uint64_t* fold1,
+                       uint64_t foldK) {
     const size_t total = (size_t)(ell + K) * d->n;
+    if (fold0 && (!fold1 || ell < 1)) {
+        record(d, "ks_inner_fold", hipErrorInvalidValue);
+        return;
+    }
     // reads beta ext rows + 2*beta key rows, writes 2 accumulator rows, per limb
     timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + 2.0), [&] {
         hipLaunchKernelGGL(k_ks_inner, dim3(ewGrid(total)), dim3(kThreads), 0, d->st(), acc0, acc1, ext,
-                           extStride, key, beta, ell, K, Lq, d->bar, d->logn);
+                           extStride, key, beta, ell, K, Lq, fold0, fold1, foldK, d->bar, d->logn);
     });
     checkLaunch(d, "ks_inner");
 }
@@ -1751,6 +1927,64 @@ void sfp_moddown2(sfp_dev* d, uint64_t* out0, uint64_t* out1, uint64_t* acc, siz
     for (uint32_t i = 0; i < ell; ++i) kS[i] = sf_shoup_precomp(pinv[i], d->hbar[i].q);
     B.k = devConst(d, pinv, ell);
     B.kS = devConst(d, kS, ell);
+    nttRows(d, B, 0);
+}
+
+void sfp_moddown_rescale(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint64_t* d0,
+                         const uint64_t* d1, uint64_t* acc, size_t accStride, uint32_t ell,
+                         uint32_t K, uint32_t Lq, const sfp_conv* c, const uint64_t* pinv,
+                         const uint64_t* pmod, const uint64_t* qlinv, uint64_t* scr) {
+    const uint32_t n = d->n, l = ell - 1;
+    if (ell < 2 || ell > SFP_MAX_LIMBS || !c || c->ns > (uint32_t)kMaxConvSrc || c->nt < ell ||
+        !limbsOk(d, sfp_limbs{K + 1, 1, Lq, l}, "moddown_rescale")) {
+        record(d, "moddown_rescale", hipErrorInvalidValue);
+        return;
+    }
+    // INTT of rows [l, ell+K) of both accumulators: the dropped q row and the P rows
+    RowGroup A = rowsOf(2, K + 1, sfp_limbs{K + 1, 1, Lq, l});
+    A.src = A.dst = RowPtr{acc + (size_t)l * n, (long long)accStride, (long long)n};
+    nttRows(d, A, 1);
+    // conversion + the dropped row's lift
+    MdrsArgs M;
+    for (int p = 0; p < 2; ++p) {
+        const u64* ap = acc + (size_t)p * accStride;
+        M.j[p] = MdrsJob{ap + (size_t)ell * n, ap, scr + (size_t)p * l * n};
+    }
+    u64 lsub[SFP_MAX_LIMBS], k1[SFP_MAX_LIMBS], k1S[SFP_MAX_LIMBS], k2S[SFP_MAX_LIMBS];
+    const u64 ql = d->hbar[l].q;
+    for (uint32_t i = 0; i < l; ++i) {
+        const u64 q = d->hbar[i].q;
+        lsub[i] = ql % q;
+        k1[i] = (u64)((unsigned __int128)pinv[i] * qlinv[i] % q);  // (P q_l)^-1
+        k1S[i] = sf_shoup_precomp(k1[i], q);
+        k2S[i] = sf_shoup_precomp(qlinv[i], q);
+    }
+    M.sidx = c->src;
+    M.inv = c->inv;
+    M.mod = c->mod;
+    M.sprod = c->sprod;
+    M.pmod = devConst(d, pmod, l);
+    M.lsub = devConst(d, lsub, l);
+    M.pinvl = pinv[l];
+    M.ns = c->ns;
+    M.nt = c->nt;
+    M.l = l;
+    const dim3 g(n / kThreads, 2, (l + kConvChunk - 1) / kConvChunk);
+    timedLaunch(d, SFP_FAM_CONV, 8.0 * n * 2 * (K + 1 + l), [&] {
+        hipLaunchKernelGGL(k_conv_mdrs, g, dim3(kThreads), 0, d->st(), M, d->bar, d->logn);
+    });
+    checkLaunch(d, "conv_mdrs");
+    // out_i = (acc_i - NTT(y_i)) (P q_l)^-1 + d_i q_l^-1
+    RowGroup B = rowsOf(2, l, sfp_limbs{l, l, 0, 0});
+    B.src = B.dst = RowPtr{scr, (long long)l * n, (long long)n};
+    B.epi = 1;
+    B.ein = RowPtr{acc, (long long)accStride, (long long)n};
+    B.eout = RowPtr{out0, (long long)(out1 - out0), (long long)n};
+    B.eadd = RowPtr{d0, (long long)(d1 - d0), (long long)n};
+    B.k = devConst(d, k1, l);
+    B.kS = devConst(d, k1S, l);
+    B.k2 = devConst(d, qlinv, l);
+    B.k2S = devConst(d, k2S, l);
     nttRows(d, B, 0);
 }
 

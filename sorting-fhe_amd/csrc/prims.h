@@ -132,6 +132,18 @@ void sfp_rescale_ext(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t ell
                      uint32_t drop_prime, const uint64_t* qlinv, uint32_t npoly, size_t in_stride,
                      size_t out_stride);
 
+// Rescale of a product, fused (the product is never written out):
+//   sfp_mul_const_rescale: out = Rescale(in * k_i), k = host array of ell
+//                          per-row residues (EvalMult(ct, double), level adjust)
+//   sfp_mul_rescale:       out = Rescale(in (.) m), m = ell plaintext rows
+//                          shared by the npoly polys (EvalMult(ct, pt))
+// Bit-identical to sfp_mul_const / sfp_mul followed by sfp_rescale.
+void sfp_mul_const_rescale(sfp_dev* d, uint64_t* out, const uint64_t* in, const uint64_t* k,
+                           uint32_t ell, const uint64_t* qlinv, uint32_t npoly, size_t in_stride,
+                           size_t out_stride);
+void sfp_mul_rescale(sfp_dev* d, uint64_t* out, const uint64_t* in, const uint64_t* m, uint32_t ell,
+                     const uint64_t* qlinv, uint32_t npoly, size_t in_stride, size_t out_stride);
+
 // ---- basis conversion / key switching ----------------------------------------
 // Upload a conversion table: ns source primes (prime indices src_idx), nt
 // target primes (dst_idx) written to output rows dst_row[t] (NULL: row t);
@@ -173,6 +185,29 @@ void sfp_ks_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ex
 void sfp_moddown2(sfp_dev* d, uint64_t* out0, uint64_t* out1, uint64_t* acc, size_t acc_stride,
                   uint32_t ell, uint32_t K, uint32_t Lq, const sfp_conv* c, const uint64_t* pinv,
                   int add0, int add1, uint64_t* scratch);
+
+// sfp_ks_inner that also folds the relinearised polys' last q row into the
+// accumulators: acc_p,l += fold_k * fold_p,l  (l = ell-1, fold_k = P mod q_l),
+// the input sfp_moddown_rescale expects.
+void sfp_ks_inner_fold(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
+                       size_t ext_stride, const uint64_t* key, uint32_t beta, uint32_t ell,
+                       uint32_t K, uint32_t Lq, const uint64_t* fold0, const uint64_t* fold1,
+                       uint64_t fold_k);
+
+// ModDown + add + rescale in one conversion (EvalMult's relinearisation and
+// its rescale).  With acc from sfp_ks_inner_fold(fold = d0, d1), l = ell-1:
+//   s_p,i = d_p,i + ModDown(acc_p)_i  (i < l),   s_p,l = ModDown(acc_p)_l
+//   out_p = Rescale(s_p)  (l rows at out0 / out1)
+// Bit-identical to sfp_moddown2(add) + sfp_rescale on unfolded accumulators:
+// the dropped row's coefficients r = (INTT(acc_l) - conv_l) P^-1 come out of
+// the conversion, and out_i = (acc_i - NTT(conv_i + P [r]_i)) (P q_l)^-1
+// + d_i q_l^-1 needs one NTT instead of two.
+//   pinv[i] = P^-1, pmod[i] = P mod q_i (i < ell);  qlinv[i] = q_l^-1 mod q_i
+//   (i < l).  acc is destroyed.  scratch: 2*l*n words.
+void sfp_moddown_rescale(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint64_t* d0,
+                         const uint64_t* d1, uint64_t* acc, size_t acc_stride, uint32_t ell,
+                         uint32_t K, uint32_t Lq, const sfp_conv* c, const uint64_t* pinv,
+                         const uint64_t* pmod, const uint64_t* qlinv, uint64_t* scratch);
 
 // ---- sampling (counter-based, deterministic) ------------------------------------
 // Uniform residues mod each limb's prime: value for (limb, i) is derived from
