@@ -528,11 +528,13 @@ __device__ __forceinline__ u64* rowAt(const RowPtr& r, uint32_t p, uint32_t i) {
 // Developer build knob: SFHE_NTT_TRACE accumulates per-phase shader clocks
 // of every block (thread 0, after each barrier) for tools/microbench.
 #ifdef SFHE_NTT_TRACE
-__device__ unsigned long long g_nttTrace[4][8];
+constexpr int kTraceSlots = 256;  // spread the atomics: no contention artefacts
+__device__ unsigned long long g_nttTrace[kTraceSlots][4][8];
 #define NTT_MARK(i)                                                          \
     if (threadIdx.x == 0) {                                                  \
         const unsigned long long t_ = clock64();                             \
-        atomicAdd(&g_nttTrace[INV * 2 + COL][(i)], t_ - tprev);              \
+        atomicAdd(&g_nttTrace[(blockIdx.x + blockIdx.y * gridDim.x) % kTraceSlots][INV * 2 + COL][(i)], \
+                  t_ - tprev);                                               \
         tprev = t_;                                                          \
     }
 #else
@@ -568,8 +570,13 @@ __global__ __launch_bounds__(kNttTile >> LE) void k_ntt(const RowGroup G, const 
     T.d = COL ? logR : 8u;
     T.logC = COL ? (uint32_t)__builtin_ctz(kNttTile) - logR : 0u;
     T.C = 1u << T.logC;
-    T.c0 = COL ? blockIdx.x * T.C : 0u;
-    T.r0 = COL ? 0u : blockIdx.x * kNttRows;
+    // XCD-aware tile order: workgroups go to the 8 XCDs round-robin by id, so
+    // block x runs on XCD x % 8.  Give each XCD a contiguous run of tiles:
+    // COL tiles of C < 16 words share 128-byte lines with their neighbours
+    // (and ROW tiles share twiddle lines), which then meet in one L2.
+    const uint32_t tile = (gridDim.x & 7) ? blockIdx.x : (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    T.c0 = COL ? tile * T.C : 0u;
+    T.r0 = COL ? 0u : tile * kNttRows;
     const uint32_t S0 = COL ? 0u : logR;
 
     // the pass's twiddle table (value, Shoup companion or W/q) for this prime
@@ -713,7 +720,8 @@ __global__ __launch_bounds__(kNttTile >> LE) void k_ntt(const RowGroup G, const 
     }
     NTT_MARK(5);
 #ifdef SFHE_NTT_TRACE
-    if (threadIdx.x == 0) atomicAdd(&g_nttTrace[INV * 2 + COL][7], 1ull);
+    if (threadIdx.x == 0)
+        atomicAdd(&g_nttTrace[(blockIdx.x + blockIdx.y * gridDim.x) % kTraceSlots][INV * 2 + COL][7], 1ull);
 #endif
 }
 
@@ -1512,8 +1520,13 @@ void sfp_ntt(sfp_dev* d, uint64_t* p, sfp_limbs m, int inverse) {
 extern "C" int sfp_ntt_trace(sfp_dev* d, unsigned long long* out32) {
 #ifdef SFHE_NTT_TRACE
     syncAll(d);
-    SFP_CHECK(hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_nttTrace), sizeof(unsigned long long) * 32));
-    static const unsigned long long zero[32] = {};
+    static unsigned long long all[kTraceSlots * 32];
+    SFP_CHECK(hipMemcpyFromSymbol(all, HIP_SYMBOL(g_nttTrace), sizeof all));
+    for (int i = 0; i < 32; ++i) {
+        out32[i] = 0;
+        for (int k = 0; k < kTraceSlots; ++k) out32[i] += all[k * 32 + i];
+    }
+    static const unsigned long long zero[kTraceSlots * 32] = {};
     SFP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_nttTrace), zero, sizeof zero));
     return 0;
 #else
