@@ -13,7 +13,7 @@ streaming read (x2); WRITE_SIZE is exact for 16-B-per-lane stores.  The NTT
 and k_conv / k_ks_inner read and write 16 B per lane where contiguous.
 
 Algorithmic bytes per launch (prims.h): NTT pass 16 B x coefficients of the
-launch (from the grid: 256 threads per 4096-word tile).
+launch (rows from the grid: k_ntt<INV, COL, LE> runs n / 2^LE threads per row).
 """
 import argparse
 import collections
@@ -21,6 +21,7 @@ import csv
 import hashlib
 import json
 import os
+import re
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -46,6 +47,14 @@ def load(path, counter):
     return per
 
 
+def ntt_rows(name: str, grid: int, n: int) -> int:
+    """Rows of one k_ntt<INV, COL, LE> launch: each thread of a pass holds
+    2^LE words, so a row takes n / 2^LE threads (Grid_Size = total threads)."""
+    m = re.search(r"k_ntt<\s*\w+,\s*\w+,\s*(\d+)>", name)
+    le = int(m.group(1)) if m else 3
+    return grid * (1 << le) // n
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch_csv")
@@ -62,21 +71,20 @@ def main():
     fam_w = collections.defaultdict(list)
     for _, (name, grid, v) in sorted(fe.items()):
         if family(name):
-            fam_f[family(name)].append((grid, v))
+            fam_f[family(name)].append((name, grid, v))
     for _, (name, grid, v) in sorted(wr.items()):
         if family(name):
-            fam_w[family(name)].append((grid, v))
+            fam_w[family(name)].append((name, grid, v))
     out = {}
     for fam in fam_f:
         F, W = fam_f[fam], fam_w.get(fam, [])
         k = min(len(F), len(W))
-        fetch = sum(v for _, v in F[:k]) * 1024 * 2
-        write = sum(v for _, v in W[:k]) * 1024
+        fetch = sum(v for _, _, v in F[:k]) * 1024 * 2
+        write = sum(v for _, _, v in W[:k]) * 1024
         entry = {"launches": k, "hbm_bytes_per_launch": (fetch + write) / k,
                  "fetch_bytes_per_launch": fetch / k, "write_bytes_per_launch": write / k}
         if fam == "ntt":
-            tiles_threads = 256 * (a.n // 4096)
-            algo = sum(16.0 * (g // tiles_threads) * a.n for g, _ in F[:k])
+            algo = sum(16.0 * ntt_rows(nm, g, a.n) * a.n for nm, g, _ in F[:k])
             entry["algorithmic_bytes_per_launch"] = algo / k
             entry["traffic_over_algorithmic"] = (fetch + write) / algo
         out[fam] = entry
