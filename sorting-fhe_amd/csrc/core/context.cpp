@@ -659,17 +659,21 @@ CryptoContextImpl<DCRTPoly>::CryptoContextImpl(const CCParams<CryptoContextCKKSR
             maxDigitBits = std::max(maxDigitBits, b);
         }
         // P must exceed every digit modulus with margin, or the key-switch
-        // noise (digit * error / P) is not negligible (special primes are
-        // just below 2^60)
-        uint32_t K = (uint32_t)std::ceil((maxDigitBits + 20.0) / 59.9);
+        // noise (digit * error / P) is not negligible.  The special primes
+        // sit just below 2^42 when the scaling primes do (so every row but
+        // q_0 takes the device's FP64 arithmetic: NTT, base conversion),
+        // just below 2^60 otherwise.
+        const u64 pTop = sbits <= 41 ? (1ull << 42) : (1ull << 60);
         std::vector<u64> P;
-        u64 bound = 1ull << 60;
-        for (uint32_t k = 0; k < K; ++k) {
+        u64 bound = pTop;
+        for (double bitsP = 0; bitsP < maxDigitBits + 20.0;) {
             u64 pr = primeBelow(bound, m, used);
             used.insert(pr);
             P.push_back(pr);
+            bitsP += std::log2((double)pr);
             bound = pr;
         }
+        const uint32_t K = (uint32_t)P.size();
         u64 qext = 0;
         if (s.ext) {
             qext = primeNear(std::ldexp(1.0, (int)sbits), m, used);

@@ -131,6 +131,15 @@ struct sfp_conv {
     u64* mod = nullptr;       // device [ns][nt]
     u64* sprod = nullptr;     // device [nt]: prod(S) mod dst_t (centred conversion)
     uint32_t* drow = nullptr; // device [nt]: output row of target t
+    // FP64 form (k_convf / k_mdrsf; see ConvJob): targets split into FP64
+    // and integer rows, FP64 multiplier tables over the FP64 targets
+    bool fpOk = false;                       // at most kMaxConvBig 60-bit sources
+    uint32_t nbig = 0;                       // 60-bit sources
+    std::vector<uint32_t> hFpT, hIntT;       // ascending target indices
+    uint32_t *fpT = nullptr, *intT = nullptr;
+    double *invD = nullptr, *invQ = nullptr;  // [ns] inv as a double, inv / s_i
+    double *vD = nullptr, *vQ = nullptr;      // [ns][hFpT.size()]
+    double *hD = nullptr, *hQ = nullptr;      // [kMaxConvBig][hFpT.size()]
     std::vector<uint32_t> hsrc, hdst;
 };
 
@@ -491,6 +500,7 @@ __device__ __forceinline__ void nttRoundDynFP(int b, double* s, const NttTile& T
     if (b == 2) return nttRoundFP<INV, COL, LE, 2>(s, T, S0, k0, q, w, wq);
     nttRoundFP<INV, COL, LE, 1>(s, T, S0, k0, q, w, wq);
 }
+
 
 // A 2-D set of rows for one NTT launch, passed by value: row (p, i) for
 // p < P, i < R lives at base + p*ps + i*is (word offsets).  Prime of row i:
@@ -922,58 +932,231 @@ constexpr int kMaxConvSrc = 32;
 // mod t once per y_i > s_i/2), which makes the ModDown conversion error
 // sum_i y_i/s_i zero-mean: a rounding, not a floor with a +K/2 bias.
 // Fast base conversion of several jobs in one launch (grid: x = coefficient
-// blocks, y = job, z = chunk of kConvChunk targets).  For source rows s_i
+// pairs, y = job, z = chunk of kConvChunk targets).  For source rows s_i
 // (coefficient domain) and targets t:
 //   y_i = [s_i * inv_i]_{q_i};  out_t = sum_i y_i * mod[i][t]  mod p_t
 // centred: subtract prod(q_i) mod p_t once per y_i > q_i/2 (value in
 // (-Q/2, Q/2] instead of [0, Q)).
 constexpr int kConvChunk = 12;
 constexpr int kMaxConvJobs = 16;
+constexpr int kMaxConvBig = 2;  // 60-bit sources the FP64 form splits in two
 struct ConvJob {
     const u64* src;
     u64* dst;
     const uint32_t *sidx, *didx, *drow;
     const u64 *inv, *mod, *sprod;
-    uint32_t ns, nt, ntUse, centered;
+    // FP64 form (k_convf): targets split into FP64 rows fpT[0..nFp) and
+    // integer rows intT[0..nInt) (indices into the table's targets, the ones
+    // below ntUse); vD/vQ [i][k] = mod[i][fpT[k]] (/ p), and for the b-th
+    // 60-bit source hD/hQ [b][k] = mod[i][fpT[k]] * 2^30 mod p (/ p)
+    const uint32_t *fpT, *intT;
+    const double *invD, *invQ, *vD, *vQ, *hD, *hQ;
+    uint32_t ns, nt, ntUse, centered, nFp, nInt, nFpAll, nbig;
 };
 struct ConvJobs {
     ConvJob j[kMaxConvJobs];
 };
 
-__global__ __launch_bounds__(kThreads) void k_conv(const ConvJobs J, const sf_barrett* __restrict__ bar,
-                                                   uint32_t logn) {
-    __shared__ u64 smod[kMaxConvSrc * kConvChunk];
-    const ConvJob& c = J.j[blockIdx.y];
-    const uint32_t t0 = blockIdx.z * kConvChunk;
-    if (t0 >= c.ntUse) return;
-    const uint32_t tc = min((uint32_t)kConvChunk, c.ntUse - t0);
-    for (uint32_t e = threadIdx.x; e < c.ns * tc; e += kThreads) {
-        const uint32_t i = e / tc, t = e % tc;
-        smod[i * kConvChunk + t] = c.mod[(size_t)i * c.nt + t0 + t];
-    }
-    __syncthreads();
-    const uint32_t n = 1u << logn;
-    const uint32_t x = blockIdx.x * kThreads + threadIdx.x;
-    if (x >= n) return;
-    u64 y[kMaxConvSrc];
-    u64 neg = 0;
+// One integer-path target row for two adjacent coefficients from canonical
+// source residues ya/yb (centred: prod(S) subtracted once per y > q/2).
+template <int NS>
+__device__ __forceinline__ ulonglong2 convIntTarget(const u64 (&ya)[NS], const u64 (&yb)[NS], uint32_t ns,
+                                                    const u64* smodCol, int stride, const sf_barrett* sB,
+                                                    const sf_barrett& B, u64 sprod, bool centred) {
+    Acc s0{0, 0}, s1{0, 0};
+    u64 na = 0, nb = 0;
 #pragma unroll
-    for (int i = 0; i < kMaxConvSrc; ++i) {
-        if ((uint32_t)i < c.ns) {
-            const sf_barrett B = loadBar(bar, c.sidx[i]);
-            y[i] = bmul(c.src[((size_t)i << logn) + x], c.inv[i], B);
-            if (c.centered && y[i] > (B.q >> 1)) ++neg;
+    for (int i = 0; i < NS; ++i) {
+        if ((uint32_t)i < ns) {
+            const u64 m = smodCol[i * stride];
+            macc(s0, ya[i], m);
+            macc(s1, yb[i], m);
+            if (centred) {
+                const u64 h = sB[i].q >> 1;
+                na += ya[i] > h;
+                nb += yb[i] > h;
+            }
         }
     }
-    for (uint32_t t = 0; t < tc; ++t) {
-        Acc acc{0, 0};
+    ulonglong2 o;
+    o.x = sf_reduce128_acc(s0.lo, s0.hi, &B);
+    o.y = sf_reduce128_acc(s1.lo, s1.hi, &B);
+    if (na) o.x = sf_sub(o.x, bmul(na, sprod, B), B.q);
+    if (nb) o.y = sf_sub(o.y, bmul(nb, sprod, B), B.q);
+    return o;
+}
+
+// Integer form: two adjacent coefficients per thread, every constant staged
+// in LDS (the output stores may alias global tables, which would otherwise
+// force a reload of each per-target constant after every store).
+__global__ __launch_bounds__(kThreads) void k_conv(const ConvJobs J, const sf_barrett* __restrict__ bar,
+                                                   uint32_t logn) {
+    constexpr int C = kConvChunk, NS = kMaxConvSrc;
+    __shared__ u64 smod[NS * C];
+    __shared__ sf_barrett sB[NS], tB[C];
+    __shared__ u64 sInv[NS], tSp[C];
+    __shared__ uint32_t tRow[C];
+    const ConvJob& c = J.j[blockIdx.y];
+    const uint32_t t0 = blockIdx.z * C;
+    if (t0 >= c.ntUse) return;
+    const uint32_t tc = min((uint32_t)C, c.ntUse - t0);
+    const uint32_t ns = c.ns;
+    if (threadIdx.x < ns) {
+        sB[threadIdx.x] = loadBar(bar, c.sidx[threadIdx.x]);
+        sInv[threadIdx.x] = c.inv[threadIdx.x];
+    } else if (threadIdx.x >= 64 && threadIdx.x < 64 + tc) {
+        const uint32_t k = threadIdx.x - 64, t = t0 + k;
+        tB[k] = loadBar(bar, c.didx[t]);
+        tSp[k] = c.sprod[t];
+        tRow[k] = c.drow[t];
+    }
+    for (uint32_t e = threadIdx.x; e < ns * tc; e += kThreads) {
+        const uint32_t i = e / tc, k = e % tc;
+        smod[i * C + k] = c.mod[(size_t)i * c.nt + t0 + k];
+    }
+    __syncthreads();
+    const uint32_t x = 2 * (blockIdx.x * kThreads + threadIdx.x);
+    if (x >= (1u << logn)) return;
+    u64 ya[NS], yb[NS];
 #pragma unroll
-        for (int i = 0; i < kMaxConvSrc; ++i)
-            if ((uint32_t)i < c.ns) macc(acc, y[i], smod[i * kConvChunk + t]);
-        const sf_barrett B = loadBar(bar, c.didx[t0 + t]);
-        u64 v = sf_reduce128_acc(acc.lo, acc.hi, &B);
-        if (neg) v = sf_sub(v, bmul(neg, c.sprod[t0 + t], B), B.q);
-        c.dst[((size_t)c.drow[t0 + t] << logn) + x] = v;
+    for (int i = 0; i < NS; ++i) {
+        if ((uint32_t)i < ns) {
+            const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(c.src + ((size_t)i << logn) + x);
+            const sf_barrett B = sB[i];
+            ya[i] = bmul(v.x, sInv[i], B);
+            yb[i] = bmul(v.y, sInv[i], B);
+        }
+    }
+    for (uint32_t k = 0; k < tc; ++k) {
+        const ulonglong2 o = convIntTarget<NS>(ya, yb, ns, smod + k, C, sB, tB[k], tSp[k], c.centered);
+        *reinterpret_cast<ulonglong2*>(c.dst + ((size_t)tRow[k] << logn) + x) = o;
+    }
+}
+
+// y = [s * inv]_q for an FP64 source, canonical or (centred) in (-q/2, q/2]
+__device__ __forceinline__ double fpSourceY(u64 s, double qd, double iv, double ivq, double qi, bool centred) {
+    const double y = fpReduce(fpMulMod((double)s, iv, ivq, qd), qd, qi);
+    return centred && y > 0.5 * (qd - 1.0) ? y - qd : y;
+}
+
+// FP64 conversion, block-cooperative form.  A block owns kConvCoefs
+// consecutive coefficients and one chunk of kConvChunk targets of one job.
+// Phase 1: the block's threads compute y_i for every (source, coefficient)
+// pair once (coalesced 8 B/lane loads) into LDS -- FP64 sources as exact
+// doubles (signed when centred), a 60-bit source as y = yh 2^30 + yl (two
+// exact doubles, the second with the multiplier mod * 2^30 mod p), and for
+// integer-target blocks every source as its canonical residue.  Phase 2:
+// each wave takes targets k = wave, wave + 4, ... for its 64 coefficients:
+// the source-major y reads are conflict-free and the multipliers are
+// wave-uniform LDS broadcasts.  Many small blocks (n / 64 per chunk) keep
+// many waves per SIMD in flight where one thread per coefficient pair had 2.
+// Arithmetic and outputs as k_conv (canonical residues, bit-identical).
+constexpr int kConvCoefs = 256;  // = kThreads: one coefficient column per thread in phase 1
+
+template <int NS>
+__global__ __launch_bounds__(kThreads) void k_convf(const ConvJobs J, const sf_barrett* __restrict__ bar,
+                                                    const double* __restrict__ qinvD, uint32_t logn) {
+    constexpr int C = kConvChunk, NB = kMaxConvBig, X = kConvCoefs, WAVES = kThreads / 64;
+    __shared__ double sD[NS * C], sQ[NS * C], hDs[NB * C], hQs[NB * C];
+    __shared__ u64 smod[NS * C];
+    __shared__ sf_barrett sB[NS], tB[C];
+    __shared__ double sInvD[NS], sInvQ[NS], sQi[NS], tQi[C];
+    __shared__ u64 sInv[NS], tSp[C];
+    __shared__ uint32_t tRow[C], sBig[NS];
+    __shared__ u64 yL[NS * X];     // FP64 blocks: doubles' bits; integer blocks: residues
+    __shared__ double yH[NB * X];  // 60-bit sources' high parts
+    const ConvJob& c = J.j[blockIdx.y];
+    const uint32_t fpChunks = (c.nFp + C - 1) / C;
+    const bool fpBlock = blockIdx.z < fpChunks;
+    const uint32_t k0 = (fpBlock ? blockIdx.z : blockIdx.z - fpChunks) * C;
+    const uint32_t cnt = fpBlock ? c.nFp : c.nInt;
+    if (k0 >= cnt) return;
+    const uint32_t tc = min((uint32_t)C, cnt - k0);
+    const uint32_t ns = c.ns;
+    const uint32_t* tl = fpBlock ? c.fpT : c.intT;
+    if (threadIdx.x < ns) {
+        const uint32_t i = threadIdx.x, pi = c.sidx[i];
+        sB[i] = loadBar(bar, pi);
+        sQi[i] = qinvD[pi];
+        sInv[i] = c.inv[i];
+        sInvD[i] = c.invD[i];
+        sInvQ[i] = c.invQ[i];
+        uint32_t rank = 0;  // 60-bit sources before i (their high-part slot)
+        for (uint32_t k = 0; k < i; ++k) rank += bar[c.sidx[k]].q >= kFpPrimeBound;
+        sBig[i] = bar[pi].q >= kFpPrimeBound ? rank : 0xffffffffu;
+    } else if (threadIdx.x >= 64 && threadIdx.x < 64 + tc) {
+        const uint32_t k = threadIdx.x - 64, t = tl[k0 + k];
+        tB[k] = loadBar(bar, c.didx[t]);
+        tQi[k] = qinvD[c.didx[t]];
+        tSp[k] = c.sprod[t];
+        tRow[k] = c.drow[t];
+    }
+    for (uint32_t e = threadIdx.x; e < ns * tc; e += kThreads) {
+        const uint32_t i = e / tc, k = e % tc;
+        if (fpBlock) {
+            sD[i * C + k] = c.vD[(size_t)i * c.nFpAll + k0 + k];
+            sQ[i * C + k] = c.vQ[(size_t)i * c.nFpAll + k0 + k];
+        } else {
+            smod[i * C + k] = c.mod[(size_t)i * c.nt + tl[k0 + k]];
+        }
+    }
+    if (fpBlock)
+        for (uint32_t e = threadIdx.x; e < NB * tc; e += kThreads) {
+            const uint32_t b = e / tc, k = e % tc;
+            hDs[b * C + k] = c.hD[(size_t)b * c.nFpAll + k0 + k];
+            hQs[b * C + k] = c.hQ[(size_t)b * c.nFpAll + k0 + k];
+        }
+    __syncthreads();
+    const uint32_t x0 = blockIdx.x * X, lane = threadIdx.x % 64, w = threadIdx.x / 64;
+    const bool cen = c.centered;
+    // phase 1: y for every (source, coefficient) pair (thread = coefficient column)
+    for (uint32_t i = 0; i < ns; ++i) {
+        const uint32_t cx = threadIdx.x;
+        const u64 s = c.src[((size_t)i << logn) + x0 + cx];
+        const sf_barrett B = sB[i];
+        if (!fpBlock) {
+            yL[i * X + cx] = bmul(s, sInv[i], B);
+        } else if (B.q < kFpPrimeBound) {
+            yL[i * X + cx] = __double_as_longlong(fpSourceY(s, (double)B.q, sInvD[i], sInvQ[i], sQi[i], cen));
+        } else {
+            long long v = (long long)bmul(s, sInv[i], B);
+            if (cen && v > (long long)(B.q >> 1)) v -= (long long)B.q;
+            yL[i * X + cx] = __double_as_longlong((double)(v & ((1ll << 30) - 1)));
+            yH[sBig[i] * X + cx] = (double)(v >> 30);
+        }
+    }
+    __syncthreads();
+    // phase 2: this wave's targets for every coefficient of the block
+    for (uint32_t kc = w * 64; kc < tc * X; kc += WAVES * 64) {  // wave w: coefficients [64w, 64w+64) of every target
+        const uint32_t k = kc / X, cx = kc % X + lane;
+        const sf_barrett B = tB[k];
+        u64 out;
+        if (fpBlock) {
+            const double pd = (double)B.q;
+            double a = 0.0;
+#pragma unroll
+            for (int i = 0; i < NS; ++i)
+                if ((uint32_t)i < ns)
+                    a += fpMulMod(__longlong_as_double(yL[i * X + cx]), sD[i * C + k], sQ[i * C + k], pd);
+#pragma unroll
+            for (int b = 0; b < NB; ++b)
+                if ((uint32_t)b < c.nbig) a += fpMulMod(yH[b * X + cx], hDs[b * C + k], hQs[b * C + k], pd);
+            out = (u64)fpReduce(a, pd, tQi[k]);
+        } else {
+            Acc s0{0, 0};
+            u64 neg = 0;
+#pragma unroll
+            for (int i = 0; i < NS; ++i) {
+                if ((uint32_t)i < ns) {
+                    const u64 y = yL[i * X + cx];
+                    macc(s0, y, smod[i * C + k]);
+                    neg += cen && y > (sB[i].q >> 1);
+                }
+            }
+            out = sf_reduce128_acc(s0.lo, s0.hi, &B);
+            if (neg) out = sf_sub(out, bmul(neg, tSp[k], B), B.q);
+        }
+        c.dst[((size_t)tRow[k] << logn) + x0 + cx] = out;
     }
 }
 
@@ -992,64 +1175,181 @@ struct MdrsArgs {
     const uint32_t* sidx;
     const u64 *inv, *mod, *sprod;  // the ModDown conversion table (targets 0..)
     const u64 *pmod, *lsub;        // P mod q_t, q_l mod q_t
+    // FP64 form (k_mdrsf): the table's FP64 companions (target rows fpT /
+    // intT as in ConvJob, restricted to t < l), the dropped row's column
+    // (lD/lQ [i * nFpAll] = mod[i][l] (/ q_l)) and P mod q_t as doubles
+    const uint32_t *fpT, *intT;
+    const double *invD, *invQ, *vD, *vQ, *lD, *lQ, *pmodD, *pmodQ;
     u64 pinvl;                     // P^-1 mod q_l
-    uint32_t ns, nt, l;
+    uint32_t ns, nt, l, nFp, nInt, nFpAll;
 };
 
+// Integer form, two coefficients per thread, constants in LDS.
 __global__ __launch_bounds__(kThreads) void k_conv_mdrs(const MdrsArgs A, const sf_barrett* __restrict__ bar,
                                                         uint32_t logn) {
-    constexpr int W = kConvChunk + 1;  // the chunk's targets + target l
-    __shared__ u64 smod[kMaxConvSrc * W];
+    constexpr int C = kConvChunk, W = C + 1, NS = kMaxConvSrc;  // column C: the dropped row l
+    __shared__ u64 smod[NS * W];
+    __shared__ sf_barrett sB[NS], tB[W];
+    __shared__ u64 sInv[NS], tSp[W], tPm[W], tLs[W];
     const MdrsJob& J = A.j[blockIdx.y];
-    const uint32_t t0 = blockIdx.z * kConvChunk;
+    const uint32_t t0 = blockIdx.z * C;
     if (t0 >= A.l) return;
-    const uint32_t tc = min((uint32_t)kConvChunk, A.l - t0);
-    for (uint32_t e = threadIdx.x; e < A.ns * W; e += kThreads) {
-        const uint32_t i = e / W, t = e % W;
-        const uint32_t tt = t < tc ? t0 + t : A.l;
-        smod[e] = t < tc || t == (uint32_t)kConvChunk ? A.mod[(size_t)i * A.nt + tt] : 0;
+    const uint32_t tc = min((uint32_t)C, A.l - t0);
+    const uint32_t ns = A.ns;
+    if (threadIdx.x < ns) {
+        sB[threadIdx.x] = loadBar(bar, A.sidx[threadIdx.x]);
+        sInv[threadIdx.x] = A.inv[threadIdx.x];
+    } else if (threadIdx.x >= 64 && threadIdx.x < 64 + W && (threadIdx.x - 64 < tc || threadIdx.x - 64 == C)) {
+        const uint32_t k = threadIdx.x - 64, tt = k < tc ? t0 + k : A.l;
+        tB[k] = loadBar(bar, tt);
+        tSp[k] = A.sprod[tt];
+        if (k < tc) {
+            tPm[k] = A.pmod[tt];
+            tLs[k] = A.lsub[tt];
+        }
+    }
+    for (uint32_t e = threadIdx.x; e < ns * W; e += kThreads) {
+        const uint32_t i = e / W, k = e % W;
+        const bool use = k < tc || k == (uint32_t)C;
+        smod[e] = use ? A.mod[(size_t)i * A.nt + (k < tc ? t0 + k : A.l)] : 0;
     }
     __syncthreads();
-    const uint32_t n = 1u << logn;
-    const uint32_t x = blockIdx.x * kThreads + threadIdx.x;
-    if (x >= n) return;
-    u64 y[kMaxConvSrc];
-    u64 neg = 0;
+    const uint32_t x = 2 * (blockIdx.x * kThreads + threadIdx.x);
+    if (x >= (1u << logn)) return;
+    u64 ya[NS], yb[NS];
 #pragma unroll
-    for (int i = 0; i < kMaxConvSrc; ++i) {
-        if ((uint32_t)i < A.ns) {
-            const sf_barrett B = loadBar(bar, A.sidx[i]);
-            y[i] = bmul(J.src[((size_t)i << logn) + x], A.inv[i], B);
-            if (y[i] > (B.q >> 1)) ++neg;
+    for (int i = 0; i < NS; ++i) {
+        if ((uint32_t)i < ns) {
+            const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(J.src + ((size_t)i << logn) + x);
+            const sf_barrett B = sB[i];
+            ya[i] = bmul(v.x, sInv[i], B);
+            yb[i] = bmul(v.y, sInv[i], B);
         }
     }
     // the dropped row: r = (a_l - conv_l) * P^-1 mod q_l
-    u64 r;
-    bool rneg;
-    {
-        Acc acc{0, 0};
-#pragma unroll
-        for (int i = 0; i < kMaxConvSrc; ++i)
-            if ((uint32_t)i < A.ns) macc(acc, y[i], smod[i * W + kConvChunk]);
-        const sf_barrett B = loadBar(bar, A.l);
-        u64 c = sf_reduce128_acc(acc.lo, acc.hi, &B);
-        if (neg) c = sf_sub(c, bmul(neg, A.sprod[A.l], B), B.q);
-        r = bmul(sf_sub(J.al[((size_t)A.l << logn) + x], c, B.q), A.pinvl, B);
-        rneg = r > (B.q >> 1);
+    const sf_barrett BL = tB[C];
+    const ulonglong2 cl = convIntTarget<NS>(ya, yb, ns, smod + C, W, sB, BL, tSp[C], true);
+    const ulonglong2 al = *reinterpret_cast<const ulonglong2*>(J.al + ((size_t)A.l << logn) + x);
+    const u64 ra = bmul(sf_sub(al.x, cl.x, BL.q), A.pinvl, BL), rb = bmul(sf_sub(al.y, cl.y, BL.q), A.pinvl, BL);
+    const bool na = ra > (BL.q >> 1), nb = rb > (BL.q >> 1);
+    for (uint32_t k = 0; k < tc; ++k) {
+        const sf_barrett B = tB[k];
+        ulonglong2 v = convIntTarget<NS>(ya, yb, ns, smod + k, W, sB, B, tSp[k], true);
+        u64 la = sf_reduce128(ra, 0, &B), lb = sf_reduce128(rb, 0, &B);
+        if (na) la = sf_sub(la, tLs[k], B.q);
+        if (nb) lb = sf_sub(lb, tLs[k], B.q);
+        v.x = sf_add(v.x, bmul(la, tPm[k], B), B.q);
+        v.y = sf_add(v.y, bmul(lb, tPm[k], B), B.q);
+        *reinterpret_cast<ulonglong2*>(J.dst + ((size_t)(t0 + k) << logn) + x) = v;
     }
-    for (uint32_t t = 0; t < tc; ++t) {
-        const uint32_t tt = t0 + t;
-        Acc acc{0, 0};
+}
+
+// FP64 form of k_conv_mdrs, block-cooperative as k_convf: every source (P
+// row) and the dropped row's prime below kFpPrimeBound.  Phase 1: the
+// centred y_i of every (source, coefficient) pair into LDS; then wave 0 forms
+// each coefficient's dropped-row value r = (a_l - conv_l) P^-1 mod q_l
+// (centred).  Phase 2: FP64 targets fold [r]_t P_t into the conversion sum;
+// integer targets (fpT / intT split as in k_convf) use canonical residues.
+template <int NS>
+__global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_barrett* __restrict__ bar,
+                                                    const double* __restrict__ qinvD, uint32_t logn) {
+    constexpr int C = kConvChunk, X = kConvCoefs, WAVES = kThreads / 64;
+    __shared__ double sD[NS * C], sQ[NS * C], sLD[NS], sLQ[NS];
+    __shared__ u64 smod[NS * C];
+    __shared__ sf_barrett sB[NS], tB[C];
+    __shared__ double sInvD[NS], sInvQ[NS], sQi[NS], tQi[C], tPd[C], tPq[C];
+    __shared__ u64 tSp[C], tPm[C], tLs[C];
+    __shared__ uint32_t tRow[C];
+    __shared__ double yL[NS * X], rL[X];
+    const MdrsJob& J = A.j[blockIdx.y];
+    const uint32_t fpChunks = (A.nFp + C - 1) / C;
+    const bool fpBlock = blockIdx.z < fpChunks;
+    const uint32_t k0 = (fpBlock ? blockIdx.z : blockIdx.z - fpChunks) * C;
+    const uint32_t cnt = fpBlock ? A.nFp : A.nInt;
+    if (k0 >= cnt) return;
+    const uint32_t tc = min((uint32_t)C, cnt - k0);
+    const uint32_t ns = A.ns;
+    const uint32_t* tl = fpBlock ? A.fpT : A.intT;
+    if (threadIdx.x < ns) {
+        const uint32_t i = threadIdx.x, pi = A.sidx[i];
+        sB[i] = loadBar(bar, pi);
+        sQi[i] = qinvD[pi];
+        sInvD[i] = A.invD[i];
+        sInvQ[i] = A.invQ[i];
+        sLD[i] = A.lD[(size_t)i * A.nFpAll];
+        sLQ[i] = A.lQ[(size_t)i * A.nFpAll];
+    } else if (threadIdx.x >= 64 && threadIdx.x < 64 + tc) {
+        const uint32_t k = threadIdx.x - 64, t = tl[k0 + k];
+        tB[k] = loadBar(bar, t);
+        tQi[k] = qinvD[t];
+        tSp[k] = A.sprod[t];
+        tPm[k] = A.pmod[t];
+        tLs[k] = A.lsub[t];
+        tPd[k] = A.pmodD[t];
+        tPq[k] = A.pmodQ[t];
+        tRow[k] = t;
+    }
+    for (uint32_t e = threadIdx.x; e < ns * tc; e += kThreads) {
+        const uint32_t i = e / tc, k = e % tc;
+        if (fpBlock) {
+            sD[i * C + k] = A.vD[(size_t)i * A.nFpAll + k0 + k];
+            sQ[i * C + k] = A.vQ[(size_t)i * A.nFpAll + k0 + k];
+        } else {
+            smod[i * C + k] = A.mod[(size_t)i * A.nt + tl[k0 + k]];
+        }
+    }
+    __syncthreads();
+    const uint32_t x0 = blockIdx.x * X, lane = threadIdx.x % 64, w = threadIdx.x / 64;
+    for (uint32_t i = 0; i < ns; ++i) {
+        const uint32_t cx = threadIdx.x;
+        const u64 s = J.src[((size_t)i << logn) + x0 + cx];
+        yL[i * X + cx] = fpSourceY(s, (double)sB[i].q, sInvD[i], sInvQ[i], sQi[i], true);
+    }
+    __syncthreads();
+    const double qld = (double)bar[A.l].q;
+    {  // the dropped row: r = (a_l - conv_l) * P^-1 mod q_l, centred (thread = coefficient)
+        const uint32_t cx = threadIdx.x;
+        double cl = 0.0;
 #pragma unroll
-        for (int i = 0; i < kMaxConvSrc; ++i)
-            if ((uint32_t)i < A.ns) macc(acc, y[i], smod[i * W + t]);
-        const sf_barrett B = loadBar(bar, tt);
-        u64 v = sf_reduce128_acc(acc.lo, acc.hi, &B);
-        if (neg) v = sf_sub(v, bmul(neg, A.sprod[tt], B), B.q);
-        u64 lift = sf_reduce128(r, 0, &B);
-        if (rneg) lift = sf_sub(lift, A.lsub[tt], B.q);
-        v = sf_add(v, bmul(lift, A.pmod[tt], B), B.q);
-        J.dst[((size_t)tt << logn) + x] = v;
+        for (int i = 0; i < NS; ++i)
+            if ((uint32_t)i < ns) cl += fpMulMod(yL[i * X + cx], sLD[i], sLQ[i], qld);
+        const double qli = qinvD[A.l];
+        const u64 al = J.al[((size_t)A.l << logn) + x0 + cx];
+        const double pl = (double)A.pinvl;
+        rL[cx] = fpSourceY((u64)fpReduce((double)al - fpReduce(cl, qld, qli), qld, qli), qld, pl, pl / qld, qli,
+                           true);
+    }
+    __syncthreads();
+    for (uint32_t kc = w * 64; kc < tc * X; kc += WAVES * 64) {  // wave w: coefficients [64w, 64w+64) of every target
+        const uint32_t k = kc / X, cx = kc % X + lane;
+        const double r = rL[cx];
+        u64 out;
+        if (fpBlock) {
+            const double pd = (double)tB[k].q;
+            double a = fpMulMod(r, tPd[k], tPq[k], pd);
+#pragma unroll
+            for (int i = 0; i < NS; ++i)
+                if ((uint32_t)i < ns) a += fpMulMod(yL[i * X + cx], sD[i * C + k], sQ[i * C + k], pd);
+            out = (u64)fpReduce(a, pd, tQi[k]);
+        } else {
+            const sf_barrett B = tB[k];
+            Acc s0{0, 0};
+            u64 neg = 0;
+#pragma unroll
+            for (int i = 0; i < NS; ++i) {
+                if ((uint32_t)i < ns) {
+                    const double y = yL[i * X + cx];
+                    macc(s0, (u64)(y < 0.0 ? y + (double)sB[i].q : y), smod[i * C + k]);
+                    neg += y < 0.0;
+                }
+            }
+            out = sf_reduce128_acc(s0.lo, s0.hi, &B);
+            if (neg) out = sf_sub(out, bmul(neg, tSp[k], B), B.q);
+            u64 lift = sf_reduce128((u64)(r < 0.0 ? r + qld : r), 0, &B);
+            if (r < 0.0) lift = sf_sub(lift, tLs[k], B.q);
+            out = sf_add(out, bmul(lift, tPm[k], B), B.q);
+        }
+        J.dst[((size_t)tRow[k] << logn) + x0 + cx] = out;
     }
 }
 
@@ -1808,6 +2108,48 @@ sfp_conv* sfp_upload_conv(sfp_dev* d, uint32_t ns, const uint32_t* src, uint32_t
     }
     hipMalloc(&c->sprod, nt * 8);
     hostToDev(d, c->sprod, sp.data(), nt * 8);
+    // FP64 form: FP64 / integer target split, multipliers over the FP64
+    // targets, the 60-bit sources' second multiplier (mod * 2^30 mod p)
+    for (uint32_t t = 0; t < nt; ++t)
+        (d->hbar[dst[t]].q < kFpPrimeBound ? c->hFpT : c->hIntT).push_back(t);
+    std::vector<uint32_t> bigs;
+    for (uint32_t i = 0; i < ns; ++i)
+        if (d->hbar[src[i]].q >= kFpPrimeBound) bigs.push_back(i);
+    c->nbig = (uint32_t)bigs.size();
+    c->fpOk = bigs.size() <= (size_t)kMaxConvBig;
+    const size_t nf = c->hFpT.size();
+    std::vector<double> invD(ns), invQ(ns), vD(ns * nf + 1), vQ(ns * nf + 1), hD(kMaxConvBig * nf + 1, 0.0),
+        hQ(kMaxConvBig * nf + 1, 0.0);
+    for (uint32_t i = 0; i < ns; ++i) {
+        invD[i] = (double)inv[i];
+        invQ[i] = (double)inv[i] / (double)d->hbar[src[i]].q;
+        for (size_t k = 0; k < nf; ++k) {
+            const uint32_t t = c->hFpT[k];
+            const u64 m = mod[(size_t)i * nt + t];
+            vD[i * nf + k] = (double)m;
+            vQ[i * nf + k] = (double)m / (double)d->hbar[dst[t]].q;
+        }
+    }
+    for (size_t b = 0; b < bigs.size() && b < (size_t)kMaxConvBig; ++b)
+        for (size_t k = 0; k < nf; ++k) {
+            const uint32_t t = c->hFpT[k];
+            const u64 p = d->hbar[dst[t]].q;
+            const u64 m = (u64)(((unsigned __int128)mod[(size_t)bigs[b] * nt + t] << 30) % p);
+            hD[b * nf + k] = (double)m;
+            hQ[b * nf + k] = (double)m / (double)p;
+        }
+    auto up = [&](auto*& dp, const auto& v) {
+        hipMalloc(&dp, v.size() * sizeof(v[0]) + 8);
+        hostToDev(d, dp, v.data(), v.size() * sizeof(v[0]));
+    };
+    up(c->fpT, c->hFpT);
+    up(c->intT, c->hIntT);
+    up(c->invD, invD);
+    up(c->invQ, invQ);
+    up(c->vD, vD);
+    up(c->vQ, vQ);
+    up(c->hD, hD);
+    up(c->hQ, hQ);
     return c;
 }
 
@@ -1820,6 +2162,9 @@ void sfp_free_conv(sfp_dev* d, sfp_conv* c) {
     hipFree(c->mod);
     hipFree(c->sprod);
     hipFree(c->drow);
+    hipFree(c->fpT);
+    hipFree(c->intT);
+    for (double* x : {c->invD, c->invQ, c->vD, c->vQ, c->hD, c->hQ}) hipFree(x);
     delete c;
 }
 
@@ -1833,24 +2178,48 @@ static ConvJob convJob(const sfp_conv* c, u64* dst, const u64* src, uint32_t ntU
     j.inv = c->inv;
     j.mod = c->mod;
     j.sprod = c->sprod;
+    j.fpT = c->fpT;
+    j.intT = c->intT;
+    j.invD = c->invD;
+    j.invQ = c->invQ;
+    j.vD = c->vD;
+    j.vQ = c->vQ;
+    j.hD = c->hD;
+    j.hQ = c->hQ;
     j.ns = c->ns;
     j.nt = c->nt;
     j.ntUse = ntUse;
     j.centered = (uint32_t)centered;
+    // the FP64 / integer target lists are ascending: their first entries are
+    // the targets below ntUse
+    j.nFp = (uint32_t)(std::lower_bound(c->hFpT.begin(), c->hFpT.end(), ntUse) - c->hFpT.begin());
+    j.nInt = (uint32_t)(std::lower_bound(c->hIntT.begin(), c->hIntT.end(), ntUse) - c->hIntT.begin());
+    j.nFpAll = (uint32_t)c->hFpT.size();
+    j.nbig = c->nbig;
     return j;
 }
 
-static void convLaunch(sfp_dev* d, const ConvJobs& J, uint32_t njobs) {
+static void convLaunch(sfp_dev* d, const ConvJobs& J, uint32_t njobs, bool fpOk) {
     if (!njobs) return;
-    uint32_t maxT = 0;
+    uint32_t maxT = 0, maxS = 0, maxZ = 0;
     double bytes = 0;
     for (uint32_t k = 0; k < njobs; ++k) {
-        maxT = std::max(maxT, J.j[k].ntUse);
-        bytes += 8.0 * d->n * (J.j[k].ns + J.j[k].ntUse);
+        const ConvJob& j = J.j[k];
+        maxT = std::max(maxT, j.ntUse);
+        maxS = std::max(maxS, j.ns);
+        maxZ = std::max(maxZ, (j.nFp + kConvChunk - 1) / kConvChunk + (j.nInt + kConvChunk - 1) / kConvChunk);
+        bytes += 8.0 * d->n * (j.ns + j.ntUse);
     }
-    const dim3 g(d->n / kThreads, njobs, (maxT + kConvChunk - 1) / kConvChunk);
+    const bool fp = nttFp() && fpOk;
+    const dim3 g(fp ? d->n / kConvCoefs : d->n / (2 * kThreads), njobs,
+                 fp ? maxZ : (maxT + kConvChunk - 1) / kConvChunk);
     timedLaunch(d, SFP_FAM_CONV, bytes, [&] {
-        hipLaunchKernelGGL(k_conv, g, dim3(kThreads), 0, d->st(), J, d->bar, d->logn);
+        if (fp && maxS <= 16)
+            hipLaunchKernelGGL(k_convf<16>, g, dim3(kThreads), 0, d->st(), J, d->bar, d->qinvD, d->logn);
+        else if (fp)
+            hipLaunchKernelGGL(k_convf<kMaxConvSrc>, g, dim3(kThreads), 0, d->st(), J, d->bar, d->qinvD, d->logn);
+        else
+            hipLaunchKernelGGL(k_conv, g, dim3(kThreads), 0, d->st(), J, d->bar, d->logn);
     });
     checkLaunch(d, "conv");
 }
@@ -1858,7 +2227,7 @@ static void convLaunch(sfp_dev* d, const ConvJobs& J, uint32_t njobs) {
 void sfp_conv_apply(sfp_dev* d, uint64_t* dst, const uint64_t* src, const sfp_conv* c) {
     ConvJobs J;
     J.j[0] = convJob(c, dst, src, c->nt, 0);
-    convLaunch(d, J, 1);
+    convLaunch(d, J, 1, c->fpOk);
 }
 
 void sfp_modup(sfp_dev* d, uint64_t* ext, const uint64_t* in, uint32_t ell, uint32_t K,
@@ -1880,9 +2249,12 @@ void sfp_modup(sfp_dev* d, uint64_t* ext, const uint64_t* in, uint32_t ell, uint
     nttRows(d, A, 1);
     // every digit's conversion in one launch
     ConvJobs J;
-    for (uint32_t j = 0; j < beta; ++j)
+    bool fpOk = true;
+    for (uint32_t j = 0; j < beta; ++j) {
         J.j[j] = convJob(convs[j], ext + j * stride, scr + (size_t)j * alpha * n, convs[j]->nt, 0);
-    convLaunch(d, J, beta);
+        fpOk = fpOk && convs[j]->fpOk;
+    }
+    convLaunch(d, J, beta, fpOk);
     // NTT of every converted row (digit-own rows skipped)
     RowGroup B = rowsOf(beta, ell + K, sfp_limbs{ell + K, ell, Lq, 0});
     B.src = B.dst = RowPtr{ext, stride, (long long)n};
@@ -1929,7 +2301,7 @@ void sfp_moddown2(sfp_dev* d, uint64_t* out0, uint64_t* out1, uint64_t* acc, siz
     ConvJobs J;
     J.j[0] = convJob(c, scr, pRows, ell, 1);
     J.j[1] = convJob(c, scr + (size_t)ell * n, pRows + accStride, ell, 1);
-    convLaunch(d, J, 2);
+    convLaunch(d, J, 2, c->fpOk);
     RowGroup B = rowsOf(2, ell, sfp_limbs{ell, ell, 0, 0});
     B.src = B.dst = RowPtr{scr, (long long)ell * n, (long long)n};
     B.epi = 1;
@@ -1982,9 +2354,39 @@ void sfp_moddown_rescale(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint6
     M.ns = c->ns;
     M.nt = c->nt;
     M.l = l;
-    const dim3 g(n / kThreads, 2, (l + kConvChunk - 1) / kConvChunk);
+    // FP64 form: every source (P row) and the dropped row's prime FP64
+    const auto lpos = std::lower_bound(c->hFpT.begin(), c->hFpT.end(), l);
+    const bool fp = nttFp() && c->fpOk && c->nbig == 0 && lpos != c->hFpT.end() && *lpos == l;
+    uint32_t zc = (l + kConvChunk - 1) / kConvChunk;
+    if (fp) {
+        M.fpT = c->fpT;
+        M.intT = c->intT;
+        M.invD = c->invD;
+        M.invQ = c->invQ;
+        M.vD = c->vD;
+        M.vQ = c->vQ;
+        M.nFpAll = (uint32_t)c->hFpT.size();
+        M.lD = c->vD + (lpos - c->hFpT.begin());
+        M.lQ = c->vQ + (lpos - c->hFpT.begin());
+        M.nFp = (uint32_t)(lpos - c->hFpT.begin());
+        M.nInt = (uint32_t)(std::lower_bound(c->hIntT.begin(), c->hIntT.end(), l) - c->hIntT.begin());
+        double pd[SFP_MAX_LIMBS], pq[SFP_MAX_LIMBS];
+        for (uint32_t i = 0; i < l; ++i) {
+            pd[i] = (double)pmod[i];
+            pq[i] = (double)pmod[i] / (double)d->hbar[i].q;
+        }
+        M.pmodD = reinterpret_cast<const double*>(devConst(d, reinterpret_cast<const u64*>(pd), l));
+        M.pmodQ = reinterpret_cast<const double*>(devConst(d, reinterpret_cast<const u64*>(pq), l));
+        zc = (M.nFp + kConvChunk - 1) / kConvChunk + (M.nInt + kConvChunk - 1) / kConvChunk;
+    }
+    const dim3 g(fp ? n / kConvCoefs : n / (2 * kThreads), 2, zc);
     timedLaunch(d, SFP_FAM_CONV, 8.0 * n * 2 * (K + 1 + l), [&] {
-        hipLaunchKernelGGL(k_conv_mdrs, g, dim3(kThreads), 0, d->st(), M, d->bar, d->logn);
+        if (fp && c->ns <= 16)
+            hipLaunchKernelGGL(k_mdrsf<16>, g, dim3(kThreads), 0, d->st(), M, d->bar, d->qinvD, d->logn);
+        else if (fp)
+            hipLaunchKernelGGL(k_mdrsf<kMaxConvSrc>, g, dim3(kThreads), 0, d->st(), M, d->bar, d->qinvD, d->logn);
+        else
+            hipLaunchKernelGGL(k_conv_mdrs, g, dim3(kThreads), 0, d->st(), M, d->bar, d->logn);
     });
     checkLaunch(d, "conv_mdrs");
     // out_i = (acc_i - NTT(y_i)) (P q_l)^-1 + d_i q_l^-1

@@ -101,6 +101,12 @@ int main(int argc, char** argv) {
     const double mu = timeIt(d, 30, [&] {
         sfp_modup(d, ext, buf, ell, K, s->Lq, s->alpha, convs.data(), scr);
     });
+    for (uint32_t j = 0; j < beta; ++j) {
+        // source rows: the digit's own primes (rows lo.. of buf hold residues mod those)
+        const uint64_t* src = buf + (size_t)j * s->alpha * n;
+        const double cv = timeIt(d, 30, [&] { sfp_conv_apply(d, ext, src, convs[j]); });
+        std::printf("conv digit %u          : %8.2f us\n", j, cv);
+    }
     const double ki = timeIt(d, 30, [&] {
         sfp_ks_inner(d, acc, acc + stride, ext, stride, s->relinKey->ptr, beta, ell, K, s->Lq);
     });
