@@ -30,7 +30,7 @@ def family(name: str):
     s = name.split("(")[0].replace("void ", "")
     if s.startswith("k_ntt"):
         return "ntt"
-    if s == "k_conv":
+    if s.startswith("k_conv") or s.startswith("k_mdrs"):
         return "conv"
     if s == "k_ks_inner":
         return "ks_inner"
