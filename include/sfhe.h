@@ -166,6 +166,30 @@ int sfhe_sorter_place(sfhe_sorter* s, const sfhe_ct* rank, sfhe_ct* in, sfhe_ct*
 int sfhe_decompose(uint32_t N, const int32_t* keys, size_t nkeys, int32_t rotation, int32_t wrapN,
                    int algo, int32_t* values, int32_t* steps, size_t cap, size_t* count);
 
+/* ---- limb sharding (no reference counterpart: the reference
+ * runs one process on one device) -------------------------------------------
+ * One process per GPU; rank r of W holds the RNS limbs q_i / p_k with
+ * i % W == r / k % W == r.  Key generation and encryption run on every limb
+ * (setup); evaluation runs on the local limbs only, with three exchanges: the
+ * ModUp input (all-gather of the coefficient-form Q limbs), the ModDown P
+ * limbs (all-gather) and a rescale's dropped limb (broadcast by its owner).
+ * Decryption and sfhe_ct_download all-gather the limbs.  Every rank makes
+ * the same calls in the same order (they are collective); results are
+ * bit-identical to the unsharded context.  Call once per context, after
+ * sfhe_context_create and before sfhe_keygen, with the same params and seed
+ * on every rank. */
+/* 128-byte RCCL unique id (one rank; shared out of band).  SFHE_ENOTIMPL on
+ * a backend without RCCL (the CPU oracle). */
+int sfhe_comm_uid(uint8_t uid[128]);
+/* RCCL communicator over xGMI (the product path). */
+int sfhe_shard_rccl(sfhe_ctx* c, int rank, int world, const uint8_t uid[128]);
+/* Host-memory collectives supplied by the caller (tests; any transport):
+ * allgather writes world blocks of `bytes`, rank-major, into recv. */
+typedef void (*sfhe_allgather_fn)(void* user, const void* send, void* recv, size_t bytes);
+typedef void (*sfhe_bcast_fn)(void* user, void* buf, size_t bytes, int root);
+int sfhe_shard_host(sfhe_ctx* c, int rank, int world, sfhe_allgather_fn ag, sfhe_bcast_fn bc,
+                    void* user);
+
 #ifdef __cplusplus
 }
 #endif

@@ -39,6 +39,11 @@ struct sfp_dev {
     u64* q;
     u64 *psi, *psiS, *ipsi, *ipsiS;
     u64 *ninv, *ninvS;
+    /* limb sharding: rank of world, host-callback collectives */
+    int rank, world;
+    sfp_host_allgather_fn ag;
+    sfp_host_bcast_fn bc;
+    void* user;
 };
 
 struct sfp_conv {
@@ -62,13 +67,14 @@ static inline uint32_t brev(uint32_t x, uint32_t bits) {
     for (uint32_t i = 0; i < bits; ++i) r |= ((x >> i) & 1u) << (bits - 1 - i);
     return r;
 }
-static inline uint32_t pidx(sfp_limbs m, uint32_t i) { return (i < m.split ? m.base + i : m.pbase + (i - m.split)); }
+static inline uint32_t pidx(sfp_limbs m, uint32_t i) { return sfp_prime_of(m, i); }
 
 const char* sfp_backend_name(void) { return "oracle-c"; }
 
 sfp_dev* sfp_create(int device, const sfp_tables* t) {
     (void)device;
     sfp_dev* d = (sfp_dev*)calloc(1, sizeof(sfp_dev));
+    d->world = 1;
     d->logn = t->logn;
     d->n = 1u << t->logn;
     d->np = t->nprimes;
@@ -397,6 +403,16 @@ void sfp_conv_apply(sfp_dev* d, uint64_t* dst, const uint64_t* src, const sfp_co
     free(rows);
 }
 
+/* centred conversion onto the first nt_use targets (the sharded ModDown's P -> local Q) */
+void sfp_conv_apply_centered(sfp_dev* d, uint64_t* dst, const uint64_t* src, const sfp_conv* c,
+                             uint32_t nt_use) {
+    if (!c || !nt_use) return;
+    u64** rows = (u64**)malloc(nt_use * sizeof(u64*));
+    for (uint32_t t = 0; t < nt_use; ++t) rows[t] = dst + (size_t)c->drow[t] * d->n;
+    conv_rows(d, c, src, rows, nt_use, 1);
+    free(rows);
+}
+
 /* every digit j: own rows copied, the others NTT(Conv_j(INTT(in[digit j]))) */
 void sfp_modup(sfp_dev* d, uint64_t* ext, const uint64_t* in, uint32_t ell, uint32_t K,
                uint32_t Lq, uint32_t alpha, const sfp_conv* const* convs, uint64_t* scratch) {
@@ -533,4 +549,90 @@ void sfp_load_i64(sfp_dev* d, uint64_t* p, const int64_t* c, sfp_limbs m) {
         u64 r = a % q;
         p[o + x] = (v < 0 && r) ? q - r : r;
     })
+}
+
+/* ---- limb sharding ---- */
+int sfp_comm_uid(void* uid128) { (void)uid128; return -1; }
+int sfp_comm_init_rccl(sfp_dev* d, int rank, int world, const void* uid128) {
+    (void)d; (void)rank; (void)world; (void)uid128;
+    return -1; /* no RCCL in the oracle: host callbacks only */
+}
+void sfp_comm_set_host(sfp_dev* d, int rank, int world, sfp_host_allgather_fn ag, sfp_host_bcast_fn bc,
+                       void* user) {
+    d->rank = rank;
+    d->world = world;
+    d->ag = ag;
+    d->bc = bc;
+    d->user = user;
+}
+void sfp_allgather(sfp_dev* d, const void* send, void* recv, size_t bytes) {
+    if (d->world <= 1 || !d->ag) {
+        if (send != recv) memmove(recv, send, bytes);
+        return;
+    }
+    void* tmp = malloc(bytes ? bytes : 1); /* send may alias recv */
+    memcpy(tmp, send, bytes);
+    d->ag(d->user, tmp, recv, bytes);
+    free(tmp);
+}
+void sfp_bcast(sfp_dev* d, void* buf, size_t bytes, int root) {
+    if (d->world <= 1 || !d->bc) return;
+    d->bc(d->user, buf, bytes, root);
+}
+
+void sfp_gather_rows(sfp_dev* d, uint64_t* dst, const uint64_t* src, const uint32_t* rows, uint32_t count) {
+    for (uint32_t i = 0; i < count; ++i)
+        memmove(dst + (size_t)i * d->n, src + (size_t)rows[i] * d->n, (size_t)d->n * 8);
+}
+
+void sfp_rescale_rows(sfp_dev* d, uint64_t* out, const uint64_t* in, const uint64_t* last,
+                      uint32_t drop_prime, sfp_limbs m, const uint64_t* qlinv, uint32_t npoly,
+                      size_t in_stride, size_t out_stride, size_t last_stride) {
+    const uint32_t n = d->n;
+    const u64 ql = d->q[drop_prime];
+    for (uint32_t p = 0; p < npoly; ++p) {
+        const u64* lp = last + p * last_stride;
+        const u64* src = in + p * in_stride;
+        u64* dst = out + p * out_stride;
+#pragma omp parallel for schedule(static)
+        for (uint32_t i = 0; i < m.count; ++i) {
+            const uint32_t pi = pidx(m, i);
+            const u64 q = d->q[pi];
+            u64* row = (u64*)malloc((size_t)n * 8);
+            const u64 qlmod = ql % q;
+            for (uint32_t x = 0; x < n; ++x) {
+                u64 v = lp[x];
+                u64 r = v % q;
+                if (v > (ql >> 1)) r = sb(r, qlmod, q);
+                row[x] = r;
+            }
+            ntt_fwd(d, row, pi);
+            const size_t o = (size_t)i * n;
+            for (uint32_t x = 0; x < n; ++x) dst[o + x] = mm(sb(src[o + x], row[x], q), qlinv[i], q);
+            free(row);
+        }
+    }
+}
+
+void sfp_ks_inner_map(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
+                      size_t ext_stride, const uint64_t* key, uint32_t beta, sfp_limbs pm,
+                      uint32_t keyQ, uint32_t key_rows) {
+    const uint32_t n = d->n;
+#pragma omp parallel for schedule(static)
+    for (uint32_t t = 0; t < pm.count; ++t) {
+        const uint32_t kr = t < pm.split ? t : keyQ + (t - pm.split);
+        const u64 q = d->q[pidx(pm, t)];
+        for (uint32_t x = 0; x < n; ++x) {
+            u128 s0 = 0, s1 = 0;
+            for (uint32_t j = 0; j < beta; ++j) {
+                u64 e = ext[j * ext_stride + (size_t)t * n + x];
+                const u64* kb = key + (size_t)j * 2 * key_rows * n;
+                const u64* ka = kb + (size_t)key_rows * n;
+                s0 += (u128)e * kb[(size_t)kr * n + x];
+                s1 += (u128)e * ka[(size_t)kr * n + x];
+            }
+            acc0[(size_t)t * n + x] = (u64)(s0 % q);
+            acc1[(size_t)t * n + x] = (u64)(s1 % q);
+        }
+    }
 }

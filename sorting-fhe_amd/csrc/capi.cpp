@@ -274,13 +274,7 @@ int sfhe_ct_download(sfhe_ctx* c, const sfhe_ct* ct, uint64_t* out, size_t cap) 
     const size_t n = c->cc->GetRingDimension();
     const size_t L = ct->ct->GetNumLimbs();
     REQUIRE(cap >= 2 * L * n, "output buffer too small");
-    return guard([&] {
-        auto* s = c->cc->state();
-        sfp_d2h(s->dev, out, ct->ct->c0, L * n * 8);
-        sfp_d2h(s->dev, out + L * n, ct->ct->c1, L * n * 8);
-        const char* e = sfp_last_error(s->dev);
-        if (e) throw OpenFHEException(std::string("device error: ") + e);
-    });
+    return guard([&] { c->cc->DownloadRows(ct->ct, out); });
 }
 
 #define BINOP(name, expr)                                                           \
@@ -420,6 +414,7 @@ int sfhe_decompose(uint32_t N, const int32_t* keys, size_t nkeys, int32_t rotati
 int sfhe_debug_decrypt_coeffs(sfhe_ctx* c, const sfhe_ct* ct, double* out, size_t cap) {
     REQUIRE(c && ct && out, "null argument");
     REQUIRE(c->keys.secretKey, "no secret key");
+    REQUIRE(c->cc->ShardWorld() == 1, "debug decrypt needs an unsharded context");
     const size_t n = c->cc->GetRingDimension();
     REQUIRE(cap >= n, "output buffer too small");
     return guard([&] {
@@ -460,6 +455,42 @@ int sfhe_context_primes(sfhe_ctx* c, uint64_t* out, size_t cap, size_t* count) {
     if (count) *count = p.size();
     for (size_t i = 0; i < p.size() && i < cap && out; ++i) out[i] = p[i];
     return SFHE_OK;
+}
+
+// ---- limb sharding ----
+int sfhe_comm_uid(uint8_t uid[128]) {
+    REQUIRE(uid, "null argument");
+    if (sfp_comm_uid(uid) != 0) {
+        g_err = std::string("no RCCL communicator in the ") + sfp_backend_name() + " backend";
+        return SFHE_ENOTIMPL;
+    }
+    return SFHE_OK;
+}
+
+int sfhe_shard_rccl(sfhe_ctx* c, int rank, int world, const uint8_t uid[128]) {
+    REQUIRE(c && uid, "null argument");
+    REQUIRE(world >= 1 && rank >= 0 && rank < world, "bad rank / world");
+    REQUIRE(!c->keys.secretKey, "shard the context before sfhe_keygen");
+    REQUIRE(c->cc->ShardWorld() == 1, "context already sharded");
+    return guard([&] {
+        auto* s = c->cc->state();
+        if (sfp_comm_init_rccl(s->dev, rank, world, uid) != 0) {
+            const char* e = sfp_last_error(s->dev);
+            throw OpenFHEException(std::string("device error: RCCL communicator: ") + (e ? e : "init failed"));
+        }
+        c->cc->EnableSharding(rank, world);
+    });
+}
+
+int sfhe_shard_host(sfhe_ctx* c, int rank, int world, sfhe_allgather_fn ag, sfhe_bcast_fn bc, void* user) {
+    REQUIRE(c && ag && bc, "null argument");
+    REQUIRE(world >= 1 && rank >= 0 && rank < world, "bad rank / world");
+    REQUIRE(!c->keys.secretKey, "shard the context before sfhe_keygen");
+    REQUIRE(c->cc->ShardWorld() == 1, "context already sharded");
+    return guard([&] {
+        c->cc->EnableSharding(rank, world);
+        sfp_comm_set_host(c->cc->state()->dev, rank, world, ag, bc, user);
+    });
 }
 
 }  // extern "C"

@@ -157,6 +157,7 @@ DeviceBuffer::~DeviceBuffer() {
 }
 
 DeviceBufferPtr SfheContextState::alloc(size_t words) {
+    if (!words) words = 1;  // a sharded rank may own no row of a low level
     uint64_t* p = nullptr;
     {
         std::lock_guard<std::mutex> g(poolMu);
@@ -236,7 +237,7 @@ class SfheInternal {
         if (!on) return ct;
         static uint64_t counter = 0;
         SfheContextState* s = cc->st.get();
-        const size_t words = (size_t)s->ellOf(ct->level) * s->n;
+        const size_t words = s->polyWords(ct->level);
         std::vector<u64> h(words * 2);
         sfp_d2h(s->dev, h.data(), ct->c0, words * 8);
         sfp_d2h(s->dev, h.data() + words, ct->c1, words * 8);
@@ -263,20 +264,21 @@ class SfheInternal {
     static Ct newCt(CC* cc, uint32_t level, uint32_t slots) {
         SfheContextState* s = cc->st.get();
         auto ct = std::make_shared<CiphertextImpl<DCRTPoly>>();
-        uint32_t ell = s->ellOf(level);
+        const size_t pw = s->polyWords(level);
         ct->cc = cc->shared_from_this();
-        ct->buf = s->alloc((size_t)2 * ell * s->n);
+        ct->buf = s->alloc(2 * pw);
         ct->c0 = ct->buf->ptr;
-        ct->c1 = ct->c0 + (size_t)ell * s->n;
+        ct->c1 = ct->c0 + pw;
         ct->level = level;
         ct->slots = slots;
         ct->scale = s->scale[level];
         return ct;
     }
 
+    // residues of round(v) modulo the primes of the local rows of ell limbs
     static std::vector<u64> constResidues(SfheContextState* s, double v, uint32_t ell) {
-        std::vector<u64> k(ell);
-        for (uint32_t i = 0; i < ell; ++i) k[i] = residueOf(v, s->primes[i]);
+        std::vector<u64> k(s->rows(ell));
+        for (uint32_t i = 0; i < k.size(); ++i) k[i] = residueOf(v, s->primes[s->qprime(i)]);
         return k;
     }
 
@@ -288,8 +290,11 @@ class SfheInternal {
         if (ell < 2) SFHE_THROW("no levels left to rescale (multiplicative depth exhausted)");
         Ct out = newCt(cc, level + 1, slots);
         if (c1 - c0 < 0) SFHE_THROW("internal: layout");
-        sfp_rescale(s->dev, out->c0, c0, ell, s->qInvTable[ell].data(), 2, (size_t)(c1 - c0),
-                    (size_t)(out->c1 - out->c0));
+        if (s->world > 1)
+            rescaleShard(s, out->c0, c0, ell, 2, (size_t)(c1 - c0), (size_t)(out->c1 - out->c0));
+        else
+            sfp_rescale(s->dev, out->c0, c0, ell, s->qInvTable[ell].data(), 2, (size_t)(c1 - c0),
+                        (size_t)(out->c1 - out->c0));
         s->stats.rescale++;
         s->countBytes(4.0 * ell * s->n * 8 * 2 / 2);  // 4 l B per poly pair
         return out;
@@ -328,16 +333,17 @@ class SfheInternal {
         SfheContextState* s = cc->st.get();
         const uint32_t ell = s->ellOf(level);
         if (ell < 2) SFHE_THROW("no levels left to rescale (multiplicative depth exhausted)");
-        if (!fusedRescale()) {
-            auto tmp = s->alloc((size_t)2 * ell * s->n);
+        if (!fusedRescale() || s->world > 1) {
+            const size_t pw = s->polyWords(level);
+            auto tmp = s->alloc(2 * pw);
             uint64_t* t0 = tmp->ptr;
-            uint64_t* t1 = t0 + (size_t)ell * s->n;
+            uint64_t* t1 = t0 + pw;
             if (k) {
-                sfp_mul_const(s->dev, t0, ct->c0, k, Q(ell));
-                sfp_mul_const(s->dev, t1, ct->c1, k, Q(ell));
+                sfp_mul_const(s->dev, t0, ct->c0, k, s->qmap(ell));
+                sfp_mul_const(s->dev, t1, ct->c1, k, s->qmap(ell));
             } else {
-                sfp_mul(s->dev, t0, ct->c0, m, Q(ell));
-                sfp_mul(s->dev, t1, ct->c1, m, Q(ell));
+                sfp_mul(s->dev, t0, ct->c0, m, s->qmap(ell));
+                sfp_mul(s->dev, t1, ct->c1, m, s->qmap(ell));
             }
             return rescale(cc, t0, t1, level, slots);
         }
@@ -360,11 +366,201 @@ class SfheInternal {
         b = adjust(cc, b, l);
     }
 
+    // ---- limb sharding: this rank computes its own rows; the
+    // exchange steps are the ModUp input (all Q rows, coefficient form), the
+    // ModDown P rows and the dropped row of a rescale.  Row order of a
+    // gathered buffer: rank-major blocks of `per` rows (rank r's local row i
+    // at r * per + i), i.e. global row g at (g % W) * per + g / W.
+    static std::vector<uint32_t> naturalOrder(const SfheContextState* s, uint32_t count, uint32_t per,
+                                              uint32_t blocks = 1, uint32_t block = 0) {
+        std::vector<uint32_t> r(count);
+        for (uint32_t g = 0; g < count; ++g)
+            r[g] = ((g % s->world) * blocks + block) * per + g / s->world;
+        return r;
+    }
+
+    // coefficient-form rows of every limb of `local` (rows(ell) local rows,
+    // evaluation domain) in natural order into `nat` (ell rows)
+    static void gatherCoeff(SfheContextState* s, uint64_t* nat, const uint64_t* local, uint32_t ell) {
+        const uint32_t n = s->n, per = (ell + s->world - 1) / s->world, lr = s->rows(ell);
+        auto send = s->alloc((size_t)per * n);
+        auto all = s->alloc((size_t)per * s->world * n);
+        if (lr) {
+            sfp_d2d(s->dev, send->ptr, local, (size_t)lr * n * 8);
+            sfp_ntt(s->dev, send->ptr, s->qmap(ell), 1);
+        }
+        sfp_allgather(s->dev, send->ptr, all->ptr, (size_t)per * n * 8);
+        auto idx = naturalOrder(s, ell, per);
+        sfp_gather_rows(s->dev, nat, all->ptr, idx.data(), ell);
+    }
+
+    // conversion tables with this rank's targets: ModUp digit j of ell limbs
+    // -> every local ext row (own-digit rows included: the conversion of a
+    // row to its own prime returns it exactly)
+    static std::vector<sfp_conv*>& modupConvShard(SfheContextState* s, uint32_t ell) {
+        auto it = s->modupConvShard.find(ell);
+        if (it != s->modupConvShard.end()) return it->second;
+        std::vector<sfp_conv*> v;
+        const uint32_t beta = (ell + s->alpha - 1) / s->alpha;
+        std::vector<uint32_t> dst;
+        for (uint32_t i = 0; i < s->rows(ell); ++i) dst.push_back(s->qprime(i));
+        for (uint32_t k = 0; k < s->prows(); ++k) dst.push_back(s->Lq + s->rank + k * s->world);
+        for (uint32_t j = 0; j < beta; ++j) {
+            std::vector<uint32_t> src;
+            for (uint32_t i = j * s->alpha; i < std::min((j + 1) * s->alpha, ell); ++i) src.push_back(i);
+            v.push_back(makeConv(s, src, dst));
+        }
+        return s->modupConvShard[ell] = v;
+    }
+
+    // ModUp of the local rows of d (ell limbs): beta blocks of extmap(ell) rows
+    static void modupShard(SfheContextState* s, uint64_t* ext, const uint64_t* d, uint32_t ell) {
+        const uint32_t n = s->n, beta = (ell + s->alpha - 1) / s->alpha;
+        const sfp_limbs em = s->extmap(ell);
+        const size_t stride = (size_t)em.count * n;
+        auto nat = s->alloc((size_t)ell * n);
+        gatherCoeff(s, nat->ptr, d, ell);
+        auto& convs = modupConvShard(s, ell);
+        for (uint32_t j = 0; j < beta; ++j) {
+            sfp_conv_apply(s->dev, ext + j * stride, nat->ptr + (size_t)j * s->alpha * n, convs[j]);
+            sfp_ntt(s->dev, ext + j * stride, em, 0);
+        }
+    }
+
+    // inner product with the local key rows + ModDown to the local Q rows
+    static void innerModDownShard(SfheContextState* s, const uint64_t* ext, size_t stride, uint32_t beta,
+                                  uint32_t ell, const DeviceBufferPtr& key, uint64_t* out0, uint64_t* out1,
+                                  int add0, int add1) {
+        const uint32_t n = s->n, K = s->K, lr = s->rows(ell), lp = s->prows();
+        const sfp_limbs em = s->extmap(ell);
+        const size_t aw = (size_t)em.count * n;
+        auto acc = s->alloc(2 * aw);
+        sfp_ks_inner_map(s->dev, acc->ptr, acc->ptr + aw, ext, stride, key->ptr, beta, em, s->rows(s->Lq),
+                         s->rows(s->Lq) + lp);
+        // P rows: coefficient form, exchanged (both polys in one all-gather)
+        const uint32_t per = (K + s->world - 1) / s->world;
+        auto send = s->alloc((size_t)2 * per * n);
+        const sfp_limbs pm{lp, 0, s->Lq + (uint32_t)s->rank, 0, (uint32_t)s->world};
+        for (int p = 0; p < 2; ++p) {
+            if (!lp) break;
+            uint64_t* dst = send->ptr + (size_t)p * per * n;
+            sfp_d2d(s->dev, dst, acc->ptr + p * aw + (size_t)lr * n, (size_t)lp * n * 8);
+            sfp_ntt(s->dev, dst, pm, 1);
+        }
+        auto all = s->alloc((size_t)2 * per * s->world * n);
+        sfp_allgather(s->dev, send->ptr, all->ptr, (size_t)2 * per * n * 8);
+        auto natP = s->alloc((size_t)2 * K * n);
+        for (uint32_t p = 0; p < 2; ++p) {
+            auto idx = naturalOrder(s, K, per, 2, p);
+            sfp_gather_rows(s->dev, natP->ptr + (size_t)p * K * n, all->ptr, idx.data(), K);
+        }
+        if (!lr) return;
+        // (acc_Q - NTT(Conv_centred(P rows))) * P^-1  (+ out)
+        std::vector<u64> pinv(lr);
+        for (uint32_t i = 0; i < lr; ++i) pinv[i] = s->pInvModQ[s->qprime(i)];
+        auto conv = s->alloc((size_t)lr * n);
+        uint64_t* outs[2] = {out0, out1};
+        const int adds[2] = {add0, add1};
+        for (int p = 0; p < 2; ++p) {
+            sfp_conv_apply_centered(s->dev, conv->ptr, natP->ptr + (size_t)p * K * n, s->moddownConvShard, lr);
+            sfp_ntt(s->dev, conv->ptr, s->qmap(ell), 0);
+            sfp_sub(s->dev, conv->ptr, acc->ptr + p * aw, conv->ptr, s->qmap(ell));
+            sfp_mul_const(s->dev, conv->ptr, conv->ptr, pinv.data(), s->qmap(ell));
+            if (adds[p])
+                sfp_add(s->dev, outs[p], outs[p], conv->ptr, s->qmap(ell));
+            else
+                sfp_d2d(s->dev, outs[p], conv->ptr, (size_t)lr * n * 8);
+        }
+    }
+
+    static void keySwitchShard(CC* cc, const uint64_t* d, uint32_t ell, const DeviceBufferPtr& key,
+                               uint64_t* out0, uint64_t* out1, int add0, int add1) {
+        SfheContextState* s = cc->st.get();
+        const uint32_t beta = (ell + s->alpha - 1) / s->alpha;
+        const size_t stride = (size_t)s->extmap(ell).count * s->n;
+        auto ext = s->alloc(stride * beta);
+        modupShard(s, ext->ptr, d, ell);
+        innerModDownShard(s, ext->ptr, stride, beta, ell, key, out0, out1, add0, add1);
+        s->stats.keyswitch++;
+        s->countBytes((3.0 * ell + 2.0 * beta * (ell + s->K)) * s->n * 8);
+    }
+
+    // rescale of npoly polys (local rows of ell limbs) by q_{ell-1}: its owner
+    // broadcasts the dropped row in coefficient form
+    static void rescaleShard(SfheContextState* s, uint64_t* out, const uint64_t* in, uint32_t ell, uint32_t npoly,
+                             size_t inStride, size_t outStride) {
+        const uint32_t n = s->n, drop = ell - 1, owner = drop % s->world;
+        auto last = s->alloc((size_t)npoly * n);
+        if ((uint32_t)s->rank == owner) {
+            const uint32_t lr = s->rows(ell);
+            for (uint32_t p = 0; p < npoly; ++p)
+                sfp_d2d(s->dev, last->ptr + (size_t)p * n, in + p * inStride + (size_t)(lr - 1) * n, (size_t)n * 8);
+            for (uint32_t p = 0; p < npoly; ++p)
+                sfp_ntt(s->dev, last->ptr + (size_t)p * n, sfp_limbs{1, 1, 0, drop, 1}, 1);
+        }
+        sfp_bcast(s->dev, last->ptr, (size_t)npoly * n * 8, (int)owner);
+        const uint32_t lo = s->rows(ell - 1);
+        std::vector<u64> qlinv(lo);
+        for (uint32_t i = 0; i < lo; ++i) qlinv[i] = s->qInvTable[ell][s->qprime(i)];
+        sfp_rescale_rows(s->dev, out, in, last->ptr, drop, s->qmap(ell - 1), qlinv.data(), npoly, inStride,
+                         outStride, n);
+    }
+
+    // this rank's rows of a ciphertext computed on every row (FullScope)
+    static Ct localize(CC* cc, const Ct& full) {
+        SfheContextState* s = cc->st.get();
+        if (s->world == 1) return full;
+        const uint32_t ell = s->ellOf(full->level), lr = s->rows(ell);
+        Ct out = newCt(cc, full->level, full->slots);
+        out->scale = full->scale;
+        std::vector<uint32_t> idx(lr);
+        for (uint32_t i = 0; i < lr; ++i) idx[i] = s->qprime(i);
+        sfp_gather_rows(s->dev, out->c0, full->c0, idx.data(), lr);
+        sfp_gather_rows(s->dev, out->c1, full->c1, idx.data(), lr);
+        return out;
+    }
+
+    // every row of a sharded ciphertext, in natural order (2 * ell rows:
+    // c0 then c1), on every rank
+    static DeviceBufferPtr gatherFull(SfheContextState* s, const Ct& a) {
+        const uint32_t n = s->n, ell = s->ellOf(a->level), lr = s->rows(ell);
+        const uint32_t per = (ell + s->world - 1) / s->world;
+        auto send = s->alloc((size_t)2 * per * n);
+        if (lr) {
+            sfp_d2d(s->dev, send->ptr, a->c0, (size_t)lr * n * 8);
+            sfp_d2d(s->dev, send->ptr + (size_t)per * n, a->c1, (size_t)lr * n * 8);
+        }
+        auto all = s->alloc((size_t)2 * per * s->world * n);
+        sfp_allgather(s->dev, send->ptr, all->ptr, (size_t)2 * per * n * 8);
+        auto full = s->alloc((size_t)2 * ell * n);
+        for (uint32_t p = 0; p < 2; ++p) {
+            auto idx = naturalOrder(s, ell, per, 2, p);
+            sfp_gather_rows(s->dev, full->ptr + (size_t)p * ell * n, all->ptr, idx.data(), ell);
+        }
+        return full;
+    }
+
+    // this rank's rows of a switching key built on every row: per digit,
+    // [b rows][a rows] of (local Q rows, local P rows)
+    static DeviceBufferPtr localizeKey(SfheContextState* s, const DeviceBufferPtr& full) {
+        if (s->world == 1) return full;
+        const uint32_t n = s->n, NP = s->Lq + s->K, lq = s->rows(s->Lq), lp = s->prows();
+        std::vector<uint32_t> idx;
+        for (uint32_t i = 0; i < lq; ++i) idx.push_back(s->qprime(i));
+        for (uint32_t k = 0; k < lp; ++k) idx.push_back(s->Lq + s->rank + k * s->world);
+        const uint32_t R = lq + lp;
+        auto key = s->alloc((size_t)s->dnum * 2 * R * n);
+        for (uint32_t h = 0; h < 2 * s->dnum; ++h)
+            sfp_gather_rows(s->dev, key->ptr + (size_t)h * R * n, full->ptr + (size_t)h * NP * n, idx.data(), R);
+        return key;
+    }
+
     // Hybrid key switch of d (ell limbs, evaluation domain) with `key`; the
     // result goes to (out0, out1) (ell limbs each), added when add0 / add1.
     static void keySwitch(CC* cc, const uint64_t* d, uint32_t ell, const DeviceBufferPtr& key,
                           uint64_t* out0, uint64_t* out1, int add0, int add1) {
         SfheContextState* s = cc->st.get();
+        if (s->world > 1) return keySwitchShard(cc, d, ell, key, out0, out1, add0, add1);
         const uint32_t n = s->n, K = s->K;
         const uint32_t beta = (ell + s->alpha - 1) / s->alpha;
         const size_t stride = (size_t)(ell + K) * n;
@@ -386,6 +582,10 @@ class SfheInternal {
         SfheContextState* s = cc->st.get();
         const uint32_t ell = s->ellOf(level);
         if (ell < 2) SFHE_THROW("no levels left to rescale (multiplicative depth exhausted)");
+        if (s->world > 1) {
+            keySwitchShard(cc, d2, ell, s->relinKey, d0, d1, 1, 1);
+            return rescale(cc, d0, d1, level, slots);
+        }
         const uint32_t n = s->n, K = s->K;
         const uint32_t beta = (ell + s->alpha - 1) / s->alpha;
         const size_t stride = (size_t)(ell + K) * n;
@@ -414,6 +614,7 @@ class SfheInternal {
                                 uint32_t ell, const DeviceBufferPtr& key, uint64_t* out0,
                                 uint64_t* out1, int add0, int add1) {
         SfheContextState* s = cc->st.get();
+        if (s->world > 1) return innerModDownShard(s, ext, stride, beta, ell, key, out0, out1, add0, add1);
         const uint32_t n = s->n, K = s->K;
         const size_t accStride = (size_t)(ell + K) * n;
         auto acc = s->alloc(2 * accStride);
@@ -469,6 +670,14 @@ class SfheInternal {
     // switching key from s' (device, Lq+K limbs, eval domain) to s
     static DeviceBufferPtr genSwitchKey(CC* cc, const uint64_t* sPrime, const uint64_t* sk) {
         SfheContextState* s = cc->st.get();
+        if (s->world > 1) {
+            DeviceBufferPtr full;
+            {
+                FullScope fs(s);
+                full = genSwitchKey(cc, sPrime, sk);
+            }
+            return localizeKey(s, full);
+        }
         const uint32_t n = s->n, NP = s->Lq + s->K;
         const sfp_limbs all{NP, NP, 0};
         auto key = s->alloc((size_t)s->dnum * 2 * NP * n);
@@ -529,9 +738,19 @@ class SfheInternal {
     static const uint64_t* encoded(CC* cc, const Plaintext& pt, uint32_t level) {
         SfheContextState* s = cc->st.get();
         std::lock_guard<std::mutex> g(pt->encMutex);
+        uint32_t ell = s->ellOf(level);
+        if (s->fullScope && s->rows(ell) != ell) SFHE_THROW("internal: encoding scope");
+        if (s->fullScope) {  // every row, uncached (a sharded context caches local rows)
+            std::vector<int64_t> coeffs;
+            ckks_encode(pt->values, pt->slots, s->n, s->scale[level], coeffs);
+            auto buf = s->alloc(s->polyWords(level));
+            sfp_load_i64(s->dev, buf->ptr, coeffs.data(), s->qmap(ell));
+            sfp_ntt(s->dev, buf->ptr, s->qmap(ell), 0);
+            s->scopeKeep.push_back(buf);
+            return buf->ptr;
+        }
         auto it = pt->encoded.find(level);
         if (it != pt->encoded.end()) return ready(s, it->second.get());
-        uint32_t ell = s->ellOf(level);
         // context-level cache: identical (values, slots, level) encode identically
         uint64_t h = 1469598103934665603ull;
         if (s->ptCacheOn) {
@@ -557,24 +776,25 @@ class SfheInternal {
         }
         std::vector<int64_t> coeffs;
         ckks_encode(pt->values, pt->slots, s->n, s->scale[level], coeffs);
-        auto buf = s->alloc((size_t)ell * s->n);
-        sfp_load_i64(s->dev, buf->ptr, coeffs.data(), Q(ell));
+        const size_t pw = s->polyWords(level);
+        auto buf = s->alloc(pw);
+        sfp_load_i64(s->dev, buf->ptr, coeffs.data(), s->qmap(ell));
         if (std::getenv("SFHE_TRACE")) {
             uint64_t f = 1469598103934665603ull;
             for (int64_t v : coeffs) f = (f ^ (uint64_t)v) * 1099511628211ull;
-            std::vector<u64> h((size_t)ell * s->n);
+            std::vector<u64> h(pw);
             sfp_d2h(s->dev, h.data(), buf->ptr, h.size() * 8);
             uint64_t g = 1469598103934665603ull;
             for (u64 v : h) g = (g ^ v) * 1099511628211ull;
             std::fprintf(stderr, "ENCODE slots=%u level=%u coeffs=%016llx loaded=%016llx\n", pt->slots,
                          level, (unsigned long long)f, (unsigned long long)g);
         }
-        sfp_ntt(s->dev, buf->ptr, Q(ell), 0);
+        sfp_ntt(s->dev, buf->ptr, s->qmap(ell), 0);
         buf->ready = sfp_event_record(s->dev);
         pt->encoded[level] = buf;
-        if (s->ptCacheOn && s->ptCacheBytes + (size_t)ell * s->n * 8 <= s->ptCacheLimit) {
+        if (s->ptCacheOn && s->ptCacheBytes + pw * 8 <= s->ptCacheLimit) {
             s->ptCache[h].push_back(PtCacheEntry{pt->values, pt->slots, buf});
-            s->ptCacheBytes += (size_t)ell * s->n * 8;
+            s->ptCacheBytes += pw * 8;
         }
         return buf->ptr;
     }
@@ -582,7 +802,7 @@ class SfheInternal {
     static Ct copyOf(CC* cc, const Ct& a) {
         SfheContextState* s = cc->st.get();
         Ct out = newCt(cc, a->level, a->slots);
-        size_t bytes = (size_t)s->ellOf(a->level) * s->n * 8;
+        size_t bytes = s->polyWords(a->level) * 8;
         sfp_d2d(s->dev, out->c0, a->c0, bytes);
         sfp_d2d(s->dev, out->c1, a->c1, bytes);
         return out;
@@ -782,6 +1002,9 @@ CryptoContextImpl<DCRTPoly>::~CryptoContextImpl() {
     for (auto& kv : st->modupConv)
         for (auto* c : kv.second) sfp_free_conv(st->dev, c);
     if (st->moddownConv) sfp_free_conv(st->dev, st->moddownConv);
+    for (auto& kv : st->modupConvShard)
+        for (auto* c : kv.second) sfp_free_conv(st->dev, c);
+    if (st->moddownConvShard) sfp_free_conv(st->dev, st->moddownConvShard);
     st->releaseAll();
     sfp_destroy(st->dev);
 }
@@ -808,7 +1031,8 @@ void CryptoContextImpl<DCRTPoly>::Synchronize() {
     if (e) SFHE_THROW(std::string("device error: ") + e);
 }
 
-int CryptoContextImpl<DCRTPoly>::LaneCount() const { return sfp_lanes(st->dev); }
+// a sharded context issues its collectives in program order on one lane
+int CryptoContextImpl<DCRTPoly>::LaneCount() const { return st->world > 1 ? 1 : sfp_lanes(st->dev); }
 
 void CryptoContextImpl<DCRTPoly>::ForkLanes(int count) {
     OpLock g(st.get());
@@ -907,6 +1131,7 @@ void CryptoContextImpl<DCRTPoly>::ResetOpStats() { st->stats = OpStats(); }
 KeyPair<DCRTPoly> CryptoContextImpl<DCRTPoly>::KeyGen() {
     OpLock g(st.get());
     SfheContextState* s = st.get();
+    FullScope fs(s);  // secret and public keys keep every row (sharding: setup only)
     const uint32_t NP = s->Lq + s->K;
     KeyPair<DCRTPoly> kp;
     auto sk = std::make_shared<PrivateKeyImpl<DCRTPoly>>();
@@ -1010,8 +1235,16 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::Encrypt(const PublicKey<DCRTPo
     OpLock g(st.get());
     SfheContextState* s = st.get();
     if (!pk) SFHE_THROW("null public key");
+    if (s->world > 1) {  // encrypt every row, keep this rank's
+        Ciphertext<DCRTPoly> full;
+        {
+            FullScope fs(s);
+            full = Encrypt(pk, pt);
+        }
+        return SfheInternal::localize(this, full);
+    }
     const uint32_t level = pt->level, ell = s->ellOf(level);
-    const sfp_limbs q = SfheInternal::Q(ell);
+    const sfp_limbs q = st->qmap(ell);
     const uint64_t* m = SfheInternal::encoded(this, pt, level);
     auto ct = SfheInternal::newCt(this, level, pt->slots);
     // FLEXIBLEAUTOEXT: one extra row modulo q_ext (prime index extIdx)
@@ -1062,6 +1295,15 @@ void CryptoContextImpl<DCRTPoly>::Decrypt(const PrivateKey<DCRTPoly>& sk,
     SfheInternal::deps(st.get(), {&ct});
     SfheContextState* s = st.get();
     if (!sk) SFHE_THROW("null secret key");
+    if (s->world > 1) {  // every rank gathers the rows and decrypts
+        auto full = SfheInternal::gatherFull(s, ct);
+        FullScope fs(s);
+        auto fc = std::make_shared<CiphertextImpl<DCRTPoly>>(*ct);
+        fc->buf = full;
+        fc->c0 = full->ptr;
+        fc->c1 = fc->c0 + (size_t)s->ellOf(ct->level) * s->n;
+        return Decrypt(sk, fc, out);
+    }
     const uint32_t ell = s->ellOf(ct->level);
     const uint32_t nl = std::min<uint32_t>(2, ell);
     const sfp_limbs q = SfheInternal::Q(nl);
@@ -1137,8 +1379,8 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalAdd(const Ciphertext<DCRTP
     SfheInternal::align(this, a, b);
     auto out = SfheInternal::newCt(this, a->level, std::max(a->slots, b->slots));
     const uint32_t ell = st->ellOf(a->level);
-    sfp_add(st->dev, out->c0, a->c0, b->c0, SfheInternal::Q(ell));
-    sfp_add(st->dev, out->c1, a->c1, b->c1, SfheInternal::Q(ell));
+    sfp_add(st->dev, out->c0, a->c0, b->c0, st->qmap(ell));
+    sfp_add(st->dev, out->c1, a->c1, b->c1, st->qmap(ell));
     st->stats.add++;
     st->countBytes(6.0 * ell * st->n * 8);
     return SfheInternal::traced(this, out, "EvalAdd");
@@ -1152,13 +1394,13 @@ void CryptoContextImpl<DCRTPoly>::EvalAddInPlace(Ciphertext<DCRTPoly>& a,
     // in place only on an exclusively owned buffer outside dataflow regions
     // (there another lane may still be reading the old value)
     if (a->level != b->level || a->buf.use_count() > 1 || st->dataflow ||
-        a->c1 - a->c0 != (ptrdiff_t)(st->ellOf(a->level) * st->n)) {
+        a->c1 - a->c0 != (ptrdiff_t)st->polyWords(a->level)) {
         a = EvalAdd(a, b);
         return;
     }
     const uint32_t ell = st->ellOf(a->level);
-    sfp_add(st->dev, a->c0, a->c0, b->c0, SfheInternal::Q(ell));
-    sfp_add(st->dev, a->c1, a->c1, b->c1, SfheInternal::Q(ell));
+    sfp_add(st->dev, a->c0, a->c0, b->c0, st->qmap(ell));
+    sfp_add(st->dev, a->c1, a->c1, b->c1, st->qmap(ell));
     st->wrote(a->buf.get());
     a->slots = std::max(a->slots, b->slots);
     st->stats.add++;
@@ -1172,8 +1414,8 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalAdd(const Ciphertext<DCRTP
     const uint32_t ell = st->ellOf(a->level);
     auto out = SfheInternal::newCt(this, a->level, a->slots);
     auto k = SfheInternal::constResidues(st.get(), c * a->scale, ell);
-    sfp_add_const(st->dev, out->c0, a->c0, k.data(), SfheInternal::Q(ell));
-    sfp_d2d(st->dev, out->c1, a->c1, (size_t)ell * st->n * 8);
+    sfp_add_const(st->dev, out->c0, a->c0, k.data(), st->qmap(ell));
+    sfp_d2d(st->dev, out->c1, a->c1, st->polyWords(a->level) * 8);
     st->stats.add++;
     st->countBytes(4.0 * ell * st->n * 8);
     return SfheInternal::traced(this, out, "EvalAdd");
@@ -1190,8 +1432,8 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalAdd(const Ciphertext<DCRTP
     const uint32_t ell = st->ellOf(a->level);
     const uint64_t* m = SfheInternal::encoded(this, p, a->level);
     auto out = SfheInternal::newCt(this, a->level, std::max(a->slots, p->slots));
-    sfp_add(st->dev, out->c0, a->c0, m, SfheInternal::Q(ell));
-    sfp_d2d(st->dev, out->c1, a->c1, (size_t)ell * st->n * 8);
+    sfp_add(st->dev, out->c0, a->c0, m, st->qmap(ell));
+    sfp_d2d(st->dev, out->c1, a->c1, st->polyWords(a->level) * 8);
     st->stats.add++;
     st->countBytes(5.0 * ell * st->n * 8);
     return SfheInternal::traced(this, out, "EvalAdd");
@@ -1209,8 +1451,8 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalSub(const Ciphertext<DCRTP
     SfheInternal::align(this, a, b);
     auto out = SfheInternal::newCt(this, a->level, std::max(a->slots, b->slots));
     const uint32_t ell = st->ellOf(a->level);
-    sfp_sub(st->dev, out->c0, a->c0, b->c0, SfheInternal::Q(ell));
-    sfp_sub(st->dev, out->c1, a->c1, b->c1, SfheInternal::Q(ell));
+    sfp_sub(st->dev, out->c0, a->c0, b->c0, st->qmap(ell));
+    sfp_sub(st->dev, out->c1, a->c1, b->c1, st->qmap(ell));
     st->stats.add++;
     st->countBytes(6.0 * ell * st->n * 8);
     return SfheInternal::traced(this, out, "EvalSub");
@@ -1226,8 +1468,8 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalNegate(const Ciphertext<DC
     SfheInternal::deps(st.get(), {&a});
     const uint32_t ell = st->ellOf(a->level);
     auto out = SfheInternal::newCt(this, a->level, a->slots);
-    sfp_neg(st->dev, out->c0, a->c0, SfheInternal::Q(ell));
-    sfp_neg(st->dev, out->c1, a->c1, SfheInternal::Q(ell));
+    sfp_neg(st->dev, out->c0, a->c0, st->qmap(ell));
+    sfp_neg(st->dev, out->c1, a->c1, st->qmap(ell));
     st->countBytes(4.0 * ell * st->n * 8);
     return SfheInternal::traced(this, out, "EvalNegate");
 }
@@ -1245,8 +1487,8 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalSub(const Ciphertext<DCRTP
     const uint32_t ell = st->ellOf(a->level);
     const uint64_t* m = SfheInternal::encoded(this, p, a->level);
     auto out = SfheInternal::newCt(this, a->level, std::max(a->slots, p->slots));
-    sfp_sub(st->dev, out->c0, a->c0, m, SfheInternal::Q(ell));
-    sfp_d2d(st->dev, out->c1, a->c1, (size_t)ell * st->n * 8);
+    sfp_sub(st->dev, out->c0, a->c0, m, st->qmap(ell));
+    sfp_d2d(st->dev, out->c1, a->c1, st->polyWords(a->level) * 8);
     st->stats.add++;
     st->countBytes(5.0 * ell * st->n * 8);
     return SfheInternal::traced(this, out, "EvalSub");
@@ -1259,8 +1501,8 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalSub(const Plaintext& p,
     const uint32_t ell = st->ellOf(a->level);
     const uint64_t* m = SfheInternal::encoded(this, p, a->level);
     auto out = SfheInternal::newCt(this, a->level, std::max(a->slots, p->slots));
-    sfp_sub(st->dev, out->c0, m, a->c0, SfheInternal::Q(ell));
-    sfp_neg(st->dev, out->c1, a->c1, SfheInternal::Q(ell));
+    sfp_sub(st->dev, out->c0, m, a->c0, st->qmap(ell));
+    sfp_neg(st->dev, out->c1, a->c1, st->qmap(ell));
     st->stats.add++;
     st->countBytes(5.0 * ell * st->n * 8);
     return SfheInternal::traced(this, out, "EvalSub");
@@ -1331,11 +1573,12 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMult(const Ciphertext<DCRT
     SfheInternal::align(this, a, b);
     const uint32_t ell = s->ellOf(a->level);
     if (ell < 2) SFHE_THROW("no levels left (multiplicative depth exhausted)");
-    auto t = s->alloc((size_t)3 * ell * s->n);
+    const size_t pw = s->polyWords(a->level);
+    auto t = s->alloc(3 * pw);
     uint64_t* d0 = t->ptr;
-    uint64_t* d1 = d0 + (size_t)ell * s->n;
-    uint64_t* d2 = d1 + (size_t)ell * s->n;
-    sfp_tensor(s->dev, d0, d1, d2, a->c0, a->c1, b->c0, b->c1, SfheInternal::Q(ell));
+    uint64_t* d1 = d0 + pw;
+    uint64_t* d2 = d1 + pw;
+    sfp_tensor(s->dev, d0, d1, d2, a->c0, a->c1, b->c0, b->c1, st->qmap(ell));
     s->stats.tensor++;
     s->countBytes(7.0 * ell * s->n * 8);
     const uint32_t slots = std::max(a->slots, b->slots);
@@ -1371,21 +1614,22 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMultAddPlain(
         x1.push_back(al[i]->c1);
         m.push_back(SfheInternal::encoded(this, p[i], level));
     }
-    auto tmp = s->alloc((size_t)2 * ell * s->n);
+    const size_t pw = s->polyWords(level);
+    auto tmp = s->alloc(2 * pw);
     uint64_t* t0 = tmp->ptr;
-    uint64_t* t1 = t0 + (size_t)ell * s->n;
+    uint64_t* t1 = t0 + pw;
     for (size_t done = 0; done < a.size(); done += SFP_MAX_WSUM) {
         uint32_t take = (uint32_t)std::min<size_t>(SFP_MAX_WSUM, a.size() - done);
         if (done == 0) {
-            sfp_mac_plain(s->dev, t0, x0.data(), m.data(), take, SfheInternal::Q(ell));
-            sfp_mac_plain(s->dev, t1, x1.data(), m.data(), take, SfheInternal::Q(ell));
+            sfp_mac_plain(s->dev, t0, x0.data(), m.data(), take, st->qmap(ell));
+            sfp_mac_plain(s->dev, t1, x1.data(), m.data(), take, st->qmap(ell));
         } else {
-            auto part = s->alloc((size_t)2 * ell * s->n);
-            sfp_mac_plain(s->dev, part->ptr, x0.data() + done, m.data() + done, take, SfheInternal::Q(ell));
-            sfp_mac_plain(s->dev, part->ptr + (size_t)ell * s->n, x1.data() + done, m.data() + done, take,
-                          SfheInternal::Q(ell));
-            sfp_add(s->dev, t0, t0, part->ptr, SfheInternal::Q(ell));
-            sfp_add(s->dev, t1, t1, part->ptr + (size_t)ell * s->n, SfheInternal::Q(ell));
+            auto part = s->alloc(2 * pw);
+            sfp_mac_plain(s->dev, part->ptr, x0.data() + done, m.data() + done, take, st->qmap(ell));
+            sfp_mac_plain(s->dev, part->ptr + pw, x1.data() + done, m.data() + done, take,
+                          st->qmap(ell));
+            sfp_add(s->dev, t0, t0, part->ptr, st->qmap(ell));
+            sfp_add(s->dev, t1, t1, part->ptr + pw, st->qmap(ell));
         }
     }
     s->stats.ptmult += a.size();
@@ -1409,9 +1653,9 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotate(const Ciphertext<DC
                    std::to_string(r) + ") is not found");
     const uint32_t ell = s->ellOf(a->level);
     auto out = SfheInternal::newCt(this, a->level, a->slots);
-    auto t = s->alloc((size_t)ell * s->n);
-    sfp_automorph(s->dev, out->c0, a->c0, gal, SfheInternal::Q(ell));
-    sfp_automorph(s->dev, t->ptr, a->c1, gal, SfheInternal::Q(ell));
+    auto t = s->alloc(s->polyWords(a->level));
+    sfp_automorph(s->dev, out->c0, a->c0, gal, st->qmap(ell));
+    sfp_automorph(s->dev, t->ptr, a->c1, gal, st->qmap(ell));
     s->stats.automorph++;
     s->countBytes(3.0 * ell * s->n * 8);
     // c0' = sigma(c0) + ks0, c1' = ks1
@@ -1428,6 +1672,12 @@ std::shared_ptr<FastRotationPrecomp> CryptoContextImpl<DCRTPoly>::EvalFastRotati
     const uint32_t ell = s->ellOf(a->level);
     pre->level = a->level;
     pre->beta = (ell + s->alpha - 1) / s->alpha;
+    if (s->world > 1) {
+        pre->stride = (size_t)s->extmap(ell).count * s->n;
+        pre->ext = s->alloc(pre->stride * pre->beta);
+        SfheInternal::modupShard(s, pre->ext->ptr, a->c1, ell);
+        return pre;
+    }
     pre->stride = (size_t)(ell + s->K) * s->n;
     pre->ext = s->alloc(pre->stride * pre->beta);
     auto scratch = s->alloc((size_t)ell * s->n);
@@ -1453,10 +1703,10 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalFastRotation(
     // the extended digits equals extending the rotated c1.
     auto ext = s->alloc(pre->stride * pre->beta);
     // one permutation launch over every digit's rows (the map is prime-independent)
-    const uint32_t rows = pre->beta * (ell + s->K);
+    const uint32_t rows = pre->beta * (uint32_t)(pre->stride / s->n);
     sfp_automorph(s->dev, ext->ptr, pre->ext->ptr, gal, sfp_limbs{rows, rows, 0, 0});
     auto out = SfheInternal::newCt(this, a->level, a->slots);
-    sfp_automorph(s->dev, out->c0, a->c0, gal, SfheInternal::Q(ell));
+    sfp_automorph(s->dev, out->c0, a->c0, gal, st->qmap(ell));
     SfheInternal::innerAndModDown(this, ext->ptr, pre->stride, pre->beta, ell, it->second,
                                   out->c0, out->c1, 1, 0);
     s->stats.keyswitch++;
@@ -1485,8 +1735,8 @@ void weightResidues(const SfheContextState* s, double w, uint32_t level, uint32_
         const double hi = std::floor(std::ldexp(a, -64));
         v = ((u128)(u64)hi << 64) + (u128)(u64)(a - std::ldexp(hi, 64));
     }
-    for (uint32_t i = 0; i < ell; ++i) {
-        const u64 q = s->primes[i];
+    for (uint32_t i = 0; i < s->rows(ell); ++i) {  // the local rows' primes
+        const u64 q = s->primes[s->qprime(i)];
         const u64 m = (u64)(v % q);
         kk.push_back(neg ? (m ? q - m : 0) : m);
     }
@@ -1503,19 +1753,22 @@ std::vector<Ciphertext<DCRTPoly>> CryptoContextImpl<DCRTPoly>::LinearWSumRescale
     if (ell < 2) SFHE_THROW("no levels left (multiplicative depth exhausted)");
     if (nin == 0 || nin > SFP_MAX_WSUM || nout == 0) SFHE_THROW("LinearWSumRescaleMulti: bad sizes");
     std::vector<uint64_t> kk;
-    kk.reserve((size_t)nout * nin * ell);
+    kk.reserve((size_t)nout * nin * s->rows(ell));
     for (const auto& row : w) {
         if (row.size() != nin) SFHE_THROW("LinearWSumRescaleMulti: weight row size");
         for (double x : row) weightResidues(s, x, level, ell, kk);
     }
-    const size_t pw = (size_t)ell * n;  // words per polynomial
+    const size_t pw = s->polyWords(level);  // words per polynomial
     auto sums = s->alloc((size_t)nout * 2 * pw);
     sfp_lin_wsum_multi(s->dev, sums->ptr, 2 * pw, pw, in0.data(), in1.data(), nin, kk.data(), nout,
-                       SfheInternal::Q(ell));
+                       s->qmap(ell));
     // one rescale of all 2 * nout polynomials; the results share one buffer
-    const size_t qw = (size_t)(ell - 1) * n;
+    const size_t qw = s->polyWords(level + 1);
     auto res = s->alloc((size_t)nout * 2 * qw);
-    sfp_rescale(s->dev, res->ptr, sums->ptr, ell, s->qInvTable[ell].data(), 2 * nout, pw, qw);
+    if (s->world > 1)
+        SfheInternal::rescaleShard(s, res->ptr, sums->ptr, ell, 2 * nout, pw, qw);
+    else
+        sfp_rescale(s->dev, res->ptr, sums->ptr, ell, s->qInvTable[ell].data(), 2 * nout, pw, qw);
     std::vector<Ciphertext<DCRTPoly>> out(nout);
     for (uint32_t o = 0; o < nout; ++o) {
         auto ct = std::make_shared<CiphertextImpl<DCRTPoly>>();
@@ -1541,10 +1794,11 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::LinearWSumRescale(
     SfheContextState* s = st.get();
     const uint32_t ell = s->ellOf(level);
     if (ell < 2) SFHE_THROW("no levels left (multiplicative depth exhausted)");
-    auto tmp = s->alloc((size_t)2 * ell * s->n);
+    const size_t pw = s->polyWords(level);
+    auto tmp = s->alloc(2 * pw);
     uint64_t* t0 = tmp->ptr;
-    uint64_t* t1 = t0 + (size_t)ell * s->n;
-    const sfp_limbs q{ell, ell, 0};
+    uint64_t* t1 = t0 + pw;
+    const sfp_limbs q = s->qmap(ell);
     // chunks of SFP_MAX_WSUM terms accumulate through the extra "previous sum" input
     size_t done = 0;
     bool first = true;
@@ -1555,14 +1809,14 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::LinearWSumRescale(
         if (!first) {
             a0.push_back(t0);
             a1.push_back(t1);
-            for (uint32_t i = 0; i < ell; ++i) kk.push_back(1);
+            for (uint32_t i = 0; i < s->rows(ell); ++i) kk.push_back(1);
         }
         for (size_t j = done; j < done + take; ++j) {
             a0.push_back(in0[j]);
             a1.push_back(in1[j]);
             double K = w[j] * s->scale[level];  // product scale Delta_l^2 -> rescale -> Delta_{l+1}
-            for (uint32_t i = 0; i < ell; ++i) {
-                u64 q = s->primes[i];
+            for (uint32_t i = 0; i < s->rows(ell); ++i) {
+                u64 q = s->primes[s->qprime(i)];
                 double r = std::nearbyint(K);
                 bool neg = r < 0;
                 double a = std::fabs(r);
@@ -1605,6 +1859,46 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::AdjustLevel(const Ciphertext<D
     SfheInternal::deps(st.get(), {&a});
     auto r = SfheInternal::adjust(this, a, targetLevel);
     return r == a ? a->Clone() : r;
+}
+
+// ============================================================================
+// limb sharding
+
+void CryptoContextImpl<DCRTPoly>::EnableSharding(int rank, int world) {
+    OpLock g(st.get());
+    SfheContextState* s = st.get();
+    if (world < 1 || rank < 0 || rank >= world) SFHE_THROW("EnableSharding: bad rank / world");
+    if (s->relinKey || !s->rotKeys.empty()) SFHE_THROW("EnableSharding must precede the key generation");
+    if (s->world > 1) SFHE_THROW("EnableSharding: already sharded");
+    s->rank = rank;
+    s->world = world;
+    s->ptCache.clear();
+    s->ptCacheBytes = 0;
+    if (world == 1) return;
+    // P -> this rank's Q rows (targets in local row order; a level's rows are a prefix)
+    std::vector<uint32_t> src, dst;
+    for (uint32_t k = 0; k < s->K; ++k) src.push_back(s->Lq + k);
+    for (uint32_t i = 0; i < s->rows(s->Lq); ++i) dst.push_back(s->qprime(i));
+    s->moddownConvShard = dst.empty() ? nullptr : SfheInternal::makeConv(s, src, dst);
+}
+
+int CryptoContextImpl<DCRTPoly>::ShardRank() const { return st->rank; }
+int CryptoContextImpl<DCRTPoly>::ShardWorld() const { return st->world; }
+
+void CryptoContextImpl<DCRTPoly>::DownloadRows(const Ciphertext<DCRTPoly>& ct, uint64_t* out) {
+    OpLock g(st.get());
+    SfheInternal::deps(st.get(), {&ct});
+    SfheContextState* s = st.get();
+    const size_t words = (size_t)s->ellOf(ct->level) * s->n;
+    if (s->world > 1) {  // collective: every rank receives every row
+        auto full = SfheInternal::gatherFull(s, ct);
+        sfp_d2h(s->dev, out, full->ptr, 2 * words * 8);
+    } else {
+        sfp_d2h(s->dev, out, ct->c0, words * 8);
+        sfp_d2h(s->dev, out + words, ct->c1, words * 8);
+    }
+    const char* e = sfp_last_error(s->dev);
+    if (e) SFHE_THROW(std::string("device error: ") + e);
 }
 
 // ============================================================================

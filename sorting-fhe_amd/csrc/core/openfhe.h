@@ -374,6 +374,15 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
     // orders lane 0 after all of them.  Objects created on a lane may be
     // read on other lanes only after the join.
     int LaneCount() const;
+    // Limb sharding (engine extension): this process holds the
+    // RNS limbs i with i % world == rank of every ciphertext and key; call
+    // before key generation, with the device communicator set up (C ABI
+    // sfhe_comm_*).  Results are bit-identical to the unsharded context.
+    void EnableSharding(int rank, int world);
+    int ShardRank() const;
+    int ShardWorld() const;
+    // raw residues [c0 rows][c1 rows] of every limb, natural order (collective when sharded)
+    void DownloadRows(const Ciphertext<DCRTPoly>& ct, uint64_t* out);
     void ForkLanes(int count);
     void SetLane(int lane);
     void JoinLanes();

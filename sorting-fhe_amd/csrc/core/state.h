@@ -103,12 +103,60 @@ struct SfheContextState {
     uint64_t seed = 0;
     CryptoContextImpl<DCRTPoly>::OpStats stats;
 
+    // limb sharding (one process per GPU): this rank holds Q limb i and P
+    // limb k iff i % world == rank / k % world == rank, in increasing order,
+    // so a ciphertext's local rows at any level are a prefix of its rows at
+    // level 0 and rescaling drops at most the last local row.
+    int rank = 0, world = 1;
+    bool fullScope = false;  // inside FullScope: world/rank read 1/0 (setup work on every row)
+    std::vector<DeviceBufferPtr> scopeKeep;  // uncached encodings alive until the scope ends
+    std::map<uint32_t, std::vector<sfp_conv*>> modupConvShard;  // ell -> per digit (owned targets)
+    sfp_conv* moddownConvShard = nullptr;                        // P -> owned Q rows
+
     // ---- helpers ----
     uint32_t ellOf(uint32_t level) const { return Lq - level; }
+    // local rows among the first `count` limbs of a set dealt round-robin
+    uint32_t owned(uint32_t count) const {
+        return (uint32_t)rank < count ? (count - rank + world - 1) / world : 0;
+    }
+    uint32_t rows(uint32_t ell) const { return owned(ell); }  // local Q rows at ell limbs
+    uint32_t prows() const { return owned(K); }                // local P rows
+    uint32_t qprime(uint32_t i) const { return rank + i * world; }  // prime of local Q row i
+    sfp_limbs qmap(uint32_t ell) const {
+        return sfp_limbs{rows(ell), rows(ell), 0, (uint32_t)rank, (uint32_t)world};
+    }
+    // local ext rows: the Q rows of ell limbs, then the P rows
+    sfp_limbs extmap(uint32_t ell) const {
+        return sfp_limbs{rows(ell) + prows(), rows(ell), Lq + (uint32_t)rank, (uint32_t)rank, (uint32_t)world};
+    }
+    size_t polyWords(uint32_t level) const { return (size_t)rows(ellOf(level)) * n; }
     uint64_t nextSeed() { return seed ^ (0x9E3779B97F4A7C15ULL * (seedCounter++)); }
     DeviceBufferPtr alloc(size_t words);
     void releaseAll();
     void countBytes(double b) { stats.algo_bytes += b; }
+};
+
+// Setup work (key generation, encryption, decryption) runs on every row of a
+// sharded context: inside this scope the state describes one rank holding all
+// rows, and plaintext encodings are not cached (they would have the full rows).
+class FullScope {
+  public:
+    explicit FullScope(SfheContextState* s) : s_(s), rank_(s->rank), world_(s->world), was_(s->fullScope) {
+        s->rank = 0;
+        s->world = 1;
+        s->fullScope = true;
+    }
+    ~FullScope() {
+        s_->rank = rank_;
+        s_->world = world_;
+        s_->fullScope = was_;
+        if (!was_) s_->scopeKeep.clear();  // later users of the blocks are stream-ordered after
+    }
+
+  private:
+    SfheContextState* s_;
+    int rank_, world_;
+    bool was_;
 };
 
 // Serialises host-side use of a context and routes the calling thread's

@@ -15,6 +15,7 @@
 // The inverse runs the mirrored Gentleman-Sande passes and folds 1/n into
 // its last pass.  Twiddles are the bit-reversed psi tables (Shoup form).
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -46,7 +47,8 @@ struct Bar {
 static_assert(sizeof(Bar) == sizeof(sf_barrett), "layout");
 
 __device__ __forceinline__ uint32_t primeOf(const sfp_limbs& m, uint32_t i) {
-    return i < m.split ? m.base + i : m.pbase + (i - m.split);
+    const uint32_t st = m.stride ? m.stride : 1;
+    return i < m.split ? m.base + i * st : m.pbase + (i - m.split) * st;
 }
 
 __device__ __forceinline__ u64 bmul(u64 a, u64 b, const sf_barrett& m) { return sf_mul(a, b, &m); }
@@ -121,6 +123,12 @@ struct sfp_dev {
     std::unordered_map<uint64_t, std::vector<std::pair<std::vector<u64>, size_t>>> cmap;
     std::mutex mu;
     std::string err;
+    // limb sharding: this process is rank `rank` of `world`
+    int rank = 0, world = 1;
+    ncclComm_t nccl = nullptr;
+    sfp_host_allgather_fn hostAg = nullptr;
+    sfp_host_bcast_fn hostBc = nullptr;
+    void* hostUser = nullptr;
 };
 
 struct sfp_conv {
@@ -179,8 +187,9 @@ static void checkLaunch(sfp_dev* d, const char* k) {
 static bool limbsOk(sfp_dev* d, const sfp_limbs& m, const char* what) {
     if (!m.count) return true;
     uint32_t hi = 0;
-    if (m.split) hi = m.base + m.split - 1;
-    if (m.count > m.split) hi = std::max(hi, m.pbase + (m.count - m.split) - 1);
+    const uint32_t st = m.stride ? m.stride : 1;
+    if (m.split) hi = m.base + (std::min(m.split, m.count) - 1) * st;
+    if (m.count > m.split) hi = std::max(hi, m.pbase + (m.count - m.split - 1) * st);
     if (hi < d->np && m.count <= (1u << 20)) return true;
     std::lock_guard<std::mutex> g(d->mu);
     if (d->err.empty()) d->err = std::string(what) + ": limb map indexes past the prime table";
@@ -1354,22 +1363,24 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
 }
 
 // key inner product over ext rows t < ell+K
+// ext row t (prime primeOf(pm, t)) uses key row t < pm.split ? t : keyQ +
+// (t - pm.split) of each digit's [b rows][a rows] block of keyRows rows.
 __global__ __launch_bounds__(kThreads) void k_ks_inner(u64* __restrict__ acc0, u64* __restrict__ acc1,
                                                        const u64* __restrict__ ext, size_t extStride,
                                                        const u64* __restrict__ key, uint32_t beta,
-                                                       uint32_t ell, uint32_t K, uint32_t Lq,
+                                                       sfp_limbs pm, uint32_t keyQ, uint32_t keyRows,
                                                        const u64* __restrict__ fold0,
                                                        const u64* __restrict__ fold1, u64 foldK,
                                                        const sf_barrett* __restrict__ bar, uint32_t logn) {
-    const uint32_t rows = ell + K, NP = Lq + K;
-    const size_t total = (size_t)rows << logn;
+    const uint32_t ell = pm.split, NP = keyRows;
+    const size_t total = (size_t)pm.count << logn;
     const uint32_t n = 1u << logn;
     for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < total;
          i += (size_t)gridDim.x * kThreads) {
         const uint32_t t = (uint32_t)(i >> logn);
         const uint32_t x = (uint32_t)(i & (n - 1));
-        const uint32_t kr = t < ell ? t : Lq + (t - ell);
-        const sf_barrett B = loadBar(bar, kr);
+        const uint32_t kr = t < ell ? t : keyQ + (t - ell);
+        const sf_barrett B = loadBar(bar, primeOf(pm, t));
         Acc s0{0, 0}, s1{0, 0};
         for (uint32_t j = 0; j < beta; ++j) {
             const u64 e = ext[j * extStride + i];
@@ -1648,6 +1659,7 @@ sfp_dev* sfp_create(int device, const sfp_tables* t) {
 void sfp_destroy(sfp_dev* d) {
     if (!d) return;
     syncAll(d);
+    if (d->nccl) ncclCommDestroy(d->nccl);
     for (sfp_event* e : d->evFree) {
         hipEventDestroy(e->e);
         delete e;
@@ -1920,7 +1932,7 @@ void sfp_lin_wsum(sfp_dev* d, uint64_t* out, const uint64_t* const* ins, const u
 void sfp_lin_wsum_multi(sfp_dev* d, uint64_t* out, size_t outStride, size_t polyStride,
                         const uint64_t* const* in0, const uint64_t* const* in1, uint32_t nin,
                         const uint64_t* k, uint32_t nout, sfp_limbs m) {
-    if (!nout || !nin) return;
+    if (!nout || !nin || !m.count) return;
     if (nin > SFP_MAX_WSUM || !limbsOk(d, m, "lin_wsum_multi")) {
         record(d, "lin_wsum_multi", hipErrorInvalidValue);
         return;
@@ -2211,8 +2223,9 @@ static void convLaunch(sfp_dev* d, const ConvJobs& J, uint32_t njobs, bool fpOk)
         bytes += 8.0 * d->n * (j.ns + j.ntUse);
     }
     const bool fp = nttFp() && fpOk;
-    const dim3 g(fp ? d->n / kConvCoefs : d->n / (2 * kThreads), njobs,
-                 fp ? maxZ : (maxT + kConvChunk - 1) / kConvChunk);
+    const uint32_t gz = fp ? maxZ : (maxT + kConvChunk - 1) / kConvChunk;
+    if (!gz) return;
+    const dim3 g(fp ? d->n / kConvCoefs : d->n / (2 * kThreads), njobs, gz);
     timedLaunch(d, SFP_FAM_CONV, bytes, [&] {
         if (fp && maxS <= 16)
             hipLaunchKernelGGL(k_convf<16>, g, dim3(kThreads), 0, d->st(), J, d->bar, d->qinvD, d->logn);
@@ -2227,6 +2240,14 @@ static void convLaunch(sfp_dev* d, const ConvJobs& J, uint32_t njobs, bool fpOk)
 void sfp_conv_apply(sfp_dev* d, uint64_t* dst, const uint64_t* src, const sfp_conv* c) {
     ConvJobs J;
     J.j[0] = convJob(c, dst, src, c->nt, 0);
+    convLaunch(d, J, 1, c->fpOk);
+}
+
+void sfp_conv_apply_centered(sfp_dev* d, uint64_t* dst, const uint64_t* src, const sfp_conv* c,
+                             uint32_t ntUse) {
+    if (!c || !ntUse) return;
+    ConvJobs J;
+    J.j[0] = convJob(c, dst, src, std::min(ntUse, c->nt), 1);
     convLaunch(d, J, 1, c->fpOk);
 }
 
@@ -2281,7 +2302,8 @@ void sfp_ks_inner_fold(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_
     // reads beta ext rows + 2*beta key rows, writes 2 accumulator rows, per limb
     timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + 2.0), [&] {
         hipLaunchKernelGGL(k_ks_inner, dim3(ewGrid(total)), dim3(kThreads), 0, d->st(), acc0, acc1, ext,
-                           extStride, key, beta, ell, K, Lq, fold0, fold1, foldK, d->bar, d->logn);
+                           extStride, key, beta, sfp_limbs{ell + K, ell, Lq, 0, 1}, Lq, Lq + K, fold0, fold1,
+                           foldK, d->bar, d->logn);
     });
     checkLaunch(d, "ks_inner");
 }
@@ -2424,3 +2446,139 @@ void sfp_load_i64(sfp_dev* d, uint64_t* p, const int64_t* c, sfp_limbs m) {
 }
 
 
+
+// ---- limb sharding ----
+// dst row i = src row rows[i]
+__global__ __launch_bounds__(kThreads) void k_gather_rows(ulonglong2* __restrict__ dst,
+                                                          const ulonglong2* __restrict__ src,
+                                                          const uint32_t* __restrict__ rows, uint32_t logn) {
+    const uint32_t half = 1u << (logn - 1);  // 16-byte pairs per row
+    const uint32_t i = blockIdx.y;
+    const uint32_t r = rows[i];
+    for (uint32_t x = blockIdx.x * kThreads + threadIdx.x; x < half; x += gridDim.x * kThreads)
+        dst[(size_t)i * half + x] = src[(size_t)r * half + x];
+}
+
+void sfp_gather_rows(sfp_dev* d, uint64_t* dst, const uint64_t* src, const uint32_t* rows, uint32_t count) {
+    if (!count) return;
+    const uint32_t* dr = (const uint32_t*)ringPut(d, rows, (size_t)count * 4);
+    const dim3 g(std::max(1u, std::min(64u, (d->n / 2) / kThreads)), count);
+    hipLaunchKernelGGL(k_gather_rows, g, dim3(kThreads), 0, d->st(), (ulonglong2*)dst, (const ulonglong2*)src, dr,
+                       d->logn);
+    checkLaunch(d, "gather_rows");
+}
+
+void sfp_rescale_rows(sfp_dev* d, uint64_t* out, const uint64_t* in, const uint64_t* last, uint32_t dropPrime,
+                      sfp_limbs m, const uint64_t* qlinv, uint32_t npoly, size_t inStride, size_t outStride,
+                      size_t lastStride) {
+    const uint32_t n = d->n, cnt = m.count;
+    if (!cnt || !npoly) return;
+    if (cnt > SFP_MAX_LIMBS || dropPrime >= d->np || !limbsOk(d, m, "rescale_rows")) {
+        record(d, "rescale_rows", hipErrorInvalidValue);
+        return;
+    }
+    u64* tmp = scratch(d, (size_t)npoly * cnt * n);
+    RowGroup B = rowsOf(npoly, cnt, m);
+    B.src = RowPtr{last, (long long)lastStride, 0};
+    B.lift = 1;
+    B.liftPrime = dropPrime;
+    B.dst = RowPtr{tmp, (long long)cnt * n, (long long)n};
+    B.epi = 1;
+    B.ein = RowPtr{in, (long long)inStride, (long long)n};
+    B.eout = RowPtr{out, (long long)outStride, (long long)n};
+    const u64 ql = d->hbar[dropPrime].q;
+    u64 kS[SFP_MAX_LIMBS], lsub[SFP_MAX_LIMBS];
+    for (uint32_t i = 0; i < cnt; ++i) {
+        const u64 q = d->hbar[sfp_prime_of(m, i)].q;
+        kS[i] = sf_shoup_precomp(qlinv[i], q);
+        lsub[i] = ql % q;
+    }
+    B.k = devConst(d, qlinv, cnt);
+    B.kS = devConst(d, kS, cnt);
+    B.liftSub = devConst(d, lsub, cnt);
+    nttRows(d, B, 0);
+}
+
+void sfp_ks_inner_map(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext, size_t extStride,
+                      const uint64_t* key, uint32_t beta, sfp_limbs pm, uint32_t keyQ, uint32_t keyRows) {
+    if (!pm.count || !limbsOk(d, pm, "ks_inner_map")) return;
+    const size_t total = (size_t)pm.count * d->n;
+    timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + 2.0), [&] {
+        hipLaunchKernelGGL(k_ks_inner, dim3(ewGrid(total)), dim3(kThreads), 0, d->st(), acc0, acc1, ext, extStride,
+                           key, beta, pm, keyQ, keyRows, (const u64*)nullptr, (const u64*)nullptr, (u64)0, d->bar,
+                           d->logn);
+    });
+    checkLaunch(d, "ks_inner_map");
+}
+
+int sfp_comm_uid(void* uid128) {
+    static_assert(sizeof(ncclUniqueId) == 128, "RCCL unique id size");
+    return ncclGetUniqueId(reinterpret_cast<ncclUniqueId*>(uid128)) == ncclSuccess ? 0 : -1;
+}
+
+int sfp_comm_init_rccl(sfp_dev* d, int rank, int world, const void* uid128) {
+    ncclUniqueId id;
+    std::memcpy(&id, uid128, sizeof id);
+    SFP_CHECK(hipSetDevice(d->device));
+    ncclComm_t c = nullptr;
+    const ncclResult_t r = ncclCommInitRank(&c, world, id, rank);
+    if (r != ncclSuccess) {
+        std::lock_guard<std::mutex> g(d->mu);
+        if (d->err.empty()) d->err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);
+        return -1;
+    }
+    d->nccl = c;
+    d->rank = rank;
+    d->world = world;
+    return 0;
+}
+
+void sfp_comm_set_host(sfp_dev* d, int rank, int world, sfp_host_allgather_fn ag, sfp_host_bcast_fn bc,
+                       void* user) {
+    d->rank = rank;
+    d->world = world;
+    d->hostAg = ag;
+    d->hostBc = bc;
+    d->hostUser = user;
+}
+
+static void ncclCheck(sfp_dev* d, const char* what, ncclResult_t r) {
+    if (r == ncclSuccess) return;
+    std::lock_guard<std::mutex> g(d->mu);
+    if (d->err.empty()) d->err = std::string(what) + ": " + ncclGetErrorString(r);
+}
+
+void sfp_allgather(sfp_dev* d, const void* send, void* recv, size_t bytes) {
+    if (d->world == 1) {
+        if (send != recv) sfp_d2d(d, recv, send, bytes);
+        return;
+    }
+    if (d->nccl) {
+        ncclCheck(d, "ncclAllGather", ncclAllGather(send, recv, bytes, ncclUint8, d->nccl, d->st()));
+        return;
+    }
+    if (!d->hostAg) {
+        record(d, "allgather (no communicator)", hipErrorInvalidValue);
+        return;
+    }
+    std::vector<char> hs(bytes), hr(bytes * d->world);
+    devToHost(d, hs.data(), send, bytes);
+    d->hostAg(d->hostUser, hs.data(), hr.data(), bytes);
+    hostToDev(d, recv, hr.data(), hr.size());
+}
+
+void sfp_bcast(sfp_dev* d, void* buf, size_t bytes, int root) {
+    if (d->world == 1) return;
+    if (d->nccl) {
+        ncclCheck(d, "ncclBroadcast", ncclBroadcast(buf, buf, bytes, ncclUint8, root, d->nccl, d->st()));
+        return;
+    }
+    if (!d->hostBc) {
+        record(d, "bcast (no communicator)", hipErrorInvalidValue);
+        return;
+    }
+    std::vector<char> h(bytes);
+    devToHost(d, h.data(), buf, bytes);
+    d->hostBc(d->hostUser, h.data(), bytes, root);
+    hostToDev(d, buf, h.data(), bytes);
+}

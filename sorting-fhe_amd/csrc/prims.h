@@ -28,14 +28,17 @@ extern "C" {
 typedef struct sfp_dev sfp_dev;
 
 typedef struct {
-    uint32_t count;  // number of limbs
-    uint32_t split;  // limbs [0, split) -> primes [base, base + split)
-    uint32_t pbase;  // limbs [split, count) -> primes [pbase, ...)
-    uint32_t base;   // (0 unless addressing a run that starts mid-table)
+    uint32_t count;   // number of limbs
+    uint32_t split;   // limbs [0, split) -> primes base, base + stride, ...
+    uint32_t pbase;   // limbs [split, count) -> primes pbase, pbase + stride, ...
+    uint32_t base;    // (0 unless addressing a run that starts mid-table)
+    uint32_t stride;  // prime step between consecutive limbs; 0 or 1 = contiguous.
+                      // A limb-sharded rank r of W holds primes r, r + W, ...
 } sfp_limbs;
 
 static inline uint32_t sfp_prime_of(sfp_limbs m, uint32_t i) {
-    return i < m.split ? m.base + i : m.pbase + (i - m.split);
+    const uint32_t st = m.stride ? m.stride : 1;
+    return i < m.split ? m.base + i * st : m.pbase + (i - m.split) * st;
 }
 
 // Tables the host computes once per context (identical for both backends).
@@ -155,6 +158,10 @@ void sfp_free_conv(sfp_dev* d, sfp_conv* c);
 // Fast base conversion in the COEFFICIENT domain: src has ns rows; target t
 // is written to dst row dst_row[t].
 void sfp_conv_apply(sfp_dev* d, uint64_t* dst, const uint64_t* src, const sfp_conv* c);
+// Centred conversion (source values taken in (-s_i/2, s_i/2], as ModDown)
+// to the first nt_use targets only.
+void sfp_conv_apply_centered(sfp_dev* d, uint64_t* dst, const uint64_t* src, const sfp_conv* c,
+                             uint32_t nt_use);
 
 // Hybrid key-switch ModUp of every digit (evaluation domain in and out).
 //   in   : ell limbs (limb map identity), evaluation domain.
@@ -233,6 +240,43 @@ int sfp_event_done(sfp_dev* d, const sfp_event* e);
 void sfp_event_free(sfp_dev* d, sfp_event* e);
 // Lane `waiter` waits for everything enqueued so far on lane `waitee`.
 void sfp_lane_wait(sfp_dev* d, int waiter, int waitee);
+
+// ---- multi-process limb sharding (one process per GPU) --------------------------
+// Collectives over the ranks of a sharded context, ordered on the current
+// lane like every other primitive.  Two transports:
+//   * RCCL (HIP backend, production): sfp_comm_uid on one rank, the 128-byte
+//     id shared out of band (torch.distributed), sfp_comm_init_rccl on all;
+//   * host callbacks (both backends; tests): the caller's allgather/bcast over
+//     host memory (e.g. torch.distributed gloo), after a stream drain.
+typedef void (*sfp_host_allgather_fn)(void* user, const void* send, void* recv, size_t bytes);
+typedef void (*sfp_host_bcast_fn)(void* user, void* buf, size_t bytes, int root);
+// 0 on success; -1 where the backend has no RCCL (the oracle)
+int sfp_comm_uid(void* uid128);
+int sfp_comm_init_rccl(sfp_dev* d, int rank, int world, const void* uid128);
+void sfp_comm_set_host(sfp_dev* d, int rank, int world, sfp_host_allgather_fn ag, sfp_host_bcast_fn bc,
+                       void* user);
+// recv = world blocks of `bytes`, rank-major (recv may contain send in place)
+void sfp_allgather(sfp_dev* d, const void* send, void* recv, size_t bytes);
+void sfp_bcast(sfp_dev* d, void* buf, size_t bytes, int root);
+
+// dst row i = src row rows[i] (count rows of n words; rows: host array)
+void sfp_gather_rows(sfp_dev* d, uint64_t* dst, const uint64_t* src, const uint32_t* rows, uint32_t count);
+
+// Rescale with the dropped row supplied in coefficient form (limb sharding:
+// the row's owner broadcast it):  out_p,i = (in_p,i - [last_p]_{q_i}) * qlinv_i
+// for the rows of map m (evaluation domain), last_p the centred lift of the
+// dropped row modulo prime drop_prime.  npoly polys: in / out / last strides.
+void sfp_rescale_rows(sfp_dev* d, uint64_t* out, const uint64_t* in, const uint64_t* last,
+                      uint32_t drop_prime, sfp_limbs m, const uint64_t* qlinv, uint32_t npoly,
+                      size_t in_stride, size_t out_stride, size_t last_stride);
+
+// Key inner product with explicit maps (limb sharding): ext rows follow the
+// prime map pm (pm.split Q rows then P rows); ext row t uses key row
+// t < pm.split ? t : keyQ + (t - pm.split) of each digit's [b rows][a rows]
+// block of key_rows rows.
+void sfp_ks_inner_map(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
+                      size_t ext_stride, const uint64_t* key, uint32_t beta, sfp_limbs pm,
+                      uint32_t keyQ, uint32_t key_rows);
 
 // ---- live kernel timing ---------------------------------------------------------
 // Kernel families timed with events recorded on the backend's stream around

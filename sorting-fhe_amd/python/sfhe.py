@@ -34,6 +34,7 @@ ABI_SYMBOLS = [
     "sfhe_direct_sort_params", "sfhe_doubled_sinc_coeffs", "sfhe_sorter_create",
     "sfhe_sorter_destroy", "sfhe_sorter_sort", "sfhe_sorter_rank", "sfhe_sorter_place",
     "sfhe_decompose", "sfhe_kernel_timing", "sfhe_kernel_timing_read",
+    "sfhe_comm_uid", "sfhe_shard_rccl", "sfhe_shard_host",
 ]
 
 
@@ -65,6 +66,10 @@ _PSZ = C.POINTER(C.c_size_t)
 _PD = C.POINTER(C.c_double)
 _PI32 = C.POINTER(C.c_int32)
 _PU64 = C.POINTER(C.c_uint64)
+
+# host collectives of sfhe_shard_host (sfhe_allgather_fn / sfhe_bcast_fn)
+_AG = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t)
+_BC = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int)
 
 _SIGS = {
     "sfhe_abi_version": (C.c_int, []),
@@ -108,6 +113,9 @@ _SIGS = {
     "sfhe_kernel_timing": (C.c_int, [_VP, _U32, _U32]),
     "sfhe_kernel_timing_read": (C.c_int, [_VP, _U32, _PU64, _PU64, _PD, _PD]),
     "sfhe_decompose": (C.c_int, [_U32, _PI32, _SZ, C.c_int32, C.c_int32, C.c_int, _PI32, _PI32, _SZ, _PSZ]),
+    "sfhe_comm_uid": (C.c_int, [_VP]),
+    "sfhe_shard_rccl": (C.c_int, [_VP, C.c_int, C.c_int, _VP]),
+    "sfhe_shard_host": (C.c_int, [_VP, C.c_int, C.c_int, _AG, _BC, _VP]),
 }
 
 _libs: dict = {}
@@ -148,7 +156,9 @@ class Engine:
                  batch_size: int = 0, scaling_mod_size: int = 40, first_mod_size: int = 60,
                  secure: bool = False, num_large_digits: int = 0, seed: int = 0x5EED5EED2025,
                  device: int = 0, rotations: Sequence[int] = (), keygen: bool = True,
-                 scaling: str = "FLEXIBLEAUTOEXT"):
+                 scaling: str = "FLEXIBLEAUTOEXT", shard=None):
+        """shard: None, ("rccl", rank, world, uid) or ("host", rank, world, comm)
+        (limb sharding, include/sfhe.h; every rank passes the same params)."""
         self.lib = load(backend)
         self.backend = backend
         p = Params()
@@ -165,6 +175,15 @@ class Engine:
         p.scaling_technique = {"FLEXIBLEAUTO": 2, "FLEXIBLEAUTOEXT": 3}[scaling]
         self.ctx = C.c_void_p()
         self._chk(self.lib.sfhe_context_create(C.byref(p), C.byref(self.ctx)))
+        self._comm_refs = None
+        if shard is not None:
+            kind, rank, world, arg = shard
+            if kind == "rccl":
+                self.shard_rccl(rank, world, arg)
+            elif kind == "host":
+                self.shard_host(rank, world, arg)
+            else:
+                raise ValueError(f"unknown shard transport {kind!r}")
         if keygen:
             self._chk(self.lib.sfhe_keygen(self.ctx))
             if rotations:
@@ -190,6 +209,19 @@ class Engine:
         out = C.c_void_p()
         self._chk(fn(*args, C.byref(out)))
         return Ct(self, out)
+
+    # -- limb sharding --
+    def shard_rccl(self, rank: int, world: int, uid: bytes):
+        buf = (C.c_uint8 * 128).from_buffer_copy(bytes(uid))
+        self._chk(self.lib.sfhe_shard_rccl(self.ctx, rank, world, buf))
+
+    def shard_host(self, rank: int, world: int, comm):
+        """comm: object with allgather(rank, send, recv, nbytes) and
+        bcast(rank, buf, nbytes, root) over raw addresses (ThreadComm, GlooComm)."""
+        ag = _AG(lambda _u, send, recv, nb: comm.allgather(rank, send, recv, nb))
+        bc = _BC(lambda _u, buf, nb, root: comm.bcast(rank, buf, nb, root))
+        self._chk(self.lib.sfhe_shard_host(self.ctx, rank, world, ag, bc, None))
+        self._comm_refs = (ag, bc, comm)  # the library keeps the raw pointers
 
     # -- context --
     def rotate_keygen(self, idx: Sequence[int]):
@@ -388,3 +420,92 @@ def decompose(N: int, keys: Sequence[int], rotation: int, wrapN: int, algo: int,
     if rc != SFHE_OK:
         raise SfheError(lib.sfhe_last_error().decode())
     return [(v[i], s[i]) for i in range(min(cnt.value, cap))]
+
+
+# ---- limb-sharding transports ------------------------------------------------
+
+def comm_uid(backend: str = "hip"):
+    """128-byte RCCL unique id (bytes), or None where the backend has no RCCL."""
+    lib = load(backend)
+    buf = (C.c_uint8 * 128)()
+    if lib.sfhe_comm_uid(buf) != SFHE_OK:
+        return None
+    return bytes(buf)
+
+
+class ThreadComm:
+    """Host collectives between `world` threads of one process (each thread
+    one rank; tests).  Callbacks run with the GIL held; the library calls
+    them with the GIL released, so the ranks' device work overlaps."""
+
+    def __init__(self, world: int, timeout: float = 600.0):
+        import threading
+        self.world = world
+        self.bar = threading.Barrier(world, timeout=timeout)
+        self.slots = [b""] * world
+
+    def allgather(self, rank, send, recv, nbytes):
+        self.slots[rank] = C.string_at(send, nbytes) if nbytes else b""
+        self.bar.wait()
+        for r in range(self.world):
+            if nbytes:
+                C.memmove(recv + r * nbytes, self.slots[r], nbytes)
+        self.bar.wait()
+
+    def bcast(self, rank, buf, nbytes, root):
+        if rank == root:
+            self.slots[root] = C.string_at(buf, nbytes) if nbytes else b""
+        self.bar.wait()
+        if rank != root and nbytes:
+            C.memmove(buf, self.slots[root], nbytes)
+        self.bar.wait()
+
+
+class GlooComm:
+    """Host collectives over an initialised torch.distributed process group
+    (gloo: CPU tensors; one process per rank)."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.dist, self.group = dist, group
+        self.world = dist.get_world_size(group)
+
+    def allgather(self, rank, send, recv, nbytes):
+        import torch
+        t = torch.frombuffer(bytearray(C.string_at(send, nbytes)), dtype=torch.uint8)
+        outs = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(self.world)]
+        self.dist.all_gather(outs, t, group=self.group)
+        for r, o in enumerate(outs):
+            C.memmove(recv + r * nbytes, o.numpy().ctypes.data, nbytes)
+
+    def bcast(self, rank, buf, nbytes, root):
+        import torch
+        t = torch.frombuffer(bytearray(C.string_at(buf, nbytes)), dtype=torch.uint8)
+        self.dist.broadcast(t, src=root, group=self.group)
+        if rank != root:
+            C.memmove(buf, t.numpy().ctypes.data, nbytes)
+
+
+def run_sharded_threads(backend: str, world: int, fn, **engine_kw):
+    """Run fn(engine) on `world` limb-sharded engines, one thread per rank,
+    over ThreadComm; returns the per-rank results (rank order)."""
+    import threading
+    comm = ThreadComm(world)
+    outs, errs = [None] * world, []
+
+    def body(r):
+        try:
+            e = Engine(backend, shard=("host", r, world, comm), **engine_kw)
+            outs[r] = fn(e)
+        except BaseException as ex:  # unblock the other ranks
+            errs.append(ex)
+            comm.bar.abort()
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if errs:
+        raise errs[0]
+    return outs

@@ -1,0 +1,140 @@
+"""Limb sharding on the CPU oracle: W ranks, each holding the
+RNS limbs i with i % W == rank, must produce exactly the residues of the
+unsharded context -- every evaluator op, and a whole DirectSort.
+
+The ranks run as threads of this process over ThreadComm (host-memory
+all-gather / broadcast through the C ABI's sfhe_shard_host), and as two
+processes over torch.distributed gloo (GlooComm), the transport a CPU-only
+multi-process job would use.  RCCL (sfhe_shard_rccl) is the GPU path
+(tests/test_gpu_shard.py, bench.py --shard).
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import sfhe
+from oracle import slotsim
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+OPS_KW = dict(mult_depth=6, ring_dim=1 << 12, batch_size=16, seed=4242, rotations=[1, 3, -2])
+
+
+def ops_program(e):
+    """Every evaluator op the sort uses, down to the last level (where a rank
+    of W = 3 holds no limb); returns the downloaded residues and a decryption."""
+    rng = np.random.default_rng(11)
+    a = rng.uniform(-1, 1, 16).tolist()
+    b = rng.uniform(-1, 1, 16).tolist()
+    ca, cb = e.encrypt(a), e.encrypt(b)
+    x = e.mult(ca, cb)
+    x2 = e.mult(x, x)
+    res = {
+        "enc": ca,
+        "add": e.add(ca, cb),
+        "sub": e.sub(ca, cb),
+        "mult": x,
+        "mult_const": e.mult_const(ca, -3.75),
+        "add_const": e.add_const(ca, 0.5),
+        "mult_plain": e.mult_plain(ca, list(range(16)), 16),
+        "rotate1": e.rotate(ca, 1),
+        "rotate-2": e.rotate(x, -2),
+        "mixed_level": e.add(x2, ca),
+        "deep": e.mult(e.mult(e.mult(e.mult(x2, x), cb), ca), x),
+        "cheb": e.chebyshev(ca, [0.1, 0.5, -0.25, 0.125, 0.05]),
+    }
+    out = {k: v.download() for k, v in res.items()}
+    out["dec"] = np.array(e.decrypt(res["deep"]))
+    out["levels"] = np.array([v.level for v in res.values()])
+    return out
+
+
+def sort_program(e, N):
+    e.set_quiet(True)
+    x = slotsim.input_vector(N).tolist()
+    s = e.sorter(N)
+    r = s.sort(e.encrypt(x), *slotsim.default_sign_config(N))
+    return {"sort": r.download(), "dec": np.array(e.decrypt(r))}
+
+
+def compare(ref, got):
+    assert sorted(ref) == sorted(got)
+    for k, v in ref.items():
+        assert got[k].shape == v.shape, k
+        bad = int(np.count_nonzero(got[k] != v))
+        assert bad == 0, f"{k}: {bad} of {v.size} values differ"
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_ops_bitexact_oracle(oracle_lib, world):
+    ref = ops_program(sfhe.Engine("oracle", **OPS_KW))
+    assert ref["levels"].max() == OPS_KW["mult_depth"]  # "deep" reached the last level
+    outs = sfhe.run_sharded_threads("oracle", world, ops_program, **OPS_KW)
+    for r in range(world):
+        compare(ref, outs[r])
+
+
+def test_sharded_sort_bitexact_oracle(oracle_lib):
+    N = 8
+    depth, rots = sfhe.direct_sort_params(N, "oracle")
+    kw = dict(mult_depth=depth, ring_dim=1 << 12, batch_size=N, rotations=rots, seed=777)
+    ref = sort_program(sfhe.Engine("oracle", **kw), N)
+    assert np.max(np.abs(ref["dec"][:N] - np.sort(slotsim.input_vector(N)))) < 0.01
+    outs = sfhe.run_sharded_threads("oracle", 2, lambda e: sort_program(e, N), **kw)
+    for r in range(2):
+        compare(ref, outs[r])
+
+
+def test_shard_argument_errors(oracle_lib):
+    e = sfhe.Engine("oracle", keygen=False, mult_depth=2, ring_dim=1 << 12)
+    with pytest.raises(sfhe.SfheError):
+        e.shard_host(3, 2, sfhe.ThreadComm(2))  # rank outside the world
+    e2 = sfhe.Engine("oracle", mult_depth=2, ring_dim=1 << 12)
+    with pytest.raises(sfhe.SfheError):  # after key generation
+        e2.shard_host(0, 2, sfhe.ThreadComm(2))
+    assert sfhe.comm_uid("oracle") is None  # the oracle has no RCCL
+    with pytest.raises(sfhe.SfheError):
+        sfhe.Engine("oracle", keygen=False, mult_depth=2, ring_dim=1 << 12, shard=("rccl", 0, 2, bytes(128)))
+
+
+GLOO_SCRIPT = r"""
+import sys
+import numpy as np
+sys.path.insert(0, {py!r}); sys.path.insert(0, {root!r}); sys.path.insert(0, {tests!r})
+import torch.distributed as dist
+import sfhe
+from test_shard import ops_program, OPS_KW
+rank = int(sys.argv[1])
+dist.init_process_group("gloo", init_method="tcp://127.0.0.1:{port}", rank=rank, world_size=2)
+e = sfhe.Engine("oracle", shard=("host", rank, 2, sfhe.GlooComm()), **OPS_KW)
+out = ops_program(e)
+np.savez({path!r} + str(rank) + ".npz", **out)
+dist.barrier()
+dist.destroy_process_group()
+"""
+
+
+def test_sharded_ops_gloo_two_processes(oracle_lib, tmp_path):
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    path = str(tmp_path / "rank")
+    code = GLOO_SCRIPT.format(py=os.path.join(ROOT, "sorting-fhe_amd", "python"), root=ROOT,
+                              tests=os.path.join(ROOT, "tests"), port=port, path=path)
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    procs = [subprocess.Popen([sys.executable, "-c", code, str(r)], env=env) for r in range(2)]
+    try:
+        for p in procs:
+            assert p.wait(timeout=600) == 0
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    ref = ops_program(sfhe.Engine("oracle", **OPS_KW))
+    for r in range(2):
+        z = np.load(f"{path}{r}.npz")
+        compare(ref, {k: z[k] for k in z.files})
