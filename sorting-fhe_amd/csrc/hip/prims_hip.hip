@@ -15,6 +15,7 @@
 // The inverse runs the mirrored Gentleman-Sande passes and folds 1/n into
 // its last pass.  Twiddles are the bit-reversed psi tables (Shoup form).
 #include <hip/hip_runtime.h>
+#include <dlfcn.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -1656,10 +1657,42 @@ sfp_dev* sfp_create(int device, const sfp_tables* t) {
     return d;
 }
 
+// RCCL is opened on first use (dlopen), not linked: processes that never
+// shard do not load it, and its threads and teardown stay out of them.
+struct RcclApi {
+    bool ok = false;
+    ncclResult_t (*getUniqueId)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*commInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*commDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*allGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*broadcast)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    const char* (*errorString)(ncclResult_t) = nullptr;
+};
+
+static RcclApi& rcclApi() {
+    static RcclApi a;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* h = nullptr;
+        for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+            if ((h = dlopen(name, RTLD_NOW | RTLD_LOCAL))) break;
+        if (!h) return;
+        auto sym = [h](auto& f, const char* n) { f = reinterpret_cast<std::remove_reference_t<decltype(f)>>(dlsym(h, n)); };
+        sym(a.getUniqueId, "ncclGetUniqueId");
+        sym(a.commInitRank, "ncclCommInitRank");
+        sym(a.commDestroy, "ncclCommDestroy");
+        sym(a.allGather, "ncclAllGather");
+        sym(a.broadcast, "ncclBroadcast");
+        sym(a.errorString, "ncclGetErrorString");
+        a.ok = a.getUniqueId && a.commInitRank && a.commDestroy && a.allGather && a.broadcast && a.errorString;
+    });
+    return a;
+}
+
 void sfp_destroy(sfp_dev* d) {
     if (!d) return;
     syncAll(d);
-    if (d->nccl) ncclCommDestroy(d->nccl);
+    if (d->nccl) rcclApi().commDestroy(d->nccl);
     for (sfp_event* e : d->evFree) {
         hipEventDestroy(e->e);
         delete e;
@@ -2513,18 +2546,24 @@ void sfp_ks_inner_map(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t
 
 int sfp_comm_uid(void* uid128) {
     static_assert(sizeof(ncclUniqueId) == 128, "RCCL unique id size");
-    return ncclGetUniqueId(reinterpret_cast<ncclUniqueId*>(uid128)) == ncclSuccess ? 0 : -1;
+    if (!rcclApi().ok) return -1;
+    return rcclApi().getUniqueId(reinterpret_cast<ncclUniqueId*>(uid128)) == ncclSuccess ? 0 : -1;
 }
 
 int sfp_comm_init_rccl(sfp_dev* d, int rank, int world, const void* uid128) {
     ncclUniqueId id;
     std::memcpy(&id, uid128, sizeof id);
     SFP_CHECK(hipSetDevice(d->device));
+    if (!rcclApi().ok) {
+        std::lock_guard<std::mutex> g(d->mu);
+        if (d->err.empty()) d->err = "RCCL library (librccl.so.1) not found";
+        return -1;
+    }
     ncclComm_t c = nullptr;
-    const ncclResult_t r = ncclCommInitRank(&c, world, id, rank);
+    const ncclResult_t r = rcclApi().commInitRank(&c, world, id, rank);
     if (r != ncclSuccess) {
         std::lock_guard<std::mutex> g(d->mu);
-        if (d->err.empty()) d->err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);
+        if (d->err.empty()) d->err = std::string("ncclCommInitRank: ") + rcclApi().errorString(r);
         return -1;
     }
     d->nccl = c;
@@ -2545,7 +2584,7 @@ void sfp_comm_set_host(sfp_dev* d, int rank, int world, sfp_host_allgather_fn ag
 static void ncclCheck(sfp_dev* d, const char* what, ncclResult_t r) {
     if (r == ncclSuccess) return;
     std::lock_guard<std::mutex> g(d->mu);
-    if (d->err.empty()) d->err = std::string(what) + ": " + ncclGetErrorString(r);
+    if (d->err.empty()) d->err = std::string(what) + ": " + rcclApi().errorString(r);
 }
 
 void sfp_allgather(sfp_dev* d, const void* send, void* recv, size_t bytes) {
@@ -2554,7 +2593,7 @@ void sfp_allgather(sfp_dev* d, const void* send, void* recv, size_t bytes) {
         return;
     }
     if (d->nccl) {
-        ncclCheck(d, "ncclAllGather", ncclAllGather(send, recv, bytes, ncclUint8, d->nccl, d->st()));
+        ncclCheck(d, "ncclAllGather", rcclApi().allGather(send, recv, bytes, ncclUint8, d->nccl, d->st()));
         return;
     }
     if (!d->hostAg) {
@@ -2570,7 +2609,7 @@ void sfp_allgather(sfp_dev* d, const void* send, void* recv, size_t bytes) {
 void sfp_bcast(sfp_dev* d, void* buf, size_t bytes, int root) {
     if (d->world == 1) return;
     if (d->nccl) {
-        ncclCheck(d, "ncclBroadcast", ncclBroadcast(buf, buf, bytes, ncclUint8, root, d->nccl, d->st()));
+        ncclCheck(d, "ncclBroadcast", rcclApi().broadcast(buf, buf, bytes, ncclUint8, root, d->nccl, d->st()));
         return;
     }
     if (!d->hostBc) {

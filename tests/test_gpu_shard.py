@@ -35,9 +35,30 @@ def test_sharded_sort_bitexact_hip(hip_lib):
     assert np.array_equal(ref["sort"], ora["sort"])
 
 
+RCCL_SCRIPT = r"""
+import sys
+sys.path.insert(0, {py!r}); sys.path.insert(0, {tests!r})
+import sfhe
+from test_shard import OPS_KW, compare, ops_program
+uid = sfhe.comm_uid("hip")
+assert uid is not None and len(uid) == 128
+e = sfhe.Engine("hip", shard=("rccl", 0, 1, uid), **OPS_KW)
+ref = sfhe.Engine("hip", **OPS_KW)
+compare(ops_program(ref), ops_program(e))
+e.close(); ref.close()
+print("RCCL communicator OK")
+"""
+
+
 def test_rccl_single_rank_communicator(hip_lib):
-    uid = sfhe.comm_uid("hip")
-    assert uid is not None and len(uid) == 128
-    e = sfhe.Engine("hip", shard=("rccl", 0, 1, uid), **OPS_KW)
-    ref = sfhe.Engine("hip", **OPS_KW)
-    compare(ops_program(ref), ops_program(e))
+    """sfhe_comm_uid + sfhe_shard_rccl (ncclCommInitRank) on one rank, then the
+    op program through the RCCL-configured context.  Own process: RCCL's
+    threads and the HIP runtime are torn down with it."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = RCCL_SCRIPT.format(py=os.path.join(os.path.dirname(here), "sorting-fhe_amd", "python"), tests=here)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "RCCL communicator OK" in r.stdout
