@@ -431,7 +431,7 @@ __device__ __forceinline__ double fpReduce(double v, double q, double qinv) {
 
 template <bool INV, bool COL, int LE, int B>
 __device__ __forceinline__ void nttRoundFP(double* s, const NttTile& T, uint32_t S0, uint32_t k0, double q,
-                                           const double* w, const double* wq) {
+                                           const double* w, const double* wq, double qinv) {
     constexpr int M = 1 << B;
     constexpr int GPT = (1 << LE) / M;
     const uint32_t D = 1u << T.d;
@@ -462,7 +462,10 @@ __device__ __forceinline__ void nttRoundFP(double* s, const NttTile& T, uint32_t
 #pragma unroll
             for (int qd = 0; qd < (1 << t); ++qd) {
                 W[(1 << t) - 1 + qd] = w[tb + qd];
-                WQ[(1 << t) - 1 + qd] = wq[tb + qd];
+                // ROW twiddles come from HBM: form W/q here (half the bytes).  A
+                // last-bit difference from the table only moves the lazy
+                // quotient estimate by < 2^-6; outputs are canonical either way.
+                WQ[(1 << t) - 1 + qd] = COL ? wq[tb + qd] : W[(1 << t) - 1 + qd] * qinv;
             }
         }
         double v[M];
@@ -503,12 +506,12 @@ __device__ __forceinline__ void nttRoundFP(double* s, const NttTile& T, uint32_t
 
 template <bool INV, bool COL, int LE>
 __device__ __forceinline__ void nttRoundDynFP(int b, double* s, const NttTile& T, uint32_t S0, uint32_t k0,
-                                              double q, const double* w, const double* wq) {
+                                              double q, const double* w, const double* wq, double qinv) {
     if constexpr (LE >= 3) {
-        if (b == 3) return nttRoundFP<INV, COL, LE, 3>(s, T, S0, k0, q, w, wq);
+        if (b == 3) return nttRoundFP<INV, COL, LE, 3>(s, T, S0, k0, q, w, wq, qinv);
     }
-    if (b == 2) return nttRoundFP<INV, COL, LE, 2>(s, T, S0, k0, q, w, wq);
-    nttRoundFP<INV, COL, LE, 1>(s, T, S0, k0, q, w, wq);
+    if (b == 2) return nttRoundFP<INV, COL, LE, 2>(s, T, S0, k0, q, w, wq, qinv);
+    nttRoundFP<INV, COL, LE, 1>(s, T, S0, k0, q, w, wq, qinv);
 }
 
 
@@ -667,7 +670,8 @@ __global__ __launch_bounds__(kNttTile >> LE) void k_ntt(const RowGroup G, const 
         const int b = (int)min((uint32_t)LE, T.d - k0);
         if (fp)
             nttRoundDynFP<INV, COL, LE>(b, reinterpret_cast<double*>(s), T, S0, k0, (double)q,
-                                        reinterpret_cast<const double*>(rw), reinterpret_cast<const double*>(rx));
+                                        reinterpret_cast<const double*>(rw), reinterpret_cast<const double*>(rx),
+                                        qinvD[prime]);
         else
             nttRoundDyn<INV, COL, LE>(b, s, T, S0, k0, q, rw, rx);
         __syncthreads();
