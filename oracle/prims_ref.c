@@ -243,6 +243,11 @@ void sfp_lin_wsum(sfp_dev* d, uint64_t* out, const uint64_t* const* ins, const u
     })
 }
 
+void sfp_mac_plain2(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint64_t* const* a0,
+                    const uint64_t* const* a1, const uint64_t* const* b, uint32_t nin, sfp_limbs m) {
+    sfp_mac_plain(d, out0, a0, b, nin, m);
+    sfp_mac_plain(d, out1, a1, b, nin, m);
+}
 void sfp_mac_plain(sfp_dev* d, uint64_t* out, const uint64_t* const* a, const uint64_t* const* b,
                    uint32_t nin, sfp_limbs m) {
     LOOP_LIMBS({

@@ -1621,13 +1621,11 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMultAddPlain(
     for (size_t done = 0; done < a.size(); done += SFP_MAX_WSUM) {
         uint32_t take = (uint32_t)std::min<size_t>(SFP_MAX_WSUM, a.size() - done);
         if (done == 0) {
-            sfp_mac_plain(s->dev, t0, x0.data(), m.data(), take, st->qmap(ell));
-            sfp_mac_plain(s->dev, t1, x1.data(), m.data(), take, st->qmap(ell));
+            sfp_mac_plain2(s->dev, t0, t1, x0.data(), x1.data(), m.data(), take, st->qmap(ell));
         } else {
             auto part = s->alloc(2 * pw);
-            sfp_mac_plain(s->dev, part->ptr, x0.data() + done, m.data() + done, take, st->qmap(ell));
-            sfp_mac_plain(s->dev, part->ptr + pw, x1.data() + done, m.data() + done, take,
-                          st->qmap(ell));
+            sfp_mac_plain2(s->dev, part->ptr, part->ptr + pw, x0.data() + done, x1.data() + done,
+                           m.data() + done, take, st->qmap(ell));
             sfp_add(s->dev, t0, t0, part->ptr, st->qmap(ell));
             sfp_add(s->dev, t1, t1, part->ptr + pw, st->qmap(ell));
         }

@@ -897,6 +897,42 @@ __global__ __launch_bounds__(kThreads) void k_lin_wsum_multi(u64* __restrict__ o
     }
 }
 
+struct PtrList3 {
+    const u64* a[SFP_MAX_WSUM];
+    const u64* c[SFP_MAX_WSUM];
+    const u64* b[SFP_MAX_WSUM];
+};
+
+// out0 = sum_j a[j] * b[j], out1 = sum_j c[j] * b[j]: two coefficients per
+// thread, 16-byte loads, each plaintext row read once for both polynomials
+__global__ __launch_bounds__(kThreads) void k_mac_plain2(u64* __restrict__ out0, u64* __restrict__ out1,
+                                                         const PtrList3 L, uint32_t nin, sfp_limbs m,
+                                                         const sf_barrett* __restrict__ bar, uint32_t logn) {
+    const size_t pairs = ((size_t)m.count << logn) >> 1;
+    for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < pairs;
+         i += (size_t)gridDim.x * kThreads) {
+        const size_t e = 2 * i;
+        const sf_barrett B = loadBar(bar, primeOf(m, (uint32_t)(e >> logn)));
+        Acc x0{0, 0}, y0{0, 0}, x1{0, 0}, y1{0, 0};
+        for (uint32_t j = 0; j < nin; ++j) {
+            const ulonglong2 p = *reinterpret_cast<const ulonglong2*>(L.b[j] + e);
+            const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(L.a[j] + e);
+            const ulonglong2 c = *reinterpret_cast<const ulonglong2*>(L.c[j] + e);
+            macc(x0, a.x, p.x);
+            macc(y0, a.y, p.y);
+            macc(x1, c.x, p.x);
+            macc(y1, c.y, p.y);
+        }
+        ulonglong2 o0, o1;
+        o0.x = sf_reduce128_acc(x0.lo, x0.hi, &B);
+        o0.y = sf_reduce128_acc(y0.lo, y0.hi, &B);
+        o1.x = sf_reduce128_acc(x1.lo, x1.hi, &B);
+        o1.y = sf_reduce128_acc(y1.lo, y1.hi, &B);
+        *reinterpret_cast<ulonglong2*>(out0 + e) = o0;
+        *reinterpret_cast<ulonglong2*>(out1 + e) = o1;
+    }
+}
+
 __global__ __launch_bounds__(kThreads) void k_mac_plain(u64* __restrict__ out, PtrList2 ab,
                                                         uint32_t nin, sfp_limbs m,
                                                         const sf_barrett* __restrict__ bar,
@@ -1377,29 +1413,43 @@ __global__ __launch_bounds__(kThreads) void k_ks_inner(u64* __restrict__ acc0, u
                                                        const u64* __restrict__ fold0,
                                                        const u64* __restrict__ fold1, u64 foldK,
                                                        const sf_barrett* __restrict__ bar, uint32_t logn) {
+    // two coefficients per thread: 16-byte loads of every ext / key row
     const uint32_t ell = pm.split, NP = keyRows;
-    const size_t total = (size_t)pm.count << logn;
+    const size_t pairs = ((size_t)pm.count << logn) >> 1;
     const uint32_t n = 1u << logn;
-    for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < total;
+    for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < pairs;
          i += (size_t)gridDim.x * kThreads) {
-        const uint32_t t = (uint32_t)(i >> logn);
-        const uint32_t x = (uint32_t)(i & (n - 1));
+        const size_t e = 2 * i;
+        const uint32_t t = (uint32_t)(e >> logn);
+        const uint32_t x = (uint32_t)(e & (n - 1));
         const uint32_t kr = t < ell ? t : keyQ + (t - ell);
         const sf_barrett B = loadBar(bar, primeOf(pm, t));
-        Acc s0{0, 0}, s1{0, 0};
+        Acc s0{0, 0}, s0b{0, 0}, s1{0, 0}, s1b{0, 0};
         for (uint32_t j = 0; j < beta; ++j) {
-            const u64 e = ext[j * extStride + i];
-            const u64* kb = key + (size_t)j * 2 * NP * n;
-            const u64* ka = kb + (size_t)NP * n;
-            macc(s0, e, kb[((size_t)kr << logn) + x]);
-            macc(s1, e, ka[((size_t)kr << logn) + x]);
+            const ulonglong2 ev = *reinterpret_cast<const ulonglong2*>(ext + j * extStride + e);
+            const u64* kb = key + (size_t)j * 2 * NP * n + ((size_t)kr << logn) + x;
+            const ulonglong2 b2 = *reinterpret_cast<const ulonglong2*>(kb);
+            const ulonglong2 a2 = *reinterpret_cast<const ulonglong2*>(kb + (size_t)NP * n);
+            macc(s0, ev.x, b2.x);
+            macc(s0b, ev.y, b2.y);
+            macc(s1, ev.x, a2.x);
+            macc(s1b, ev.y, a2.y);
         }
         if (fold0 && t == ell - 1) {  // + P * d_l (sfp_ks_inner_fold)
-            macc(s0, fold0[i], foldK);
-            macc(s1, fold1[i], foldK);
+            const ulonglong2 f0 = *reinterpret_cast<const ulonglong2*>(fold0 + e);
+            const ulonglong2 f1 = *reinterpret_cast<const ulonglong2*>(fold1 + e);
+            macc(s0, f0.x, foldK);
+            macc(s0b, f0.y, foldK);
+            macc(s1, f1.x, foldK);
+            macc(s1b, f1.y, foldK);
         }
-        acc0[i] = sf_reduce128_acc(s0.lo, s0.hi, &B);
-        acc1[i] = sf_reduce128_acc(s1.lo, s1.hi, &B);
+        ulonglong2 o0, o1;
+        o0.x = sf_reduce128_acc(s0.lo, s0.hi, &B);
+        o0.y = sf_reduce128_acc(s0b.lo, s0b.hi, &B);
+        o1.x = sf_reduce128_acc(s1.lo, s1.hi, &B);
+        o1.y = sf_reduce128_acc(s1b.lo, s1b.hi, &B);
+        *reinterpret_cast<ulonglong2*>(acc0 + e) = o0;
+        *reinterpret_cast<ulonglong2*>(acc1 + e) = o1;
     }
 }
 
@@ -1986,6 +2036,26 @@ void sfp_lin_wsum_multi(sfp_dev* d, uint64_t* out, size_t outStride, size_t poly
     checkLaunch(d, "lin_wsum_multi");
 }
 
+void sfp_mac_plain2(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint64_t* const* a0,
+                    const uint64_t* const* a1, const uint64_t* const* b, uint32_t nin, sfp_limbs m) {
+    if (!m.count || !nin) return;
+    if (!limbsOk(d, m, "mac_plain2")) return;
+    if (nin > SFP_MAX_WSUM) {
+        record(d, "mac_plain2", hipErrorInvalidValue);
+        return;
+    }
+    PtrList3 L;
+    for (uint32_t j = 0; j < nin; ++j) {
+        L.a[j] = a0[j];
+        L.c[j] = a1[j];
+        L.b[j] = b[j];
+    }
+    const size_t total = (size_t)m.count * d->n;
+    hipLaunchKernelGGL(k_mac_plain2, dim3(ewGrid(total / 2)), dim3(kThreads), 0, d->st(), out0, out1, L, nin, m,
+                       d->bar, d->logn);
+    checkLaunch(d, "mac_plain2");
+}
+
 void sfp_mac_plain(sfp_dev* d, uint64_t* out, const uint64_t* const* a, const uint64_t* const* b,
                    uint32_t nin, sfp_limbs m) {
     if (!limbsOk(d, m, "mac_plain")) return;
@@ -2338,7 +2408,7 @@ void sfp_ks_inner_fold(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_
     }
     // reads beta ext rows + 2*beta key rows, writes 2 accumulator rows, per limb
     timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + 2.0), [&] {
-        hipLaunchKernelGGL(k_ks_inner, dim3(ewGrid(total)), dim3(kThreads), 0, d->st(), acc0, acc1, ext,
+        hipLaunchKernelGGL(k_ks_inner, dim3(ewGrid(total / 2)), dim3(kThreads), 0, d->st(), acc0, acc1, ext,
                            extStride, key, beta, sfp_limbs{ell + K, ell, Lq, 0, 1}, Lq, Lq + K, fold0, fold1,
                            foldK, d->bar, d->logn);
     });
@@ -2541,7 +2611,7 @@ void sfp_ks_inner_map(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t
     if (!pm.count || !limbsOk(d, pm, "ks_inner_map")) return;
     const size_t total = (size_t)pm.count * d->n;
     timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + 2.0), [&] {
-        hipLaunchKernelGGL(k_ks_inner, dim3(ewGrid(total)), dim3(kThreads), 0, d->st(), acc0, acc1, ext, extStride,
+        hipLaunchKernelGGL(k_ks_inner, dim3(ewGrid(total / 2)), dim3(kThreads), 0, d->st(), acc0, acc1, ext, extStride,
                            key, beta, pm, keyQ, keyRows, (const u64*)nullptr, (const u64*)nullptr, (u64)0, d->bar,
                            d->logn);
     });

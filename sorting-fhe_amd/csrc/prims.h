@@ -115,6 +115,10 @@ void sfp_lin_wsum_multi(sfp_dev* d, uint64_t* out, size_t out_stride, size_t pol
 // a, b: host arrays of device pointers.
 void sfp_mac_plain(sfp_dev* d, uint64_t* out, const uint64_t* const* a, const uint64_t* const* b,
                    uint32_t nin, sfp_limbs m);
+// Both polynomials of a ciphertext sum at once (each plaintext read once):
+// out0 = sum_j a0[j] * b[j], out1 = sum_j a1[j] * b[j]  (nin <= SFP_MAX_WSUM).
+void sfp_mac_plain2(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint64_t* const* a0,
+                    const uint64_t* const* a1, const uint64_t* const* b, uint32_t nin, sfp_limbs m);
 
 // ---- automorphism ----------------------------------------------------------
 // out = sigma_g(in) in the evaluation domain (g odd, < 2n); out != in.
