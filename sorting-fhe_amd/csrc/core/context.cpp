@@ -259,6 +259,22 @@ class SfheInternal {
     }
 
     static sfp_limbs Q(uint32_t ell) { return sfp_limbs{ell, ell, 0}; }
+    // both polynomials of ciphertexts laid out [c0 rows][c1 rows] in one launch:
+    // rows [r, 2r) repeat the primes of rows [0, r)
+    static bool packed(const SfheContextState* s, std::initializer_list<const uint64_t*> c0s,
+                       std::initializer_list<const uint64_t*> c1s, uint32_t level) {
+        const size_t pw = s->polyWords(level);
+        auto a = c0s.begin();
+        for (auto b = c1s.begin(); b != c1s.end(); ++a, ++b)
+            if (*b != *a + pw) return false;
+        return true;
+    }
+    static sfp_limbs both(const SfheContextState* s, uint32_t ell) {
+        sfp_limbs m = s->qmap(ell);
+        m.count *= 2;
+        m.pbase = m.base;
+        return m;
+    }
     static sfp_limbs Range(uint32_t lo, uint32_t cnt) { return sfp_limbs{cnt, 0, lo}; }
 
     static Ct newCt(CC* cc, uint32_t level, uint32_t slots) {
@@ -1379,8 +1395,12 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalAdd(const Ciphertext<DCRTP
     SfheInternal::align(this, a, b);
     auto out = SfheInternal::newCt(this, a->level, std::max(a->slots, b->slots));
     const uint32_t ell = st->ellOf(a->level);
-    sfp_add(st->dev, out->c0, a->c0, b->c0, st->qmap(ell));
-    sfp_add(st->dev, out->c1, a->c1, b->c1, st->qmap(ell));
+    if (SfheInternal::packed(st.get(), {out->c0, a->c0, b->c0}, {out->c1, a->c1, b->c1}, a->level)) {
+        sfp_add(st->dev, out->c0, a->c0, b->c0, SfheInternal::both(st.get(), ell));
+    } else {
+        sfp_add(st->dev, out->c0, a->c0, b->c0, st->qmap(ell));
+        sfp_add(st->dev, out->c1, a->c1, b->c1, st->qmap(ell));
+    }
     st->stats.add++;
     st->countBytes(6.0 * ell * st->n * 8);
     return SfheInternal::traced(this, out, "EvalAdd");
@@ -1399,8 +1419,12 @@ void CryptoContextImpl<DCRTPoly>::EvalAddInPlace(Ciphertext<DCRTPoly>& a,
         return;
     }
     const uint32_t ell = st->ellOf(a->level);
-    sfp_add(st->dev, a->c0, a->c0, b->c0, st->qmap(ell));
-    sfp_add(st->dev, a->c1, a->c1, b->c1, st->qmap(ell));
+    if (SfheInternal::packed(st.get(), {a->c0, b->c0}, {a->c1, b->c1}, a->level)) {
+        sfp_add(st->dev, a->c0, a->c0, b->c0, SfheInternal::both(st.get(), ell));
+    } else {
+        sfp_add(st->dev, a->c0, a->c0, b->c0, st->qmap(ell));
+        sfp_add(st->dev, a->c1, a->c1, b->c1, st->qmap(ell));
+    }
     st->wrote(a->buf.get());
     a->slots = std::max(a->slots, b->slots);
     st->stats.add++;
@@ -1414,8 +1438,14 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalAdd(const Ciphertext<DCRTP
     const uint32_t ell = st->ellOf(a->level);
     auto out = SfheInternal::newCt(this, a->level, a->slots);
     auto k = SfheInternal::constResidues(st.get(), c * a->scale, ell);
-    sfp_add_const(st->dev, out->c0, a->c0, k.data(), st->qmap(ell));
-    sfp_d2d(st->dev, out->c1, a->c1, st->polyWords(a->level) * 8);
+    if (2 * k.size() <= SFP_MAX_LIMBS &&
+        SfheInternal::packed(st.get(), {out->c0, a->c0}, {out->c1, a->c1}, a->level)) {
+        k.resize(2 * k.size(), 0);  // c1 rows: + 0, i.e. the copy, in the same launch
+        sfp_add_const(st->dev, out->c0, a->c0, k.data(), SfheInternal::both(st.get(), ell));
+    } else {
+        sfp_add_const(st->dev, out->c0, a->c0, k.data(), st->qmap(ell));
+        sfp_d2d(st->dev, out->c1, a->c1, st->polyWords(a->level) * 8);
+    }
     st->stats.add++;
     st->countBytes(4.0 * ell * st->n * 8);
     return SfheInternal::traced(this, out, "EvalAdd");
@@ -1451,8 +1481,12 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalSub(const Ciphertext<DCRTP
     SfheInternal::align(this, a, b);
     auto out = SfheInternal::newCt(this, a->level, std::max(a->slots, b->slots));
     const uint32_t ell = st->ellOf(a->level);
-    sfp_sub(st->dev, out->c0, a->c0, b->c0, st->qmap(ell));
-    sfp_sub(st->dev, out->c1, a->c1, b->c1, st->qmap(ell));
+    if (SfheInternal::packed(st.get(), {out->c0, a->c0, b->c0}, {out->c1, a->c1, b->c1}, a->level)) {
+        sfp_sub(st->dev, out->c0, a->c0, b->c0, SfheInternal::both(st.get(), ell));
+    } else {
+        sfp_sub(st->dev, out->c0, a->c0, b->c0, st->qmap(ell));
+        sfp_sub(st->dev, out->c1, a->c1, b->c1, st->qmap(ell));
+    }
     st->stats.add++;
     st->countBytes(6.0 * ell * st->n * 8);
     return SfheInternal::traced(this, out, "EvalSub");
@@ -1468,8 +1502,12 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalNegate(const Ciphertext<DC
     SfheInternal::deps(st.get(), {&a});
     const uint32_t ell = st->ellOf(a->level);
     auto out = SfheInternal::newCt(this, a->level, a->slots);
-    sfp_neg(st->dev, out->c0, a->c0, st->qmap(ell));
-    sfp_neg(st->dev, out->c1, a->c1, st->qmap(ell));
+    if (SfheInternal::packed(st.get(), {out->c0, a->c0}, {out->c1, a->c1}, a->level)) {
+        sfp_neg(st->dev, out->c0, a->c0, SfheInternal::both(st.get(), ell));
+    } else {
+        sfp_neg(st->dev, out->c0, a->c0, st->qmap(ell));
+        sfp_neg(st->dev, out->c1, a->c1, st->qmap(ell));
+    }
     st->countBytes(4.0 * ell * st->n * 8);
     return SfheInternal::traced(this, out, "EvalNegate");
 }
