@@ -174,6 +174,8 @@ def main(argv=None):
     ap.add_argument("--workload", default="directsort_n256_2e16", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-seconds", type=float, default=15.0)
+    ap.add_argument("--trials", type=int, default=10,
+                    help="per-sort trials after the timed region (median/min/max, pure and as-test)")
     ap.add_argument("--shard", choices=("rccl", "host"), default=None,
                     help="limb-shard one sort over the ranks instead of running replicas")
     args = ap.parse_args(argv)
@@ -218,6 +220,32 @@ def main(argv=None):
     dt = timed_steps(step, eng.sync, world, args.steps, args.warmup, start_counters)
     stats = eng.op_stats()
     kt = {fam: eng.kernel_timing_read(fam) for fam in families}
+    for fam in families:
+        eng.kernel_timing(fam, 0)
+
+    # per-sort trials, "pure" (plain Encryption, SortNBenchmark)
+    # and "as-test" (DebugEncryption: the three PRINT_PT decrypts inside sort(),
+    # DirectSortTest.cpp:129-136), median / min / max like run_experiments.sh
+    def trial_ms(srt, k):
+        ts = []
+        for _ in range(k):
+            eng.sync()
+            t0 = time.perf_counter()
+            o = srt.sort(ct, *cfg)
+            eng.sync()
+            ts.append((time.perf_counter() - t0) * 1e3)
+            del o
+        return ts
+
+    def stats3(ts):
+        import statistics
+        return {"median": statistics.median(ts), "min": min(ts), "max": max(ts)} if ts else None
+    trials = None
+    if args.trials > 0:
+        pure = trial_ms(sorter, args.trials)
+        as_test = trial_ms(eng.sorter(N, debug=True), args.trials)
+        trials = {"count": args.trials, "pure_ms": stats3(pure), "as_test_ms": stats3(as_test),
+                  "note": "each trial one sort with a device sync on both sides (rank-local, after the timed region)"}
 
     # dominant timed family: estimated total time = timed ms * launches / timed
     def est_ms(k):
@@ -269,6 +297,7 @@ def main(argv=None):
         "algorithmic_gb_per_sort": stats["algo_bytes"] / args.steps / 1e9,
         "roofline": roofline,
         "kernels": kernels,
+        "trials": trials,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

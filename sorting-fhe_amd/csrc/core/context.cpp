@@ -161,12 +161,20 @@ DeviceBufferPtr SfheContextState::alloc(size_t words) {
     uint64_t* p = nullptr;
     {
         std::lock_guard<std::mutex> g(poolMu);
-        auto& fl = freeList[lane];
-        auto it = fl.find(words);
-        if (it != fl.end() && !it->second.empty()) {
+        auto take = [&](std::map<size_t, std::vector<uint64_t*>>& fl) {
+            auto it = fl.find(words);
+            if (it == fl.end() || it->second.empty()) return false;
             p = it->second.back();
             it->second.pop_back();
-        }
+            return true;
+        };
+        // own lane first; then blocks this lane is already ordered after: the
+        // pre-fork pool (every lane of a region waited for lane 0 at the fork),
+        // and in a dataflow sub-region the parent's free list (all of it freed
+        // before the helpers waited for the parent)
+        if (!take(freeList[lane]) && !(forkedLanes && take(forkPool)) && dataflow && dataflowParent >= 0 &&
+            lane != dataflowParent)
+            take(freeList[dataflowParent]);
     }
     if (!p) {
         p = (uint64_t*)sfp_alloc(dev, words * 8);
@@ -212,14 +220,16 @@ void SfheContextState::wrote(DeviceBuffer* b) {
 void SfheContextState::releaseAll() {
     std::lock_guard<std::mutex> g(poolMu);
     sfp_sync(dev);
-    for (auto& fl : freeList) {
+    auto drop = [&](std::map<size_t, std::vector<uint64_t*>>& fl) {
         for (auto& kv : fl)
             for (auto* p : kv.second) {
                 sfp_free(dev, p);
                 poolBytes -= kv.first * 8;
             }
         fl.clear();
-    }
+    };
+    for (auto& fl : freeList) drop(fl);
+    drop(forkPool);
 }
 
 // ============================================================================
@@ -1059,6 +1069,12 @@ void CryptoContextImpl<DCRTPoly>::ForkLanes(int count) {
     s->lane = 0;
     s->setMyLane(0);
     for (int i = 1; i < count; ++i) s->laneWait(i, 0);
+    {
+        std::lock_guard<std::mutex> pg(s->poolMu);
+        for (auto& kv : s->freeList[0])
+            for (auto* p : kv.second) s->forkPool[kv.first].push_back(p);
+        s->freeList[0].clear();
+    }
     s->forkedLanes = count;
     s->region = ++s->regionCount;
 }
@@ -1068,6 +1084,7 @@ std::vector<int> CryptoContextImpl<DCRTPoly>::ForkHelpers() {
     SfheContextState* s = st.get();
     std::vector<int> lanes{s->lane};
     if (!s->dataflow) {
+        s->dataflowParent = s->lane;
         // helpers: lanes that are not primaries of an open batch region
         const int first = s->forkedLanes ? s->forkedLanes : 0;
         for (int l = first; l < sfp_lanes(s->dev); ++l)
@@ -1093,6 +1110,13 @@ void CryptoContextImpl<DCRTPoly>::JoinHelpers(const std::vector<int>& lanes) {
         std::lock_guard<std::mutex> pg(s->poolMu);
         for (auto& e : s->dataflowFree) s->freeList[parent][e.first].push_back(e.second);
         s->dataflowFree.clear();
+        // helpers' own lists: ordered behind the parent after the waits above
+        for (size_t i = 1; i < lanes.size(); ++i) {
+            for (auto& kv : s->freeList[lanes[i]])
+                for (auto* p : kv.second) s->freeList[parent][kv.first].push_back(p);
+            s->freeList[lanes[i]].clear();
+        }
+        s->dataflowParent = -1;
     }
 }
 
@@ -1121,6 +1145,9 @@ void CryptoContextImpl<DCRTPoly>::JoinLanes() {
     }
     for (auto& e : s->deferredFree) s->freeList[0][e.first].push_back(e.second);
     s->deferredFree.clear();
+    for (auto& kv : s->forkPool)
+        for (auto* p : kv.second) s->freeList[0][kv.first].push_back(p);
+    s->forkPool.clear();
     s->lane = 0;
     s->setMyLane(0);
     s->forkedLanes = 0;

@@ -71,6 +71,11 @@ struct SfheContextState {
     // ordered after it (same lane, or any lane after a join)
     std::map<size_t, std::vector<uint64_t*>> freeList[SFP_MAX_LANES];
     std::vector<std::pair<size_t, uint64_t*>> deferredFree;  // cross-lane frees inside a region
+    // lane 0's free blocks at ForkLanes: every lane of the region is ordered
+    // after them, so any lane may reuse them (without this, blocks a lane
+    // allocates migrate to lane 0 at every join and the pool grows per region)
+    std::map<size_t, std::vector<uint64_t*>> forkPool;
+    int dataflowParent = -1;  // helpers of a dataflow sub-region may reuse its free blocks
     int lane = 0;          // lane new work goes to
     int forkedLanes = 0;   // > 0 while a fork/join region is open
     uint64_t region = 0;   // id of the open region (0: none)

@@ -858,7 +858,8 @@ __global__ __launch_bounds__(kThreads) void k_lin_wsum_multi(u64* __restrict__ o
                                                              const u64* __restrict__ k, uint32_t nin,
                                                              uint32_t nout, sfp_limbs m,
                                                              const sf_barrett* __restrict__ bar,
-                                                             uint32_t logn) {
+                                                             uint32_t logn, const double* __restrict__ qinvD,
+                                                             int useFp) {
     __shared__ u64 sk[kWsumChunk * SFP_MAX_WSUM];
     const uint32_t limb = blockIdx.y;
     const uint32_t o0 = blockIdx.z * kWsumChunk;
@@ -872,6 +873,34 @@ __global__ __launch_bounds__(kThreads) void k_lin_wsum_multi(u64* __restrict__ o
     const uint32_t x = blockIdx.x * kThreads + threadIdx.x;
     if (x >= n) return;
     const size_t off = ((size_t)limb << logn) + x;
+    const uint32_t prime = primeOf(m, limb);
+    const u64 qq = bar[prime].q;
+    if (useFp && qq < kFpPrimeBound) {  // uniform per block: FP64 products (fpMulMod), exact
+        const double qd = (double)qq, qi = qinvD[prime];
+        double f0[kWsumChunk], f1[kWsumChunk];
+#pragma unroll
+        for (int o = 0; o < kWsumChunk; ++o) f0[o] = f1[o] = 0.0;
+        for (uint32_t j = 0; j < nin; ++j) {  // |sum| < nin * 2q < 2^50
+            const double v0 = (double)ins.a[j][off], v1 = (double)ins.b[j][off];
+#pragma unroll
+            for (int o = 0; o < kWsumChunk; ++o) {
+                if ((uint32_t)o < oc) {
+                    const double w = (double)sk[o * SFP_MAX_WSUM + j], wq = w * qi;
+                    f0[o] += fpMulMod(v0, w, wq, qd);
+                    f1[o] += fpMulMod(v1, w, wq, qd);
+                }
+            }
+        }
+#pragma unroll
+        for (int o = 0; o < kWsumChunk; ++o) {
+            if ((uint32_t)o < oc) {
+                u64* dst = out + (size_t)(o0 + o) * outStride + off;
+                dst[0] = (u64)fpReduce(f0[o], qd, qi);
+                dst[polyStride] = (u64)fpReduce(f1[o], qd, qi);
+            }
+        }
+        return;
+    }
     Acc a0[kWsumChunk], a1[kWsumChunk];
 #pragma unroll
     for (int o = 0; o < kWsumChunk; ++o) a0[o] = a1[o] = Acc{0, 0};
@@ -2032,7 +2061,7 @@ void sfp_lin_wsum_multi(sfp_dev* d, uint64_t* out, size_t outStride, size_t poly
     const u64* dk = (const u64*)ringPut(d, k, (size_t)nout * nin * m.count * 8);
     const dim3 g(d->n / kThreads, m.count, (nout + kWsumChunk - 1) / kWsumChunk);
     hipLaunchKernelGGL(k_lin_wsum_multi, g, dim3(kThreads), 0, d->st(), out, outStride, polyStride, pl, dk,
-                       nin, nout, m, d->bar, d->logn);
+                       nin, nout, m, d->bar, d->logn, d->qinvD, (int)nttFp());
     checkLaunch(d, "lin_wsum_multi");
 }
 
