@@ -807,20 +807,30 @@ __global__ __launch_bounds__(kThreads) void k_tensor(u64* __restrict__ d0, u64* 
                                                      const u64* __restrict__ a1, const u64* __restrict__ b0,
                                                      const u64* __restrict__ b1, sfp_limbs m,
                                                      const sf_barrett* __restrict__ bar, uint32_t logn) {
-    const size_t total = (size_t)m.count << logn;
-    for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < total;
+    // two coefficients per thread (16-byte loads and stores)
+    const size_t pairs = ((size_t)m.count << logn) >> 1;
+    for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < pairs;
          i += (size_t)gridDim.x * kThreads) {
-        const sf_barrett B = loadBar(bar, primeOf(m, (uint32_t)(i >> logn)));
-        u64 x0 = a0[i], x1 = a1[i], y0 = b0[i], y1 = b1[i];
-        Acc t{0, 0};
-        macc(t, x0, y1);
-        macc(t, x1, y0);
-        u64 r0 = bmul(x0, y0, B);
-        u64 r1 = sf_reduce128_acc(t.lo, t.hi, &B);
-        u64 r2 = bmul(x1, y1, B);
-        d0[i] = r0;
-        d1[i] = r1;
-        d2[i] = r2;
+        const sf_barrett B = loadBar(bar, primeOf(m, (uint32_t)((2 * i) >> logn)));
+        const ulonglong2 x0 = reinterpret_cast<const ulonglong2*>(a0)[i];
+        const ulonglong2 x1 = reinterpret_cast<const ulonglong2*>(a1)[i];
+        const ulonglong2 y0 = reinterpret_cast<const ulonglong2*>(b0)[i];
+        const ulonglong2 y1 = reinterpret_cast<const ulonglong2*>(b1)[i];
+        Acc t{0, 0}, u{0, 0};
+        macc(t, x0.x, y1.x);
+        macc(t, x1.x, y0.x);
+        macc(u, x0.y, y1.y);
+        macc(u, x1.y, y0.y);
+        ulonglong2 r0, r1, r2;
+        r0.x = bmul(x0.x, y0.x, B);
+        r0.y = bmul(x0.y, y0.y, B);
+        r1.x = sf_reduce128_acc(t.lo, t.hi, &B);
+        r1.y = sf_reduce128_acc(u.lo, u.hi, &B);
+        r2.x = bmul(x1.x, y1.x, B);
+        r2.y = bmul(x1.y, y1.y, B);
+        reinterpret_cast<ulonglong2*>(d0)[i] = r0;
+        reinterpret_cast<ulonglong2*>(d1)[i] = r1;
+        reinterpret_cast<ulonglong2*>(d2)[i] = r2;
     }
 }
 
@@ -2024,7 +2034,7 @@ void sfp_tensor(sfp_dev* d, uint64_t* d0, uint64_t* d1, uint64_t* d2, const uint
                 const uint64_t* a1, const uint64_t* b0, const uint64_t* b1, sfp_limbs m) {
     if (!limbsOk(d, m, "tensor")) return;
     const size_t total = (size_t)m.count * d->n;
-    hipLaunchKernelGGL(k_tensor, dim3(ewGrid(total)), dim3(kThreads), 0, d->st(), d0, d1, d2, a0, a1,
+    hipLaunchKernelGGL(k_tensor, dim3(ewGrid(total / 2)), dim3(kThreads), 0, d->st(), d0, d1, d2, a0, a1,
                        b0, b1, m, d->bar, d->logn);
     checkLaunch(d, "tensor");
 }
