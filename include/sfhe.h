@@ -90,6 +90,8 @@ int sfhe_sync(sfhe_ctx* c);
 /* counts[9]: keyswitch, rescale, tensor, ptmult, constmult, add, automorph,
  * ntt_limbs, wsum_terms; bytes: algorithmic HBM bytes (SURVEY §8(d) model). */
 int sfhe_op_stats(sfhe_ctx* c, uint64_t* counts, double* bytes, int reset);
+/* Device memory held by the context's buffer pool (live and free blocks). */
+int sfhe_pool_bytes(sfhe_ctx* c, uint64_t* bytes);
 /* Live kernel timing (bench roofline; no reference counterpart): kernel
  * families SFHE_KFAM_*; every `period`-th launch of the family is bracketed
  * by HIP events on the context's stream (period 0 = off; resets counters).

@@ -457,6 +457,12 @@ int sfhe_context_primes(sfhe_ctx* c, uint64_t* out, size_t cap, size_t* count) {
     return SFHE_OK;
 }
 
+int sfhe_pool_bytes(sfhe_ctx* c, uint64_t* bytes) {
+    REQUIRE(c && bytes, "null argument");
+    *bytes = c->cc->GetOpStats().pool_bytes;
+    return SFHE_OK;
+}
+
 // ---- limb sharding ----
 int sfhe_comm_uid(uint8_t uid[128]) {
     REQUIRE(uid, "null argument");

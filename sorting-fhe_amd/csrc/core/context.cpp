@@ -1164,7 +1164,10 @@ void CryptoContextImpl<DCRTPoly>::SetPlaintextCache(bool on) {
 }
 
 CryptoContextImpl<DCRTPoly>::OpStats CryptoContextImpl<DCRTPoly>::GetOpStats() const {
-    return st->stats;
+    OpStats o = st->stats;
+    std::lock_guard<std::mutex> g(st->poolMu);
+    o.pool_bytes = st->poolBytes;
+    return o;
 }
 void CryptoContextImpl<DCRTPoly>::ResetOpStats() { st->stats = OpStats(); }
 

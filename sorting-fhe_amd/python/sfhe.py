@@ -34,7 +34,7 @@ ABI_SYMBOLS = [
     "sfhe_direct_sort_params", "sfhe_doubled_sinc_coeffs", "sfhe_sorter_create",
     "sfhe_sorter_destroy", "sfhe_sorter_sort", "sfhe_sorter_rank", "sfhe_sorter_place",
     "sfhe_decompose", "sfhe_kernel_timing", "sfhe_kernel_timing_read",
-    "sfhe_comm_uid", "sfhe_shard_rccl", "sfhe_shard_host",
+    "sfhe_comm_uid", "sfhe_shard_rccl", "sfhe_shard_host", "sfhe_pool_bytes",
 ]
 
 
@@ -114,6 +114,7 @@ _SIGS = {
     "sfhe_kernel_timing_read": (C.c_int, [_VP, _U32, _PU64, _PU64, _PD, _PD]),
     "sfhe_decompose": (C.c_int, [_U32, _PI32, _SZ, C.c_int32, C.c_int32, C.c_int, _PI32, _PI32, _SZ, _PSZ]),
     "sfhe_comm_uid": (C.c_int, [_VP]),
+    "sfhe_pool_bytes": (C.c_int, [_VP, _PU64]),
     "sfhe_shard_rccl": (C.c_int, [_VP, C.c_int, C.c_int, _VP]),
     "sfhe_shard_host": (C.c_int, [_VP, C.c_int, C.c_int, _AG, _BC, _VP]),
 }
@@ -259,6 +260,11 @@ class Engine:
         d = dict(zip(keys, list(c)))
         d["algo_bytes"] = b.value
         return d
+
+    def pool_bytes(self) -> int:
+        v = C.c_uint64()
+        self._chk(self.lib.sfhe_pool_bytes(self.ctx, C.byref(v)))
+        return v.value
 
     KFAM = {"ntt": 0, "conv": 1, "ks_inner": 2}
 
