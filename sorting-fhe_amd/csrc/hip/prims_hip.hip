@@ -275,9 +275,14 @@ static unsigned gridFor(size_t work, unsigned perBlock) {
 constexpr int kNttTile = SFHE_NTT_TILE;         // words per tile (one block)
 constexpr int kNttRows = kNttTile / 256;        // ROW pass: whole rows per tile
 // LE = stages per register round (2^LE words per thread, kNttTile >> LE
-// threads).  Launches of few rows are latency-bound and run LE = 2 (twice the
-// waves per tile); larger ones run LE = 3 (fewer rounds and barriers).
-constexpr int kNttSmallRows = 12;
+// threads).  Launches below kNttSmallRows rows run LE = 2 (twice the waves per
+// tile), larger ones LE = 3 (fewer rounds and barriers).  Measured on the
+// sort (N=256 @ 2^16): thresholds 6 / 12 / 24 / 36 / all rows gave 64.6 / 63.8 /
+// 63.3 / 62.5 / 62.2 ms, so every launch takes LE = 2 by default.
+#ifndef SFHE_NTT_SMALL_ROWS
+#define SFHE_NTT_SMALL_ROWS 4096
+#endif
+constexpr int kNttSmallRows = SFHE_NTT_SMALL_ROWS;
 
 __device__ __forceinline__ uint32_t ldsSw(uint32_t e) {
     const uint32_t x = e >> 5;

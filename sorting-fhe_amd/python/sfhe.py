@@ -123,7 +123,8 @@ _libs: dict = {}
 
 
 def lib_path(backend: str = "hip") -> str:
-    return PRODUCT_LIB if backend == "hip" else ORACLE_LIB
+    # SFHE_PRODUCT_LIB: an alternative HIP build (tools: kernel-variant sweeps)
+    return os.environ.get("SFHE_PRODUCT_LIB", PRODUCT_LIB) if backend == "hip" else ORACLE_LIB
 
 
 def load(backend: str = "hip"):
