@@ -829,8 +829,12 @@ class SfheInternal {
         SfheContextState* s = cc->st.get();
         Ct out = newCt(cc, a->level, a->slots);
         size_t bytes = s->polyWords(a->level) * 8;
-        sfp_d2d(s->dev, out->c0, a->c0, bytes);
-        sfp_d2d(s->dev, out->c1, a->c1, bytes);
+        if (a->c1 == a->c0 + s->polyWords(a->level)) {  // [c0][c1] packed: one copy
+            sfp_d2d(s->dev, out->c0, a->c0, 2 * bytes);
+        } else {
+            sfp_d2d(s->dev, out->c0, a->c0, bytes);
+            sfp_d2d(s->dev, out->c1, a->c1, bytes);
+        }
         return out;
     }
     // make `a` exclusively owned before an in-place update
