@@ -5,10 +5,13 @@ bit -- every op at W = 2, 3 and a whole DirectSort<8> at W = 2.  The RCCL
 transport is exercised by the communicator set-up (a one-rank communicator;
 RCCL does not place two ranks on one GPU) and by bench.py --shard on a node.
 """
+import os
+
 import numpy as np
 import pytest
 
 import sfhe
+from oracle import slotsim
 from test_shard import OPS_KW, compare, ops_program, sort_program
 
 pytestmark = pytest.mark.gpu
@@ -35,10 +38,26 @@ def test_sharded_sort_bitexact_hip(hip_lib):
     assert np.array_equal(ref["sort"], ora["sort"])
 
 
+@pytest.mark.skipif(not os.environ.get("SFHE_SHARD_LARGE"),
+                    reason="open issue (DESIGN.md §6): intermittent host segfault inside sort() with 3-4 "
+                           "thread ranks on one GPU; set SFHE_SHARD_LARGE=1 to run")
+@pytest.mark.parametrize("N,logn,world", [(64, 15, 3), (128, 16, 4)])
+def test_sharded_sort_large_bitexact_hip(hip_lib, N, logn, world):
+    """Larger rings and limb counts (31 Q limbs at N=128), more ranks."""
+    depth, rots = sfhe.direct_sort_params(N, "hip")
+    kw = dict(mult_depth=depth, ring_dim=1 << logn, batch_size=N, rotations=rots, seed=4099)
+    ref = sort_program(sfhe.Engine("hip", **kw), N)
+    assert np.max(np.abs(ref["dec"][:N] - np.sort(slotsim.input_vector(N)))) < 0.01
+    outs = sfhe.run_sharded_threads("hip", world, lambda e: sort_program(e, N), **kw)
+    for r in range(world):
+        compare(ref, outs[r])
+
+
 RCCL_SCRIPT = r"""
 import sys
 sys.path.insert(0, {py!r}); sys.path.insert(0, {tests!r})
 import sfhe
+from oracle import slotsim
 from test_shard import OPS_KW, compare, ops_program
 uid = sfhe.comm_uid("hip")
 assert uid is not None and len(uid) == 128
