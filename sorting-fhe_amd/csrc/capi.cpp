@@ -2,6 +2,7 @@
 #include <cstring>
 #include <iostream>
 #include <memory>
+#include <mutex>
 #include <sstream>
 #include <streambuf>
 #include <string>
@@ -36,15 +37,27 @@ struct NullBuf : std::streambuf {
     int overflow(int c) override { return c; }
 };
 
-// silences std::cout while alive (reference prints inside sort())
+// silences std::cout while alive (reference prints inside sort()).  Contexts
+// may sort concurrently from several threads (one per lane or per shard rank),
+// so the swap is reference-counted under a lock with one shared null buffer:
+// a per-object buffer restored out of order would leave std::cout pointing at
+// a destroyed stack object.
+std::mutex g_quietMu;
+int g_quietDepth = 0;
+std::streambuf* g_quietOld = nullptr;
+NullBuf g_nullBuf;
+
 struct Quiet {
-    std::streambuf* old = nullptr;
-    NullBuf nb;
-    explicit Quiet(bool on) {
-        if (on) old = std::cout.rdbuf(&nb);
+    bool on;
+    explicit Quiet(bool q) : on(q) {
+        if (!on) return;
+        std::lock_guard<std::mutex> g(g_quietMu);
+        if (g_quietDepth++ == 0) g_quietOld = std::cout.rdbuf(&g_nullBuf);
     }
     ~Quiet() {
-        if (old) std::cout.rdbuf(old);
+        if (!on) return;
+        std::lock_guard<std::mutex> g(g_quietMu);
+        if (--g_quietDepth == 0) std::cout.rdbuf(g_quietOld);
     }
 };
 

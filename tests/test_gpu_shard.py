@@ -5,8 +5,6 @@ bit -- every op at W = 2, 3 and a whole DirectSort<8> at W = 2.  The RCCL
 transport is exercised by the communicator set-up (a one-rank communicator;
 RCCL does not place two ranks on one GPU) and by bench.py --shard on a node.
 """
-import os
-
 import numpy as np
 import pytest
 
@@ -38,9 +36,6 @@ def test_sharded_sort_bitexact_hip(hip_lib):
     assert np.array_equal(ref["sort"], ora["sort"])
 
 
-@pytest.mark.skipif(not os.environ.get("SFHE_SHARD_LARGE"),
-                    reason="open issue (DESIGN.md §6): intermittent host segfault inside sort() with 3-4 "
-                           "thread ranks on one GPU; set SFHE_SHARD_LARGE=1 to run")
 @pytest.mark.parametrize("N,logn,world", [(64, 15, 3), (128, 16, 4)])
 def test_sharded_sort_large_bitexact_hip(hip_lib, N, logn, world):
     """Larger rings and limb counts (31 Q limbs at N=128), more ranks."""
