@@ -1366,23 +1366,36 @@ void CryptoContextImpl<DCRTPoly>::Decrypt(const PrivateKey<DCRTPoly>& sk,
     if (err) SFHE_THROW(std::string("device error: ") + err);
     std::vector<double> c(s->n);
     const u64 q0 = s->primes[0];
+    // the decoder reads coefficients i*gap and n/2 + i*gap only (sparse
+    // packing): reconstruct just those (all of them when slots = n/2)
+    const uint32_t gap = (s->n / 2) / std::max<uint32_t>(1, ct->slots);
+    auto each = [&](auto&& f) {
+        for (uint32_t j = 0; j < s->n / 2; j += gap) {
+            f(j);
+            f(s->n / 2 + j);
+        }
+    };
     if (nl == 1) {
-        for (uint32_t i = 0; i < s->n; ++i) {
+        each([&](uint32_t i) {
             u64 x = h[i];
             double v = x > q0 / 2 ? -(double)(q0 - x) : (double)x;
             c[i] = v / ct->scale;
-        }
+        });
     } else {
         const u64 q1 = s->primes[1];
         const u64 q0inv = invmod(q0 % q1, q1);
+        const u64 q0invS = (u64)(((u128)q0inv << 64) / q1);  // Shoup companion
         const u128 Q = (u128)q0 * q1;
-        for (uint32_t i = 0; i < s->n; ++i) {
-            u64 a0 = h[i], a1 = h[s->n + i];
-            u64 d = (a1 + q1 - a0 % q1) % q1;
-            u128 x = (u128)a0 + (u128)q0 * mulmod(d, q0inv, q1);
+        each([&](uint32_t i) {
+            const u64 a0 = h[i], a1 = h[s->n + i];
+            const u64 r0 = a0 % q1;
+            const u64 d = a1 >= r0 ? a1 - r0 : a1 + q1 - r0;
+            u64 m = d * q0inv - (u64)(((u128)d * q0invS) >> 64) * q1;  // d * q0^-1 mod q1, in [0, 2 q1)
+            if (m >= q1) m -= q1;
+            u128 x = (u128)a0 + (u128)q0 * m;
             double v = x > Q / 2 ? -(double)(Q - x) : (double)x;
             c[i] = v / ct->scale;
-        }
+        });
     }
     std::vector<std::complex<double>> vals;
     ckks_decode(c, ct->slots, s->n, vals);
