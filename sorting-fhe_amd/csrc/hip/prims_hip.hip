@@ -1031,7 +1031,10 @@ constexpr int kMaxConvSrc = 32;
 //   y_i = [s_i * inv_i]_{q_i};  out_t = sum_i y_i * mod[i][t]  mod p_t
 // centred: subtract prod(q_i) mod p_t once per y_i > q_i/2 (value in
 // (-Q/2, Q/2] instead of [0, Q)).
-constexpr int kConvChunk = 12;
+#ifndef SFHE_CONV_CHUNK
+#define SFHE_CONV_CHUNK 32  // targets per block; sweep on the sort: 6-16 ~ 12, 24 -0.6 ms, 32 -1.0 ms, 48 +1.1 ms
+#endif
+constexpr int kConvChunk = SFHE_CONV_CHUNK;
 constexpr int kMaxConvJobs = 16;
 constexpr int kMaxConvBig = 2;  // 60-bit sources the FP64 form splits in two
 struct ConvJob {
