@@ -2182,8 +2182,10 @@ static void rescaleCore(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t 
     RowGroup A = rowsOf(npoly, 1, sfp_limbs{1, 0, dropPrime, 0});
     A.src = RowPtr{in + (size_t)cnt * n, (long long)inStride, 0};
     A.dst = RowPtr{last, (long long)n, 0};
-    // per-call multipliers go through the upload ring (stream-ordered, not
-    // cached: a cached entry would need cross-lane ordering)
+    // per-call multipliers: content-cached device constants (a miss uploads
+    // synchronously after draining every lane, so any lane may read a hit);
+    // the sort's scalars repeat every call, so after the first sort this
+    // launches no upload copy at all
     u64 mk[2 * SFP_MAX_LIMBS + 2];
     const u64* dmk = nullptr;
     if (mulRows) A.pre = RowPtr{mulRows + (size_t)cnt * n, 0, 0};
@@ -2194,7 +2196,7 @@ static void rescaleCore(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t 
         }
         mk[2 * cnt] = mulK[cnt];
         mk[2 * cnt + 1] = sf_shoup_precomp(mulK[cnt], d->hbar[dropPrime].q);
-        dmk = (const u64*)ringPut(d, mk, (2 * cnt + 2) * 8);
+        dmk = devConst(d, mk, 2 * cnt + 2);
         A.preK = dmk + 2 * cnt;
         A.preKS = dmk + 2 * cnt + 1;
     }
