@@ -2,8 +2,12 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdint>
 #include <cstdlib>
+#include <cstring>
+#include <algorithm>
 #include <map>
+#include <tuple>
 #include <memory>
 #include <mutex>
 
@@ -61,7 +65,62 @@ const std::vector<double>& cached(int N, bool doubled) {
     return *p;
 }
 
+std::vector<double> rebase(const std::vector<double>& c, double lo, double hi) {
+    const size_t D = c.size() - 1;
+    // p at the D+1 Chebyshev nodes of y (Clenshaw in long double), then the
+    // discrete Chebyshev transform: exact for a degree-D polynomial
+    std::vector<long double> pv(D + 1);
+    for (size_t j = 0; j <= D; ++j) {
+        const long double y = std::cos((long double)M_PI * ((long double)j + 0.5L) / (long double)(D + 1));
+        const long double z = (long double)lo + (y + 1.0L) * ((long double)hi - (long double)lo) / 2.0L;
+        long double b1 = 0, b2 = 0;
+        for (size_t k = D; k >= 1; --k) {
+            const long double b0 = 2.0L * z * b1 - b2 + (long double)c[k];
+            b2 = b1;
+            b1 = b0;
+        }
+        pv[j] = z * b1 - b2 + 0.5L * (long double)c[0];
+    }
+    // cos(pi k (2j+1) / (2(D+1))) depends on k(2j+1) mod 4(D+1)
+    const size_t P = 4 * (D + 1);
+    std::vector<long double> ctab(P);
+    for (size_t m = 0; m < P; ++m) ctab[m] = std::cos((long double)M_PI * (long double)m / (2.0L * (D + 1)));
+    std::vector<double> d(D + 1);
+    double mx = 0;
+    for (size_t k = 0; k <= D; ++k) {
+        long double acc = 0;
+        size_t idx = k % P;
+        const size_t step = (2 * k) % P;
+        for (size_t j = 0; j <= D; ++j) {
+            acc += pv[j] * ctab[idx];
+            idx += step;
+            if (idx >= P) idx -= P;
+        }
+        d[k] = (double)(acc * 2.0L / (long double)(D + 1));
+        mx = std::max(mx, std::fabs(d[k]));
+    }
+    for (double& v : d)
+        if (std::fabs(v) < 1e-12 * mx) v = 0.0;
+    while (d.size() > 1 && d.back() == 0.0) d.pop_back();
+    return d;
+}
+
 }  // namespace
+
+const std::vector<double>& rebasedChebyshev(const std::vector<double>& c, double lo, double hi) {
+    static std::mutex mu;
+    static std::map<std::tuple<uint64_t, size_t, double, double>, std::unique_ptr<std::vector<double>>> tab;
+    uint64_t h = 1469598103934665603ull;  // content key (FNV-1a over the bits)
+    for (double v : c) {
+        uint64_t b;
+        std::memcpy(&b, &v, 8);
+        h = (h ^ b) * 1099511628211ull;
+    }
+    std::lock_guard<std::mutex> g(mu);
+    auto& p = tab[std::make_tuple(h, c.size(), lo, hi)];
+    if (!p) p.reset(new std::vector<double>(c.empty() ? c : rebase(c, lo, hi)));
+    return *p;
+}
 
 const std::vector<double>& doubledSincCoefficients(int N) { return cached(N, true); }
 const std::vector<double>& scaledSincCoefficients(int N) { return cached(N, false); }

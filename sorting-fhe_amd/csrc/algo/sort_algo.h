@@ -150,6 +150,13 @@ void parallelLanes(const CryptoContext<DCRTPoly>& cc, int lanes, int count, F&& 
     if (err) std::rethrow_exception(err);
 }
 
+// Placement evaluates the doubled sinc in the rebased variable (on unless
+// SFHE_SINC_REBASE=0; see rotationIndexCheckN).
+inline bool sincRebase() {
+    const char* v = std::getenv("SFHE_SINC_REBASE");
+    return !v || *v != '0';
+}
+
 // SFHE_PHASES=1: device-synchronised wall time of each sort phase on stderr
 // (diagnostics only; adds synchronisation, so never on in benchmarks).
 class PhaseTimer {
@@ -380,7 +387,16 @@ class DirectSort : public SortBase<N> {
         indexMinusRank->SetSlots(L.S);
         input_array->SetSlots(L.S);  // reference side effect (sort_algo.h:711)
 
-        const auto& sincCoeffs = selectDoubledSincCoefficients<N>();
+        // The doubled sinc p is evaluated on y = (4z + 1)/3, its argument's
+        // range z in (-1, 1/2) mapped onto [-1, 1]: the same polynomial
+        // (re-expanded, sfhe::rebasedChebyshev), the same levels, but the
+        // hits z = 0 land at y = 1/3 instead of an extremum of every giant
+        // step T_{2^i}, which cuts the CKKS noise of the placement ~2^8-fold
+        // (DESIGN.md §2).  SFHE_SINC_REBASE=0 evaluates p(z) as the reference.
+        const bool rebase = sfhe::sincRebase();
+        const auto& sincCoeffs = rebase ? sfhe::rebasedChebyshev(selectDoubledSincCoefficients<N>(), -1.0, 0.5)
+                                        : selectDoubledSincCoefficients<N>();
+        const double zmul = rebase ? 4.0 / 3.0 : 1.0, zadd = rebase ? 1.0 / 3.0 : 0.0;
         std::vector<Ciphertext<DCRTPoly>> parts(L.B);
         const int lanes = std::min(L.B, m_cc->LaneCount());
         m_cc->ForkLanes(lanes);
@@ -390,8 +406,14 @@ class DirectSort : public SortBase<N> {
                                                           indexMinusRank->GetLevel(), nullptr, L.S));
             })[0];
             // (r - rank_r - c) / 2N  in (-1, 1/2)
-            auto z = m_cc->EvalMult(m_cc->EvalSub(indexMinusRank, chk), 1.0 / N / 2);
+            auto z = m_cc->EvalMult(m_cc->EvalSub(indexMinusRank, chk), zmul / N / 2);
+            if (rebase) z = m_cc->EvalAdd(z, zadd);
             auto hit = m_cc->EvalChebyshevSeriesPS(z, sincCoeffs, -1, 1);
+            // the rebased series may be shorter (tiny tail terms dropped) and so
+            // shallower: consume exactly the reference's PS depth (level tables)
+            const uint32_t psLevel = z->GetLevel() + lbcrypto::ChebyshevPSDepth(
+                (uint32_t)selectDoubledSincCoefficients<N>().size() - 1);
+            if (hit->GetLevel() < psLevel) hit = m_cc->AdjustLevel(hit, psLevel);
             auto masked = m_cc->EvalMult(hit, input_array);
             std::vector<int> amounts(L.npPlace);
             for (int i = 0; i < L.npPlace; ++i) amounts[i] = i;

@@ -689,8 +689,12 @@ class SfheInternal {
                 mod[(size_t)i * nt + t] = pr;
             }
         }
-        return sfp_upload_conv(s->dev, ns, src.data(), nt, dst.data(), dstRow, inv.data(),
-                               mod.data());
+        sfp_conv* c = sfp_upload_conv(s->dev, ns, src.data(), nt, dst.data(), dstRow, inv.data(), mod.data());
+        if (!c) {
+            const char* e = sfp_last_error(s->dev);
+            SFHE_THROW(std::string("base-conversion table upload failed: ") + (e ? e : "unknown"));
+        }
+        return c;
     }
 
     // switching key from s' (device, Lq+K limbs, eval domain) to s
@@ -1087,7 +1091,9 @@ std::vector<int> CryptoContextImpl<DCRTPoly>::ForkHelpers() {
     OpLock g(st.get());
     SfheContextState* s = st.get();
     std::vector<int> lanes{s->lane};
-    if (!s->dataflow) {
+    // a sharded context issues its collectives in program order on one lane
+    // (LaneCount): no helper lanes, or ranks could order them differently
+    if (!s->dataflow && s->world == 1) {
         s->dataflowParent = s->lane;
         // helpers: lanes that are not primaries of an open batch region
         const int first = s->forkedLanes ? s->forkedLanes : 0;

@@ -130,6 +130,11 @@ struct sfp_dev {
     sfp_host_allgather_fn hostAg = nullptr;
     sfp_host_bcast_fn hostBc = nullptr;
     void* hostUser = nullptr;
+    // per-lane scratch (scratch()), and buffers retired by its growth
+    std::mutex scrMu;
+    u64* scr[SFP_MAX_LANES] = {};
+    size_t scrWords[SFP_MAX_LANES] = {};
+    std::vector<void*> retired;
 };
 
 struct sfp_conv {
@@ -1813,6 +1818,8 @@ void sfp_destroy(sfp_dev* d) {
     hipHostFree(d->bounce);
     hipFree(d->cpool);
     hipFree(d->cpoolOld);
+    for (u64* p : d->scr) hipFree(p);
+    for (void* p : d->retired) hipFree(p);
     for (int l = 0; l < d->nLanes; ++l) hipStreamDestroy(d->streams[l]);
     delete d;
 }
@@ -2128,33 +2135,31 @@ void sfp_automorph(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t g, sf
     checkLaunch(d, "automorph");
 }
 
-// ---- scratch owned by the backend (grow-only) ----
+// ---- scratch owned by the device (per lane, grow-only) ----
+// A lane's scratch is reused by every prim on that lane (stream-ordered).  A
+// buffer that has to grow is retired, not freed: work already queued (or a
+// captured graph) may still address it; retired buffers are released by
+// sfp_destroy.  Returns nullptr (and records the error) when HBM is exhausted.
 static u64* scratch(sfp_dev* d, size_t words) {
-    static thread_local sfp_dev* owner = nullptr;
-    struct S {
-        u64* p = nullptr;
-        size_t w = 0;
-    };
-    static std::mutex mu;
-    static std::vector<std::pair<const void*, S>> pool;
-    std::lock_guard<std::mutex> g(mu);
-    (void)owner;
-    const void* key = (const char*)d + d->cur;  // one scratch buffer per lane
-    for (auto& e : pool)
-        if (e.first == key) {
-            if (e.second.w < words) {
-                syncAll(d);
-                hipFree(e.second.p);
-                hipMalloc(&e.second.p, words * 8);
-                e.second.w = words;
-            }
-            return e.second.p;
+    std::lock_guard<std::mutex> g(d->scrMu);
+    const int l = d->cur;
+    if (d->scrWords[l] >= words) return d->scr[l];
+    const size_t grow = std::max(words, d->scrWords[l] + d->scrWords[l] / 2);
+    u64* p = nullptr;
+    if (hipMalloc((void**)&p, grow * 8) != hipSuccess) {
+        hipGetLastError();
+        p = nullptr;
+        if (hipMalloc((void**)&p, words * 8) != hipSuccess) {
+            record(d, "scratch allocation", hipErrorOutOfMemory);
+            return nullptr;
         }
-    S s;
-    hipMalloc(&s.p, words * 8);
-    s.w = words;
-    pool.push_back({key, s});
-    return s.p;
+        d->scrWords[l] = words;
+    } else {
+        d->scrWords[l] = grow;
+    }
+    if (d->scr[l]) d->retired.push_back(d->scr[l]);
+    d->scr[l] = p;
+    return p;
 }
 
 void sfp_rescale(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t ell, const uint64_t* qlinv,
@@ -2178,6 +2183,7 @@ static void rescaleCore(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t 
         return;
     }
     u64* last = scratch(d, (size_t)npoly * n + (size_t)npoly * cnt * n);
+    if (!last) return;
     u64* tmp = last + (size_t)npoly * n;
     RowGroup A = rowsOf(npoly, 1, sfp_limbs{1, 0, dropPrime, 0});
     A.src = RowPtr{in + (size_t)cnt * n, (long long)inStride, 0};
@@ -2255,11 +2261,28 @@ sfp_conv* sfp_upload_conv(sfp_dev* d, uint32_t ns, const uint32_t* src, uint32_t
     c->nt = nt;
     c->hsrc.assign(src, src + ns);
     c->hdst.assign(dst, dst + nt);
-    hipMalloc(&c->src, ns * 4);
-    hipMalloc(&c->dst, nt * 4);
-    hipMalloc(&c->inv, ns * 8);
-    hipMalloc(&c->mod, (size_t)ns * nt * 8);
-    hipMalloc(&c->drow, nt * 4);
+    // every device table is checked: a failed allocation must surface as an
+    // error here, not as a conversion kernel writing through a null pointer
+    bool ok = true;
+    auto dmalloc = [&](auto*& dp, size_t bytes) {
+        if (!ok) return;
+        if (hipMalloc((void**)&dp, bytes + 8) != hipSuccess) {
+            hipGetLastError();
+            dp = nullptr;
+            ok = false;
+        }
+    };
+    dmalloc(c->src, ns * 4);
+    dmalloc(c->dst, nt * 4);
+    dmalloc(c->inv, ns * 8);
+    dmalloc(c->mod, (size_t)ns * nt * 8);
+    dmalloc(c->drow, nt * 4);
+    dmalloc(c->sprod, nt * 8);
+    if (!ok) {
+        record(d, "upload_conv allocation", hipErrorOutOfMemory);
+        sfp_free_conv(d, c);
+        return nullptr;
+    }
     std::vector<uint32_t> rows(nt);
     for (uint32_t t = 0; t < nt; ++t) rows[t] = drow ? drow[t] : t;
     hostToDev(d, c->drow, rows.data(), nt * 4);
@@ -2274,7 +2297,6 @@ sfp_conv* sfp_upload_conv(sfp_dev* d, uint32_t ns, const uint32_t* src, uint32_t
         for (uint32_t i = 0; i < ns; ++i) r = sf_mul(r, d->hbar[src[i]].q % B.q, &B);
         sp[t] = r;
     }
-    hipMalloc(&c->sprod, nt * 8);
     hostToDev(d, c->sprod, sp.data(), nt * 8);
     // FP64 form: FP64 / integer target split, multipliers over the FP64
     // targets, the 60-bit sources' second multiplier (mod * 2^30 mod p)
@@ -2307,8 +2329,8 @@ sfp_conv* sfp_upload_conv(sfp_dev* d, uint32_t ns, const uint32_t* src, uint32_t
             hQ[b * nf + k] = (double)m / (double)p;
         }
     auto up = [&](auto*& dp, const auto& v) {
-        hipMalloc(&dp, v.size() * sizeof(v[0]) + 8);
-        hostToDev(d, dp, v.data(), v.size() * sizeof(v[0]));
+        dmalloc(dp, v.size() * sizeof(v[0]));
+        if (ok) hostToDev(d, dp, v.data(), v.size() * sizeof(v[0]));
     };
     up(c->fpT, c->hFpT);
     up(c->intT, c->hIntT);
@@ -2318,6 +2340,11 @@ sfp_conv* sfp_upload_conv(sfp_dev* d, uint32_t ns, const uint32_t* src, uint32_t
     up(c->vQ, vQ);
     up(c->hD, hD);
     up(c->hQ, hQ);
+    if (!ok) {
+        record(d, "upload_conv allocation", hipErrorOutOfMemory);
+        sfp_free_conv(d, c);
+        return nullptr;
+    }
     return c;
 }
 
@@ -2634,6 +2661,7 @@ void sfp_rescale_rows(sfp_dev* d, uint64_t* out, const uint64_t* in, const uint6
         return;
     }
     u64* tmp = scratch(d, (size_t)npoly * cnt * n);
+    if (!tmp) return;
     RowGroup B = rowsOf(npoly, cnt, m);
     B.src = RowPtr{last, (long long)lastStride, 0};
     B.lift = 1;

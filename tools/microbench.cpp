@@ -66,11 +66,12 @@ int main(int argc, char** argv) {
     std::printf("n=2^%d Lq=%u K=%u dnum=%u alpha=%u\n", logn, s->Lq, s->K, s->dnum, s->alpha);
     std::printf("%-10s %6s %10s %10s %10s %10s\n", "op", "rows", "fwd us", "fwd GB/s", "inv us",
                 "inv GB/s");
-    for (uint32_t rows : {1u, 2u, 4u, 8u, 16u, 24u, 35u, 44u}) {
-        if (rows > NP) continue;
+    for (uint32_t rows : {1u, 2u, 4u, 8u, 16u, 24u, 35u, 44u, 70u, 96u, 140u}) {
         static const uint32_t base = std::getenv("MB_BASE") ? std::atoi(std::getenv("MB_BASE")) : 0;
-        if (rows + base > NP) continue;
-        const sfp_limbs m{rows, rows, base, 0};
+        if (rows > maxRows || (rows <= NP && rows + base > NP)) continue;
+        // beyond NP rows the map wraps: rows [NP, rows) reuse primes 0.. (batched launches)
+        const sfp_limbs m = rows <= NP ? sfp_limbs{rows, rows, base, 0} : sfp_limbs{rows, NP, 0, 0};
+        if (rows > 2 * NP) continue;
         unsigned long long scratch[32];
         sfp_ntt_trace(d, scratch);
         const double f = timeIt(d, 50, [&] { sfp_ntt(d, buf, m, 0); });
