@@ -103,6 +103,9 @@ int sfhe_pool_bytes(sfhe_ctx* c, uint64_t* bytes);
 int sfhe_kernel_timing(sfhe_ctx* c, uint32_t family, uint32_t period);
 int sfhe_kernel_timing_read(sfhe_ctx* c, uint32_t family, uint64_t* launches, uint64_t* timed,
                             double* ms, double* bytes);
+/* on != 0: all of the context's lanes (streams) issue on one stream, so timed
+ * launches run alone, as under rocprofv3 (bench profiling leg; slower). */
+int sfhe_serialize_lanes(sfhe_ctx* c, int on);
 
 /* ---- encryption ------------------------------------------------------------
  * Replaces Encryption::encryptInput (encryption.cpp:5-12, MakeCKKSPacked-

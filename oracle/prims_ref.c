@@ -133,6 +133,7 @@ void sfp_event_free(sfp_dev* d, sfp_event* e) { (void)d; (void)e; }
 void sfp_lane_wait(sfp_dev* d, int waiter, int waitee) { (void)d; (void)waiter; (void)waitee; }
 /* kernel timing is a device-backend feature; the oracle reports nothing */
 void sfp_prof_set(sfp_dev* d, uint32_t fam, uint32_t period) { (void)d; (void)fam; (void)period; }
+void sfp_serialize(sfp_dev* d, int on) { (void)d; (void)on; }
 int sfp_prof_read(sfp_dev* d, uint32_t fam, uint64_t* launches, uint64_t* timed, double* ms,
                   double* bytes) {
     (void)d; (void)fam;

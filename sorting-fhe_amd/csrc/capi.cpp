@@ -452,6 +452,14 @@ int sfhe_kernel_timing(sfhe_ctx* c, uint32_t family, uint32_t period) {
     });
 }
 
+int sfhe_serialize_lanes(sfhe_ctx* c, int on) {
+    REQUIRE(c, "null context");
+    return guard([&] {
+        OpLock g(c->cc->state());
+        sfp_serialize(c->cc->state()->dev, on);
+    });
+}
+
 int sfhe_kernel_timing_read(sfhe_ctx* c, uint32_t family, uint64_t* launches, uint64_t* timed,
                             double* ms, double* bytes) {
     REQUIRE(c, "null context");

@@ -88,7 +88,8 @@ struct sfp_dev {
     // lanes: independent in-order streams; every launch goes to streams[cur]
     hipStream_t streams[SFP_MAX_LANES] = {};
     int nLanes = 1, cur = 0;
-    hipStream_t st() const { return streams[cur]; }
+    bool serial = false;  // sfp_serialize: every lane on streams[0]
+    hipStream_t st() const { return streams[serial ? 0 : cur]; }
     std::vector<sfp_event*> evFree;
     std::mutex evMu;  // evFree: buffers release events from any host thread
     uint32_t n = 0, logn = 0, np = 0;
@@ -1995,6 +1996,11 @@ void sfp_prof_set(sfp_dev* d, uint32_t fam, uint32_t period) {
     profFlush(d, f);
     f = sfp_dev::ProfFam{};
     f.period = period;
+}
+
+void sfp_serialize(sfp_dev* d, int on) {
+    syncAll(d);
+    d->serial = on != 0;
 }
 
 int sfp_prof_read(sfp_dev* d, uint32_t fam, uint64_t* launches, uint64_t* timed, double* ms,

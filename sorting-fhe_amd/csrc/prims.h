@@ -295,6 +295,10 @@ void sfp_prof_set(sfp_dev* d, uint32_t fam, uint32_t period);
 // duration (ms) and summed algorithmic bytes.  Synchronises the stream.
 int sfp_prof_read(sfp_dev* d, uint32_t fam, uint64_t* launches, uint64_t* timed, double* ms,
                   double* bytes);
+// on != 0: every lane's work goes to lane 0's stream in issue order (a valid
+// order: the host issues each op after its inputs), so timed launches do not
+// overlap other lanes' kernels -- per-launch durations as rocprof reports them.
+void sfp_serialize(sfp_dev* d, int on);
 
 #ifdef __cplusplus
 }

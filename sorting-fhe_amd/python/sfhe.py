@@ -35,6 +35,7 @@ ABI_SYMBOLS = [
     "sfhe_sorter_destroy", "sfhe_sorter_sort", "sfhe_sorter_rank", "sfhe_sorter_place",
     "sfhe_decompose", "sfhe_kernel_timing", "sfhe_kernel_timing_read",
     "sfhe_comm_uid", "sfhe_shard_rccl", "sfhe_shard_host", "sfhe_pool_bytes",
+    "sfhe_serialize_lanes",
 ]
 
 
@@ -111,6 +112,7 @@ _SIGS = {
     "sfhe_sorter_rank": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_int, _PVP]),
     "sfhe_sorter_place": (C.c_int, [_VP, _VP, _VP, _PVP]),
     "sfhe_kernel_timing": (C.c_int, [_VP, _U32, _U32]),
+    "sfhe_serialize_lanes": (C.c_int, [_VP, C.c_int]),
     "sfhe_kernel_timing_read": (C.c_int, [_VP, _U32, _PU64, _PU64, _PD, _PD]),
     "sfhe_decompose": (C.c_int, [_U32, _PI32, _SZ, C.c_int32, C.c_int32, C.c_int, _PI32, _PI32, _SZ, _PSZ]),
     "sfhe_comm_uid": (C.c_int, [_VP]),
@@ -271,6 +273,9 @@ class Engine:
 
     def kernel_timing(self, family: str, period: int = 1):
         self._chk(self.lib.sfhe_kernel_timing(self.ctx, self.KFAM[family], period))
+
+    def serialize_lanes(self, on: bool = True):
+        self._chk(self.lib.sfhe_serialize_lanes(self.ctx, int(on)))
 
     def kernel_timing_read(self, family: str) -> dict:
         la, ti = C.c_uint64(), C.c_uint64()
