@@ -220,25 +220,29 @@ def main(argv=None):
     eng.sync()
     cold_ms = (time.perf_counter() - t0) * 1e3
 
-    dt = timed_steps(step, eng.sync, world, args.steps, args.warmup, lambda: eng.op_stats(reset=True))
-    stats = eng.op_stats()
+    dt = timed_steps(step, eng.sync, world, args.steps, args.warmup)
 
     # profiling leg (after the timed region): one sort with the lanes
     # serialised on one stream and every launch of each family bracketed by
     # HIP events on that stream -- per-launch durations as rocprofv3 measures
     # them (no other lane's kernels inside a timed interval)
+    graph_nodes = sorter.graph_nodes()
     eng.sync()
+    os.environ["SFHE_GRAPH"] = "0"  # per-launch timing needs the eager path
     eng.serialize_lanes(True)
     for fam in families:
         eng.kernel_timing(fam, 1)
+    eng.op_stats(reset=True)
     t0 = time.perf_counter()
     step()
     eng.sync()
     serial_ms = (time.perf_counter() - t0) * 1e3
+    stats = eng.op_stats()  # the SURVEY §8(d) byte model over one (eager) sort
     kt = {fam: eng.kernel_timing_read(fam) for fam in families}
     for fam in families:
         eng.kernel_timing(fam, 0)
     eng.serialize_lanes(False)
+    os.environ.pop("SFHE_GRAPH", None)
 
     # per-sort trials, "pure" (plain Encryption, SortNBenchmark)
     # and "as-test" (DebugEncryption: the three PRINT_PT decrypts inside sort(),
@@ -317,7 +321,10 @@ def main(argv=None):
         "config": {"workload": args.workload, "N": N, "ring_dim": 1 << logn, "mult_depth": depth,
                    "sign": list(cfg), "scale_bits": 40, "secure": secure,
                    "parallelism": f"limb-shard x{world} ({args.shard})" if shard else f"replicas x{world}"},
-        "algorithmic_gb_per_sort": stats["algo_bytes"] / args.steps / 1e9,
+        "algorithmic_gb_per_sort": stats["algo_bytes"] / 1e9,
+        "graph": {"replayed": graph_nodes > 0, "nodes": graph_nodes,
+                  "note": "timed steps replay the sort as one hipGraph (captured during warmup; "
+                          "SFHE_GRAPH=0 runs them eagerly)"},
         "roofline": roofline,
         "kernels": kernels,
         "trials": trials,

@@ -165,6 +165,12 @@ int sfhe_sorter_sort(sfhe_sorter* s, sfhe_ct* in, int n, int dg, int df, sfhe_ct
 int sfhe_sorter_rank(sfhe_sorter* s, const sfhe_ct* in, int n, int dg, int df, sfhe_ct** out);
 /* DirectSort<N>::rotationIndexCheckN (sort_algo.h:658-750) */
 int sfhe_sorter_place(sfhe_sorter* s, const sfhe_ct* rank, sfhe_ct* in, sfhe_ct** out);
+/* Kernel / dependency nodes of the sorter's captured sort graph (engine
+ * extension, no reference counterpart): sort() runs its first call of a shape
+ * eagerly, captures the second into a hipGraph and replays it from then on
+ * (SFHE_GRAPH=0 keeps every sort eager; debug sorters never capture).
+ * 0 while no graph exists. */
+int sfhe_sorter_graph_nodes(const sfhe_sorter* s, uint64_t* nodes);
 
 /* Decomposer<N>::decompose (rotation.h:54-102); algo 0 NAF, 1 BNAF, 2 BINARY.
  * N in {4..1024}; writes (value, stepSize) pairs. */

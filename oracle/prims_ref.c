@@ -134,6 +134,13 @@ void sfp_lane_wait(sfp_dev* d, int waiter, int waitee) { (void)d; (void)waiter; 
 /* kernel timing is a device-backend feature; the oracle reports nothing */
 void sfp_prof_set(sfp_dev* d, uint32_t fam, uint32_t period) { (void)d; (void)fam; (void)period; }
 void sfp_serialize(sfp_dev* d, int on) { (void)d; (void)on; }
+/* no graphs: the host layer runs every region eagerly */
+int sfp_capture_begin(sfp_dev* d) { (void)d; return -1; }
+sfp_graph* sfp_capture_end(sfp_dev* d) { (void)d; return NULL; }
+int sfp_capturing(sfp_dev* d) { (void)d; return 0; }
+void sfp_graph_launch(sfp_dev* d, sfp_graph* g) { (void)d; (void)g; }
+size_t sfp_graph_nodes(const sfp_graph* g) { (void)g; return 0; }
+void sfp_graph_destroy(sfp_dev* d, sfp_graph* g) { (void)d; (void)g; }
 int sfp_prof_read(sfp_dev* d, uint32_t fam, uint64_t* launches, uint64_t* timed, double* ms,
                   double* bytes) {
     (void)d; (void)fam;

@@ -429,8 +429,98 @@ class DirectSort : public SortBase<N> {
         return output;
     }
 
+    // ---- hipGraph replay (north_star: "the Chebyshev tree / rotations /
+    // rank-matrix EvalMults run as a hipGraph") ----
+    // The op sequence of sort() depends only on (N, the input's level and
+    // slots, the sign configuration), never on the data (reference
+    // sort_algo.h:752-774).  The first sort of a shape runs eagerly (it
+    // generates and encodes the masks); the second is captured into a graph
+    // over a sorter-owned copy of the input; from then on a sort is: copy the
+    // caller's input into that buffer, launch the graph, clone its result.
+    // Debug sorts (PRINT_PT decrypts) and sharded contexts stay eager;
+    // SFHE_GRAPH=0 disables graphs.
+    struct GraphKey {
+        uint32_t level = 0, slots = 0;
+        int func = -1, n = 0, dg = 0, df = 0;
+        bool operator==(const GraphKey& o) const {
+            return level == o.level && slots == o.slots && func == o.func && n == o.n && dg == o.dg && df == o.df;
+        }
+    };
+    struct Graph {
+        std::shared_ptr<CryptoContextImpl<DCRTPoly>::CapturedGraph> g;
+        Ciphertext<DCRTPoly> in, out;
+        GraphKey key;
+    };
+    std::unique_ptr<Graph> m_graph;
+    GraphKey m_warmKey;
+    bool m_warm = false, m_graphOff = false;
+
+    static bool graphsEnabled() {
+        const char* v = std::getenv("SFHE_GRAPH");
+        return !v || *v != '0';
+    }
+
+  public:
+    ~DirectSort() override { m_graph.reset(); }
+    // nodes of the captured sort (0: none yet / eager)
+    size_t graphNodes() const { return m_graph ? m_cc->GraphNodes(m_graph->g) : 0; }
+
     Ciphertext<DCRTPoly> sort(const Ciphertext<DCRTPoly>& input_array, SignFunc SignFunc,
                               SignConfig& Cfg) override {
+        const bool debug = dynamic_cast<const DebugEncryption*>(m_enc.get()) != nullptr;
+        if (debug || m_graphOff || !graphsEnabled() || m_cc->ShardWorld() > 1)
+            return sortEager(input_array, SignFunc, Cfg);
+        GraphKey key;
+        key.level = input_array->GetLevel();
+        // sort() leaves its input at S slots (:711): N and S select the same
+        // op sequence (rotation amounts < N), so they share a graph
+        const sfhe::RankLayout L(N, max_batch);
+        key.slots = input_array->GetSlots() == (uint32_t)L.S ? (uint32_t)N : input_array->GetSlots();
+        key.func = (int)SignFunc;
+        key.n = Cfg.compos.n;
+        key.dg = Cfg.compos.dg;
+        key.df = Cfg.compos.df;
+        if (!(m_graph && m_graph->key == key)) {
+            if (!(m_warm && m_warmKey == key)) {  // first sort of this shape: eager, builds the masks
+                m_warm = true;
+                m_warmKey = key;
+                return sortEager(input_array, SignFunc, Cfg);
+            }
+            m_graph.reset();
+            auto g = std::make_unique<Graph>();
+            g->key = key;
+            g->in = input_array->Clone();  // sorter-owned input buffer (eager copy)
+            if (!m_cc->BeginCapture()) {
+                m_graphOff = true;
+                return sortEager(input_array, SignFunc, Cfg);
+            }
+            Ciphertext<DCRTPoly> out;
+            try {
+                out = sortEager(g->in, SignFunc, Cfg);
+            } catch (...) {
+                m_cc->EndCapture(nullptr);
+                m_graphOff = true;
+                throw;
+            }
+            g->g = m_cc->EndCapture(out);
+            if (!g->g) {
+                m_graphOff = true;
+                return sortEager(input_array, SignFunc, Cfg);
+            }
+            g->out = out;
+            m_graph = std::move(g);
+        } else if (m_graph->in != input_array) {
+            m_cc->CopyCiphertextInto(m_graph->in, input_array);
+        }
+        m_cc->Launch(m_graph->g);
+        input_array->SetSlots(m_graph->in->GetSlots());  // sort()'s side effect on its input (:711)
+        auto result = m_graph->out->Clone();
+        result->SetSlots(m_graph->out->GetSlots());
+        return result;
+    }
+
+    Ciphertext<DCRTPoly> sortEager(const Ciphertext<DCRTPoly>& input_array, SignFunc SignFunc,
+                                   SignConfig& Cfg) {
         std::cout << "\n===== Direct Sort Input Array: \n";
         PRINT_PT(m_enc, input_array);
         auto ctx_Rank = constructRank(input_array, SignFunc, Cfg);

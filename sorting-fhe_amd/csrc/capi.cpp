@@ -96,6 +96,7 @@ struct SorterBase {
     virtual Ct sort(const Ct& in, SignConfig& cfg) = 0;
     virtual Ct rank(const Ct& in, SignConfig& cfg) = 0;
     virtual Ct place(const Ct& rank, const Ct& in) = 0;
+    virtual size_t graphNodes() const = 0;
 };
 
 template <int N>
@@ -109,6 +110,7 @@ struct Sorter : SorterBase {
         return ds.constructRank(in, SignFunc::CompositeSign, cfg);
     }
     Ct place(const Ct& r, const Ct& in) override { return ds.rotationIndexCheckN(r, in); }
+    size_t graphNodes() const override { return ds.graphNodes(); }
 };
 
 template <int N>
@@ -408,6 +410,12 @@ int sfhe_sorter_rank(sfhe_sorter* s, const sfhe_ct* in, int n, int dg, int df, s
 int sfhe_sorter_place(sfhe_sorter* s, const sfhe_ct* rank, sfhe_ct* in, sfhe_ct** out) {
     REQUIRE(s && rank && in && out, "null argument");
     return guard([&] { *out = wrap(s->impl->place(rank->ct, in->ct)); });
+}
+
+int sfhe_sorter_graph_nodes(const sfhe_sorter* s, uint64_t* nodes) {
+    REQUIRE(s && nodes, "null argument");
+    *nodes = s->impl->graphNodes();
+    return SFHE_OK;
 }
 
 int sfhe_decompose(uint32_t N, const int32_t* keys, size_t nkeys, int32_t rotation, int32_t wrapN,

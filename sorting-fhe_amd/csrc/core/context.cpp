@@ -146,6 +146,13 @@ DeviceBuffer::~DeviceBuffer() {
     if (ready) sfp_event_free(st->dev, ready);
     if (!ptr) return;
     std::lock_guard<std::mutex> g(st->poolMu);
+    if (!st->graphOwned.empty()) {
+        auto it = st->graphOwned.find(ptr);
+        if (it != st->graphOwned.end()) {  // a graph addresses it: the graph releases it
+            it->second = false;
+            return;
+        }
+    }
     if (st->dataflow)
         st->dataflowFree.push_back({words, ptr});  // any lane may still read it: after the sub-join
     else if (!st->forkedLanes)
@@ -188,6 +195,10 @@ DeviceBufferPtr SfheContextState::alloc(size_t words) {
     }
     auto b = std::make_shared<DeviceBuffer>(this, p, words, lane, forkedLanes ? region : 0);
     b->seq = ++laneSeq[lane];
+    if (capturing) {
+        std::lock_guard<std::mutex> g(poolMu);
+        capAllocs.push_back({p, words});
+    }
     return b;
 }
 
@@ -754,6 +765,10 @@ class SfheInternal {
     // An encoding produced on another lane that may still be in flight is
     // waited for (device-side) before use.
     static const uint64_t* ready(SfheContextState* s, DeviceBuffer* b) {
+        if (b->ready && s->capturing) {  // the capture began after a full drain
+            sfp_event_free(s->dev, b->ready);
+            b->ready = nullptr;
+        }
         if (b->ready) {
             if (sfp_event_done(s->dev, b->ready)) {
                 sfp_event_free(s->dev, b->ready);
@@ -1988,6 +2003,125 @@ void CryptoContextImpl<DCRTPoly>::DownloadRows(const Ciphertext<DCRTPoly>& ct, u
     }
     const char* e = sfp_last_error(s->dev);
     if (e) SFHE_THROW(std::string("device error: ") + e);
+}
+
+// ============================================================================
+// graph capture (engine extension)
+
+struct CryptoContextImpl<DCRTPoly>::CapturedGraph {
+    std::weak_ptr<CryptoContextImpl<DCRTPoly>> cc;
+    sfp_graph* g = nullptr;
+    std::vector<std::pair<uint64_t*, size_t>> owned;  // pool blocks the graph addresses
+    Ciphertext<DCRTPoly> keep;
+    ~CapturedGraph() {
+        keep.reset();
+        auto c = cc.lock();
+        if (!c) return;  // the context is gone: its pool and device went with it
+        SfheContextState* s = c->state();
+        OpLock lk(s);
+        sfp_graph_destroy(s->dev, g);  // drains the device first
+        std::lock_guard<std::mutex> pg(s->poolMu);
+        for (auto& o : owned) {
+            auto it = s->graphOwned.find(o.first);
+            if (it == s->graphOwned.end()) continue;
+            const bool live = it->second;
+            s->graphOwned.erase(it);
+            if (!live) s->freeList[0][o.second].push_back(o.first);  // else its holder frees it
+        }
+    }
+};
+
+bool CryptoContextImpl<DCRTPoly>::BeginCapture() {
+    OpLock g(st.get());
+    SfheContextState* s = st.get();
+    if (s->capturing) SFHE_THROW("BeginCapture: a capture is already open");
+    if (s->forkedLanes || s->dataflow) SFHE_THROW("BeginCapture inside a lane region");
+    if (s->world > 1) return false;  // collectives stay eager (host transports synchronise)
+    sfp_sync(s->dev);
+    if (sfp_capture_begin(s->dev) != 0) {
+        std::fprintf(stderr, "sfhe: this backend cannot capture graphs (%s); sorting eagerly\n", sfp_backend_name());
+        return false;
+    }
+    s->capturing = true;
+    s->capAllocs.clear();
+    // every cross-lane dependency inside the region must become a graph edge
+    std::memset(s->synced, 0, sizeof s->synced);
+    return true;
+}
+
+std::shared_ptr<CryptoContextImpl<DCRTPoly>::CapturedGraph> CryptoContextImpl<DCRTPoly>::EndCapture(
+    const Ciphertext<DCRTPoly>& keep) {
+    OpLock lk(st.get());
+    SfheContextState* s = st.get();
+    if (!s->capturing) SFHE_THROW("EndCapture without BeginCapture");
+    sfp_graph* g = sfp_capture_end(s->dev);
+    s->capturing = false;
+    std::memset(s->synced, 0, sizeof s->synced);
+    std::vector<std::pair<uint64_t*, size_t>> blocks;
+    {
+        std::lock_guard<std::mutex> pg(s->poolMu);
+        blocks.swap(s->capAllocs);
+    }
+    if (!g) {
+        const char* e = sfp_last_error(s->dev);
+        std::fprintf(stderr, "sfhe: graph capture abandoned, running eagerly (%s)\n", e ? e : "unknown");
+        return nullptr;
+    }
+    auto out = std::make_shared<CapturedGraph>();
+    out->cc = shared_from_this();
+    out->g = g;
+    out->keep = keep;
+    std::sort(blocks.begin(), blocks.end());
+    blocks.erase(std::unique(blocks.begin(), blocks.end()), blocks.end());
+    std::lock_guard<std::mutex> pg(s->poolMu);
+    // a recorded block is either back in a free list (the region freed it:
+    // take it out, the graph owns it now) or still held (the result, keep)
+    std::unordered_map<uint64_t*, size_t> want(blocks.begin(), blocks.end());
+    auto scrub = [&](std::map<size_t, std::vector<uint64_t*>>& fl) {
+        for (auto& kv : fl) {
+            auto& v = kv.second;
+            v.erase(std::remove_if(v.begin(), v.end(),
+                                   [&](uint64_t* p) {
+                                       auto it = want.find(p);
+                                       if (it == want.end()) return false;
+                                       s->graphOwned[p] = false;
+                                       return true;
+                                   }),
+                    v.end());
+        }
+    };
+    for (auto& fl : s->freeList) scrub(fl);
+    scrub(s->forkPool);
+    for (auto& b : blocks)
+        if (!s->graphOwned.count(b.first)) s->graphOwned[b.first] = true;  // live
+    out->owned = std::move(blocks);
+    return out;
+}
+
+void CryptoContextImpl<DCRTPoly>::Launch(const std::shared_ptr<CapturedGraph>& g) {
+    OpLock lk(st.get());
+    SfheContextState* s = st.get();
+    if (!g || !g->g) SFHE_THROW("Launch: no graph");
+    if (s->forkedLanes || s->dataflow) SFHE_THROW("Launch inside a lane region");
+    sfp_graph_launch(s->dev, g->g);
+    // the graph ran (stream-ordered) on lane 0: so did every write it made
+    if (g->keep) s->wrote(g->keep->buf.get());
+}
+
+size_t CryptoContextImpl<DCRTPoly>::GraphNodes(const std::shared_ptr<CapturedGraph>& g) const {
+    return g ? sfp_graph_nodes(g->g) : 0;
+}
+
+void CryptoContextImpl<DCRTPoly>::CopyCiphertextInto(const Ciphertext<DCRTPoly>& dst,
+                                                     const Ciphertext<DCRTPoly>& src) {
+    OpLock lk(st.get());
+    SfheContextState* s = st.get();
+    SfheInternal::deps(s, {&dst, &src});
+    if (dst->level != src->level) SFHE_THROW("CopyCiphertextInto: level mismatch");
+    const size_t bytes = s->polyWords(src->level) * 8;
+    sfp_d2d(s->dev, dst->c0, src->c0, bytes);
+    sfp_d2d(s->dev, dst->c1, src->c1, bytes);
+    s->wrote(dst->buf.get());
 }
 
 // ============================================================================

@@ -404,6 +404,21 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
     };
     OpStats GetOpStats() const;
     void ResetOpStats();
+    // Engine extension: hipGraph capture of a data-independent op sequence
+    // (the sort's steady state).  BeginCapture() drains the device and starts
+    // recording (false: the backend has no graphs -- run eagerly);
+    // EndCapture(keep) finishes it: nullptr if the region could not be
+    // captured (a host synchronisation inside; the reason is in the log),
+    // otherwise a graph that owns every pool block the region allocated plus
+    // `keep` (the region's result, read after each launch).  Launch() replays
+    // it on the current lane, stream-ordered with everything else.
+    struct CapturedGraph;
+    bool BeginCapture();
+    std::shared_ptr<CapturedGraph> EndCapture(const Ciphertext<DCRTPoly>& keep);
+    void Launch(const std::shared_ptr<CapturedGraph>& g);
+    size_t GraphNodes(const std::shared_ptr<CapturedGraph>& g) const;
+    // dst's rows (same level) overwritten with src's: refills a graph's input
+    void CopyCiphertextInto(const Ciphertext<DCRTPoly>& dst, const Ciphertext<DCRTPoly>& src);
 
   private:
     std::unique_ptr<SfheContextState> st;

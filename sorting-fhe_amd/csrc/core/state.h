@@ -6,6 +6,7 @@
 #include <map>
 #include <mutex>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../modarith.h"
@@ -103,6 +104,13 @@ struct SfheContextState {
     size_t ptCacheBytes = 0;
     size_t ptCacheLimit = (size_t)48 << 30;
     std::unordered_map<uint64_t, std::vector<PtCacheEntry>> ptCache;  // key hash (incl. level)
+
+    // graph capture: every block alloc() hands out while capturing (with its
+    // size); blocks owned by a live graph are never recycled by the pool --
+    // graphOwned[p] = true while a DeviceBuffer still holds p
+    bool capturing = false;
+    std::vector<std::pair<uint64_t*, size_t>> capAllocs;
+    std::unordered_map<uint64_t*, bool> graphOwned;
 
     std::atomic<uint64_t> seedCounter{1};
     uint64_t seed = 0;

@@ -83,6 +83,23 @@ struct sfp_event {
     int lane = 0;
 };
 
+// A captured graph and the device arena its launches read their small
+// argument arrays from (filled once, when the capture ends).
+struct GraphChunk {
+    u64* dev = nullptr;
+    std::vector<u64> host;
+    size_t used = 0;  // words
+};
+struct sfp_graph {
+    hipGraph_t g = nullptr;
+    hipGraphExec_t exec = nullptr;
+    std::vector<GraphChunk> arena;
+    std::unordered_map<uint64_t, std::vector<std::pair<std::vector<u64>, const u64*>>> consts;
+    size_t nodes = 0;
+    bool failed = false;
+    std::string why;
+};
+
 struct sfp_dev {
     int device = 0;
     // lanes: independent in-order streams; every launch goes to streams[cur]
@@ -136,6 +153,7 @@ struct sfp_dev {
     u64* scr[SFP_MAX_LANES] = {};
     size_t scrWords[SFP_MAX_LANES] = {};
     std::vector<void*> retired;
+    sfp_graph* capture = nullptr;  // open capture (sfp_capture_begin)
 };
 
 struct sfp_conv {
@@ -163,8 +181,16 @@ static void record(sfp_dev* d, const char* what, hipError_t e) {
     if (d->err.empty()) d->err = std::string(what) + ": " + hipGetErrorString(e);
 }
 
+static void captureFail(sfp_dev* d, const char* why) {
+    if (!d->capture->failed) {
+        d->capture->failed = true;
+        d->capture->why = why;
+    }
+}
+
 // Drain every lane (shared host-visible resources: ring, bounce, constant pool).
 static void syncAll(sfp_dev* d) {
+    if (d->capture) return captureFail(d, "host synchronisation inside the captured region");
     for (int i = 0; i < d->nLanes; ++i) {
         hipError_t e = hipStreamSynchronize(d->streams[i]);
         if (e != hipSuccess) record(d, "synchronize", e);
@@ -182,7 +208,7 @@ static bool debugSync() {
 static void checkLaunch(sfp_dev* d, const char* k) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) record(d, k, e);
-    if (debugSync()) {
+    if (debugSync() && !d->capture) {
         e = hipStreamSynchronize(d->st());
         if (e != hipSuccess) record(d, k, e);
     }
@@ -232,7 +258,7 @@ static void profFlush(sfp_dev* d, sfp_dev::ProfFam& f) {
 template <class F>
 static void timedLaunch(sfp_dev* d, uint32_t fam, double bytes, F&& launch) {
     sfp_dev::ProfFam& f = d->prof[fam];
-    if (!f.period || (f.seen++ % f.period) != 0) {
+    if (d->capture || !f.period || (f.seen++ % f.period) != 0) {
         launch();
         return;
     }
@@ -324,6 +350,14 @@ template <bool COL>
 __device__ __forceinline__ uint32_t twIndex(const NttTile& T, uint32_t S0, uint32_t k, uint32_t x0) {
     if (COL) return (1u << k) - 1 + (x0 >> (T.logn - k));
     return (1u << (S0 + k)) + (x0 >> (8 - k));
+}
+// ROW pass, FP64 rows: the tile's 8 rows need, at stage k, the contiguous
+// table run [2^(S0+k) + r0 2^k, + 8 2^k) -- 2040 doubles over the 8 stages,
+// staged in LDS with the tile (one load latency instead of one per round):
+// stage k's run at LDS offset 8 (2^k - 1).
+constexpr uint32_t kNttRowTw = (kNttTile / 256) * 255;
+__device__ __forceinline__ uint32_t twIndexRowLds(const NttTile& T, uint32_t k, uint32_t x0) {
+    return kNttRows * ((1u << k) - 1) + (x0 >> (8 - k)) - (T.r0 << k);
 }
 
 // One round: stages k0..k0+B-1 of the pass (k relative to the pass's first
@@ -442,7 +476,7 @@ __device__ __forceinline__ double fpReduce(double v, double q, double qinv) {
 
 template <bool INV, bool COL, int LE, int B>
 __device__ __forceinline__ void nttRoundFP(double* s, const NttTile& T, uint32_t S0, uint32_t k0, double q,
-                                           const double* w, const double* wq, double qinv) {
+                                           const double* w, const double* wq, double qinv, bool rowLds) {
     constexpr int M = 1 << B;
     constexpr int GPT = (1 << LE) / M;
     const uint32_t D = 1u << T.d;
@@ -469,7 +503,7 @@ __device__ __forceinline__ void nttRoundFP(double* s, const NttTile& T, uint32_t
         double W[M - 1], WQ[M - 1];
 #pragma unroll
         for (int t = 0; t < B; ++t) {
-            const uint32_t tb = twIndex<COL>(T, S0, k0 + t, x0);
+            const uint32_t tb = (!COL && rowLds) ? twIndexRowLds(T, k0 + t, x0) : twIndex<COL>(T, S0, k0 + t, x0);
 #pragma unroll
             for (int qd = 0; qd < (1 << t); ++qd) {
                 W[(1 << t) - 1 + qd] = w[tb + qd];
@@ -517,12 +551,13 @@ __device__ __forceinline__ void nttRoundFP(double* s, const NttTile& T, uint32_t
 
 template <bool INV, bool COL, int LE>
 __device__ __forceinline__ void nttRoundDynFP(int b, double* s, const NttTile& T, uint32_t S0, uint32_t k0,
-                                              double q, const double* w, const double* wq, double qinv) {
+                                              double q, const double* w, const double* wq, double qinv,
+                                              bool rowLds) {
     if constexpr (LE >= 3) {
-        if (b == 3) return nttRoundFP<INV, COL, LE, 3>(s, T, S0, k0, q, w, wq, qinv);
+        if (b == 3) return nttRoundFP<INV, COL, LE, 3>(s, T, S0, k0, q, w, wq, qinv, rowLds);
     }
-    if (b == 2) return nttRoundFP<INV, COL, LE, 2>(s, T, S0, k0, q, w, wq, qinv);
-    nttRoundFP<INV, COL, LE, 1>(s, T, S0, k0, q, w, wq, qinv);
+    if (b == 2) return nttRoundFP<INV, COL, LE, 2>(s, T, S0, k0, q, w, wq, qinv, rowLds);
+    nttRoundFP<INV, COL, LE, 1>(s, T, S0, k0, q, w, wq, qinv, rowLds);
 }
 
 
@@ -682,7 +717,7 @@ __global__ __launch_bounds__(kNttTile >> LE) void k_ntt(const RowGroup G, const 
         if (fp)
             nttRoundDynFP<INV, COL, LE>(b, reinterpret_cast<double*>(s), T, S0, k0, (double)q,
                                         reinterpret_cast<const double*>(rw), reinterpret_cast<const double*>(rx),
-                                        qinvD[prime]);
+                                        qinvD[prime], false);
         else
             nttRoundDyn<INV, COL, LE>(b, s, T, S0, k0, q, rw, rx);
         __syncthreads();
@@ -1608,7 +1643,31 @@ static void devZero(sfp_dev* d, void* dst, size_t b) {
 // Small host array -> device memory, ordered on the stream: staged in the
 // pinned ring, pulled across by a copy kernel.  The ring region is reused
 // only after the stream has drained past every earlier pull.
+// Copy of a small host array in the open capture's arena (device address;
+// the arena is uploaded when the capture ends).
+static const u64* arenaPut(sfp_dev* d, const void* src, size_t bytes) {
+    sfp_graph* g = d->capture;
+    const size_t words = ((bytes + 255) & ~(size_t)255) / 8;
+    if (g->arena.empty() || g->arena.back().used + words > g->arena.back().host.size()) {
+        GraphChunk c;
+        const size_t cap = std::max(words, (size_t)1 << 19);  // 4 MiB chunks
+        if (hipMalloc((void**)&c.dev, cap * 8) != hipSuccess) {
+            hipGetLastError();
+            captureFail(d, "graph arena allocation");
+            return nullptr;
+        }
+        c.host.assign(cap, 0);
+        g->arena.push_back(std::move(c));
+    }
+    GraphChunk& c = g->arena.back();
+    std::memcpy(c.host.data() + c.used, src, bytes);
+    const u64* dv = c.dev + c.used;
+    c.used += words;
+    return dv;
+}
+
 static void* ringPut(sfp_dev* d, const void* src, size_t bytes) {
+    if (d->capture) return const_cast<u64*>(arenaPut(d, src, bytes));
     const size_t span = (bytes + 255) & ~(size_t)255;  // keep entries 256-B aligned
     if (d->ringOff + span > d->ringCap) {
         syncAll(d);
@@ -1624,6 +1683,7 @@ static void* ringPut(sfp_dev* d, const void* src, size_t bytes) {
 
 // Bulk host -> device through the bounce buffer, chunk by chunk.
 static void hostToDev(sfp_dev* d, void* dst, const void* src, size_t b) {
+    if (d->capture) return captureFail(d, "host-to-device upload inside the captured region");
     syncAll(d);  // the bounce buffer is shared by every lane
     for (size_t off = 0; off < b; off += d->bounceCap) {
         const size_t c = b - off < d->bounceCap ? b - off : d->bounceCap;
@@ -1634,6 +1694,7 @@ static void hostToDev(sfp_dev* d, void* dst, const void* src, size_t b) {
 }
 
 static void devToHost(sfp_dev* d, void* dst, const void* src, size_t b) {
+    if (d->capture) return captureFail(d, "device-to-host download inside the captured region");
     syncAll(d);
     for (size_t off = 0; off < b; off += d->bounceCap) {
         const size_t c = b - off < d->bounceCap ? b - off : d->bounceCap;
@@ -1648,6 +1709,14 @@ static void devToHost(sfp_dev* d, void* dst, const void* src, size_t b) {
 static const u64* devConst(sfp_dev* d, const u64* v, size_t count) {
     uint64_t h = 1469598103934665603ull ^ count;
     for (size_t i = 0; i < count; ++i) h = (h ^ v[i]) * 1099511628211ull;
+    if (d->capture) {  // the graph's own immutable copy (the pool's generations retire)
+        auto& b = d->capture->consts[h];
+        for (auto& e : b)
+            if (e.first.size() == count && std::equal(v, v + count, e.first.begin())) return e.second;
+        const u64* p = arenaPut(d, v, count * 8);
+        if (p) b.push_back({std::vector<u64>(v, v + count), p});
+        return p;
+    }
     auto& bucket = d->cmap[h];
     for (auto& e : bucket)
         if (e.first.size() == count && std::equal(v, v + count, e.first.begin())) return d->cpool + e.second;
@@ -1881,7 +1950,8 @@ void sfp_event_wait(sfp_dev* d, const sfp_event* e) {
     if (e && e->lane != d->cur) SFP_CHECK(hipStreamWaitEvent(d->st(), e->e, 0));
 }
 int sfp_event_done(sfp_dev* d, const sfp_event* e) {
-    (void)d;
+    // a capture starts after every lane drained: earlier events are complete
+    if (d->capture) return 1;
     return !e || hipEventQuery(e->e) == hipSuccess;
 }
 void sfp_event_free(sfp_dev* d, sfp_event* e) {
@@ -1900,8 +1970,10 @@ void sfp_lane_wait(sfp_dev* d, int waiter, int waitee) {
     d->cur = keep;
 }
 const char* sfp_last_error(sfp_dev* d) {
-    hipError_t e = hipStreamQuery(d->st());
-    if (e != hipSuccess && e != hipErrorNotReady) record(d, "stream", e);
+    if (!d->capture) {  // (querying a capturing stream would invalidate the capture)
+        hipError_t e = hipStreamQuery(d->st());
+        if (e != hipSuccess && e != hipErrorNotReady) record(d, "stream", e);
+    }
     std::lock_guard<std::mutex> g(d->mu);
     return d->err.empty() ? nullptr : d->err.c_str();
 }
@@ -1997,6 +2069,69 @@ void sfp_prof_set(sfp_dev* d, uint32_t fam, uint32_t period) {
     f = sfp_dev::ProfFam{};
     f.period = period;
 }
+
+// ---- graph capture ----
+int sfp_capture_begin(sfp_dev* d) {
+    if (d->capture) {
+        record(d, "capture_begin (a capture is already open)", hipErrorInvalidValue);
+        return -1;
+    }
+    syncAll(d);
+    d->cur = 0;
+    auto* g = new sfp_graph;
+    const hipError_t e = hipStreamBeginCapture(d->streams[0], hipStreamCaptureModeRelaxed);
+    if (e != hipSuccess) {
+        hipGetLastError();
+        delete g;
+        std::fprintf(stderr, "sfhe: hipStreamBeginCapture: %s\n", hipGetErrorString(e));
+        return -1;
+    }
+    d->capture = g;
+    return 0;
+}
+
+int sfp_capturing(sfp_dev* d) { return d->capture != nullptr; }
+
+void sfp_graph_destroy(sfp_dev* d, sfp_graph* g) {
+    if (!g) return;
+    if (!d->capture) syncAll(d);
+    if (g->exec) hipGraphExecDestroy(g->exec);
+    if (g->g) hipGraphDestroy(g->g);
+    for (auto& c : g->arena) hipFree(c.dev);
+    delete g;
+}
+
+sfp_graph* sfp_capture_end(sfp_dev* d) {
+    sfp_graph* g = d->capture;
+    if (!g) return nullptr;
+    d->cur = 0;
+    const hipError_t e = hipStreamEndCapture(d->streams[0], &g->g);
+    d->capture = nullptr;
+    if (e != hipSuccess || g->failed || !g->g) {
+        hipGetLastError();
+        std::string why = g->failed ? g->why : std::string("hipStreamEndCapture: ") + hipGetErrorString(e);
+        sfp_graph_destroy(d, g);
+        std::lock_guard<std::mutex> lk(d->mu);
+        if (d->err.empty()) d->err = "graph capture failed: " + why;
+        return nullptr;
+    }
+    for (auto& c : g->arena) hostToDev(d, c.dev, c.host.data(), c.used * 8);
+    if (hipGraphGetNodes(g->g, nullptr, &g->nodes) != hipSuccess) g->nodes = 0;
+    if (hipGraphInstantiate(&g->exec, g->g, nullptr, nullptr, 0) != hipSuccess) {
+        const hipError_t ie = hipGetLastError();
+        sfp_graph_destroy(d, g);
+        record(d, "hipGraphInstantiate", ie);
+        return nullptr;
+    }
+    return g;
+}
+
+void sfp_graph_launch(sfp_dev* d, sfp_graph* g) {
+    if (!g || !g->exec) return record(d, "graph_launch", hipErrorInvalidValue);
+    SFP_CHECK(hipGraphLaunch(g->exec, d->st()));
+}
+
+size_t sfp_graph_nodes(const sfp_graph* g) { return g ? g->nodes : 0; }
 
 void sfp_serialize(sfp_dev* d, int on) {
     syncAll(d);

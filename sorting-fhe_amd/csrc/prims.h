@@ -282,6 +282,25 @@ void sfp_ks_inner_map(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t
                       size_t ext_stride, const uint64_t* key, uint32_t beta, sfp_limbs pm,
                       uint32_t keyQ, uint32_t key_rows);
 
+// ---- graph capture (hipGraph) ---------------------------------------------------
+// Between sfp_capture_begin and sfp_capture_end every prim enqueued on lane 0
+// -- and on any lane that waited for it (sfp_lane_wait / sfp_event_wait) -- is
+// recorded into a graph instead of running; the lanes must be joined back to
+// lane 0 before the end.  Small host arrays the prims upload (weights, row
+// tables, kernel constants) go to a per-graph device arena filled once at the
+// end, so the recorded launches read immutable copies.  Any host
+// synchronisation inside the region (a download, an upload, a ring wrap)
+// invalidates the capture: sfp_capture_end then returns NULL and records why.
+// The oracle backend has no graphs: sfp_capture_begin returns -1.
+typedef struct sfp_graph sfp_graph;
+int sfp_capture_begin(sfp_dev* d);
+sfp_graph* sfp_capture_end(sfp_dev* d);
+int sfp_capturing(sfp_dev* d);
+// Enqueue the whole graph on the current lane (stream-ordered like a prim).
+void sfp_graph_launch(sfp_dev* d, sfp_graph* g);
+size_t sfp_graph_nodes(const sfp_graph* g);
+void sfp_graph_destroy(sfp_dev* d, sfp_graph* g);
+
 // ---- live kernel timing ---------------------------------------------------------
 // Kernel families timed with events recorded on the backend's stream around
 // single launches.  Algorithmic bytes per launch (minimum HBM traffic):

@@ -35,7 +35,7 @@ ABI_SYMBOLS = [
     "sfhe_sorter_destroy", "sfhe_sorter_sort", "sfhe_sorter_rank", "sfhe_sorter_place",
     "sfhe_decompose", "sfhe_kernel_timing", "sfhe_kernel_timing_read",
     "sfhe_comm_uid", "sfhe_shard_rccl", "sfhe_shard_host", "sfhe_pool_bytes",
-    "sfhe_serialize_lanes",
+    "sfhe_serialize_lanes", "sfhe_sorter_graph_nodes",
 ]
 
 
@@ -111,6 +111,7 @@ _SIGS = {
     "sfhe_sorter_sort": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_int, _PVP]),
     "sfhe_sorter_rank": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_int, _PVP]),
     "sfhe_sorter_place": (C.c_int, [_VP, _VP, _VP, _PVP]),
+    "sfhe_sorter_graph_nodes": (C.c_int, [_VP, _PU64]),
     "sfhe_kernel_timing": (C.c_int, [_VP, _U32, _U32]),
     "sfhe_serialize_lanes": (C.c_int, [_VP, C.c_int]),
     "sfhe_kernel_timing_read": (C.c_int, [_VP, _U32, _PU64, _PU64, _PD, _PD]),
@@ -396,6 +397,11 @@ class Sorter:
 
     def place(self, rank: Ct, ct: Ct) -> Ct:
         return self.eng._new(self.eng.lib.sfhe_sorter_place, self.h, rank.h, ct.h)
+
+    def graph_nodes(self) -> int:
+        v = C.c_uint64()
+        self.eng._chk(self.eng.lib.sfhe_sorter_graph_nodes(self.h, C.byref(v)))
+        return v.value
 
 
 def direct_sort_params(N: int, backend: str = "hip"):

@@ -1,0 +1,70 @@
+"""hipGraph replay of DirectSort<N>::sort (north_star: the Chebyshev tree,
+rotations and rank-matrix EvalMults run as a hipGraph).
+
+The sorter runs the first sort of a shape eagerly, captures the second and
+replays the graph afterwards.  The op sequence is data-independent (reference
+src/sort_algo.h:752-774), so every replay must be bit-identical to the eager
+sort of the same input on the same sorter (same zero-cache encryption), for
+the captured input and for a different one copied into the graph's buffer.
+"""
+import numpy as np
+import pytest
+
+import sfhe
+from oracle import slotsim
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("N,logn", [(64, 14), (256, 16)])
+def test_graph_replay_bitexact(N, logn, monkeypatch):
+    depth, rots = sfhe.direct_sort_params(N, "hip")
+    e = sfhe.Engine("hip", mult_depth=depth, ring_dim=1 << logn, batch_size=N, rotations=rots,
+                    seed=20251205 + N)
+    e.set_quiet(True)
+    x = slotsim.input_vector(N)
+    cfg = slotsim.default_sign_config(N)
+    s = e.sorter(N)
+    ct = e.encrypt(x.tolist())
+    monkeypatch.setenv("SFHE_GRAPH", "1")
+    eager = s.sort(ct, *cfg)             # first sort of the shape: eager
+    assert s.graph_nodes() == 0
+    cap = s.sort(ct, *cfg)               # captured, then launched
+    nodes = s.graph_nodes()
+    rep = s.sort(ct, *cfg)               # replayed
+    assert nodes > 100, nodes
+    ref = eager.download()
+    assert np.array_equal(cap.download(), ref)
+    assert np.array_equal(rep.download(), ref)
+    assert cap.level == rep.level == depth
+    # a different input: copied into the graph's input buffer
+    y = slotsim.input_vector(N)[::-1].copy()
+    ct2 = e.encrypt(y.tolist())
+    g2 = s.sort(ct2, *cfg)
+    monkeypatch.setenv("SFHE_GRAPH", "0")
+    e2 = s.sort(ct2, *cfg)
+    assert np.array_equal(g2.download(), e2.download())
+    err = np.max(np.abs(np.array(e.decrypt(g2)) - np.sort(y)))
+    print(f"N={N}: graph of {nodes} nodes, replay bit-identical to eager; max err {err:.3g}")
+    assert err < 0.01
+
+
+def test_graph_pool_steady(monkeypatch):
+    """Replays allocate nothing new: the graph owns its blocks, the pool
+    stays flat across sorts (outputs are clones the caller frees)."""
+    N, logn = 64, 14
+    depth, rots = sfhe.direct_sort_params(N, "hip")
+    e = sfhe.Engine("hip", mult_depth=depth, ring_dim=1 << logn, batch_size=N, rotations=rots)
+    e.set_quiet(True)
+    monkeypatch.setenv("SFHE_GRAPH", "1")
+    s = e.sorter(N)
+    ct = e.encrypt(slotsim.input_vector(N).tolist())
+    cfg = slotsim.default_sign_config(N)
+    sizes = []
+    for _ in range(8):
+        o = s.sort(ct, *cfg)
+        e.sync()
+        del o
+        sizes.append(e.pool_bytes())
+    assert s.graph_nodes() > 0
+    assert sizes[-1] == sizes[3], sizes
