@@ -444,6 +444,9 @@ __device__ __forceinline__ void nttRound(u64* s, const NttTile& T, uint32_t S0, 
 template <bool INV, bool COL, int LE>
 __device__ __forceinline__ void nttRoundDyn(int b, u64* s, const NttTile& T, uint32_t S0, uint32_t k0,
                                             u64 q, const u64* w, const u64* wS) {
+    if constexpr (LE >= 4) {
+        if (b == 4) return nttRound<INV, COL, LE, 4>(s, T, S0, k0, q, w, wS);
+    }
     if constexpr (LE >= 3) {
         if (b == 3) return nttRound<INV, COL, LE, 3>(s, T, S0, k0, q, w, wS);
     }
@@ -553,6 +556,9 @@ template <bool INV, bool COL, int LE>
 __device__ __forceinline__ void nttRoundDynFP(int b, double* s, const NttTile& T, uint32_t S0, uint32_t k0,
                                               double q, const double* w, const double* wq, double qinv,
                                               bool rowLds) {
+    if constexpr (LE >= 4) {
+        if (b == 4) return nttRoundFP<INV, COL, LE, 4>(s, T, S0, k0, q, w, wq, qinv, rowLds);
+    }
     if constexpr (LE >= 3) {
         if (b == 3) return nttRoundFP<INV, COL, LE, 3>(s, T, S0, k0, q, w, wq, qinv, rowLds);
     }
@@ -2015,8 +2021,16 @@ static void nttRows(sfp_dev* d, const RowGroup& G, int inverse) {
                                d->ninvS, d->logn, twD, twQ, d->qinvD, d->ninvD, d->ninvQ, nttFp());
         });
     };
+    static const int le = [] {  // SFHE_NTT_LE: register-round width experiments (2, 3, 4)
+        const char* v = std::getenv("SFHE_NTT_LE");
+        return v ? std::atoi(v) : 0;
+    }();
+    const int L = le ? le : (small ? 2 : 3);
     if (!inverse) {
-        if (small) {
+        if (L == 4) {
+            pass(k_ntt<false, true, 4>, 4);
+            pass(k_ntt<false, false, 4>, 4);
+        } else if (L == 2) {
             pass(k_ntt<false, true, 2>, 2);
             pass(k_ntt<false, false, 2>, 2);
         } else {
@@ -2024,7 +2038,10 @@ static void nttRows(sfp_dev* d, const RowGroup& G, int inverse) {
             pass(k_ntt<false, false, 3>, 3);
         }
     } else {
-        if (small) {
+        if (L == 4) {
+            pass(k_ntt<true, false, 4>, 4);
+            pass(k_ntt<true, true, 4>, 4);
+        } else if (L == 2) {
             pass(k_ntt<true, false, 2>, 2);
             pass(k_ntt<true, true, 2>, 2);
         } else {

@@ -1,0 +1,111 @@
+"""Build the reference's own test and benchmark sources UNCHANGED against this
+engine (DirectSortTest, SortNBenchmark, CompareTest,
+SignTest, RotationTest, DecomposeTest must compile and link as-is).
+
+Container-only (needs /root/reference; nothing is copied from it): every
+source is compiled where it lies, with the engine's reference-level headers
+(sorting-fhe_amd/csrc/{core,algo}) first on the include path, the reference's
+tests/ directory only for its utils.h / memory_tracker.h, and the gtest /
+google-benchmark shims of tests/cxx/shim (the reference's googletest and
+benchmark submodules are empty).  Each program is linked twice:
+  <name>_oracle  against oracle/_build/libsfhe_oracle.so (runs here, on CPU)
+  <name>_hip     against sorting-fhe_amd/build/libsfhe.so (the product; runs
+                 on the GPU box from the tree: tests/test_gpu_reference_sources.py)
+into tests/cxx/build/ (git-ignored build output).
+
+    python tests/cxx/reference_harness.py [--jobs 8]
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+REF = os.environ.get("SFHE_REFERENCE", "/root/reference")
+OUT = os.path.join(HERE, "build")
+CSRC = os.path.join(ROOT, "sorting-fhe_amd", "csrc")
+SHIM = os.path.join(HERE, "shim")
+LIBS = {
+    "oracle": (os.path.join(ROOT, "oracle", "_build"), "sfhe_oracle"),
+    "hip": (os.path.join(ROOT, "sorting-fhe_amd", "build"), "sfhe"),
+}
+
+# program -> (sources relative to the reference, needs gtest_main, needs memory_tracker)
+PROGRAMS = {
+    "DirectSortTest": (["tests/DirectSortTest.cpp"], True, True),
+    "CompareTest": (["tests/CompareTest.cpp"], False, False),
+    "SignTest": (["tests/SignTest.cpp"], False, False),
+    "RotationTest": (["tests/RotationTest.cpp"], True, False),
+    "DecomposeTest": (["tests/DecomposeTest.cpp"], True, False),
+    "SortNBenchmark": (["benchmarks/SortNBenchmark.cpp"], False, False),
+}
+
+
+def available() -> bool:
+    return os.path.isdir(os.path.join(REF, "tests")) and os.path.isfile(os.path.join(REF, "tests", "DirectSortTest.cpp"))
+
+
+def flags():
+    return ["-O2", "-std=c++17", "-fopenmp", "-DENABLE_PRINT_PT",
+            "-I" + os.path.join(CSRC, "core"), "-I" + os.path.join(CSRC, "algo"), "-I" + CSRC,
+            "-I" + os.path.join(ROOT, "include"), "-I" + SHIM, "-I" + os.path.join(REF, "tests"),
+            "-w"]
+
+
+def compile_obj(src: str, obj: str):
+    os.makedirs(os.path.dirname(obj), exist_ok=True)
+    if os.path.exists(obj) and os.path.getmtime(obj) >= os.path.getmtime(src):
+        return
+    subprocess.run(["g++"] + flags() + ["-c", src, "-o", obj], check=True)
+
+
+def build(jobs: int = 8, programs=None):
+    if not available():
+        raise FileNotFoundError(f"reference sources not found under {REF}")
+    programs = programs or list(PROGRAMS)
+    objs = {}
+    work = []
+    extra = {"gtest_main": os.path.join(SHIM, "gtest_main.cc"),
+             "memory_tracker": os.path.join(REF, "tests", "memory_tracker.cpp")}
+    for k, src in extra.items():
+        objs[k] = os.path.join(OUT, "obj", k + ".o")
+        work.append((src, objs[k]))
+    for p in programs:
+        srcs, _, _ = PROGRAMS[p]
+        for s in srcs:
+            o = os.path.join(OUT, "obj", p + "_" + os.path.basename(s) + ".o")
+            objs[(p, s)] = o
+            work.append((os.path.join(REF, s), o))
+    with ThreadPoolExecutor(jobs) as ex:
+        for f in [ex.submit(compile_obj, s, o) for s, o in work]:
+            f.result()
+    built = {}
+    for p in programs:
+        srcs, gmain, mtrack = PROGRAMS[p]
+        o = [objs[(p, s)] for s in srcs]
+        if gmain:
+            o.append(objs["gtest_main"])
+        if mtrack:
+            o.append(objs["memory_tracker"])
+        for backend, (libdir, lib) in LIBS.items():
+            exe = os.path.join(OUT, f"{p}_{backend}")
+            subprocess.run(["g++", "-fopenmp", "-o", exe] + o +
+                           ["-L" + libdir, "-l" + lib, "-Wl,-rpath," + libdir, "-lpthread"], check=True)
+            built[(p, backend)] = exe
+    return built
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--jobs", type=int, default=8)
+    a = ap.parse_args()
+    for (p, b), exe in sorted(build(a.jobs).items()):
+        print(f"{p:16s} {b:7s} {exe}")
+
+
+if __name__ == "__main__":
+    sys.exit(main())
