@@ -780,16 +780,33 @@ class SfheInternal {
         return b->ptr;
     }
 
+    // Coefficient-domain rows of pt's encoding at `level` for the rows of map
+    // m; values whose scaled coefficients need more than 62 bits are encoded
+    // at scale / 2^shift and the residues multiplied by 2^shift mod q_i.
+    static void encodeRows(SfheContextState* s, const Plaintext& pt, uint32_t level, uint64_t* dst,
+                           sfp_limbs m, std::vector<int64_t>* keep = nullptr) {
+        std::vector<int64_t> local;
+        std::vector<int64_t>& coeffs = keep ? *keep : local;
+        const int shift = ckks_encode(pt->values, pt->slots, s->n, s->scale[level], coeffs);
+        sfp_load_i64(s->dev, dst, coeffs.data(), m);
+        if (shift) {
+            std::vector<u64> k(m.count);
+            for (uint32_t i = 0; i < m.count; ++i) {
+                const u64 q = s->primes[sfp_prime_of(m, i)];
+                k[i] = (u64)(((unsigned __int128)1 << shift) % q);
+            }
+            sfp_mul_const(s->dev, dst, dst, k.data(), m);
+        }
+    }
+
     static const uint64_t* encoded(CC* cc, const Plaintext& pt, uint32_t level) {
         SfheContextState* s = cc->st.get();
         std::lock_guard<std::mutex> g(pt->encMutex);
         uint32_t ell = s->ellOf(level);
         if (s->fullScope && s->rows(ell) != ell) SFHE_THROW("internal: encoding scope");
         if (s->fullScope) {  // every row, uncached (a sharded context caches local rows)
-            std::vector<int64_t> coeffs;
-            ckks_encode(pt->values, pt->slots, s->n, s->scale[level], coeffs);
             auto buf = s->alloc(s->polyWords(level));
-            sfp_load_i64(s->dev, buf->ptr, coeffs.data(), s->qmap(ell));
+            encodeRows(s, pt, level, buf->ptr, s->qmap(ell));
             sfp_ntt(s->dev, buf->ptr, s->qmap(ell), 0);
             s->scopeKeep.push_back(buf);
             return buf->ptr;
@@ -820,10 +837,9 @@ class SfheInternal {
                     }
         }
         std::vector<int64_t> coeffs;
-        ckks_encode(pt->values, pt->slots, s->n, s->scale[level], coeffs);
         const size_t pw = s->polyWords(level);
         auto buf = s->alloc(pw);
-        sfp_load_i64(s->dev, buf->ptr, coeffs.data(), s->qmap(ell));
+        encodeRows(s, pt, level, buf->ptr, s->qmap(ell), &coeffs);
         if (std::getenv("SFHE_TRACE")) {
             uint64_t f = 1469598103934665603ull;
             for (int64_t v : coeffs) f = (f ^ (uint64_t)v) * 1099511628211ull;

@@ -7,6 +7,7 @@
 // the vector with period `slots` across all n/2 slots (a-12(i)).
 // The transform is the standard O(S log S) "special FFT" over the rotation
 // group <5> mod 2n (Cheon-Kim-Kim-Song).
+#include <algorithm>
 #include <cmath>
 #include <complex>
 #include <vector>
@@ -97,23 +98,35 @@ void fftSpecial(std::complex<double>* v, uint32_t size, const FFTTables& t) {
 
 }  // namespace
 
-void ckks_encode(const std::vector<std::complex<double>>& vals, uint32_t slots, uint32_t n,
-                 double scale, std::vector<int64_t>& coeffs) {
+int ckks_encode(const std::vector<std::complex<double>>& vals, uint32_t slots, uint32_t n,
+                double scale, std::vector<int64_t>& coeffs) {
     const FFTTables& t = tables(n);
     std::vector<std::complex<double>> u(slots, 0.0);
     for (size_t i = 0; i < vals.size() && i < slots; ++i) u[i] = vals[i];
     fftSpecialInv(u.data(), slots, t);
     coeffs.assign(n, 0);
     const uint32_t gap = (n / 2) / slots;
-    const double lim = 9.0e18;
-    for (uint32_t i = 0; i < slots; ++i) {
-        double re = std::nearbyint(u[i].real() * scale);
-        double im = std::nearbyint(u[i].imag() * scale);
-        if (std::fabs(re) > lim || std::fabs(im) > lim)
-            SFHE_THROW("encoded value exceeds 63 bits (|value * scale| too large)");
-        coeffs[(size_t)i * gap] = (int64_t)re;
-        coeffs[(size_t)n / 2 + (size_t)i * gap] = (int64_t)im;
+    // Coefficients beyond 62 bits (large values at a large scale, e.g.
+    // RotationTest's [0, 255) at scale 2^59): like OpenFHE's CKKS encoder,
+    // encode value * scale / 2^shift and let the caller multiply every
+    // residue by 2^shift (the low `shift` bits are below double precision
+    // anyway: a double carries 53 significant bits).
+    double mx = 0.0;
+    for (uint32_t i = 0; i < slots; ++i)
+        mx = std::max(mx, std::max(std::fabs(u[i].real()), std::fabs(u[i].imag())) * scale);
+    if (!std::isfinite(mx)) SFHE_THROW("encoded value is not finite");
+    int shift = 0;
+    while (mx >= 4.0e18) {  // < 2^62 after the shift
+        mx *= 0.5;
+        ++shift;
     }
+    if (shift > 60) SFHE_THROW("encoded value exceeds the supported range (|value * scale| >= 2^122)");
+    const double sc = std::ldexp(scale, -shift);
+    for (uint32_t i = 0; i < slots; ++i) {
+        coeffs[(size_t)i * gap] = (int64_t)std::nearbyint(u[i].real() * sc);
+        coeffs[(size_t)n / 2 + (size_t)i * gap] = (int64_t)std::nearbyint(u[i].imag() * sc);
+    }
+    return shift;
 }
 
 void ckks_decode(const std::vector<double>& c, uint32_t slots, uint32_t n,

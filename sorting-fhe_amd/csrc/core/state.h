@@ -195,8 +195,11 @@ static inline uint64_t sf_splitmix64(uint64_t x) {
 }
 
 // CKKS special-FFT encoder (encoder.cpp)
-void ckks_encode(const std::vector<std::complex<double>>& v, uint32_t slots, uint32_t n,
-                 double scale, std::vector<int64_t>& coeffs);
+// Returns shift >= 0: the coefficients are round(value * scale / 2^shift)
+// (shift > 0 only when value * scale needs more than 62 bits); the caller
+// multiplies the residues by 2^shift.
+int ckks_encode(const std::vector<std::complex<double>>& v, uint32_t slots, uint32_t n,
+                double scale, std::vector<int64_t>& coeffs);
 void ckks_decode(const std::vector<double>& coeffs, uint32_t slots, uint32_t n,
                  std::vector<std::complex<double>>& out);
 
