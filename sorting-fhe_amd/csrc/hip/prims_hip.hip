@@ -1190,12 +1190,24 @@ __device__ __forceinline__ double fpSourceY(u64 s, double qd, double iv, double 
 // doubles (signed when centred), a 60-bit source as y = yh 2^30 + yl (two
 // exact doubles, the second with the multiplier mod * 2^30 mod p), and for
 // integer-target blocks every source as its canonical residue.  Phase 2:
-// each wave takes targets k = wave, wave + 4, ... for its 64 coefficients:
-// the source-major y reads are conflict-free and the multipliers are
-// wave-uniform LDS broadcasts.  Many small blocks (n / 64 per chunk) keep
-// many waves per SIMD in flight where one thread per coefficient pair had 2.
+// lane = coefficient; wave w takes the target groups w, w + 4, ... of
+// kConvTpi targets each: one y read from LDS feeds kConvTpi independent
+// product chains, the source-major y reads are conflict-free and the
+// multipliers are wave-uniform LDS broadcasts.
 // Arithmetic and outputs as k_conv (canonical residues, bit-identical).
-constexpr int kConvCoefs = 256;  // = kThreads: one coefficient column per thread in phase 1
+// Coefficients per block (a multiple of 64: phase 2 works on 64-coefficient
+// chunks x kConvTpi-target groups).  A/B on the sort (same box): 64 / 128 /
+// 256 gave 58.6 / 57.7 / 57.8 ms; smaller blocks put more of them on a CU,
+// larger ones repeat phase 1 less often.
+#ifndef SFHE_CONV_COEFS
+#define SFHE_CONV_COEFS 128
+#endif
+constexpr int kConvCoefs = SFHE_CONV_COEFS;
+#ifndef SFHE_CONV_TPI
+#define SFHE_CONV_TPI 4
+#endif
+constexpr int kConvTpi = SFHE_CONV_TPI;  // FP64 targets per phase-2 iteration
+static_assert(kConvChunk % kConvTpi == 0 && kConvCoefs % 64 == 0 && kConvCoefs <= kThreads, "conversion block shape");
 
 template <int NS>
 __global__ __launch_bounds__(kThreads) void k_convf(const ConvJobs J, const sf_barrett* __restrict__ bar,
@@ -1253,9 +1265,9 @@ __global__ __launch_bounds__(kThreads) void k_convf(const ConvJobs J, const sf_b
     __syncthreads();
     const uint32_t x0 = blockIdx.x * X, lane = threadIdx.x % 64, w = threadIdx.x / 64;
     const bool cen = c.centered;
-    // phase 1: y for every (source, coefficient) pair (thread = coefficient column)
-    for (uint32_t i = 0; i < ns; ++i) {
-        const uint32_t cx = threadIdx.x;
+    // phase 1: y for every (source, coefficient) pair
+    for (uint32_t e = threadIdx.x; e < ns * X; e += kThreads) {
+        const uint32_t i = e / X, cx = e % X;
         const u64 s = c.src[((size_t)i << logn) + x0 + cx];
         const sf_barrett B = sB[i];
         if (!fpBlock) {
@@ -1270,23 +1282,50 @@ __global__ __launch_bounds__(kThreads) void k_convf(const ConvJobs J, const sf_b
         }
     }
     __syncthreads();
-    // phase 2: this wave's targets for every coefficient of the block
-    for (uint32_t kc = w * 64; kc < tc * X; kc += WAVES * 64) {  // wave w: coefficients [64w, 64w+64) of every target
+    // phase 2: wave w takes coefficients [64w, 64w+64) of every target.
+    // FP64 targets go kConvTpi at a time: each y read from LDS feeds
+    // kConvTpi independent product chains (ILP; a quarter of the y reads).
+    if (fpBlock) {
+        // work items (64-coefficient chunk, group of kConvTpi targets), wave w
+        // takes items w, w + WAVES, ...
+        constexpr uint32_t CH = X / 64;
+        const uint32_t items = CH * ((tc + kConvTpi - 1) / kConvTpi);
+        for (uint32_t it = w; it < items; it += WAVES) {
+            const uint32_t cx = (it % CH) * 64 + lane, k = (it / CH) * kConvTpi;
+            double a[kConvTpi], pd[kConvTpi];
+#pragma unroll
+            for (int u = 0; u < kConvTpi; ++u) {
+                a[u] = 0.0;
+                pd[u] = (double)tB[min(k + u, tc - 1)].q;
+            }
+#pragma unroll
+            for (int i = 0; i < NS; ++i)
+                if ((uint32_t)i < ns) {
+                    const double y = __longlong_as_double(yL[i * X + cx]);
+#pragma unroll
+                    for (int u = 0; u < kConvTpi; ++u)
+                        a[u] += fpMulMod(y, sD[i * C + k + u], sQ[i * C + k + u], pd[u]);
+                }
+#pragma unroll
+            for (int b = 0; b < NB; ++b)
+                if ((uint32_t)b < c.nbig) {
+                    const double y = yH[b * X + cx];
+#pragma unroll
+                    for (int u = 0; u < kConvTpi; ++u)
+                        a[u] += fpMulMod(y, hDs[b * C + k + u], hQs[b * C + k + u], pd[u]);
+                }
+#pragma unroll
+            for (int u = 0; u < kConvTpi; ++u)
+                if (k + u < tc)
+                    c.dst[((size_t)tRow[k + u] << logn) + x0 + cx] = (u64)fpReduce(a[u], pd[u], tQi[k + u]);
+        }
+        return;
+    }
+    for (uint32_t kc = w * 64; kc < tc * X; kc += WAVES * 64) {  // integer targets, one at a time
         const uint32_t k = kc / X, cx = kc % X + lane;
         const sf_barrett B = tB[k];
         u64 out;
-        if (fpBlock) {
-            const double pd = (double)B.q;
-            double a = 0.0;
-#pragma unroll
-            for (int i = 0; i < NS; ++i)
-                if ((uint32_t)i < ns)
-                    a += fpMulMod(__longlong_as_double(yL[i * X + cx]), sD[i * C + k], sQ[i * C + k], pd);
-#pragma unroll
-            for (int b = 0; b < NB; ++b)
-                if ((uint32_t)b < c.nbig) a += fpMulMod(yH[b * X + cx], hDs[b * C + k], hQs[b * C + k], pd);
-            out = (u64)fpReduce(a, pd, tQi[k]);
-        } else {
+        {
             Acc s0{0, 0};
             u64 neg = 0;
 #pragma unroll
@@ -1444,15 +1483,14 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
     }
     __syncthreads();
     const uint32_t x0 = blockIdx.x * X, lane = threadIdx.x % 64, w = threadIdx.x / 64;
-    for (uint32_t i = 0; i < ns; ++i) {
-        const uint32_t cx = threadIdx.x;
+    for (uint32_t e = threadIdx.x; e < ns * X; e += kThreads) {
+        const uint32_t i = e / X, cx = e % X;
         const u64 s = J.src[((size_t)i << logn) + x0 + cx];
         yL[i * X + cx] = fpSourceY(s, (double)sB[i].q, sInvD[i], sInvQ[i], sQi[i], true);
     }
     __syncthreads();
     const double qld = (double)bar[A.l].q;
-    {  // the dropped row: r = (a_l - conv_l) * P^-1 mod q_l, centred (thread = coefficient)
-        const uint32_t cx = threadIdx.x;
+    for (uint32_t cx = threadIdx.x; cx < X; cx += kThreads) {  // the dropped row: r = (a_l - conv_l) * P^-1 mod q_l, centred
         double cl = 0.0;
 #pragma unroll
         for (int i = 0; i < NS; ++i)
@@ -1464,18 +1502,39 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
                            true);
     }
     __syncthreads();
-    for (uint32_t kc = w * 64; kc < tc * X; kc += WAVES * 64) {  // wave w: coefficients [64w, 64w+64) of every target
+    if (fpBlock) {  // kConvTpi targets at a time, work items as k_convf
+        constexpr uint32_t CH = X / 64;
+        const uint32_t items = CH * ((tc + kConvTpi - 1) / kConvTpi);
+        for (uint32_t it = w; it < items; it += WAVES) {
+            const uint32_t cx = (it % CH) * 64 + lane, k = (it / CH) * kConvTpi;
+            const double r = rL[cx];
+            double a[kConvTpi], pd[kConvTpi];
+#pragma unroll
+            for (int u = 0; u < kConvTpi; ++u) {
+                const uint32_t kk = min(k + u, tc - 1);
+                pd[u] = (double)tB[kk].q;
+                a[u] = fpMulMod(r, tPd[kk], tPq[kk], pd[u]);
+            }
+#pragma unroll
+            for (int i = 0; i < NS; ++i)
+                if ((uint32_t)i < ns) {
+                    const double y = yL[i * X + cx];
+#pragma unroll
+                    for (int u = 0; u < kConvTpi; ++u)
+                        a[u] += fpMulMod(y, sD[i * C + k + u], sQ[i * C + k + u], pd[u]);
+                }
+#pragma unroll
+            for (int u = 0; u < kConvTpi; ++u)
+                if (k + u < tc)
+                    J.dst[((size_t)tRow[k + u] << logn) + x0 + cx] = (u64)fpReduce(a[u], pd[u], tQi[k + u]);
+        }
+        return;
+    }
+    for (uint32_t kc = w * 64; kc < tc * X; kc += WAVES * 64) {  // integer targets, one at a time
         const uint32_t k = kc / X, cx = kc % X + lane;
         const double r = rL[cx];
         u64 out;
-        if (fpBlock) {
-            const double pd = (double)tB[k].q;
-            double a = fpMulMod(r, tPd[k], tPq[k], pd);
-#pragma unroll
-            for (int i = 0; i < NS; ++i)
-                if ((uint32_t)i < ns) a += fpMulMod(yL[i * X + cx], sD[i * C + k], sQ[i * C + k], pd);
-            out = (u64)fpReduce(a, pd, tQi[k]);
-        } else {
+        {
             const sf_barrett B = tB[k];
             Acc s0{0, 0};
             u64 neg = 0;
