@@ -157,6 +157,12 @@ int sfhe_doubled_sinc_coeffs(uint32_t N, double* out, size_t cap, size_t* count)
  * debug != 0 uses DebugEncryption, so sort() runs the reference's three
  * PRINT_PT decrypts ("as-test" timing); 0 = plain Encryption ("pure"). */
 int sfhe_sorter_create(sfhe_ctx* c, uint32_t N, int debug, sfhe_sorter** out);
+/* The same with the rotation-key list the DirectSort<N> constructor receives
+ * (sort_algo.h:74-81, its rotIndices argument: the amounts RotationComposer
+ * uses as single steps); NULL / 0 = the getSizeParameters list.  The context
+ * must hold keys for them (sfhe_keygen's rotation list). */
+int sfhe_sorter_create_rot(sfhe_ctx* c, uint32_t N, int debug, const int32_t* rotations, size_t nrot,
+                           sfhe_sorter** out);
 void sfhe_sorter_destroy(sfhe_sorter* s);
 /* DirectSort<N>::sort (sort_algo.h:752-774).  Sets the input's slots to
  * the partition size as the reference does (sort_algo.h:711). */
@@ -171,6 +177,14 @@ int sfhe_sorter_place(sfhe_sorter* s, const sfhe_ct* rank, sfhe_ct* in, sfhe_ct*
  * (SFHE_GRAPH=0 keeps every sort eager; debug sorters never capture).
  * 0 while no graph exists. */
 int sfhe_sorter_graph_nodes(const sfhe_sorter* s, uint64_t* nodes);
+/* DirectSort<N>::sort_hybrid1 (sort_algo.h:1213-1229): constructRank, then
+ * rotationIndexCheckHybrid1 (:1067-1209, MEHP24 indicatorAdv placement,
+ * mehp24_utils.cpp:166-174, :246-261).  Needs ring dimension >= 2 N^2 for
+ * N <= 256 and the DirectSortH1Test keys (sfhe_hybrid1_params). */
+int sfhe_sorter_sort_hybrid1(sfhe_sorter* s, sfhe_ct* in, int n, int dg, int df, sfhe_ct** out);
+/* Depth and rotation keys of tests/DirectSortH1Test.cpp:36-117 for N
+ * (the reference keeps them in the test; ring 2^17, HEStd_128_classic). */
+int sfhe_hybrid1_params(uint32_t N, uint32_t* mult_depth, int32_t* rotations, size_t cap, size_t* count);
 
 /* Decomposer<N>::decompose (rotation.h:54-102); algo 0 NAF, 1 BNAF, 2 BINARY.
  * N in {4..1024}; writes (value, stepSize) pairs. */

@@ -148,3 +148,84 @@ def direct_sort(x, N, ring, cfg=None):
     cfg = cfg or default_sign_config(N)
     rank = construct_rank(np.asarray(x, dtype=np.float64), N, ring, cfg)
     return rotation_index_check(rank, np.asarray(x, dtype=np.float64), N, ring), rank
+
+
+# ---- hybrid placement I (sort_hybrid1): src/sort_algo.h:815-891 (matrix
+# helpers), :1067-1229 (rotationIndexCheckHybrid1, sort_hybrid1);
+# src/mehp24/mehp24_utils.cpp:166-174 (indicatorAdv), :246-261 (signAdv) ----
+def sign_adv(x, dg: int, df: int):
+    """signAdv: dg x g3, (df - 1) x f3, then 1/2 + f3/2 (coeffF3_final)."""
+    y = np.asarray(x, dtype=np.float64)
+    for _ in range(dg):
+        y = odd_poly(G3, y)
+    for _ in range(df - 1):
+        y = odd_poly(F3, y)
+    return 0.5 + 0.5 * odd_poly(F3, y)
+
+
+def indicator_adv(c, b: float, dg: int, df: int):
+    tmp = np.asarray(c, dtype=np.float64) / b
+    return sign_adv(tmp + 0.5 / b, dg, df) * (1.0 - sign_adv(tmp - 0.5 / b, dg, df))
+
+
+def hybrid1_dg(N: int) -> int:
+    return int((math.log2(N) + 1) / 2)  # uint32_t dg_i = (log2(N) + 1) / 2 (:1126)
+
+
+def hybrid1_depth(N: int, cfg=None) -> int:
+    """rank + [2 + 4 (dg_i + 2)] + 3."""
+    n, dg, df = cfg or default_sign_config(N)
+    return 2 + sign_depth(n, dg, df) + 2 + 4 * (hybrid1_dg(N) + 2) + 3
+
+
+def _binary_path(idx: int, m: int):
+    bits = int(math.ceil(math.log2(m)))
+    return [(idx >> (bits - 1 - i)) & 1 for i in range(bits)]
+
+
+def sum_columns_to_target(c, m: int, col: int):
+    step = m >> 1
+    for bit in _binary_path(col, m):
+        c = c + rot(c, -step if bit else step)
+        step >>= 1
+    msk = np.zeros(len(c))
+    msk[np.arange(m) * m + col] = 1.0
+    return c * msk
+
+
+def transpose_column_target(c, m: int, row: int):
+    step = m * (m - 1) // 2
+    for bit in _binary_path(row, m):
+        c = c + rot(c, -step if bit else step)
+        step >>= 1
+    msk = np.zeros(len(c))
+    msk[m * row + np.arange(m)] = 1.0
+    return c * msk
+
+
+def rotation_index_check_hybrid1(rank, x, N, ring):
+    maxa = 256
+    num_slots, num_batch = (ring // 2, N // maxa) if N > maxa else (N * N, 1)
+    M = min(N, maxa)
+    rk = np.tile(np.asarray(rank, dtype=np.float64), num_slots // N)
+    xs = np.tile(np.asarray(x, dtype=np.float64), num_slots // N)
+    rots_rank = [rot(rk, k * maxa) for k in range(num_batch)]
+    rots_in = [rot(xs, k * maxa) for k in range(num_batch)]
+    dg = hybrid1_dg(N)
+    out = np.zeros(num_slots)
+    for b in range(num_batch):
+        sub = np.zeros(num_slots)
+        for i in range(M):
+            sub[i * M:(i + 1) * M] = b * M + i
+        acc = np.zeros(num_slots)
+        for k in range(num_batch):
+            acc = acc + rots_in[k] * indicator_adv(sub - rots_rank[k], N, dg, 2)
+        acc = sum_columns_to_target(acc, N // num_batch, b)
+        out = out + transpose_column_target(acc, N // num_batch, b)
+    return out[:N]
+
+
+def sort_hybrid1(x, N, ring, cfg=None):
+    cfg = cfg or default_sign_config(N)
+    rank = construct_rank(np.asarray(x, dtype=np.float64), N, ring, cfg)
+    return rotation_index_check_hybrid1(rank, np.asarray(x, dtype=np.float64), N, ring), rank

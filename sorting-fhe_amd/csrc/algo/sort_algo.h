@@ -429,6 +429,122 @@ class DirectSort : public SortBase<N> {
         return output;
     }
 
+    // ---- hybrid placement I (reference :815-891,
+    // :1067-1229).  Rank as DirectSort; placement by an indicator matrix:
+    // with M = min(N, 256) and num_slots = M*M per batch, slot (i, j) of
+    // batch b holds indicator(b*M + i - rank_{(j + k M) mod N}) * x_{(j + k M) mod N}
+    // summed over the rank rotations k; the row sums land in column b
+    // (sumColumnsToTarget) and that column becomes row b (transposeColumnTarget),
+    // so the first N slots of the sum over batches hold the sorted array.
+    std::vector<bool> getBinaryPath(size_t columnIndex, size_t matrixSize) {
+        const size_t bits = LOG2(matrixSize);
+        std::vector<bool> path(bits);
+        for (size_t i = 0; i < bits; ++i) path[i] = (columnIndex >> (bits - 1 - i)) & 1;
+        return path;
+    }
+
+    // sums the matrixSize entries of every row into column columnIndex (a
+    // binary tree of rotations by +-matrixSize/2, ..., 1: left child on 0,
+    // right child on 1), optionally masking everything else out
+    Ciphertext<DCRTPoly> sumColumnsToTarget(Ciphertext<DCRTPoly> c, const size_t matrixSize,
+                                            const size_t columnIndex, bool maskOutput) {
+        const auto path = getBinaryPath(columnIndex, matrixSize);
+        size_t step = matrixSize >> 1;
+        c->SetSlots((uint32_t)(matrixSize * matrixSize));
+        for (size_t i = 0; i < path.size(); ++i, step >>= 1)
+            c = m_cc->EvalAdd(c, rot.rotate(c, path[i] ? -(int)step : (int)step));
+        if (maskOutput) {
+            const Plaintext& pmsk = maskMemo({4, (int)matrixSize, (int)columnIndex, (int)c->GetLevel(), 0},
+                                             [&](auto& v) {
+                                                 std::vector<double> msk(matrixSize * matrixSize, 0.0);
+                                                 for (size_t i = 0; i < matrixSize; ++i)
+                                                     msk[matrixSize * i + columnIndex] = 1.0;
+                                                 v.push_back(m_cc->MakeCKKSPackedPlaintext(
+                                                     msk, 1, c->GetLevel(), nullptr,
+                                                     (uint32_t)(matrixSize * matrixSize)));
+                                             })[0];
+            c = m_cc->EvalMult(c, pmsk);
+        }
+        return c;
+    }
+
+    // moves column rowIndex to row rowIndex: rotations by
+    // +-M(M-1)/2, +-M(M-1)/4, ..., the path of rowIndex choosing the sign
+    Ciphertext<DCRTPoly> transposeColumnTarget(Ciphertext<DCRTPoly> c, const size_t matrixSize,
+                                               const size_t rowIndex, bool maskOutput) {
+        const auto path = getBinaryPath(rowIndex, matrixSize);
+        size_t step = matrixSize * (matrixSize - 1) / 2;
+        c->SetSlots((uint32_t)(matrixSize * matrixSize));
+        for (size_t i = 0; i < path.size(); ++i, step >>= 1)
+            c = m_cc->EvalAdd(c, rot.rotate(c, path[i] ? -(int)step : (int)step));
+        if (maskOutput) {
+            const Plaintext& pmsk = maskMemo({5, (int)matrixSize, (int)rowIndex, (int)c->GetLevel(), 0},
+                                             [&](auto& v) {
+                                                 std::vector<double> msk(matrixSize * matrixSize, 0.0);
+                                                 for (size_t i = 0; i < matrixSize; ++i)
+                                                     msk[matrixSize * rowIndex + i] = 1.0;
+                                                 v.push_back(m_cc->MakeCKKSPackedPlaintext(
+                                                     msk, 1, c->GetLevel(), nullptr,
+                                                     (uint32_t)(matrixSize * matrixSize)));
+                                             })[0];
+            c = m_cc->EvalMult(c, pmsk);
+        }
+        return c;
+    }
+
+    Ciphertext<DCRTPoly> rotationIndexCheckHybrid1(const Ciphertext<DCRTPoly>& ctx_Rank,
+                                                   const Ciphertext<DCRTPoly>& input_array,
+                                                   PrivateKey<DCRTPoly> sk) {
+        (void)sk;  // (unused by the reference as well)
+        constexpr size_t maxArraySize = 256;
+        const size_t num_slots = N > (int)maxArraySize ? (size_t)max_batch : (size_t)N * N;
+        const size_t num_batch = N > (int)maxArraySize ? N / maxArraySize : 1;
+        const size_t M = std::min((size_t)N, maxArraySize);
+        if (num_slots > (size_t)max_batch || M * M > num_slots)
+            throw OpenFHEException("sort_hybrid1: N*N slots exceed the ring (needs ring dimension >= 2 N^2)");
+        ctx_Rank->SetSlots((uint32_t)num_slots);
+        input_array->SetSlots((uint32_t)num_slots);
+        std::vector<Ciphertext<DCRTPoly>> rots_Rank(num_batch), rots_Input(num_batch);
+        for (size_t k = 0; k < num_batch; ++k) {
+            rots_Rank[k] = rot.rotate(ctx_Rank, (int)(k * maxArraySize));
+            rots_Input[k] = rot.rotate(input_array, (int)(k * maxArraySize));
+        }
+        // dg_i = (log2 N + 1) / 2 truncated (reference :1126-1127)
+        const uint32_t dg_i = (uint32_t)((std::log2((double)N) + 1) / 2);
+        const uint32_t df_i = 2;
+        std::vector<Ciphertext<DCRTPoly>> Masked(num_batch);
+        const int lanes = std::min((int)num_batch, m_cc->LaneCount());
+        m_cc->ForkLanes(lanes);
+        sfhe::parallelLanes(m_cc, lanes, (int)num_batch, [&](int bi) {
+            const size_t b = (size_t)bi;
+            // subMask_b[i M + j] = b M + i (reference :1089-1098)
+            const Plaintext& subMask = maskMemo({6, bi, 0, (int)ctx_Rank->GetLevel(), (int)num_slots}, [&](auto& v) {
+                std::vector<double> m(num_slots, 0.0);
+                for (size_t i = 0; i < M; ++i)
+                    for (size_t j = 0; j < M; ++j) m[i * M + j] = (double)(b * M + i);
+                v.push_back(m_cc->MakeCKKSPackedPlaintext(m, 1, ctx_Rank->GetLevel(), nullptr,
+                                                          (uint32_t)num_slots));
+            })[0];
+            auto subMasked = this->getZero()->Clone();
+            subMasked->SetSlots((uint32_t)num_slots);
+            for (size_t k = 0; k < num_batch; ++k) {
+                auto rotationMask = m_cc->EvalSub(subMask, rots_Rank[k]);
+                rotationMask = mehp24::utils::indicatorAdv(rotationMask, (double)N, dg_i, df_i);
+                subMasked = m_cc->EvalAdd(subMasked, m_cc->EvalMult(rots_Input[k], rotationMask));
+            }
+            subMasked = sumColumnsToTarget(subMasked, N / num_batch, b, true);
+            Masked[b] = transposeColumnTarget(subMasked, N / num_batch, b, true);
+        });
+        m_cc->JoinLanes();
+        return m_cc->EvalAddMany(Masked);
+    }
+
+    Ciphertext<DCRTPoly> sort_hybrid1(const Ciphertext<DCRTPoly>& input_array, SignFunc SignFunc,
+                                      SignConfig& Cfg, PrivateKey<DCRTPoly> sk) {
+        auto ctx_Rank = constructRank(input_array, SignFunc, Cfg);
+        return rotationIndexCheckHybrid1(ctx_Rank, input_array, sk);
+    }
+
     // ---- hipGraph replay (north_star: "the Chebyshev tree / rotations /
     // rank-matrix EvalMults run as a hipGraph") ----
     // The op sequence of sort() depends only on (N, the input's level and

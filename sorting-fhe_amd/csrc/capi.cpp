@@ -96,6 +96,7 @@ struct SorterBase {
     virtual Ct sort(const Ct& in, SignConfig& cfg) = 0;
     virtual Ct rank(const Ct& in, SignConfig& cfg) = 0;
     virtual Ct place(const Ct& rank, const Ct& in) = 0;
+    virtual Ct hybrid1(const Ct& in, SignConfig& cfg, const PrivateKey<DCRTPoly>& sk) = 0;
     virtual size_t graphNodes() const = 0;
 };
 
@@ -110,6 +111,9 @@ struct Sorter : SorterBase {
         return ds.constructRank(in, SignFunc::CompositeSign, cfg);
     }
     Ct place(const Ct& r, const Ct& in) override { return ds.rotationIndexCheckN(r, in); }
+    Ct hybrid1(const Ct& in, SignConfig& cfg, const PrivateKey<DCRTPoly>& sk) override {
+        return ds.sort_hybrid1(in, SignFunc::CompositeSign, cfg, sk);
+    }
     size_t graphNodes() const override { return ds.graphNodes(); }
 };
 
@@ -368,14 +372,21 @@ int sfhe_doubled_sinc_coeffs(uint32_t N, double* out, size_t cap, size_t* count)
 }
 
 int sfhe_sorter_create(sfhe_ctx* c, uint32_t N, int debug, sfhe_sorter** out) {
+    return sfhe_sorter_create_rot(c, N, debug, nullptr, 0, out);
+}
+
+int sfhe_sorter_create_rot(sfhe_ctx* c, uint32_t N, int debug, const int32_t* rotations, size_t nrot,
+                           sfhe_sorter** out) {
     REQUIRE(c && out, "null argument");
     REQUIRE(validN(N), "N must be a power of two in [4, 1024]");
     REQUIRE(c->keys.publicKey, "sfhe_keygen must be called first");
+    REQUIRE(!nrot || rotations, "null rotation list");
     return guard([&] {
         std::shared_ptr<Encryption> enc =
             debug ? std::shared_ptr<Encryption>(std::make_shared<DebugEncryption>(c->cc, c->keys))
                   : std::make_shared<Encryption>(c->cc, c->keys.publicKey);
-        const auto rot = sfhe::sizeParams((int)N)->rotations;
+        const auto rot = rotations ? std::vector<int>(rotations, rotations + nrot)
+                                   : sfhe::sizeParams((int)N)->rotations;
         auto s = std::make_unique<sfhe_sorter>();
         s->ctx = c;
         switch (N) {
@@ -410,6 +421,25 @@ int sfhe_sorter_rank(sfhe_sorter* s, const sfhe_ct* in, int n, int dg, int df, s
 int sfhe_sorter_place(sfhe_sorter* s, const sfhe_ct* rank, sfhe_ct* in, sfhe_ct** out) {
     REQUIRE(s && rank && in && out, "null argument");
     return guard([&] { *out = wrap(s->impl->place(rank->ct, in->ct)); });
+}
+
+int sfhe_sorter_sort_hybrid1(sfhe_sorter* s, sfhe_ct* in, int n, int dg, int df, sfhe_ct** out) {
+    REQUIRE(s && in && out, "null argument");
+    REQUIRE(s->ctx->keys.secretKey, "sfhe_keygen must be called first");
+    return guard([&] {
+        Quiet q(s->ctx->quiet);
+        auto cfg = cfgOf(n, dg, df);
+        *out = wrap(s->impl->hybrid1(in->ct, cfg, s->ctx->keys.secretKey));
+    });
+}
+
+int sfhe_hybrid1_params(uint32_t N, uint32_t* mult_depth, int32_t* rotations, size_t cap, size_t* count) {
+    REQUIRE(validN(N), "N must be a power of two in [4, 1024]");
+    const sfhe::SizeParams* p = sfhe::hybrid1Params((int)N);
+    if (mult_depth) *mult_depth = (uint32_t)p->multDepth;
+    if (count) *count = p->rotations.size();
+    for (size_t i = 0; i < p->rotations.size() && i < cap && rotations; ++i) rotations[i] = p->rotations[i];
+    return SFHE_OK;
 }
 
 int sfhe_sorter_graph_nodes(const sfhe_sorter* s, uint64_t* nodes) {

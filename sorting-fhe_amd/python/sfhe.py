@@ -35,7 +35,8 @@ ABI_SYMBOLS = [
     "sfhe_sorter_destroy", "sfhe_sorter_sort", "sfhe_sorter_rank", "sfhe_sorter_place",
     "sfhe_decompose", "sfhe_kernel_timing", "sfhe_kernel_timing_read",
     "sfhe_comm_uid", "sfhe_shard_rccl", "sfhe_shard_host", "sfhe_pool_bytes",
-    "sfhe_serialize_lanes", "sfhe_sorter_graph_nodes",
+    "sfhe_serialize_lanes", "sfhe_sorter_graph_nodes", "sfhe_sorter_create_rot",
+    "sfhe_sorter_sort_hybrid1", "sfhe_hybrid1_params",
 ]
 
 
@@ -112,6 +113,9 @@ _SIGS = {
     "sfhe_sorter_rank": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_int, _PVP]),
     "sfhe_sorter_place": (C.c_int, [_VP, _VP, _VP, _PVP]),
     "sfhe_sorter_graph_nodes": (C.c_int, [_VP, _PU64]),
+    "sfhe_sorter_create_rot": (C.c_int, [_VP, _U32, C.c_int, _PI32, _SZ, _PVP]),
+    "sfhe_sorter_sort_hybrid1": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_int, _PVP]),
+    "sfhe_hybrid1_params": (C.c_int, [_U32, _PU32, _PI32, _SZ, _PSZ]),
     "sfhe_kernel_timing": (C.c_int, [_VP, _U32, _U32]),
     "sfhe_serialize_lanes": (C.c_int, [_VP, C.c_int]),
     "sfhe_kernel_timing_read": (C.c_int, [_VP, _U32, _PU64, _PU64, _PD, _PD]),
@@ -329,9 +333,15 @@ class Engine:
     def compare(self, a, b, n: int, dg: int, df: int):
         return self._new(self.lib.sfhe_compare, self.ctx, a.h, b.h, n, dg, df)
 
-    def sorter(self, N: int, debug: bool = False) -> "Sorter":
+    def sorter(self, N: int, debug: bool = False, rotations=None) -> "Sorter":
+        """DirectSort<N>; rotations = the constructor's rotIndices (None: the
+        getSizeParameters list)."""
         h = C.c_void_p()
-        self._chk(self.lib.sfhe_sorter_create(self.ctx, N, int(debug), C.byref(h)))
+        if rotations is None:
+            self._chk(self.lib.sfhe_sorter_create(self.ctx, N, int(debug), C.byref(h)))
+        else:
+            buf = (C.c_int32 * len(rotations))(*rotations)
+            self._chk(self.lib.sfhe_sorter_create_rot(self.ctx, N, int(debug), buf, len(rotations), C.byref(h)))
         return Sorter(self, h, N)
 
 
@@ -398,6 +408,10 @@ class Sorter:
     def place(self, rank: Ct, ct: Ct) -> Ct:
         return self.eng._new(self.eng.lib.sfhe_sorter_place, self.h, rank.h, ct.h)
 
+    def sort_hybrid1(self, ct: Ct, n: int = 3, dg: int = 2, df: int = 2) -> Ct:
+        """DirectSort<N>::sort_hybrid1 (reference sort_algo.h:1213-1229)."""
+        return self.eng._new(self.eng.lib.sfhe_sorter_sort_hybrid1, self.h, ct.h, n, dg, df)
+
     def graph_nodes(self) -> int:
         v = C.c_uint64()
         self.eng._chk(self.eng.lib.sfhe_sorter_graph_nodes(self.h, C.byref(v)))
@@ -413,6 +427,19 @@ def direct_sort_params(N: int, backend: str = "hip"):
         raise SfheError(lib.sfhe_last_error().decode())
     buf = (C.c_int32 * cnt.value)()
     lib.sfhe_direct_sort_params(N, None, buf, cnt.value, None)
+    return depth.value, list(buf)
+
+
+def hybrid1_params(N: int, backend: str = "hip"):
+    """(depth, rotation keys) of tests/DirectSortH1Test.cpp:36-117 for N."""
+    lib = load(backend)
+    depth = C.c_uint32()
+    cnt = C.c_size_t()
+    rc = lib.sfhe_hybrid1_params(N, C.byref(depth), None, 0, C.byref(cnt))
+    if rc != SFHE_OK:
+        raise SfheError(lib.sfhe_last_error().decode())
+    buf = (C.c_int32 * cnt.value)()
+    lib.sfhe_hybrid1_params(N, None, buf, cnt.value, None)
     return depth.value, list(buf)
 
 

@@ -37,6 +37,7 @@ LIBS = {
 # program -> (sources relative to the reference, needs gtest_main, needs memory_tracker)
 PROGRAMS = {
     "DirectSortTest": (["tests/DirectSortTest.cpp"], True, True),
+    "DirectSortH1Test": (["tests/DirectSortH1Test.cpp"], True, True),
     "CompareTest": (["tests/CompareTest.cpp"], False, False),
     "SignTest": (["tests/SignTest.cpp"], False, False),
     "RotationTest": (["tests/RotationTest.cpp"], True, False),

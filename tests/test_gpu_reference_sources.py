@@ -110,3 +110,19 @@ def test_sortn_benchmark_direct(hip_lib):
     way (a C++ exception out of sort()), not silently return garbage."""
     rc, out = run(exe("SortNBenchmark"), "--benchmark_filter=BM_DirectSort<4>")
     assert rc != 0 and "multiplicative depth exhausted" in out, out[-3000:]
+
+
+def test_direct_sort_h1_test(hip_lib):
+    """tests/DirectSortH1Test.cpp as-is (sort_hybrid1):
+    N = 4 ... 256 at ring 2^17, HEStd_128_classic, its own depth / key
+    tables; gates: level == multDepth, max error < 0.01.  The reference
+    publishes 93.53 s and 2^-19.30 at N=256 (comparison/experimental_results/
+    ours_hybrid1/total_results.txt:151-174)."""
+    rc, out = run(exe("DirectSortH1Test"), "--gtest_filter=*/0.*:*/1.*:*/2.*:*/3.*:*/4.*:*/5.*:*/6.*",
+                  timeout=600)
+    errs = [float(x) for x in re.findall(r"Maximum error: ([0-9.e+-]+)", out)]
+    times = [int(x) for x in re.findall(r"Execution time: (\d+) ms", out)]
+    print("max errors:", errs, "\nexecution ms:", times)
+    assert rc == 0, out[-4000:]
+    assert "7 tests ran, 0 failed" in out
+    assert len(errs) == 7 and max(errs) < 0.01

@@ -78,3 +78,15 @@ def test_direct_sort_test_n4(built):
 def test_sortn_benchmark_lists(built):
     rc, out = run(built[("SortNBenchmark", "oracle")], "--benchmark_list_tests")
     assert rc == 0 and "BM_DirectSort<256>" in out and "BM_BitonicSort<4>" in out, out
+
+
+def test_direct_sort_h1_test_n4(built):
+    """tests/DirectSortH1Test.cpp as-is (sort_hybrid1), its first
+    instantiation (N=4, ring 2^17, HEStd_128_classic): level == multDepth 31,
+    max error < 0.01 (the float64 schedule itself gives 3.4e-4 at N=4)."""
+    rc, out = run(built[("DirectSortH1Test", "oracle")], "--gtest_filter=*/0.*", timeout=900)
+    assert rc == 0, out[-3000:]
+    assert "[       OK ] HybridSort/HybridSortTestFixture/0.SortHybridTest" in out
+    assert "Result Level: 31" in out
+    err = float(re.search(r"Maximum error: ([0-9.e+-]+)", out).group(1))
+    assert err < 1e-3, err
