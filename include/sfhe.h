@@ -177,6 +177,12 @@ int sfhe_sorter_place(sfhe_sorter* s, const sfhe_ct* rank, sfhe_ct* in, sfhe_ct*
  * (SFHE_GRAPH=0 keeps every sort eager; debug sorters never capture).
  * 0 while no graph exists. */
 int sfhe_sorter_graph_nodes(const sfhe_sorter* s, uint64_t* nodes);
+/* Roofline measurement (engine extension): the NTT kernel nodes of the
+ * sorter's captured sort graph re-instantiated alone, in captured order, and
+ * replayed `reps` times, timed with HIP events: *ms per replay (= the NTT
+ * kernel time of one sort), *launches, *bytes (algorithmic: 16 B per
+ * coefficient per pass).  SFHE_EINVAL-class error when no graph exists. */
+int sfhe_sorter_graph_ntt_time(sfhe_sorter* s, int reps, double* ms, uint64_t* launches, double* bytes);
 /* DirectSort<N>::sort_hybrid1 (sort_algo.h:1213-1229): constructRank, then
  * rotationIndexCheckHybrid1 (:1067-1209, MEHP24 indicatorAdv placement,
  * mehp24_utils.cpp:166-174, :246-261).  Needs ring dimension >= 2 N^2 for

@@ -133,6 +133,11 @@ void sfp_event_free(sfp_dev* d, sfp_event* e) { (void)d; (void)e; }
 void sfp_lane_wait(sfp_dev* d, int waiter, int waitee) { (void)d; (void)waiter; (void)waitee; }
 /* kernel timing is a device-backend feature; the oracle reports nothing */
 void sfp_prof_set(sfp_dev* d, uint32_t fam, uint32_t period) { (void)d; (void)fam; (void)period; }
+int sfp_graph_family_time(sfp_dev* d, sfp_graph* g, uint32_t fam, int reps, double* ms, uint64_t* launches,
+                          double* bytes) {
+    (void)d; (void)g; (void)fam; (void)reps; (void)ms; (void)launches; (void)bytes;
+    return -1;
+}
 void sfp_serialize(sfp_dev* d, int on) { (void)d; (void)on; }
 /* no graphs: the host layer runs every region eagerly */
 int sfp_capture_begin(sfp_dev* d) { (void)d; return -1; }

@@ -580,6 +580,10 @@ class DirectSort : public SortBase<N> {
     ~DirectSort() override { m_graph.reset(); }
     // nodes of the captured sort (0: none yet / eager)
     size_t graphNodes() const { return m_graph ? m_cc->GraphNodes(m_graph->g) : 0; }
+    // the captured sort's NTT kernels replayed alone (bench roofline)
+    bool graphNttTime(int reps, double* ms, uint64_t* launches, double* bytes) {
+        return m_graph && m_cc->GraphNttTime(m_graph->g, reps, ms, launches, bytes);
+    }
 
     Ciphertext<DCRTPoly> sort(const Ciphertext<DCRTPoly>& input_array, SignFunc SignFunc,
                               SignConfig& Cfg) override {

@@ -98,6 +98,7 @@ struct SorterBase {
     virtual Ct place(const Ct& rank, const Ct& in) = 0;
     virtual Ct hybrid1(const Ct& in, SignConfig& cfg, const PrivateKey<DCRTPoly>& sk) = 0;
     virtual size_t graphNodes() const = 0;
+    virtual bool graphNttTime(int reps, double* ms, uint64_t* launches, double* bytes) = 0;
 };
 
 template <int N>
@@ -115,6 +116,9 @@ struct Sorter : SorterBase {
         return ds.sort_hybrid1(in, SignFunc::CompositeSign, cfg, sk);
     }
     size_t graphNodes() const override { return ds.graphNodes(); }
+    bool graphNttTime(int reps, double* ms, uint64_t* launches, double* bytes) override {
+        return ds.graphNttTime(reps, ms, launches, bytes);
+    }
 };
 
 template <int N>
@@ -440,6 +444,14 @@ int sfhe_hybrid1_params(uint32_t N, uint32_t* mult_depth, int32_t* rotations, si
     if (count) *count = p->rotations.size();
     for (size_t i = 0; i < p->rotations.size() && i < cap && rotations; ++i) rotations[i] = p->rotations[i];
     return SFHE_OK;
+}
+
+int sfhe_sorter_graph_ntt_time(sfhe_sorter* s, int reps, double* ms, uint64_t* launches, double* bytes) {
+    REQUIRE(s && ms && reps > 0, "null argument");
+    return guard([&] {
+        if (!s->impl->graphNttTime(reps, ms, launches, bytes))
+            throw std::runtime_error("no captured sort graph (or no graphs on this backend)");
+    });
 }
 
 int sfhe_sorter_graph_nodes(const sfhe_sorter* s, uint64_t* nodes) {

@@ -1,0 +1,4 @@
+// Forwarding header: the reference includes OpenFHE's ciphertext-ser.h; the engine's
+// facade declares everything in openfhe.h.
+#pragma once
+#include "openfhe.h"

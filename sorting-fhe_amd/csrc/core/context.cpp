@@ -2124,6 +2124,13 @@ void CryptoContextImpl<DCRTPoly>::Launch(const std::shared_ptr<CapturedGraph>& g
     if (g->keep) s->wrote(g->keep->buf.get());
 }
 
+bool CryptoContextImpl<DCRTPoly>::GraphNttTime(const std::shared_ptr<CapturedGraph>& g, int reps, double* ms,
+                                               uint64_t* launches, double* bytes) {
+    if (!g || !g->g) return false;
+    OpLock lk(st.get());
+    return sfp_graph_family_time(st->dev, g->g, SFP_FAM_NTT, reps, ms, launches, bytes) == 0;
+}
+
 size_t CryptoContextImpl<DCRTPoly>::GraphNodes(const std::shared_ptr<CapturedGraph>& g) const {
     return g ? sfp_graph_nodes(g->g) : 0;
 }

@@ -1,4 +1,4 @@
 // Forwarding header: the reference includes this OpenFHE path; everything it
 // needs is declared by the engine's openfhe.h.
 #pragma once
-#include "../../openfhe.h"
+#include "openfhe.h"

@@ -21,6 +21,7 @@
 #pragma once
 
 #include <complex>
+#include <fstream>
 #include <cstdint>
 #include <functional>
 #include <iostream>
@@ -32,7 +33,7 @@
 #include <string>
 #include <vector>
 
-#include "../prims.h"
+#include "prims.h"
 
 namespace lbcrypto {
 
@@ -62,6 +63,10 @@ enum PKESchemeFeature {
 };
 enum ScalingTechnique { FIXEDMANUAL, FIXEDAUTO, FLEXIBLEAUTO, FLEXIBLEAUTOEXT, NORESCALE };
 enum KeySwitchTechnique { BV, HYBRID };
+// serialization formats (OpenFHE SerType::BINARY / JSON; see Serial below)
+namespace SerType {
+enum Kind { JSON = 0, BINARY = 1 };
+}
 
 template <class T>
 class CCParams;
@@ -250,6 +255,18 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
     }
     void ClearEvalMultKeys();
     void ClearEvalAutomorphismKeys();
+    // Key serialization (OpenFHE's static forms: every registered context's
+    // keys are written, each record tagged with its context's fingerprint;
+    // deserialization installs them into the live context with that
+    // fingerprint).  keyTag is accepted and ignored (one key set per context).
+    static bool SerializeEvalMultKey(std::ostream& os, SerType::Kind k, const std::string& keyTag = "");
+    static bool DeserializeEvalMultKey(std::istream& is, SerType::Kind k);
+    static bool SerializeEvalAutomorphismKey(std::ostream& os, SerType::Kind k, const std::string& keyTag = "");
+    static bool DeserializeEvalAutomorphismKey(std::istream& is, SerType::Kind k);
+    // parameter fingerprint: ring, prime chain, special primes, digits, scales
+    uint64_t Fingerprint() const;
+    const CCParams<CryptoContextCKKSRNS>& GetParams() const;
+    uint32_t GetEnabledMask() const { return enabled; }
 
     // encode / encrypt / decrypt
     Plaintext MakeCKKSPackedPlaintext(const std::vector<double>& v, uint32_t scaleDeg = 1,
@@ -417,6 +434,9 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
     std::shared_ptr<CapturedGraph> EndCapture(const Ciphertext<DCRTPoly>& keep);
     void Launch(const std::shared_ptr<CapturedGraph>& g);
     size_t GraphNodes(const std::shared_ptr<CapturedGraph>& g) const;
+    // the graph's NTT kernels replayed alone (sfp_graph_family_time)
+    bool GraphNttTime(const std::shared_ptr<CapturedGraph>& g, int reps, double* ms, uint64_t* launches,
+                      double* bytes);
     // dst's rows (same level) overwritten with src's: refills a graph's input
     void CopyCiphertextInto(const Ciphertext<DCRTPoly>& dst, const Ciphertext<DCRTPoly>& src);
 
@@ -426,9 +446,47 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
     friend class SfheInternal;
 };
 
+// Registers the context for key deserialization (Deserialize*Key below find
+// their context by its parameter fingerprint, as OpenFHE's static key maps do).
+void RegisterCryptoContext(const CryptoContext<DCRTPoly>& cc);
+
 inline CryptoContext<DCRTPoly> GenCryptoContext(const CCParams<CryptoContextCKKSRNS>& p) {
-    return std::make_shared<CryptoContextImpl<DCRTPoly>>(p);
+    auto cc = std::make_shared<CryptoContextImpl<DCRTPoly>>(p);
+    RegisterCryptoContext(cc);
+    return cc;
 }
+
+// ---------------------------------------------------------------------------
+// Serialization (OpenFHE utils/serial.h surface the reference's src/sort.h:31-102
+// uses).  Format: the engine's own binary records (magic "SFHE", a type
+// tag, the context's parameter fingerprint, raw residues) -- OpenFHE's
+// cereal BINARY layout cannot be reproduced without OpenFHE (SURVEY §8(f)
+// row 4), so files round-trip between processes of this engine, not with
+// OpenFHE.  SerType::JSON is rejected.
+class Serial {
+  public:
+    static bool Serialize(const CryptoContext<DCRTPoly>& cc, std::ostream& os, SerType::Kind k);
+    static bool Deserialize(CryptoContext<DCRTPoly>& cc, std::istream& is, SerType::Kind k);
+    static bool Serialize(const PublicKey<DCRTPoly>& pk, std::ostream& os, SerType::Kind k);
+    static bool Deserialize(PublicKey<DCRTPoly>& pk, std::istream& is, SerType::Kind k);
+    static bool Serialize(const PrivateKey<DCRTPoly>& sk, std::ostream& os, SerType::Kind k);
+    static bool Deserialize(PrivateKey<DCRTPoly>& sk, std::istream& is, SerType::Kind k);
+    static bool Serialize(const Ciphertext<DCRTPoly>& ct, std::ostream& os, SerType::Kind k);
+    static bool Deserialize(Ciphertext<DCRTPoly>& ct, std::istream& is, SerType::Kind k);
+
+    template <class T>
+    static bool SerializeToFile(const std::string& path, const T& obj, SerType::Kind k) {
+        std::ofstream f(path, std::ios::out | std::ios::binary | std::ios::trunc);
+        if (!f.is_open()) return false;
+        return Serialize(obj, f, k) && f.good();
+    }
+    template <class T>
+    static bool DeserializeFromFile(const std::string& path, T& obj, SerType::Kind k) {
+        std::ifstream f(path, std::ios::in | std::ios::binary);
+        if (!f.is_open()) return false;
+        return Deserialize(obj, f, k);
+    }
+};
 
 template <class E>
 class CryptoContextFactory {

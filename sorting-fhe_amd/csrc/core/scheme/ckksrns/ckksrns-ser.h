@@ -1,0 +1,4 @@
+// Forwarding header: the reference includes OpenFHE's scheme/ckksrns/ckksrns-ser.h; the engine's
+// facade declares everything in openfhe.h.
+#pragma once
+#include "openfhe.h"

@@ -9,7 +9,7 @@
 #include <unordered_set>
 #include <vector>
 
-#include "../modarith.h"
+#include "modarith.h"
 #include "openfhe.h"
 
 namespace lbcrypto {

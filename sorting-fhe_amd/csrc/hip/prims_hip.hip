@@ -2209,6 +2209,72 @@ void sfp_graph_launch(sfp_dev* d, sfp_graph* g) {
 
 size_t sfp_graph_nodes(const sfp_graph* g) { return g ? g->nodes : 0; }
 
+int sfp_graph_family_time(sfp_dev* d, sfp_graph* g, uint32_t fam, int reps, double* ms, uint64_t* launches,
+                          double* bytes) {
+    if (!g || !g->g || fam != SFP_FAM_NTT || reps < 1 || d->capture) return -1;
+    const void* fns[] = {(const void*)k_ntt<false, true, 2>, (const void*)k_ntt<false, false, 2>,
+                         (const void*)k_ntt<true, true, 2>,  (const void*)k_ntt<true, false, 2>,
+                         (const void*)k_ntt<false, true, 3>, (const void*)k_ntt<false, false, 3>,
+                         (const void*)k_ntt<true, true, 3>,  (const void*)k_ntt<true, false, 3>,
+                         (const void*)k_ntt<false, true, 4>, (const void*)k_ntt<false, false, 4>,
+                         (const void*)k_ntt<true, true, 4>,  (const void*)k_ntt<true, false, 4>};
+    size_t nn = 0;
+    if (hipGraphGetNodes(g->g, nullptr, &nn) != hipSuccess) return -1;
+    std::vector<hipGraphNode_t> nodes(nn);
+    if (hipGraphGetNodes(g->g, nodes.data(), &nn) != hipSuccess) return -1;
+    // capture order = topological order of a stream capture; keep it
+    hipGraph_t sub = nullptr;
+    if (hipGraphCreate(&sub, 0) != hipSuccess) return -1;
+    hipGraphNode_t prev = nullptr;
+    uint64_t cnt = 0;
+    double b = 0;
+    for (hipGraphNode_t nd : nodes) {
+        hipGraphNodeType t;
+        if (hipGraphNodeGetType(nd, &t) != hipSuccess || t != hipGraphNodeTypeKernel) continue;
+        hipKernelNodeParams kp;
+        std::memset(&kp, 0, sizeof kp);
+        if (hipGraphKernelNodeGetParams(nd, &kp) != hipSuccess) continue;
+        if (!kp.func || (!kp.kernelParams && !kp.extra)) {  // (a tool may rewrite the nodes)
+            hipGraphDestroy(sub);
+            return -1;
+        }
+        bool ntt = false;
+        for (const void* f : fns) ntt = ntt || kp.func == f;
+        if (!ntt) continue;
+        hipGraphNode_t nn2 = nullptr;
+        if (hipGraphAddKernelNode(&nn2, sub, prev ? &prev : nullptr, prev ? 1 : 0, &kp) != hipSuccess) {
+            hipGraphDestroy(sub);
+            return -1;
+        }
+        prev = nn2;
+        ++cnt;
+        b += 16.0 * kp.gridDim.y * d->n;  // one pass reads and writes each row once
+    }
+    hipGraphExec_t ex = nullptr;
+    if (!cnt || hipGraphInstantiate(&ex, sub, nullptr, nullptr, 0) != hipSuccess) {
+        hipGetLastError();
+        hipGraphDestroy(sub);
+        return -1;
+    }
+    syncAll(d);
+    hipEvent_t e0 = takeEvent(d), e1 = takeEvent(d);
+    SFP_CHECK(hipGraphLaunch(ex, d->st()));  // warm
+    SFP_CHECK(hipEventRecord(e0, d->st()));
+    for (int r = 0; r < reps; ++r) SFP_CHECK(hipGraphLaunch(ex, d->st()));
+    SFP_CHECK(hipEventRecord(e1, d->st()));
+    SFP_CHECK(hipEventSynchronize(e1));
+    float t = 0;
+    SFP_CHECK(hipEventElapsedTime(&t, e0, e1));
+    d->evPool.push_back(e0);
+    d->evPool.push_back(e1);
+    hipGraphExecDestroy(ex);
+    hipGraphDestroy(sub);
+    if (ms) *ms = t / reps;
+    if (launches) *launches = cnt;
+    if (bytes) *bytes = b;
+    return 0;
+}
+
 void sfp_serialize(sfp_dev* d, int on) {
     syncAll(d);
     d->serial = on != 0;

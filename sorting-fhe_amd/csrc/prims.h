@@ -299,6 +299,14 @@ int sfp_capturing(sfp_dev* d);
 // Enqueue the whole graph on the current lane (stream-ordered like a prim).
 void sfp_graph_launch(sfp_dev* d, sfp_graph* g);
 size_t sfp_graph_nodes(const sfp_graph* g);
+// The graph's kernel nodes of family `fam` (SFP_FAM_NTT only), re-instantiated
+// in their captured order as a graph of their own and replayed `reps` times,
+// timed with HIP events on the current lane: the family's kernels alone,
+// back to back, with exactly the captured launch parameters.  Returns 0 and
+// the milliseconds per replay, the launches and their algorithmic bytes per
+// replay; -1 where the backend has no graphs.
+int sfp_graph_family_time(sfp_dev* d, sfp_graph* g, uint32_t fam, int reps, double* ms, uint64_t* launches,
+                          double* bytes);
 void sfp_graph_destroy(sfp_dev* d, sfp_graph* g);
 
 // ---- live kernel timing ---------------------------------------------------------

@@ -36,7 +36,7 @@ ABI_SYMBOLS = [
     "sfhe_decompose", "sfhe_kernel_timing", "sfhe_kernel_timing_read",
     "sfhe_comm_uid", "sfhe_shard_rccl", "sfhe_shard_host", "sfhe_pool_bytes",
     "sfhe_serialize_lanes", "sfhe_sorter_graph_nodes", "sfhe_sorter_create_rot",
-    "sfhe_sorter_sort_hybrid1", "sfhe_hybrid1_params",
+    "sfhe_sorter_sort_hybrid1", "sfhe_hybrid1_params", "sfhe_sorter_graph_ntt_time",
 ]
 
 
@@ -116,6 +116,7 @@ _SIGS = {
     "sfhe_sorter_create_rot": (C.c_int, [_VP, _U32, C.c_int, _PI32, _SZ, _PVP]),
     "sfhe_sorter_sort_hybrid1": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_int, _PVP]),
     "sfhe_hybrid1_params": (C.c_int, [_U32, _PU32, _PI32, _SZ, _PSZ]),
+    "sfhe_sorter_graph_ntt_time": (C.c_int, [_VP, C.c_int, _PD, _PU64, _PD]),
     "sfhe_kernel_timing": (C.c_int, [_VP, _U32, _U32]),
     "sfhe_serialize_lanes": (C.c_int, [_VP, C.c_int]),
     "sfhe_kernel_timing_read": (C.c_int, [_VP, _U32, _PU64, _PU64, _PD, _PD]),
@@ -411,6 +412,13 @@ class Sorter:
     def sort_hybrid1(self, ct: Ct, n: int = 3, dg: int = 2, df: int = 2) -> Ct:
         """DirectSort<N>::sort_hybrid1 (reference sort_algo.h:1213-1229)."""
         return self.eng._new(self.eng.lib.sfhe_sorter_sort_hybrid1, self.h, ct.h, n, dg, df)
+
+    def graph_ntt_time(self, reps: int = 5):
+        """(ms per sort, launches, algorithmic bytes) of the captured sort's
+        NTT kernels replayed alone (sfhe_sorter_graph_ntt_time)."""
+        ms, n, b = C.c_double(), C.c_uint64(), C.c_double()
+        self.eng._chk(self.eng.lib.sfhe_sorter_graph_ntt_time(self.h, reps, C.byref(ms), C.byref(n), C.byref(b)))
+        return ms.value, n.value, b.value
 
     def graph_nodes(self) -> int:
         v = C.c_uint64()

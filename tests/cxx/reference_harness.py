@@ -29,6 +29,8 @@ REF = os.environ.get("SFHE_REFERENCE", "/root/reference")
 OUT = os.path.join(HERE, "build")
 CSRC = os.path.join(ROOT, "sorting-fhe_amd", "csrc")
 SHIM = os.path.join(HERE, "shim")
+PSTL = next((os.path.join("/usr/include/c++", v, "pstl") for v in sorted(os.listdir("/usr/include/c++"), reverse=True)
+             if os.path.isdir(os.path.join("/usr/include/c++", v, "pstl"))), "/usr/include")
 LIBS = {
     "oracle": (os.path.join(ROOT, "oracle", "_build"), "sfhe_oracle"),
     "hip": (os.path.join(ROOT, "sorting-fhe_amd", "build"), "sfhe"),
@@ -43,7 +45,35 @@ PROGRAMS = {
     "RotationTest": (["tests/RotationTest.cpp"], True, False),
     "DecomposeTest": (["tests/DecomposeTest.cpp"], True, False),
     "SortNBenchmark": (["benchmarks/SortNBenchmark.cpp"], False, False),
+    # the FHERMA-style server (src/sort.h SortContext + src/main.cpp), SURVEY §8(f) row 4
+    "main": (["src/main.cpp"], False, False),
 }
+
+# the engine's own test programs (no reference sources; always buildable)
+OWN = {"fherma_client": os.path.join(HERE, "fherma_client.cpp")}
+
+
+def _engine_mtime() -> float:
+    """Newest engine header: objects compiled against older headers are stale."""
+    t = 0.0
+    for d, _, fs in os.walk(CSRC):
+        for f in fs:
+            if f.endswith(".h"):
+                t = max(t, os.path.getmtime(os.path.join(d, f)))
+    return t
+
+
+def build_own():
+    built = {}
+    for name, src in OWN.items():
+        for backend, (libdir, lib) in LIBS.items():
+            exe = os.path.join(OUT, f"{name}_{backend}")
+            os.makedirs(OUT, exist_ok=True)
+            if not (os.path.exists(exe) and os.path.getmtime(exe) >= max(os.path.getmtime(src), _engine_mtime())):
+                subprocess.run(["g++"] + flags() + [src, "-o", exe, "-L" + libdir, "-l" + lib,
+                                                    "-Wl,-rpath," + libdir, "-lpthread"], check=True)
+            built[(name, backend)] = exe
+    return built
 
 
 def available() -> bool:
@@ -51,15 +81,20 @@ def available() -> bool:
 
 
 def flags():
-    return ["-O2", "-std=c++17", "-fopenmp", "-DENABLE_PRINT_PT",
+    # -I- first: #include "x" never resolves next to the including source
+    # file, so the reference's src/main.cpp picks up this engine's sort.h /
+    # sort_algo.h, not the reference's own (every -I after it serves both
+    # include forms; libstdc++'s pstl headers quote-include their siblings,
+    # hence their directory)
+    return ["-O2", "-std=c++17", "-fopenmp", "-DENABLE_PRINT_PT", "-I-",
             "-I" + os.path.join(CSRC, "core"), "-I" + os.path.join(CSRC, "algo"), "-I" + CSRC,
             "-I" + os.path.join(ROOT, "include"), "-I" + SHIM, "-I" + os.path.join(REF, "tests"),
-            "-w"]
+            "-I" + PSTL, "-w"]
 
 
 def compile_obj(src: str, obj: str):
     os.makedirs(os.path.dirname(obj), exist_ok=True)
-    if os.path.exists(obj) and os.path.getmtime(obj) >= os.path.getmtime(src):
+    if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), _engine_mtime()):
         return
     subprocess.run(["g++"] + flags() + ["-c", src, "-o", obj], check=True)
 
@@ -104,7 +139,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--jobs", type=int, default=8)
     a = ap.parse_args()
-    for (p, b), exe in sorted(build(a.jobs).items()):
+    built = build_own()
+    if available():
+        built.update(build(a.jobs))
+    for (p, b), exe in sorted(built.items()):
         print(f"{p:16s} {b:7s} {exe}")
 
 

@@ -1,0 +1,64 @@
+"""Serialized I/O front end: the reference's own
+src/main.cpp (SortContext<128>, src/sort.h:15-102), compiled unchanged by
+tests/cxx/reference_harness.py, sorts files a key holder wrote -- the
+FHERMA-style flow: tests/cxx/fherma_client.cpp generates the context and keys
+with src/config.json's parameters, encrypts a permutation of {k/128} and
+serializes everything; main deserializes, sorts with CompositeSign(4,3,3)
+and serializes the result; the client decrypts and checks it (< 0.01).
+
+CPU: the C oracle at ring 2^12 (container only: main is built from the
+reference's sources).  GPU: the product at config.json's ring 2^17 / depth 44
+from the prebuilt binaries.  Files are this engine's records, not OpenFHE's
+cereal layout (openfhe.h, Serial)."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "cxx"))
+import reference_harness as H  # noqa: E402
+
+BUILD = os.path.join(HERE, "cxx", "build")
+
+
+def exe(name):
+    p = os.path.join(BUILD, name)
+    if not os.access(p, os.X_OK):
+        pytest.skip(f"{name} not built (tests/cxx/reference_harness.py)")
+    return p
+
+
+def flow(tmp_path, backend, logn, depth):
+    d = str(tmp_path)
+    r = subprocess.run([exe(f"fherma_client_{backend}"), "keygen", d, str(logn), str(depth), "128", "128", "7"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    r = subprocess.run([exe(f"main_{backend}"), "--key_pub", f"{d}/pub.bin", "--key_mult", f"{d}/mult.bin",
+                        "--key_rot", f"{d}/rot.bin", "--cc", f"{d}/cc.bin", "--input", f"{d}/input.bin",
+                        "--output", f"{d}/output.bin"], capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
+    r = subprocess.run([exe(f"fherma_client_{backend}"), "check", d, "128"], capture_output=True, text=True,
+                       timeout=600)
+    print(r.stdout.strip())
+    assert r.returncode == 0, r.stdout + r.stderr
+    return r.stdout
+
+
+def test_main_rejects_missing_files(tmp_path):
+    r = subprocess.run([exe("main_oracle"), "--cc", str(tmp_path / "nope.bin")], capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode == 1 and "Could not deserialize cryptocontext file" in r.stderr
+
+
+def test_fherma_flow_oracle(tmp_path, oracle_lib):
+    out = flow(tmp_path, "oracle", 12, 44)
+    assert "level 42" in out  # rank 29 (CompositeSign(4,3,3)) + placement 13
+
+
+@pytest.mark.gpu
+def test_fherma_flow_config_json(tmp_path, hip_lib):
+    """src/config.json: ring 2^17, depth 44, scale 40, batch 128, its rotation indexes."""
+    out = flow(tmp_path, "hip", 17, 44)
+    assert "level 42" in out
