@@ -1681,8 +1681,23 @@ static unsigned ewGrid(size_t work) {
 
 // Device-side byte copy on the compute stream (either side may be pinned
 // host memory).  Never uses the DMA engines: see DESIGN.md "transfers".
+// SFHE_DMA_COPY=1 (experiment): the same copies as
+// hipMemcpyAsync on the compute stream (the SDMA engines), ordered like every
+// other prim of the lane.
+static bool dmaCopy() {
+    static const bool on = [] {
+        const char* v = std::getenv("SFHE_DMA_COPY");
+        return v && *v == '1';
+    }();
+    return on;
+}
+
 static void devCopy(sfp_dev* d, void* dst, const void* src, size_t b) {
     if (!b) return;
+    if (dmaCopy()) {
+        SFP_CHECK(hipMemcpyAsync(dst, src, b, hipMemcpyDefault, d->st()));
+        return;
+    }
     if ((((uintptr_t)dst | (uintptr_t)src | b) & 15) == 0) {
         const size_t cnt = b / 16;
         hipLaunchKernelGGL(k_copy16, dim3(ewGrid(cnt)), dim3(kThreads), 0, d->st(), (ulonglong2*)dst,

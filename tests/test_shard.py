@@ -138,3 +138,51 @@ def test_sharded_ops_gloo_two_processes(oracle_lib, tmp_path):
     for r in range(2):
         z = np.load(f"{path}{r}.npz")
         compare(ref, {k: z[k] for k in z.files})
+
+
+GLOO_SORT_SCRIPT = r"""
+import sys
+import numpy as np
+sys.path.insert(0, {py!r}); sys.path.insert(0, {root!r}); sys.path.insert(0, {tests!r})
+import torch.distributed as dist
+import sfhe
+from test_shard import sort_program
+rank = int(sys.argv[1])
+dist.init_process_group("gloo", init_method="tcp://127.0.0.1:{port}", rank=rank, world_size=2)
+kw = {kw!r}
+e = sfhe.Engine("oracle", shard=("host", rank, 2, sfhe.GlooComm()), **kw)
+out = sort_program(e, {N})
+np.savez({path!r} + str(rank) + ".npz", **out)
+dist.barrier()
+dist.destroy_process_group()
+"""
+
+
+def test_sharded_sort_gloo_two_processes(oracle_lib, tmp_path):
+    """A whole DirectSort<8> limb-sharded over two PROCESSES (one per
+    'GPU', gloo host transport): every exchange of a real sharded sort
+    (ModUp / ModDown all-gathers, rescale broadcasts) crosses a process
+    boundary; both ranks' results are bit-identical to the unsharded sort."""
+    import socket
+    N = 8
+    depth, rots = sfhe.direct_sort_params(N, "oracle")
+    kw = dict(mult_depth=depth, ring_dim=1 << 12, batch_size=N, rotations=rots, seed=777)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    path = str(tmp_path / "rank")
+    code = GLOO_SORT_SCRIPT.format(py=os.path.join(ROOT, "sorting-fhe_amd", "python"), root=ROOT,
+                                   tests=os.path.join(ROOT, "tests"), port=port, path=path, kw=kw, N=N)
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    procs = [subprocess.Popen([sys.executable, "-c", code, str(r)], env=env) for r in range(2)]
+    try:
+        for p in procs:
+            assert p.wait(timeout=900) == 0
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    ref = sort_program(sfhe.Engine("oracle", **kw), N)
+    for r in range(2):
+        z = np.load(f"{path}{r}.npz")
+        compare(ref, {k: z[k] for k in z.files})
