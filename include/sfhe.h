@@ -136,6 +136,15 @@ int sfhe_eval_mult_plain(sfhe_ctx* c, const sfhe_ct* a, const double* values, si
 int sfhe_eval_mult(sfhe_ctx* c, const sfhe_ct* a, const sfhe_ct* b, sfhe_ct** out);
 /* EvalRotate (rotation.h:224) */
 int sfhe_eval_rotate(sfhe_ctx* c, const sfhe_ct* a, int32_t r, sfhe_ct** out);
+/* CKKS bootstrapping (OpenFHE's EvalBootstrapSetup + EvalBootstrapKeyGen and
+ * EvalBootstrap, as src/k-way/EvalUtils.cpp:57-86 and src/sort_algo.h:1437
+ * call them): setup for ciphertexts of `slots` slots with the level budget
+ * {budget_c2s, budget_s2c} (and its rotation / conjugation keys); depth =
+ * the level a bootstrapped ciphertext comes out at; iterations 2 with
+ * precision p = meta-bootstrapping. */
+int sfhe_bootstrap_setup(sfhe_ctx* c, uint32_t budget_c2s, uint32_t budget_s2c, uint32_t slots);
+int sfhe_bootstrap_depth(sfhe_ctx* c, uint32_t budget_c2s, uint32_t budget_s2c, uint32_t slots, uint32_t* depth);
+int sfhe_bootstrap(sfhe_ctx* c, const sfhe_ct* a, uint32_t iterations, uint32_t precision, sfhe_ct** out);
 /* EvalChebyshevSeriesPS (sort_algo.h:727-728, sign.cpp:76); c0/2 convention */
 int sfhe_eval_chebyshev(sfhe_ctx* c, const sfhe_ct* x, const double* coeffs, size_t count,
                         double a, double b, sfhe_ct** out);

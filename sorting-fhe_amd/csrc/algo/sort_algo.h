@@ -30,6 +30,7 @@
 #include <cmath>
 #include <iostream>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "ciphertext-fwd.h"
@@ -654,20 +655,100 @@ class DirectSort : public SortBase<N> {
     }
 };
 
-// Compare-and-swap network (reference :1393-1487).  It bootstraps, which is
-// the SURVEY §8(f) rank-2/3 "next" row: linkable, throws until then.
+// Compare-and-swap bitonic network over the N slots (reference
+// src/sort_algo.h:1393-1487, same schedule: values / 255, stages k = 2..N,
+// distances j = k/2..1, EvalBootstrap(ct, 2, 20) once the level passes 29,
+// CompositeSign comparisons, * 255 at the end).  Per stage the reference
+// masks the array four times and rotates each masked copy (four key
+// switches); here the array is rotated by -j and +j ONCE, both rotations
+// sharing one hoisted ModUp, and the masks are rotated in the clear instead
+// (Rot(x (.) m, r) = Rot(x, r) (.) Rot(m, r)), so each stage's partner
+// vectors are fused plaintext-weighted sums (EvalMultAddPlain) of three
+// ciphertexts.  The swap c a + (1 - c) b is b + c (a - b): one
+// ciphertext product instead of two.  Same levels as the reference.
 template <int N>
 class BitonicSort : public SortBase<N> {
   public:
+    std::shared_ptr<Encryption> m_enc;
+
     BitonicSort(CryptoContext<DCRTPoly> cc, PublicKey<DCRTPoly> publicKey,
                 std::vector<int> rotIndices, std::shared_ptr<Encryption> enc)
-        : SortBase<N>(enc), m_cc(cc), m_PublicKey(publicKey), m_rot(rotIndices) {}
-    Ciphertext<DCRTPoly> sort(const Ciphertext<DCRTPoly>&, SignFunc, SignConfig&) override {
-        throw OpenFHEException("BitonicSort needs CKKS bootstrapping (not implemented yet)");
+        : SortBase<N>(enc), m_enc(enc), m_cc(cc), m_PublicKey(publicKey), m_comp(enc),
+          m_rot(cc, enc, rotIndices) {}
+
+    Ciphertext<DCRTPoly> sort(const Ciphertext<DCRTPoly>& input_array, SignFunc SignFunc,
+                              SignConfig& Cfg) override {
+        auto cur = m_cc->EvalMult(input_array, 1.0 / 255);
+        for (int k = 2; k <= N; k *= 2)
+            for (int j = k / 2; j > 0; j /= 2) {
+                std::cout << "Loop k: " << k << " j: " << j << "\n";
+                if (cur->GetLevel() > kBootstrapLevel) cur = m_cc->EvalBootstrap(cur, 2, 20);
+                cur = stage(cur, k, j, SignFunc, Cfg);
+            }
+        return m_cc->EvalMult(cur, 255.0);
     }
 
   private:
+    static constexpr uint32_t kBootstrapLevel = 29;
+
+    // slot i and its partner i ^ j (i < partner): `lo` marks the lower slot of
+    // an ascending pair (bit k of i clear), `hi` the upper one; the
+    // descending pairs likewise.  Rotated copies are what the hoisted
+    // rotations of the array line up with.
+    struct StageMasks {
+        Plaintext ascLo, ascHi, desLo, desHi;          // at the slot
+        Plaintext ascLoUp, desLoUp, ascHiDn, desHiDn;  // shifted by +j / -j
+        Plaintext partnerUp, partnerDn;                // ascLoUp + desLoUp, ascHiDn + desHiDn
+    };
+
+    StageMasks& masks(int k, int j, uint32_t level) {
+        auto key = std::make_tuple(k, j, level);
+        auto it = m_masks.find(key);
+        if (it != m_masks.end()) return it->second;
+        std::vector<double> aL(N, 0), aH(N, 0), dL(N, 0), dH(N, 0);
+        for (int i = 0; i < N; ++i) {
+            const int l = i ^ j;
+            if (i >= l) continue;
+            ((i & k) ? dL : aL)[i] = 1;
+            ((i & k) ? dH : aH)[l] = 1;
+        }
+        auto shift = [](const std::vector<double>& v, int by) {  // out[p] = v[p - by]
+            std::vector<double> o(N);
+            for (int p = 0; p < N; ++p) o[p] = v[((p - by) % N + N) % N];
+            return o;
+        };
+        auto sum = [](std::vector<double> a, const std::vector<double>& b) {
+            for (int p = 0; p < N; ++p) a[p] += b[p];
+            return a;
+        };
+        auto pt = [&](const std::vector<double>& v) { return m_cc->MakeCKKSPackedPlaintext(v, 1, level); };
+        StageMasks m;
+        m.ascLo = pt(aL), m.ascHi = pt(aH), m.desLo = pt(dL), m.desHi = pt(dH);
+        m.ascLoUp = pt(shift(aL, j)), m.desLoUp = pt(shift(dL, j));
+        m.ascHiDn = pt(shift(aH, -j)), m.desHiDn = pt(shift(dH, -j));
+        m.partnerUp = pt(sum(shift(aL, j), shift(dL, j)));
+        m.partnerDn = pt(sum(shift(aH, -j), shift(dH, -j)));
+        return m_masks.emplace(key, std::move(m)).first->second;
+    }
+
+    Ciphertext<DCRTPoly> stage(const Ciphertext<DCRTPoly>& x, int k, int j, SignFunc SignFunc, SignConfig& Cfg) {
+        const StageMasks& m = masks(k, j, x->GetLevel());
+        // up[p] = x[p - j] (lower slots moved onto their partners), dn[p] = x[p + j]
+        auto r = m_rot.rotateMany(x, {-j, j});
+        const auto& up = r[0];
+        const auto& dn = r[1];
+        // every slot's partner value
+        auto partner = m_cc->EvalMultAddPlain({up, dn}, {m.partnerUp, m.partnerDn});
+        // the pair's larger-if-ascending / smaller-if-ascending arrangements
+        auto keep = m_cc->EvalMultAddPlain({up, x, dn, x}, {m.ascLoUp, m.ascLo, m.desHiDn, m.desHi});
+        auto swap = m_cc->EvalMultAddPlain({up, x, dn, x}, {m.desLoUp, m.desLo, m.ascHiDn, m.ascHi});
+        auto c = m_comp.compare(m_cc, partner, x, SignFunc, Cfg);
+        return m_cc->EvalAdd(swap, m_cc->EvalMult(c, m_cc->EvalSub(keep, swap)));
+    }
+
     CryptoContext<DCRTPoly> m_cc;
     PublicKey<DCRTPoly> m_PublicKey;
-    std::vector<int> m_rot;
+    Comparison m_comp;
+    RotationComposer<N> m_rot;
+    std::map<std::tuple<int, int, uint32_t>, StageMasks> m_masks;
 };

@@ -330,6 +330,22 @@ int sfhe_eval_rotate(sfhe_ctx* c, const sfhe_ct* a, int32_t r, sfhe_ct** out) {
     REQUIRE(c && a && out, "null argument");
     return guard([&] { *out = wrap(c->cc->EvalRotate(a->ct, r)); });
 }
+int sfhe_bootstrap_setup(sfhe_ctx* c, uint32_t budget_c2s, uint32_t budget_s2c, uint32_t slots) {
+    REQUIRE(c, "null argument");
+    REQUIRE(c->keys.secretKey, "sfhe_keygen must be called first");
+    return guard([&] {
+        c->cc->EvalBootstrapSetup({budget_c2s, budget_s2c}, {0, 0}, slots);
+        c->cc->EvalBootstrapKeyGen(c->keys.secretKey, slots);
+    });
+}
+int sfhe_bootstrap_depth(sfhe_ctx* c, uint32_t budget_c2s, uint32_t budget_s2c, uint32_t slots, uint32_t* depth) {
+    REQUIRE(c && depth, "null argument");
+    return guard([&] { *depth = c->cc->GetBootstrapDepth({budget_c2s, budget_s2c}, slots); });
+}
+int sfhe_bootstrap(sfhe_ctx* c, const sfhe_ct* a, uint32_t iterations, uint32_t precision, sfhe_ct** out) {
+    REQUIRE(c && a && out, "null argument");
+    return guard([&] { *out = wrap(c->cc->EvalBootstrap(a->ct, iterations, precision)); });
+}
 int sfhe_eval_chebyshev(sfhe_ctx* c, const sfhe_ct* x, const double* coeffs, size_t count,
                         double a, double b, sfhe_ct** out) {
     REQUIRE(c && x && coeffs && count && out, "null argument");

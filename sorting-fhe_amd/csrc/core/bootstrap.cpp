@@ -1,0 +1,392 @@
+// CKKS bootstrapping (the OpenFHE 1.1.4 surface the
+// reference calls: EvalBootstrapSetup / EvalBootstrapKeyGen / EvalBootstrap,
+// src/sort_algo.h:1437, src/sign.cpp:164-171, src/k-way/EvalUtils.cpp:57-86,
+// tests/k-way/KWaySort*Test.cpp, benchmarks/SortNBenchmark.cpp:86-89).
+//
+// The published algorithm (Cheon-Han-Kim-Kim-Song; Chen-Chillotti-Song's
+// sparse-slot trace; Han-Ki's cosine + double angle), restated over this
+// engine's encoder and level model.  For a ciphertext with S slots (S <= n/2,
+// periodic packing: the message polynomial lives in Z[X^gap], gap = n/2S):
+//
+//  1. scale the values by 2^-k and drop to the last level (one limb, q_0):
+//     one scaled level adjustment, m = Delta_L tau^-1(z 2^-k), |m| << q_0;
+//  2. ModRaise: the centred residues mod q_0 lifted to the whole chain, so
+//     the ciphertext decrypts to P = m + q_0 I(X) (|I| <= K);
+//  3. sparse trace: ct += Rot(ct, S 2^t), t < log2(gap), maps P to
+//     gap (m + q_0 I_sub) with I_sub in Z[X^gap];
+//  4. CoeffsToSlots: the special inverse FFT of the encoder
+//     (encoder.cpp fftSpecialInv) as log2(S) butterfly stages, each a slot
+//     map with three diagonals (offsets 0, +-len/2), grouped into
+//     levelBudget[0] products evaluated as hoisted-rotation diagonal sums
+//     (one level each).  The bit reversal is skipped: the slots end in
+//     bit-reversed coefficient order, which step 6 consumes as is;
+//  5. real / imaginary halves by one conjugation: re = h + conj(h),
+//     i im = h - conj(h) (h = u / 2);
+//  6. EvalMod of each half: x = I + m/q_0 in [-K, K];
+//     sin(2 pi x) = cos(2 pi (x - 1/4)): a Chebyshev series of
+//     cos(2 pi (x - 1/4) / 2^r) on [-K-1, K+1] (degree 89), then r double
+//     angles c <- 2c^2 - 1;
+//  7. SlotsToCoeffs: the encoder's forward special FFT (fftSpecial) stages
+//     grouped into levelBudget[1] products, the first taking both halves
+//     (re + i im), with q_0 2^k / (2 pi Delta_L) folded in.
+//
+// Levels: levelBudget[0] + 1 + PS depth (7) + r (6) + levelBudget[1]
+// (24 for {5, 5}), as OpenFHE's FLEXIBLEAUTO bootstrapping with a uniform
+// ternary secret; EvalBootstrap(ct, 2, p) is meta-bootstrapping (Bossuat et
+// al.): the residual ct - BTS(ct) bootstrapped again at 2^p and added back.
+#include <algorithm>
+#include <cmath>
+#include <complex>
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <set>
+#include <memory>
+#include <vector>
+
+#include "openfhe.h"
+#include "state.h"
+
+namespace lbcrypto {
+
+namespace {
+
+using cd = std::complex<double>;
+
+constexpr int kTargetBits = 13;   // step 1: |m/q_0| <~ 2^-13 (sin(2 pi x)/(2 pi) ~ x to 2^-25)
+constexpr uint32_t kDoubleAngles = 6;
+constexpr uint32_t kChebDegree = 89;
+constexpr double kOverflowBound = 512.0;  // |I| bound, uniform ternary secret (OpenFHE K_UNIFORM)
+
+}  // namespace
+// one diagonal of a slot map: out[p] += v[p] * in[(p + offset) mod S]
+using DiagMap = std::map<uint32_t, std::vector<std::complex<double>>>;
+namespace {
+
+DiagMap compose(const DiagMap& A, const DiagMap& B, uint32_t S) {  // A after B
+    DiagMap C;
+    for (const auto& [a, av] : A)
+        for (const auto& [b, bv] : B) {
+            auto& c = C[(a + b) % S];
+            if (c.empty()) c.assign(S, 0.0);
+            for (uint32_t p = 0; p < S; ++p) c[p] += av[p] * bv[(p + a) % S];
+        }
+    for (auto it = C.begin(); it != C.end();) {  // drop diagonals that cancelled
+        double mx = 0;
+        for (const cd& x : it->second) mx = std::max(mx, std::abs(x));
+        it = mx < 1e-300 ? C.erase(it) : std::next(it);
+    }
+    return C;
+}
+
+void scaleMap(DiagMap& M, cd f) {
+    for (auto& [k, v] : M)
+        for (cd& x : v) x *= f;
+}
+
+}  // namespace
+
+namespace boot {
+struct Group {
+    DiagMap diags;
+    std::map<uint32_t, Plaintext> pts;    // offset -> encoding at the level the group runs at
+    std::map<uint32_t, Plaintext> ptsIm;  // S2C first group: the diagonals times i (imaginary half)
+    uint32_t level = ~0u;
+};
+}  // namespace boot
+using boot::Group;
+
+struct BootstrapPrecomp {
+    uint32_t slots = 0, gap = 0;
+    std::vector<Group> c2s, s2c;        // in application order
+    std::map<double, Group> s2cFirst;   // s2c[0] with the output factor folded in, per factor
+    std::vector<double> cheb;           // cos(2 pi (x - 1/4) / 2^r) on [-K-1, K+1]
+    std::vector<int32_t> rotations;
+};
+
+namespace {
+
+// The butterfly stages of the encoder's special FFT over S slots (encoder.cpp
+// fftSpecialInv / fftSpecial), as three-diagonal slot maps, in application
+// order.  inverse: len = S .. 2 (coefficients <- slots), else len = 2 .. S.
+std::vector<DiagMap> fftStages(uint32_t n, uint32_t S, bool inverse) {
+    const uint64_t M = 2ull * n;
+    std::vector<uint64_t> rot(S);
+    uint64_t g = 1;
+    for (uint32_t j = 0; j < S; ++j) {
+        rot[j] = g;
+        g = (g * 5) % M;
+    }
+    auto ksi = [&](uint64_t k) { return std::polar(1.0, 2.0 * M_PI * (double)k / (double)M); };
+    std::vector<DiagMap> st;
+    for (uint32_t len = inverse ? S : 2; inverse ? len >= 2 : len <= S; len = inverse ? len / 2 : len * 2) {
+        const uint32_t h = len / 2;
+        const uint64_t lenq = (uint64_t)len << 2;
+        DiagMap D;
+        auto& d0 = D[0];
+        auto& dp = D[h % S];
+        auto& dm = D[(S - h) % S];
+        d0.assign(S, 0.0);
+        if (dp.empty()) dp.assign(S, 0.0);
+        if (dm.empty()) dm.assign(S, 0.0);
+        for (uint32_t p = 0; p < S; ++p) {
+            const uint32_t j = p % len;
+            if (inverse) {  // v[i+j] = a + b ; v[i+j+h] = (a - b) w,  w = ksi[(lenq - rot_j % lenq) M / lenq]
+                if (j < h) {
+                    d0[p] += 1.0;
+                    dp[p] += 1.0;
+                } else {
+                    const cd w = ksi((lenq - rot[j - h] % lenq) * M / lenq);
+                    dm[p] += w;
+                    d0[p] -= w;
+                }
+            } else {  // v[i+j] = a + b w ; v[i+j+h] = a - b w,  w = ksi[(rot_j % lenq) M / lenq]
+                if (j < h) {
+                    d0[p] += 1.0;
+                    dp[p] += ksi((rot[j] % lenq) * M / lenq);
+                } else {
+                    dm[p] += 1.0;
+                    d0[p] -= ksi((rot[j - h] % lenq) * M / lenq);
+                }
+            }
+        }
+        st.push_back(std::move(D));
+    }
+    return st;
+}
+
+// log2(S) stages into `budget` consecutive groups (earlier groups one stage
+// more when uneven), each collapsed into one diagonal map
+std::vector<Group> groupStages(const std::vector<DiagMap>& stages, uint32_t budget, uint32_t S) {
+    const uint32_t ns = (uint32_t)stages.size();
+    budget = std::max(1u, std::min(budget, ns));
+    std::vector<Group> gs(budget);
+    uint32_t at = 0;
+    for (uint32_t g = 0; g < budget; ++g) {
+        const uint32_t cnt = ns / budget + (g < ns % budget ? 1 : 0);
+        DiagMap m = stages[at++];
+        for (uint32_t c = 1; c < cnt; ++c) m = compose(stages[at++], m, S);
+        gs[g].diags = std::move(m);
+    }
+    return gs;
+}
+
+int32_t signedOffset(uint32_t k, uint32_t S) { return k > S / 2 ? (int32_t)k - (int32_t)S : (int32_t)k; }
+
+// SFHE_BOOT_DEBUG=1: decrypt and print every stage (diagnostics; the key
+// EvalBootstrapKeyGen saw is kept for it)
+PrivateKey<DCRTPoly> g_dbgSk;
+void dbg(CryptoContextImpl<DCRTPoly>* cc, const char* what, const Ciphertext<DCRTPoly>& c) {
+    static const bool on = std::getenv("SFHE_BOOT_DEBUG") != nullptr;
+    if (!on || !g_dbgSk) return;
+    Plaintext pt;
+    cc->Decrypt(g_dbgSk, c, &pt);
+    const auto& v = pt->GetCKKSPackedValue();
+    std::fprintf(stderr, "BOOT %-10s L%-3u", what, c->GetLevel());
+    for (size_t i = 0; i < std::min<size_t>(8, v.size()); ++i)
+        std::fprintf(stderr, " (%.9g,%.9g)", v[i].real(), v[i].imag());
+    std::fprintf(stderr, "\n");
+}
+
+
+}  // namespace
+
+void CryptoContextImpl<DCRTPoly>::EvalBootstrapSetup(std::vector<uint32_t> levelBudget, std::vector<uint32_t>,
+                                                     uint32_t slots, uint32_t) {
+    OpLock g(st.get());
+    SfheContextState* s = st.get();
+    if (s->world > 1) SFHE_THROW("bootstrapping a limb-sharded context is not supported");
+    if (!slots) slots = s->n / 2;
+    if (slots > s->n / 2 || (slots & (slots - 1))) SFHE_THROW("EvalBootstrapSetup: slots must be a power of two <= n/2");
+    if (levelBudget.size() != 2 || !levelBudget[0] || !levelBudget[1])
+        SFHE_THROW("EvalBootstrapSetup: levelBudget must hold two positive entries");
+    auto b = std::make_shared<BootstrapPrecomp>();
+    b->slots = slots;
+    b->gap = s->n / (2 * slots);
+    // slots 1 has no FFT stage: the one-slot transforms are the identity, kept
+    // as a single diagonal so both transforms still consume their level
+    auto c2sStages = slots > 1 ? fftStages(s->n, slots, true) : std::vector<DiagMap>{DiagMap{{0u, {cd(1.0)}}}};
+    auto s2cStages = slots > 1 ? fftStages(s->n, slots, false) : std::vector<DiagMap>{DiagMap{{0u, {cd(1.0)}}}};
+    b->c2s = groupStages(c2sStages, levelBudget[0], slots);
+    b->s2c = groupStages(s2cStages, levelBudget[1], slots);
+    // C2S scale: 1/S of the inverse FFT, 1/gap of the trace, the raised
+    // ciphertext's scale label Delta_0 / q_0, and 1/2 for the re/im split
+    const double q0 = (double)s->primes[0];
+    scaleMap(b->c2s.front().diags, cd(s->scale[0] / (q0 * b->gap * slots * 2.0)));
+    std::set<int32_t> rot;
+    for (const auto* gs : {&b->c2s, &b->s2c})
+        for (const auto& gr : *gs)
+            for (const auto& kv : gr.diags)
+                if (kv.first) rot.insert(signedOffset(kv.first, slots));
+    for (uint32_t t = slots; t < s->n / 2; t <<= 1) rot.insert((int32_t)t);  // sparse trace
+    b->rotations.assign(rot.begin(), rot.end());
+    const double Kb = kOverflowBound + 1.0;
+    b->cheb = EvalChebyshevCoefficients(
+        [](double x) { return std::cos(2.0 * M_PI * (x - 0.25) / (double)(1u << kDoubleAngles)); }, -Kb, Kb,
+        kChebDegree + 1);
+    s->boot[slots] = b;
+}
+
+void CryptoContextImpl<DCRTPoly>::EvalBootstrapKeyGen(const PrivateKey<DCRTPoly>& sk, uint32_t slots) {
+    SfheContextState* s = st.get();
+    if (!slots) slots = s->n / 2;
+    auto it = s->boot.find(slots);
+    if (it == s->boot.end()) SFHE_THROW("EvalBootstrapKeyGen: call EvalBootstrapSetup for these slots first");
+    EvalRotateKeyGen(sk, it->second->rotations);
+    EvalConjugateKeyGen(sk);
+    if (std::getenv("SFHE_BOOT_DEBUG")) g_dbgSk = sk;
+    if (!s->relinKey) EvalMultKeyGen(sk);
+}
+
+uint32_t CryptoContextImpl<DCRTPoly>::GetBootstrapDepth(const std::vector<uint32_t>& levelBudget, uint32_t slots) const {
+    const SfheContextState* s = st.get();
+    if (!slots) slots = s->n / 2;
+    const uint32_t ls = slots > 1 ? (uint32_t)std::log2((double)slots) : 1u;
+    const uint32_t b0 = std::max(1u, std::min(levelBudget.at(0), ls)), b1 = std::max(1u, std::min(levelBudget.at(1), ls));
+    return b0 + 1 + ChebyshevPSDepth(kChebDegree) + kDoubleAngles + b1;
+}
+
+namespace {
+
+// sum over the group's diagonals of diag_k (.) Rot(in_t, k) for every input
+// (one hoisted ModUp per input), one rescale
+Ciphertext<DCRTPoly> applyGroup(CryptoContextImpl<DCRTPoly>* cc, Group& gr, uint32_t S,
+                                const std::vector<Ciphertext<DCRTPoly>>& in, bool withIm) {
+    const uint32_t level = in[0]->GetLevel();
+    if (gr.level != level) {  // (re)encode the diagonals at the level this group runs at
+        gr.pts.clear();
+        gr.ptsIm.clear();
+        for (const auto& [k, v] : gr.diags) {
+            gr.pts[k] = cc->MakeCKKSPackedPlaintext(v, 1, level, nullptr, S);
+            if (withIm) {
+                std::vector<cd> vi(v.size());
+                for (size_t p = 0; p < v.size(); ++p) vi[p] = v[p] * cd(0.0, 1.0);
+                gr.ptsIm[k] = cc->MakeCKKSPackedPlaintext(vi, 1, level, nullptr, S);
+            }
+        }
+        gr.level = level;
+    }
+    std::vector<Ciphertext<DCRTPoly>> cts;
+    std::vector<Plaintext> pts;
+    for (size_t t = 0; t < in.size(); ++t) {
+        std::shared_ptr<FastRotationPrecomp> pre;
+        for (const auto& [k, v] : gr.diags) {
+            (void)v;
+            Ciphertext<DCRTPoly> r;
+            if (!k) {
+                r = in[t];
+            } else {
+                if (!pre) pre = cc->EvalFastRotationPrecompute(in[t]);
+                r = cc->EvalFastRotation(in[t], signedOffset(k, S), cc->GetCyclotomicOrder(), pre);
+            }
+            cts.push_back(r);
+            pts.push_back(t == 0 ? gr.pts.at(k) : gr.ptsIm.at(k));
+        }
+    }
+    // EvalMultAddPlain sums at most SFP_MAX_WSUM products per call
+    std::vector<Ciphertext<DCRTPoly>> parts;
+    for (size_t lo = 0; lo < cts.size(); lo += SFP_MAX_WSUM) {
+        const size_t hi = std::min(cts.size(), lo + SFP_MAX_WSUM);
+        parts.push_back(cc->EvalMultAddPlain(std::vector<Ciphertext<DCRTPoly>>(cts.begin() + lo, cts.begin() + hi),
+                                             std::vector<Plaintext>(pts.begin() + lo, pts.begin() + hi)));
+    }
+    auto out = parts.size() == 1 ? parts[0] : cc->EvalAddMany(parts);
+    out->SetSlots(S);
+    return out;
+}
+
+Ciphertext<DCRTPoly> evalMod(CryptoContextImpl<DCRTPoly>* cc, const BootstrapPrecomp& b, Ciphertext<DCRTPoly> y) {
+    auto c = cc->EvalChebyshevSeriesPS(y, b.cheb, -1.0, 1.0);
+    for (uint32_t i = 0; i < kDoubleAngles; ++i) {
+        auto sq = cc->EvalSquare(c);
+        c = cc->EvalAdd(cc->EvalAdd(sq, sq), -1.0);
+    }
+    return c;
+}
+
+}  // namespace
+
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::BootstrapOnce(const Ciphertext<DCRTPoly>& ct, double inFactor,
+                                                                double outFactor) {
+    SfheContextState* s = st.get();
+    auto it = s->boot.find(ct->GetSlots());
+    if (it == s->boot.end())
+        SFHE_THROW("EvalBootstrap: no EvalBootstrapSetup for " + std::to_string(ct->GetSlots()) + " slots");
+    BootstrapPrecomp& b = *it->second;
+    const uint32_t S = b.slots;
+    // 1-2: values * 2^-k at the last level, then the modulus raise; k puts
+    // m / q_0 = 2^-k Delta_L / q_0 (.) coefficients at about 2^-13 (OpenFHE's
+    // FLEXIBLEAUTO correction factor plays the same part)
+    const double deltaL = s->scale[s->L];
+    const int preScaleBits =
+        std::max(0, kTargetBits - (int)std::lround(std::log2((double)s->primes[0] / deltaL)));
+    auto low = AdjustLevelScaled(ct, s->L, inFactor * std::ldexp(1.0, -preScaleBits));
+    dbg(this, "low", low);
+    auto raised = ModRaise(low);
+    raised->SetSlots(S);
+    dbg(this, "raised", raised);
+    // 3: sparse trace
+    for (uint32_t t = S; t < s->n / 2; t <<= 1) raised = EvalAdd(raised, EvalRotate(raised, (int32_t)t));
+    dbg(this, "traced", raised);
+    // 4: CoeffsToSlots (h = u / 2 in bit-reversed order)
+    Ciphertext<DCRTPoly> h = raised;
+    for (auto& gr : b.c2s) {
+        h = applyGroup(this, gr, S, {h}, false);
+        dbg(this, "c2s", h);
+    }
+    // 5: real and imaginary halves
+    auto hc = EvalConjugate(h);
+    auto re = EvalAdd(h, hc);
+    auto imi = EvalSub(h, hc);  // i * im
+    // 6: EvalMod on y = x / (K + 1) in [-1, 1]
+    const double Kb = kOverflowBound + 1.0;
+    auto yre = EvalMult(re, 1.0 / Kb);
+    Plaintext negi = MakeCKKSPackedPlaintext(std::vector<cd>(S, cd(0.0, -1.0 / Kb)), 1, imi->GetLevel(), nullptr, S);
+    auto yim = EvalMult(imi, negi);
+    dbg(this, "re", re);
+    dbg(this, "yim", yim);
+    auto wre = evalMod(this, b, yre);
+    auto wim = evalMod(this, b, yim);
+    dbg(this, "wre", wre);
+    dbg(this, "wim", wim);
+    // 7: SlotsToCoeffs of w_re + i w_im, times q_0 2^k outFactor / (2 pi Delta_L)
+    const double cOut = (double)s->primes[0] * std::ldexp(1.0, preScaleBits) * outFactor / (2.0 * M_PI * deltaL);
+    // the first S2C group with cOut folded into its diagonals (one copy per
+    // factor: meta-bootstrapping's two passes use two)
+    auto fit = b.s2cFirst.find(cOut);
+    if (fit == b.s2cFirst.end()) {
+        Group g0;
+        g0.diags = b.s2c.front().diags;
+        scaleMap(g0.diags, cd(cOut));
+        fit = b.s2cFirst.emplace(cOut, std::move(g0)).first;
+    }
+    auto out = applyGroup(this, fit->second, S, {wre, wim}, true);
+    dbg(this, "s2c", out);
+    for (size_t g = 1; g < b.s2c.size(); ++g) {
+        out = applyGroup(this, b.s2c[g], S, {out}, false);
+        dbg(this, "s2c", out);
+    }
+    return out;
+}
+
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalBootstrap(const Ciphertext<DCRTPoly>& ct, uint32_t numIterations,
+                                                               uint32_t precision) {
+    if (numIterations <= 1) return BootstrapOnce(ct, 1.0, 1.0);
+    // meta-bootstrapping: out = BTS(ct) + BTS((ct - BTS(ct)) 2^p) 2^-p; the
+    // residual is formed at the deeper of the two levels
+    const double p2 = std::ldexp(1.0, precision ? (int)precision : 10);
+    auto first = BootstrapOnce(ct, 1.0, 1.0);
+    const uint32_t lv = std::max(ct->GetLevel(), first->GetLevel());
+    auto residual = [&](const Ciphertext<DCRTPoly>& approx) {
+        auto a = AdjustLevel(ct, lv), b = AdjustLevel(approx, lv);
+        a->SetSlots(ct->GetSlots());
+        b->SetSlots(ct->GetSlots());
+        return EvalSub(a, b);
+    };
+    auto fix = BootstrapOnce(residual(first), p2, 1.0 / p2);
+    for (uint32_t it = 2; it < numIterations; ++it)  // further passes on the residual (every BTS ends at one level)
+        fix = EvalAdd(fix, BootstrapOnce(residual(EvalAdd(first, fix)), p2, 1.0 / p2));
+    return EvalAdd(first, fix);
+}
+
+}  // namespace lbcrypto

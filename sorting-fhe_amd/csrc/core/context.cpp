@@ -337,16 +337,18 @@ class SfheInternal {
         return out;
     }
 
-    // Align ct to targetLevel (>= its level) with a scale-exact adjustment.
-    static Ct adjust(CC* cc, const Ct& ct, uint32_t target) {
+    // Align ct to targetLevel (>= its level) with a scale-exact adjustment;
+    // factor != 1 also multiplies the values by factor (same constant).
+    static Ct adjust(CC* cc, const Ct& ct, uint32_t target, double factor = 1.0) {
         SfheContextState* s = cc->st.get();
-        if (target == ct->level) return ct;
+        if (target == ct->level && factor == 1.0) return ct;
+        if (target <= ct->level && factor != 1.0) SFHE_THROW("a scaled adjustment needs a level to consume");
         if (target < ct->level) SFHE_THROW("cannot raise a ciphertext's level");
         if (target > s->L) SFHE_THROW("target level beyond multiplicative depth");
         uint32_t mid = target - 1;  // drop limbs (free), then one scaled rescale
         uint32_t ell = s->ellOf(mid);
         // result scale = scale_ct * K / q_{ell-1} = Delta_target
-        double K = s->scale[target] * (double)s->primes[ell - 1] / ct->scale;
+        double K = factor * s->scale[target] * (double)s->primes[ell - 1] / ct->scale;
         auto k = constResidues(s, K, ell);
         s->stats.constmult++;
         s->countBytes(4.0 * ell * s->n * 8);
@@ -1064,6 +1066,7 @@ CryptoContextImpl<DCRTPoly>::~CryptoContextImpl() {
     st->relinKey.reset();
     st->rotKeys.clear();
     st->ptCache.clear();
+    st->boot.clear();  // its diagonal encodings return blocks to the pool below
     for (auto& kv : st->modupConv)
         for (auto* c : kv.second) sfp_free_conv(st->dev, c);
     if (st->moddownConv) sfp_free_conv(st->dev, st->moddownConv);
@@ -1981,6 +1984,73 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::AdjustLevel(const Ciphertext<D
     return r == a ? a->Clone() : r;
 }
 
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::AdjustLevelScaled(const Ciphertext<DCRTPoly>& a,
+                                                                   uint32_t targetLevel, double factor) {
+    OpLock g(st.get());
+    SfheInternal::deps(st.get(), {&a});
+    auto r = SfheInternal::adjust(this, a, targetLevel, factor);
+    return r == a ? a->Clone() : r;
+}
+
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::ModRaise(const Ciphertext<DCRTPoly>& a) {
+    OpLock g(st.get());
+    SfheInternal::deps(st.get(), {&a});
+    SfheContextState* s = st.get();
+    if (s->world > 1) SFHE_THROW("bootstrapping a limb-sharded context is not supported");
+    if (s->ellOf(a->level) != 1) SFHE_THROW("ModRaise needs a ciphertext at the last level (one limb)");
+    const uint32_t n = s->n;
+    const u64 q0 = s->primes[0];
+    // coefficient form of both single-limb polys, centred lift to every Q limb
+    auto t = s->alloc(2 * (size_t)n);
+    sfp_d2d(s->dev, t->ptr, a->c0, (size_t)n * 8);
+    sfp_d2d(s->dev, t->ptr + n, a->c1, (size_t)n * 8);
+    sfp_ntt(s->dev, t->ptr, sfp_limbs{1, 1, 0, 0}, 1);
+    sfp_ntt(s->dev, t->ptr + n, sfp_limbs{1, 1, 0, 0}, 1);
+    std::vector<u64> h(2 * (size_t)n);
+    sfp_d2h(s->dev, h.data(), t->ptr, h.size() * 8);
+    auto out = SfheInternal::newCt(this, 0, a->slots);
+    std::vector<int64_t> c(n);
+    for (int p = 0; p < 2; ++p) {
+        for (uint32_t i = 0; i < n; ++i) {
+            const u64 v = h[(size_t)p * n + i];
+            c[i] = v > q0 / 2 ? -(int64_t)(q0 - v) : (int64_t)v;
+        }
+        uint64_t* dst = p ? out->c1 : out->c0;
+        sfp_load_i64(s->dev, dst, c.data(), s->qmap(s->Lq));
+        sfp_ntt(s->dev, dst, s->qmap(s->Lq), 0);
+    }
+    s->wrote(out->buf.get());
+    return SfheInternal::traced(this, out, "ModRaise");
+}
+
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalConjugate(const Ciphertext<DCRTPoly>& a) {
+    OpLock g(st.get());
+    SfheInternal::deps(st.get(), {&a});
+    SfheContextState* s = st.get();
+    const uint32_t gal = 2 * s->n - 1;  // X -> X^-1: complex conjugation of every slot
+    auto it = s->rotKeys.find(gal);
+    if (it == s->rotKeys.end()) SFHE_THROW("conjugation key not found (EvalConjugateKeyGen)");
+    const uint32_t ell = s->ellOf(a->level);
+    auto out = SfheInternal::newCt(this, a->level, a->slots);
+    auto t = s->alloc(s->polyWords(a->level));
+    sfp_automorph(s->dev, out->c0, a->c0, gal, st->qmap(ell));
+    sfp_automorph(s->dev, t->ptr, a->c1, gal, st->qmap(ell));
+    s->stats.automorph++;
+    SfheInternal::keySwitch(this, t->ptr, ell, it->second, out->c0, out->c1, 1, 0);
+    return SfheInternal::traced(this, out, "EvalConjugate");
+}
+
+void CryptoContextImpl<DCRTPoly>::EvalConjugateKeyGen(const PrivateKey<DCRTPoly>& sk) {
+    OpLock g(st.get());
+    SfheContextState* s = st.get();
+    const uint32_t gal = 2 * s->n - 1;
+    if (s->rotKeys.count(gal)) return;
+    const uint32_t NP = s->Lq + s->K;
+    auto sg = s->alloc((size_t)NP * s->n);
+    sfp_automorph(s->dev, sg->ptr, sk->s->ptr, gal, sfp_limbs{NP, NP, 0});
+    s->rotKeys[gal] = SfheInternal::genSwitchKey(this, sg->ptr, sk->s->ptr);
+}
+
 // ============================================================================
 // limb sharding
 
@@ -2150,17 +2220,5 @@ void CryptoContextImpl<DCRTPoly>::CopyCiphertextInto(const Ciphertext<DCRTPoly>&
 // ============================================================================
 // bootstrapping: the k-way / bitonic rows are next;
 // link-compatible entry points throw until then.
-
-void CryptoContextImpl<DCRTPoly>::EvalBootstrapSetup(std::vector<uint32_t>, std::vector<uint32_t>,
-                                                     uint32_t, uint32_t) {
-    SFHE_THROW("CKKS bootstrapping is not implemented in this engine yet (SURVEY §8(f) rank 2)");
-}
-void CryptoContextImpl<DCRTPoly>::EvalBootstrapKeyGen(const PrivateKey<DCRTPoly>&, uint32_t) {
-    SFHE_THROW("CKKS bootstrapping is not implemented in this engine yet (SURVEY §8(f) rank 2)");
-}
-Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalBootstrap(const Ciphertext<DCRTPoly>&,
-                                                               uint32_t, uint32_t) {
-    SFHE_THROW("CKKS bootstrapping is not implemented in this engine yet (SURVEY §8(f) rank 2)");
-}
 
 }  // namespace lbcrypto

@@ -359,6 +359,18 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
     Ciphertext<DCRTPoly> ModReduce(const Ciphertext<DCRTPoly>& a) { return Rescale(a); }
     void LevelReduceInPlace(Ciphertext<DCRTPoly>& a, std::nullptr_t, size_t levels);
     Ciphertext<DCRTPoly> AdjustLevel(const Ciphertext<DCRTPoly>& a, uint32_t targetLevel);
+    // Engine internals of CKKS bootstrapping (bootstrap.cpp):
+    //  * AdjustLevelScaled: AdjustLevel that also multiplies the values by
+    //    `factor` (folded into the level adjustment's constant; no extra level);
+    //  * ModRaise: a ciphertext at the last level (one limb, q_0) lifted to the
+    //    whole chain: its centred residues mod q_0 taken as integers, so it now
+    //    decrypts to m + q_0 I(X) at level 0 (labelled with level 0's scale);
+    //  * EvalConjugate: slot-wise complex conjugation (automorphism X -> X^-1)
+    //    with the key EvalConjugateKeyGen makes.
+    Ciphertext<DCRTPoly> AdjustLevelScaled(const Ciphertext<DCRTPoly>& a, uint32_t targetLevel, double factor);
+    Ciphertext<DCRTPoly> ModRaise(const Ciphertext<DCRTPoly>& a);
+    Ciphertext<DCRTPoly> EvalConjugate(const Ciphertext<DCRTPoly>& a);
+    void EvalConjugateKeyGen(const PrivateKey<DCRTPoly>& sk);
 
     // bootstrapping (needed only by the k-way / bitonic rows; link-only here)
     void EvalBootstrapSetup(std::vector<uint32_t> levelBudget, std::vector<uint32_t> dim1 = {0, 0},
@@ -366,6 +378,11 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
     void EvalBootstrapKeyGen(const PrivateKey<DCRTPoly>& sk, uint32_t slots);
     Ciphertext<DCRTPoly> EvalBootstrap(const Ciphertext<DCRTPoly>& ct, uint32_t numIterations = 1,
                                        uint32_t precision = 0);
+    // Engine extensions: the levels EvalBootstrap consumes (counted from the
+    // top of the chain: its output level), and one bootstrapping pass with
+    // the values scaled by inFactor on the way in and outFactor on the way out
+    uint32_t GetBootstrapDepth(const std::vector<uint32_t>& levelBudget, uint32_t slots = 0) const;
+    Ciphertext<DCRTPoly> BootstrapOnce(const Ciphertext<DCRTPoly>& ct, double inFactor, double outFactor);
 
     // ---------------- engine extensions (not OpenFHE) ----------------
     SfheContextState* state() const { return st.get(); }

@@ -28,6 +28,8 @@ class DeviceBuffer {
     sfp_event* ready = nullptr;    // shared encodings: end of the producing work
 };
 
+struct BootstrapPrecomp;  // bootstrap.cpp
+
 struct PtCacheEntry {
     std::vector<std::complex<double>> values;
     uint32_t slots;
@@ -65,6 +67,8 @@ struct SfheContextState {
     DeviceBufferPtr relinKey;
     std::map<uint32_t, DeviceBufferPtr> rotKeys;  // galois -> key
     std::set<int32_t> rotIndices;
+    // bootstrapping precomputations per slot count (EvalBootstrapSetup)
+    std::map<uint32_t, std::shared_ptr<BootstrapPrecomp>> boot;
 
     // memory pool (device words -> free list)
     std::mutex poolMu;

@@ -37,6 +37,7 @@ ABI_SYMBOLS = [
     "sfhe_comm_uid", "sfhe_shard_rccl", "sfhe_shard_host", "sfhe_pool_bytes",
     "sfhe_serialize_lanes", "sfhe_sorter_graph_nodes", "sfhe_sorter_create_rot",
     "sfhe_sorter_sort_hybrid1", "sfhe_hybrid1_params", "sfhe_sorter_graph_ntt_time",
+    "sfhe_bootstrap_setup", "sfhe_bootstrap_depth", "sfhe_bootstrap",
 ]
 
 
@@ -102,6 +103,9 @@ _SIGS = {
     "sfhe_eval_mult_plain": (C.c_int, [_VP, _VP, _PD, _SZ, _U32, _PVP]),
     "sfhe_eval_mult": (C.c_int, [_VP, _VP, _VP, _PVP]),
     "sfhe_eval_rotate": (C.c_int, [_VP, _VP, C.c_int32, _PVP]),
+    "sfhe_bootstrap_setup": (C.c_int, [_VP, _U32, _U32, _U32]),
+    "sfhe_bootstrap_depth": (C.c_int, [_VP, _U32, _U32, _U32, _PU32]),
+    "sfhe_bootstrap": (C.c_int, [_VP, _VP, _U32, _U32, _PVP]),
     "sfhe_eval_chebyshev": (C.c_int, [_VP, _VP, _PD, _SZ, C.c_double, C.c_double, _PVP]),
     "sfhe_sign": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_int, _PVP]),
     "sfhe_compare": (C.c_int, [_VP, _VP, _VP, C.c_int, C.c_int, C.c_int, _PVP]),
@@ -323,6 +327,18 @@ class Engine:
 
     def rotate(self, a, r: int):
         return self._new(self.lib.sfhe_eval_rotate, self.ctx, a.h, int(r))
+
+    def bootstrap_setup(self, level_budget=(5, 5), slots: int = 0):
+        """EvalBootstrapSetup + EvalBootstrapKeyGen for `slots`-slot ciphertexts."""
+        self._chk(self.lib.sfhe_bootstrap_setup(self.ctx, level_budget[0], level_budget[1], slots))
+
+    def bootstrap_depth(self, level_budget=(5, 5), slots: int = 0) -> int:
+        v = C.c_uint32()
+        self._chk(self.lib.sfhe_bootstrap_depth(self.ctx, level_budget[0], level_budget[1], slots, C.byref(v)))
+        return v.value
+
+    def bootstrap(self, a, iterations: int = 1, precision: int = 0):
+        return self._new(self.lib.sfhe_bootstrap, self.ctx, a.h, iterations, precision)
 
     def chebyshev(self, x, coeffs: Sequence[float], a: float = -1.0, b: float = 1.0):
         return self._new(self.lib.sfhe_eval_chebyshev, self.ctx, x.h, _darr(coeffs), len(coeffs),

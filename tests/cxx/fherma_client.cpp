@@ -3,12 +3,13 @@
 // and keys, encrypt an input array, serialize everything for src/main.cpp;
 // afterwards decrypt its output and check it is the sorted input.
 //   fherma_client keygen <dir> <logn> <depth> <batch> <N> <seed>
-//   fherma_client check  <dir> <N>           (exit 0: max error < 0.01)
+//   fherma_client check  <dir> <N> [tol]     (exit 0: max error < tol, default 0.01)
 // Mirrors the reference's src/config.json parameters (ring, depth, scale 40,
 // batch, rotation indexes).
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <fstream>
 #include <random>
 #include <string>
@@ -83,7 +84,8 @@ int main(int argc, char** argv) {
         double err = 0;
         for (int i = 0; i < N; ++i) err = std::max(err, std::fabs(got[i] - x[i]));
         std::printf("check: level %u, max error %.3g\n", out->GetLevel(), err);
-        return err < 0.01 ? 0 : 1;
+        const double tol = argc > 4 ? std::atof(argv[4]) : 0.01;
+        return err < tol ? 0 : 1;
     }
     return 2;
 }

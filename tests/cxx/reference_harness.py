@@ -45,6 +45,9 @@ PROGRAMS = {
     "RotationTest": (["tests/RotationTest.cpp"], True, False),
     "DecomposeTest": (["tests/DecomposeTest.cpp"], True, False),
     "SortNBenchmark": (["benchmarks/SortNBenchmark.cpp"], False, False),
+    # BitonicSort<N> + CKKS bootstrapping, SURVEY §8(f) rows 2-3
+    "BitonicSortTest": (["tests/BitonicSortTest.cpp"], True, False),
+    "BitonicSortBenchmark": (["benchmarks/BitonicSortBenchmark.cpp"], False, False),
     # the FHERMA-style server (src/sort.h SortContext + src/main.cpp), SURVEY §8(f) row 4
     "main": (["src/main.cpp"], False, False),
 }

@@ -126,3 +126,23 @@ def test_direct_sort_h1_test(hip_lib):
     assert rc == 0, out[-4000:]
     assert "7 tests ran, 0 failed" in out
     assert len(errs) == 7 and max(errs) < 0.01
+
+
+def test_bitonic_sort_test(hip_lib):
+    """tests/BitonicSortTest.cpp as-is: BitonicSort<4> at ring 2^12, depth 58,
+    two meta-bootstraps (EvalBootstrap(ct, 2, 20)); max error < 1, none > 0.1."""
+    rc, out = run(exe("BitonicSortTest"))
+    assert rc == 0 and "1 tests ran, 0 failed" in out, out[-3000:]
+    err = float(re.search(r"Maximum error: ([0-9.e+-]+)", out).group(1))
+    print("BitonicSortTest max error", err)
+    assert err < 1e-3
+
+
+def test_sortn_benchmark_bitonic(hip_lib):
+    """benchmarks/SortNBenchmark.cpp as-is, BM_BitonicSort<4> and <8>: ring
+    2^17, depth 58, levelBudget {4,4} (SortNBenchmark.cpp:62-91) -- the
+    bitonic half of the benchmark runs to completion on the engine."""
+    rc, out = run(exe("SortNBenchmark"), "--benchmark_filter=BM_BitonicSort<(4|8)>", timeout=600)
+    print(out[-1500:])
+    assert rc == 0, out[-3000:]
+    assert re.search(r"BM_BitonicSort<4>\S*\s+[0-9.]+ ms", out) and re.search(r"BM_BitonicSort<8>\S*\s+[0-9.]+ ms", out)

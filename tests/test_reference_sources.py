@@ -90,3 +90,14 @@ def test_direct_sort_h1_test_n4(built):
     assert "Result Level: 31" in out
     err = float(re.search(r"Maximum error: ([0-9.e+-]+)", out).group(1))
     assert err < 1e-3, err
+
+
+def test_bitonic_sort_test(built):
+    """tests/BitonicSortTest.cpp as-is (BitonicSort<4>, ring 2^12, depth 58,
+    scale 59, levelBudget {3,3}, EvalBootstrap(ct, 2, 20) whenever the level
+    passes 29): max error < 1, none above 0.1."""
+    rc, out = run(built[("BitonicSortTest", "oracle")], timeout=900)
+    assert rc == 0 and "1 tests ran, 0 failed" in out, out[-3000:]
+    assert out.count("Loop k:") == 3
+    err = float(re.search(r"Maximum error: ([0-9.e+-]+)", out).group(1))
+    assert err < 1e-3, err
