@@ -53,7 +53,7 @@ namespace {
 
 using cd = std::complex<double>;
 
-constexpr int kTargetBits = 13;   // step 1: |m/q_0| <~ 2^-13 (sin(2 pi x)/(2 pi) ~ x to 2^-25)
+constexpr int kTargetBits = 10;   // step 1: |m/q_0| <~ 2^-10 (sin(2 pi x)/(2 pi) ~ x to 2^-17, OpenFHE's default correction)
 constexpr uint32_t kDoubleAngles = 6;
 constexpr uint32_t kChebDegree = 89;
 constexpr double kOverflowBound = 512.0;  // |I| bound, uniform ternary secret (OpenFHE K_UNIFORM)

@@ -801,6 +801,94 @@ __global__ __launch_bounds__(kNttTile >> LE) void k_ntt(const RowGroup G, const 
 #endif
 }
 
+// Rings of at most one tile per row (n <= kNttTile = 2^11: the test
+// rings the reference's k-way unit tests use, 2^10): the whole row in LDS, every
+// stage in one block, exact radix-2 butterflies (the oracle's schedule, so
+// canonical outputs), the same prologue (copy / pre / preK / lift) and
+// epilogue (epi / emul / emK / addMask / eadd) as the two-pass kernel.  Not a
+// performance path: one 256-thread block per row.
+constexpr int kNttSmallThreads = 256;
+template <bool INV>
+__global__ __launch_bounds__(kNttSmallThreads) void k_ntt_small(const RowGroup G, const sf_barrett* __restrict__ bar,
+                                                               const u64* __restrict__ tw, const u64* __restrict__ twS,
+                                                               const u64* __restrict__ ninv,
+                                                               const u64* __restrict__ ninvS, uint32_t logn) {
+    __shared__ u64 s[kNttTile];
+    const uint32_t n = 1u << logn;
+    const uint32_t rid = blockIdx.y;
+    const uint32_t pp = rid / G.R, ii = rid % G.R;
+    if (G.skipEll && ii >= G.alpha * pp && ii < min(G.alpha * (pp + 1), G.skipEll)) return;
+    const uint32_t prime = primeOf(G.pm, ii);
+    const u64 q = bar[prime].q;
+    const u64* in = rowAt(G.src, pp, ii);
+    u64* cp = nullptr;
+    if (G.copy.base)
+        cp = G.copyByAlpha ? const_cast<u64*>(G.copy.base) + (ii / G.alpha) * G.copy.ps + ii * G.copy.is
+                           : rowAt(G.copy, pp, ii);
+    const u64* pre = G.pre.base ? rowAt(G.pre, pp, ii) : nullptr;
+    const bool preK = G.preK != nullptr;
+    const u64 pk = preK ? G.preK[ii] : 0, pkS = preK ? G.preKS[ii] : 0;
+    const sf_barrett LB = (G.lift || pre) ? loadBar(bar, prime) : sf_barrett{};
+    const u64 lsub = G.lift ? G.liftSub[ii] : 0;
+    const u64 lhalf = G.lift ? (bar[G.liftPrime].q >> 1) : 0;
+    for (uint32_t x = threadIdx.x; x < n; x += kNttSmallThreads) {
+        u64 v = in[x];
+        if (cp) cp[x] = v;
+        if (pre) v = bmul(v, pre[x], LB);
+        if (preK) v = sf_mul_shoup(v, pk, pkS, q);
+        if (G.lift) {
+            u64 r = sf_reduce128(v, 0, &LB);
+            v = v > lhalf ? sf_sub(r, lsub, q) : r;
+        }
+        s[x] = v;
+    }
+    __syncthreads();
+    const u64* w = tw + (size_t)prime * n;
+    const u64* wS = twS + (size_t)prime * n;
+    for (uint32_t st = 0; st < logn; ++st) {
+        // forward: m = 2^st groups of span 2t; inverse: the same stages reversed
+        const uint32_t m = INV ? (n >> (st + 1)) : (1u << st);
+        const uint32_t t = (n >> 1) / m;
+        for (uint32_t b = threadIdx.x; b < n / 2; b += kNttSmallThreads) {
+            const uint32_t i = b / t, j = b % t, x = 2 * i * t + j;
+            const u64 S = w[m + i], Sp = wS[m + i];
+            const u64 U = s[x], V = s[x + t];
+            if (INV) {
+                s[x] = sf_add(U, V, q);
+                s[x + t] = sf_mul_shoup(sf_sub(U, V, q), S, Sp, q);
+            } else {
+                const u64 VW = sf_mul_shoup(V, S, Sp, q);
+                s[x] = sf_add(U, VW, q);
+                s[x + t] = sf_sub(U, VW, q);
+            }
+        }
+        __syncthreads();
+    }
+    const bool epi = G.epi != 0;
+    u64* out = epi ? rowAt(G.eout, pp, ii) : rowAt(G.dst, pp, ii);
+    const u64* ein = epi ? rowAt(G.ein, pp, ii) : nullptr;
+    const u64 ek = epi ? G.k[ii] : 0, ekS = epi ? G.kS[ii] : 0;
+    const u64* ead = epi && G.eadd.base ? rowAt(G.eadd, pp, ii) : nullptr;
+    const u64 ek2 = ead ? G.k2[ii] : 0, ek2S = ead ? G.k2S[ii] : 0;
+    const u64* emul = epi && G.emul.base ? rowAt(G.emul, pp, ii) : nullptr;
+    const bool emK = epi && G.emK;
+    const u64 emk = emK ? G.emK[ii] : 0, emkS = emK ? G.emKS[ii] : 0;
+    const sf_barrett EB = emul ? loadBar(bar, prime) : sf_barrett{};
+    for (uint32_t x = threadIdx.x; x < n; x += kNttSmallThreads) {
+        u64 v = s[x];
+        if (INV) v = sf_mul_shoup(v, ninv[prime], ninvS[prime], q);
+        if (epi) {
+            u64 a = ein[x];
+            if (emul) a = bmul(a, emul[x], EB);
+            if (emK) a = sf_mul_shoup(a, emk, emkS, q);
+            v = sf_mul_shoup(sf_sub(a, v, q), ek, ekS, q);
+            if ((G.addMask >> pp) & 1u) v = sf_add(v, out[x], q);
+            if (ead) v = sf_add(v, sf_mul_shoup(ead[x], ek2, ek2S, q), q);
+        }
+        out[x] = v;
+    }
+}
+
 // ============================================================================
 // elementwise kernels: one thread per pair of coefficients (16 B per lane)
 
@@ -1836,9 +1924,9 @@ sfp_dev* sfp_create(int device, const sfp_tables* t) {
     d->logn = t->logn;
     d->n = 1u << t->logn;
     d->np = t->nprimes;
-    if (d->logn < 12) {
+    if (d->logn < 10) {
         delete d;
-        return nullptr;  // kernels assume n >= 4096
+        return nullptr;  // rings from 2^10 (up to 2^11 the NTT runs k_ntt_small)
     }
     d->nLanes = 4;
     if (const char* v = std::getenv("SFHE_LANES")) d->nLanes = std::max(1, std::min(SFP_MAX_LANES, std::atoi(v)));
@@ -2082,8 +2170,20 @@ static void nttRows(sfp_dev* d, const RowGroup& G, int inverse) {
     const uint32_t rows = G.P * G.R;
     if (!rows || !limbsOk(d, G.pm, "ntt")) return;
     if (G.lift && G.liftPrime >= d->np) return (void)limbsOk(d, sfp_limbs{1, 1, G.liftPrime, G.liftPrime}, "ntt lift");
-    const dim3 g(d->n / kNttTile, rows);
     const double bytes = 16.0 * rows * d->n;
+    if (d->n <= (uint32_t)kNttTile) {  // small rings: one single-pass block per row
+        timedLaunch(d, SFP_FAM_NTT, bytes, [&] {
+            if (inverse)
+                hipLaunchKernelGGL(k_ntt_small<true>, dim3(1, rows), dim3(kNttSmallThreads), 0, d->st(), G, d->bar,
+                                   d->ipsi, d->ipsiS, d->ninv, d->ninvS, d->logn);
+            else
+                hipLaunchKernelGGL(k_ntt_small<false>, dim3(1, rows), dim3(kNttSmallThreads), 0, d->st(), G, d->bar,
+                                   d->psi, d->psiS, d->ninv, d->ninvS, d->logn);
+        });
+        checkLaunch(d, "ntt");
+        return;
+    }
+    const dim3 g(d->n / kNttTile, rows);
     const u64* tw = inverse ? d->ipsi : d->psi;
     const u64* twS = inverse ? d->ipsiS : d->psiS;
     const double* twD = inverse ? d->ipsiD : d->psiD;

@@ -48,6 +48,16 @@ PROGRAMS = {
     # BitonicSort<N> + CKKS bootstrapping, SURVEY §8(f) rows 2-3
     "BitonicSortTest": (["tests/BitonicSortTest.cpp"], True, False),
     "BitonicSortBenchmark": (["benchmarks/BitonicSortBenchmark.cpp"], False, False),
+    # the k-way network (src/k-way/*, src/kway_adapter.h; SURVEY §8(f) row 2, BASELINE config 4)
+    "KWaySortTest": (["tests/KWaySortTest.cpp"], False, False),
+    "KWayMaskingTest": (["tests/k-way/MaskingTest.cpp"], False, False),
+    "KWayEvalUtilsTest": (["tests/k-way/EvalUtilsTest.cpp"], False, False),
+    "KWaySortUtilsTest": (["tests/k-way/SortUtilsTest.cpp"], False, False),
+    "KWaySorterTest": (["tests/k-way/SorterTest.cpp"], False, False),
+    "KWaySort2Test": (["tests/k-way/KWaySort2Test.cpp"], False, True),
+    "KWaySort3Test": (["tests/k-way/KWaySort3Test.cpp"], False, True),
+    "KWaySort5Test": (["tests/k-way/KWaySort5Test.cpp"], False, True),
+    "KWaySort235Test": (["tests/k-way/KWaySort235Test.cpp"], False, False),
     # the FHERMA-style server (src/sort.h SortContext + src/main.cpp), SURVEY §8(f) row 4
     "main": (["src/main.cpp"], False, False),
 }
@@ -59,7 +69,7 @@ OWN = {"fherma_client": os.path.join(HERE, "fherma_client.cpp")}
 def _engine_mtime() -> float:
     """Newest engine header: objects compiled against older headers are stale."""
     t = 0.0
-    for d, _, fs in os.walk(CSRC):
+    for d, _, fs in list(os.walk(CSRC)) + list(os.walk(SHIM)):
         for f in fs:
             if f.endswith(".h"):
                 t = max(t, os.path.getmtime(os.path.join(d, f)))
@@ -90,8 +100,11 @@ def flags():
     # include forms; libstdc++'s pstl headers quote-include their siblings,
     # hence their directory)
     return ["-O2", "-std=c++17", "-fopenmp", "-DENABLE_PRINT_PT", "-I-",
-            "-I" + os.path.join(CSRC, "core"), "-I" + os.path.join(CSRC, "algo"), "-I" + CSRC,
+            "-I" + os.path.join(CSRC, "core"), "-I" + os.path.join(CSRC, "algo"), "-I" + os.path.join(CSRC, "algo", "k-way"),
+            "-I" + CSRC,
             "-I" + os.path.join(ROOT, "include"), "-I" + SHIM, "-I" + os.path.join(REF, "tests"),
+            # the k-way tests include "../utils.h" from tests/k-way (test .cpp files only there)
+            "-I" + os.path.join(REF, "tests", "k-way"),
             "-I" + PSTL, "-w"]
 
 

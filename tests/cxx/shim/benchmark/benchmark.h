@@ -2,13 +2,14 @@
 // the API for the reference's benchmarks/SortNBenchmark.cpp to compile
 // unchanged (its third_party/benchmark submodule is empty here).  Each
 // registered benchmark runs `--benchmark_min_iters` (default 1) iterations,
-// selected by --benchmark_filter=<substring>, and prints wall ms/iteration.
+// selected by --benchmark_filter=<regex> (searched, as google-benchmark does), and prints wall ms/iteration.
 #pragma once
 #include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <functional>
 #include <map>
+#include <regex>
 #include <string>
 #include <vector>
 
@@ -66,7 +67,7 @@ inline int run(int argc, char** argv) {
         if (!std::strcmp(argv[i], "--benchmark_list_tests")) list = true;
     }
     for (auto* b : all()) {
-        if (!filter.empty() && b->name.find(filter) == std::string::npos) continue;
+        if (!filter.empty() && !std::regex_search(b->name, std::regex(filter))) continue;
         if (list) {
             std::printf("%s\n", b->name.c_str());
             continue;

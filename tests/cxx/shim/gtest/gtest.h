@@ -4,9 +4,10 @@
 // UNCHANGED against this engine's headers by tests/cxx/reference_harness.py;
 // googletest itself is not in this image (its submodule in the reference is
 // empty), so this header provides the subset those files use: TEST, TEST_F,
-// typed-parameterised suites (TYPED_TEST_SUITE_P / TYPED_TEST_P /
+// typed suites (TYPED_TEST_SUITE / TYPED_TEST), typed-parameterised suites
+// (TYPED_TEST_SUITE_P / TYPED_TEST_P /
 // REGISTER_TYPED_TEST_SUITE_P / INSTANTIATE_TYPED_TEST_SUITE_P over
-// ::testing::Types), EXPECT_/ASSERT_ {EQ,NE,LT,LE,GT,GE,NEAR,TRUE,FALSE} with
+// ::testing::Types), FAIL, EXPECT_/ASSERT_ {EQ,NE,LT,LE,GT,GE,NEAR,TRUE,FALSE} with
 // streamed messages, AssertionResult, InitGoogleTest, RUN_ALL_TESTS and
 // --gtest_filter (':'-separated globs, '-' for negatives).
 #pragma once
@@ -106,7 +107,15 @@ inline bool anyMatch(const std::string& pats, const std::string& name) {
     }
     return false;
 }
+inline bool& alsoRunDisabled() {
+    static bool b = false;
+    return b;
+}
 inline bool selected(const std::string& name) {
+    // DISABLED_ suites / tests run only on request, as in googletest
+    if (!alsoRunDisabled() && (name.rfind("DISABLED_", 0) == 0 || name.find(".DISABLED_") != std::string::npos ||
+                               name.find("/DISABLED_") != std::string::npos))
+        return false;
     const std::string& f = filter();
     const size_t dash = f.find('-');
     const std::string pos = dash == std::string::npos ? f : f.substr(0, dash);
@@ -158,7 +167,10 @@ inline std::string why(bool) { return ""; }
 
 inline void InitGoogleTest(int* argc, char** argv) {
     for (int i = 1; argc && i < *argc; ++i)
-        if (std::strncmp(argv[i], "--gtest_filter=", 15) == 0) internal::filter() = argv[i] + 15;
+        if (std::strncmp(argv[i], "--gtest_filter=", 15) == 0)
+            internal::filter() = argv[i] + 15;
+        else if (std::strcmp(argv[i], "--gtest_also_run_disabled_tests") == 0)
+            internal::alsoRunDisabled() = true;
 }
 inline void InitGoogleTest() {}
 
@@ -266,6 +278,31 @@ struct ForTypes<R, ::testing::Types<Ts...>> {
     static const bool SHIM_CAT(SHIM_CAT(Prefix, F), _inst) =                                      \
         ::testing::internal::ForTypes<SHIM_CAT(F, _ShimRegs), TypesList>::run(#Prefix "/" #F)
 
+// typed suites: TYPED_TEST_SUITE(F, Types) names the type list, each
+// TYPED_TEST(F, Name) registers itself for every type in it (F/0.Name, ...)
+#define TYPED_TEST_SUITE(F, TypesList) typedef TypesList SHIM_CAT(F, _ShimTypes)
+#define TYPED_TEST(F, Name)                                                                       \
+    template <class gtest_TypeParam_>                                                             \
+    class SHIM_CAT(F, SHIM_CAT(_, Name)) : public F<gtest_TypeParam_> {                          \
+      public:                                                                                     \
+        typedef F<gtest_TypeParam_> TestFixture;                                                  \
+        typedef gtest_TypeParam_ TypeParam;                                                       \
+        void TestBody() override;                                                                 \
+    };                                                                                            \
+    template <class T>                                                                            \
+    struct SHIM_CAT(F, SHIM_CAT(_, SHIM_CAT(Name, _TReg))) {                                      \
+        static void reg(const std::string& prefix) {                                              \
+            ::testing::internal::registerTest(prefix + "." #Name, [] {                            \
+                return static_cast<::testing::Test*>(new SHIM_CAT(F, SHIM_CAT(_, Name))<T>());    \
+            });                                                                                   \
+        }                                                                                         \
+    };                                                                                            \
+    static const bool SHIM_CAT(F, SHIM_CAT(_, SHIM_CAT(Name, _inst))) =                           \
+        ::testing::internal::ForTypes<SHIM_CAT(F, SHIM_CAT(_, SHIM_CAT(Name, _TReg))),            \
+                                      SHIM_CAT(F, _ShimTypes)>::run(#F);                          \
+    template <class gtest_TypeParam_>                                                             \
+    void SHIM_CAT(F, SHIM_CAT(_, Name))<gtest_TypeParam_>::TestBody()
+
 // assertions
 #define SHIM_ASSERT_(ok, text, fatal) \
     if (ok)                           \
@@ -276,6 +313,8 @@ struct ForTypes<R, ::testing::Types<Ts...>> {
 #define SHIM_FAIL_0(text) ::testing::internal::Helper{__FILE__, __LINE__, text, false} = ::testing::Message()
 #define SHIM_CMP_(a, op, b, fatal) \
     SHIM_ASSERT_(((a)op(b)), ::testing::internal::cmpText(#a, #op, #b, (a), (b)), fatal)
+#define FAIL() SHIM_FAIL_1("Failed")
+#define ADD_FAILURE() SHIM_FAIL_0("Failed")
 #define EXPECT_EQ(a, b) SHIM_CMP_(a, ==, b, 0)
 #define EXPECT_NE(a, b) SHIM_CMP_(a, !=, b, 0)
 #define EXPECT_LT(a, b) SHIM_CMP_(a, <, b, 0)

@@ -105,13 +105,13 @@ def test_bootstrap_bitexact_hip_vs_oracle(hip_lib, oracle_lib):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("S,budget,depth,iters,bound", [
-    (1024, (5, 5), 40, 1, 2.0 ** -12),   # k-way config: kway_adapter.h:41-64
-    (128, (4, 4), 58, 2, 2.0 ** -25),    # BitonicSortBenchmark.cpp:27-51, EvalBootstrap(ct, 2, 20)
+@pytest.mark.parametrize("S,budget,depth,iters,secure,bound", [
+    (1024, (5, 5), 40, 1, True, 2.0 ** -12),   # k-way config: kway_adapter.h:41-64, HEStd_128_classic
+    (128, (4, 4), 58, 2, False, 2.0 ** -25),   # SortNBenchmark.cpp:62-91 (HEStd_NotSet), EvalBootstrap(ct, 2, 20)
 ])
-def test_bootstrap_ring17(hip_lib, S, budget, depth, iters, bound):
+def test_bootstrap_ring17(hip_lib, S, budget, depth, iters, secure, bound):
     import time
-    e = boot_engine("hip", 17, S, depth, budget, secure=True)
+    e = boot_engine("hip", 17, S, depth, budget, secure=secure)
     _, err = bootstrap_error(e, S, iters)  # first call encodes the diagonals
     t0 = time.perf_counter()
     out, err = bootstrap_error(e, S, iters, seed=2)

@@ -102,3 +102,25 @@ def test_direct_sort_bitexact(hip_lib, oracle_lib, N):
     assert outs[0].level == depth
     got = np.array(g.decrypt(outs[0]))
     assert np.max(np.abs(got - np.sort(x))) < 0.01
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("logn", [10, 11])
+def test_small_ring_bitexact(hip_lib, oracle_lib, logn):
+    """Rings below 2^12 (k_ntt_small: one single-pass block per row) -- the
+    ring the reference's k-way unit tests use (tests/k-way/MaskingTest.cpp:15,
+    tests/KWaySortTest.cpp:24): encrypt, multiply, rotate, rescale bit for bit
+    against the oracle."""
+    raw = {}
+    for backend in ("hip", "oracle"):
+        e = sfhe.Engine(backend, mult_depth=4, ring_dim=1 << logn, batch_size=8, rotations=[1, -2],
+                        seed=77, device=0)
+        e.set_quiet(True)
+        a = e.encrypt([0.5, -0.25, 0.125, 0.75, 0.1, 0.2, 0.3, 0.4])
+        b = e.rotate(e.mult(a, a), 1)
+        c = e.rotate(e.mult_const(b, 0.5), -2)
+        raw[backend] = c.download()
+        got = np.array(e.decrypt(c))[:8]
+        x = np.array([0.5, -0.25, 0.125, 0.75, 0.1, 0.2, 0.3, 0.4]) ** 2 * 0.5
+        assert np.allclose(got, np.roll(np.roll(x, -1), 2), atol=1e-4), (backend, got)
+    assert np.array_equal(raw["hip"], raw["oracle"])

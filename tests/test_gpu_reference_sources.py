@@ -146,3 +146,36 @@ def test_sortn_benchmark_bitonic(hip_lib):
     print(out[-1500:])
     assert rc == 0, out[-3000:]
     assert re.search(r"BM_BitonicSort<4>\S*\s+[0-9.]+ ms", out) and re.search(r"BM_BitonicSort<8>\S*\s+[0-9.]+ ms", out)
+
+
+@pytest.mark.parametrize("prog,count", [("KWayMaskingTest", 4), ("KWaySortUtilsTest", 11), ("KWayEvalUtilsTest", 6),
+                                        ("KWaySorterTest", 5), ("KWaySortTest", 1)])
+def test_kway_unit_tests(hip_lib, prog, count):
+    """The k-way unit tests and KWaySortTest (512 at ring 2^10) on the product."""
+    rc, out = run(exe(prog), timeout=400)
+    assert rc == 0 and f"{count} tests ran, 0 failed" in out, out[-3000:]
+
+
+def test_kway_sort2_test(hip_lib):
+    """tests/k-way/KWaySort2Test.cpp as-is: KWayAdapter<N>, k = 2, at ring 2^17,
+    HEStd_128_classic, depth 40, scale 59, levelBudget {4,4} / {5,5}, sparse
+    slots = N, CompositeSign(3, d_f, d_g) with lazy bootstrapping; max error
+    < 0.01 and none >= 0.01.  N = 4 .. 1024 (BASELINE config 4 is N = 1024)."""
+    rc, out = run(exe("KWaySort2Test"), timeout=900)
+    errs = [float(x) for x in re.findall(r"Maximum error: ([0-9.e+-]+)", out)]
+    times = [int(x) for x in re.findall(r"Execution time: (\d+) ms", out)]
+    print("max errors:", errs, "\nexecution ms:", times)
+    assert rc == 0, out[-4000:]
+    assert "9 tests ran, 0 failed" in out
+
+
+@pytest.mark.parametrize("prog,count", [("KWaySort3Test", 5), ("KWaySort5Test", 3)])
+def test_kway_sort35_test(hip_lib, prog, count):
+    """tests/k-way/KWaySort{3,5}Test.cpp as-is: k = 3 (N = 9 .. 729) and k = 5
+    (N = 25 .. 625) at ring 2^17, the 3- / 4- / 5- / mixed 2..5-sorter stages."""
+    rc, out = run(exe(prog), timeout=900)
+    errs = [float(x) for x in re.findall(r"Maximum error: ([0-9.e+-]+)", out)]
+    times = [int(x) for x in re.findall(r"Execution time: (\d+) ms", out)]
+    print(prog, "max errors:", errs, "\nexecution ms:", times)
+    assert rc == 0, out[-4000:]
+    assert f"{count} tests ran, 0 failed" in out

@@ -101,3 +101,24 @@ def test_bitonic_sort_test(built):
     assert out.count("Loop k:") == 3
     err = float(re.search(r"Maximum error: ([0-9.e+-]+)", out).group(1))
     assert err < 1e-3, err
+
+
+@pytest.mark.parametrize("prog,count", [("KWayMaskingTest", 4), ("KWaySortUtilsTest", 11), ("KWayEvalUtilsTest", 6),
+                                        ("KWaySorterTest", 5)])
+def test_kway_unit_tests(built, prog, count):
+    """tests/k-way/{Masking,SortUtils,EvalUtils,Sorter}Test.cpp as-is against the
+    engine's k-way module (SorterTest's DISABLED_Run2345Sorter stays disabled,
+    as googletest runs it)."""
+    rc, out = run(built[(prog, "oracle")], timeout=900)
+    assert rc == 0 and f"{count} tests ran, 0 failed" in out, out[-3000:]
+
+
+def test_kway_sort_test(built):
+    """tests/KWaySortTest.cpp as-is: KWayAdapter<512> (k = 2, M = 9: 45 network
+    stages) at ring 2^10 with full-slot bootstrapping ({5,5}) under
+    CompositeSign(3, 2, 5) with lazy bootstrapping; max error < 0.01."""
+    rc, out = run(built[("KWaySortTest", "oracle")], timeout=900)
+    assert rc == 0 and "1 tests ran, 0 failed" in out, out[-3000:]
+    assert out.count(" == End stage ") == 45
+    err = float(re.search(r"Maximum error: ([0-9.e+-]+)", out).group(1))
+    assert err < 1e-3, err
