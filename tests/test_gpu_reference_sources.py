@@ -149,7 +149,7 @@ def test_sortn_benchmark_bitonic(hip_lib):
 
 
 @pytest.mark.parametrize("prog,count", [("KWayMaskingTest", 4), ("KWaySortUtilsTest", 11), ("KWayEvalUtilsTest", 6),
-                                        ("KWaySorterTest", 5), ("KWaySortTest", 1)])
+                                        ("KWaySorterTest", 7), ("KWaySortTest", 1)])
 def test_kway_unit_tests(hip_lib, prog, count):
     """The k-way unit tests and KWaySortTest (512 at ring 2^10) on the product."""
     rc, out = run(exe(prog), timeout=400)

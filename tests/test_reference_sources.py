@@ -104,7 +104,7 @@ def test_bitonic_sort_test(built):
 
 
 @pytest.mark.parametrize("prog,count", [("KWayMaskingTest", 4), ("KWaySortUtilsTest", 11), ("KWayEvalUtilsTest", 6),
-                                        ("KWaySorterTest", 5)])
+                                        ("KWaySorterTest", 7)])
 def test_kway_unit_tests(built, prog, count):
     """tests/k-way/{Masking,SortUtils,EvalUtils,Sorter}Test.cpp as-is against the
     engine's k-way module (SorterTest's DISABLED_Run2345Sorter stays disabled,
