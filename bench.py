@@ -180,6 +180,34 @@ def hybrid1_leg(device, N=256, logn=17, trials=3):
             "speedup_vs_published": PUBLISHED_HYBRID1_S * 1e3 / med}
 
 
+def kway_leg(device, k=2, M=10, logn=17):
+    """BASELINE config 4: the k-way network KWayAdapter<1024>::sort (k = 2,
+    M = 10: 55 stages) at ring 2^17, HEStd_128_classic, depth 40, scale 59,
+    bootstrapping {5,5} over 1024 sparse slots, CompositeSign(3, d_f = 2,
+    d_g = 5) as tests/k-way/KWaySort2Test.cpp:124-157 passes it.  One sort
+    (about 14 s); the reference publishes no k-way timing."""
+    import numpy as np
+    N = k ** M
+    batch, depth, budget, rots = sfhe.kway_params(N)
+    eng = sfhe.Engine("hip", mult_depth=depth, ring_dim=1 << logn, batch_size=batch, scaling_mod_size=59,
+                      secure=True, rotations=rots, seed=7 + N, device=device)
+    eng.set_quiet(True)
+    t0 = time.perf_counter()
+    eng.bootstrap_setup(budget, batch)
+    setup_s = time.perf_counter() - t0
+    x = np.random.default_rng(N).permutation(N) / N
+    ct = eng.encrypt(x.tolist())
+    eng.sync()
+    t0 = time.perf_counter()
+    out = eng.kway_sort(ct, k, M, 3, 2, 5, depth)  # (3, d_f, d_g) as the test passes it
+    eng.sync()
+    ms = (time.perf_counter() - t0) * 1e3
+    err = float(np.max(np.abs(np.array(eng.decrypt(out))[:N] - np.sort(x))))
+    return {"workload": f"k-way sort N={N} (k={k}, M={M}) @ ring 2^{logn}, depth {depth}, bootstrapping {budget}",
+            "ms": ms, "bootstrap_keygen_s": setup_s, "level": out.level, "max_err": err,
+            "stages": M + M * (M - 1) // 2 * ((k + 1) // 2)}
+
+
 def pmc_traffic(family: str):
     """HBM bytes per launch for `family` from the committed PMC summary
     (tools/pmc_traffic.py output), if it was taken on the current kernels."""
@@ -207,6 +235,8 @@ def main(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--trials", type=int, default=10,
                     help="per-sort trials after the timed region (median/min/max, pure and as-test)")
+    ap.add_argument("--no-kway", dest="kway", action="store_false",
+                    help="skip the k-way leg (BASELINE config 4: N=1024 @ 2^17, one ~14 s sort)")
     ap.add_argument("--no-hybrid1", dest="hybrid1", action="store_false",
                     help="skip the sort_hybrid1 leg (N=256 @ 2^17, the published-timing path)")
     ap.add_argument("--shard", choices=("rccl", "host"), default=None,
@@ -381,8 +411,13 @@ def main(argv=None):
     if rank == 0 and world == 1 and args.hybrid1:
         try:
             result["hybrid1"] = hybrid1_leg(device)
-        except Exception as e:
+        except Exception as e:  # noqa: BLE001 -- an extra leg must not lose the metric line
             result["hybrid1"] = {"error": str(e)}
+    if rank == 0 and world == 1 and args.kway:
+        try:
+            result["kway"] = kway_leg(device)
+        except Exception as e:  # noqa: BLE001
+            result["kway"] = {"error": str(e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             result["cpu_baseline"] = cpu_baseline(N, logn, secure, depth, rots, cfg)

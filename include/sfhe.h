@@ -200,6 +200,25 @@ int sfhe_sorter_sort_hybrid1(sfhe_sorter* s, sfhe_ct* in, int n, int dg, int df,
 /* Depth and rotation keys of tests/DirectSortH1Test.cpp:36-117 for N
  * (the reference keeps them in the test; ring 2^17, HEStd_128_classic). */
 int sfhe_hybrid1_params(uint32_t N, uint32_t* mult_depth, int32_t* rotations, size_t cap, size_t* count);
+/* BitonicSort<N>::sort (sort_algo.h:1421-1486): the compare-and-swap network
+ * over the sorter's N slots with EvalBootstrap(ct, 2, 20) whenever the level
+ * passes 29 -- needs sfhe_bootstrap_setup for N slots and the +-2^i keys the
+ * sorter was created with; input values in [0, 255]. */
+int sfhe_sorter_sort_bitonic(sfhe_sorter* s, sfhe_ct* in, int n, int dg, int df, sfhe_ct** out);
+
+/* k-way sorting network: KWayAdapter<N>::sort = kwaySort::Sorter::sorter
+ * (src/kway_adapter.h:66-72, src/k-way/Sorter.cpp:284-404) over k^M = the
+ * ciphertext's first slots, k in {2, 3, 5}; comparisons CompositeSign(n, dg,
+ * df) with lazy bootstrapping against mult_depth (SignConfig(cfg, multDepth),
+ * tests/k-way/KWaySort2Test.cpp:157 -- note that test passes (3, d_f, d_g));
+ * needs sfhe_bootstrap_setup for the ciphertext's slots. */
+int sfhe_kway_sort(sfhe_ctx* c, const sfhe_ct* in, int k, int M, int n, int dg, int df, uint32_t mult_depth,
+                   sfhe_ct** out);
+/* KWayAdapter<N>::getSizeParameters (kway_adapter.h:41-64): batch (next power
+ * of two >= N), depth 40, first modulus 60 / scale 59 bits, level budget
+ * {4,4} (N <= 128) or {5,5}, the +-2^i rotation keys below N. */
+int sfhe_kway_params(uint32_t N, uint32_t* batch, uint32_t* mult_depth, uint32_t* budget_c2s, uint32_t* budget_s2c,
+                     int32_t* rotations, size_t cap, size_t* count);
 
 /* Decomposer<N>::decompose (rotation.h:54-102); algo 0 NAF, 1 BNAF, 2 BINARY.
  * N in {4..1024}; writes (value, stepSize) pairs. */

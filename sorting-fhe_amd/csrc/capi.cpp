@@ -14,6 +14,7 @@
 #include "algo/rotation.h"
 #include "algo/sign.h"
 #include "algo/sort_algo.h"
+#include "algo/kway_adapter.h"
 #include "core/openfhe.h"
 #include "core/state.h"
 
@@ -97,6 +98,7 @@ struct SorterBase {
     virtual Ct rank(const Ct& in, SignConfig& cfg) = 0;
     virtual Ct place(const Ct& rank, const Ct& in) = 0;
     virtual Ct hybrid1(const Ct& in, SignConfig& cfg, const PrivateKey<DCRTPoly>& sk) = 0;
+    virtual Ct bitonic(const Ct& in, SignConfig& cfg) = 0;
     virtual size_t graphNodes() const = 0;
     virtual bool graphNttTime(int reps, double* ms, uint64_t* launches, double* bytes) = 0;
 };
@@ -104,9 +106,18 @@ struct SorterBase {
 template <int N>
 struct Sorter : SorterBase {
     DirectSort<N> ds;
+    std::unique_ptr<BitonicSort<N>> bs;  // built on first use (its mask memo lives across sorts)
+    CryptoContext<DCRTPoly> cc_;
+    PublicKey<DCRTPoly> pk_;
+    std::vector<int> rot_;
+    std::shared_ptr<Encryption> enc_;
     Sorter(CryptoContext<DCRTPoly> cc, PublicKey<DCRTPoly> pk, std::vector<int> rot,
            std::shared_ptr<Encryption> enc)
-        : ds(cc, pk, rot, enc) {}
+        : ds(cc, pk, rot, enc), cc_(cc), pk_(pk), rot_(rot), enc_(enc) {}
+    Ct bitonic(const Ct& in, SignConfig& cfg) override {
+        if (!bs) bs = std::make_unique<BitonicSort<N>>(cc_, pk_, rot_, enc_);
+        return bs->sort(in, SignFunc::CompositeSign, cfg);
+    }
     Ct sort(const Ct& in, SignConfig& cfg) override { return ds.sort(in, SignFunc::CompositeSign, cfg); }
     Ct rank(const Ct& in, SignConfig& cfg) override {
         return ds.constructRank(in, SignFunc::CompositeSign, cfg);
@@ -451,6 +462,57 @@ int sfhe_sorter_sort_hybrid1(sfhe_sorter* s, sfhe_ct* in, int n, int dg, int df,
         auto cfg = cfgOf(n, dg, df);
         *out = wrap(s->impl->hybrid1(in->ct, cfg, s->ctx->keys.secretKey));
     });
+}
+
+int sfhe_sorter_sort_bitonic(sfhe_sorter* s, sfhe_ct* in, int n, int dg, int df, sfhe_ct** out) {
+    REQUIRE(s && in && out, "null argument");
+    REQUIRE(n == 3 || n == 4, "composite sign degree n must be 3 or 4");
+    return guard([&] {
+        Quiet q(s->ctx->quiet);
+        auto cfg = cfgOf(n, dg, df);
+        *out = wrap(s->impl->bitonic(in->ct, cfg));
+    });
+}
+
+int sfhe_kway_sort(sfhe_ctx* c, const sfhe_ct* in, int k, int M, int n, int dg, int df, uint32_t mult_depth,
+                   sfhe_ct** out) {
+    REQUIRE(c && in && out, "null argument");
+    REQUIRE(k == 2 || k == 3 || k == 5, "k must be 2, 3 or 5");
+    REQUIRE(M >= 1 && M <= 16, "M out of range");
+    REQUIRE(n == 3 || n == 4, "composite sign degree n must be 3 or 4");
+    long len = 1;
+    for (int i = 0; i < M; ++i) len *= k;
+    REQUIRE(len <= (long)in->ct->GetSlots(), "k^M exceeds the ciphertext's slots");
+    return guard([&] {
+        Quiet q(c->quiet);
+        // (the sorter keeps the keys only for its debug decryptions)
+        kwaySort::Sorter sorter(c->cc, nullptr, (long)in->ct->GetSlots(), k, M, c->keys.secretKey,
+                                c->keys.publicKey);
+        SignConfig cfg(CompositeSignConfig(n, dg, df), (int)mult_depth);
+        Ct x = in->ct->Clone(), y;
+        sorter.sorter(x, y, cfg);
+        if (!y) throw OpenFHEException("k-way sorter: no stage schedule for this k");
+        *out = wrap(y);
+    });
+}
+
+int sfhe_kway_params(uint32_t N, uint32_t* batch, uint32_t* mult_depth, uint32_t* budget_c2s, uint32_t* budget_s2c,
+                     int32_t* rotations, size_t cap, size_t* count) {
+    REQUIRE(N >= 2 && N <= (1u << 16), "N out of range");
+    uint32_t b = 1;
+    while (b < N) b <<= 1;
+    if (batch) *batch = b;
+    if (mult_depth) *mult_depth = 40;
+    if (budget_c2s) *budget_c2s = N <= 128 ? 4 : 5;
+    if (budget_s2c) *budget_s2c = N <= 128 ? 4 : 5;
+    std::vector<int32_t> r;
+    for (uint32_t i = 1; i < N; i *= 2) {
+        r.push_back((int32_t)i);
+        r.push_back(-(int32_t)i);
+    }
+    if (count) *count = r.size();
+    for (size_t i = 0; i < r.size() && i < cap && rotations; ++i) rotations[i] = r[i];
+    return SFHE_OK;
 }
 
 int sfhe_hybrid1_params(uint32_t N, uint32_t* mult_depth, int32_t* rotations, size_t cap, size_t* count) {

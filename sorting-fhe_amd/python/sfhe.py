@@ -38,6 +38,7 @@ ABI_SYMBOLS = [
     "sfhe_serialize_lanes", "sfhe_sorter_graph_nodes", "sfhe_sorter_create_rot",
     "sfhe_sorter_sort_hybrid1", "sfhe_hybrid1_params", "sfhe_sorter_graph_ntt_time",
     "sfhe_bootstrap_setup", "sfhe_bootstrap_depth", "sfhe_bootstrap",
+    "sfhe_sorter_sort_bitonic", "sfhe_kway_sort", "sfhe_kway_params",
 ]
 
 
@@ -120,6 +121,9 @@ _SIGS = {
     "sfhe_sorter_create_rot": (C.c_int, [_VP, _U32, C.c_int, _PI32, _SZ, _PVP]),
     "sfhe_sorter_sort_hybrid1": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_int, _PVP]),
     "sfhe_hybrid1_params": (C.c_int, [_U32, _PU32, _PI32, _SZ, _PSZ]),
+    "sfhe_sorter_sort_bitonic": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_int, _PVP]),
+    "sfhe_kway_sort": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _U32, _PVP]),
+    "sfhe_kway_params": (C.c_int, [_U32, _PU32, _PU32, _PU32, _PU32, _PI32, _SZ, _PSZ]),
     "sfhe_sorter_graph_ntt_time": (C.c_int, [_VP, C.c_int, _PD, _PU64, _PD]),
     "sfhe_kernel_timing": (C.c_int, [_VP, _U32, _U32]),
     "sfhe_serialize_lanes": (C.c_int, [_VP, C.c_int]),
@@ -340,6 +344,11 @@ class Engine:
     def bootstrap(self, a, iterations: int = 1, precision: int = 0):
         return self._new(self.lib.sfhe_bootstrap, self.ctx, a.h, iterations, precision)
 
+    def kway_sort(self, a, k: int, M: int, n: int = 3, dg: int = 2, df: int = 2, mult_depth: int = 40):
+        """KWayAdapter<k^M>::sort (reference kway_adapter.h:66-72): the k-way
+        network with CompositeSign(n, dg, df) and lazy bootstrapping."""
+        return self._new(self.lib.sfhe_kway_sort, self.ctx, a.h, k, M, n, dg, df, mult_depth)
+
     def chebyshev(self, x, coeffs: Sequence[float], a: float = -1.0, b: float = 1.0):
         return self._new(self.lib.sfhe_eval_chebyshev, self.ctx, x.h, _darr(coeffs), len(coeffs),
                          float(a), float(b))
@@ -429,6 +438,10 @@ class Sorter:
         """DirectSort<N>::sort_hybrid1 (reference sort_algo.h:1213-1229)."""
         return self.eng._new(self.eng.lib.sfhe_sorter_sort_hybrid1, self.h, ct.h, n, dg, df)
 
+    def sort_bitonic(self, ct: Ct, n: int = 4, dg: int = 3, df: int = 3) -> Ct:
+        """BitonicSort<N>::sort (reference sort_algo.h:1421-1486); values in [0, 255]."""
+        return self.eng._new(self.eng.lib.sfhe_sorter_sort_bitonic, self.h, ct.h, n, dg, df)
+
     def graph_ntt_time(self, reps: int = 5):
         """(ms per sort, launches, algorithmic bytes) of the captured sort's
         NTT kernels replayed alone (sfhe_sorter_graph_ntt_time)."""
@@ -452,6 +465,18 @@ def direct_sort_params(N: int, backend: str = "hip"):
     buf = (C.c_int32 * cnt.value)()
     lib.sfhe_direct_sort_params(N, None, buf, cnt.value, None)
     return depth.value, list(buf)
+
+
+def kway_params(N: int, backend: str = "hip"):
+    """KWayAdapter<N>::getSizeParameters: (batch, depth, level budget, rotations)."""
+    lib = load(backend)
+    b, d, b0, b1, cnt = C.c_uint32(), C.c_uint32(), C.c_uint32(), C.c_uint32(), C.c_size_t()
+    rc = lib.sfhe_kway_params(N, C.byref(b), C.byref(d), C.byref(b0), C.byref(b1), None, 0, C.byref(cnt))
+    if rc != SFHE_OK:
+        raise SfheError(f"sfhe error {rc}: {lib.sfhe_last_error().decode()}")
+    buf = (C.c_int32 * cnt.value)()
+    lib.sfhe_kway_params(N, None, None, None, None, buf, cnt.value, None)
+    return b.value, d.value, (b0.value, b1.value), list(buf)
 
 
 def hybrid1_params(N: int, backend: str = "hip"):

@@ -1,0 +1,80 @@
+"""k-way sorting network and BitonicSort through the C ABI (SURVEY.md §8(f)
+rows 2-3; reference src/kway_adapter.h, src/k-way/*, src/sort_algo.h:1393-1487).
+
+The reference's own k-way tests (tests/k-way/*, tests/KWaySortTest.cpp) and
+BitonicSortTest run unchanged in tests/test_reference_sources.py (CPU oracle)
+and tests/test_gpu_reference_sources.py (MI355X); here the ABI entries are
+checked on small rings against std::sort, and the HIP path bit for bit
+against the oracle.
+"""
+import numpy as np
+import pytest
+
+import sfhe
+
+
+def test_kway_params(oracle_lib):
+    """KWayAdapter<N>::getSizeParameters (kway_adapter.h:41-64)."""
+    b, d, budget, rots = sfhe.kway_params(1024, "oracle")
+    assert (b, d, budget) == (1024, 40, (5, 5))
+    assert sorted(rots) == sorted([s * (1 << i) for i in range(10) for s in (1, -1)])
+    b, d, budget, rots = sfhe.kway_params(729, "oracle")
+    assert (b, budget) == (1024, (5, 5))
+    b, d, budget, _ = sfhe.kway_params(27, "oracle")
+    assert (b, budget) == (32, (4, 4))
+
+
+def run_kway(backend, k, M, logn=12):
+    N = k ** M
+    batch, depth, budget, rots = sfhe.kway_params(N, backend)
+    e = sfhe.Engine(backend, mult_depth=depth, ring_dim=1 << logn, batch_size=batch, scaling_mod_size=59,
+                    rotations=rots, seed=11, device=0)
+    e.set_quiet(True)
+    e.bootstrap_setup(budget, batch)
+    x = np.random.default_rng(k * 100 + M).permutation(N) / N
+    out = e.kway_sort(e.encrypt(x.tolist()), k, M, 3, 2, 2, depth)
+    return e, x, out
+
+
+@pytest.mark.parametrize("k,M", [(2, 3), (3, 2)])
+def test_kway_sort_oracle(oracle_lib, k, M):
+    e, x, out = run_kway("oracle", k, M)
+    got = np.array(e.decrypt(out))[: len(x)]
+    err = np.max(np.abs(got - np.sort(x)))
+    print(f"k={k} M={M}: max err {err:.3g}")
+    assert err < 0.01
+
+
+def test_kway_sort_errors(oracle_lib):
+    e = sfhe.Engine("oracle", mult_depth=10, ring_dim=1 << 12, batch_size=8, seed=3)
+    e.set_quiet(True)
+    ct = e.encrypt([0.1] * 8)
+    with pytest.raises(sfhe.SfheError, match="k must be"):
+        e.kway_sort(ct, 4, 2)
+    with pytest.raises(sfhe.SfheError, match="exceeds"):
+        e.kway_sort(ct, 2, 4)
+
+
+def test_bitonic_sort_oracle(oracle_lib):
+    """BitonicSortTest's configuration (ring 2^12, depth 58, scale 59, {3,3})
+    through sfhe_sorter_sort_bitonic."""
+    N = 4
+    rots = [r for i in range(2) for r in (1 << i, -(1 << i))]
+    e = sfhe.Engine("oracle", mult_depth=58, ring_dim=1 << 12, batch_size=N, scaling_mod_size=59,
+                    rotations=rots, seed=4)
+    e.set_quiet(True)
+    e.bootstrap_setup((3, 3), N)
+    x = np.array([123.73, 115.91, 245.11, 250.48])
+    out = e.sorter(N, rotations=rots).sort_bitonic(e.encrypt(x.tolist()))
+    got = np.array(e.decrypt(out))[:N]
+    assert np.max(np.abs(got - np.sort(x))) < 1e-3
+
+
+@pytest.mark.gpu
+def test_kway_bitexact_hip_vs_oracle(hip_lib, oracle_lib):
+    raw = {}
+    for backend in ("hip", "oracle"):
+        e, x, out = run_kway(backend, 2, 2)
+        assert np.max(np.abs(np.array(e.decrypt(out))[:4] - np.sort(x))) < 0.01
+        raw[backend] = out.download()
+    assert np.array_equal(raw["hip"], raw["oracle"])
