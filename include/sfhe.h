@@ -206,6 +206,16 @@ int sfhe_hybrid1_params(uint32_t N, uint32_t* mult_depth, int32_t* rotations, si
  * sorter was created with; input values in [0, 255]. */
 int sfhe_sorter_sort_bitonic(sfhe_sorter* s, sfhe_ct* in, int n, int dg, int df, sfhe_ct** out);
 
+/* Serialized I/O (src/sort.h:31-102, src/main.cpp:9-44: the FHERMA-style file
+ * set).  sfhe_save writes <dir>/cc.bin, pub.bin, mult.bin, rot.bin and, if the
+ * context holds it, sk.bin; sfhe_load reads them back into a new context
+ * (sk.bin optional).  Records are this engine's (magic, version, kind, context
+ * fingerprint), not OpenFHE's cereal layout. */
+int sfhe_save(sfhe_ctx* c, const char* dir);
+int sfhe_load(const char* dir, sfhe_ctx** out);
+int sfhe_ct_save(sfhe_ctx* c, const sfhe_ct* ct, const char* path);
+int sfhe_ct_load(sfhe_ctx* c, const char* path, sfhe_ct** out);
+
 /* k-way sorting network: KWayAdapter<N>::sort = kwaySort::Sorter::sorter
  * (src/kway_adapter.h:66-72, src/k-way/Sorter.cpp:284-404) over k^M = the
  * ciphertext's first slots, k in {2, 3, 5}; comparisons CompositeSign(n, dg,

@@ -1,5 +1,6 @@
 // extern "C" boundary (include/sfhe.h) over the lbcrypto-compatible engine.
 #include <cstring>
+#include <fstream>
 #include <iostream>
 #include <memory>
 #include <mutex>
@@ -471,6 +472,69 @@ int sfhe_sorter_sort_bitonic(sfhe_sorter* s, sfhe_ct* in, int n, int dg, int df,
         Quiet q(s->ctx->quiet);
         auto cfg = cfgOf(n, dg, df);
         *out = wrap(s->impl->bitonic(in->ct, cfg));
+    });
+}
+
+int sfhe_save(sfhe_ctx* c, const char* dir) {
+    REQUIRE(c && dir, "null argument");
+    return guard([&] {
+        const std::string d(dir);
+        auto put = [&](const std::string& name, auto&& write) {
+            std::ofstream f(d + "/" + name, std::ios::binary | std::ios::trunc);
+            if (!f.is_open() || !write(f) || !f.good()) throw std::invalid_argument("cannot write " + d + "/" + name);
+        };
+        put("cc.bin", [&](std::ostream& f) { return Serial::Serialize(c->cc, f, SerType::BINARY); });
+        put("pub.bin", [&](std::ostream& f) { return Serial::Serialize(c->keys.publicKey, f, SerType::BINARY); });
+        if (c->keys.secretKey)
+            put("sk.bin", [&](std::ostream& f) { return Serial::Serialize(c->keys.secretKey, f, SerType::BINARY); });
+        put("mult.bin", [&](std::ostream& f) {
+            return CryptoContextImpl<DCRTPoly>::SerializeEvalMultKey(f, SerType::BINARY);
+        });
+        put("rot.bin", [&](std::ostream& f) {
+            return CryptoContextImpl<DCRTPoly>::SerializeEvalAutomorphismKey(f, SerType::BINARY);
+        });
+    });
+}
+
+int sfhe_load(const char* dir, sfhe_ctx** out) {
+    REQUIRE(dir && out, "null argument");
+    return guard([&] {
+        const std::string d(dir);
+        auto get = [&](const std::string& name, bool required, auto&& read) {
+            std::ifstream f(d + "/" + name, std::ios::binary);
+            if (!f.is_open()) {
+                if (required) throw std::invalid_argument("cannot open " + d + "/" + name);
+                return;
+            }
+            if (!read(f)) throw std::invalid_argument("cannot deserialize " + d + "/" + name);
+        };
+        auto ctx = std::make_unique<sfhe_ctx>();
+        get("cc.bin", true, [&](std::istream& f) { return Serial::Deserialize(ctx->cc, f, SerType::BINARY); });
+        get("pub.bin", true, [&](std::istream& f) { return Serial::Deserialize(ctx->keys.publicKey, f, SerType::BINARY); });
+        get("sk.bin", false, [&](std::istream& f) { return Serial::Deserialize(ctx->keys.secretKey, f, SerType::BINARY); });
+        get("mult.bin", true, [&](std::istream& f) { return CryptoContextImpl<DCRTPoly>::DeserializeEvalMultKey(f, SerType::BINARY); });
+        get("rot.bin", true, [&](std::istream& f) {
+            return CryptoContextImpl<DCRTPoly>::DeserializeEvalAutomorphismKey(f, SerType::BINARY);
+        });
+        *out = ctx.release();
+    });
+}
+
+int sfhe_ct_save(sfhe_ctx* c, const sfhe_ct* ct, const char* path) {
+    REQUIRE(c && ct && path, "null argument");
+    return guard([&] {
+        if (!Serial::SerializeToFile(std::string(path), ct->ct, SerType::BINARY))
+            throw std::invalid_argument(std::string("cannot write ") + path);
+    });
+}
+
+int sfhe_ct_load(sfhe_ctx* c, const char* path, sfhe_ct** out) {
+    REQUIRE(c && path && out, "null argument");
+    return guard([&] {
+        Ct ct;
+        if (!Serial::DeserializeFromFile(std::string(path), ct, SerType::BINARY))
+            throw std::invalid_argument(std::string("cannot read ") + path);
+        *out = wrap(ct);
     });
 }
 

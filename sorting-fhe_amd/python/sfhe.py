@@ -39,6 +39,7 @@ ABI_SYMBOLS = [
     "sfhe_sorter_sort_hybrid1", "sfhe_hybrid1_params", "sfhe_sorter_graph_ntt_time",
     "sfhe_bootstrap_setup", "sfhe_bootstrap_depth", "sfhe_bootstrap",
     "sfhe_sorter_sort_bitonic", "sfhe_kway_sort", "sfhe_kway_params",
+    "sfhe_save", "sfhe_load", "sfhe_ct_save", "sfhe_ct_load",
 ]
 
 
@@ -122,6 +123,10 @@ _SIGS = {
     "sfhe_sorter_sort_hybrid1": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_int, _PVP]),
     "sfhe_hybrid1_params": (C.c_int, [_U32, _PU32, _PI32, _SZ, _PSZ]),
     "sfhe_sorter_sort_bitonic": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_int, _PVP]),
+    "sfhe_save": (C.c_int, [_VP, C.c_char_p]),
+    "sfhe_load": (C.c_int, [C.c_char_p, _PVP]),
+    "sfhe_ct_save": (C.c_int, [_VP, _VP, C.c_char_p]),
+    "sfhe_ct_load": (C.c_int, [_VP, C.c_char_p, _PVP]),
     "sfhe_kway_sort": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _U32, _PVP]),
     "sfhe_kway_params": (C.c_int, [_U32, _PU32, _PU32, _PU32, _PU32, _PI32, _SZ, _PSZ]),
     "sfhe_sorter_graph_ntt_time": (C.c_int, [_VP, C.c_int, _PD, _PU64, _PD]),
@@ -206,6 +211,26 @@ class Engine:
             self._chk(self.lib.sfhe_keygen(self.ctx))
             if rotations:
                 self.rotate_keygen(rotations)
+
+    @classmethod
+    def load(cls, directory: str, backend: str = "hip") -> "Engine":
+        """A context and keys from sfhe_save's file set (src/sort.h:31-102)."""
+        self = cls.__new__(cls)
+        self.lib = load(backend)
+        self.backend = backend
+        self._comm_refs = None
+        self.ctx = C.c_void_p()
+        self._chk(self.lib.sfhe_load(directory.encode(), C.byref(self.ctx)))
+        return self
+
+    def save(self, directory: str):
+        self._chk(self.lib.sfhe_save(self.ctx, directory.encode()))
+
+    def save_ct(self, ct: "Ct", path: str):
+        self._chk(self.lib.sfhe_ct_save(self.ctx, ct.h, path.encode()))
+
+    def load_ct(self, path: str) -> "Ct":
+        return self._new(self.lib.sfhe_ct_load, self.ctx, path.encode())
 
     # -- plumbing --
     def _chk(self, rc: int):

@@ -67,3 +67,24 @@ def test_fherma_flow_config_json(tmp_path, hip_lib):
     tolerance scaled to that trend (0.05), the level the exact one."""
     out = flow(tmp_path, "hip", 17, 44, tol=0.05)
     assert "level 42" in out
+
+
+def test_c_abi_save_load_roundtrip(tmp_path, oracle_lib):
+    """sfhe_save / sfhe_load / sfhe_ct_save / sfhe_ct_load: a context, its keys
+    and a ciphertext survive the file round trip; the loaded context
+    evaluates with the loaded keys (mult + rotation) and decrypts."""
+    import numpy as np
+    import sfhe
+    e = sfhe.Engine("oracle", mult_depth=4, ring_dim=1 << 12, batch_size=8, rotations=[1], seed=9)
+    e.set_quiet(True)
+    x = np.array([0.5, -0.25, 0.125, 0.75, 0.1, 0.2, 0.3, 0.4])
+    e.save(str(tmp_path))
+    e.save_ct(e.encrypt(x.tolist()), str(tmp_path / "ct.bin"))
+    del e
+    f = sfhe.Engine.load(str(tmp_path), "oracle")
+    f.set_quiet(True)
+    ct = f.load_ct(str(tmp_path / "ct.bin"))
+    got = np.array(f.decrypt(f.rotate(f.mult(ct, ct), 1)))[:8]
+    assert np.allclose(got, np.roll(x * x, -1), atol=1e-4)
+    with pytest.raises(sfhe.SfheError, match="cannot open"):
+        sfhe.Engine.load(str(tmp_path / "missing"), "oracle")
