@@ -209,8 +209,9 @@ def kway_leg(device, k=2, M=10, logn=17):
 
 
 def pmc_traffic(family: str):
-    """HBM bytes per launch for `family` from the committed PMC summary
-    (tools/pmc_traffic.py output), if it was taken on the current kernels."""
+    """HBM traffic / algorithmic bytes for `family` from the committed PMC
+    summary (tools/pmc_traffic.py over tools/profile_round.sh's two PMC passes
+    on the kernel microbenchmark), if it was taken on the current kernels."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
@@ -223,7 +224,7 @@ def pmc_traffic(family: str):
         sha = hashlib.sha256(f.read()).hexdigest()[:16]
     if j.get("kernel_source_sha") != sha:
         return None
-    return j.get("families", {}).get(family, {}).get("hbm_bytes_per_launch")
+    return j.get("families", {}).get(family, {}).get("traffic_over_algorithmic")
 
 
 def main(argv=None):
@@ -364,6 +365,7 @@ def main(argv=None):
         timing = ("HIP events around every launch of the family on the stream it runs on, during one "
                   f"profiling sort after the timed region with the lanes serialised ({serial_ms:.1f} ms)")
     achieved = r_bytes / (r_ms / 1e3) / 1e9 if r_ms else 0.0
+    ratio = pmc_traffic(dom)
     roofline = {
         "bound": "hbm",
         "kernel": kernel_name[dom],
@@ -371,7 +373,10 @@ def main(argv=None):
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
         "frac": achieved / HBM_PEAK_GBS,
-        "traffic": pmc_traffic(dom),
+        # HBM bytes per launch: the PMC ratio (FETCH_SIZE x2 + WRITE_SIZE, KiB -> B, over the
+        # same kernels on tools/microbench at 1..96 limbs) x this sort's algorithmic bytes per launch
+        "traffic": ratio * r_bytes / r_launch if (ratio and r_launch) else None,
+        "traffic_over_algorithmic": ratio,
         "avg_launch_us": r_ms / r_launch * 1e3 if r_launch else None,
         "algorithmic_bytes_per_launch": r_bytes / r_launch if r_launch else None,
         "launches_per_sort": r_launch,

@@ -346,6 +346,10 @@ __device__ __forceinline__ uint32_t nttLocal(const NttTile& T, uint32_t st, uint
 //       bytes); staging them cost more occupancy than it saved, so the ROW
 //       rounds read the table directly (index 2^S + (x0 >> (8 - k))).
 constexpr uint32_t kNttColTw = 512;  // 2^logR - 1 entries, logR <= 9
+#ifndef SFHE_NTT_ROW_LDS
+#define SFHE_NTT_ROW_LDS 0  // measured slower (+4 ms/sort at SFHE_NTT_FP=2): the rounds are not twiddle-latency bound
+#endif
+constexpr bool kNttRowLdsBuild = SFHE_NTT_ROW_LDS != 0;
 template <bool COL>
 __device__ __forceinline__ uint32_t twIndex(const NttTile& T, uint32_t S0, uint32_t k, uint32_t x0) {
     if (COL) return (1u << k) - 1 + (x0 >> (T.logn - k));
@@ -356,13 +360,14 @@ __device__ __forceinline__ uint32_t twIndex(const NttTile& T, uint32_t S0, uint3
 // staged in LDS with the tile (one load latency instead of one per round):
 // stage k's run at LDS offset 8 (2^k - 1).
 constexpr uint32_t kNttRowTw = (kNttTile / 256) * 255;
+template <int TILE>
 __device__ __forceinline__ uint32_t twIndexRowLds(const NttTile& T, uint32_t k, uint32_t x0) {
-    return kNttRows * ((1u << k) - 1) + (x0 >> (8 - k)) - (T.r0 << k);
+    return (TILE / 256) * ((1u << k) - 1) + (x0 >> (8 - k)) - (T.r0 << k);
 }
 
 // One round: stages k0..k0+B-1 of the pass (k relative to the pass's first
 // global stage S0).  8/2^B groups of 2^B words per thread.
-template <bool INV, bool COL, int LE, int B>
+template <bool INV, bool COL, int LE, int B, int TILE>
 __device__ __forceinline__ void nttRound(u64* s, const NttTile& T, uint32_t S0, uint32_t k0, u64 q,
                                          const u64* w, const u64* wS) {
     constexpr int M = 1 << B;
@@ -374,7 +379,7 @@ __device__ __forceinline__ void nttRound(u64* s, const NttTile& T, uint32_t S0, 
     const u64 q2 = 2 * q;
 #pragma unroll
     for (int gi = 0; gi < GPT; ++gi) {
-        const uint32_t gid = threadIdx.x + gi * (kNttTile >> LE);
+        const uint32_t gid = threadIdx.x + gi * (TILE >> LE);
         uint32_t st, lo, hi;
         if (COL) {  // every extent is a power of two: shifts and masks only
             st = gid & (T.C - 1);
@@ -441,17 +446,17 @@ __device__ __forceinline__ void nttRound(u64* s, const NttTile& T, uint32_t S0, 
     }
 }
 
-template <bool INV, bool COL, int LE>
+template <bool INV, bool COL, int LE, int TILE>
 __device__ __forceinline__ void nttRoundDyn(int b, u64* s, const NttTile& T, uint32_t S0, uint32_t k0,
                                             u64 q, const u64* w, const u64* wS) {
     if constexpr (LE >= 4) {
-        if (b == 4) return nttRound<INV, COL, LE, 4>(s, T, S0, k0, q, w, wS);
+        if (b == 4) return nttRound<INV, COL, LE, 4, TILE>(s, T, S0, k0, q, w, wS);
     }
     if constexpr (LE >= 3) {
-        if (b == 3) return nttRound<INV, COL, LE, 3>(s, T, S0, k0, q, w, wS);
+        if (b == 3) return nttRound<INV, COL, LE, 3, TILE>(s, T, S0, k0, q, w, wS);
     }
-    if (b == 2) return nttRound<INV, COL, LE, 2>(s, T, S0, k0, q, w, wS);
-    nttRound<INV, COL, LE, 1>(s, T, S0, k0, q, w, wS);
+    if (b == 2) return nttRound<INV, COL, LE, 2, TILE>(s, T, S0, k0, q, w, wS);
+    nttRound<INV, COL, LE, 1, TILE>(s, T, S0, k0, q, w, wS);
 }
 
 // ---- FP64 butterflies (primes q < 2^42) ------------------------------------
@@ -477,7 +482,7 @@ __device__ __forceinline__ double fpReduce(double v, double q, double qinv) {
     return r < 0.0 ? r + q : r;
 }
 
-template <bool INV, bool COL, int LE, int B>
+template <bool INV, bool COL, int LE, int B, int TILE>
 __device__ __forceinline__ void nttRoundFP(double* s, const NttTile& T, uint32_t S0, uint32_t k0, double q,
                                            const double* w, const double* wq, double qinv, bool rowLds) {
     constexpr int M = 1 << B;
@@ -488,7 +493,7 @@ __device__ __forceinline__ void nttRoundFP(double* s, const NttTile& T, uint32_t
     const uint32_t span = D >> k0;
 #pragma unroll
     for (int gi = 0; gi < GPT; ++gi) {
-        const uint32_t gid = threadIdx.x + gi * (kNttTile >> LE);
+        const uint32_t gid = threadIdx.x + gi * (TILE >> LE);
         uint32_t st, lo, hi;
         if (COL) {
             st = gid & (T.C - 1);
@@ -506,7 +511,7 @@ __device__ __forceinline__ void nttRoundFP(double* s, const NttTile& T, uint32_t
         double W[M - 1], WQ[M - 1];
 #pragma unroll
         for (int t = 0; t < B; ++t) {
-            const uint32_t tb = (!COL && rowLds) ? twIndexRowLds(T, k0 + t, x0) : twIndex<COL>(T, S0, k0 + t, x0);
+            const uint32_t tb = (!COL && rowLds) ? twIndexRowLds<TILE>(T, k0 + t, x0) : twIndex<COL>(T, S0, k0 + t, x0);
 #pragma unroll
             for (int qd = 0; qd < (1 << t); ++qd) {
                 W[(1 << t) - 1 + qd] = w[tb + qd];
@@ -552,18 +557,18 @@ __device__ __forceinline__ void nttRoundFP(double* s, const NttTile& T, uint32_t
     }
 }
 
-template <bool INV, bool COL, int LE>
+template <bool INV, bool COL, int LE, int TILE>
 __device__ __forceinline__ void nttRoundDynFP(int b, double* s, const NttTile& T, uint32_t S0, uint32_t k0,
                                               double q, const double* w, const double* wq, double qinv,
                                               bool rowLds) {
     if constexpr (LE >= 4) {
-        if (b == 4) return nttRoundFP<INV, COL, LE, 4>(s, T, S0, k0, q, w, wq, qinv, rowLds);
+        if (b == 4) return nttRoundFP<INV, COL, LE, 4, TILE>(s, T, S0, k0, q, w, wq, qinv, rowLds);
     }
     if constexpr (LE >= 3) {
-        if (b == 3) return nttRoundFP<INV, COL, LE, 3>(s, T, S0, k0, q, w, wq, qinv, rowLds);
+        if (b == 3) return nttRoundFP<INV, COL, LE, 3, TILE>(s, T, S0, k0, q, w, wq, qinv, rowLds);
     }
-    if (b == 2) return nttRoundFP<INV, COL, LE, 2>(s, T, S0, k0, q, w, wq, qinv, rowLds);
-    nttRoundFP<INV, COL, LE, 1>(s, T, S0, k0, q, w, wq, qinv, rowLds);
+    if (b == 2) return nttRoundFP<INV, COL, LE, 2, TILE>(s, T, S0, k0, q, w, wq, qinv, rowLds);
+    nttRoundFP<INV, COL, LE, 1, TILE>(s, T, S0, k0, q, w, wq, qinv, rowLds);
 }
 
 
@@ -616,8 +621,8 @@ __device__ unsigned long long g_nttTrace[kTraceSlots][4][8];
 #define NTT_MARK(i)
 #endif
 
-template <bool INV, bool COL, int LE>
-__global__ __launch_bounds__(kNttTile >> LE) void k_ntt(const RowGroup G, const sf_barrett* __restrict__ bar,
+template <bool INV, bool COL, int LE, int TILE>
+__global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_barrett* __restrict__ bar,
                                                   const u64* __restrict__ tw, const u64* __restrict__ twS,
                                                   const u64* __restrict__ ninv,
                                                   const u64* __restrict__ ninvS, uint32_t logn,
@@ -626,8 +631,12 @@ __global__ __launch_bounds__(kNttTile >> LE) void k_ntt(const RowGroup G, const 
                                                   const double* __restrict__ qinvD,
                                                   const double* __restrict__ ninvD,
                                                   const double* __restrict__ ninvQ, int useFp) {
-    __shared__ u64 s[kNttTile];
+    __shared__ u64 s[TILE];
     __shared__ u64 tW[COL ? kNttColTw : 1], tX[COL ? kNttColTw : 1];  // COL twiddles (value, Shoup or W/q)
+    // ROW pass, FP64 rows, when SFHE_NTT_ROW_LDS: the tile's twiddle runs
+    // (stage k: 2^k entries per row) staged with the tile, one load latency
+    // instead of one per register round
+    __shared__ u64 tR[(COL || !kNttRowLdsBuild) ? 1 : (TILE / 256) * 255];
 #ifdef SFHE_NTT_TRACE
     unsigned long long tprev = clock64();
 #endif
@@ -643,7 +652,7 @@ __global__ __launch_bounds__(kNttTile >> LE) void k_ntt(const RowGroup G, const 
     NttTile T;
     T.logn = logn;
     T.d = COL ? logR : 8u;
-    T.logC = COL ? (uint32_t)__builtin_ctz(kNttTile) - logR : 0u;
+    T.logC = COL ? (uint32_t)__builtin_ctz(TILE) - logR : 0u;
     T.C = 1u << T.logC;
     // XCD-aware tile order: workgroups go to the 8 XCDs round-robin by id, so
     // block x runs on XCD x % 8.  Give each XCD a contiguous run of tiles:
@@ -651,19 +660,28 @@ __global__ __launch_bounds__(kNttTile >> LE) void k_ntt(const RowGroup G, const 
     // (and ROW tiles share twiddle lines), which then meet in one L2.
     const uint32_t tile = (gridDim.x & 7) ? blockIdx.x : (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
     T.c0 = COL ? tile * T.C : 0u;
-    T.r0 = COL ? 0u : tile * kNttRows;
+    T.r0 = COL ? 0u : tile * (TILE / 256);
     const uint32_t S0 = COL ? 0u : logR;
 
     // the pass's twiddle table (value, Shoup companion or W/q) for this prime
     const u64* gw = fp ? reinterpret_cast<const u64*>(twD) + (size_t)prime * n : tw + (size_t)prime * n;
     const u64* gx = fp ? reinterpret_cast<const u64*>(twQ) + (size_t)prime * n : twS + (size_t)prime * n;
     if (COL) {  // entries [1, 2^logR) -> LDS
-        for (uint32_t e = threadIdx.x; e < (1u << logR) - 1; e += (kNttTile >> LE)) {
+        for (uint32_t e = threadIdx.x; e < (1u << logR) - 1; e += (TILE >> LE)) {
             tW[e] = gw[e + 1];
             tX[e] = gx[e + 1];
         }
     }
-    const u64* rw = COL ? tW : gw;
+    const bool rowLds = kNttRowLdsBuild && !COL && fp && useFp >= 2;
+    if (rowLds) {
+        constexpr uint32_t rowsT = TILE / 256;
+        for (uint32_t k = 0; k < 8; ++k) {
+            const uint32_t len = rowsT << k;
+            const u64* src = gw + (1u << (S0 + k)) + (T.r0 << k);
+            for (uint32_t j = threadIdx.x; j < len; j += (TILE >> LE)) tR[rowsT * ((1u << k) - 1) + j] = src[j];
+        }
+    }
+    const u64* rw = COL ? tW : (rowLds ? tR : gw);
     const u64* rx = COL ? tX : gx;
 
     const u64* in = FIRST ? rowAt(G.src, pp, ii) : rowAt(G.dst, pp, ii);
@@ -683,7 +701,7 @@ __global__ __launch_bounds__(kNttTile >> LE) void k_ntt(const RowGroup G, const 
     // global -> LDS, 16 B per lane; tile-linear word e is row-major (u, st)
 #pragma unroll
     for (int k = 0; k < (1 << LE) / 2; ++k) {
-        const uint32_t e = 2 * (threadIdx.x + k * (kNttTile >> LE));
+        const uint32_t e = 2 * (threadIdx.x + k * (TILE >> LE));
         const size_t g = COL ? (size_t)(e >> T.logC) * 256 + T.c0 + (e & (T.C - 1)) : (size_t)T.r0 * 256 + e;
         ulonglong2 x = *reinterpret_cast<const ulonglong2*>(in + g);
         if (FIRST) {
@@ -721,11 +739,11 @@ __global__ __launch_bounds__(kNttTile >> LE) void k_ntt(const RowGroup G, const 
         const uint32_t k0 = LE * r;
         const int b = (int)min((uint32_t)LE, T.d - k0);
         if (fp)
-            nttRoundDynFP<INV, COL, LE>(b, reinterpret_cast<double*>(s), T, S0, k0, (double)q,
+            nttRoundDynFP<INV, COL, LE, TILE>(b, reinterpret_cast<double*>(s), T, S0, k0, (double)q,
                                         reinterpret_cast<const double*>(rw), reinterpret_cast<const double*>(rx),
-                                        qinvD[prime], false);
+                                        qinvD[prime], rowLds);
         else
-            nttRoundDyn<INV, COL, LE>(b, s, T, S0, k0, q, rw, rx);
+            nttRoundDyn<INV, COL, LE, TILE>(b, s, T, S0, k0, q, rw, rx);
         __syncthreads();
         NTT_MARK(1 + ri);
     }
@@ -743,7 +761,7 @@ __global__ __launch_bounds__(kNttTile >> LE) void k_ntt(const RowGroup G, const 
     const sf_barrett EB = emul ? loadBar(bar, prime) : sf_barrett{};
 #pragma unroll
     for (int k = 0; k < (1 << LE) / 2; ++k) {
-        const uint32_t e = 2 * (threadIdx.x + k * (kNttTile >> LE));
+        const uint32_t e = 2 * (threadIdx.x + k * (TILE >> LE));
         const size_t g = COL ? (size_t)(e >> T.logC) * 256 + T.c0 + (e & (T.C - 1)) : (size_t)T.r0 * 256 + e;
         ulonglong2 x;
         x.x = s[ldsSw(e)];
@@ -2183,15 +2201,26 @@ static void nttRows(sfp_dev* d, const RowGroup& G, int inverse) {
         checkLaunch(d, "ntt");
         return;
     }
-    const dim3 g(d->n / kNttTile, rows);
     const u64* tw = inverse ? d->ipsi : d->psi;
     const u64* twS = inverse ? d->ipsiS : d->psiS;
     const double* twD = inverse ? d->ipsiD : d->psiD;
     const double* twQ = inverse ? d->ipsiQ : d->psiQ;
+    // Launches over few rows are latency-bound (a one-limb pass is one tile
+    // round trip per block: ~1.5 us load, ~1 us per register round, tools/
+    // microbench with SFHE_NTT_TRACE): up to SFHE_NTT_T1K_ROWS rows (default
+    // 64) they run 1024-word tiles -- twice the blocks, half the work each;
+    // needs >= 2 columns per COL tile, i.e. n <= 2^17.  Measured on the metric
+    // sort: NTT 47.9 -> 46.0 ms, wall 58.1 -> 57.5 ms.
+    static const uint32_t t1kRows = [] {
+        const char* v = std::getenv("SFHE_NTT_T1K_ROWS");
+        return v ? (uint32_t)std::atoi(v) : 64u;
+    }();
+    const bool t1k = rows <= t1kRows && d->n <= (1u << 17);
+    const dim3 g(d->n / (t1k ? 1024u : (uint32_t)kNttTile), rows);
     const bool small = rows < (uint32_t)kNttSmallRows;
-    auto pass = [&](auto kern, int le) {
+    auto pass = [&](auto kern, int threads) {
         timedLaunch(d, SFP_FAM_NTT, bytes, [&] {
-            hipLaunchKernelGGL(kern, g, dim3(kNttTile >> le), 0, d->st(), G, d->bar, tw, twS, d->ninv,
+            hipLaunchKernelGGL(kern, g, dim3(threads), 0, d->st(), G, d->bar, tw, twS, d->ninv,
                                d->ninvS, d->logn, twD, twQ, d->qinvD, d->ninvD, d->ninvQ, nttFp());
         });
     };
@@ -2200,27 +2229,36 @@ static void nttRows(sfp_dev* d, const RowGroup& G, int inverse) {
         return v ? std::atoi(v) : 0;
     }();
     const int L = le ? le : (small ? 2 : 3);
-    if (!inverse) {
-        if (L == 4) {
-            pass(k_ntt<false, true, 4>, 4);
-            pass(k_ntt<false, false, 4>, 4);
-        } else if (L == 2) {
-            pass(k_ntt<false, true, 2>, 2);
-            pass(k_ntt<false, false, 2>, 2);
+    constexpr int T = kNttTile;
+    if (t1k) {
+        if (!inverse) {
+            pass(k_ntt<false, true, 2, 1024>, 1024 >> 2);
+            pass(k_ntt<false, false, 2, 1024>, 1024 >> 2);
         } else {
-            pass(k_ntt<false, true, 3>, 3);
-            pass(k_ntt<false, false, 3>, 3);
+            pass(k_ntt<true, false, 2, 1024>, 1024 >> 2);
+            pass(k_ntt<true, true, 2, 1024>, 1024 >> 2);
+        }
+    } else if (!inverse) {
+        if (L == 4) {
+            pass(k_ntt<false, true, 4, T>, T >> 4);
+            pass(k_ntt<false, false, 4, T>, T >> 4);
+        } else if (L == 2) {
+            pass(k_ntt<false, true, 2, T>, T >> 2);
+            pass(k_ntt<false, false, 2, T>, T >> 2);
+        } else {
+            pass(k_ntt<false, true, 3, T>, T >> 3);
+            pass(k_ntt<false, false, 3, T>, T >> 3);
         }
     } else {
         if (L == 4) {
-            pass(k_ntt<true, false, 4>, 4);
-            pass(k_ntt<true, true, 4>, 4);
+            pass(k_ntt<true, false, 4, T>, T >> 4);
+            pass(k_ntt<true, true, 4, T>, T >> 4);
         } else if (L == 2) {
-            pass(k_ntt<true, false, 2>, 2);
-            pass(k_ntt<true, true, 2>, 2);
+            pass(k_ntt<true, false, 2, T>, T >> 2);
+            pass(k_ntt<true, true, 2, T>, T >> 2);
         } else {
-            pass(k_ntt<true, false, 3>, 3);
-            pass(k_ntt<true, true, 3>, 3);
+            pass(k_ntt<true, false, 3, T>, T >> 3);
+            pass(k_ntt<true, true, 3, T>, T >> 3);
         }
     }
     checkLaunch(d, "ntt");
@@ -2327,12 +2365,15 @@ size_t sfp_graph_nodes(const sfp_graph* g) { return g ? g->nodes : 0; }
 int sfp_graph_family_time(sfp_dev* d, sfp_graph* g, uint32_t fam, int reps, double* ms, uint64_t* launches,
                           double* bytes) {
     if (!g || !g->g || fam != SFP_FAM_NTT || reps < 1 || d->capture) return -1;
-    const void* fns[] = {(const void*)k_ntt<false, true, 2>, (const void*)k_ntt<false, false, 2>,
-                         (const void*)k_ntt<true, true, 2>,  (const void*)k_ntt<true, false, 2>,
-                         (const void*)k_ntt<false, true, 3>, (const void*)k_ntt<false, false, 3>,
-                         (const void*)k_ntt<true, true, 3>,  (const void*)k_ntt<true, false, 3>,
-                         (const void*)k_ntt<false, true, 4>, (const void*)k_ntt<false, false, 4>,
-                         (const void*)k_ntt<true, true, 4>,  (const void*)k_ntt<true, false, 4>};
+    constexpr int T = kNttTile;
+    const void* fns[] = {(const void*)k_ntt<false, true, 2, T>, (const void*)k_ntt<false, false, 2, T>,
+                         (const void*)k_ntt<true, true, 2, T>,  (const void*)k_ntt<true, false, 2, T>,
+                         (const void*)k_ntt<false, true, 3, T>, (const void*)k_ntt<false, false, 3, T>,
+                         (const void*)k_ntt<true, true, 3, T>,  (const void*)k_ntt<true, false, 3, T>,
+                         (const void*)k_ntt<false, true, 4, T>, (const void*)k_ntt<false, false, 4, T>,
+                         (const void*)k_ntt<true, true, 4, T>,  (const void*)k_ntt<true, false, 4, T>,
+                         (const void*)k_ntt<false, true, 2, 1024>, (const void*)k_ntt<false, false, 2, 1024>,
+                         (const void*)k_ntt<true, true, 2, 1024>,  (const void*)k_ntt<true, false, 2, 1024>};
     size_t nn = 0;
     if (hipGraphGetNodes(g->g, nullptr, &nn) != hipSuccess) return -1;
     std::vector<hipGraphNode_t> nodes(nn);

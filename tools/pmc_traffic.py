@@ -50,7 +50,7 @@ def load(path, counter):
 def ntt_rows(name: str, grid: int, n: int) -> int:
     """Rows of one k_ntt<INV, COL, LE> launch: each thread of a pass holds
     2^LE words, so a row takes n / 2^LE threads (Grid_Size = total threads)."""
-    m = re.search(r"k_ntt<\s*\w+,\s*\w+,\s*(\d+)>", name)
+    m = re.search(r"k_ntt<\s*\w+,\s*\w+,\s*(\d+)", name)
     le = int(m.group(1)) if m else 3
     return grid * (1 << le) // n
 

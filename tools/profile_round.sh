@@ -1,9 +1,13 @@
 # One GPU call's worth of round profiling (run from the repo root on the box):
-# rocprofv3 kernel trace + stats of the bench (graph-replayed timed sorts),
-# two PMC passes (FETCH_SIZE / WRITE_SIZE) -> HBM traffic per launch
-# (profiles/pmc_traffic.json, copied back through gpurun_out/).  The PMC
-# passes run the sorts eagerly (SFHE_GRAPH=0): counter collection over
-# graph-launched kernels stalled past the box's 180 s silence limit.
+#  1. rocprofv3 kernel trace + stats of the bench (graph-replayed timed sorts)
+#     -> gpurun_out/<tag>_rocprof_summary.txt (tools/trace_segments.py) and
+#        <tag>_kernel_stats.csv;
+#  2. two PMC passes (FETCH_SIZE / WRITE_SIZE, separate runs: gfx950 cannot
+#     collect both in one) over tools/build/microbench -- the NTT at 1..96
+#     limbs plus the key-switch prims at the top level, eagerly launched.  A
+#     whole sort under PMC serialises ~5.5 k dispatches with counter reads and
+#     outlives the box's 180 s silence limit, so the traffic ratio comes from
+#     the same kernels on the microbench -> gpurun_out/pmc_traffic.json.
 #   bash tools/profile_round.sh <tag>
 set -e
 tag=${1:-rXX}
@@ -12,9 +16,9 @@ export TMPDIR=/tmp
 # the bench's roofline replay re-instantiates graph nodes; the profiler's
 # rewritten nodes are not replayed (the trace itself gives the durations)
 export SFHE_NO_GRAPH_REPLAY=1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 3 --warmup 1 --trials 0 --no-cpu-baseline --no-hybrid1 > gpurun_out/prof_bench.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 3 --warmup 1 --trials 0 --no-cpu-baseline --no-hybrid1 --no-kway > gpurun_out/prof_bench.log 2>&1
 python3 tools/trace_segments.py gpurun_out/prof/run_kernel_trace.csv > gpurun_out/${tag}_rocprof_summary.txt 2>&1
 cp gpurun_out/prof/run_kernel_stats.csv gpurun_out/${tag}_kernel_stats.csv
-SFHE_GRAPH=0 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcF -o run -- python3 bench.py --steps 1 --warmup 1 --trials 0 --no-cpu-baseline --no-hybrid1 > gpurun_out/pmcF.log 2>&1
-SFHE_GRAPH=0 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcW -o run -- python3 bench.py --steps 1 --warmup 1 --trials 0 --no-cpu-baseline --no-hybrid1 > gpurun_out/pmcW.log 2>&1
+timeout -s KILL 170 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcF -o run -- tools/build/microbench 16 > gpurun_out/pmcF.log 2>&1
+timeout -s KILL 170 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcW -o run -- tools/build/microbench 16 > gpurun_out/pmcW.log 2>&1
 python3 tools/pmc_traffic.py gpurun_out/pmcF/run_counter_collection.csv gpurun_out/pmcW/run_counter_collection.csv --n 65536 --out gpurun_out/pmc_traffic.json > gpurun_out/pmc.log 2>&1
