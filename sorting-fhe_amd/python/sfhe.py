@@ -536,6 +536,10 @@ def decompose(N: int, keys: Sequence[int], rotation: int, wrapN: int, algo: int,
     s = (C.c_int32 * cap)()
     cnt = C.c_size_t()
     rc = lib.sfhe_decompose(N, k, len(keys), rotation, wrapN, algo, v, s, cap, C.byref(cnt))
+    if rc == SFHE_OK and cnt.value > cap:  # long chains: ask again with room for all of them
+        cap = cnt.value
+        v, s = (C.c_int32 * cap)(), (C.c_int32 * cap)()
+        rc = lib.sfhe_decompose(N, k, len(keys), rotation, wrapN, algo, v, s, cap, C.byref(cnt))
     if rc != SFHE_OK:
         raise SfheError(lib.sfhe_last_error().decode())
     return [(v[i], s[i]) for i in range(min(cnt.value, cap))]
