@@ -78,3 +78,22 @@ def test_kway_bitexact_hip_vs_oracle(hip_lib, oracle_lib):
         assert np.max(np.abs(np.array(e.decrypt(out))[:4] - np.sort(x))) < 0.01
         raw[backend] = out.download()
     assert np.array_equal(raw["hip"], raw["oracle"])
+
+
+def test_kway_schedule_matches_reference_masking():
+    """The network schedule pinned to the reference's own code: the reference's
+    src/k-way/Masking.cpp, compiled where it lies (oracle/Makefile `ref`), and
+    the engine's algo/k-way/Masking.cpp print identical sortType /
+    getRotateDistance / genIndices / genMask output for every stage of every
+    k in {2, 3, 5} network up to 1024 slots."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    ref = os.environ.get("SFHE_REFERENCE", "/root/reference")
+    if not os.path.isfile(os.path.join(ref, "src", "k-way", "Masking.cpp")):
+        pytest.skip("reference sources absent")
+    subprocess.run(["make", "-C", os.path.join(root, "oracle"), "ref"], check=True, stdout=subprocess.DEVNULL)
+    outs = [subprocess.run([os.path.join(root, "oracle", "_ref", f"masking_dump_{w}")], capture_output=True,
+                           text=True, check=True).stdout for w in ("ref", "engine")]
+    assert outs[0].count("stage=") > 100
+    assert outs[0] == outs[1]
