@@ -208,6 +208,46 @@ def kway_leg(device, k=2, M=10, logn=17):
             "stages": M + M * (M - 1) // 2 * ((k + 1) // 2)}
 
 
+def c5_leg(device, world=1, rank=0, steps=2):
+    """BASELINE config 5's sort: DirectSort<256> at ring 2^17 (DirectSortTest's
+    ring, HEStd_128_classic, ~40 limbs).  world == 1: one GPU, unsharded (the
+    reference point).  world > 1: the ranks LIMB-SHARD one sort over RCCL
+    (SURVEY §8(e)): per-sort wall-clock at W GPUs.  Run after the replica
+    measurement, as an extra field; a watchdog (SFHE_C5_TIMEOUT s, default
+    240) prints the line without it and exits if the collective path stalls."""
+    import numpy as np
+    N, logn, secure = WORKLOADS["directsort_n256_2e17"]
+    depth, rots = sfhe.direct_sort_params(N, "hip")
+    shard = None
+    transport = os.environ.get("SFHE_C5_TRANSPORT", "rccl")  # "host": gloo rehearsal (ranks may share a GPU)
+    if world > 1 and transport == "host":
+        shard = ("host", rank, world, sfhe.GlooComm())
+    elif world > 1:
+        import torch.distributed as dist
+        uid = [sfhe.comm_uid("hip") if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        shard = ("rccl", rank, world, uid[0])
+    t0 = time.perf_counter()
+    eng = sfhe.Engine("hip", mult_depth=depth, ring_dim=1 << logn, batch_size=N, secure=secure,
+                      rotations=rots, seed=20251205 + N, device=device, shard=shard)
+    eng.set_quiet(True)
+    setup_s = time.perf_counter() - t0
+    x = input_vector(N)
+    ct = eng.encrypt(x.tolist())
+    sorter = eng.sorter(N)
+    cfg = sign_config(N)
+    holder = {}
+
+    def step():
+        holder["out"] = sorter.sort(ct, *cfg)
+
+    dt = timed_steps(step, eng.sync, world, steps, 1)
+    err = float(np.max(np.abs(np.array(eng.decrypt(holder["out"]))[:N] - np.sort(x))))
+    return {"workload": f"DirectSort<{N}> @ ring 2^{logn} (HEStd_128_classic, depth {depth})",
+            "parallelism": f"limb-shard x{world} ({transport})" if world > 1 else "1 GPU, unsharded",
+            "ms_per_sort": dt / steps * 1e3, "setup_s": setup_s, "max_err": err, "level": holder["out"].level}
+
+
 def pmc_traffic(family: str):
     """HBM traffic / algorithmic bytes for `family` from the committed PMC
     summary (tools/pmc_traffic.py over tools/profile_round.sh's two PMC passes
@@ -240,6 +280,8 @@ def main(argv=None):
                     help="skip the k-way leg (BASELINE config 4: N=1024 @ 2^17, one ~14 s sort)")
     ap.add_argument("--no-hybrid1", dest="hybrid1", action="store_false",
                     help="skip the sort_hybrid1 leg (N=256 @ 2^17, the published-timing path)")
+    ap.add_argument("--no-c5", dest="c5", action="store_false",
+                    help="skip the config-5 leg (N=256 @ 2^17: unsharded at N=1, limb-sharded over RCCL at N>1)")
     ap.add_argument("--shard", choices=("rccl", "host"), default=None,
                     help="limb-shard one sort over the ranks instead of running replicas")
     args = ap.parse_args(argv)
@@ -413,6 +455,23 @@ def main(argv=None):
         "trials": trials,
         "cpu_baseline": None,
     }
+    if args.c5 and not shard:
+        import threading
+
+        def stalled():  # the collective path hung: report what was measured and leave
+            if rank == 0:
+                result["c5"] = {"error": f"timeout after {limit:.0f} s"}
+                print(json.dumps(result), flush=True)
+            os._exit(0)
+        limit = float(os.environ.get("SFHE_C5_TIMEOUT", "240"))
+        dog = threading.Timer(limit, stalled)
+        dog.daemon = True
+        dog.start()
+        try:
+            result["c5"] = c5_leg(device, world, rank)
+        except Exception as e:  # noqa: BLE001 -- an extra leg must not lose the metric line
+            result["c5"] = {"error": str(e)}
+        dog.cancel()
     if rank == 0 and world == 1 and args.hybrid1:
         try:
             result["hybrid1"] = hybrid1_leg(device)

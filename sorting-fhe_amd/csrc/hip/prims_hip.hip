@@ -25,6 +25,7 @@
 #include <mutex>
 #include <unordered_map>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../modarith.h"
@@ -2215,8 +2216,18 @@ static void nttRows(sfp_dev* d, const RowGroup& G, int inverse) {
         const char* v = std::getenv("SFHE_NTT_T1K_ROWS");
         return v ? (uint32_t)std::atoi(v) : 64u;
     }();
-    const bool t1k = rows <= t1kRows && d->n <= (1u << 17);
-    const dim3 g(d->n / (t1k ? 1024u : (uint32_t)kNttTile), rows);
+    // SFHE_NTT_SMALL_TILE (512 / 1024) and SFHE_NTT_SMALL_LE (2 / 3): the
+    // small-launch tile and register-round width (A/B knobs; defaults measured)
+    static const uint32_t smallTile = [] {
+        const char* v = std::getenv("SFHE_NTT_SMALL_TILE");
+        return v ? (uint32_t)std::atoi(v) : 1024u;
+    }();
+    static const int smallLe = [] {
+        const char* v = std::getenv("SFHE_NTT_SMALL_LE");
+        return v ? std::atoi(v) : 2;
+    }();
+    const bool t1k = rows <= t1kRows && d->n <= smallTile * 128u;
+    const dim3 g(d->n / (t1k ? smallTile : (uint32_t)kNttTile), rows);
     const bool small = rows < (uint32_t)kNttSmallRows;
     auto pass = [&](auto kern, int threads) {
         timedLaunch(d, SFP_FAM_NTT, bytes, [&] {
@@ -2230,14 +2241,29 @@ static void nttRows(sfp_dev* d, const RowGroup& G, int inverse) {
     }();
     const int L = le ? le : (small ? 2 : 3);
     constexpr int T = kNttTile;
-    if (t1k) {
-        if (!inverse) {
-            pass(k_ntt<false, true, 2, 1024>, 1024 >> 2);
-            pass(k_ntt<false, false, 2, 1024>, 1024 >> 2);
+    auto smallPasses = [&](auto tileC) {
+        constexpr int ST = decltype(tileC)::value;
+        if (smallLe == 3) {
+            if (!inverse) {
+                pass(k_ntt<false, true, 3, ST>, ST >> 3);
+                pass(k_ntt<false, false, 3, ST>, ST >> 3);
+            } else {
+                pass(k_ntt<true, false, 3, ST>, ST >> 3);
+                pass(k_ntt<true, true, 3, ST>, ST >> 3);
+            }
+        } else if (!inverse) {
+            pass(k_ntt<false, true, 2, ST>, ST >> 2);
+            pass(k_ntt<false, false, 2, ST>, ST >> 2);
         } else {
-            pass(k_ntt<true, false, 2, 1024>, 1024 >> 2);
-            pass(k_ntt<true, true, 2, 1024>, 1024 >> 2);
+            pass(k_ntt<true, false, 2, ST>, ST >> 2);
+            pass(k_ntt<true, true, 2, ST>, ST >> 2);
         }
+    };
+    if (t1k) {
+        if (smallTile == 512)
+            smallPasses(std::integral_constant<int, 512>{});
+        else
+            smallPasses(std::integral_constant<int, 1024>{});
     } else if (!inverse) {
         if (L == 4) {
             pass(k_ntt<false, true, 4, T>, T >> 4);
@@ -2373,7 +2399,13 @@ int sfp_graph_family_time(sfp_dev* d, sfp_graph* g, uint32_t fam, int reps, doub
                          (const void*)k_ntt<false, true, 4, T>, (const void*)k_ntt<false, false, 4, T>,
                          (const void*)k_ntt<true, true, 4, T>,  (const void*)k_ntt<true, false, 4, T>,
                          (const void*)k_ntt<false, true, 2, 1024>, (const void*)k_ntt<false, false, 2, 1024>,
-                         (const void*)k_ntt<true, true, 2, 1024>,  (const void*)k_ntt<true, false, 2, 1024>};
+                         (const void*)k_ntt<true, true, 2, 1024>,  (const void*)k_ntt<true, false, 2, 1024>,
+                         (const void*)k_ntt<false, true, 3, 1024>, (const void*)k_ntt<false, false, 3, 1024>,
+                         (const void*)k_ntt<true, true, 3, 1024>,  (const void*)k_ntt<true, false, 3, 1024>,
+                         (const void*)k_ntt<false, true, 2, 512>, (const void*)k_ntt<false, false, 2, 512>,
+                         (const void*)k_ntt<true, true, 2, 512>,  (const void*)k_ntt<true, false, 2, 512>,
+                         (const void*)k_ntt<false, true, 3, 512>, (const void*)k_ntt<false, false, 3, 512>,
+                         (const void*)k_ntt<true, true, 3, 512>,  (const void*)k_ntt<true, false, 3, 512>};
     size_t nn = 0;
     if (hipGraphGetNodes(g->g, nullptr, &nn) != hipSuccess) return -1;
     std::vector<hipGraphNode_t> nodes(nn);
