@@ -1943,9 +1943,11 @@ sfp_dev* sfp_create(int device, const sfp_tables* t) {
     d->logn = t->logn;
     d->n = 1u << t->logn;
     d->np = t->nprimes;
-    if (d->logn < 10) {
+    if (d->logn < 10 || d->logn > 17) {
         delete d;
-        return nullptr;  // rings from 2^10 (up to 2^11 the NTT runs k_ntt_small)
+        // rings 2^10 .. 2^17: up to 2^11 the NTT runs k_ntt_small; the COL
+        // pass stages 2^logR - 1 <= kNttColTw twiddles in LDS (logR <= 9)
+        return nullptr;
     }
     d->nLanes = 4;
     if (const char* v = std::getenv("SFHE_LANES")) d->nLanes = std::max(1, std::min(SFP_MAX_LANES, std::atoi(v)));
