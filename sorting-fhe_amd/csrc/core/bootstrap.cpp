@@ -102,6 +102,7 @@ struct BootstrapPrecomp {
     std::map<double, Group> s2cFirst;   // s2c[0] with the output factor folded in, per factor
     std::vector<double> cheb;           // cos(2 pi (x - 1/4) / 2^r) on [-K-1, K+1]
     std::vector<int32_t> rotations;
+    PrivateKey<DCRTPoly> dbgSk;  // SFHE_BOOT_DEBUG only: the key EvalBootstrapKeyGen saw
 };
 
 namespace {
@@ -174,13 +175,12 @@ std::vector<Group> groupStages(const std::vector<DiagMap>& stages, uint32_t budg
 int32_t signedOffset(uint32_t k, uint32_t S) { return k > S / 2 ? (int32_t)k - (int32_t)S : (int32_t)k; }
 
 // SFHE_BOOT_DEBUG=1: decrypt and print every stage (diagnostics; the key
-// EvalBootstrapKeyGen saw is kept for it)
-PrivateKey<DCRTPoly> g_dbgSk;
-void dbg(CryptoContextImpl<DCRTPoly>* cc, const char* what, const Ciphertext<DCRTPoly>& c) {
+// EvalBootstrapKeyGen saw is kept in the context's precomputation for it)
+void dbg(CryptoContextImpl<DCRTPoly>* cc, const BootstrapPrecomp& b, const char* what, const Ciphertext<DCRTPoly>& c) {
     static const bool on = std::getenv("SFHE_BOOT_DEBUG") != nullptr;
-    if (!on || !g_dbgSk) return;
+    if (!on || !b.dbgSk) return;
     Plaintext pt;
-    cc->Decrypt(g_dbgSk, c, &pt);
+    cc->Decrypt(b.dbgSk, c, &pt);
     const auto& v = pt->GetCKKSPackedValue();
     std::fprintf(stderr, "BOOT %-10s L%-3u", what, c->GetLevel());
     for (size_t i = 0; i < std::min<size_t>(8, v.size()); ++i)
@@ -234,7 +234,7 @@ void CryptoContextImpl<DCRTPoly>::EvalBootstrapKeyGen(const PrivateKey<DCRTPoly>
     if (it == s->boot.end()) SFHE_THROW("EvalBootstrapKeyGen: call EvalBootstrapSetup for these slots first");
     EvalRotateKeyGen(sk, it->second->rotations);
     EvalConjugateKeyGen(sk);
-    if (std::getenv("SFHE_BOOT_DEBUG")) g_dbgSk = sk;
+    if (std::getenv("SFHE_BOOT_DEBUG")) it->second->dbgSk = sk;
     if (!s->relinKey) EvalMultKeyGen(sk);
 }
 
@@ -321,18 +321,18 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::BootstrapOnce(const Ciphertext
     const int preScaleBits =
         std::max(0, kTargetBits - (int)std::lround(std::log2((double)s->primes[0] / deltaL)));
     auto low = AdjustLevelScaled(ct, s->L, inFactor * std::ldexp(1.0, -preScaleBits));
-    dbg(this, "low", low);
+    dbg(this, b, "low", low);
     auto raised = ModRaise(low);
     raised->SetSlots(S);
-    dbg(this, "raised", raised);
+    dbg(this, b, "raised", raised);
     // 3: sparse trace
     for (uint32_t t = S; t < s->n / 2; t <<= 1) raised = EvalAdd(raised, EvalRotate(raised, (int32_t)t));
-    dbg(this, "traced", raised);
+    dbg(this, b, "traced", raised);
     // 4: CoeffsToSlots (h = u / 2 in bit-reversed order)
     Ciphertext<DCRTPoly> h = raised;
     for (auto& gr : b.c2s) {
         h = applyGroup(this, gr, S, {h}, false);
-        dbg(this, "c2s", h);
+        dbg(this, b, "c2s", h);
     }
     // 5: real and imaginary halves
     auto hc = EvalConjugate(h);
@@ -343,12 +343,12 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::BootstrapOnce(const Ciphertext
     auto yre = EvalMult(re, 1.0 / Kb);
     Plaintext negi = MakeCKKSPackedPlaintext(std::vector<cd>(S, cd(0.0, -1.0 / Kb)), 1, imi->GetLevel(), nullptr, S);
     auto yim = EvalMult(imi, negi);
-    dbg(this, "re", re);
-    dbg(this, "yim", yim);
+    dbg(this, b, "re", re);
+    dbg(this, b, "yim", yim);
     auto wre = evalMod(this, b, yre);
     auto wim = evalMod(this, b, yim);
-    dbg(this, "wre", wre);
-    dbg(this, "wim", wim);
+    dbg(this, b, "wre", wre);
+    dbg(this, b, "wim", wim);
     // 7: SlotsToCoeffs of w_re + i w_im, times q_0 2^k outFactor / (2 pi Delta_L)
     const double cOut = (double)s->primes[0] * std::ldexp(1.0, preScaleBits) * outFactor / (2.0 * M_PI * deltaL);
     // the first S2C group with cOut folded into its diagonals (one copy per
@@ -361,10 +361,10 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::BootstrapOnce(const Ciphertext
         fit = b.s2cFirst.emplace(cOut, std::move(g0)).first;
     }
     auto out = applyGroup(this, fit->second, S, {wre, wim}, true);
-    dbg(this, "s2c", out);
+    dbg(this, b, "s2c", out);
     for (size_t g = 1; g < b.s2c.size(); ++g) {
         out = applyGroup(this, b.s2c[g], S, {out}, false);
-        dbg(this, "s2c", out);
+        dbg(this, b, "s2c", out);
     }
     return out;
 }
