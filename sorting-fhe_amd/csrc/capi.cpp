@@ -560,6 +560,74 @@ int sfhe_kway_sort(sfhe_ctx* c, const sfhe_ct* in, int k, int M, int n, int dg, 
     });
 }
 
+}  // extern "C"
+
+namespace {
+struct KWayBase {
+    virtual ~KWayBase() = default;
+    virtual Ct run(const Ct& in, SignConfig& cfg) = 0;
+    virtual size_t nodes() const = 0;
+};
+template <int N>
+struct KWayImpl : KWayBase {
+    KWayAdapter<N> a;
+    KWayImpl(sfhe_ctx* c, int k, int M)
+        : a(c->cc, c->keys.publicKey, c->keys.secretKey,
+            std::make_shared<Encryption>(c->cc, c->keys.publicKey), k, M) {}
+    Ct run(const Ct& in, SignConfig& cfg) override { return a.sort(in, SignFunc::CompositeSign, cfg); }
+    size_t nodes() const override { return a.graphNodes(); }
+};
+std::unique_ptr<KWayBase> makeKWay(sfhe_ctx* c, uint32_t N, int k, int M) {
+    switch (N) {
+#define SFHE_KWAY_N(v) \
+    case v: return std::make_unique<KWayImpl<v>>(c, k, M);
+        SFHE_KWAY_N(4) SFHE_KWAY_N(8) SFHE_KWAY_N(16) SFHE_KWAY_N(32) SFHE_KWAY_N(64) SFHE_KWAY_N(128)
+        SFHE_KWAY_N(256) SFHE_KWAY_N(512) SFHE_KWAY_N(1024) SFHE_KWAY_N(9) SFHE_KWAY_N(27) SFHE_KWAY_N(81)
+        SFHE_KWAY_N(243) SFHE_KWAY_N(729) SFHE_KWAY_N(25) SFHE_KWAY_N(125) SFHE_KWAY_N(625)
+#undef SFHE_KWAY_N
+    }
+    return nullptr;
+}
+}  // namespace
+
+struct sfhe_kway {
+    sfhe_ctx* ctx;
+    std::unique_ptr<KWayBase> impl;
+};
+
+extern "C" {
+
+int sfhe_kway_create(sfhe_ctx* c, uint32_t N, int k, int M, sfhe_kway** out) {
+    REQUIRE(c && out, "null argument");
+    REQUIRE(k == 2 || k == 3 || k == 5, "k must be 2, 3 or 5");
+    long len = 1;
+    for (int i = 0; i < M && len <= (1 << 20); ++i) len *= k;
+    REQUIRE(M >= 1 && len == (long)N, "N must equal k^M");
+    return guard([&] {
+        auto impl = makeKWay(c, N, k, M);
+        if (!impl) throw std::invalid_argument("unsupported N for the k-way network");
+        *out = new sfhe_kway{c, std::move(impl)};
+    });
+}
+
+int sfhe_kway_run(sfhe_kway* s, const sfhe_ct* in, int n, int dg, int df, uint32_t mult_depth, sfhe_ct** out) {
+    REQUIRE(s && in && out, "null argument");
+    REQUIRE(n == 3 || n == 4, "composite sign degree n must be 3 or 4");
+    return guard([&] {
+        Quiet q(s->ctx->quiet);
+        SignConfig cfg(CompositeSignConfig(n, dg, df), (int)mult_depth);
+        *out = wrap(s->impl->run(in->ct, cfg));
+    });
+}
+
+int sfhe_kway_graph_nodes(sfhe_kway* s, uint64_t* nodes) {
+    REQUIRE(s && nodes, "null argument");
+    *nodes = s->impl->nodes();
+    return SFHE_OK;
+}
+
+void sfhe_kway_destroy(sfhe_kway* s) { delete s; }
+
 int sfhe_kway_params(uint32_t N, uint32_t* batch, uint32_t* mult_depth, uint32_t* budget_c2s, uint32_t* budget_s2c,
                      int32_t* rotations, size_t cap, size_t* count) {
     REQUIRE(N >= 2 && N <= (1u << 16), "N out of range");

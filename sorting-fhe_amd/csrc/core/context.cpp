@@ -1999,26 +1999,23 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::ModRaise(const Ciphertext<DCRT
     if (s->world > 1) SFHE_THROW("bootstrapping a limb-sharded context is not supported");
     if (s->ellOf(a->level) != 1) SFHE_THROW("ModRaise needs a ciphertext at the last level (one limb)");
     const uint32_t n = s->n;
-    const u64 q0 = s->primes[0];
-    // coefficient form of both single-limb polys, centred lift to every Q limb
+    // coefficient form of both single-limb polys, then their centred lift to
+    // every Q limb, NTT'd there -- on the device: the rescale-with-given-row
+    // prim computes (in - [last]_{q_i}) * k_i; with in = 0 and k_i = -1 that is
+    // [last]_{q_i} (no host round trip, so bootstrapping can be captured)
     auto t = s->alloc(2 * (size_t)n);
     sfp_d2d(s->dev, t->ptr, a->c0, (size_t)n * 8);
     sfp_d2d(s->dev, t->ptr + n, a->c1, (size_t)n * 8);
-    sfp_ntt(s->dev, t->ptr, sfp_limbs{1, 1, 0, 0}, 1);
-    sfp_ntt(s->dev, t->ptr + n, sfp_limbs{1, 1, 0, 0}, 1);
-    std::vector<u64> h(2 * (size_t)n);
-    sfp_d2h(s->dev, h.data(), t->ptr, h.size() * 8);
+    sfp_ntt(s->dev, t->ptr, sfp_limbs{1, 1, 0, 0, 0}, 1);
+    sfp_ntt(s->dev, t->ptr + n, sfp_limbs{1, 1, 0, 0, 0}, 1);
     auto out = SfheInternal::newCt(this, 0, a->slots);
-    std::vector<int64_t> c(n);
-    for (int p = 0; p < 2; ++p) {
-        for (uint32_t i = 0; i < n; ++i) {
-            const u64 v = h[(size_t)p * n + i];
-            c[i] = v > q0 / 2 ? -(int64_t)(q0 - v) : (int64_t)v;
-        }
-        uint64_t* dst = p ? out->c1 : out->c0;
-        sfp_load_i64(s->dev, dst, c.data(), s->qmap(s->Lq));
-        sfp_ntt(s->dev, dst, s->qmap(s->Lq), 0);
-    }
+    const size_t pw = s->polyWords(0);
+    auto zero = s->alloc(2 * pw);
+    sfp_zero(s->dev, zero->ptr, 2 * pw * 8);
+    std::vector<uint64_t> minus1(s->Lq);
+    for (uint32_t i = 0; i < s->Lq; ++i) minus1[i] = s->primes[i] - 1;
+    sfp_rescale_rows(s->dev, out->c0, zero->ptr, t->ptr, 0, s->qmap(s->Lq), minus1.data(), 2, pw,
+                     (size_t)(out->c1 - out->c0), n);
     s->wrote(out->buf.get());
     return SfheInternal::traced(this, out, "ModRaise");
 }

@@ -40,6 +40,7 @@ ABI_SYMBOLS = [
     "sfhe_bootstrap_setup", "sfhe_bootstrap_depth", "sfhe_bootstrap",
     "sfhe_sorter_sort_bitonic", "sfhe_kway_sort", "sfhe_kway_params",
     "sfhe_save", "sfhe_load", "sfhe_ct_save", "sfhe_ct_load",
+    "sfhe_kway_create", "sfhe_kway_run", "sfhe_kway_graph_nodes", "sfhe_kway_destroy",
 ]
 
 
@@ -124,6 +125,10 @@ _SIGS = {
     "sfhe_hybrid1_params": (C.c_int, [_U32, _PU32, _PI32, _SZ, _PSZ]),
     "sfhe_sorter_sort_bitonic": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_int, _PVP]),
     "sfhe_save": (C.c_int, [_VP, C.c_char_p]),
+    "sfhe_kway_create": (C.c_int, [_VP, _U32, C.c_int, C.c_int, _PVP]),
+    "sfhe_kway_run": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_int, _U32, _PVP]),
+    "sfhe_kway_graph_nodes": (C.c_int, [_VP, C.POINTER(C.c_uint64)]),
+    "sfhe_kway_destroy": (None, [_VP]),
     "sfhe_load": (C.c_int, [C.c_char_p, _PVP]),
     "sfhe_ct_save": (C.c_int, [_VP, _VP, C.c_char_p]),
     "sfhe_ct_load": (C.c_int, [_VP, C.c_char_p, _PVP]),
@@ -369,6 +374,12 @@ class Engine:
     def bootstrap(self, a, iterations: int = 1, precision: int = 0):
         return self._new(self.lib.sfhe_bootstrap, self.ctx, a.h, iterations, precision)
 
+    def kway(self, k: int, M: int) -> "KWay":
+        """A persistent KWayAdapter<k^M> (graph-replayed from its second sort)."""
+        h = C.c_void_p()
+        self._chk(self.lib.sfhe_kway_create(self.ctx, k ** M, k, M, C.byref(h)))
+        return KWay(self, h)
+
     def kway_sort(self, a, k: int, M: int, n: int = 3, dg: int = 2, df: int = 2, mult_depth: int = 40):
         """KWayAdapter<k^M>::sort (reference kway_adapter.h:66-72): the k-way
         network with CompositeSign(n, dg, df) and lazy bootstrapping."""
@@ -490,6 +501,27 @@ def direct_sort_params(N: int, backend: str = "hip"):
     buf = (C.c_int32 * cnt.value)()
     lib.sfhe_direct_sort_params(N, None, buf, cnt.value, None)
     return depth.value, list(buf)
+
+
+class KWay:
+    def __init__(self, eng: "Engine", h):
+        self.eng, self.h = eng, h
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.eng.lib.sfhe_kway_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    def sort(self, ct: "Ct", n: int = 3, dg: int = 2, df: int = 2, mult_depth: int = 40) -> "Ct":
+        return self.eng._new(self.eng.lib.sfhe_kway_run, self.h, ct.h, n, dg, df, mult_depth)
+
+    def graph_nodes(self) -> int:
+        v = C.c_uint64()
+        self.eng._chk(self.eng.lib.sfhe_kway_graph_nodes(self.h, C.byref(v)))
+        return v.value
 
 
 def kway_params(N: int, backend: str = "hip"):
