@@ -225,12 +225,12 @@ int sfhe_ct_load(sfhe_ctx* c, const char* path, sfhe_ct** out);
 int sfhe_kway_sort(sfhe_ctx* c, const sfhe_ct* in, int k, int M, int n, int dg, int df, uint32_t mult_depth,
                    sfhe_ct** out);
 /* A persistent KWayAdapter<N> (N = k^M; k = 2: N = 4 .. 1024, k = 3: 9 .. 729,
- * k = 5: 25 .. 625): its second and later sorts of one shape replay a hipGraph
- * of the whole network, bootstraps included (kway_adapter.h). */
+ * k = 5: 25 .. 625): the reference's adapter object (kway_adapter.h:23-35),
+ * whose sorts after the first reuse the encoded masks and bootstrapping
+ * diagonals. */
 typedef struct sfhe_kway sfhe_kway;
 int sfhe_kway_create(sfhe_ctx* c, uint32_t N, int k, int M, sfhe_kway** out);
 int sfhe_kway_run(sfhe_kway* s, const sfhe_ct* in, int n, int dg, int df, uint32_t mult_depth, sfhe_ct** out);
-int sfhe_kway_graph_nodes(sfhe_kway* s, uint64_t* nodes);
 void sfhe_kway_destroy(sfhe_kway* s);
 /* KWayAdapter<N>::getSizeParameters (kway_adapter.h:41-64): batch (next power
  * of two >= N), depth 40, first modulus 60 / scale 59 bits, level budget

@@ -141,6 +141,7 @@ int sfp_graph_family_time(sfp_dev* d, sfp_graph* g, uint32_t fam, int reps, doub
 void sfp_serialize(sfp_dev* d, int on) { (void)d; (void)on; }
 /* no graphs: the host layer runs every region eagerly */
 int sfp_capture_begin(sfp_dev* d) { (void)d; return -1; }
+void sfp_clear_error(sfp_dev* d) { (void)d; }
 sfp_graph* sfp_capture_end(sfp_dev* d) { (void)d; return NULL; }
 int sfp_capturing(sfp_dev* d) { (void)d; return 0; }
 void sfp_graph_launch(sfp_dev* d, sfp_graph* g) { (void)d; (void)g; }

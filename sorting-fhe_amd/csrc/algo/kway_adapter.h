@@ -5,7 +5,6 @@
 
 #include <cassert>
 #include <cmath>
-#include <cstdlib>
 #include <memory>
 
 #include "k-way/Sorter.h"
@@ -44,57 +43,14 @@ class KWayAdapter : public SortBase<N> {
         parameters.SetMultiplicativeDepth(40);
     }
 
-    // The network's op sequence -- including where it bootstraps (levels
-    // only) -- depends on (N, k, M, the input's level and slots, the sign
-    // configuration), never on the data.  As DirectSort::sort (sort_algo.h),
-    // the first sort of a shape runs eagerly (encoding the masks and the
-    // bootstrapping diagonals), the second is captured into one hipGraph over
-    // an adapter-owned input copy, and later sorts replay it.  Debug sorts,
-    // sharded contexts and SFHE_GRAPH=0 stay eager.
+    // (Not graph-captured, unlike DirectSort::sort: a captured graph pins
+    // every buffer it touches for its lifetime.  One hipGraph per stage was
+    // tried at N = 1024 @ 2^17: each stage is ~4.1 k nodes, and the capture
+    // of stage 17 failed on a host synchronisation -- the pool, whose blocks
+    // 16 captured stages now pinned, had to grow.)
     Ciphertext<DCRTPoly> sort(const Ciphertext<DCRTPoly>& input_array, SignFunc, SignConfig& Cfg) override {
-        const bool debug = dynamic_cast<const DebugEncryption*>(m_enc.get()) != nullptr;
-        const char* env = std::getenv("SFHE_GRAPH");
-        if (debug || m_graphOff || (env && *env == '0') || m_cc->ShardWorld() > 1) return sortEager(input_array, Cfg);
-        const Key key{input_array->GetLevel(), input_array->GetSlots(), Cfg.compos.n, Cfg.compos.dg,
-                      Cfg.compos.df, Cfg.multDepth};
-        if (!(m_graph && m_graphKey == key)) {
-            if (!(m_warm && m_warmKey == key)) {
-                m_warm = true;
-                m_warmKey = key;
-                return sortEager(input_array, Cfg);
-            }
-            m_graph.reset();
-            m_graphIn = input_array->Clone();
-            if (!m_cc->BeginCapture()) {
-                m_graphOff = true;
-                return sortEager(input_array, Cfg);
-            }
-            Ciphertext<DCRTPoly> out;
-            try {
-                out = sortEager(m_graphIn, Cfg);
-            } catch (...) {
-                m_cc->EndCapture(nullptr);
-                m_graphOff = true;
-                throw;
-            }
-            m_graph = m_cc->EndCapture(out);
-            if (!m_graph) {
-                m_graphOff = true;
-                return sortEager(input_array, Cfg);
-            }
-            m_graphOut = out;
-            m_graphKey = key;
-        } else if (m_graphIn != input_array) {
-            m_cc->CopyCiphertextInto(m_graphIn, input_array);
-        }
-        m_cc->Launch(m_graph);
-        auto result = m_graphOut->Clone();
-        result->SetSlots(m_graphOut->GetSlots());
-        return result;
+        return sortEager(input_array, Cfg);
     }
-
-    // nodes of the captured network (0: none yet / eager)
-    size_t graphNodes() const { return m_graph ? m_cc->GraphNodes(m_graph) : 0; }
 
   private:
     Ciphertext<DCRTPoly> sortEager(const Ciphertext<DCRTPoly>& input_array, SignConfig& Cfg) {
@@ -103,20 +59,8 @@ class KWayAdapter : public SortBase<N> {
         return out;
     }
 
-    struct Key {
-        uint32_t level = 0, slots = 0;
-        int n = 0, dg = 0, df = 0, depth = 0;
-        bool operator==(const Key& o) const {
-            return level == o.level && slots == o.slots && n == o.n && dg == o.dg && df == o.df && depth == o.depth;
-        }
-    };
     CryptoContext<DCRTPoly> m_cc;
     PublicKey<DCRTPoly> m_PublicKey;
     std::shared_ptr<Encryption> m_enc;
     std::unique_ptr<kwaySort::Sorter> m_sorter;
-    // (declared last: released before the context handle above)
-    std::shared_ptr<CryptoContextImpl<DCRTPoly>::CapturedGraph> m_graph;
-    Ciphertext<DCRTPoly> m_graphIn, m_graphOut;
-    Key m_graphKey, m_warmKey;
-    bool m_warm = false, m_graphOff = false;
 };

@@ -566,7 +566,6 @@ namespace {
 struct KWayBase {
     virtual ~KWayBase() = default;
     virtual Ct run(const Ct& in, SignConfig& cfg) = 0;
-    virtual size_t nodes() const = 0;
 };
 template <int N>
 struct KWayImpl : KWayBase {
@@ -575,7 +574,6 @@ struct KWayImpl : KWayBase {
         : a(c->cc, c->keys.publicKey, c->keys.secretKey,
             std::make_shared<Encryption>(c->cc, c->keys.publicKey), k, M) {}
     Ct run(const Ct& in, SignConfig& cfg) override { return a.sort(in, SignFunc::CompositeSign, cfg); }
-    size_t nodes() const override { return a.graphNodes(); }
 };
 std::unique_ptr<KWayBase> makeKWay(sfhe_ctx* c, uint32_t N, int k, int M) {
     switch (N) {
@@ -618,12 +616,6 @@ int sfhe_kway_run(sfhe_kway* s, const sfhe_ct* in, int n, int dg, int df, uint32
         SignConfig cfg(CompositeSignConfig(n, dg, df), (int)mult_depth);
         *out = wrap(s->impl->run(in->ct, cfg));
     });
-}
-
-int sfhe_kway_graph_nodes(sfhe_kway* s, uint64_t* nodes) {
-    REQUIRE(s && nodes, "null argument");
-    *nodes = s->impl->nodes();
-    return SFHE_OK;
 }
 
 void sfhe_kway_destroy(sfhe_kway* s) { delete s; }

@@ -2148,6 +2148,7 @@ std::shared_ptr<CryptoContextImpl<DCRTPoly>::CapturedGraph> CryptoContextImpl<DC
     if (!g) {
         const char* e = sfp_last_error(s->dev);
         std::fprintf(stderr, "sfhe: graph capture abandoned, running eagerly (%s)\n", e ? e : "unknown");
+        sfp_clear_error(s->dev);  // not a device fault: the eager rerun must not inherit it
         return nullptr;
     }
     auto out = std::make_shared<CapturedGraph>();

@@ -2358,6 +2358,11 @@ void sfp_graph_destroy(sfp_dev* d, sfp_graph* g) {
     delete g;
 }
 
+void sfp_clear_error(sfp_dev* d) {
+    std::lock_guard<std::mutex> g(d->mu);
+    d->err.clear();
+}
+
 sfp_graph* sfp_capture_end(sfp_dev* d) {
     sfp_graph* g = d->capture;
     if (!g) return nullptr;
@@ -2374,6 +2379,17 @@ sfp_graph* sfp_capture_end(sfp_dev* d) {
     }
     for (auto& c : g->arena) hostToDev(d, c.dev, c.host.data(), c.used * 8);
     if (hipGraphGetNodes(g->g, nullptr, &g->nodes) != hipSuccess) g->nodes = 0;
+    static const size_t maxNodes = [] {  // SFHE_GRAPH_MAX_NODES: larger captures fall back to eager
+        const char* v = std::getenv("SFHE_GRAPH_MAX_NODES");
+        return v ? (size_t)std::atoll(v) : (size_t)200000;
+    }();
+    if (std::getenv("SFHE_GRAPH_DEBUG")) std::fprintf(stderr, "[sfhe] captured graph: %zu nodes\n", g->nodes);
+    if (g->nodes > maxNodes) {
+        sfp_graph_destroy(d, g);
+        std::lock_guard<std::mutex> lk(d->mu);
+        if (d->err.empty()) d->err = "graph capture failed: more nodes than SFHE_GRAPH_MAX_NODES";
+        return nullptr;
+    }
     if (hipGraphInstantiate(&g->exec, g->g, nullptr, nullptr, 0) != hipSuccess) {
         const hipError_t ie = hipGetLastError();
         sfp_graph_destroy(d, g);

@@ -294,6 +294,8 @@ void sfp_ks_inner_map(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t
 // The oracle backend has no graphs: sfp_capture_begin returns -1.
 typedef struct sfp_graph sfp_graph;
 int sfp_capture_begin(sfp_dev* d);
+// forget the recorded error (an abandoned capture is not a device fault)
+void sfp_clear_error(sfp_dev* d);
 sfp_graph* sfp_capture_end(sfp_dev* d);
 int sfp_capturing(sfp_dev* d);
 // Enqueue the whole graph on the current lane (stream-ordered like a prim).

@@ -40,7 +40,7 @@ ABI_SYMBOLS = [
     "sfhe_bootstrap_setup", "sfhe_bootstrap_depth", "sfhe_bootstrap",
     "sfhe_sorter_sort_bitonic", "sfhe_kway_sort", "sfhe_kway_params",
     "sfhe_save", "sfhe_load", "sfhe_ct_save", "sfhe_ct_load",
-    "sfhe_kway_create", "sfhe_kway_run", "sfhe_kway_graph_nodes", "sfhe_kway_destroy",
+    "sfhe_kway_create", "sfhe_kway_run", "sfhe_kway_destroy",
 ]
 
 
@@ -127,7 +127,6 @@ _SIGS = {
     "sfhe_save": (C.c_int, [_VP, C.c_char_p]),
     "sfhe_kway_create": (C.c_int, [_VP, _U32, C.c_int, C.c_int, _PVP]),
     "sfhe_kway_run": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_int, _U32, _PVP]),
-    "sfhe_kway_graph_nodes": (C.c_int, [_VP, C.POINTER(C.c_uint64)]),
     "sfhe_kway_destroy": (None, [_VP]),
     "sfhe_load": (C.c_int, [C.c_char_p, _PVP]),
     "sfhe_ct_save": (C.c_int, [_VP, _VP, C.c_char_p]),
@@ -375,7 +374,7 @@ class Engine:
         return self._new(self.lib.sfhe_bootstrap, self.ctx, a.h, iterations, precision)
 
     def kway(self, k: int, M: int) -> "KWay":
-        """A persistent KWayAdapter<k^M> (graph-replayed from its second sort)."""
+        """A persistent KWayAdapter<k^M> (reuses its encoded masks across sorts)."""
         h = C.c_void_p()
         self._chk(self.lib.sfhe_kway_create(self.ctx, k ** M, k, M, C.byref(h)))
         return KWay(self, h)
@@ -517,11 +516,6 @@ class KWay:
 
     def sort(self, ct: "Ct", n: int = 3, dg: int = 2, df: int = 2, mult_depth: int = 40) -> "Ct":
         return self.eng._new(self.eng.lib.sfhe_kway_run, self.h, ct.h, n, dg, df, mult_depth)
-
-    def graph_nodes(self) -> int:
-        v = C.c_uint64()
-        self.eng._chk(self.eng.lib.sfhe_kway_graph_nodes(self.h, C.byref(v)))
-        return v.value
 
 
 def kway_params(N: int, backend: str = "hip"):
