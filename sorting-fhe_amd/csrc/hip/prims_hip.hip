@@ -483,9 +483,12 @@ __device__ __forceinline__ double fpReduce(double v, double q, double qinv) {
     return r < 0.0 ? r + q : r;
 }
 
-template <bool INV, bool COL, int LE, int B, int TILE>
+// PF: the round's 2^B - 1 twiddles were loaded into registers (pw) at the top
+// of the kernel (ROW pass, see k_ntt), so the round does not wait on HBM.
+template <bool INV, bool COL, int LE, int B, int TILE, bool PF = false>
 __device__ __forceinline__ void nttRoundFP(double* s, const NttTile& T, uint32_t S0, uint32_t k0, double q,
-                                           const double* w, const double* wq, double qinv, bool rowLds) {
+                                           const double* w, const double* wq, double qinv, bool rowLds,
+                                           const double* pw = nullptr) {
     constexpr int M = 1 << B;
     constexpr int GPT = (1 << LE) / M;
     const uint32_t D = 1u << T.d;
@@ -510,16 +513,26 @@ __device__ __forceinline__ void nttRoundFP(double* s, const NttTile& T, uint32_t
         const uint32_t ub = hi * span + lo;
         const uint32_t x0 = nttGlobal<COL>(T, st, ub);
         double W[M - 1], WQ[M - 1];
+        if constexpr (PF) {
+            static_assert(!COL && GPT == 1, "prefetched twiddles: ROW pass, one group per thread");
 #pragma unroll
-        for (int t = 0; t < B; ++t) {
-            const uint32_t tb = (!COL && rowLds) ? twIndexRowLds<TILE>(T, k0 + t, x0) : twIndex<COL>(T, S0, k0 + t, x0);
+            for (int e = 0; e < M - 1; ++e) {
+                W[e] = pw[e];
+                WQ[e] = pw[e] * qinv;
+            }
+        } else {
 #pragma unroll
-            for (int qd = 0; qd < (1 << t); ++qd) {
-                W[(1 << t) - 1 + qd] = w[tb + qd];
-                // ROW twiddles come from HBM: form W/q here (half the bytes).  A
-                // last-bit difference from the table only moves the lazy
-                // quotient estimate by < 2^-6; outputs are canonical either way.
-                WQ[(1 << t) - 1 + qd] = COL ? wq[tb + qd] : W[(1 << t) - 1 + qd] * qinv;
+            for (int t = 0; t < B; ++t) {
+                const uint32_t tb =
+                    (!COL && rowLds) ? twIndexRowLds<TILE>(T, k0 + t, x0) : twIndex<COL>(T, S0, k0 + t, x0);
+#pragma unroll
+                for (int qd = 0; qd < (1 << t); ++qd) {
+                    W[(1 << t) - 1 + qd] = w[tb + qd];
+                    // ROW twiddles come from HBM: form W/q here (half the bytes).  A
+                    // last-bit difference from the table only moves the lazy
+                    // quotient estimate by < 2^-6; outputs are canonical either way.
+                    WQ[(1 << t) - 1 + qd] = COL ? wq[tb + qd] : W[(1 << t) - 1 + qd] * qinv;
+                }
             }
         }
         double v[M];
@@ -649,7 +662,7 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_b
     if (G.skipEll && ii >= G.alpha * pp && ii < min(G.alpha * (pp + 1), G.skipEll)) return;
     const uint32_t prime = primeOf(G.pm, ii);
     const u64 q = bar[prime].q;
-    const bool fp = useFp && q < kFpPrimeBound;  // uniform per block
+    const bool fp = (useFp & 7) && q < kFpPrimeBound;  // uniform per block
     NttTile T;
     T.logn = logn;
     T.d = COL ? logR : 8u;
@@ -673,7 +686,7 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_b
             tX[e] = gx[e + 1];
         }
     }
-    const bool rowLds = kNttRowLdsBuild && !COL && fp && useFp >= 2;
+    const bool rowLds = kNttRowLdsBuild && !COL && fp && (useFp & 7) >= 2;
     if (rowLds) {
         constexpr uint32_t rowsT = TILE / 256;
         for (uint32_t k = 0; k < 8; ++k) {
@@ -684,6 +697,35 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_b
     }
     const u64* rw = COL ? tW : (rowLds ? tR : gw);
     const u64* rx = COL ? tX : gx;
+    // ROW pass, FP64 rows, one group per thread per round (LE = 2): every
+    // round's twiddles are data-independent, so all 4 x 3 of them are loaded
+    // here, in flight together with the tile, instead of one HBM latency per
+    // register round (useFp bit 3 turns this off for A/B runs).
+    constexpr bool kPfBuild = !COL && LE == 2;
+    constexpr int kPfRounds = 8 / 2;
+    const bool rowPf = kPfBuild && fp && !rowLds && !(useFp & 8);
+    double PW[kPfBuild ? kPfRounds * 3 : 1];
+    if constexpr (kPfBuild) {
+        if (rowPf) {
+            const double* gd = reinterpret_cast<const double*>(gw);
+            const uint32_t gid = threadIdx.x;
+#pragma unroll
+            for (int r = 0; r < kPfRounds; ++r) {
+                const uint32_t k0 = 2 * r, logh = 8 - k0 - 2;
+                const uint32_t lo = gid & ((1u << logh) - 1);
+                const uint32_t rest = gid >> logh;
+                const uint32_t hi = rest & ((1u << k0) - 1);
+                const uint32_t st = rest >> k0;
+                const uint32_t x0 = nttGlobal<false>(T, st, hi * (256u >> k0) + lo);
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    const uint32_t tb = twIndex<false>(T, S0, k0 + t, x0);
+#pragma unroll
+                    for (int qd = 0; qd < (1 << t); ++qd) PW[3 * r + (1 << t) - 1 + qd] = gd[tb + qd];
+                }
+            }
+        }
+    }
 
     const u64* in = FIRST ? rowAt(G.src, pp, ii) : rowAt(G.dst, pp, ii);
     u64* cp = nullptr;
@@ -735,7 +777,19 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_b
     __syncthreads();
     NTT_MARK(0);
     const uint32_t nr = (T.d + LE - 1) / LE;
-    for (uint32_t ri = 0; ri < nr; ++ri) {
+    if constexpr (kPfBuild) {
+        if (rowPf) {
+#pragma unroll
+            for (int ri = 0; ri < kPfRounds; ++ri) {
+                const int r = INV ? kPfRounds - 1 - ri : ri;
+                nttRoundFP<INV, false, 2, 2, TILE, true>(reinterpret_cast<double*>(s), T, S0, 2 * r, (double)q,
+                                                         nullptr, nullptr, qinvD[prime], false, PW + 3 * r);
+                __syncthreads();
+                NTT_MARK(1 + ri);
+            }
+        }
+    }
+    for (uint32_t ri = 0; ri < (rowPf ? 0u : nr); ++ri) {
         const uint32_t r = INV ? nr - 1 - ri : ri;
         const uint32_t k0 = LE * r;
         const int b = (int)min((uint32_t)LE, T.d - k0);
@@ -2169,12 +2223,21 @@ const char* sfp_last_error(sfp_dev* d) {
 
 // ---- NTT ----
 // FP64 butterflies for primes < 2^42 (SFHE_NTT_FP=0 selects the integer path)
+// Bit 3 (SFHE_NTT_ROW_PF=0, an A/B knob) turns off the ROW pass's register
+// twiddle prefetch.
 static int nttFp() {
     static const int on = [] {
         const char* v = std::getenv("SFHE_NTT_FP");
         return v ? std::atoi(v) : SFHE_NTT_FP;
     }();
     return on;
+}
+static int nttFlags() {
+    static const int f = [] {
+        const char* pf = std::getenv("SFHE_NTT_ROW_PF");
+        return nttFp() | ((pf && std::atoi(pf) == 0) ? 8 : 0);
+    }();
+    return f;
 }
 
 static RowGroup rowsOf(uint32_t P, uint32_t R, sfp_limbs pm) {
@@ -2234,7 +2297,7 @@ static void nttRows(sfp_dev* d, const RowGroup& G, int inverse) {
     auto pass = [&](auto kern, int threads) {
         timedLaunch(d, SFP_FAM_NTT, bytes, [&] {
             hipLaunchKernelGGL(kern, g, dim3(threads), 0, d->st(), G, d->bar, tw, twS, d->ninv,
-                               d->ninvS, d->logn, twD, twQ, d->qinvD, d->ninvD, d->ninvQ, nttFp());
+                               d->ninvS, d->logn, twD, twQ, d->qinvD, d->ninvD, d->ninvQ, nttFlags());
         });
     };
     static const int le = [] {  // SFHE_NTT_LE: register-round width experiments (2, 3, 4)
