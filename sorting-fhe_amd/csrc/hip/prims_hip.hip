@@ -485,14 +485,17 @@ __device__ __forceinline__ double fpReduce(double v, double q, double qinv) {
 
 // PF: the round's 2^B - 1 twiddles were loaded into registers (pw) at the top
 // of the kernel (ROW pass, see k_ntt), so the round does not wait on HBM.
-template <bool INV, bool COL, int LE, int B, int TILE, bool PF = false>
+// DC > 0: the pass's stage count is the compile-time DC (== T.d), so with an
+// unrolled round loop every shift and mask below folds to a constant.
+template <bool INV, bool COL, int LE, int B, int TILE, bool PF = false, int DC = 0>
 __device__ __forceinline__ void nttRoundFP(double* s, const NttTile& T, uint32_t S0, uint32_t k0, double q,
                                            const double* w, const double* wq, double qinv, bool rowLds,
                                            const double* pw = nullptr) {
     constexpr int M = 1 << B;
     constexpr int GPT = (1 << LE) / M;
-    const uint32_t D = 1u << T.d;
-    const uint32_t logh = T.d - k0 - B;
+    const uint32_t d = DC ? (uint32_t)DC : T.d;
+    const uint32_t D = 1u << d;
+    const uint32_t logh = d - k0 - B;
     const uint32_t h = 1u << logh;
     const uint32_t span = D >> k0;
 #pragma unroll
@@ -662,7 +665,7 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_b
     if (G.skipEll && ii >= G.alpha * pp && ii < min(G.alpha * (pp + 1), G.skipEll)) return;
     const uint32_t prime = primeOf(G.pm, ii);
     const u64 q = bar[prime].q;
-    const bool fp = (useFp & 7) && q < kFpPrimeBound;  // uniform per block
+    const bool fp = (useFp & 7) && q < kFpPrimeBound;  // uniform per block (bits 3-4: A/B knobs)
     NttTile T;
     T.logn = logn;
     T.d = COL ? logR : 8u;
@@ -782,14 +785,34 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_b
 #pragma unroll
             for (int ri = 0; ri < kPfRounds; ++ri) {
                 const int r = INV ? kPfRounds - 1 - ri : ri;
-                nttRoundFP<INV, false, 2, 2, TILE, true>(reinterpret_cast<double*>(s), T, S0, 2 * r, (double)q,
-                                                         nullptr, nullptr, qinvD[prime], false, PW + 3 * r);
+                nttRoundFP<INV, false, 2, 2, TILE, true, 8>(reinterpret_cast<double*>(s), T, S0, 2 * r,
+                                                            (double)q, nullptr, nullptr, qinvD[prime], false,
+                                                            PW + 3 * r);
                 __syncthreads();
                 NTT_MARK(1 + ri);
             }
         }
     }
-    for (uint32_t ri = 0; ri < (rowPf ? 0u : nr); ++ri) {
+    // COL pass over 2^8 rows (ring 2^16), FP64 rows, LE = 2: the same four
+    // rounds unrolled with compile-time strides (twiddles already in LDS);
+    // useFp bit 4 (SFHE_NTT_COL_UNROLL=0) keeps the generic loop for A/B runs.
+    constexpr bool kColUnrollBuild = COL && LE == 2;
+    const bool colUnroll = kColUnrollBuild && fp && T.d == 8u && !(useFp & 16);
+    if constexpr (kColUnrollBuild) {
+        if (colUnroll) {
+#pragma unroll
+            for (int ri = 0; ri < 4; ++ri) {
+                const int r = INV ? 3 - ri : ri;
+                nttRoundFP<INV, true, 2, 2, TILE, false, 8>(reinterpret_cast<double*>(s), T, S0, 2 * r, (double)q,
+                                                            reinterpret_cast<const double*>(rw),
+                                                            reinterpret_cast<const double*>(rx), qinvD[prime],
+                                                            false);
+                __syncthreads();
+                NTT_MARK(1 + ri);
+            }
+        }
+    }
+    for (uint32_t ri = 0; ri < ((rowPf || colUnroll) ? 0u : nr); ++ri) {
         const uint32_t r = INV ? nr - 1 - ri : ri;
         const uint32_t k0 = LE * r;
         const int b = (int)min((uint32_t)LE, T.d - k0);
@@ -2223,8 +2246,8 @@ const char* sfp_last_error(sfp_dev* d) {
 
 // ---- NTT ----
 // FP64 butterflies for primes < 2^42 (SFHE_NTT_FP=0 selects the integer path)
-// Bit 3 (SFHE_NTT_ROW_PF=0, an A/B knob) turns off the ROW pass's register
-// twiddle prefetch.
+// A/B knobs for k_ntt: bit 3 (SFHE_NTT_ROW_PF=0) turns off the ROW pass's
+// register twiddle prefetch, bit 4 (SFHE_NTT_COL_UNROLL=0) the unrolled COL rounds.
 static int nttFp() {
     static const int on = [] {
         const char* v = std::getenv("SFHE_NTT_FP");
@@ -2235,7 +2258,8 @@ static int nttFp() {
 static int nttFlags() {
     static const int f = [] {
         const char* pf = std::getenv("SFHE_NTT_ROW_PF");
-        return nttFp() | ((pf && std::atoi(pf) == 0) ? 8 : 0);
+        const char* cu = std::getenv("SFHE_NTT_COL_UNROLL");
+        return nttFp() | ((pf && std::atoi(pf) == 0) ? 8 : 0) | ((cu && std::atoi(cu) == 0) ? 16 : 0);
     }();
     return f;
 }
