@@ -16,7 +16,7 @@ export TMPDIR=/tmp
 # the bench's roofline replay re-instantiates graph nodes; the profiler's
 # rewritten nodes are not replayed (the trace itself gives the durations)
 export SFHE_NO_GRAPH_REPLAY=1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 3 --warmup 1 --trials 0 --no-cpu-baseline --no-hybrid1 --no-kway > gpurun_out/prof_bench.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 3 --warmup 1 --trials 0 --no-cpu-baseline --no-hybrid1 --no-kway --no-c5 > gpurun_out/prof_bench.log 2>&1
 python3 tools/trace_segments.py gpurun_out/prof/run_kernel_trace.csv > gpurun_out/${tag}_rocprof_summary.txt 2>&1
 cp gpurun_out/prof/run_kernel_stats.csv gpurun_out/${tag}_kernel_stats.csv
 timeout -s KILL 170 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcF -o run -- tools/build/microbench 16 > gpurun_out/pmcF.log 2>&1
