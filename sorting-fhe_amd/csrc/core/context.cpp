@@ -1126,8 +1126,11 @@ std::vector<int> CryptoContextImpl<DCRTPoly>::ForkHelpers() {
     SfheContextState* s = st.get();
     std::vector<int> lanes{s->lane};
     // a sharded context issues its collectives in program order on one lane
-    // (LaneCount): no helper lanes, or ranks could order them differently
-    if (!s->dataflow && s->world == 1) {
+    // (LaneCount): no helper lanes, or ranks could order them differently.
+    // Nor while a graph is being captured: the diagnostic helper lanes
+    // (SFHE_PS_LANES) were never made capture-safe (a captured sort with
+    // them crashed on the host), so a capture records the single-lane PS.
+    if (!s->dataflow && s->world == 1 && !s->capturing) {
         s->dataflowParent = s->lane;
         // helpers: lanes that are not primaries of an open batch region
         const int first = s->forkedLanes ? s->forkedLanes : 0;
