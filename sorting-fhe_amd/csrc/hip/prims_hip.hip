@@ -1107,8 +1107,23 @@ __global__ __launch_bounds__(kThreads) void k_lin_wsum_multi(u64* __restrict__ o
                                                              uint32_t logn, const double* __restrict__ qinvD,
                                                              int useFp) {
     __shared__ u64 sk[kWsumChunk * SFP_MAX_WSUM];
+    // blockIdx.x -> (coefficient block, output chunk): every chunk re-streams
+    // the nin inputs of its coefficients, so the chunks of one coefficient
+    // block go to the same XCD (block id = XCD mod 8), 8 ids apart in dispatch
+    // order, and their input reads meet in that XCD's L2
+    const uint32_t chunks = (nout + kWsumChunk - 1) / kWsumChunk;
+    const uint32_t cbs = gridDim.x / chunks;
+    uint32_t cb, chunk;
+    if ((cbs & 7) == 0) {
+        const uint32_t r = blockIdx.x >> 3;
+        chunk = r % chunks;
+        cb = (r / chunks) * 8 + (blockIdx.x & 7);
+    } else {
+        chunk = blockIdx.x % chunks;
+        cb = blockIdx.x / chunks;
+    }
     const uint32_t limb = blockIdx.y;
-    const uint32_t o0 = blockIdx.z * kWsumChunk;
+    const uint32_t o0 = chunk * kWsumChunk;
     const uint32_t oc = min((uint32_t)kWsumChunk, nout - o0);
     for (uint32_t e = threadIdx.x; e < oc * nin; e += kThreads) {
         const uint32_t o = e / nin, j = e % nin;
@@ -1116,7 +1131,7 @@ __global__ __launch_bounds__(kThreads) void k_lin_wsum_multi(u64* __restrict__ o
     }
     __syncthreads();
     const uint32_t n = 1u << logn;
-    const uint32_t x = blockIdx.x * kThreads + threadIdx.x;
+    const uint32_t x = cb * kThreads + threadIdx.x;
     if (x >= n) return;
     const size_t off = ((size_t)limb << logn) + x;
     const uint32_t prime = primeOf(m, limb);
@@ -2660,7 +2675,7 @@ void sfp_lin_wsum_multi(sfp_dev* d, uint64_t* out, size_t outStride, size_t poly
         pl.b[j] = in1[j];
     }
     const u64* dk = (const u64*)ringPut(d, k, (size_t)nout * nin * m.count * 8);
-    const dim3 g(d->n / kThreads, m.count, (nout + kWsumChunk - 1) / kWsumChunk);
+    const dim3 g((d->n / kThreads) * ((nout + kWsumChunk - 1) / kWsumChunk), m.count);
     hipLaunchKernelGGL(k_lin_wsum_multi, g, dim3(kThreads), 0, d->st(), out, outStride, polyStride, pl, dk,
                        nin, nout, m, d->bar, d->logn, d->qinvD, (int)nttFp());
     checkLaunch(d, "lin_wsum_multi");

@@ -1,10 +1,10 @@
-# A/B of the PS helper lanes under graph replay (parity first; every step time-limited)
+# lin_wsum_multi chunk ordering: parity, bench x2, kernel trace (each step time-limited)
 set -e
 mkdir -p gpurun_out
-SFHE_PS_LANES=2 timeout -k 10 300 python -u -m pytest tests/test_gpu_graph.py tests/test_gpu_sort.py -x -q --timeout 120 --timeout-method thread > gpurun_out/ab3_parity.log 2>&1
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_graph.py tests/test_gpu_sort.py -x -q --timeout 120 --timeout-method thread > gpurun_out/ab5_parity.log 2>&1
 B="--steps 5 --warmup 2 --trials 6 --no-cpu-baseline --no-hybrid1 --no-kway --no-c5"
-timeout -k 10 200 python bench.py $B > gpurun_out/ab3_l0.log 2>&1
-SFHE_PS_LANES=1 timeout -k 10 200 python bench.py $B > gpurun_out/ab3_l1.log 2>&1
-SFHE_PS_LANES=2 timeout -k 10 200 python bench.py $B > gpurun_out/ab3_l2.log 2>&1
-timeout -k 10 200 python bench.py $B > gpurun_out/ab3_l0b.log 2>&1
-SFHE_PS_LANES=2 timeout -k 10 200 python bench.py $B > gpurun_out/ab3_l2b.log 2>&1
+timeout -k 10 200 python bench.py $B > gpurun_out/ab5_a.log 2>&1
+timeout -k 10 200 python bench.py $B > gpurun_out/ab5_b.log 2>&1
+SFHE_NO_GRAPH_REPLAY=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof5 -o run -- python3 bench.py --steps 3 --warmup 1 --trials 0 --no-cpu-baseline --no-hybrid1 --no-kway --no-c5 > gpurun_out/prof5_bench.log 2>&1
+python3 tools/trace_segments.py gpurun_out/prof5/run_kernel_trace.csv > gpurun_out/ab5_rocprof_summary.txt 2>&1
