@@ -837,6 +837,8 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_b
     const bool emK = epi && G.emK;
     const u64 emk = emK ? G.emK[ii] : 0, emkS = emK ? G.emKS[ii] : 0;
     const sf_barrett EB = emul ? loadBar(bar, prime) : sf_barrett{};
+    const bool wt = (useFp & 32) != 0;  // SFHE_NTT_WT=1: write-through output stores (A/B knob)
+    const auto orsrc = __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)(n * 8u), 0x00020000);
 #pragma unroll
     for (int k = 0; k < (1 << LE) / 2; ++k) {
         const uint32_t e = 2 * (threadIdx.x + k * (TILE >> LE));
@@ -888,7 +890,19 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_b
                 x.y = sf_add(x.y, sf_mul_shoup(o.y, ek2, ek2S, q), q);
             }
         }
-        *reinterpret_cast<ulonglong2*>(out + g) = x;
+        if (wt) {
+            // write-through (sc1): the pass leaves no dirty L2 lines for the
+            // kernel boundary's writeback
+            typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+            v4u v;
+            v.x = (unsigned)x.x;
+            v.y = (unsigned)(x.x >> 32);
+            v.z = (unsigned)x.y;
+            v.w = (unsigned)(x.y >> 32);
+            __builtin_amdgcn_raw_buffer_store_b128(v, orsrc, (int)(g * 8), 0, 16);
+        } else {
+            *reinterpret_cast<ulonglong2*>(out + g) = x;
+        }
     }
     NTT_MARK(5);
 #ifdef SFHE_NTT_TRACE
@@ -2274,7 +2288,9 @@ static int nttFlags() {
     static const int f = [] {
         const char* pf = std::getenv("SFHE_NTT_ROW_PF");
         const char* cu = std::getenv("SFHE_NTT_COL_UNROLL");
-        return nttFp() | ((pf && std::atoi(pf) == 0) ? 8 : 0) | ((cu && std::atoi(cu) == 0) ? 16 : 0);
+        const char* wt = std::getenv("SFHE_NTT_WT");
+        return nttFp() | ((pf && std::atoi(pf) == 0) ? 8 : 0) | ((cu && std::atoi(cu) == 0) ? 16 : 0) |
+               ((wt && std::atoi(wt) != 0) ? 32 : 0);
     }();
     return f;
 }

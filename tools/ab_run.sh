@@ -1,10 +1,11 @@
-# lin_wsum_multi chunk ordering: parity, bench x2, kernel trace (each step time-limited)
+# NTT write-through stores (SFHE_NTT_WT=1) A/B: parity with the knob on, microbench, bench x2 each
 set -e
 mkdir -p gpurun_out
-export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_graph.py tests/test_gpu_sort.py -x -q --timeout 120 --timeout-method thread > gpurun_out/ab5_parity.log 2>&1
+SFHE_NTT_WT=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_graph.py -x -q --timeout 120 --timeout-method thread > gpurun_out/ab6_parity.log 2>&1
+timeout -k 10 120 tools/build/microbench 16 > gpurun_out/ab6_mb_base.log 2>&1
+SFHE_NTT_WT=1 timeout -k 10 120 tools/build/microbench 16 > gpurun_out/ab6_mb_wt.log 2>&1
 B="--steps 5 --warmup 2 --trials 6 --no-cpu-baseline --no-hybrid1 --no-kway --no-c5"
-timeout -k 10 200 python bench.py $B > gpurun_out/ab5_a.log 2>&1
-timeout -k 10 200 python bench.py $B > gpurun_out/ab5_b.log 2>&1
-SFHE_NO_GRAPH_REPLAY=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof5 -o run -- python3 bench.py --steps 3 --warmup 1 --trials 0 --no-cpu-baseline --no-hybrid1 --no-kway --no-c5 > gpurun_out/prof5_bench.log 2>&1
-python3 tools/trace_segments.py gpurun_out/prof5/run_kernel_trace.csv > gpurun_out/ab5_rocprof_summary.txt 2>&1
+timeout -k 10 200 python bench.py $B > gpurun_out/ab6_base.log 2>&1
+SFHE_NTT_WT=1 timeout -k 10 200 python bench.py $B > gpurun_out/ab6_wt.log 2>&1
+timeout -k 10 200 python bench.py $B > gpurun_out/ab6_base2.log 2>&1
+SFHE_NTT_WT=1 timeout -k 10 200 python bench.py $B > gpurun_out/ab6_wt2.log 2>&1
