@@ -58,7 +58,12 @@ def main():
         if len(s) > 500:
             span = max(r[1] for r in s) - s[0][0]
             print(f"seg {i:3d}: {len(s):6d} kernels, span {span/1e6:8.2f} ms, busy {busy(s)/1e6:8.2f} ms")
-    k = a.seg if a.seg >= 0 else big[-2] if len(big) > 1 else big[-1]
+    # default: the first whole sort -- the first segment with (nearly) the
+    # largest kernel count (a timed sort; later ones may be split by gaps or
+    # followed by other legs' segments)
+    most = max(len(segs[i]) for i in big)
+    whole = [i for i in big if len(segs[i]) >= 0.99 * most]
+    k = a.seg if a.seg >= 0 else whole[0]
     seg = segs[k]
     agg = collections.defaultdict(lambda: [0, 0])
     for s, e, name, *_ in seg:
