@@ -1,0 +1,49 @@
+"""GPU parity of the NTT kernel's A/B variants: each knob is read
+once per process, so every variant runs in a child process that checks
+encrypt / mult / rotate bit for bit against the CPU oracle at ring 2^16,
+where the ROW pass prefetches its twiddles and the COL pass runs unrolled
+rounds by default:
+  SFHE_NTT_ROW_PF=0      ROW rounds load twiddles per round again
+  SFHE_NTT_COL_UNROLL=0  COL rounds in the generic loop
+  SFHE_NTT_WT=1          write-through (sc1) output stores
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r"""
+import numpy as np, sfhe
+kw = dict(mult_depth=4, ring_dim=1 << 16, batch_size=16, scaling_mod_size=40, secure=False,
+          seed=99, rotations=[1, -3])
+g, o = sfhe.Engine("hip", **kw), sfhe.Engine("oracle", **kw)
+rng = np.random.default_rng(5)
+a, b = rng.uniform(-1, 1, 16).tolist(), rng.uniform(-1, 1, 16).tolist()
+outs = []
+for e in (g, o):
+    x, y = e.encrypt(a), e.encrypt(b)
+    m = e.mult(x, y)
+    outs.append([x, m, e.rotate(m, 1), e.rotate(e.mult(m, x), -3)])
+for cg, co in zip(*outs):
+    assert np.array_equal(cg.download(), co.download())
+got = np.array(g.decrypt(outs[0][1]))
+assert np.max(np.abs(got - np.array(a) * np.array(b))) < 1e-6
+print("variant ok")
+"""
+
+
+@pytest.mark.parametrize("env", [{"SFHE_NTT_ROW_PF": "0"}, {"SFHE_NTT_COL_UNROLL": "0"},
+                                 {"SFHE_NTT_WT": "1"}], ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
+def test_ntt_variant_bitexact(hip_lib, oracle_lib, env):
+    child_env = dict(os.environ, **env)
+    child_env["PYTHONPATH"] = os.pathsep.join(
+        [os.path.join(ROOT, "sorting-fhe_amd", "python"), ROOT, child_env.get("PYTHONPATH", "")])
+    r = subprocess.run([sys.executable, "-c", CHILD], cwd=ROOT, env=child_env, capture_output=True,
+                       text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "variant ok" in r.stdout
