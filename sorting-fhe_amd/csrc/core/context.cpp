@@ -220,7 +220,16 @@ void SfheContextState::laneWait(int waiter, int waitee) {
 }
 
 void SfheContextState::dep(DeviceBuffer* b) {
-    if (b && b->lane != lane && synced[lane][b->lane] < b->seq) laneWait(lane, b->lane);
+    if (b && b->lane != lane && synced[lane][b->lane] < b->seq) {
+        static const bool stats = std::getenv("SFHE_LANE_STATS") != nullptr;
+        if (stats && forkedLanes) {
+            ++regionDepWaits;
+            std::fprintf(stderr, "LANEWAIT lane %d waits for lane %d (buffer %zu words, seq %llu > synced %llu)\n",
+                         lane, b->lane, b->words, (unsigned long long)b->seq,
+                         (unsigned long long)synced[lane][b->lane]);
+        }
+        laneWait(lane, b->lane);
+    }
 }
 
 void SfheContextState::wrote(DeviceBuffer* b) {
@@ -1182,6 +1191,12 @@ void CryptoContextImpl<DCRTPoly>::JoinLanes() {
     OpLock g(st.get());
     SfheContextState* s = st.get();
     if (!s->forkedLanes) return;
+    static const bool stats = std::getenv("SFHE_LANE_STATS") != nullptr;
+    if (stats) {
+        std::fprintf(stderr, "LANESTATS region %d: %llu data-dependency waits across lanes\n", s->region,
+                     (unsigned long long)s->regionDepWaits);
+        s->regionDepWaits = 0;
+    }
     for (int i = 1; i < s->forkedLanes; ++i) s->laneWait(0, i);
     sfp_set_lane(s->dev, 0);
     std::lock_guard<std::mutex> pg(s->poolMu);

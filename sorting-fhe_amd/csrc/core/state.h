@@ -93,6 +93,9 @@ struct SfheContextState {
     // synced[h][x] = laneSeq[x] at the last time lane h waited for lane x
     uint64_t laneSeq[SFP_MAX_LANES] = {};
     uint64_t synced[SFP_MAX_LANES][SFP_MAX_LANES] = {};
+    // SFHE_LANE_STATS (diagnostic): data-dependency waits (dep) issued inside
+    // fork/join regions, printed at each JoinLanes
+    uint64_t regionDepWaits = 0;
     void laneWait(int waiter, int waitee);
     int myLane() const;            // the calling thread's lane (0 unless SetLane)
     void setMyLane(int l);

@@ -81,6 +81,30 @@ int main(int argc, char** argv) {
                     bytes / i / 1e3);
         printTrace(d);
     }
+    // Lane concurrency: K forward NTTs on lane 0 alone, then K on each of
+    // lanes 0 and 1 (independent buffers, issued alternately).  ratio = the
+    // two-lane time / the one-lane time: 1.0 = the lanes overlap fully, 2.0 =
+    // they serialise (the sort's two batches are such lanes).
+    if (sfp_lanes(d) >= 2) {
+        std::printf("%-10s %6s %10s %10s %8s\n", "lanes", "rows", "1 lane us", "2 lanes us", "ratio");
+        for (uint32_t rows : {1u, 4u, 8u, 16u, 35u}) {
+            if (rows > NP || 2 * rows > maxRows) continue;
+            const sfp_limbs m{rows, rows, 0, 0};
+            uint64_t* b1 = buf + (size_t)(maxRows / 2) * n;
+            const double one = timeIt(d, 50, [&] {
+                sfp_set_lane(d, 0);
+                sfp_ntt(d, buf, m, 0);
+            });
+            const double two = timeIt(d, 50, [&] {
+                sfp_set_lane(d, 0);
+                sfp_ntt(d, buf, m, 0);
+                sfp_set_lane(d, 1);
+                sfp_ntt(d, b1, m, 0);
+            });
+            sfp_set_lane(d, 0);
+            std::printf("%-10s %6u %10.2f %10.2f %8.2f\n", "ntt", rows, one, two, two / one);
+        }
+    }
     // key switch pieces at the top level (ell = Lq)
     const uint32_t ell = s->Lq, K = s->K, beta = (ell + s->alpha - 1) / s->alpha;
     const size_t stride = (size_t)(ell + K) * n;
