@@ -1426,8 +1426,14 @@ template <int NS>
 __global__ __launch_bounds__(kThreads) void k_convf(const ConvJobs J, const sf_barrett* __restrict__ bar,
                                                     const double* __restrict__ qinvD, uint32_t logn) {
     constexpr int C = kConvChunk, NB = kMaxConvBig, X = kConvCoefs, WAVES = kThreads / 64;
-    __shared__ double sD[NS * C], sQ[NS * C], hDs[NB * C], hQs[NB * C];
-    __shared__ u64 smod[NS * C];
+    // FP64 blocks use the multipliers (sD, sQ), integer blocks the residues
+    // (smod): one LDS region serves both (4 KB less per block at NS = 16:
+    // 5 blocks per CU instead of 4)
+    __shared__ double sDQ[2 * NS * C];
+    double* const sD = sDQ;
+    double* const sQ = sDQ + NS * C;
+    u64* const smod = reinterpret_cast<u64*>(sDQ);
+    __shared__ double hDs[NB * C], hQs[NB * C];
     __shared__ sf_barrett sB[NS], tB[C];
     __shared__ double sInvD[NS], sInvQ[NS], sQi[NS], tQi[C];
     __shared__ u64 sInv[NS], tSp[C];
@@ -1650,8 +1656,12 @@ template <int NS>
 __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_barrett* __restrict__ bar,
                                                     const double* __restrict__ qinvD, uint32_t logn) {
     constexpr int C = kConvChunk, X = kConvCoefs, WAVES = kThreads / 64;
-    __shared__ double sD[NS * C], sQ[NS * C], sLD[NS], sLQ[NS];
-    __shared__ u64 smod[NS * C];
+    // one LDS region for the FP64 multipliers or the integer residues (as k_convf)
+    __shared__ double sDQ[2 * NS * C];
+    double* const sD = sDQ;
+    double* const sQ = sDQ + NS * C;
+    u64* const smod = reinterpret_cast<u64*>(sDQ);
+    __shared__ double sLD[NS], sLQ[NS];
     __shared__ sf_barrett sB[NS], tB[C];
     __shared__ double sInvD[NS], sInvQ[NS], sQi[NS], tQi[C], tPd[C], tPq[C];
     __shared__ u64 tSp[C], tPm[C], tLs[C];
@@ -3001,6 +3011,15 @@ static ConvJob convJob(const sfp_conv* c, u64* dst, const u64* src, uint32_t ntU
     return j;
 }
 
+// SFHE_CONV_NS13=0 (A/B knob): every FP64 conversion on the NS = 16 kernels
+static bool convNs13() {
+    static const bool on = [] {
+        const char* v = std::getenv("SFHE_CONV_NS13");
+        return !(v && std::atoi(v) == 0);
+    }();
+    return on;
+}
+
 static void convLaunch(sfp_dev* d, const ConvJobs& J, uint32_t njobs, bool fpOk) {
     if (!njobs) return;
     uint32_t maxT = 0, maxS = 0, maxZ = 0;
@@ -3017,7 +3036,11 @@ static void convLaunch(sfp_dev* d, const ConvJobs& J, uint32_t njobs, bool fpOk)
     if (!gz) return;
     const dim3 g(fp ? d->n / kConvCoefs : d->n / (2 * kThreads), njobs, gz);
     timedLaunch(d, SFP_FAM_CONV, bytes, [&] {
-        if (fp && maxS <= 16)
+        // NS = 13 (ModDown's K P-rows, ModUp digits of <= 13 primes) sizes the
+        // LDS for 6 blocks per CU instead of 5 (the loops keep their guards)
+        if (fp && maxS <= 13 && convNs13())
+            hipLaunchKernelGGL(k_convf<13>, g, dim3(kThreads), 0, d->st(), J, d->bar, d->qinvD, d->logn);
+        else if (fp && maxS <= 16)
             hipLaunchKernelGGL(k_convf<16>, g, dim3(kThreads), 0, d->st(), J, d->bar, d->qinvD, d->logn);
         else if (fp)
             hipLaunchKernelGGL(k_convf<kMaxConvSrc>, g, dim3(kThreads), 0, d->st(), J, d->bar, d->qinvD, d->logn);
@@ -3193,7 +3216,9 @@ void sfp_moddown_rescale(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint6
     }
     const dim3 g(fp ? n / kConvCoefs : n / (2 * kThreads), 2, zc);
     timedLaunch(d, SFP_FAM_CONV, 8.0 * n * 2 * (K + 1 + l), [&] {
-        if (fp && c->ns <= 16)
+        if (fp && c->ns <= 13 && convNs13())  // LDS for 6 blocks per CU (as convLaunch)
+            hipLaunchKernelGGL(k_mdrsf<13>, g, dim3(kThreads), 0, d->st(), M, d->bar, d->qinvD, d->logn);
+        else if (fp && c->ns <= 16)
             hipLaunchKernelGGL(k_mdrsf<16>, g, dim3(kThreads), 0, d->st(), M, d->bar, d->qinvD, d->logn);
         else if (fp)
             hipLaunchKernelGGL(k_mdrsf<kMaxConvSrc>, g, dim3(kThreads), 0, d->st(), M, d->bar, d->qinvD, d->logn);
