@@ -1139,19 +1139,29 @@ __global__ __launch_bounds__(kThreads) void k_lin_wsum_multi(u64* __restrict__ o
     const uint32_t limb = blockIdx.y;
     const uint32_t o0 = chunk * kWsumChunk;
     const uint32_t oc = min((uint32_t)kWsumChunk, nout - o0);
+    // FP64 rows also stage each weight as (w, w/q) doubles: the product loop
+    // then neither converts nor rescales a weight per coefficient
+    __shared__ double skD[kWsumChunk * SFP_MAX_WSUM], skQ[kWsumChunk * SFP_MAX_WSUM];
+    const uint32_t prime = primeOf(m, limb);
+    const u64 qq = bar[prime].q;
+    const bool fpRow = useFp && qq < kFpPrimeBound;  // uniform per block
+    const double qi = fpRow ? qinvD[prime] : 0.0;
     for (uint32_t e = threadIdx.x; e < oc * nin; e += kThreads) {
         const uint32_t o = e / nin, j = e % nin;
-        sk[o * SFP_MAX_WSUM + j] = k[((size_t)(o0 + o) * nin + j) * m.count + limb];
+        const u64 w = k[((size_t)(o0 + o) * nin + j) * m.count + limb];
+        sk[o * SFP_MAX_WSUM + j] = w;
+        if (fpRow) {
+            skD[o * SFP_MAX_WSUM + j] = (double)w;
+            skQ[o * SFP_MAX_WSUM + j] = (double)w * qi;
+        }
     }
     __syncthreads();
     const uint32_t n = 1u << logn;
     const uint32_t x = cb * kThreads + threadIdx.x;
     if (x >= n) return;
     const size_t off = ((size_t)limb << logn) + x;
-    const uint32_t prime = primeOf(m, limb);
-    const u64 qq = bar[prime].q;
-    if (useFp && qq < kFpPrimeBound) {  // uniform per block: FP64 products (fpMulMod), exact
-        const double qd = (double)qq, qi = qinvD[prime];
+    if (fpRow) {  // FP64 products (fpMulMod), exact
+        const double qd = (double)qq;
         double f0[kWsumChunk], f1[kWsumChunk];
 #pragma unroll
         for (int o = 0; o < kWsumChunk; ++o) f0[o] = f1[o] = 0.0;
@@ -1160,7 +1170,7 @@ __global__ __launch_bounds__(kThreads) void k_lin_wsum_multi(u64* __restrict__ o
 #pragma unroll
             for (int o = 0; o < kWsumChunk; ++o) {
                 if ((uint32_t)o < oc) {
-                    const double w = (double)sk[o * SFP_MAX_WSUM + j], wq = w * qi;
+                    const double w = skD[o * SFP_MAX_WSUM + j], wq = skQ[o * SFP_MAX_WSUM + j];
                     f0[o] += fpMulMod(v0, w, wq, qd);
                     f1[o] += fpMulMod(v1, w, wq, qd);
                 }
