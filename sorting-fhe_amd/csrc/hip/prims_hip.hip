@@ -490,7 +490,7 @@ __device__ __forceinline__ double fpReduce(double v, double q, double qinv) {
 template <bool INV, bool COL, int LE, int B, int TILE, bool PF = false, int DC = 0>
 __device__ __forceinline__ void nttRoundFP(double* s, const NttTile& T, uint32_t S0, uint32_t k0, double q,
                                            const double* w, const double* wq, double qinv, bool rowLds,
-                                           const double* pw = nullptr) {
+                                           const double* pw = nullptr, bool wqCalc = false) {
     constexpr int M = 1 << B;
     constexpr int GPT = (1 << LE) / M;
     const uint32_t d = DC ? (uint32_t)DC : T.d;
@@ -534,7 +534,7 @@ __device__ __forceinline__ void nttRoundFP(double* s, const NttTile& T, uint32_t
                     // ROW twiddles come from HBM: form W/q here (half the bytes).  A
                     // last-bit difference from the table only moves the lazy
                     // quotient estimate by < 2^-6; outputs are canonical either way.
-                    WQ[(1 << t) - 1 + qd] = COL ? wq[tb + qd] : W[(1 << t) - 1 + qd] * qinv;
+                    WQ[(1 << t) - 1 + qd] = (COL && !wqCalc) ? wq[tb + qd] : W[(1 << t) - 1 + qd] * qinv;
                 }
             }
         }
@@ -577,15 +577,15 @@ __device__ __forceinline__ void nttRoundFP(double* s, const NttTile& T, uint32_t
 template <bool INV, bool COL, int LE, int TILE>
 __device__ __forceinline__ void nttRoundDynFP(int b, double* s, const NttTile& T, uint32_t S0, uint32_t k0,
                                               double q, const double* w, const double* wq, double qinv,
-                                              bool rowLds) {
+                                              bool rowLds, bool wqCalc) {
     if constexpr (LE >= 4) {
-        if (b == 4) return nttRoundFP<INV, COL, LE, 4, TILE>(s, T, S0, k0, q, w, wq, qinv, rowLds);
+        if (b == 4) return nttRoundFP<INV, COL, LE, 4, TILE>(s, T, S0, k0, q, w, wq, qinv, rowLds, nullptr, wqCalc);
     }
     if constexpr (LE >= 3) {
-        if (b == 3) return nttRoundFP<INV, COL, LE, 3, TILE>(s, T, S0, k0, q, w, wq, qinv, rowLds);
+        if (b == 3) return nttRoundFP<INV, COL, LE, 3, TILE>(s, T, S0, k0, q, w, wq, qinv, rowLds, nullptr, wqCalc);
     }
-    if (b == 2) return nttRoundFP<INV, COL, LE, 2, TILE>(s, T, S0, k0, q, w, wq, qinv, rowLds);
-    nttRoundFP<INV, COL, LE, 1, TILE>(s, T, S0, k0, q, w, wq, qinv, rowLds);
+    if (b == 2) return nttRoundFP<INV, COL, LE, 2, TILE>(s, T, S0, k0, q, w, wq, qinv, rowLds, nullptr, wqCalc);
+    nttRoundFP<INV, COL, LE, 1, TILE>(s, T, S0, k0, q, w, wq, qinv, rowLds, nullptr, wqCalc);
 }
 
 
@@ -683,10 +683,14 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_b
     // the pass's twiddle table (value, Shoup companion or W/q) for this prime
     const u64* gw = fp ? reinterpret_cast<const u64*>(twD) + (size_t)prime * n : tw + (size_t)prime * n;
     const u64* gx = fp ? reinterpret_cast<const u64*>(twQ) + (size_t)prime * n : twS + (size_t)prime * n;
+    // FP64 COL rounds form W/q from W (as the ROW rounds do) instead of
+    // staging the table's W/q: half the twiddle loads of the prologue
+    // (useFp bit 6, SFHE_NTT_COL_WQ=0, stages the table for A/B runs)
+    const bool wqCalc = COL && fp && !(useFp & 64);
     if (COL) {  // entries [1, 2^logR) -> LDS
         for (uint32_t e = threadIdx.x; e < (1u << logR) - 1; e += (TILE >> LE)) {
             tW[e] = gw[e + 1];
-            tX[e] = gx[e + 1];
+            if (!wqCalc) tX[e] = gx[e + 1];
         }
     }
     const bool rowLds = kNttRowLdsBuild && !COL && fp && (useFp & 7) >= 2;
@@ -806,7 +810,7 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_b
                 nttRoundFP<INV, true, 2, 2, TILE, false, 8>(reinterpret_cast<double*>(s), T, S0, 2 * r, (double)q,
                                                             reinterpret_cast<const double*>(rw),
                                                             reinterpret_cast<const double*>(rx), qinvD[prime],
-                                                            false);
+                                                            false, nullptr, wqCalc);
                 __syncthreads();
                 NTT_MARK(1 + ri);
             }
@@ -819,7 +823,7 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_b
         if (fp)
             nttRoundDynFP<INV, COL, LE, TILE>(b, reinterpret_cast<double*>(s), T, S0, k0, (double)q,
                                         reinterpret_cast<const double*>(rw), reinterpret_cast<const double*>(rx),
-                                        qinvD[prime], rowLds);
+                                        qinvD[prime], rowLds, wqCalc);
         else
             nttRoundDyn<INV, COL, LE, TILE>(b, s, T, S0, k0, q, rw, rx);
         __syncthreads();
@@ -2309,8 +2313,9 @@ static int nttFlags() {
         const char* pf = std::getenv("SFHE_NTT_ROW_PF");
         const char* cu = std::getenv("SFHE_NTT_COL_UNROLL");
         const char* wt = std::getenv("SFHE_NTT_WT");
+        const char* cq = std::getenv("SFHE_NTT_COL_WQ");
         return nttFp() | ((pf && std::atoi(pf) == 0) ? 8 : 0) | ((cu && std::atoi(cu) == 0) ? 16 : 0) |
-               ((wt && std::atoi(wt) != 0) ? 32 : 0);
+               ((wt && std::atoi(wt) != 0) ? 32 : 0) | ((cq && std::atoi(cq) == 0) ? 64 : 0);
     }();
     return f;
 }

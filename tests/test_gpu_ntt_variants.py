@@ -6,6 +6,7 @@ rounds by default:
   SFHE_NTT_ROW_PF=0      ROW rounds load twiddles per round again
   SFHE_NTT_COL_UNROLL=0  COL rounds in the generic loop
   SFHE_NTT_WT=1          write-through (sc1) output stores
+  SFHE_NTT_COL_WQ=0      COL rounds read the staged W/q table instead of forming it
 """
 import os
 import subprocess
@@ -38,7 +39,7 @@ print("variant ok")
 
 
 @pytest.mark.parametrize("env", [{"SFHE_NTT_ROW_PF": "0"}, {"SFHE_NTT_COL_UNROLL": "0"},
-                                 {"SFHE_NTT_WT": "1"}], ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
+                                 {"SFHE_NTT_WT": "1"}, {"SFHE_NTT_COL_WQ": "0"}], ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
 def test_ntt_variant_bitexact(hip_lib, oracle_lib, env):
     child_env = dict(os.environ, **env)
     child_env["PYTHONPATH"] = os.pathsep.join(
