@@ -220,7 +220,8 @@ def c5_leg(device, world=1, rank=0, steps=2):
     reference point).  world > 1: the ranks LIMB-SHARD one sort over RCCL
     (SURVEY §8(e)): per-sort wall-clock at W GPUs.  Run after the replica
     measurement, as an extra field; a watchdog (SFHE_C5_TIMEOUT s, default
-    240) prints the line without it and exits if the collective path stalls."""
+    240) prints the line without it and exits with status 2 if the collective
+    path stalls."""
     import numpy as np
     N, logn, secure = WORKLOADS["directsort_n256_2e17"]
     depth, rots = sfhe.direct_sort_params(N, "hip")
@@ -464,11 +465,13 @@ def main(argv=None):
     if args.c5 and not shard:
         import threading
 
-        def stalled():  # the collective path hung: report what was measured and leave
+        def stalled():  # the collective path hung: report what was measured, then fail loudly
             if rank == 0:
-                result["c5"] = {"error": f"timeout after {limit:.0f} s"}
+                result["c5"] = {"error": f"timeout after {limit:.0f} s (collective stalled)"}
                 print(json.dumps(result), flush=True)
-            os._exit(0)
+            sys.stderr.write(f"bench: c5 leg stalled after {limit:.0f} s\n")
+            sys.stderr.flush()
+            os._exit(2)
         limit = float(os.environ.get("SFHE_C5_TIMEOUT", "240"))
         dog = threading.Timer(limit, stalled)
         dog.daemon = True

@@ -200,6 +200,23 @@ int sfhe_sorter_sort_hybrid1(sfhe_sorter* s, sfhe_ct* in, int n, int dg, int df,
 /* Depth and rotation keys of tests/DirectSortH1Test.cpp:36-117 for N
  * (the reference keeps them in the test; ring 2^17, HEStd_128_classic). */
 int sfhe_hybrid1_params(uint32_t N, uint32_t* mult_depth, int32_t* rotations, size_t cap, size_t* count);
+
+/* DirectSort<N>::sort_hybrid (variant 0; sort_algo.h:1049-1062) and
+ * sort_hybrid2 (variant 2; :1376-1389): constructRank, then the MEHP24 matrix
+ * placement on rank / N with the scaled-sinc Chebyshev indicator (hybrid2;
+ * hybrid below N = 256) or the composite-sign indicator |d| < 1/2N (hybrid at
+ * N >= 256: CompositeSign(3,4,2) at 256, (3,5,2) above; rotationIndexCheck-
+ * Hybrid :894-1047, -Hybrid2 :1233-1374).  Needs 2 N^2 <= the ring
+ * dimension for N <= 256 and the keys of sfhe_hybrid_params. */
+int sfhe_sorter_sort_hybrid(sfhe_sorter* s, sfhe_ct* in, int variant, int n, int dg, int df, sfhe_ct** out);
+/* the DirectSortHTest (variant 0, tests/DirectSortHTest.cpp:29-100) and
+ * DirectSortH2Test (variant 2, tests/DirectSortH2Test.cpp:39-108) depth and
+ * rotation keys at ring 2^17 */
+int sfhe_hybrid_params(uint32_t N, int variant, uint32_t* mult_depth, int32_t* rotations, size_t cap,
+                       size_t* count);
+/* DirectSort<N>::rotationIndexCheck2N (sort_algo.h:587-656): placement over
+ * 2N-slot blocks with the scaled sinc (rank from sfhe_sorter_rank). */
+int sfhe_sorter_place_2n(sfhe_sorter* s, const sfhe_ct* rank, sfhe_ct* in, sfhe_ct** out);
 /* BitonicSort<N>::sort (sort_algo.h:1421-1486): the compare-and-swap network
  * over the sorter's N slots with EvalBootstrap(ct, 2, 20) whenever the level
  * passes 29 -- needs sfhe_bootstrap_setup for N slots and the +-2^i keys the

@@ -24,6 +24,7 @@
  * reference's test vectors and gates in tests/golden/ 
  * and serves as the bit-exact cross-check of the HIP kernels.
  */
+#include <math.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -389,27 +390,42 @@ void sfp_free_conv(sfp_dev* d, sfp_conv* c) {
 }
 
 /* dst row t (prime c->dst[t]) = sum_i [src_i * inv_i]_{s_i} * mod[i][t]  (coefficient domain).
- * centered: each y_i is taken in (-s_i/2, s_i/2], i.e. y_i - s_i when y_i > s_i/2, which
- * subtracts prod(S) mod t once per such i; the conversion error sum_i y_i/s_i is then
- * zero-mean (ModDown rounds instead of flooring with a +K/2 bias). */
+ * centered: the EXACT centred conversion (ModDown).  Each y_i is taken in
+ * (-s_i/2, s_i/2], and the overflow v = round(sum_i y_i / s_i) is removed:
+ *   out_t = sum_i y_i * mod[i][t] - v * prod(S)   (mod t),
+ * which is the centred representative of x mod prod(S) itself, so ModDown's
+ * division by P leaves only its rounding (|x / P| <= 1/2) instead of the fast
+ * conversion's integer overflow v (variance ~K/12: ~sqrt(K+1) x the noise).
+ * v is estimated in FP64 exactly as the HIP kernels do it (same operations,
+ * same order): acc = fma((double)y_i, 1.0 / (double)s_i, acc), v = rint(acc). */
 static void conv_rows(const sfp_dev* d, const sfp_conv* c, const u64* src, u64* const* dstRows,
                       uint32_t ntUse, int centered) {
     const uint32_t n = d->n;
 #pragma omp parallel for schedule(static)
     for (uint32_t x = 0; x < n; ++x) {
         u64 y[SFP_MAX_LIMBS];
-        u64 neg = 0;
+        int64_t m = 0; /* multiples of prod(S) to subtract: one per negative y_i, plus v */
+        double acc = 0.0;
         for (uint32_t i = 0; i < c->ns; ++i) {
             u64 qi = d->q[c->src[i]];
             y[i] = mm(src[(size_t)i * n + x], c->inv[i], qi);
-            if (centered && y[i] > (qi >> 1)) ++neg;
+            if (centered) {
+                int64_t yc = (int64_t)y[i];
+                if (y[i] > (qi >> 1)) {
+                    ++m;
+                    yc -= (int64_t)qi;
+                }
+                acc = fma((double)yc, 1.0 / (double)qi, acc);
+            }
         }
+        if (centered) m += (int64_t)rint(acc);
         for (uint32_t t = 0; t < ntUse; ++t) {
             u64 pt = d->q[c->dst[t]];
-            u128 acc = 0;
-            for (uint32_t i = 0; i < c->ns; ++i) acc += (u128)y[i] * c->mod[(size_t)i * c->nt + t];
-            u64 v = (u64)(acc % pt);
-            if (neg) v = sb(v, mm(neg, c->sprod[t], pt), pt);
+            u128 a = 0;
+            for (uint32_t i = 0; i < c->ns; ++i) a += (u128)y[i] * c->mod[(size_t)i * c->nt + t];
+            u64 v = (u64)(a % pt);
+            if (m > 0) v = sb(v, mm((u64)m, c->sprod[t], pt), pt);
+            if (m < 0) v = ad(v, mm((u64)(-m), c->sprod[t], pt), pt);
             dstRows[t][x] = v;
         }
     }

@@ -9,6 +9,7 @@ reference evaluates.  Restated from:
   src/sort_algo.h:326-366  vecRotsOpt          src/sort_algo.h:368-506 constructRank
   src/sort_algo.h:561-584  blindRotationOptN   src/sort_algo.h:658-750 rotationIndexCheckN
   src/comparison.cpp:4-22  compare             src/sign.cpp:9-185 composite sign
+  src/sort_algo.h:894-1062, :1067-1229, :1233-1389  the hybrid placements
   tests/utils.h:28-51      getVectorWithMinDiff (seeded instead of random_device)
 """
 from __future__ import annotations
@@ -229,3 +230,55 @@ def sort_hybrid1(x, N, ring, cfg=None):
     cfg = cfg or default_sign_config(N)
     rank = construct_rank(np.asarray(x, dtype=np.float64), N, ring, cfg)
     return rotation_index_check_hybrid1(rank, np.asarray(x, dtype=np.float64), N, ring), rank
+
+
+# ---- hybrid placements with rank / N (src/sort_algo.h:894-1062 sort_hybrid,
+# :1233-1389 sort_hybrid2); src/comparison.cpp:24-40 (Comparison::indicator) ----
+def indicator(x, c: float, cfg):
+    """step(x + c) * (1 - step(x - c)), step(d) = (sign(d) + 1) / 2."""
+    step = lambda d: (composite_sign(d, *cfg) + 1.0) * 0.5  # noqa: E731
+    return step(np.asarray(x) + c) * (1.0 - step(np.asarray(x) - c))
+
+
+def hybrid_depth(N: int, variant: int, cfg=None) -> int:
+    """hybrid / hybrid2 depth tables."""
+    n, dg, df = cfg or default_sign_config(N)
+    rank = 2 + sign_depth(n, dg, df)
+    ps = cheb.ps_depth(len(cheb.scaled_sinc_coeffs(N)) - 1)
+    if variant == 2 or N < 256:
+        return rank + 1 + ps + 3
+    dgi = 4 if N < 512 else 5
+    return rank + 1 + (3 * (dgi + 2) + 2) + 3
+
+
+def rotation_index_check_hybrid(rank, x, N, ring, variant: int):
+    maxa = 256
+    num_slots, num_batch = (ring // 2, N // maxa) if N > maxa else (N * N, 1)
+    M = min(N, maxa)
+    r = np.tile(np.asarray(rank, dtype=np.float64), num_slots // N) / N
+    xs = np.tile(np.asarray(x, dtype=np.float64), num_slots // N)
+    rots_rank = [rot(r, k * maxa) for k in range(num_batch)]
+    rots_in = [rot(xs, k * maxa) for k in range(num_batch)]
+    coeffs = cheb.scaled_sinc_coeffs(N)
+    out = np.zeros(num_slots)
+    for b in range(num_batch):
+        sub = np.zeros(num_slots)
+        for i in range(M):
+            sub[i * M:(i + 1) * M] = (b * M + i) / N
+        acc = np.zeros(num_slots)
+        for k in range(num_batch):
+            d = sub - rots_rank[k]
+            if variant == 2 or N < 256:
+                ind = cheb.cheb_eval(coeffs, d)
+            else:
+                ind = indicator(d, 0.5 / N, (3, 4 if N < 512 else 5, 2))
+            acc = acc + rots_in[k] * ind
+        acc = sum_columns_to_target(acc, N // num_batch, b)
+        out = out + transpose_column_target(acc, N // num_batch, b)
+    return out[:N]
+
+
+def sort_hybrid(x, N, ring, variant: int = 0, cfg=None):
+    cfg = cfg or default_sign_config(N)
+    rank = construct_rank(np.asarray(x, dtype=np.float64), N, ring, cfg)
+    return rotation_index_check_hybrid(rank, np.asarray(x, dtype=np.float64), N, ring, variant), rank

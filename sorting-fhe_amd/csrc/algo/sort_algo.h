@@ -158,6 +158,17 @@ inline bool sincRebase() {
     return !v || *v != '0';
 }
 
+// constructRank moves the self comparison off the sign's steep point (on
+// unless SFHE_SELF_OFFSET=0, which computes step(0) = 1/2 as the reference).
+constexpr double kSelfOffset = 0.5;
+inline bool selfOffset() {
+    static const bool on = [] {
+        const char* v = std::getenv("SFHE_SELF_OFFSET");
+        return !v || *v != '0';
+    }();
+    return on;
+}
+
 // SFHE_PHASES=1: device-synchronised wall time of each sort phase on stderr
 // (diagnostics only; adds synchronisation, so never on in benchmarks).
 class PhaseTimer {
@@ -336,6 +347,15 @@ class DirectSort : public SortBase<N> {
 
         auto rank = this->getZero()->Clone();
         rank->SetSlots(L.S);
+        // The self comparison x_r vs x_r sits in partition 0 of batch 0
+        // (shift 0).  Its difference is pure CKKS noise at the composite
+        // sign's steepest point (slope ~ 4.5^dg), which made it the largest
+        // term of the rank error (~1e-4 at N=256).  The engine moves those N
+        // slots' difference to +selfOffset (an exact plaintext addition), where
+        // the sign is saturated: the term contributes 1 instead of 1/2 and the
+        // final correction is -1 instead of the reference's -1/2 (:503-504).
+        // Same rank up to the sign's approximation error; DESIGN.md §2.
+        const bool offsetSelf = sfhe::selfOffset();
         // the batches are independent: each runs on its own lane (stream)
         std::vector<Ciphertext<DCRTPoly>> parts(L.B);
         const int lanes = std::min(L.B, m_cc->LaneCount());
@@ -344,6 +364,14 @@ class DirectSort : public SortBase<N> {
             auto shifted = vecRotsOpt(pre, L.P, L.S, L.npRank, b);
             auto dup = input_array->Clone();
             dup->SetSlots(L.S);
+            if (b == 0 && offsetSelf) {
+                const Plaintext& off = maskMemo({7, 0, 0, (int)dup->GetLevel(), L.S}, [&](auto& v) {
+                    std::vector<double> o(L.S, 0.0);
+                    std::fill(o.begin(), o.begin() + N, sfhe::kSelfOffset);
+                    v.push_back(m_cc->MakeCKKSPackedPlaintext(o, 1, dup->GetLevel(), nullptr, L.S));
+                })[0];
+                dup = m_cc->EvalAdd(dup, off);
+            }
             parts[b] = comp.compare(m_cc, dup, shifted, SignFunc, Cfg);
         });
         m_cc->JoinLanes();
@@ -353,8 +381,8 @@ class DirectSort : public SortBase<N> {
         for (int s = L.S / 2; s >= N; s /= 2) m_cc->EvalAddInPlace(rank, rot.rotate(rank, s));
         ph.mark("rank: folds");
         rank->SetSlots(N);
-        // remove the self comparison step(0) = 1/2
-        return m_cc->EvalSub(rank, 0.5);
+        // remove the self comparison: step(selfOffset) = 1 (reference: step(0) = 1/2)
+        return m_cc->EvalSub(rank, offsetSelf ? 1.0 : 0.5);
     }
 
     // Rotates partition k = np*i + j of the masked inputs left by ib*P + k.
@@ -493,44 +521,48 @@ class DirectSort : public SortBase<N> {
         return c;
     }
 
-    Ciphertext<DCRTPoly> rotationIndexCheckHybrid1(const Ciphertext<DCRTPoly>& ctx_Rank,
-                                                   const Ciphertext<DCRTPoly>& input_array,
-                                                   PrivateKey<DCRTPoly> sk) {
-        (void)sk;  // (unused by the reference as well)
+    // The MEHP24 matrix placement shared by the three hybrid sorts (reference
+    // :894-1062 hybrid, :1067-1229 hybrid1, :1233-1389 hybrid2): with
+    // M = min(N, 256) and num_slots = M*M per batch (the whole ring above 256),
+    // slot (i, j) of batch b holds ind(sub_b(i) - rank_{(j + kM) mod N}) *
+    // x_{(j + kM) mod N} summed over the rank rotations k; the row sums land
+    // in column b (sumColumnsToTarget), that column becomes row b
+    // (transposeColumnTarget), and the sum over batches holds the sorted array
+    // in its first N slots.  `rank` is the (possibly 1/N-scaled) rank,
+    // sub_b(i) = subScale (b M + i), `ind` the indicator of each variant.
+    template <class Ind>
+    Ciphertext<DCRTPoly> matrixPlacement(const Ciphertext<DCRTPoly>& rank, const Ciphertext<DCRTPoly>& input_array,
+                                         double subScale, int memoTag, Ind&& ind) {
         constexpr size_t maxArraySize = 256;
         const size_t num_slots = N > (int)maxArraySize ? (size_t)max_batch : (size_t)N * N;
         const size_t num_batch = N > (int)maxArraySize ? N / maxArraySize : 1;
         const size_t M = std::min((size_t)N, maxArraySize);
         if (num_slots > (size_t)max_batch || M * M > num_slots)
-            throw OpenFHEException("sort_hybrid1: N*N slots exceed the ring (needs ring dimension >= 2 N^2)");
-        ctx_Rank->SetSlots((uint32_t)num_slots);
+            throw OpenFHEException("hybrid sort: N*N slots exceed the ring (needs ring dimension >= 2 N^2)");
+        rank->SetSlots((uint32_t)num_slots);
         input_array->SetSlots((uint32_t)num_slots);
         std::vector<Ciphertext<DCRTPoly>> rots_Rank(num_batch), rots_Input(num_batch);
         for (size_t k = 0; k < num_batch; ++k) {
-            rots_Rank[k] = rot.rotate(ctx_Rank, (int)(k * maxArraySize));
+            rots_Rank[k] = rot.rotate(rank, (int)(k * maxArraySize));
             rots_Input[k] = rot.rotate(input_array, (int)(k * maxArraySize));
         }
-        // dg_i = (log2 N + 1) / 2 truncated (reference :1126-1127)
-        const uint32_t dg_i = (uint32_t)((std::log2((double)N) + 1) / 2);
-        const uint32_t df_i = 2;
         std::vector<Ciphertext<DCRTPoly>> Masked(num_batch);
         const int lanes = std::min((int)num_batch, m_cc->LaneCount());
         m_cc->ForkLanes(lanes);
         sfhe::parallelLanes(m_cc, lanes, (int)num_batch, [&](int bi) {
             const size_t b = (size_t)bi;
-            // subMask_b[i M + j] = b M + i (reference :1089-1098)
-            const Plaintext& subMask = maskMemo({6, bi, 0, (int)ctx_Rank->GetLevel(), (int)num_slots}, [&](auto& v) {
-                std::vector<double> m(num_slots, 0.0);
-                for (size_t i = 0; i < M; ++i)
-                    for (size_t j = 0; j < M; ++j) m[i * M + j] = (double)(b * M + i);
-                v.push_back(m_cc->MakeCKKSPackedPlaintext(m, 1, ctx_Rank->GetLevel(), nullptr,
-                                                          (uint32_t)num_slots));
-            })[0];
+            // subMask_b[i M + j] = subScale (b M + i) (reference :1089-1098, :929-939)
+            const Plaintext& subMask =
+                maskMemo({memoTag, bi, 0, (int)rank->GetLevel(), (int)num_slots}, [&](auto& v) {
+                    std::vector<double> m(num_slots, 0.0);
+                    for (size_t i = 0; i < M; ++i)
+                        for (size_t j = 0; j < M; ++j) m[i * M + j] = subScale * (double)(b * M + i);
+                    v.push_back(m_cc->MakeCKKSPackedPlaintext(m, 1, rank->GetLevel(), nullptr, (uint32_t)num_slots));
+                })[0];
             auto subMasked = this->getZero()->Clone();
             subMasked->SetSlots((uint32_t)num_slots);
             for (size_t k = 0; k < num_batch; ++k) {
-                auto rotationMask = m_cc->EvalSub(subMask, rots_Rank[k]);
-                rotationMask = mehp24::utils::indicatorAdv(rotationMask, (double)N, dg_i, df_i);
+                auto rotationMask = ind(m_cc->EvalSub(subMask, rots_Rank[k]));
                 subMasked = m_cc->EvalAdd(subMasked, m_cc->EvalMult(rots_Input[k], rotationMask));
             }
             subMasked = sumColumnsToTarget(subMasked, N / num_batch, b, true);
@@ -540,10 +572,120 @@ class DirectSort : public SortBase<N> {
         return m_cc->EvalAddMany(Masked);
     }
 
+    // hybrid I: MEHP24 indicatorAdv on the unscaled rank (reference :1067-1229)
+    Ciphertext<DCRTPoly> rotationIndexCheckHybrid1(const Ciphertext<DCRTPoly>& ctx_Rank,
+                                                   const Ciphertext<DCRTPoly>& input_array,
+                                                   PrivateKey<DCRTPoly> sk) {
+        (void)sk;  // (unused by the reference as well)
+        // dg_i = (log2 N + 1) / 2 truncated (reference :1126-1127)
+        const uint32_t dg_i = (uint32_t)((std::log2((double)N) + 1) / 2);
+        const uint32_t df_i = 2;
+        return matrixPlacement(ctx_Rank, input_array, 1.0, 6, [&](const Ciphertext<DCRTPoly>& c) {
+            return mehp24::utils::indicatorAdv(c, (double)N, dg_i, df_i);
+        });
+    }
+
     Ciphertext<DCRTPoly> sort_hybrid1(const Ciphertext<DCRTPoly>& input_array, SignFunc SignFunc,
                                       SignConfig& Cfg, PrivateKey<DCRTPoly> sk) {
         auto ctx_Rank = constructRank(input_array, SignFunc, Cfg);
         return rotationIndexCheckHybrid1(ctx_Rank, input_array, sk);
+    }
+
+    // hybrid: rank / N against (b M + i) / N; the scaled-sinc Chebyshev series
+    // below N = 256, the composite-sign indicator |d| < 1/2N at and above
+    // (CompositeSign(3,4,2) at 256, (3,5,2) beyond; reference :894-1062)
+    Ciphertext<DCRTPoly> rotationIndexCheckHybrid(const Ciphertext<DCRTPoly>& ctx_Rank,
+                                                  const Ciphertext<DCRTPoly>& input_array,
+                                                  PrivateKey<DCRTPoly> sk) {
+        (void)sk;
+        ctx_Rank->SetSlots(N > 256 ? (uint32_t)max_batch : (uint32_t)(N * N));
+        auto r = m_cc->EvalMult(ctx_Rank, 1.0 / N);
+        return matrixPlacement(r, input_array, 1.0 / N, 8, [&](const Ciphertext<DCRTPoly>& c) {
+            if (N < 256) return m_cc->EvalChebyshevSeriesPS(c, selectCoefficients<N>(), -1, 1);
+            SignConfig icfg(CompositeSignConfig(3, N < 512 ? 4 : 5, 2));
+            return comp.indicator(m_cc, c, 0.5 / N, SignFunc::CompositeSign, icfg);
+        });
+    }
+
+    Ciphertext<DCRTPoly> sort_hybrid(const Ciphertext<DCRTPoly>& input_array, SignFunc SignFunc,
+                                     SignConfig& Cfg, PrivateKey<DCRTPoly> sk) {
+        auto ctx_Rank = constructRank(input_array, SignFunc, Cfg);
+        return rotationIndexCheckHybrid(ctx_Rank, input_array, sk);
+    }
+
+    // hybrid II: the scaled-sinc series at every N (reference :1233-1389)
+    Ciphertext<DCRTPoly> rotationIndexCheckHybrid2(const Ciphertext<DCRTPoly>& ctx_Rank,
+                                                   const Ciphertext<DCRTPoly>& input_array,
+                                                   PrivateKey<DCRTPoly> sk) {
+        (void)sk;
+        ctx_Rank->SetSlots(N > 256 ? (uint32_t)max_batch : (uint32_t)(N * N));
+        auto r = m_cc->EvalMult(ctx_Rank, 1.0 / N);
+        return matrixPlacement(r, input_array, 1.0 / N, 8, [&](const Ciphertext<DCRTPoly>& c) {
+            return m_cc->EvalChebyshevSeriesPS(c, selectCoefficients<N>(), -1, 1);
+        });
+    }
+
+    Ciphertext<DCRTPoly> sort_hybrid2(const Ciphertext<DCRTPoly>& input_array, SignFunc SignFunc,
+                                      SignConfig& Cfg, PrivateKey<DCRTPoly> sk) {
+        auto ctx_Rank = constructRank(input_array, SignFunc, Cfg);
+        return rotationIndexCheckHybrid2(ctx_Rank, input_array, sk);
+    }
+
+    // Placement over 2N-slot blocks with the scaled sinc (reference :537-656;
+    // not called by the reference's sorts): P = min(2N, n/2/N) partitions of N
+    // slots, B = 2N/P batches; batch b checks i - rank_i against the
+    // 2N-periodic checking vector and rotates each N-slot block left by its
+    // offset (blindRotationOpt2N).
+    Ciphertext<DCRTPoly> blindRotationOpt2N(const std::vector<Ciphertext<DCRTPoly>>& masked_inputs, int num_slots,
+                                            int np, int ib) {
+        (void)ib;
+        std::vector<Ciphertext<DCRTPoly>> giants;
+        for (int i = 0; i < (num_slots / N / 2) / np; ++i) {
+            auto& masks = maskMemo({9, 0, i, (int)masked_inputs[0]->GetLevel(), num_slots}, [&](auto& v) {
+                for (int j = 0; j < np; ++j)
+                    v.push_back(m_cc->MakeCKKSPackedPlaintext(vectorRotate(generateMaskVector2N(num_slots, np * i + j), j),
+                                                              1, masked_inputs[j]->GetLevel(), nullptr, num_slots));
+            });
+            giants.push_back(rot.rotate(m_cc->EvalMultAddPlain(masked_inputs, masks), i * np));
+        }
+        auto result = this->getZero()->Clone();
+        m_cc->EvalAddInPlace(result, m_cc->EvalAddMany(giants));
+        return result;
+    }
+
+    Ciphertext<DCRTPoly> rotationIndexCheck2N(const Ciphertext<DCRTPoly>& ctx_Rank,
+                                              const Ciphertext<DCRTPoly>& input_array) {
+        const int num_partition = std::min(2 * N, max_batch / N);
+        const int num_batch = 2 * N / num_partition;
+        const int num_slots = num_partition * N;
+        // np = 2^floor(log2(num_partition / 2) / 2), halved while np^2 > num_partition / 2 (:597-600)
+        int np = 1 << (sfhe::ilog2(num_partition / 2) >> 1);
+        if (np * np > num_partition / 2) np >>= 1;
+        auto output = this->getZero()->Clone();
+        Plaintext idx = maskMemo({2, 0, 0, (int)ctx_Rank->GetLevel(), N}, [&](auto& v) {
+            v.push_back(m_cc->MakeCKKSPackedPlaintext(generateIndexVector(), 1, ctx_Rank->GetLevel(), nullptr, N));
+        })[0];
+        auto indexMinusRank = m_cc->EvalSub(idx, ctx_Rank);
+        indexMinusRank->SetSlots(num_slots);
+        input_array->SetSlots(num_slots);
+        const int off = num_slots / N / 2;
+        for (int b = 0; b < num_batch; ++b) {
+            Plaintext chk = maskMemo({10, b, 0, (int)indexMinusRank->GetLevel(), num_slots}, [&](auto& v) {
+                v.push_back(m_cc->MakeCKKSPackedPlaintext(generateCheckingVector2N(num_slots, b * off), 1,
+                                                          indexMinusRank->GetLevel(), nullptr, num_slots));
+            })[0];
+            // sinc on (i - rank - c) / 2N in (-1, 1)
+            auto z = m_cc->EvalMult(m_cc->EvalSub(indexMinusRank, chk), 1.0 / N / 2);
+            auto hit = m_cc->EvalChebyshevSeriesPS(z, selectCoefficients<N>(), -1, 1);
+            auto masked = m_cc->EvalMult(hit, input_array);
+            std::vector<Ciphertext<DCRTPoly>> masked_inputs(np);
+            for (int i = 0; i < np; ++i) masked_inputs[i] = rot.rotate(masked, b * off + i);
+            m_cc->EvalAddInPlace(output, blindRotationOpt2N(masked_inputs, num_slots, np, b));
+        }
+        for (int s = num_slots / 2; s >= num_slots / num_partition; s /= 2)
+            m_cc->EvalAddInPlace(output, rot.rotate(output, s));
+        output->SetSlots(N);
+        return output;
     }
 
     // ---- hipGraph replay (north_star: "the Chebyshev tree / rotations /
@@ -559,8 +701,10 @@ class DirectSort : public SortBase<N> {
     struct GraphKey {
         uint32_t level = 0, slots = 0;
         int func = -1, n = 0, dg = 0, df = 0;
+        int multDepth = 0;  // decides whether compositeSign records bootstraps
         bool operator==(const GraphKey& o) const {
-            return level == o.level && slots == o.slots && func == o.func && n == o.n && dg == o.dg && df == o.df;
+            return level == o.level && slots == o.slots && func == o.func && n == o.n && dg == o.dg && df == o.df &&
+                   multDepth == o.multDepth;
         }
     };
     struct Graph {
@@ -601,6 +745,7 @@ class DirectSort : public SortBase<N> {
         key.n = Cfg.compos.n;
         key.dg = Cfg.compos.dg;
         key.df = Cfg.compos.df;
+        key.multDepth = Cfg.multDepth;
         if (!(m_graph && m_graph->key == key)) {
             if (!(m_warm && m_warmKey == key)) {  // first sort of this shape: eager, builds the masks
                 m_warm = true;

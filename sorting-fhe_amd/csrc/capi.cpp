@@ -99,6 +99,8 @@ struct SorterBase {
     virtual Ct rank(const Ct& in, SignConfig& cfg) = 0;
     virtual Ct place(const Ct& rank, const Ct& in) = 0;
     virtual Ct hybrid1(const Ct& in, SignConfig& cfg, const PrivateKey<DCRTPoly>& sk) = 0;
+    virtual Ct hybrid(const Ct& in, SignConfig& cfg, const PrivateKey<DCRTPoly>& sk, int variant) = 0;
+    virtual Ct place2N(const Ct& rank, const Ct& in) = 0;
     virtual Ct bitonic(const Ct& in, SignConfig& cfg) = 0;
     virtual size_t graphNodes() const = 0;
     virtual bool graphNttTime(int reps, double* ms, uint64_t* launches, double* bytes) = 0;
@@ -127,6 +129,11 @@ struct Sorter : SorterBase {
     Ct hybrid1(const Ct& in, SignConfig& cfg, const PrivateKey<DCRTPoly>& sk) override {
         return ds.sort_hybrid1(in, SignFunc::CompositeSign, cfg, sk);
     }
+    Ct hybrid(const Ct& in, SignConfig& cfg, const PrivateKey<DCRTPoly>& sk, int variant) override {
+        return variant == 2 ? ds.sort_hybrid2(in, SignFunc::CompositeSign, cfg, sk)
+                            : ds.sort_hybrid(in, SignFunc::CompositeSign, cfg, sk);
+    }
+    Ct place2N(const Ct& r, const Ct& in) override { return ds.rotationIndexCheck2N(r, in); }
     size_t graphNodes() const override { return ds.graphNodes(); }
     bool graphNttTime(int reps, double* ms, uint64_t* launches, double* bytes) override {
         return ds.graphNttTime(reps, ms, launches, bytes);
@@ -465,6 +472,22 @@ int sfhe_sorter_sort_hybrid1(sfhe_sorter* s, sfhe_ct* in, int n, int dg, int df,
     });
 }
 
+int sfhe_sorter_sort_hybrid(sfhe_sorter* s, sfhe_ct* in, int variant, int n, int dg, int df, sfhe_ct** out) {
+    REQUIRE(s && in && out, "null argument");
+    REQUIRE(variant == 0 || variant == 2, "variant must be 0 (sort_hybrid) or 2 (sort_hybrid2)");
+    REQUIRE(s->ctx->keys.secretKey, "sfhe_keygen must be called first");
+    return guard([&] {
+        Quiet q(s->ctx->quiet);
+        auto cfg = cfgOf(n, dg, df);
+        *out = wrap(s->impl->hybrid(in->ct, cfg, s->ctx->keys.secretKey, variant));
+    });
+}
+
+int sfhe_sorter_place_2n(sfhe_sorter* s, const sfhe_ct* rank, sfhe_ct* in, sfhe_ct** out) {
+    REQUIRE(s && rank && in && out, "null argument");
+    return guard([&] { *out = wrap(s->impl->place2N(rank->ct, in->ct)); });
+}
+
 int sfhe_sorter_sort_bitonic(sfhe_sorter* s, sfhe_ct* in, int n, int dg, int df, sfhe_ct** out) {
     REQUIRE(s && in && out, "null argument");
     REQUIRE(n == 3 || n == 4, "composite sign degree n must be 3 or 4");
@@ -487,11 +510,13 @@ int sfhe_save(sfhe_ctx* c, const char* dir) {
         put("pub.bin", [&](std::ostream& f) { return Serial::Serialize(c->keys.publicKey, f, SerType::BINARY); });
         if (c->keys.secretKey)
             put("sk.bin", [&](std::ostream& f) { return Serial::Serialize(c->keys.secretKey, f, SerType::BINARY); });
+        // this context's key pair only (other engines in the process keep theirs)
+        const std::string tag = KeyTagString(c->cc->KeyTag());
         put("mult.bin", [&](std::ostream& f) {
-            return CryptoContextImpl<DCRTPoly>::SerializeEvalMultKey(f, SerType::BINARY);
+            return CryptoContextImpl<DCRTPoly>::SerializeEvalMultKey(f, SerType::BINARY, tag);
         });
         put("rot.bin", [&](std::ostream& f) {
-            return CryptoContextImpl<DCRTPoly>::SerializeEvalAutomorphismKey(f, SerType::BINARY);
+            return CryptoContextImpl<DCRTPoly>::SerializeEvalAutomorphismKey(f, SerType::BINARY, tag);
         });
     });
 }
@@ -648,6 +673,17 @@ int sfhe_hybrid1_params(uint32_t N, uint32_t* mult_depth, int32_t* rotations, si
     return SFHE_OK;
 }
 
+int sfhe_hybrid_params(uint32_t N, int variant, uint32_t* mult_depth, int32_t* rotations, size_t cap,
+                       size_t* count) {
+    REQUIRE(validN(N), "N must be a power of two in [4, 1024]");
+    REQUIRE(variant == 0 || variant == 2, "variant must be 0 (sort_hybrid) or 2 (sort_hybrid2)");
+    const sfhe::SizeParams* p = sfhe::hybridParams((int)N, variant);
+    if (mult_depth) *mult_depth = (uint32_t)p->multDepth;
+    if (count) *count = p->rotations.size();
+    for (size_t i = 0; i < p->rotations.size() && i < cap && rotations; ++i) rotations[i] = p->rotations[i];
+    return SFHE_OK;
+}
+
 int sfhe_sorter_graph_ntt_time(sfhe_sorter* s, int reps, double* ms, uint64_t* launches, double* bytes) {
     REQUIRE(s && ms && reps > 0, "null argument");
     return guard([&] {
@@ -684,6 +720,7 @@ int sfhe_debug_decrypt_coeffs(sfhe_ctx* c, const sfhe_ct* ct, double* out, size_
     REQUIRE(cap >= n, "output buffer too small");
     return guard([&] {
         auto* s = c->cc->state();
+        c->cc->Settle(ct->ct);
         auto t = s->alloc(n);
         const sfp_limbs q{1, 1, 0, 0};
         sfp_mul_add(s->dev, t->ptr, ct->ct->c1, c->keys.secretKey->s->ptr, ct->ct->c0, q);

@@ -309,6 +309,10 @@ Ciphertext<DCRTPoly> evalMod(CryptoContextImpl<DCRTPoly>* cc, const BootstrapPre
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::BootstrapOnce(const Ciphertext<DCRTPoly>& ct, double inFactor,
                                                                 double outFactor) {
     SfheContextState* s = st.get();
+    // the precomputation's group plaintexts and s2cFirst are shared state:
+    // host threads of a lane region (compositeSign's refresh inside compare)
+    // bootstrap one at a time
+    OpLock lk(s);
     auto it = s->boot.find(ct->GetSlots());
     if (it == s->boot.end())
         SFHE_THROW("EvalBootstrap: no EvalBootstrapSetup for " + std::to_string(ct->GetSlots()) + " slots");

@@ -65,15 +65,6 @@ namespace {
 
 using Ct = Ciphertext<DCRTPoly>;
 
-// SFHE_PS_LANES (diagnostic): 0 no helper lanes, 1 baby steps, 2 + recursion
-int psMode() {
-    static const int m = [] {
-        const char* v = std::getenv("SFHE_PS_LANES");
-        return v ? std::atoi(v) : 0;
-    }();
-    return m;
-}
-
 struct Val {
     bool isConst = true;
     double c = 0.0;
@@ -82,16 +73,11 @@ struct Val {
 
 class PSEvaluator {
   public:
-    // lanes: {parent, helpers...} of a dataflow region; independent products
-    // are spread over them (inputs from other lanes are waited for device-side)
-    PSEvaluator(CryptoContextImpl<DCRTPoly>* cc, const Ct& y, uint32_t l, uint32_t D,
-                std::vector<int> lanes)
-        : cc(cc), l(l), k(1u << l), D(D), lanes(std::move(lanes)) {
+    PSEvaluator(CryptoContextImpl<DCRTPoly>* cc, const Ct& y, uint32_t l, uint32_t D)
+        : cc(cc), l(l), k(1u << l), D(D) {
         T.resize(k + 1);
         T[1] = y;
-        // T_j for 2^(t-1) < j <= 2^t only need T_i with i <= 2^(t-1): one wave
         for (uint32_t j = 2; j <= k; ++j) {
-            if (psMode() >= 1) cc->SetLane(this->lanes[j % this->lanes.size()]);
             Ct prod;
             if (j % 2 == 0)
                 prod = cc->EvalSquare(T[j / 2]);
@@ -101,7 +87,6 @@ class PSEvaluator {
             T[j] = (j % 2 == 0) ? cc->EvalAdd(two, -1.0) : cc->EvalSub(two, atLevel(1, two->GetLevel()));
         }
         giant[l] = T[k];
-        cc->SetLane(this->lanes[0]);
     }
 
     // Collect the leaves eval() will visit, in visiting order (same control
@@ -127,11 +112,13 @@ class PSEvaluator {
                         break;
                     }
             std::vector<const uint64_t*> ins0, ins1;
+            std::vector<double> sc;
             for (uint32_t j : js) {
-                const Ct& t = atLevel(j, L);
-                cc->state()->dep(t->buf.get());
+                const Ct& t = T[j];  // its first ellOf(L) rows; its scale is folded into the weights
+                cc->Settle(t);  // raw rows below: a lazy product's rescale first
                 ins0.push_back(t->c0);
                 ins1.push_back(t->c1);
+                sc.push_back(t->scale);
             }
             for (size_t b0 = 0; b0 < kv.second.size(); b0 += 64) {
                 std::vector<std::vector<double>> w;
@@ -142,7 +129,7 @@ class PSEvaluator {
                     for (uint32_t j : js) row.push_back(j < pl.size() ? pl[j] : 0.0);
                     w.push_back(std::move(row));
                 }
-                auto cts = cc->LinearWSumRescaleMulti(ins0, ins1, w, L, T[1]->GetSlots());
+                auto cts = cc->LinearWSumRescaleMulti(ins0, ins1, w, L, T[1]->GetSlots(), &sc);
                 for (size_t t = b0; t < b1; ++t) pre[kv.second[t]] = cts[t - b0];
             }
         }
@@ -166,12 +153,7 @@ class PSEvaluator {
                 r[2 * M - j] -= p[j];
             }
         }
-        // the quotient and remainder subtrees are independent: quotient on the
-        // next lane, remainder here; the product and sum run on this lane
-        const int here = cc->state()->lane;
-        if (psMode() >= 2) cc->SetLane(lanes[(nextLane++) % lanes.size()]);
         Val qv = eval(q, depth - 1);
-        cc->SetLane(here);
         Val rv = eval(r, depth);
         const Ct& TM = power(M);
         Val out;
@@ -269,26 +251,25 @@ class PSEvaluator {
             }
         if (!any) return Val{true, p[0], nullptr};
         std::vector<const uint64_t*> ins0, ins1;
-        std::vector<double> w;
+        std::vector<double> w, sc;
         for (uint32_t j = 1; j <= deg; ++j) {
             if (p[j] == 0.0) continue;
-            const Ct& t = atLevel(j, lev);
-            cc->state()->dep(t->buf.get());  // raw pointers below: order after their writers
+            const Ct& t = T[j];  // unadjusted: its scale is folded into the weight
+            cc->Settle(t);  // raw pointers below: canonical rows, ordered after their writers
             ins0.push_back(t->c0);
             ins1.push_back(t->c1);
             w.push_back(p[j]);
+            sc.push_back(t->scale);
         }
         Val out;
         out.isConst = false;
-        out.ct = cc->LinearWSumRescale(ins0, ins1, w, lev, T[1]->GetSlots());
+        out.ct = cc->LinearWSumRescale(ins0, ins1, w, lev, T[1]->GetSlots(), &sc);
         if (p[0] != 0.0) out.ct = cc->EvalAdd(out.ct, p[0]);
         return out;
     }
 
     CryptoContextImpl<DCRTPoly>* cc;
     uint32_t l, k, D;
-    std::vector<int> lanes;
-    uint32_t nextLane = 1;
     std::vector<Ct> pre;  // precomputed leaves in visiting order
     size_t nextLeaf = 0;
     std::vector<Ct> T;
@@ -326,16 +307,14 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalChebyshevSeriesPS(
         }
     }
     const uint32_t l = std::min(bestL, (uint32_t)(31 - __builtin_clz(std::max<uint32_t>(d, 2))));
-    const auto lanes = psMode() ? ForkHelpers() : std::vector<int>{};
     Ciphertext<DCRTPoly> out;
     {
-        PSEvaluator ps(this, y, l, D, lanes.empty() ? std::vector<int>{st->lane} : lanes);
+        PSEvaluator ps(this, y, l, D);
         static const bool batched = std::getenv("SFHE_PS_UNBATCHED") == nullptr;
         if (batched) ps.precomputeLeaves(p, D);
         auto v = ps.eval(p, D);
         out = v.isConst ? EvalAdd(EvalMult(y, 0.0), v.c) : v.ct;
     }
-    if (!lanes.empty()) JoinHelpers(lanes);
     const uint32_t target = y->GetLevel() + D;
     if (out->GetLevel() > target)
         SFHE_THROW("internal: Chebyshev evaluation exceeded OpenFHE depth");
@@ -364,18 +343,19 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalPolyLinear(
     uint32_t lev = 0;
     for (uint32_t j = 1; j <= d; ++j)
         if (p[j] != 0.0) lev = std::max(lev, pw[j]->GetLevel());
+    // powers below the top level enter with their own scale folded into the
+    // weight (no level adjustment, no extra rounding)
     std::vector<const uint64_t*> i0, i1;
-    std::vector<double> w;
-    std::vector<Ciphertext<DCRTPoly>> keep;
+    std::vector<double> w, sc;
     for (uint32_t j = 1; j <= d; ++j) {
         if (p[j] == 0.0) continue;
-        auto t = pw[j]->GetLevel() == lev ? pw[j] : AdjustLevel(pw[j], lev);
-        keep.push_back(t);
-        i0.push_back(t->c0);
-        i1.push_back(t->c1);
+        Settle(pw[j]);  // raw rows below
+        i0.push_back(pw[j]->c0);
+        i1.push_back(pw[j]->c1);
         w.push_back(p[j]);
+        sc.push_back(pw[j]->scale);
     }
-    auto out = LinearWSumRescale(i0, i1, w, lev, x->GetSlots());
+    auto out = LinearWSumRescale(i0, i1, w, lev, x->GetSlots(), &sc);
     if (p[0] != 0.0) out = EvalAdd(out, p[0]);
     return out;
 }

@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <random>
 
 #include "state.h"
 
@@ -153,9 +154,7 @@ DeviceBuffer::~DeviceBuffer() {
             return;
         }
     }
-    if (st->dataflow)
-        st->dataflowFree.push_back({words, ptr});  // any lane may still read it: after the sub-join
-    else if (!st->forkedLanes)
+    if (!st->forkedLanes)
         st->freeList[0][words].push_back(ptr);  // everything is ordered behind lane 0 again
     else if (region == st->region && lane == st->myLane())
         st->freeList[lane][words].push_back(ptr);  // private to this lane in this region
@@ -175,13 +174,9 @@ DeviceBufferPtr SfheContextState::alloc(size_t words) {
             it->second.pop_back();
             return true;
         };
-        // own lane first; then blocks this lane is already ordered after: the
-        // pre-fork pool (every lane of a region waited for lane 0 at the fork),
-        // and in a dataflow sub-region the parent's free list (all of it freed
-        // before the helpers waited for the parent)
-        if (!take(freeList[lane]) && !(forkedLanes && take(forkPool)) && dataflow && dataflowParent >= 0 &&
-            lane != dataflowParent)
-            take(freeList[dataflowParent]);
+        // own lane first; then the pre-fork pool, which every lane of a region
+        // is ordered after (each waited for lane 0 at the fork)
+        if (!take(freeList[lane]) && forkedLanes) take(forkPool);
     }
     if (!p) {
         p = (uint64_t*)sfp_alloc(dev, words * 8);
@@ -195,6 +190,7 @@ DeviceBufferPtr SfheContextState::alloc(size_t words) {
     }
     auto b = std::make_shared<DeviceBuffer>(this, p, words, lane, forkedLanes ? region : 0);
     b->seq = ++laneSeq[lane];
+    b->capEpoch = capturing ? captureEpoch : 0;
     if (capturing) {
         std::lock_guard<std::mutex> g(poolMu);
         capAllocs.push_back({p, words});
@@ -264,7 +260,7 @@ class SfheInternal {
     // traces of two backends can be diffed to find the first divergent op.
     static Ct traced(CC* cc, Ct ct, const char* what) {
         static const bool on = std::getenv("SFHE_TRACE") != nullptr;
-        if (!on) return ct;
+        if (!on || ct->def) return ct;  // a deferred product is traced where it is computed
         static uint64_t counter = 0;
         SfheContextState* s = cc->st.get();
         const size_t words = s->polyWords(ct->level);
@@ -278,14 +274,151 @@ class SfheInternal {
         return ct;
     }
 
-    // order the current lane after the writers of the inputs (lanes)
+    // Inputs in canonical form (lazy rescaling: deferred products computed,
+    // pending rows rescaled), with the current lane ordered after their writers.
     static void deps(SfheContextState* s, std::initializer_list<const Ct*> in) {
         for (const Ct* c : in)
-            if (c && *c) s->dep((*c)->buf.get());
+            if (c && *c) {
+                materialize(**c, false);
+                s->dep((*c)->buf.get());
+            }
     }
     static void depsv(SfheContextState* s, const std::vector<Ct>& in) {
         for (const Ct& c : in)
-            if (c) s->dep(c->buf.get());
+            if (c) {
+                materialize(*c, false);
+                s->dep(c->buf.get());
+            }
+    }
+
+    // ---- lazy rescaling ------------------------------------------------------
+    // Products (ct x ct, ct x pt, ct x double, sums of ct x pt) return deferred
+    // ciphertexts.  A consumer that can work on the product BEFORE its rescale
+    // -- a rotation, or a sum with another such product or with a ciphertext
+    // of a lower level (lifted exactly by an integer) -- takes the pending
+    // rows; everything else takes the canonical form (the fused product +
+    // rescale, as before).  Rotations of pending rows divide their key-switch
+    // rounding by the prime the final rescale drops, and a sum of products is
+    // rescaled once: OpenFHE's FLEXIBLEAUTO rescales lazily the same way.
+    // SFHE_LAZY=0 computes every product in canonical form at once.
+    static bool lazy(const SfheContextState* s) {
+        static const bool on = [] {
+            const char* v = std::getenv("SFHE_LAZY");
+            return !v || *v != '0';
+        }();
+        return on;
+    }
+    static bool isLazy(const Ct& c) { return c && (c->def || c->pend); }
+    static uint32_t ctEll(const SfheContextState* s, const CiphertextImpl<DCRTPoly>& c) {
+        return s->ellOf(c.level) + (c.pend ? 1u : 0u);
+    }
+    static void materialize(CiphertextImpl<DCRTPoly>& c, bool pendingOk) {
+        if (c.def) {
+            std::shared_ptr<DeferredOp> d = std::move(c.def);
+            c.def.reset();
+            d->run(c.cc.get(), c, pendingOk);
+        }
+        if (c.pend && !pendingOk) settleRows(c);
+    }
+    // pending rows -> their rescale (canonical, at c.level)
+    static void settleRows(CiphertextImpl<DCRTPoly>& c) {
+        CC* cc = c.cc.get();
+        SfheContextState* s = cc->st.get();
+        s->dep(c.buf.get());
+        const uint32_t ell = ctEll(s, c);
+        const size_t pw = s->polyWords(c.level);
+        auto out = s->alloc(2 * pw);
+        if (s->world > 1)  // the dropped row's owner broadcasts it
+            rescaleShard(s, out->ptr, c.c0, ell, 2, (size_t)(c.c1 - c.c0), pw);
+        else
+            sfp_rescale(s->dev, out->ptr, c.c0, ell, s->qInvTable[ell].data(), 2, (size_t)(c.c1 - c.c0), pw);
+        s->stats.rescale++;
+        s->countBytes(4.0 * ell * s->n * 8);
+        c.buf = out;
+        c.c0 = out->ptr;
+        c.c1 = out->ptr + pw;
+        c.pend = false;
+        c.scale = s->scale[c.level];
+    }
+    // a deferred result at post-rescale `level`
+    static Ct deferredCt(CC* cc, uint32_t level, uint32_t slots, std::shared_ptr<DeferredOp> op) {
+        SfheContextState* s = cc->st.get();
+        auto ct = std::make_shared<CiphertextImpl<DCRTPoly>>();
+        ct->cc = cc->shared_from_this();
+        ct->level = level;
+        ct->slots = slots;
+        ct->scale = s->scale[level];
+        ct->def = std::move(op);
+        return ct;
+    }
+    // a fresh pending ciphertext: rows for ellOf(level) + 1 limbs
+    static Ct newPendingCt(CC* cc, uint32_t level, uint32_t slots) {
+        SfheContextState* s = cc->st.get();
+        auto ct = std::make_shared<CiphertextImpl<DCRTPoly>>();
+        const size_t pw = s->polyWords(level - 1);
+        ct->cc = cc->shared_from_this();
+        ct->buf = s->alloc(2 * pw);
+        ct->c0 = ct->buf->ptr;
+        ct->c1 = ct->c0 + pw;
+        ct->level = level;
+        ct->slots = slots;
+        ct->scale = s->preScale(level);
+        ct->pend = true;
+        return ct;
+    }
+    // Sum / difference of two ciphertexts where at least one is a lazy
+    // product: null if the canonical path must be taken instead.  The result
+    // is pending at their common level; a canonical operand of a lower level
+    // is lifted onto the product's scale by an integer multiple (exact up to
+    // a relative 2^-41 of its value -- no rounding noise).
+    static Ct lazyAdd(CC* cc, const Ct& a, const Ct& b, bool sub) {
+        SfheContextState* s = cc->st.get();
+        if (!lazy(s) || !(isLazy(a) || isLazy(b))) return nullptr;
+        const Ct* lz[2] = {&a, &b};
+        bool liftIdx[2] = {false, false};
+        if (isLazy(a) && isLazy(b)) {
+            if (a->level != b->level) return nullptr;
+        } else {
+            const Ct& c = isLazy(a) ? b : a;   // the canonical one
+            const Ct& p = isLazy(a) ? a : b;
+            if (c->level >= p->level) return nullptr;
+            liftIdx[isLazy(a) ? 1 : 0] = true;
+        }
+        const uint32_t level = a->level > b->level ? a->level : b->level;
+        for (int i = 0; i < 2; ++i) {
+            materialize(**lz[i], !liftIdx[i]);
+            s->dep((*lz[i])->buf.get());
+        }
+        const uint32_t ell = s->ellOf(level) + 1;
+        const sfp_limbs m = s->qmap(ell);
+        Ct out = newPendingCt(cc, level, std::max(a->slots, b->slots));
+        const uint64_t* x0[2];
+        const uint64_t* x1[2];
+        DeviceBufferPtr lifted;
+        for (int i = 0; i < 2; ++i) {
+            const Ct& c = *lz[i];
+            x0[i] = c->c0;
+            x1[i] = c->c1;
+            if (!liftIdx[i]) continue;
+            const size_t pw = s->polyWords(level - 1);
+            lifted = s->alloc(2 * pw);
+            auto k = constResidues(s, s->preScale(level) / c->scale, ell);
+            sfp_mul_const(s->dev, lifted->ptr, c->c0, k.data(), m);
+            sfp_mul_const(s->dev, lifted->ptr + pw, c->c1, k.data(), m);
+            x0[i] = lifted->ptr;
+            x1[i] = lifted->ptr + pw;
+            s->countBytes(4.0 * ell * s->n * 8);
+        }
+        if (sub) {
+            sfp_sub(s->dev, out->c0, x0[0], x0[1], m);
+            sfp_sub(s->dev, out->c1, x1[0], x1[1], m);
+        } else {
+            sfp_add(s->dev, out->c0, x0[0], x0[1], m);
+            sfp_add(s->dev, out->c1, x1[0], x1[1], m);
+        }
+        s->stats.add++;
+        s->countBytes(6.0 * ell * s->n * 8);
+        return out;
     }
 
     static sfp_limbs Q(uint32_t ell) { return sfp_limbs{ell, ell, 0}; }
@@ -774,13 +907,17 @@ class SfheInternal {
 
     // device encoding of a plaintext at `level` with scale Delta_level
     // An encoding produced on another lane that may still be in flight is
-    // waited for (device-side) before use.
+    // waited for (device-side) before use.  Inside a capture, an event
+    // recorded before it is dropped (BeginCapture drained the device); one
+    // recorded inside it is waited for, which makes it a graph edge.
     static const uint64_t* ready(SfheContextState* s, DeviceBuffer* b) {
-        if (b->ready && s->capturing) {  // the capture began after a full drain
+        if (b->ready && s->capturing && b->readyEpoch != s->captureEpoch) {
             sfp_event_free(s->dev, b->ready);
             b->ready = nullptr;
         }
-        if (b->ready) {
+        if (b->ready && s->capturing) {
+            sfp_event_wait(s->dev, b->ready);
+        } else if (b->ready) {
             if (sfp_event_done(s->dev, b->ready)) {
                 sfp_event_free(s->dev, b->ready);
                 b->ready = nullptr;
@@ -822,7 +959,13 @@ class SfheInternal {
             s->scopeKeep.push_back(buf);
             return buf->ptr;
         }
+        // an encoding made inside an abandoned capture never ran: make it again
+        auto stale = [&](const DeviceBufferPtr& b) { return b->capEpoch && s->abandonedEpochs.count(b->capEpoch); };
         auto it = pt->encoded.find(level);
+        if (it != pt->encoded.end() && stale(it->second)) {
+            pt->encoded.erase(it);
+            it = pt->encoded.end();
+        }
         if (it != pt->encoded.end()) return ready(s, it->second.get());
         // context-level cache: identical (values, slots, level) encode identically
         uint64_t h = 1469598103934665603ull;
@@ -840,12 +983,21 @@ class SfheInternal {
             mix(level);
             mix(pt->values.size());
             auto ci = s->ptCache.find(h);
-            if (ci != s->ptCache.end())
-                for (auto& e : ci->second)
+            if (ci != s->ptCache.end()) {
+                auto& v = ci->second;
+                for (auto e = v.begin(); e != v.end();)
+                    if (stale(e->buf)) {
+                        s->ptCacheBytes -= e->buf->words * 8;
+                        e = v.erase(e);
+                    } else {
+                        ++e;
+                    }
+                for (auto& e : v)
                     if (e.slots == pt->slots && e.values == pt->values) {
                         pt->encoded[level] = e.buf;
                         return ready(s, e.buf.get());
                     }
+            }
         }
         std::vector<int64_t> coeffs;
         const size_t pw = s->polyWords(level);
@@ -863,6 +1015,7 @@ class SfheInternal {
         }
         sfp_ntt(s->dev, buf->ptr, s->qmap(ell), 0);
         buf->ready = sfp_event_record(s->dev);
+        buf->readyEpoch = s->capturing ? s->captureEpoch : 0;
         pt->encoded[level] = buf;
         if (s->ptCacheOn && s->ptCacheBytes + pw * 8 <= s->ptCacheLimit) {
             s->ptCache[h].push_back(PtCacheEntry{pt->values, pt->slots, buf});
@@ -871,11 +1024,45 @@ class SfheInternal {
         return buf->ptr;
     }
 
+    // a canonical ciphertext over existing rows (deferred ops keep the rows
+    // they were given pinned, never the caller's possibly reassigned handle)
+    static Ct view(CC* cc, const DeviceBufferPtr& buf, uint64_t* c0, uint64_t* c1, uint32_t level, double scale,
+                   uint32_t slots) {
+        auto ct = std::make_shared<CiphertextImpl<DCRTPoly>>();
+        ct->cc = cc->shared_from_this();
+        ct->buf = buf;
+        ct->c0 = c0;
+        ct->c1 = c1;
+        ct->level = level;
+        ct->scale = scale;
+        ct->slots = slots;
+        return ct;
+    }
+    // fill `dst` (a deferred ciphertext) with the rows of `src`
+    static void adopt(CiphertextImpl<DCRTPoly>& dst, const Ct& src) {
+        dst.buf = src->buf;
+        dst.c0 = src->c0;
+        dst.c1 = src->c1;
+        dst.scale = src->scale;
+        dst.pend = src->pend;
+    }
+    static void adoptPending(CiphertextImpl<DCRTPoly>& dst, const DeviceBufferPtr& buf, uint64_t* c0,
+                             uint64_t* c1) {
+        SfheContextState* s = dst.cc->st.get();
+        dst.buf = buf;
+        dst.c0 = c0;
+        dst.c1 = c1;
+        dst.pend = true;
+        dst.scale = s->preScale(dst.level);
+        s->wrote(buf.get());
+    }
+
     static Ct copyOf(CC* cc, const Ct& a) {
         SfheContextState* s = cc->st.get();
-        Ct out = newCt(cc, a->level, a->slots);
-        size_t bytes = s->polyWords(a->level) * 8;
-        if (a->c1 == a->c0 + s->polyWords(a->level)) {  // [c0][c1] packed: one copy
+        Ct out = a->pend ? newPendingCt(cc, a->level, a->slots) : newCt(cc, a->level, a->slots);
+        const size_t pw = s->polyWords(a->pend ? a->level - 1 : a->level);
+        size_t bytes = pw * 8;
+        if (a->c1 == a->c0 + pw) {  // [c0][c1] packed: one copy
             sfp_d2d(s->dev, out->c0, a->c0, 2 * bytes);
         } else {
             sfp_d2d(s->dev, out->c0, a->c0, bytes);
@@ -893,6 +1080,118 @@ class SfheInternal {
         }
     }
 };
+
+// ============================================================================
+// deferred products (lazy rescaling; see SfheInternal::materialize)
+
+namespace {
+using CtI = CiphertextImpl<DCRTPoly>;
+using CCI = CryptoContextImpl<DCRTPoly>;
+
+// EvalMult(ct, double): rows x per-row residues K (the constant times the
+// product scale), then the rescale
+struct DeferredConstMult : DeferredOp {
+    DeviceBufferPtr pin;
+    uint64_t *c0, *c1;
+    uint32_t level, slots;
+    double scale;
+    std::vector<uint64_t> k;
+    void run(CCI* cc, CtI& ct, bool pending) override {
+        SfheContextState* s = cc->state();
+        s->dep(pin.get());
+        if (!pending) {
+            auto src = SfheInternal::view(cc, pin, c0, c1, level, scale, slots);
+            SfheInternal::adopt(ct, SfheInternal::mulRescale(cc, src, level, k.data(), nullptr, slots));
+            return;
+        }
+        const size_t pw = s->polyWords(level);
+        auto out = s->alloc(2 * pw);
+        sfp_mul_const(s->dev, out->ptr, c0, k.data(), s->qmap(s->ellOf(level)));
+        sfp_mul_const(s->dev, out->ptr + pw, c1, k.data(), s->qmap(s->ellOf(level)));
+        SfheInternal::adoptPending(ct, out, out->ptr, out->ptr + pw);
+    }
+};
+
+// EvalMult(ct, pt): rows (.) the plaintext's encoding at `level`
+struct DeferredPlainMult : DeferredOp {
+    DeviceBufferPtr pin;
+    uint64_t *c0, *c1;
+    uint32_t level, slots;
+    double scale;
+    Plaintext pt;
+    void run(CCI* cc, CtI& ct, bool pending) override {
+        SfheContextState* s = cc->state();
+        s->dep(pin.get());
+        const uint64_t* m = SfheInternal::encoded(cc, pt, level);
+        if (!pending) {
+            auto src = SfheInternal::view(cc, pin, c0, c1, level, scale, slots);
+            SfheInternal::adopt(ct, SfheInternal::mulRescale(cc, src, level, nullptr, m, slots));
+            return;
+        }
+        const size_t pw = s->polyWords(level);
+        auto out = s->alloc(2 * pw);
+        sfp_mul(s->dev, out->ptr, c0, m, s->qmap(s->ellOf(level)));
+        sfp_mul(s->dev, out->ptr + pw, c1, m, s->qmap(s->ellOf(level)));
+        SfheInternal::adoptPending(ct, out, out->ptr, out->ptr + pw);
+    }
+};
+
+// EvalMultAddPlain: sum_i a_i (.) p_i, then one rescale
+struct DeferredMacPlain : DeferredOp {
+    std::vector<DeviceBufferPtr> pins;
+    std::vector<const uint64_t*> x0, x1;
+    std::vector<Plaintext> pts;
+    uint32_t level, slots;
+    void run(CCI* cc, CtI& ct, bool pending) override {
+        SfheContextState* s = cc->state();
+        for (auto& b : pins) s->dep(b.get());
+        std::vector<const uint64_t*> m;
+        for (auto& p : pts) m.push_back(SfheInternal::encoded(cc, p, level));
+        const uint32_t ell = s->ellOf(level);
+        const size_t pw = s->polyWords(level);
+        auto tmp = s->alloc(2 * pw);
+        uint64_t* t0 = tmp->ptr;
+        uint64_t* t1 = t0 + pw;
+        for (size_t done = 0; done < x0.size(); done += SFP_MAX_WSUM) {
+            const uint32_t take = (uint32_t)std::min<size_t>(SFP_MAX_WSUM, x0.size() - done);
+            if (done == 0) {
+                sfp_mac_plain2(s->dev, t0, t1, x0.data(), x1.data(), m.data(), take, s->qmap(ell));
+            } else {
+                auto part = s->alloc(2 * pw);
+                sfp_mac_plain2(s->dev, part->ptr, part->ptr + pw, x0.data() + done, x1.data() + done,
+                               m.data() + done, take, s->qmap(ell));
+                sfp_add(s->dev, t0, t0, part->ptr, s->qmap(ell));
+                sfp_add(s->dev, t1, t1, part->ptr + pw, s->qmap(ell));
+            }
+        }
+        if (pending) {
+            SfheInternal::adoptPending(ct, tmp, t0, t1);
+            return;
+        }
+        SfheInternal::adopt(ct, SfheInternal::rescale(cc, t0, t1, level, slots));
+    }
+};
+
+// EvalMult(ct, ct): tensor done; relinearisation (+ rescale) deferred
+struct DeferredRelin : DeferredOp {
+    DeviceBufferPtr t;  // d0, d1, d2 (polyWords(level) apart)
+    uint32_t level, slots;
+    void run(CCI* cc, CtI& ct, bool pending) override {
+        SfheContextState* s = cc->state();
+        s->dep(t.get());
+        const size_t pw = s->polyWords(level);
+        uint64_t* d0 = t->ptr;
+        uint64_t* d1 = d0 + pw;
+        uint64_t* d2 = d1 + pw;
+        if (!pending) {
+            SfheInternal::adopt(ct, SfheInternal::relinRescale(cc, d0, d1, d2, level, slots));
+            return;
+        }
+        SfheInternal::keySwitch(cc, d2, s->ellOf(level), s->relinKey, d0, d1, 1, 1);
+        SfheInternal::adoptPending(ct, t, d0, d1);
+    }
+};
+}  // namespace
 
 // ============================================================================
 // context construction
@@ -1130,56 +1429,10 @@ void CryptoContextImpl<DCRTPoly>::ForkLanes(int count) {
     s->region = ++s->regionCount;
 }
 
-std::vector<int> CryptoContextImpl<DCRTPoly>::ForkHelpers() {
-    OpLock g(st.get());
-    SfheContextState* s = st.get();
-    std::vector<int> lanes{s->lane};
-    // a sharded context issues its collectives in program order on one lane
-    // (LaneCount): no helper lanes, or ranks could order them differently.
-    // Nor while a graph is being captured: the diagnostic helper lanes
-    // (SFHE_PS_LANES) were never made capture-safe (a captured sort with
-    // them crashed on the host), so a capture records the single-lane PS.
-    if (!s->dataflow && s->world == 1 && !s->capturing) {
-        s->dataflowParent = s->lane;
-        // helpers: lanes that are not primaries of an open batch region
-        const int first = s->forkedLanes ? s->forkedLanes : 0;
-        for (int l = first; l < sfp_lanes(s->dev); ++l)
-            if (l != s->lane) {
-                s->laneWait(l, s->lane);
-                lanes.push_back(l);
-            }
-    }
-    s->dataflow++;
-    return lanes;
-}
-
-void CryptoContextImpl<DCRTPoly>::JoinHelpers(const std::vector<int>& lanes) {
-    OpLock g(st.get());
-    SfheContextState* s = st.get();
-    if (!s->dataflow) return;
-    const int parent = lanes.empty() ? s->lane : lanes[0];
-    s->lane = parent;
-    s->setMyLane(parent);
-    sfp_set_lane(s->dev, parent);
-    for (size_t i = 1; i < lanes.size(); ++i) s->laneWait(parent, lanes[i]);
-    if (--s->dataflow == 0) {
-        std::lock_guard<std::mutex> pg(s->poolMu);
-        for (auto& e : s->dataflowFree) s->freeList[parent][e.first].push_back(e.second);
-        s->dataflowFree.clear();
-        // helpers' own lists: ordered behind the parent after the waits above
-        for (size_t i = 1; i < lanes.size(); ++i) {
-            for (auto& kv : s->freeList[lanes[i]])
-                for (auto* p : kv.second) s->freeList[parent][kv.first].push_back(p);
-            s->freeList[lanes[i]].clear();
-        }
-        s->dataflowParent = -1;
-    }
-}
-
 void CryptoContextImpl<DCRTPoly>::SetLane(int lane) {
     OpLock g(st.get());
     SfheContextState* s = st.get();
-    if (lane != 0 && !s->dataflow && (!s->forkedLanes || lane >= s->forkedLanes))
+    if (lane != 0 && (!s->forkedLanes || lane >= s->forkedLanes))
         SFHE_THROW("SetLane: lane " + std::to_string(lane) + " outside the open region");
     if (lane < 0 || lane >= sfp_lanes(s->dev)) SFHE_THROW("SetLane: no lane " + std::to_string(lane));
     s->setMyLane(lane);
@@ -1193,7 +1446,7 @@ void CryptoContextImpl<DCRTPoly>::JoinLanes() {
     if (!s->forkedLanes) return;
     static const bool stats = std::getenv("SFHE_LANE_STATS") != nullptr;
     if (stats) {
-        std::fprintf(stderr, "LANESTATS region %d: %llu data-dependency waits across lanes\n", s->region,
+        std::fprintf(stderr, "LANESTATS region %llu: %llu data-dependency waits across lanes\n", (unsigned long long)s->region,
                      (unsigned long long)s->regionDepWaits);
         s->regionDepWaits = 0;
     }
@@ -1236,6 +1489,14 @@ void CryptoContextImpl<DCRTPoly>::ResetOpStats() { st->stats = OpStats(); }
 // ============================================================================
 // keys
 
+std::string KeyTagString(uint64_t tag) {
+    char b[17];
+    std::snprintf(b, sizeof b, "%016llx", (unsigned long long)tag);
+    return b;
+}
+
+uint64_t CryptoContextImpl<DCRTPoly>::KeyTag() const { return st->keyTag; }
+
 KeyPair<DCRTPoly> CryptoContextImpl<DCRTPoly>::KeyGen() {
     OpLock g(st.get());
     SfheContextState* s = st.get();
@@ -1244,6 +1505,12 @@ KeyPair<DCRTPoly> CryptoContextImpl<DCRTPoly>::KeyGen() {
     KeyPair<DCRTPoly> kp;
     auto sk = std::make_shared<PrivateKeyImpl<DCRTPoly>>();
     sk->cc = shared_from_this();
+    // the key pair's tag: random (not from the sampling seed), never 0
+    {
+        std::random_device rd;
+        sk->tag = ((uint64_t)rd() << 32 | rd()) | 1;
+    }
+    s->keyTag = sk->tag;
     std::vector<int64_t> tern(s->n);
     SfheInternal::sampleTernary(s, tern);
     sk->ternary.assign(tern.begin(), tern.end());
@@ -1272,6 +1539,7 @@ KeyPair<DCRTPoly> CryptoContextImpl<DCRTPoly>::KeyGen() {
         sfp_mul(s->dev, t->ptr + (size_t)s->Lq * s->n, pk->a->ptr + (size_t)s->Lq * s->n,
                 sk->s->ptr + (size_t)s->extIdx * s->n, sfp_limbs{1, 0, s->extIdx, 0});
     sfp_sub(s->dev, pk->b->ptr, pk->b->ptr, t->ptr, q);
+    pk->tag = sk->tag;
     kp.publicKey = pk;
     kp.secretKey = sk;
     return kp;
@@ -1284,6 +1552,7 @@ void CryptoContextImpl<DCRTPoly>::EvalMultKeyGen(const PrivateKey<DCRTPoly>& sk)
     auto s2 = s->alloc((size_t)NP * s->n);
     sfp_mul(s->dev, s2->ptr, sk->s->ptr, sk->s->ptr, sfp_limbs{NP, NP, 0});
     s->relinKey = SfheInternal::genSwitchKey(this, s2->ptr, sk->s->ptr);
+    s->keyTag = sk->tag;
 }
 
 void CryptoContextImpl<DCRTPoly>::EvalRotateKeyGen(const PrivateKey<DCRTPoly>& sk,
@@ -1292,6 +1561,7 @@ void CryptoContextImpl<DCRTPoly>::EvalRotateKeyGen(const PrivateKey<DCRTPoly>& s
     OpLock g(st.get());
     SfheContextState* s = st.get();
     const uint32_t NP = s->Lq + s->K;
+    s->keyTag = sk->tag;
     auto sg = s->alloc((size_t)NP * s->n);
     for (int32_t r : idx) {
         s->rotIndices.insert(r);
@@ -1482,6 +1752,11 @@ std::ostream& operator<<(std::ostream& os, const Plaintext& pt) {
 
 Ciphertext<DCRTPoly> CiphertextImpl<DCRTPoly>::Clone() const {
     OpLock g(cc->state());
+    // a deferred product is computed first (unrescaled while rescaling is
+    // lazy: the copy's consumer decides); pending rows are copied as they are
+    if (def)
+        SfheInternal::materialize(const_cast<CiphertextImpl<DCRTPoly>&>(*this),
+                                  SfheInternal::lazy(cc->state()));
     cc->state()->dep(buf.get());
     auto self = std::make_shared<CiphertextImpl<DCRTPoly>>(*this);
     return SfheInternal::copyOf(cc.get(), self);
@@ -1495,6 +1770,7 @@ uint32_t CiphertextImpl<DCRTPoly>::GetNumLimbs() const { return cc->state()->ell
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalAdd(const Ciphertext<DCRTPoly>& a0,
                                                          const Ciphertext<DCRTPoly>& b0) {
     OpLock g(st.get());
+    if (auto r = SfheInternal::lazyAdd(this, a0, b0, false)) return SfheInternal::traced(this, r, "EvalAdd");
     SfheInternal::deps(st.get(), {&a0, &b0});
     auto a = a0, b = b0;
     SfheInternal::align(this, a, b);
@@ -1514,11 +1790,14 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalAdd(const Ciphertext<DCRTP
 void CryptoContextImpl<DCRTPoly>::EvalAddInPlace(Ciphertext<DCRTPoly>& a,
                                                  const Ciphertext<DCRTPoly>& b0) {
     OpLock g(st.get());
+    if (SfheInternal::isLazy(a) || SfheInternal::isLazy(b0)) {
+        a = EvalAdd(a, b0);
+        return;
+    }
     SfheInternal::deps(st.get(), {&a, &b0});
     auto b = b0;
-    // in place only on an exclusively owned buffer outside dataflow regions
-    // (there another lane may still be reading the old value)
-    if (a->level != b->level || a->buf.use_count() > 1 || st->dataflow ||
+    // in place only on an exclusively owned buffer
+    if (a->level != b->level || a->buf.use_count() > 1 ||
         a->c1 - a->c0 != (ptrdiff_t)st->polyWords(a->level)) {
         a = EvalAdd(a, b);
         return;
@@ -1539,6 +1818,17 @@ void CryptoContextImpl<DCRTPoly>::EvalAddInPlace(Ciphertext<DCRTPoly>& a,
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalAdd(const Ciphertext<DCRTPoly>& a,
                                                          double c) {
     OpLock g(st.get());
+    if (a->pend && !a->def) {  // unrescaled rows: the constant at the product's scale
+        st->dep(a->buf.get());
+        const uint32_t ell = st->ellOf(a->level) + 1;
+        auto out = SfheInternal::newPendingCt(this, a->level, a->slots);
+        auto k = SfheInternal::constResidues(st.get(), c * a->scale, ell);
+        sfp_add_const(st->dev, out->c0, a->c0, k.data(), st->qmap(ell));
+        sfp_d2d(st->dev, out->c1, a->c1, (size_t)st->rows(ell) * st->n * 8);
+        st->stats.add++;
+        st->countBytes(4.0 * ell * st->n * 8);
+        return SfheInternal::traced(this, out, "EvalAdd");
+    }
     SfheInternal::deps(st.get(), {&a});
     const uint32_t ell = st->ellOf(a->level);
     auto out = SfheInternal::newCt(this, a->level, a->slots);
@@ -1581,6 +1871,7 @@ void CryptoContextImpl<DCRTPoly>::EvalAddInPlace(Ciphertext<DCRTPoly>& a, const 
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalSub(const Ciphertext<DCRTPoly>& a0,
                                                          const Ciphertext<DCRTPoly>& b0) {
     OpLock g(st.get());
+    if (auto r = SfheInternal::lazyAdd(this, a0, b0, true)) return SfheInternal::traced(this, r, "EvalSub");
     SfheInternal::deps(st.get(), {&a0, &b0});
     auto a = a0, b = b0;
     SfheInternal::align(this, a, b);
@@ -1604,6 +1895,15 @@ void CryptoContextImpl<DCRTPoly>::EvalSubInPlace(Ciphertext<DCRTPoly>& a,
 
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalNegate(const Ciphertext<DCRTPoly>& a) {
     OpLock g(st.get());
+    if (a->pend && !a->def) {
+        st->dep(a->buf.get());
+        const uint32_t ell = st->ellOf(a->level) + 1;
+        auto out = SfheInternal::newPendingCt(this, a->level, a->slots);
+        sfp_neg(st->dev, out->c0, a->c0, st->qmap(ell));
+        sfp_neg(st->dev, out->c1, a->c1, st->qmap(ell));
+        st->countBytes(4.0 * ell * st->n * 8);
+        return SfheInternal::traced(this, out, "EvalNegate");
+    }
     SfheInternal::deps(st.get(), {&a});
     const uint32_t ell = st->ellOf(a->level);
     auto out = SfheInternal::newCt(this, a->level, a->slots);
@@ -1680,6 +1980,17 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMult(const Ciphertext<DCRT
     auto k = SfheInternal::constResidues(s, K, ell);
     s->stats.constmult++;
     s->countBytes(4.0 * ell * s->n * 8);
+    if (SfheInternal::lazy(s)) {
+        auto op = std::make_shared<DeferredConstMult>();
+        op->pin = a->buf;
+        op->c0 = a->c0;
+        op->c1 = a->c1;
+        op->level = a->level;
+        op->slots = a->slots;
+        op->scale = a->scale;
+        op->k = std::move(k);
+        return SfheInternal::deferredCt(this, a->level + 1, a->slots, op);
+    }
     return SfheInternal::traced(this, SfheInternal::mulRescale(this, a, a->level, k.data(), nullptr, a->slots),
                                 "EvalMult");
 }
@@ -1695,9 +2006,20 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMult(const Ciphertext<DCRT
     SfheContextState* s = st.get();
     const uint32_t ell = s->ellOf(a->level);
     if (ell < 2) SFHE_THROW("no levels left (multiplicative depth exhausted)");
-    const uint64_t* m = SfheInternal::encoded(this, p, a->level);
     s->stats.ptmult++;
     s->countBytes(5.0 * ell * s->n * 8);
+    if (SfheInternal::lazy(s)) {
+        auto op = std::make_shared<DeferredPlainMult>();
+        op->pin = a->buf;
+        op->c0 = a->c0;
+        op->c1 = a->c1;
+        op->level = a->level;
+        op->slots = std::max(a->slots, p->slots);
+        op->scale = a->scale;
+        op->pt = p;
+        return SfheInternal::deferredCt(this, a->level + 1, op->slots, op);
+    }
+    const uint64_t* m = SfheInternal::encoded(this, p, a->level);
     return SfheInternal::traced(
         this, SfheInternal::mulRescale(this, a, a->level, nullptr, m, std::max(a->slots, p->slots)), "EvalMult");
 }
@@ -1725,6 +2047,13 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMult(const Ciphertext<DCRT
     s->stats.tensor++;
     s->countBytes(7.0 * ell * s->n * 8);
     const uint32_t slots = std::max(a->slots, b->slots);
+    if (SfheInternal::lazy(s) && SfheInternal::fusedRescale()) {
+        auto op = std::make_shared<DeferredRelin>();
+        op->t = t;
+        op->level = a->level;
+        op->slots = slots;
+        return SfheInternal::deferredCt(this, a->level + 1, slots, op);
+    }
     if (SfheInternal::fusedRescale())
         return SfheInternal::traced(this, SfheInternal::relinRescale(this, d0, d1, d2, a->level, slots),
                                     "EvalMult");
@@ -1755,8 +2084,20 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMultAddPlain(
         al[i] = SfheInternal::adjust(this, a[i], level);
         x0.push_back(al[i]->c0);
         x1.push_back(al[i]->c1);
-        m.push_back(SfheInternal::encoded(this, p[i], level));
     }
+    s->stats.ptmult += a.size();
+    if (SfheInternal::lazy(s)) {
+        auto op = std::make_shared<DeferredMacPlain>();
+        for (auto& c : al) op->pins.push_back(c->buf);
+        op->x0 = x0;
+        op->x1 = x1;
+        op->pts = p;
+        op->level = level;
+        op->slots = slots;
+        s->countBytes((3.0 * a.size() + 2.0) * ell * s->n * 8);
+        return SfheInternal::deferredCt(this, level + 1, slots, op);
+    }
+    for (size_t i = 0; i < a.size(); ++i) m.push_back(SfheInternal::encoded(this, p[i], level));
     const size_t pw = s->polyWords(level);
     auto tmp = s->alloc(2 * pw);
     uint64_t* t0 = tmp->ptr;
@@ -1773,7 +2114,6 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMultAddPlain(
             sfp_add(s->dev, t1, t1, part->ptr + pw, st->qmap(ell));
         }
     }
-    s->stats.ptmult += a.size();
     s->countBytes((3.0 * a.size() + 2.0) * ell * s->n * 8);
     return SfheInternal::traced(this, SfheInternal::rescale(this, t0, t1, level, slots), "EvalMultAddPlain");
 }
@@ -1784,17 +2124,24 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMultAddPlain(
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotate(const Ciphertext<DCRTPoly>& a,
                                                             int32_t r) {
     OpLock g(st.get());
-    SfheInternal::deps(st.get(), {&a});
     SfheContextState* s = st.get();
+    if (!(SfheInternal::lazy(s) && SfheInternal::isLazy(a))) SfheInternal::deps(s, {&a});
     uint32_t gal = GaloisForRotation(r);
     if (gal == 1) return a->Clone();
     auto it = s->rotKeys.find(gal);
     if (it == s->rotKeys.end())
         SFHE_THROW("EvalKey for index [" + std::to_string(gal) + "] (rotation " +
                    std::to_string(r) + ") is not found");
-    const uint32_t ell = s->ellOf(a->level);
-    auto out = SfheInternal::newCt(this, a->level, a->slots);
-    auto t = s->alloc(s->polyWords(a->level));
+    // a lazy product rotates before its rescale: the key switch's rounding is
+    // then divided by the prime the settling rescale drops
+    const bool pend = SfheInternal::lazy(s) && SfheInternal::isLazy(a);
+    if (pend) {
+        SfheInternal::materialize(*a, true);
+        s->dep(a->buf.get());
+    }
+    const uint32_t ell = SfheInternal::ctEll(s, *a);
+    auto out = pend ? SfheInternal::newPendingCt(this, a->level, a->slots) : SfheInternal::newCt(this, a->level, a->slots);
+    auto t = s->alloc((size_t)s->rows(ell) * s->n);
     sfp_automorph(s->dev, out->c0, a->c0, gal, st->qmap(ell));
     sfp_automorph(s->dev, t->ptr, a->c1, gal, st->qmap(ell));
     s->stats.automorph++;
@@ -1807,11 +2154,22 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotate(const Ciphertext<DC
 std::shared_ptr<FastRotationPrecomp> CryptoContextImpl<DCRTPoly>::EvalFastRotationPrecompute(
     const Ciphertext<DCRTPoly>& a) {
     OpLock g(st.get());
-    SfheInternal::deps(st.get(), {&a});
     SfheContextState* s = st.get();
+    // Pending rows are rotated as they are (see EvalRotate).  A deferred
+    // product is computed in canonical form first: its hoisted rotations
+    // feed plaintext products (the blind rotations), which would otherwise
+    // settle every rotated copy separately.
+    const bool pend = SfheInternal::lazy(s) && a->pend && !a->def;
+    if (pend) {
+        SfheInternal::materialize(*a, true);
+        s->dep(a->buf.get());
+    } else {
+        SfheInternal::deps(s, {&a});
+    }
     auto pre = std::make_shared<FastRotationPrecomp>();
-    const uint32_t ell = s->ellOf(a->level);
+    const uint32_t ell = SfheInternal::ctEll(s, *a);
     pre->level = a->level;
+    pre->pend = pend;
     pre->beta = (ell + s->alpha - 1) / s->alpha;
     if (s->world > 1) {
         pre->stride = (size_t)s->extmap(ell).count * s->n;
@@ -1831,22 +2189,29 @@ std::shared_ptr<FastRotationPrecomp> CryptoContextImpl<DCRTPoly>::EvalFastRotati
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalFastRotation(
     const Ciphertext<DCRTPoly>& a, int32_t r, uint32_t, const std::shared_ptr<FastRotationPrecomp>& pre) {
     OpLock g(st.get());
-    SfheInternal::deps(st.get(), {&a});
     SfheContextState* s = st.get();
+    if (pre && pre->pend) {  // the precomputation took a's unrescaled rows: so does the rotation
+        SfheInternal::materialize(*a, true);
+        s->dep(a->buf.get());
+    } else {
+        SfheInternal::deps(s, {&a});
+    }
     uint32_t gal = GaloisForRotation(r);
     if (gal == 1) return a->Clone();
-    if (!pre || pre->level != a->level) SFHE_THROW("fast-rotation precomputation does not match");
+    if (!pre || pre->level != a->level || pre->pend != a->pend)
+        SFHE_THROW("fast-rotation precomputation does not match");
     auto it = s->rotKeys.find(gal);
     if (it == s->rotKeys.end())
         SFHE_THROW("EvalKey for rotation " + std::to_string(r) + " is not found");
-    const uint32_t ell = s->ellOf(a->level);
+    const uint32_t ell = SfheInternal::ctEll(s, *a);
     // sigma commutes with the (coefficient-wise) base extension, so rotating
     // the extended digits equals extending the rotated c1.
     auto ext = s->alloc(pre->stride * pre->beta);
     // one permutation launch over every digit's rows (the map is prime-independent)
     const uint32_t rows = pre->beta * (uint32_t)(pre->stride / s->n);
     sfp_automorph(s->dev, ext->ptr, pre->ext->ptr, gal, sfp_limbs{rows, rows, 0, 0});
-    auto out = SfheInternal::newCt(this, a->level, a->slots);
+    auto out = pre->pend ? SfheInternal::newPendingCt(this, a->level, a->slots)
+                         : SfheInternal::newCt(this, a->level, a->slots);
     sfp_automorph(s->dev, out->c0, a->c0, gal, st->qmap(ell));
     SfheInternal::innerAndModDown(this, ext->ptr, pre->stride, pre->beta, ell, it->second,
                                   out->c0, out->c1, 1, 0);
@@ -1861,11 +2226,13 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalFastRotation(
 
 // sum_j w_j * (c0_j, c1_j) at `level` (canonical scale), then one rescale
 namespace {
-// residue of round(w * Delta_level) modulo each of the ell primes (weight of a
-// ciphertext at `level` whose product is rescaled to the next level)
+// residue of round(w * Delta_level^2 / inScale) modulo each of the ell primes:
+// the weight of a ciphertext of scale inScale (Delta_level unless an input of
+// a lower level enters unadjusted) whose product, at scale Delta_level^2, is
+// rescaled to the next level
 void weightResidues(const SfheContextState* s, double w, uint32_t level, uint32_t ell,
-                    std::vector<uint64_t>& kk) {
-    const double K = w * s->scale[level];
+                    std::vector<uint64_t>& kk, double inScale = 0.0) {
+    const double K = inScale > 0.0 ? w * s->scale[level] * (s->scale[level] / inScale) : w * s->scale[level];
     const double r = std::nearbyint(K);
     const bool neg = r < 0;
     const double a = std::fabs(r);
@@ -1886,18 +2253,19 @@ void weightResidues(const SfheContextState* s, double w, uint32_t level, uint32_
 
 std::vector<Ciphertext<DCRTPoly>> CryptoContextImpl<DCRTPoly>::LinearWSumRescaleMulti(
     const std::vector<const uint64_t*>& in0, const std::vector<const uint64_t*>& in1,
-    const std::vector<std::vector<double>>& w, uint32_t level, uint32_t slots) {
+    const std::vector<std::vector<double>>& w, uint32_t level, uint32_t slots, const std::vector<double>* inScale) {
     OpLock g(st.get());
     SfheContextState* s = st.get();
     const uint32_t ell = s->ellOf(level), n = s->n;
     const uint32_t nin = (uint32_t)in0.size(), nout = (uint32_t)w.size();
     if (ell < 2) SFHE_THROW("no levels left (multiplicative depth exhausted)");
     if (nin == 0 || nin > SFP_MAX_WSUM || nout == 0) SFHE_THROW("LinearWSumRescaleMulti: bad sizes");
+    if (inScale && inScale->size() != nin) SFHE_THROW("LinearWSumRescaleMulti: scale count");
     std::vector<uint64_t> kk;
     kk.reserve((size_t)nout * nin * s->rows(ell));
     for (const auto& row : w) {
         if (row.size() != nin) SFHE_THROW("LinearWSumRescaleMulti: weight row size");
-        for (double x : row) weightResidues(s, x, level, ell, kk);
+        for (uint32_t j = 0; j < nin; ++j) weightResidues(s, row[j], level, ell, kk, inScale ? (*inScale)[j] : 0.0);
     }
     const size_t pw = s->polyWords(level);  // words per polynomial
     auto sums = s->alloc((size_t)nout * 2 * pw);
@@ -1930,11 +2298,12 @@ std::vector<Ciphertext<DCRTPoly>> CryptoContextImpl<DCRTPoly>::LinearWSumRescale
 
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::LinearWSumRescale(
     const std::vector<const uint64_t*>& in0, const std::vector<const uint64_t*>& in1,
-    const std::vector<double>& w, uint32_t level, uint32_t slots) {
+    const std::vector<double>& w, uint32_t level, uint32_t slots, const std::vector<double>* inScale) {
     OpLock g(st.get());
     SfheContextState* s = st.get();
     const uint32_t ell = s->ellOf(level);
     if (ell < 2) SFHE_THROW("no levels left (multiplicative depth exhausted)");
+    if (inScale && inScale->size() != w.size()) SFHE_THROW("LinearWSumRescale: scale count");
     const size_t pw = s->polyWords(level);
     auto tmp = s->alloc(2 * pw);
     uint64_t* t0 = tmp->ptr;
@@ -1955,21 +2324,8 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::LinearWSumRescale(
         for (size_t j = done; j < done + take; ++j) {
             a0.push_back(in0[j]);
             a1.push_back(in1[j]);
-            double K = w[j] * s->scale[level];  // product scale Delta_l^2 -> rescale -> Delta_{l+1}
-            for (uint32_t i = 0; i < s->rows(ell); ++i) {
-                u64 q = s->primes[s->qprime(i)];
-                double r = std::nearbyint(K);
-                bool neg = r < 0;
-                double a = std::fabs(r);
-                u128 v;
-                if (a < 1.8e19) v = (u128)(u64)a;
-                else {
-                    double hi = std::floor(std::ldexp(a, -64));
-                    v = ((u128)(u64)hi << 64) + (u128)(u64)(a - std::ldexp(hi, 64));
-                }
-                u64 m = (u64)(v % q);
-                kk.push_back(neg ? (m ? q - m : 0) : m);
-            }
+            // product scale Delta_l^2 -> rescale -> Delta_{l+1}
+            weightResidues(s, w[j], level, ell, kk, inScale ? (*inScale)[j] : 0.0);
         }
         sfp_lin_wsum(s->dev, t0, a0.data(), kk.data(), (uint32_t)a0.size(), q);
         sfp_lin_wsum(s->dev, t1, a1.data(), kk.data(), (uint32_t)a1.size(), q);
@@ -1986,7 +2342,14 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::LinearWSumRescale(
 // level management
 
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::Rescale(const Ciphertext<DCRTPoly>& a) {
-    return a->Clone();  // automatic rescaling: nothing pending
+    Settle(a);  // a lazy product's pending rescale
+    return a->Clone();
+}
+
+void CryptoContextImpl<DCRTPoly>::Settle(const Ciphertext<DCRTPoly>& ct) {
+    if (!ct) return;
+    OpLock g(st.get());
+    SfheInternal::deps(st.get(), {&ct});
 }
 
 void CryptoContextImpl<DCRTPoly>::LevelReduceInPlace(Ciphertext<DCRTPoly>& a, std::nullptr_t,
@@ -2136,7 +2499,7 @@ bool CryptoContextImpl<DCRTPoly>::BeginCapture() {
     OpLock g(st.get());
     SfheContextState* s = st.get();
     if (s->capturing) SFHE_THROW("BeginCapture: a capture is already open");
-    if (s->forkedLanes || s->dataflow) SFHE_THROW("BeginCapture inside a lane region");
+    if (s->forkedLanes) SFHE_THROW("BeginCapture inside a lane region");
     if (s->world > 1) return false;  // collectives stay eager (host transports synchronise)
     sfp_sync(s->dev);
     if (sfp_capture_begin(s->dev) != 0) {
@@ -2144,6 +2507,7 @@ bool CryptoContextImpl<DCRTPoly>::BeginCapture() {
         return false;
     }
     s->capturing = true;
+    s->captureEpoch = ++s->epochCount;
     s->capAllocs.clear();
     // every cross-lane dependency inside the region must become a graph edge
     std::memset(s->synced, 0, sizeof s->synced);
@@ -2155,8 +2519,13 @@ std::shared_ptr<CryptoContextImpl<DCRTPoly>::CapturedGraph> CryptoContextImpl<DC
     OpLock lk(st.get());
     SfheContextState* s = st.get();
     if (!s->capturing) SFHE_THROW("EndCapture without BeginCapture");
+    // the graph must write the kept result's final rows: a lazy result is
+    // settled inside the region
+    if (keep) SfheInternal::deps(s, {&keep});
     sfp_graph* g = sfp_capture_end(s->dev);
     s->capturing = false;
+    if (!g) s->abandonedEpochs.insert(s->captureEpoch);  // its encodings are stale (encoded())
+    s->captureEpoch = 0;
     std::memset(s->synced, 0, sizeof s->synced);
     std::vector<std::pair<uint64_t*, size_t>> blocks;
     {
@@ -2204,7 +2573,7 @@ void CryptoContextImpl<DCRTPoly>::Launch(const std::shared_ptr<CapturedGraph>& g
     OpLock lk(st.get());
     SfheContextState* s = st.get();
     if (!g || !g->g) SFHE_THROW("Launch: no graph");
-    if (s->forkedLanes || s->dataflow) SFHE_THROW("Launch inside a lane region");
+    if (s->forkedLanes) SFHE_THROW("Launch inside a lane region");
     sfp_graph_launch(s->dev, g->g);
     // the graph ran (stream-ordered) on lane 0: so did every write it made
     if (g->keep) s->wrote(g->keep->buf.get());

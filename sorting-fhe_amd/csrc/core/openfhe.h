@@ -144,6 +144,7 @@ struct KeyPair {
 
 class DeviceBuffer;  // pooled device allocation (context.cpp)
 using DeviceBufferPtr = std::shared_ptr<DeviceBuffer>;
+struct DeferredOp;   // a product whose rescale awaits its consumer (context.cpp)
 
 // ---------------------------------------------------------------------------
 class EncodingParamsImpl {
@@ -204,13 +205,28 @@ class CiphertextImpl<DCRTPoly> {
     uint32_t level = 0;
     uint32_t slots = 0;
     double scale = 1.0;
+    // Lazy rescaling.  `level` is always the level AFTER the
+    // product's rescale (what GetLevel reports and the level tables count).
+    //  * def: the product is not computed yet (c0 / c1 unset); its first
+    //    consumer picks the form it can use;
+    //  * pend: the rows hold the product BEFORE its rescale (one limb more,
+    //    scale = the product's scale): rotations and sums run on that form, so
+    //    their key-switch and rescale rounding is divided away by the one
+    //    rescale that settles the result.
+    std::shared_ptr<DeferredOp> def;
+    bool pend = false;
 };
 
+// Key pairs carry a random 64-bit tag (OpenFHE's keyTag): evaluation keys,
+// ciphertexts and their serialized records name the key pair they belong to.
+std::string KeyTagString(uint64_t tag);
 template <>
 class PublicKeyImpl<DCRTPoly> {
   public:
     DeviceBufferPtr b, a;  // over Q (L+1 limbs), evaluation domain
     CryptoContext<DCRTPoly> cc;
+    uint64_t tag = 0;
+    std::string GetKeyTag() const { return KeyTagString(tag); }
 };
 template <>
 class PrivateKeyImpl<DCRTPoly> {
@@ -218,12 +234,15 @@ class PrivateKeyImpl<DCRTPoly> {
     DeviceBufferPtr s;            // over Q u P, evaluation domain
     std::vector<int8_t> ternary;  // coefficient form, for export / tests
     CryptoContext<DCRTPoly> cc;
+    uint64_t tag = 0;
+    std::string GetKeyTag() const { return KeyTagString(tag); }
 };
 
 // Hoisted-rotation digits (EvalFastRotationPrecompute result).
 struct FastRotationPrecomp {
     DeviceBufferPtr ext;
     uint32_t level = 0;
+    bool pend = false;  // taken of the ciphertext's unrescaled rows (one limb more)
     uint32_t beta = 0;
     size_t stride = 0;
 };
@@ -255,16 +274,22 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
     }
     void ClearEvalMultKeys();
     void ClearEvalAutomorphismKeys();
-    // Key serialization (OpenFHE's static forms: every registered context's
-    // keys are written, each record tagged with its context's fingerprint;
-    // deserialization installs them into the live context with that
-    // fingerprint).  keyTag is accepted and ignored (one key set per context).
+    // Key serialization (OpenFHE's static forms).  Each record names its
+    // context's parameter fingerprint and its key pair's tag; keyTag = ""
+    // writes the evaluation keys of every registered context, a tag only
+    // those of the key pair with that tag.  Deserialization installs a
+    // record into a context with the record's fingerprint that holds no key
+    // pair yet (the newest one: a context deserialized before its keys), or
+    // else into the context that holds the record's own key pair -- never
+    // into a context of another key pair.
     static bool SerializeEvalMultKey(std::ostream& os, SerType::Kind k, const std::string& keyTag = "");
     static bool DeserializeEvalMultKey(std::istream& is, SerType::Kind k);
     static bool SerializeEvalAutomorphismKey(std::ostream& os, SerType::Kind k, const std::string& keyTag = "");
     static bool DeserializeEvalAutomorphismKey(std::istream& is, SerType::Kind k);
     // parameter fingerprint: ring, prime chain, special primes, digits, scales
     uint64_t Fingerprint() const;
+    // tag of the key pair this context's evaluation keys belong to (0: none yet)
+    uint64_t KeyTag() const;
     const CCParams<CryptoContextCKKSRNS>& GetParams() const;
     uint32_t GetEnabledMask() const { return enabled; }
 
@@ -389,19 +414,28 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
     // Galois element for a left rotation by r.
     uint32_t GaloisForRotation(int32_t r) const;
     bool HasRotationKey(int32_t r) const;
-    // sum_j w_j * ct_j (given as c0/c1 device rows at `level`, canonical
-    // scale) followed by one rescale: the Chebyshev-leaf kernel.
+    // sum_j w_j * ct_j followed by one rescale to level + 1: the Chebyshev-
+    // leaf kernel.  ct_j is given as c0/c1 device rows; its first ellOf(level)
+    // rows are used, so an input at a LOWER level (more limbs) enters without
+    // a level adjustment: inScale[j] (its scale; nullptr: every input at
+    // Delta_level) is folded into its integer weight, which removes the
+    // adjustment's rescale and its rounding noise.
     Ciphertext<DCRTPoly> LinearWSumRescale(const std::vector<const uint64_t*>& in0,
                                            const std::vector<const uint64_t*>& in1,
                                            const std::vector<double>& w, uint32_t level,
-                                           uint32_t slots);
+                                           uint32_t slots, const std::vector<double>* inScale = nullptr);
     // Engine extension: nout weighted sums of the same inputs in one pass
     // (one multi-output kernel + one batched rescale); w[o] has nin weights.
     std::vector<Ciphertext<DCRTPoly>> LinearWSumRescaleMulti(
         const std::vector<const uint64_t*>& in0, const std::vector<const uint64_t*>& in1,
-        const std::vector<std::vector<double>>& w, uint32_t level, uint32_t slots);
+        const std::vector<std::vector<double>>& w, uint32_t level, uint32_t slots,
+        const std::vector<double>* inScale = nullptr);
     // Wait for all device work; throws on an asynchronous device error.
     void Synchronize();
+    // Lazy rescaling: compute / rescale ct's rows now (canonical form at its
+    // level); every evaluator entry point does this for inputs it cannot take
+    // unrescaled.  Needed only before reading c0 / c1 directly.
+    void Settle(const Ciphertext<DCRTPoly>& ct);
     // Engine extension: independent work on concurrent lanes (HIP streams).
     // ForkLanes(k) orders lanes 1..k-1 after everything issued so far on lane
     // 0; SetLane(i) routes the following operations to lane i; JoinLanes()
@@ -420,13 +454,6 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
     void ForkLanes(int count);
     void SetLane(int lane);
     void JoinLanes();
-    // Dataflow sub-region on helper lanes (lanes that are not primaries of the
-    // open region): returns {current lane, helpers...}, all ordered after the
-    // current lane.  Inside, operations may read results of other lanes (they
-    // wait for them device-side) and frees are deferred to JoinHelpers, which
-    // orders the parent lane after every helper.
-    std::vector<int> ForkHelpers();
-    void JoinHelpers(const std::vector<int>& lanes);
     // Plaintext-encoding cache across calls (default on); see DESIGN.md.
     void SetPlaintextCache(bool on);
     // Operation counters (for the roofline byte model).

@@ -5,9 +5,12 @@
 //
 // Record layout (little-endian):  "SFHE" | u32 version | u32 kind | u64
 // fingerprint | body.  A context record carries the parameters and the prime
-// chain (the chain is re-derived on load and must match); keys and
-// ciphertexts carry their device words.  A key / ciphertext record is bound
-// to the live context whose fingerprint it names.
+// chain (the chain is re-derived on load and must match); key and
+// ciphertext records carry their key pair's tag, then their device words,
+// whose counts are checked against the context's sizes before anything is
+// allocated.  A key record binds to a context of its fingerprint holding no
+// key pair yet (newest first), else to the one holding its own key pair; a
+// ciphertext record the other way round (openfhe.h, Serialize*Key).
 #include <algorithm>
 #include <cstring>
 #include <mutex>
@@ -18,19 +21,34 @@
 namespace lbcrypto {
 namespace {
 
-constexpr uint32_t kVersion = 1;
+constexpr uint32_t kVersion = 2;  // 2: key-pair tags in key / ciphertext records
 enum RecKind : uint32_t { R_CC = 1, R_PK = 2, R_SK = 3, R_CT = 4, R_MULT = 5, R_ROT = 6 };
 
 std::mutex g_regMu;
 std::vector<std::weak_ptr<CryptoContextImpl<DCRTPoly>>> g_registry;
 
-CryptoContext<DCRTPoly> findContext(uint64_t fp) {
+// The live context a record of fingerprint fp and key-pair tag `tag` binds
+// to: a context holding that key pair, or one holding none yet (which the
+// record then claims), in the order `keysFirst` gives; newest first within
+// each.  Never a context of another key pair.
+CryptoContext<DCRTPoly> findContext(uint64_t fp, uint64_t tag, bool freshFirst) {
     std::lock_guard<std::mutex> g(g_regMu);
-    for (auto it = g_registry.rbegin(); it != g_registry.rend(); ++it)  // newest first
-        if (auto cc = it->lock())
-            if (cc->Fingerprint() == fp) return cc;
+    for (int pass = 0; pass < 2; ++pass) {
+        const bool wantFresh = (pass == 0) == freshFirst;
+        for (auto it = g_registry.rbegin(); it != g_registry.rend(); ++it)
+            if (auto cc = it->lock()) {
+                if (cc->Fingerprint() != fp) continue;
+                SfheContextState* s = cc->state();
+                if (wantFresh && s->keyTag == 0) {
+                    s->keyTag = tag;
+                    return cc;
+                }
+                if (!wantFresh && tag && s->keyTag == tag) return cc;
+            }
+    }
     return nullptr;
 }
+
 
 template <class T>
 void put(std::ostream& os, const T& v) {
@@ -76,16 +94,26 @@ void putWords(std::ostream& os, SfheContextState* s, const uint64_t* p, size_t w
     put(os, (uint64_t)words);
     os.write(reinterpret_cast<const char*>(h.data()), (std::streamsize)(words * 8));
 }
-// stream -> a new pooled device buffer
-DeviceBufferPtr getWords(std::istream& is, SfheContextState* s, size_t expect = 0) {
+// stream -> a new pooled device buffer of exactly `expect` words (the size
+// the context implies: a record of another size is rejected before anything
+// is allocated); null on a short record or a failed allocation
+DeviceBufferPtr getWords(std::istream& is, SfheContextState* s, size_t expect) {
     uint64_t words = 0;
-    if (!get(is, words) || (expect && words != expect) || words > ((uint64_t)1 << 36)) return nullptr;
-    std::vector<uint64_t> h(words);
-    if (!is.read(reinterpret_cast<char*>(h.data()), (std::streamsize)(words * 8))) return nullptr;
-    auto b = s->alloc(words);
-    if (words) sfp_h2d(s->dev, b->ptr, h.data(), words * 8);
-    return b;
+    if (!get(is, words) || words != expect || !words) return nullptr;
+    try {
+        std::vector<uint64_t> h(words);
+        if (!is.read(reinterpret_cast<char*>(h.data()), (std::streamsize)(words * 8))) return nullptr;
+        auto b = s->alloc(words);
+        sfp_h2d(s->dev, b->ptr, h.data(), words * 8);
+        return b;
+    } catch (const std::exception&) {
+        return nullptr;
+    }
 }
+// word counts of the key kinds
+size_t pkWords(const SfheContextState* s) { return (size_t)(s->Lq + (s->ext ? 1 : 0)) * s->n; }
+size_t skWords(const SfheContextState* s) { return (size_t)s->tablePrimes() * s->n; }
+size_t switchKeyWords(const SfheContextState* s) { return (size_t)s->dnum * 2 * (s->Lq + s->K) * s->n; }
 
 }  // namespace
 
@@ -162,10 +190,8 @@ bool Serial::Deserialize(CryptoContext<DCRTPoly>& cc, std::istream& is, SerType:
     p.SetScalingTechnique((ScalingTechnique)tech);
     p.SetKeySwitchTechnique((KeySwitchTechnique)ks);
     p.SetSeed(seed);
-    if (auto live = findContext(fp)) {  // OpenFHE also returns the existing context
-        cc = live;
-        return true;
-    }
+    // always a context of its own: the key records that follow bind to it
+    // (a live context with the same parameters keeps its own key pair)
     auto c = GenCryptoContext(p);
     c->Enable(mask);
     if (c->state()->primes != primes || c->Fingerprint() != fp) {
@@ -182,6 +208,7 @@ bool Serial::Serialize(const PublicKey<DCRTPoly>& pk, std::ostream& os, SerType:
     SfheContextState* s = unsharded(pk->cc);
     OpLock g(s);
     header(os, R_PK, pk->cc->Fingerprint());
+    put(os, pk->tag);
     putWords(os, s, pk->b->ptr, pk->b->words);
     putWords(os, s, pk->a->ptr, pk->a->words);
     return os.good();
@@ -190,8 +217,9 @@ bool Serial::Serialize(const PublicKey<DCRTPoly>& pk, std::ostream& os, SerType:
 bool Serial::Deserialize(PublicKey<DCRTPoly>& pk, std::istream& is, SerType::Kind k) {
     if (!binaryOnly(k)) return false;
     uint64_t fp = 0;
-    if (!readHeader(is, R_PK, fp)) return false;
-    auto cc = findContext(fp);
+    uint64_t tag = 0;
+    if (!readHeader(is, R_PK, fp) || !get(is, tag) || !tag) return false;
+    auto cc = findContext(fp, tag, true);
     if (!cc) {
         std::cerr << "sfhe: no live crypto context matches the public key (deserialize the context first)"
                   << std::endl;
@@ -201,8 +229,9 @@ bool Serial::Deserialize(PublicKey<DCRTPoly>& pk, std::istream& is, SerType::Kin
     OpLock g(s);
     auto out = std::make_shared<PublicKeyImpl<DCRTPoly>>();
     out->cc = cc;
-    out->b = getWords(is, s);
-    out->a = out->b ? getWords(is, s, out->b->words) : nullptr;
+    out->tag = tag;
+    out->b = getWords(is, s, pkWords(s));
+    out->a = out->b ? getWords(is, s, pkWords(s)) : nullptr;
     if (!out->a) return false;
     pk = out;
     return true;
@@ -213,6 +242,7 @@ bool Serial::Serialize(const PrivateKey<DCRTPoly>& sk, std::ostream& os, SerType
     SfheContextState* s = unsharded(sk->cc);
     OpLock g(s);
     header(os, R_SK, sk->cc->Fingerprint());
+    put(os, sk->tag);
     putWords(os, s, sk->s->ptr, sk->s->words);
     put(os, (uint64_t)sk->ternary.size());
     os.write(reinterpret_cast<const char*>(sk->ternary.data()), (std::streamsize)sk->ternary.size());
@@ -222,14 +252,16 @@ bool Serial::Serialize(const PrivateKey<DCRTPoly>& sk, std::ostream& os, SerType
 bool Serial::Deserialize(PrivateKey<DCRTPoly>& sk, std::istream& is, SerType::Kind k) {
     if (!binaryOnly(k)) return false;
     uint64_t fp = 0;
-    if (!readHeader(is, R_SK, fp)) return false;
-    auto cc = findContext(fp);
+    uint64_t tag = 0;
+    if (!readHeader(is, R_SK, fp) || !get(is, tag) || !tag) return false;
+    auto cc = findContext(fp, tag, true);
     if (!cc) return false;
     SfheContextState* s = unsharded(cc);
     OpLock g(s);
     auto out = std::make_shared<PrivateKeyImpl<DCRTPoly>>();
     out->cc = cc;
-    out->s = getWords(is, s);
+    out->tag = tag;
+    out->s = getWords(is, s, skWords(s));
     uint64_t nt = 0;
     if (!out->s || !get(is, nt) || nt != s->n) return false;
     out->ternary.resize(nt);
@@ -243,8 +275,9 @@ bool Serial::Serialize(const Ciphertext<DCRTPoly>& ct, std::ostream& os, SerType
     if (!binaryOnly(k) || !ct) return false;
     SfheContextState* s = unsharded(ct->cc);
     OpLock g(s);
-    s->dep(ct->buf.get());
+    ct->cc->Settle(ct);  // a lazy product's rows, rescaled
     header(os, R_CT, ct->cc->Fingerprint());
+    put(os, s->keyTag);
     put(os, ct->level);
     put(os, ct->slots);
     put(os, ct->scale);
@@ -257,8 +290,9 @@ bool Serial::Serialize(const Ciphertext<DCRTPoly>& ct, std::ostream& os, SerType
 bool Serial::Deserialize(Ciphertext<DCRTPoly>& ct, std::istream& is, SerType::Kind k) {
     if (!binaryOnly(k)) return false;
     uint64_t fp = 0;
-    if (!readHeader(is, R_CT, fp)) return false;
-    auto cc = findContext(fp);
+    uint64_t tag = 0;
+    if (!readHeader(is, R_CT, fp) || !get(is, tag)) return false;
+    auto cc = findContext(fp, tag, false);
     if (!cc) {
         std::cerr << "sfhe: no live crypto context matches the ciphertext (deserialize the context first)"
                   << std::endl;
@@ -304,17 +338,21 @@ void forEachContext(F&& f) {
 }
 }  // namespace
 
-bool CryptoContextImpl<DCRTPoly>::SerializeEvalMultKey(std::ostream& os, SerType::Kind k, const std::string&) {
+bool CryptoContextImpl<DCRTPoly>::SerializeEvalMultKey(std::ostream& os, SerType::Kind k, const std::string& keyTag) {
     if (!binaryOnly(k)) return false;
+    auto want = [&](const CryptoContext<DCRTPoly>& c) {
+        return c->state()->relinKey && (keyTag.empty() || KeyTagString(c->state()->keyTag) == keyTag);
+    };
     uint32_t n = 0;
-    forEachContext([&](const CryptoContext<DCRTPoly>& c) { n += c->state()->relinKey ? 1 : 0; });
+    forEachContext([&](const CryptoContext<DCRTPoly>& c) { n += want(c) ? 1 : 0; });
     if (!n) return false;
     put(os, n);
     forEachContext([&](const CryptoContext<DCRTPoly>& c) {
+        if (!want(c)) return;
         SfheContextState* s = unsharded(c);
-        if (!s->relinKey) return;
         OpLock g(s);
         header(os, R_MULT, c->Fingerprint());
+        put(os, s->keyTag);
         putWords(os, s, s->relinKey->ptr, s->relinKey->words);
     });
     return os.good();
@@ -325,13 +363,13 @@ bool CryptoContextImpl<DCRTPoly>::DeserializeEvalMultKey(std::istream& is, SerTy
     uint32_t n = 0;
     if (!get(is, n) || !n) return false;
     for (uint32_t i = 0; i < n; ++i) {
-        uint64_t fp = 0;
-        if (!readHeader(is, R_MULT, fp)) return false;
-        auto cc = findContext(fp);
+        uint64_t fp = 0, tag = 0;
+        if (!readHeader(is, R_MULT, fp) || !get(is, tag) || !tag) return false;
+        auto cc = findContext(fp, tag, true);
         if (!cc) return false;
         SfheContextState* s = unsharded(cc);
         OpLock g(s);
-        auto key = getWords(is, s);
+        auto key = getWords(is, s, switchKeyWords(s));
         if (!key) return false;
         s->relinKey = key;
     }
@@ -339,17 +377,21 @@ bool CryptoContextImpl<DCRTPoly>::DeserializeEvalMultKey(std::istream& is, SerTy
 }
 
 bool CryptoContextImpl<DCRTPoly>::SerializeEvalAutomorphismKey(std::ostream& os, SerType::Kind k,
-                                                               const std::string&) {
+                                                               const std::string& keyTag) {
     if (!binaryOnly(k)) return false;
+    auto want = [&](const CryptoContext<DCRTPoly>& c) {
+        return !c->state()->rotKeys.empty() && (keyTag.empty() || KeyTagString(c->state()->keyTag) == keyTag);
+    };
     uint32_t n = 0;
-    forEachContext([&](const CryptoContext<DCRTPoly>& c) { n += c->state()->rotKeys.empty() ? 0 : 1; });
+    forEachContext([&](const CryptoContext<DCRTPoly>& c) { n += want(c) ? 1 : 0; });
     if (!n) return false;
     put(os, n);
     forEachContext([&](const CryptoContext<DCRTPoly>& c) {
+        if (!want(c)) return;
         SfheContextState* s = unsharded(c);
-        if (s->rotKeys.empty()) return;
         OpLock g(s);
         header(os, R_ROT, c->Fingerprint());
+        put(os, s->keyTag);
         put(os, (uint32_t)s->rotKeys.size());
         for (auto& kv : s->rotKeys) {
             put(os, kv.first);
@@ -366,9 +408,9 @@ bool CryptoContextImpl<DCRTPoly>::DeserializeEvalAutomorphismKey(std::istream& i
     uint32_t n = 0;
     if (!get(is, n) || !n) return false;
     for (uint32_t i = 0; i < n; ++i) {
-        uint64_t fp = 0;
-        if (!readHeader(is, R_ROT, fp)) return false;
-        auto cc = findContext(fp);
+        uint64_t fp = 0, tag = 0;
+        if (!readHeader(is, R_ROT, fp) || !get(is, tag) || !tag) return false;
+        auto cc = findContext(fp, tag, true);
         if (!cc) return false;
         SfheContextState* s = unsharded(cc);
         OpLock g(s);
@@ -376,8 +418,8 @@ bool CryptoContextImpl<DCRTPoly>::DeserializeEvalAutomorphismKey(std::istream& i
         if (!get(is, nk)) return false;
         for (uint32_t j = 0; j < nk; ++j) {
             uint32_t gal = 0;
-            if (!get(is, gal)) return false;
-            auto key = getWords(is, s);
+            if (!get(is, gal) || !(gal & 1) || gal >= 2 * s->n) return false;
+            auto key = getWords(is, s, switchKeyWords(s));
             if (!key) return false;
             s->rotKeys[gal] = key;
         }

@@ -26,9 +26,19 @@ class DeviceBuffer {
     uint64_t region;               // fork/join region it was allocated in (0: none)
     uint64_t seq = 0;              // position of its last write in lane's sequence
     sfp_event* ready = nullptr;    // shared encodings: end of the producing work
+    uint64_t readyEpoch = 0;       // capture epoch `ready` was recorded in (0: none)
+    uint64_t capEpoch = 0;         // capture epoch it was allocated in (0: none)
 };
 
 struct BootstrapPrecomp;  // bootstrap.cpp
+
+// A product whose rescale is deferred to its first consumer (lazy
+// rescaling, context.cpp): run() fills ct's rows either in the canonical
+// form (the fused product + rescale) or, pending = true, before the rescale.
+struct DeferredOp {
+    virtual ~DeferredOp() = default;
+    virtual void run(CryptoContextImpl<DCRTPoly>* cc, CiphertextImpl<DCRTPoly>& ct, bool pending) = 0;
+};
 
 struct PtCacheEntry {
     std::vector<std::complex<double>> values;
@@ -63,7 +73,9 @@ struct SfheContextState {
     std::vector<std::vector<uint64_t>> qInvTable;  // [ell][i] = q_{ell-1}^{-1} mod q_i
     uint32_t tablePrimes() const { return Lq + K + (ext ? 1 : 0); }
 
-    // keys
+    // keys (of the key pair tagged keyTag; 0 until a key generation or a
+    // deserialized key record claims the context)
+    uint64_t keyTag = 0;
     DeviceBufferPtr relinKey;
     std::map<uint32_t, DeviceBufferPtr> rotKeys;  // galois -> key
     std::set<int32_t> rotIndices;
@@ -80,15 +92,10 @@ struct SfheContextState {
     // after them, so any lane may reuse them (without this, blocks a lane
     // allocates migrate to lane 0 at every join and the pool grows per region)
     std::map<size_t, std::vector<uint64_t*>> forkPool;
-    int dataflowParent = -1;  // helpers of a dataflow sub-region may reuse its free blocks
     int lane = 0;          // lane new work goes to
     int forkedLanes = 0;   // > 0 while a fork/join region is open
     uint64_t region = 0;   // id of the open region (0: none)
     uint64_t regionCount = 0;
-    // dataflow sub-regions (cross-lane reads allowed; every free is deferred
-    // to the sub-join, where the parent lane has waited for all helpers)
-    int dataflow = 0;
-    std::vector<std::pair<size_t, uint64_t*>> dataflowFree;
     // cross-lane ordering: laneSeq[l] counts writes issued on lane l;
     // synced[h][x] = laneSeq[x] at the last time lane h waited for lane x
     uint64_t laneSeq[SFP_MAX_LANES] = {};
@@ -116,6 +123,8 @@ struct SfheContextState {
     // size); blocks owned by a live graph are never recycled by the pool --
     // graphOwned[p] = true while a DeviceBuffer still holds p
     bool capturing = false;
+    uint64_t captureEpoch = 0, epochCount = 0;  // id of the open capture (0: none)
+    std::set<uint64_t> abandonedEpochs;         // captures that were abandoned (their work never ran)
     std::vector<std::pair<uint64_t*, size_t>> capAllocs;
     std::unordered_map<uint64_t*, bool> graphOwned;
 
@@ -135,6 +144,10 @@ struct SfheContextState {
 
     // ---- helpers ----
     uint32_t ellOf(uint32_t level) const { return Lq - level; }
+    // scale of a product whose rescale to `level` is pending: Delta_level
+    // times the prime that rescale drops (products of canonical operands at
+    // level - 1 have exactly this scale: Delta_l^2 = Delta_{l+1} q)
+    double preScale(uint32_t level) const { return scale[level] * (double)primes[ellOf(level)]; }
     // local rows among the first `count` limbs of a set dealt round-robin
     uint32_t owned(uint32_t count) const {
         return (uint32_t)rank < count ? (count - rank + world - 1) / world : 0;

@@ -116,7 +116,7 @@ struct sfp_dev {
     u64 *ninv = nullptr, *ninvS = nullptr;
     // FP64 twiddles for primes < 2^42 (exact doubles w and rounded w/q), and
     // per-prime 1/q and n^-1 as doubles
-    double *psiD = nullptr, *psiQ = nullptr, *ipsiD = nullptr, *ipsiQ = nullptr;
+    double *psiD = nullptr, *ipsiD = nullptr;
     double *qinvD = nullptr, *ninvD = nullptr, *ninvQ = nullptr;
     std::vector<sf_barrett> hbar;
     // pinned argument ring (host) mirrored on the device
@@ -347,25 +347,11 @@ __device__ __forceinline__ uint32_t nttLocal(const NttTile& T, uint32_t st, uint
 //       bytes); staging them cost more occupancy than it saved, so the ROW
 //       rounds read the table directly (index 2^S + (x0 >> (8 - k))).
 constexpr uint32_t kNttColTw = 512;  // 2^logR - 1 entries, logR <= 9
-#ifndef SFHE_NTT_ROW_LDS
-#define SFHE_NTT_ROW_LDS 0  // measured slower (+4 ms/sort at SFHE_NTT_FP=2): the rounds are not twiddle-latency bound
-#endif
-constexpr bool kNttRowLdsBuild = SFHE_NTT_ROW_LDS != 0;
 template <bool COL>
 __device__ __forceinline__ uint32_t twIndex(const NttTile& T, uint32_t S0, uint32_t k, uint32_t x0) {
     if (COL) return (1u << k) - 1 + (x0 >> (T.logn - k));
     return (1u << (S0 + k)) + (x0 >> (8 - k));
 }
-// ROW pass, FP64 rows: the tile's 8 rows need, at stage k, the contiguous
-// table run [2^(S0+k) + r0 2^k, + 8 2^k) -- 2040 doubles over the 8 stages,
-// staged in LDS with the tile (one load latency instead of one per round):
-// stage k's run at LDS offset 8 (2^k - 1).
-constexpr uint32_t kNttRowTw = (kNttTile / 256) * 255;
-template <int TILE>
-__device__ __forceinline__ uint32_t twIndexRowLds(const NttTile& T, uint32_t k, uint32_t x0) {
-    return (TILE / 256) * ((1u << k) - 1) + (x0 >> (8 - k)) - (T.r0 << k);
-}
-
 // One round: stages k0..k0+B-1 of the pass (k relative to the pass's first
 // global stage S0).  8/2^B groups of 2^B words per thread.
 template <bool INV, bool COL, int LE, int B, int TILE>
@@ -487,10 +473,12 @@ __device__ __forceinline__ double fpReduce(double v, double q, double qinv) {
 // of the kernel (ROW pass, see k_ntt), so the round does not wait on HBM.
 // DC > 0: the pass's stage count is the compile-time DC (== T.d), so with an
 // unrolled round loop every shift and mask below folds to a constant.
+// W/q is formed from W in registers (half the twiddle bytes of a W/q table;
+// a last-bit difference only moves the lazy quotient estimate by < 2^-6, and
+// the outputs are canonical either way).
 template <bool INV, bool COL, int LE, int B, int TILE, bool PF = false, int DC = 0>
 __device__ __forceinline__ void nttRoundFP(double* s, const NttTile& T, uint32_t S0, uint32_t k0, double q,
-                                           const double* w, const double* wq, double qinv, bool rowLds,
-                                           const double* pw = nullptr, bool wqCalc = false) {
+                                           const double* w, double qinv, const double* pw = nullptr) {
     constexpr int M = 1 << B;
     constexpr int GPT = (1 << LE) / M;
     const uint32_t d = DC ? (uint32_t)DC : T.d;
@@ -526,15 +514,11 @@ __device__ __forceinline__ void nttRoundFP(double* s, const NttTile& T, uint32_t
         } else {
 #pragma unroll
             for (int t = 0; t < B; ++t) {
-                const uint32_t tb =
-                    (!COL && rowLds) ? twIndexRowLds<TILE>(T, k0 + t, x0) : twIndex<COL>(T, S0, k0 + t, x0);
+                const uint32_t tb = twIndex<COL>(T, S0, k0 + t, x0);
 #pragma unroll
                 for (int qd = 0; qd < (1 << t); ++qd) {
                     W[(1 << t) - 1 + qd] = w[tb + qd];
-                    // ROW twiddles come from HBM: form W/q here (half the bytes).  A
-                    // last-bit difference from the table only moves the lazy
-                    // quotient estimate by < 2^-6; outputs are canonical either way.
-                    WQ[(1 << t) - 1 + qd] = (COL && !wqCalc) ? wq[tb + qd] : W[(1 << t) - 1 + qd] * qinv;
+                    WQ[(1 << t) - 1 + qd] = W[(1 << t) - 1 + qd] * qinv;
                 }
             }
         }
@@ -576,16 +560,15 @@ __device__ __forceinline__ void nttRoundFP(double* s, const NttTile& T, uint32_t
 
 template <bool INV, bool COL, int LE, int TILE>
 __device__ __forceinline__ void nttRoundDynFP(int b, double* s, const NttTile& T, uint32_t S0, uint32_t k0,
-                                              double q, const double* w, const double* wq, double qinv,
-                                              bool rowLds, bool wqCalc) {
+                                              double q, const double* w, double qinv) {
     if constexpr (LE >= 4) {
-        if (b == 4) return nttRoundFP<INV, COL, LE, 4, TILE>(s, T, S0, k0, q, w, wq, qinv, rowLds, nullptr, wqCalc);
+        if (b == 4) return nttRoundFP<INV, COL, LE, 4, TILE>(s, T, S0, k0, q, w, qinv);
     }
     if constexpr (LE >= 3) {
-        if (b == 3) return nttRoundFP<INV, COL, LE, 3, TILE>(s, T, S0, k0, q, w, wq, qinv, rowLds, nullptr, wqCalc);
+        if (b == 3) return nttRoundFP<INV, COL, LE, 3, TILE>(s, T, S0, k0, q, w, qinv);
     }
-    if (b == 2) return nttRoundFP<INV, COL, LE, 2, TILE>(s, T, S0, k0, q, w, wq, qinv, rowLds, nullptr, wqCalc);
-    nttRoundFP<INV, COL, LE, 1, TILE>(s, T, S0, k0, q, w, wq, qinv, rowLds, nullptr, wqCalc);
+    if (b == 2) return nttRoundFP<INV, COL, LE, 2, TILE>(s, T, S0, k0, q, w, qinv);
+    nttRoundFP<INV, COL, LE, 1, TILE>(s, T, S0, k0, q, w, qinv);
 }
 
 
@@ -644,16 +627,11 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_b
                                                   const u64* __restrict__ ninv,
                                                   const u64* __restrict__ ninvS, uint32_t logn,
                                                   const double* __restrict__ twD,
-                                                  const double* __restrict__ twQ,
                                                   const double* __restrict__ qinvD,
                                                   const double* __restrict__ ninvD,
                                                   const double* __restrict__ ninvQ, int useFp) {
     __shared__ u64 s[TILE];
-    __shared__ u64 tW[COL ? kNttColTw : 1], tX[COL ? kNttColTw : 1];  // COL twiddles (value, Shoup or W/q)
-    // ROW pass, FP64 rows, when SFHE_NTT_ROW_LDS: the tile's twiddle runs
-    // (stage k: 2^k entries per row) staged with the tile, one load latency
-    // instead of one per register round
-    __shared__ u64 tR[(COL || !kNttRowLdsBuild) ? 1 : (TILE / 256) * 255];
+    __shared__ u64 tW[COL ? kNttColTw : 1], tX[COL ? kNttColTw : 1];  // COL twiddles (value; Shoup for integer rows)
 #ifdef SFHE_NTT_TRACE
     unsigned long long tprev = clock64();
 #endif
@@ -665,7 +643,7 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_b
     if (G.skipEll && ii >= G.alpha * pp && ii < min(G.alpha * (pp + 1), G.skipEll)) return;
     const uint32_t prime = primeOf(G.pm, ii);
     const u64 q = bar[prime].q;
-    const bool fp = (useFp & 7) && q < kFpPrimeBound;  // uniform per block (bits 3-4: A/B knobs)
+    const bool fp = useFp && q < kFpPrimeBound;  // uniform per block
     NttTile T;
     T.logn = logn;
     T.d = COL ? logR : 8u;
@@ -680,37 +658,25 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_b
     T.r0 = COL ? 0u : tile * (TILE / 256);
     const uint32_t S0 = COL ? 0u : logR;
 
-    // the pass's twiddle table (value, Shoup companion or W/q) for this prime
+    // the pass's twiddle table for this prime: FP64 values (W/q is formed in
+    // registers) or integer values with their Shoup companions
     const u64* gw = fp ? reinterpret_cast<const u64*>(twD) + (size_t)prime * n : tw + (size_t)prime * n;
-    const u64* gx = fp ? reinterpret_cast<const u64*>(twQ) + (size_t)prime * n : twS + (size_t)prime * n;
-    // FP64 COL rounds form W/q from W (as the ROW rounds do) instead of
-    // staging the table's W/q: half the twiddle loads of the prologue
-    // (useFp bit 6, SFHE_NTT_COL_WQ=0, stages the table for A/B runs)
-    const bool wqCalc = COL && fp && !(useFp & 64);
+    const u64* gx = twS + (size_t)prime * n;
     if (COL) {  // entries [1, 2^logR) -> LDS
         for (uint32_t e = threadIdx.x; e < (1u << logR) - 1; e += (TILE >> LE)) {
             tW[e] = gw[e + 1];
-            if (!wqCalc) tX[e] = gx[e + 1];
+            if (!fp) tX[e] = gx[e + 1];
         }
     }
-    const bool rowLds = kNttRowLdsBuild && !COL && fp && (useFp & 7) >= 2;
-    if (rowLds) {
-        constexpr uint32_t rowsT = TILE / 256;
-        for (uint32_t k = 0; k < 8; ++k) {
-            const uint32_t len = rowsT << k;
-            const u64* src = gw + (1u << (S0 + k)) + (T.r0 << k);
-            for (uint32_t j = threadIdx.x; j < len; j += (TILE >> LE)) tR[rowsT * ((1u << k) - 1) + j] = src[j];
-        }
-    }
-    const u64* rw = COL ? tW : (rowLds ? tR : gw);
+    const u64* rw = COL ? tW : gw;
     const u64* rx = COL ? tX : gx;
     // ROW pass, FP64 rows, one group per thread per round (LE = 2): every
     // round's twiddles are data-independent, so all 4 x 3 of them are loaded
     // here, in flight together with the tile, instead of one HBM latency per
-    // register round (useFp bit 3 turns this off for A/B runs).
+    // register round.
     constexpr bool kPfBuild = !COL && LE == 2;
     constexpr int kPfRounds = 8 / 2;
-    const bool rowPf = kPfBuild && fp && !rowLds && !(useFp & 8);
+    const bool rowPf = kPfBuild && fp;
     double PW[kPfBuild ? kPfRounds * 3 : 1];
     if constexpr (kPfBuild) {
         if (rowPf) {
@@ -790,27 +756,23 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_b
             for (int ri = 0; ri < kPfRounds; ++ri) {
                 const int r = INV ? kPfRounds - 1 - ri : ri;
                 nttRoundFP<INV, false, 2, 2, TILE, true, 8>(reinterpret_cast<double*>(s), T, S0, 2 * r,
-                                                            (double)q, nullptr, nullptr, qinvD[prime], false,
-                                                            PW + 3 * r);
+                                                            (double)q, nullptr, qinvD[prime], PW + 3 * r);
                 __syncthreads();
                 NTT_MARK(1 + ri);
             }
         }
     }
     // COL pass over 2^8 rows (ring 2^16), FP64 rows, LE = 2: the same four
-    // rounds unrolled with compile-time strides (twiddles already in LDS);
-    // useFp bit 4 (SFHE_NTT_COL_UNROLL=0) keeps the generic loop for A/B runs.
+    // rounds unrolled with compile-time strides (twiddles already in LDS).
     constexpr bool kColUnrollBuild = COL && LE == 2;
-    const bool colUnroll = kColUnrollBuild && fp && T.d == 8u && !(useFp & 16);
+    const bool colUnroll = kColUnrollBuild && fp && T.d == 8u;
     if constexpr (kColUnrollBuild) {
         if (colUnroll) {
 #pragma unroll
             for (int ri = 0; ri < 4; ++ri) {
                 const int r = INV ? 3 - ri : ri;
                 nttRoundFP<INV, true, 2, 2, TILE, false, 8>(reinterpret_cast<double*>(s), T, S0, 2 * r, (double)q,
-                                                            reinterpret_cast<const double*>(rw),
-                                                            reinterpret_cast<const double*>(rx), qinvD[prime],
-                                                            false, nullptr, wqCalc);
+                                                            reinterpret_cast<const double*>(rw), qinvD[prime]);
                 __syncthreads();
                 NTT_MARK(1 + ri);
             }
@@ -822,8 +784,7 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_b
         const int b = (int)min((uint32_t)LE, T.d - k0);
         if (fp)
             nttRoundDynFP<INV, COL, LE, TILE>(b, reinterpret_cast<double*>(s), T, S0, k0, (double)q,
-                                        reinterpret_cast<const double*>(rw), reinterpret_cast<const double*>(rx),
-                                        qinvD[prime], rowLds, wqCalc);
+                                              reinterpret_cast<const double*>(rw), qinvD[prime]);
         else
             nttRoundDyn<INV, COL, LE, TILE>(b, s, T, S0, k0, q, rw, rx);
         __syncthreads();
@@ -841,8 +802,6 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_b
     const bool emK = epi && G.emK;
     const u64 emk = emK ? G.emK[ii] : 0, emkS = emK ? G.emKS[ii] : 0;
     const sf_barrett EB = emul ? loadBar(bar, prime) : sf_barrett{};
-    const bool wt = (useFp & 32) != 0;  // SFHE_NTT_WT=1: write-through output stores (A/B knob)
-    const auto orsrc = __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)(n * 8u), 0x00020000);
 #pragma unroll
     for (int k = 0; k < (1 << LE) / 2; ++k) {
         const uint32_t e = 2 * (threadIdx.x + k * (TILE >> LE));
@@ -894,19 +853,7 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_b
                 x.y = sf_add(x.y, sf_mul_shoup(o.y, ek2, ek2S, q), q);
             }
         }
-        if (wt) {
-            // write-through (sc1): the pass leaves no dirty L2 lines for the
-            // kernel boundary's writeback
-            typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-            v4u v;
-            v.x = (unsigned)x.x;
-            v.y = (unsigned)(x.x >> 32);
-            v.z = (unsigned)x.y;
-            v.w = (unsigned)(x.y >> 32);
-            __builtin_amdgcn_raw_buffer_store_b128(v, orsrc, (int)(g * 8), 0, 16);
-        } else {
-            *reinterpret_cast<ulonglong2*>(out + g) = x;
-        }
+        *reinterpret_cast<ulonglong2*>(out + g) = x;
     }
     NTT_MARK(5);
 #ifdef SFHE_NTT_TRACE
@@ -1328,14 +1275,31 @@ struct ConvJobs {
     ConvJob j[kMaxConvJobs];
 };
 
+// Exact centred conversion (every centred use is a ModDown): the overflow
+// v = round(sum_i y_i / s_i) of the centred y_i, estimated in FP64 with the
+// oracle's operations in the oracle's order (oracle/prims_ref.c conv_rows),
+// so out_t = sum_i y_i mod_i,t - v prod(S) is x's centred residue itself and
+// ModDown keeps only its rounding.  yd: y_i as a correctly rounded double.
+__device__ __forceinline__ double centredY(u64 y, u64 q) {
+    return (double)(y > (q >> 1) ? (long long)y - (long long)q : (long long)y);
+}
+// out - m * sprod  (m: signed multiple count)
+__device__ __forceinline__ u64 subMultiple(u64 out, long long m, u64 sprod, const sf_barrett& B) {
+    if (m > 0) return sf_sub(out, bmul((u64)m, sprod, B), B.q);
+    if (m < 0) return sf_add(out, bmul((u64)(-m), sprod, B), B.q);
+    return out;
+}
+
 // One integer-path target row for two adjacent coefficients from canonical
-// source residues ya/yb (centred: prod(S) subtracted once per y > q/2).
+// source residues ya/yb.  centred: the exact centred conversion, with the
+// overflow estimates va / vb (the number of y > q/2 is added here).
 template <int NS>
 __device__ __forceinline__ ulonglong2 convIntTarget(const u64 (&ya)[NS], const u64 (&yb)[NS], uint32_t ns,
                                                     const u64* smodCol, int stride, const sf_barrett* sB,
-                                                    const sf_barrett& B, u64 sprod, bool centred) {
+                                                    const sf_barrett& B, u64 sprod, bool centred, long long va = 0,
+                                                    long long vb = 0) {
     Acc s0{0, 0}, s1{0, 0};
-    u64 na = 0, nb = 0;
+    long long na = va, nb = vb;
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
         if ((uint32_t)i < ns) {
@@ -1350,22 +1314,36 @@ __device__ __forceinline__ ulonglong2 convIntTarget(const u64 (&ya)[NS], const u
         }
     }
     ulonglong2 o;
-    o.x = sf_reduce128_acc(s0.lo, s0.hi, &B);
-    o.y = sf_reduce128_acc(s1.lo, s1.hi, &B);
-    if (na) o.x = sf_sub(o.x, bmul(na, sprod, B), B.q);
-    if (nb) o.y = sf_sub(o.y, bmul(nb, sprod, B), B.q);
+    o.x = subMultiple(sf_reduce128_acc(s0.lo, s0.hi, &B), na, sprod, B);
+    o.y = subMultiple(sf_reduce128_acc(s1.lo, s1.hi, &B), nb, sprod, B);
     return o;
+}
+
+// v for two coefficients from canonical residues (integer kernels)
+template <int NS>
+__device__ __forceinline__ void convOverflow(const u64 (&ya)[NS], const u64 (&yb)[NS], uint32_t ns,
+                                             const sf_barrett* sB, const double* sQi, long long& va, long long& vb) {
+    double aa = 0.0, ab = 0.0;
+#pragma unroll
+    for (int i = 0; i < NS; ++i)
+        if ((uint32_t)i < ns) {
+            aa = fma(centredY(ya[i], sB[i].q), sQi[i], aa);
+            ab = fma(centredY(yb[i], sB[i].q), sQi[i], ab);
+        }
+    va = (long long)rint(aa);
+    vb = (long long)rint(ab);
 }
 
 // Integer form: two adjacent coefficients per thread, every constant staged
 // in LDS (the output stores may alias global tables, which would otherwise
 // force a reload of each per-target constant after every store).
 __global__ __launch_bounds__(kThreads) void k_conv(const ConvJobs J, const sf_barrett* __restrict__ bar,
-                                                   uint32_t logn) {
+                                                   const double* __restrict__ qinvD, uint32_t logn) {
     constexpr int C = kConvChunk, NS = kMaxConvSrc;
     __shared__ u64 smod[NS * C];
     __shared__ sf_barrett sB[NS], tB[C];
     __shared__ u64 sInv[NS], tSp[C];
+    __shared__ double sQi[NS];
     __shared__ uint32_t tRow[C];
     const ConvJob& c = J.j[blockIdx.y];
     const uint32_t t0 = blockIdx.z * C;
@@ -1375,6 +1353,7 @@ __global__ __launch_bounds__(kThreads) void k_conv(const ConvJobs J, const sf_ba
     if (threadIdx.x < ns) {
         sB[threadIdx.x] = loadBar(bar, c.sidx[threadIdx.x]);
         sInv[threadIdx.x] = c.inv[threadIdx.x];
+        sQi[threadIdx.x] = qinvD[c.sidx[threadIdx.x]];
     } else if (threadIdx.x >= 64 && threadIdx.x < 64 + tc) {
         const uint32_t k = threadIdx.x - 64, t = t0 + k;
         tB[k] = loadBar(bar, c.didx[t]);
@@ -1398,8 +1377,10 @@ __global__ __launch_bounds__(kThreads) void k_conv(const ConvJobs J, const sf_ba
             yb[i] = bmul(v.y, sInv[i], B);
         }
     }
+    long long va = 0, vb = 0;
+    if (c.centered) convOverflow<NS>(ya, yb, ns, sB, sQi, va, vb);
     for (uint32_t k = 0; k < tc; ++k) {
-        const ulonglong2 o = convIntTarget<NS>(ya, yb, ns, smod + k, C, sB, tB[k], tSp[k], c.centered);
+        const ulonglong2 o = convIntTarget<NS>(ya, yb, ns, smod + k, C, sB, tB[k], tSp[k], c.centered, va, vb);
         *reinterpret_cast<ulonglong2*>(c.dst + ((size_t)tRow[k] << logn) + x) = o;
     }
 }
@@ -1454,6 +1435,8 @@ __global__ __launch_bounds__(kThreads) void k_convf(const ConvJobs J, const sf_b
     __shared__ uint32_t tRow[C], sBig[NS];
     __shared__ u64 yL[NS * X];     // FP64 blocks: doubles' bits; integer blocks: residues
     __shared__ double yH[NB * X];  // 60-bit sources' high parts
+    __shared__ double vL[X];       // centred: the overflow v of each coefficient
+    __shared__ double tSpD[C], tSpQ[C];
     const ConvJob& c = J.j[blockIdx.y];
     const uint32_t fpChunks = (c.nFp + C - 1) / C;
     const bool fpBlock = blockIdx.z < fpChunks;
@@ -1478,6 +1461,8 @@ __global__ __launch_bounds__(kThreads) void k_convf(const ConvJobs J, const sf_b
         tB[k] = loadBar(bar, c.didx[t]);
         tQi[k] = qinvD[c.didx[t]];
         tSp[k] = c.sprod[t];
+        tSpD[k] = (double)c.sprod[t];
+        tSpQ[k] = tSpD[k] / (double)tB[k].q;
         tRow[k] = c.drow[t];
     }
     for (uint32_t e = threadIdx.x; e < ns * tc; e += kThreads) {
@@ -1515,6 +1500,25 @@ __global__ __launch_bounds__(kThreads) void k_convf(const ConvJobs J, const sf_b
         }
     }
     __syncthreads();
+    if (cen) {  // exact centred conversion: v = rint(sum_i y_i / s_i) per coefficient (convOverflow)
+        for (uint32_t cx = threadIdx.x; cx < X; cx += kThreads) {
+            double acc = 0.0;
+#pragma unroll
+            for (int i = 0; i < NS; ++i)
+                if ((uint32_t)i < ns) {
+                    double yd;
+                    if (!fpBlock)
+                        yd = centredY(yL[i * X + cx], sB[i].q);
+                    else if (sBig[i] == 0xffffffffu)
+                        yd = __longlong_as_double(yL[i * X + cx]);
+                    else  // yh 2^30 + yl, correctly rounded as (double)(long long) y
+                        yd = fma(yH[sBig[i] * X + cx], 1073741824.0, __longlong_as_double(yL[i * X + cx]));
+                    acc = fma(yd, sQi[i], acc);
+                }
+            vL[cx] = rint(acc);
+        }
+        __syncthreads();
+    }
     // phase 2: wave w takes coefficients [64w, 64w+64) of every target.
     // FP64 targets go kConvTpi at a time: each y read from LDS feeds
     // kConvTpi independent product chains (ILP; a quarter of the y reads).
@@ -1526,10 +1530,12 @@ __global__ __launch_bounds__(kThreads) void k_convf(const ConvJobs J, const sf_b
         for (uint32_t it = w; it < items; it += WAVES) {
             const uint32_t cx = (it % CH) * 64 + lane, k = (it / CH) * kConvTpi;
             double a[kConvTpi], pd[kConvTpi];
+            const double nv = cen ? -vL[cx] : 0.0;
 #pragma unroll
             for (int u = 0; u < kConvTpi; ++u) {
-                a[u] = 0.0;
-                pd[u] = (double)tB[min(k + u, tc - 1)].q;
+                const uint32_t kk = min(k + u, tc - 1);
+                pd[u] = (double)tB[kk].q;
+                a[u] = cen ? fpMulMod(nv, tSpD[kk], tSpQ[kk], pd[u]) : 0.0;
             }
 #pragma unroll
             for (int i = 0; i < NS; ++i)
@@ -1560,7 +1566,7 @@ __global__ __launch_bounds__(kThreads) void k_convf(const ConvJobs J, const sf_b
         u64 out;
         {
             Acc s0{0, 0};
-            u64 neg = 0;
+            long long neg = cen ? (long long)vL[cx] : 0;
 #pragma unroll
             for (int i = 0; i < NS; ++i) {
                 if ((uint32_t)i < ns) {
@@ -1569,8 +1575,7 @@ __global__ __launch_bounds__(kThreads) void k_convf(const ConvJobs J, const sf_b
                     neg += cen && y > (sB[i].q >> 1);
                 }
             }
-            out = sf_reduce128_acc(s0.lo, s0.hi, &B);
-            if (neg) out = sf_sub(out, bmul(neg, tSp[k], B), B.q);
+            out = subMultiple(sf_reduce128_acc(s0.lo, s0.hi, &B), neg, tSp[k], B);
         }
         c.dst[((size_t)tRow[k] << logn) + x0 + cx] = out;
     }
@@ -1602,11 +1607,12 @@ struct MdrsArgs {
 
 // Integer form, two coefficients per thread, constants in LDS.
 __global__ __launch_bounds__(kThreads) void k_conv_mdrs(const MdrsArgs A, const sf_barrett* __restrict__ bar,
-                                                        uint32_t logn) {
+                                                        const double* __restrict__ qinvD, uint32_t logn) {
     constexpr int C = kConvChunk, W = C + 1, NS = kMaxConvSrc;  // column C: the dropped row l
     __shared__ u64 smod[NS * W];
     __shared__ sf_barrett sB[NS], tB[W];
     __shared__ u64 sInv[NS], tSp[W], tPm[W], tLs[W];
+    __shared__ double sQi[NS];
     const MdrsJob& J = A.j[blockIdx.y];
     const uint32_t t0 = blockIdx.z * C;
     if (t0 >= A.l) return;
@@ -1615,6 +1621,7 @@ __global__ __launch_bounds__(kThreads) void k_conv_mdrs(const MdrsArgs A, const 
     if (threadIdx.x < ns) {
         sB[threadIdx.x] = loadBar(bar, A.sidx[threadIdx.x]);
         sInv[threadIdx.x] = A.inv[threadIdx.x];
+        sQi[threadIdx.x] = qinvD[A.sidx[threadIdx.x]];
     } else if (threadIdx.x >= 64 && threadIdx.x < 64 + W && (threadIdx.x - 64 < tc || threadIdx.x - 64 == C)) {
         const uint32_t k = threadIdx.x - 64, tt = k < tc ? t0 + k : A.l;
         tB[k] = loadBar(bar, tt);
@@ -1642,15 +1649,17 @@ __global__ __launch_bounds__(kThreads) void k_conv_mdrs(const MdrsArgs A, const 
             yb[i] = bmul(v.y, sInv[i], B);
         }
     }
+    long long va, vb;
+    convOverflow<NS>(ya, yb, ns, sB, sQi, va, vb);
     // the dropped row: r = (a_l - conv_l) * P^-1 mod q_l
     const sf_barrett BL = tB[C];
-    const ulonglong2 cl = convIntTarget<NS>(ya, yb, ns, smod + C, W, sB, BL, tSp[C], true);
+    const ulonglong2 cl = convIntTarget<NS>(ya, yb, ns, smod + C, W, sB, BL, tSp[C], true, va, vb);
     const ulonglong2 al = *reinterpret_cast<const ulonglong2*>(J.al + ((size_t)A.l << logn) + x);
     const u64 ra = bmul(sf_sub(al.x, cl.x, BL.q), A.pinvl, BL), rb = bmul(sf_sub(al.y, cl.y, BL.q), A.pinvl, BL);
     const bool na = ra > (BL.q >> 1), nb = rb > (BL.q >> 1);
     for (uint32_t k = 0; k < tc; ++k) {
         const sf_barrett B = tB[k];
-        ulonglong2 v = convIntTarget<NS>(ya, yb, ns, smod + k, W, sB, B, tSp[k], true);
+        ulonglong2 v = convIntTarget<NS>(ya, yb, ns, smod + k, W, sB, B, tSp[k], true, va, vb);
         u64 la = sf_reduce128(ra, 0, &B), lb = sf_reduce128(rb, 0, &B);
         if (na) la = sf_sub(la, tLs[k], B.q);
         if (nb) lb = sf_sub(lb, tLs[k], B.q);
@@ -1680,7 +1689,8 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
     __shared__ double sInvD[NS], sInvQ[NS], sQi[NS], tQi[C], tPd[C], tPq[C];
     __shared__ u64 tSp[C], tPm[C], tLs[C];
     __shared__ uint32_t tRow[C];
-    __shared__ double yL[NS * X], rL[X];
+    __shared__ double yL[NS * X], rL[X], vL[X];
+    __shared__ double tSpD[C], tSpQ[C];
     const MdrsJob& J = A.j[blockIdx.y];
     const uint32_t fpChunks = (A.nFp + C - 1) / C;
     const bool fpBlock = blockIdx.z < fpChunks;
@@ -1703,6 +1713,8 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
         tB[k] = loadBar(bar, t);
         tQi[k] = qinvD[t];
         tSp[k] = A.sprod[t];
+        tSpD[k] = (double)A.sprod[t];
+        tSpQ[k] = tSpD[k] / (double)tB[k].q;
         tPm[k] = A.pmod[t];
         tLs[k] = A.lsub[t];
         tPd[k] = A.pmodD[t];
@@ -1728,7 +1740,15 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
     __syncthreads();
     const double qld = (double)bar[A.l].q;
     for (uint32_t cx = threadIdx.x; cx < X; cx += kThreads) {  // the dropped row: r = (a_l - conv_l) * P^-1 mod q_l, centred
-        double cl = 0.0;
+        // exact centred conversion: the overflow v (convOverflow), removed from every target
+        double acc = 0.0;
+#pragma unroll
+        for (int i = 0; i < NS; ++i)
+            if ((uint32_t)i < ns) acc = fma(yL[i * X + cx], sQi[i], acc);
+        const double v = rint(acc);
+        vL[cx] = v;
+        const double spl = (double)A.sprod[A.l];
+        double cl = fpMulMod(-v, spl, spl / qld, qld);
 #pragma unroll
         for (int i = 0; i < NS; ++i)
             if ((uint32_t)i < ns) cl += fpMulMod(yL[i * X + cx], sLD[i], sLQ[i], qld);
@@ -1744,13 +1764,13 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
         const uint32_t items = CH * ((tc + kConvTpi - 1) / kConvTpi);
         for (uint32_t it = w; it < items; it += WAVES) {
             const uint32_t cx = (it % CH) * 64 + lane, k = (it / CH) * kConvTpi;
-            const double r = rL[cx];
+            const double r = rL[cx], nv = -vL[cx];
             double a[kConvTpi], pd[kConvTpi];
 #pragma unroll
             for (int u = 0; u < kConvTpi; ++u) {
                 const uint32_t kk = min(k + u, tc - 1);
                 pd[u] = (double)tB[kk].q;
-                a[u] = fpMulMod(r, tPd[kk], tPq[kk], pd[u]);
+                a[u] = fpMulMod(r, tPd[kk], tPq[kk], pd[u]) + fpMulMod(nv, tSpD[kk], tSpQ[kk], pd[u]);
             }
 #pragma unroll
             for (int i = 0; i < NS; ++i)
@@ -1774,7 +1794,7 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
         {
             const sf_barrett B = tB[k];
             Acc s0{0, 0};
-            u64 neg = 0;
+            long long neg = (long long)vL[cx];
 #pragma unroll
             for (int i = 0; i < NS; ++i) {
                 if ((uint32_t)i < ns) {
@@ -1783,8 +1803,7 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
                     neg += y < 0.0;
                 }
             }
-            out = sf_reduce128_acc(s0.lo, s0.hi, &B);
-            if (neg) out = sf_sub(out, bmul(neg, tSp[k], B), B.q);
+            out = subMultiple(sf_reduce128_acc(s0.lo, s0.hi, &B), neg, tSp[k], B);
             u64 lift = sf_reduce128((u64)(r < 0.0 ? r + qld : r), 0, &B);
             if (r < 0.0) lift = sf_sub(lift, tLs[k], B.q);
             out = sf_add(out, bmul(lift, tPm[k], B), B.q);
@@ -2095,8 +2114,7 @@ sfp_dev* sfp_create(int device, const sfp_tables* t) {
               hipMalloc(&d->ipsi, tn) == hipSuccess && hipMalloc(&d->ipsiS, tn) == hipSuccess &&
               hipMalloc(&d->ninv, d->np * 8) == hipSuccess &&
               hipMalloc(&d->ninvS, d->np * 8) == hipSuccess && hipMalloc(&d->psiD, tn) == hipSuccess &&
-              hipMalloc(&d->psiQ, tn) == hipSuccess && hipMalloc(&d->ipsiD, tn) == hipSuccess &&
-              hipMalloc(&d->ipsiQ, tn) == hipSuccess && hipMalloc(&d->qinvD, d->np * 8) == hipSuccess &&
+              hipMalloc(&d->ipsiD, tn) == hipSuccess && hipMalloc(&d->qinvD, d->np * 8) == hipSuccess &&
               hipMalloc(&d->ninvD, d->np * 8) == hipSuccess && hipMalloc(&d->ninvQ, d->np * 8) == hipSuccess;
     d->ringCap = (size_t)16 << 20;
     d->bounceCap = (size_t)32 << 20;
@@ -2118,23 +2136,15 @@ sfp_dev* sfp_create(int device, const sfp_tables* t) {
     hostToDev(d, d->ninv, t->n_inv, d->np * 8);
     hostToDev(d, d->ninvS, t->n_inv_shoup, d->np * 8);
     {
-        std::vector<double> a((size_t)d->np * d->n), b((size_t)d->np * d->n), qi(d->np), ni(d->np), nq(d->np);
-        auto fill = [&](const uint64_t* tab, double* A, double* Bq) {
-            for (uint32_t p = 0; p < d->np; ++p) {
-                const double q = (double)d->hbar[p].q;
-                for (uint32_t k = 0; k < d->n; ++k) {
-                    const size_t o = (size_t)p * d->n + k;
-                    A[o] = (double)tab[o];
-                    Bq[o] = (double)tab[o] / q;
-                }
-            }
+        // FP64 twiddle values (the kernels form W/q in registers)
+        std::vector<double> a((size_t)d->np * d->n), qi(d->np), ni(d->np), nq(d->np);
+        auto fill = [&](const uint64_t* tab, double* A) {
+            for (size_t o = 0; o < (size_t)d->np * d->n; ++o) A[o] = (double)tab[o];
         };
-        fill(t->psi_rev, a.data(), b.data());
+        fill(t->psi_rev, a.data());
         hostToDev(d, d->psiD, a.data(), tn);
-        hostToDev(d, d->psiQ, b.data(), tn);
-        fill(t->ipsi_rev, a.data(), b.data());
+        fill(t->ipsi_rev, a.data());
         hostToDev(d, d->ipsiD, a.data(), tn);
-        hostToDev(d, d->ipsiQ, b.data(), tn);
         for (uint32_t p = 0; p < d->np; ++p) {
             const double q = (double)d->hbar[p].q;
             qi[p] = 1.0 / q;
@@ -2201,7 +2211,7 @@ void sfp_destroy(sfp_dev* d) {
     hipFree(d->ipsiS);
     hipFree(d->ninv);
     hipFree(d->ninvS);
-    for (double* x : {d->psiD, d->psiQ, d->ipsiD, d->ipsiQ, d->qinvD, d->ninvD, d->ninvQ}) hipFree(x);
+    for (double* x : {d->psiD, d->ipsiD, d->qinvD, d->ninvD, d->ninvQ}) hipFree(x);
     hipFree(d->dring);
     hipHostFree(d->hring);
     hipHostFree(d->bounce);
@@ -2298,26 +2308,14 @@ const char* sfp_last_error(sfp_dev* d) {
 }
 
 // ---- NTT ----
-// FP64 butterflies for primes < 2^42 (SFHE_NTT_FP=0 selects the integer path)
-// A/B knobs for k_ntt: bit 3 (SFHE_NTT_ROW_PF=0) turns off the ROW pass's
-// register twiddle prefetch, bit 4 (SFHE_NTT_COL_UNROLL=0) the unrolled COL rounds.
+// FP64 butterflies for primes < 2^42 (SFHE_NTT_FP=0 runs every row on the
+// integer path, which 60-bit primes always take)
 static int nttFp() {
     static const int on = [] {
         const char* v = std::getenv("SFHE_NTT_FP");
-        return v ? std::atoi(v) : SFHE_NTT_FP;
+        return (v ? std::atoi(v) : SFHE_NTT_FP) ? 1 : 0;
     }();
     return on;
-}
-static int nttFlags() {
-    static const int f = [] {
-        const char* pf = std::getenv("SFHE_NTT_ROW_PF");
-        const char* cu = std::getenv("SFHE_NTT_COL_UNROLL");
-        const char* wt = std::getenv("SFHE_NTT_WT");
-        const char* cq = std::getenv("SFHE_NTT_COL_WQ");
-        return nttFp() | ((pf && std::atoi(pf) == 0) ? 8 : 0) | ((cu && std::atoi(cu) == 0) ? 16 : 0) |
-               ((wt && std::atoi(wt) != 0) ? 32 : 0) | ((cq && std::atoi(cq) == 0) ? 64 : 0);
-    }();
-    return f;
 }
 
 static RowGroup rowsOf(uint32_t P, uint32_t R, sfp_limbs pm) {
@@ -2350,7 +2348,6 @@ static void nttRows(sfp_dev* d, const RowGroup& G, int inverse) {
     const u64* tw = inverse ? d->ipsi : d->psi;
     const u64* twS = inverse ? d->ipsiS : d->psiS;
     const double* twD = inverse ? d->ipsiD : d->psiD;
-    const double* twQ = inverse ? d->ipsiQ : d->psiQ;
     // Launches over few rows are latency-bound (a one-limb pass is one tile
     // round trip per block: ~1.5 us load, ~1 us per register round, tools/
     // microbench with SFHE_NTT_TRACE): up to SFHE_NTT_T1K_ROWS rows (default
@@ -2377,7 +2374,7 @@ static void nttRows(sfp_dev* d, const RowGroup& G, int inverse) {
     auto pass = [&](auto kern, int threads) {
         timedLaunch(d, SFP_FAM_NTT, bytes, [&] {
             hipLaunchKernelGGL(kern, g, dim3(threads), 0, d->st(), G, d->bar, tw, twS, d->ninv,
-                               d->ninvS, d->logn, twD, twQ, d->qinvD, d->ninvD, d->ninvQ, nttFlags());
+                               d->ninvS, d->logn, twD, d->qinvD, d->ninvD, d->ninvQ, nttFp());
         });
     };
     static const int le = [] {  // SFHE_NTT_LE: register-round width experiments (2, 3, 4)
@@ -3026,14 +3023,6 @@ static ConvJob convJob(const sfp_conv* c, u64* dst, const u64* src, uint32_t ntU
     return j;
 }
 
-// SFHE_CONV_NS13=0 (A/B knob): every FP64 conversion on the NS = 16 kernels
-static bool convNs13() {
-    static const bool on = [] {
-        const char* v = std::getenv("SFHE_CONV_NS13");
-        return !(v && std::atoi(v) == 0);
-    }();
-    return on;
-}
 
 static void convLaunch(sfp_dev* d, const ConvJobs& J, uint32_t njobs, bool fpOk) {
     if (!njobs) return;
@@ -3053,14 +3042,14 @@ static void convLaunch(sfp_dev* d, const ConvJobs& J, uint32_t njobs, bool fpOk)
     timedLaunch(d, SFP_FAM_CONV, bytes, [&] {
         // NS = 13 (ModDown's K P-rows, ModUp digits of <= 13 primes) sizes the
         // LDS for 6 blocks per CU instead of 5 (the loops keep their guards)
-        if (fp && maxS <= 13 && convNs13())
+        if (fp && maxS <= 13)
             hipLaunchKernelGGL(k_convf<13>, g, dim3(kThreads), 0, d->st(), J, d->bar, d->qinvD, d->logn);
         else if (fp && maxS <= 16)
             hipLaunchKernelGGL(k_convf<16>, g, dim3(kThreads), 0, d->st(), J, d->bar, d->qinvD, d->logn);
         else if (fp)
             hipLaunchKernelGGL(k_convf<kMaxConvSrc>, g, dim3(kThreads), 0, d->st(), J, d->bar, d->qinvD, d->logn);
         else
-            hipLaunchKernelGGL(k_conv, g, dim3(kThreads), 0, d->st(), J, d->bar, d->logn);
+            hipLaunchKernelGGL(k_conv, g, dim3(kThreads), 0, d->st(), J, d->bar, d->qinvD, d->logn);
     });
     checkLaunch(d, "conv");
 }
@@ -3231,14 +3220,14 @@ void sfp_moddown_rescale(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint6
     }
     const dim3 g(fp ? n / kConvCoefs : n / (2 * kThreads), 2, zc);
     timedLaunch(d, SFP_FAM_CONV, 8.0 * n * 2 * (K + 1 + l), [&] {
-        if (fp && c->ns <= 13 && convNs13())  // LDS for 6 blocks per CU (as convLaunch)
+        if (fp && c->ns <= 13)  // LDS for 6 blocks per CU (as convLaunch)
             hipLaunchKernelGGL(k_mdrsf<13>, g, dim3(kThreads), 0, d->st(), M, d->bar, d->qinvD, d->logn);
         else if (fp && c->ns <= 16)
             hipLaunchKernelGGL(k_mdrsf<16>, g, dim3(kThreads), 0, d->st(), M, d->bar, d->qinvD, d->logn);
         else if (fp)
             hipLaunchKernelGGL(k_mdrsf<kMaxConvSrc>, g, dim3(kThreads), 0, d->st(), M, d->bar, d->qinvD, d->logn);
         else
-            hipLaunchKernelGGL(k_conv_mdrs, g, dim3(kThreads), 0, d->st(), M, d->bar, d->logn);
+            hipLaunchKernelGGL(k_conv_mdrs, g, dim3(kThreads), 0, d->st(), M, d->bar, d->qinvD, d->logn);
     });
     checkLaunch(d, "conv_mdrs");
     // out_i = (acc_i - NTT(y_i)) (P q_l)^-1 + d_i q_l^-1

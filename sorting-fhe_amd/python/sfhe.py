@@ -37,6 +37,7 @@ ABI_SYMBOLS = [
     "sfhe_comm_uid", "sfhe_shard_rccl", "sfhe_shard_host", "sfhe_pool_bytes",
     "sfhe_serialize_lanes", "sfhe_sorter_graph_nodes", "sfhe_sorter_create_rot",
     "sfhe_sorter_sort_hybrid1", "sfhe_hybrid1_params", "sfhe_sorter_graph_ntt_time",
+    "sfhe_sorter_sort_hybrid", "sfhe_hybrid_params", "sfhe_sorter_place_2n",
     "sfhe_bootstrap_setup", "sfhe_bootstrap_depth", "sfhe_bootstrap",
     "sfhe_sorter_sort_bitonic", "sfhe_kway_sort", "sfhe_kway_params",
     "sfhe_save", "sfhe_load", "sfhe_ct_save", "sfhe_ct_load",
@@ -123,6 +124,9 @@ _SIGS = {
     "sfhe_sorter_create_rot": (C.c_int, [_VP, _U32, C.c_int, _PI32, _SZ, _PVP]),
     "sfhe_sorter_sort_hybrid1": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_int, _PVP]),
     "sfhe_hybrid1_params": (C.c_int, [_U32, _PU32, _PI32, _SZ, _PSZ]),
+    "sfhe_sorter_sort_hybrid": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_int, C.c_int, _PVP]),
+    "sfhe_hybrid_params": (C.c_int, [_U32, C.c_int, _PU32, _PI32, _SZ, _PSZ]),
+    "sfhe_sorter_place_2n": (C.c_int, [_VP, _VP, _VP, _PVP]),
     "sfhe_sorter_sort_bitonic": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_int, _PVP]),
     "sfhe_save": (C.c_int, [_VP, C.c_char_p]),
     "sfhe_kway_create": (C.c_int, [_VP, _U32, C.c_int, C.c_int, _PVP]),
@@ -473,6 +477,15 @@ class Sorter:
         """DirectSort<N>::sort_hybrid1 (reference sort_algo.h:1213-1229)."""
         return self.eng._new(self.eng.lib.sfhe_sorter_sort_hybrid1, self.h, ct.h, n, dg, df)
 
+    def sort_hybrid(self, ct: Ct, n: int = 3, dg: int = 2, df: int = 2, variant: int = 0) -> Ct:
+        """DirectSort<N>::sort_hybrid (variant 0, reference sort_algo.h:1049-1062) or
+        sort_hybrid2 (variant 2, :1376-1389)."""
+        return self.eng._new(self.eng.lib.sfhe_sorter_sort_hybrid, self.h, ct.h, variant, n, dg, df)
+
+    def place_2n(self, rank: Ct, ct: Ct) -> Ct:
+        """DirectSort<N>::rotationIndexCheck2N (reference sort_algo.h:587-656)."""
+        return self.eng._new(self.eng.lib.sfhe_sorter_place_2n, self.h, rank.h, ct.h)
+
     def sort_bitonic(self, ct: Ct, n: int = 4, dg: int = 3, df: int = 3) -> Ct:
         """BitonicSort<N>::sort (reference sort_algo.h:1421-1486); values in [0, 255]."""
         return self.eng._new(self.eng.lib.sfhe_sorter_sort_bitonic, self.h, ct.h, n, dg, df)
@@ -528,6 +541,20 @@ def kway_params(N: int, backend: str = "hip"):
     buf = (C.c_int32 * cnt.value)()
     lib.sfhe_kway_params(N, None, None, None, None, buf, cnt.value, None)
     return b.value, d.value, (b0.value, b1.value), list(buf)
+
+
+def hybrid_params(N: int, variant: int = 0, backend: str = "hip"):
+    """(depth, rotation keys) of tests/DirectSortHTest.cpp (variant 0) or
+    tests/DirectSortH2Test.cpp (variant 2) for N."""
+    lib = load(backend)
+    depth = C.c_uint32()
+    cnt = C.c_size_t()
+    rc = lib.sfhe_hybrid_params(N, variant, C.byref(depth), None, 0, C.byref(cnt))
+    if rc != SFHE_OK:
+        raise SfheError(f"sfhe error {rc}: {lib.sfhe_last_error().decode()}")
+    buf = (C.c_int32 * cnt.value)()
+    lib.sfhe_hybrid_params(N, variant, None, buf, cnt.value, None)
+    return depth.value, list(buf)
 
 
 def hybrid1_params(N: int, backend: str = "hip"):

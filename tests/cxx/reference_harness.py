@@ -40,6 +40,11 @@ LIBS = {
 PROGRAMS = {
     "DirectSortTest": (["tests/DirectSortTest.cpp"], True, True),
     "DirectSortH1Test": (["tests/DirectSortH1Test.cpp"], True, True),
+    "DirectSortHTest": (["tests/DirectSortHTest.cpp"], True, True),
+    "DirectSortH2Test": (["tests/DirectSortH2Test.cpp"], True, True),
+    "DirectSortNTest": (["tests/DirectSortNTest.cpp"], True, False),
+    "SincTest": (["tests/SincTest.cpp"], False, False),
+    "DirectSortBenchmark": (["benchmarks/DirectSortBenchmark.cpp"], False, False),
     "CompareTest": (["tests/CompareTest.cpp"], False, False),
     "SignTest": (["tests/SignTest.cpp"], False, False),
     "RotationTest": (["tests/RotationTest.cpp"], True, False),
@@ -82,9 +87,9 @@ def build_own():
         for backend, (libdir, lib) in LIBS.items():
             exe = os.path.join(OUT, f"{name}_{backend}")
             os.makedirs(OUT, exist_ok=True)
-            if not (os.path.exists(exe) and os.path.getmtime(exe) >= max(os.path.getmtime(src), _engine_mtime())):
-                subprocess.run(["g++"] + flags() + [src, "-o", exe, "-L" + libdir, "-l" + lib,
-                                                    "-Wl,-rpath," + libdir, "-lpthread"], check=True)
+            if not _fresh(exe, src):
+                _atomic(["g++"] + flags() + [src, "-o"], exe,
+                        ["-L" + libdir, "-l" + lib, "-Wl,-rpath," + libdir, "-lpthread"])
             built[(name, backend)] = exe
     return built
 
@@ -93,13 +98,32 @@ def available() -> bool:
     return os.path.isdir(os.path.join(REF, "tests")) and os.path.isfile(os.path.join(REF, "tests", "DirectSortTest.cpp"))
 
 
+def _forwarders() -> str:
+    """Include directory of one-line forwarding headers to reference sources
+    the engine does not re-provide: src/sort.h (SortContext, the FHERMA-style
+    serialized I/O glue of src/main.cpp) calls only the lbcrypto facade, so
+    the reference's own file is compiled where it lies (its quote-includes of
+    sort_algo.h / sign.h / comparison.h / openfhe.h resolve to the engine's
+    headers through -I-)."""
+    d = os.path.join(OUT, "forward")
+    os.makedirs(d, exist_ok=True)
+    for name, target in {"sort.h": os.path.join(REF, "src", "sort.h")}.items():
+        text = f'#include "{target}"\n'
+        path = os.path.join(d, name)
+        if not (os.path.exists(path) and open(path).read() == text):
+            with open(path, "w") as f:
+                f.write(text)
+    return d
+
+
 def flags():
     # -I- first: #include "x" never resolves next to the including source
-    # file, so the reference's src/main.cpp picks up this engine's sort.h /
+    # file, so the reference's src/main.cpp picks up this engine's
     # sort_algo.h, not the reference's own (every -I after it serves both
     # include forms; libstdc++'s pstl headers quote-include their siblings,
     # hence their directory)
     return ["-O2", "-std=c++17", "-fopenmp", "-DENABLE_PRINT_PT", "-I-",
+            "-I" + _forwarders(),
             "-I" + os.path.join(CSRC, "core"), "-I" + os.path.join(CSRC, "algo"), "-I" + os.path.join(CSRC, "algo", "k-way"),
             "-I" + CSRC,
             "-I" + os.path.join(ROOT, "include"), "-I" + SHIM, "-I" + os.path.join(REF, "tests"),
@@ -108,11 +132,24 @@ def flags():
             "-I" + PSTL, "-w"]
 
 
+def _fresh(out: str, *deps: str) -> bool:
+    return os.path.exists(out) and os.path.getmtime(out) >= max([os.path.getmtime(d) for d in deps] +
+                                                                [_engine_mtime()])
+
+
+def _atomic(cmd_before_out, out, cmd_after_out=()):
+    """Run a compiler writing to a private temp name, then rename over `out`:
+    concurrent pytest-xdist workers never see a half-written file."""
+    tmp = f"{out}.tmp{os.getpid()}"
+    subprocess.run(list(cmd_before_out) + [tmp] + list(cmd_after_out), check=True)
+    os.replace(tmp, out)
+
+
 def compile_obj(src: str, obj: str):
     os.makedirs(os.path.dirname(obj), exist_ok=True)
-    if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), _engine_mtime()):
+    if _fresh(obj, src):
         return
-    subprocess.run(["g++"] + flags() + ["-c", src, "-o", obj], check=True)
+    _atomic(["g++"] + flags() + ["-c", src, "-o"], obj)
 
 
 def build(jobs: int = 8, programs=None):
@@ -145,8 +182,9 @@ def build(jobs: int = 8, programs=None):
             o.append(objs["memory_tracker"])
         for backend, (libdir, lib) in LIBS.items():
             exe = os.path.join(OUT, f"{p}_{backend}")
-            subprocess.run(["g++", "-fopenmp", "-o", exe] + o +
-                           ["-L" + libdir, "-l" + lib, "-Wl,-rpath," + libdir, "-lpthread"], check=True)
+            if not _fresh(exe, *o):
+                _atomic(["g++", "-fopenmp", "-o"], exe,
+                        o + ["-L" + libdir, "-l" + lib, "-Wl,-rpath," + libdir, "-lpthread"])
             built[(p, backend)] = exe
     return built
 

@@ -48,6 +48,7 @@ def test_bootstrap_depth_model(oracle_lib):
 
 @pytest.mark.parametrize("S,budget,bound", [(8, (2, 2), 2.0 ** -20), (64, (3, 1), 2.0 ** -16),
                                              (512, (3, 3), 2.0 ** -13)])
+@pytest.mark.slow
 def test_bootstrap_sparse_slots(oracle_lib, S, budget, bound):
     """One bootstrap at ring 2^12, scale 2^59 (the reference's bootstrapping
     scale, BitonicSortTest.cpp:17 / kway_adapter.h:45-46).  The error grows
@@ -59,6 +60,7 @@ def test_bootstrap_sparse_slots(oracle_lib, S, budget, bound):
     assert err < bound
 
 
+@pytest.mark.slow
 def test_meta_bootstrap(oracle_lib):
     """EvalBootstrap(ct, 2, p): the residual bootstrapped again at 2^p."""
     e = boot_engine("oracle", 12, 16, 40, (2, 2))
@@ -68,6 +70,7 @@ def test_meta_bootstrap(oracle_lib):
     assert e2 < 2.0 ** -28 and e2 < e1 / 256
 
 
+@pytest.mark.slow
 def test_meta_bootstrap_input_deeper_than_output(oracle_lib):
     """BitonicSort bootstraps once the level passes 29, i.e. the input sits
     deeper than the bootstrapped output (src/sort_algo.h:1436-1438)."""

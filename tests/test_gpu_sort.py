@@ -6,11 +6,13 @@ of the input.  Bars:
     multDepth (tests/DirectSortTest.cpp:140-141, :194), at every size the
     reference's DirectSortTest instantiates at ring 2^17 / HEStd_128_classic
     (DirectSortTest.cpp:35-37, :203-208: N = 256, 512, 1024 here);
-  * a measured bar (4x the error measured on MI355X): the
-    rank's CKKS noise (the self comparison's sign gain ~2^11 at d = 0) is
-    what remains once the placement evaluates the doubled sinc in the
-    rebased variable; evaluated as the reference orders it (SFHE_SINC_REBASE
-    =0) the placement adds ~2^-6.7 at N=256 (test_precision_attribution).
+  * a measured bar (~3x the error measured on MI355X, DESIGN.md §2,
+    tools/precision_table.py): with the engine's precision choices (exact
+    ModDown, lazy rescaling, the self comparison moved off the sign's steep
+    point, the doubled sinc in the rebased variable) the rank is within
+    ~1e-6 of exact and the sort is limited by the placement's
+    Paterson-Stockmeyer noise; test_precision_attribution measures each
+    choice against the reference's order of operations.
 """
 import numpy as np
 import pytest
@@ -33,13 +35,13 @@ def run_sort(N, logn, secure=False, debug=False, scale_bits=40):
 
 
 @pytest.mark.parametrize("N,logn,secure,scale_bits,tol", [
-    (8, 17, True, 40, 2 ** -12),     # config 1 (DirectSortTest N=8: ring 2^17, 128-bit)
-    (128, 16, False, 40, 3e-4),      # config 3 (measured 7.4e-5)
-    (256, 16, False, 40, 1.5e-3),    # metric config (measured 3.7e-4)
-    (256, 16, False, 50, 2 ** -19),  # same circuit, 50-bit scale (measured 4.9e-7): noise-limited
-    (256, 17, True, 40, 3.5e-3),     # DirectSortTest N=256 / config 5 shape on one GPU (8.3e-4)
-    (512, 17, True, 40, 4e-3),       # DirectSortTest N=512 (9.3e-4)
-    (1024, 17, True, 40, 7.5e-3),    # DirectSortTest N=1024 (1.8e-3)
+    (8, 17, True, 40, 1e-6),       # config 1 (DirectSortTest N=8: ring 2^17, 128-bit; measured 2.3e-7)
+    (128, 16, False, 40, 3e-5),    # config 3 (measured 1.1e-5, approximation floor 9.6e-6)
+    (256, 16, False, 40, 8e-5),    # metric config (measured 2.6e-5)
+    (256, 16, False, 50, 2 ** -19),  # same circuit, 50-bit scale: noise-limited
+    (256, 17, True, 40, 1.2e-4),   # DirectSortTest N=256 / config 5 shape on one GPU (4.0e-5)
+    (512, 17, True, 40, 3e-4),     # DirectSortTest N=512 (9.8e-5)
+    (1024, 17, True, 40, 7e-4),    # DirectSortTest N=1024 (2.2e-4)
 ])
 def test_direct_sort(N, logn, secure, scale_bits, tol):
     e, x, out, depth = run_sort(N, logn, secure, scale_bits=scale_bits)
@@ -54,37 +56,53 @@ def test_direct_sort(N, logn, secure, scale_bits, tol):
     assert np.max(np.abs(got - sim)) < tol
 
 
-def test_precision_attribution(monkeypatch):
-    """Metric config (N=256 @ 2^16, 40-bit scale), stage by stage against
-    slotsim: the rank's error, the sort's error with the placement's doubled
-    sinc evaluated in the rebased variable (default), and as the reference
-    orders it (SFHE_SINC_REBASE=0: every PS giant step T_{2^i} sits at +-1 on
-    the hits z = 0, so noise grows 4x per doubling)."""
-    N, logn = 256, 16
-    depth, rots = sfhe.direct_sort_params(N, "hip")
-    e = sfhe.Engine("hip", mult_depth=depth, ring_dim=1 << logn, batch_size=N, rotations=rots,
-                    seed=20251205 + N)
-    e.set_quiet(True)
-    x = slotsim.input_vector(N)
-    cfg = slotsim.default_sign_config(N)
-    s = e.sorter(N)
-    ct = e.encrypt(x.tolist())
-    r = s.rank(ct, *cfg)
-    rank = np.array(e.decrypt(r))
-    sim = slotsim.construct_rank(x, N, 1 << logn, cfg)
-    rank_err = np.max(np.abs(rank - sim))
-    errs = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("SFHE_SINC_REBASE", mode)
-        out = s.place(r, ct)
-        assert out.level == depth
-        errs[mode] = np.max(np.abs(np.array(e.decrypt(out)) - np.sort(x)))
-    print(f"rank err {rank_err:.3g} (log2 {np.log2(rank_err):.2f}); sort err rebased {errs['1']:.3g} "
-          f"(log2 {np.log2(errs['1']):.2f}), reference order {errs['0']:.3g} (log2 {np.log2(errs['0']):.2f})")
-    assert rank_err < 2e-3          # measured 4.2e-4 (2^-11.2)
-    assert errs["1"] < 2e-3         # measured 3.7e-4 (2^-11.4)
-    assert errs["0"] < 0.02         # measured 9.8e-3 (2^-6.7)
-    assert errs["1"] * 8 < errs["0"]
+PREC_CHILD = r"""
+import json, numpy as np, sfhe
+from oracle import slotsim
+N, logn = 256, 16
+depth, rots = sfhe.direct_sort_params(N, "hip")
+e = sfhe.Engine("hip", mult_depth=depth, ring_dim=1 << logn, batch_size=N, rotations=rots, seed=20251205 + N)
+e.set_quiet(True)
+x = slotsim.input_vector(N)
+s = e.sorter(N)
+ct = e.encrypt(x.tolist())
+r = s.rank(ct, *slotsim.default_sign_config(N))
+rank = np.array(e.decrypt(r))
+out = s.place(r, ct)
+assert out.level == depth
+print(json.dumps({"rank": float(np.max(np.abs(rank - np.argsort(np.argsort(x))))),
+                  "sort": float(np.max(np.abs(np.array(e.decrypt(out)) - np.sort(x))))}))
+"""
+
+
+def _prec(env):
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    child = dict(os.environ, **env)
+    child["PYTHONPATH"] = os.pathsep.join([os.path.join(root, "sorting-fhe_amd", "python"), root])
+    p = subprocess.run([sys.executable, "-c", PREC_CHILD], cwd=root, env=child, capture_output=True, text=True,
+                       timeout=110)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    return json.loads(p.stdout.strip().splitlines()[-1])
+
+
+def test_precision_attribution():
+    """Metric config (N=256 @ 2^16, 40-bit scale): the rank's and the sort's
+    error with each of the engine's precision choices switched off in turn
+    (each knob is read once per process, so every variant is a child
+    process).  DESIGN.md §2 tabulates the same measurement."""
+    base = _prec({})
+    no_off = _prec({"SFHE_SELF_OFFSET": "0"})   # self comparison at the sign's steep point (reference)
+    no_lazy = _prec({"SFHE_LAZY": "0"})          # every product rescaled at once
+    no_reb = _prec({"SFHE_SINC_REBASE": "0"})    # doubled sinc in the reference's variable
+    print(f"default {base}\nno self offset {no_off}\nno lazy rescaling {no_lazy}\nno sinc rebase {no_reb}")
+    assert base["rank"] < 5e-6 and base["sort"] < 8e-5       # measured 1.1e-6 / 2.6e-5
+    assert no_off["rank"] > 20 * base["rank"]                 # ~1e-4: the self term's sign gain
+    assert no_lazy["sort"] > 1.3 * base["sort"]               # unrescaled rotations / sums
+    assert no_reb["sort"] > 20 * base["sort"]                 # giant steps at +-1 on the hits
 
 
 def test_rank_matches_oracle():

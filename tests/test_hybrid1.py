@@ -73,11 +73,15 @@ def test_hybrid1_bitexact_hip_vs_oracle(hip_lib, oracle_lib):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("N,tol", [(64, 1e-3), (256, 1e-3)])
-def test_hybrid1_directsorth1test_config(hip_lib, N, tol):
+@pytest.mark.parametrize("N,tol,exact_tol", [(64, 1e-6, 2e-5), (256, 3e-6, 1.8e-6)])
+def test_hybrid1_directsorth1test_config(hip_lib, N, tol, exact_tol):
     """DirectSortH1Test's configuration: ring 2^17, HEStd_128_classic, its
-    depth and keys; the reference publishes 2^-19.3 max error at N=256
-    (comparison/experimental_results/ours_hybrid1/total_results.txt:172)."""
+    depth and keys.  The reference publishes N=256 over 10 trials: max error
+    1.33e-6 .. 1.74e-6, log2 -19.13 .. -19.52 (comparison/experimental_results/
+    ours_hybrid1/trials/trial_*/size_256.txt; total_results.txt:151-174).
+    Measured here 1.67e-6 (2^-19.19): gated at 1.8e-6, the top of
+    the reference's range.  N=64 sits on the approximation floor (slotsim
+    9.2e-6)."""
     import time
     t0 = time.perf_counter()
     e, x, out, depth = run_hybrid1("hip", N, 17, secure=True)
@@ -89,4 +93,5 @@ def test_hybrid1_directsorth1test_config(hip_lib, N, tol):
     print(f"hybrid1 N={N} @2^17: max err {err:.3g} (log2 {np.log2(err):.2f}), vs slotsim "
           f"{np.max(np.abs(got - sim)):.3g}; {dt:.1f} s incl. keygen")
     assert err < 0.01
+    assert err < exact_tol
     assert np.max(np.abs(got - sim)) < tol

@@ -36,6 +36,7 @@ def run_kway(backend, k, M, logn=12):
     return e, x, out
 
 
+@pytest.mark.slow
 @pytest.mark.parametrize("k,M", [(2, 3), (3, 2)])
 def test_kway_sort_oracle(oracle_lib, k, M):
     e, x, out = run_kway("oracle", k, M)
@@ -55,6 +56,7 @@ def test_kway_sort_errors(oracle_lib):
         e.kway_sort(ct, 2, 4)
 
 
+@pytest.mark.slow
 def test_bitonic_sort_oracle(oracle_lib):
     """BitonicSortTest's configuration (ring 2^12, depth 58, scale 59, {3,3})
     through sfhe_sorter_sort_bitonic."""
@@ -99,6 +101,7 @@ def test_kway_schedule_matches_reference_masking():
     assert outs[0] == outs[1]
 
 
+@pytest.mark.slow
 def test_kway_handle_oracle(oracle_lib):
     """sfhe_kway_create / sfhe_kway_run: a persistent KWayAdapter; repeated
     sorts of one input agree bit for bit."""

@@ -80,6 +80,7 @@ def test_sortn_benchmark_lists(built):
     assert rc == 0 and "BM_DirectSort<256>" in out and "BM_BitonicSort<4>" in out, out
 
 
+@pytest.mark.slow
 def test_direct_sort_h1_test_n4(built):
     """tests/DirectSortH1Test.cpp as-is (sort_hybrid1), its first
     instantiation (N=4, ring 2^17, HEStd_128_classic): level == multDepth 31,
@@ -92,6 +93,7 @@ def test_direct_sort_h1_test_n4(built):
     assert err < 1e-3, err
 
 
+@pytest.mark.slow
 def test_bitonic_sort_test(built):
     """tests/BitonicSortTest.cpp as-is (BitonicSort<4>, ring 2^12, depth 58,
     scale 59, levelBudget {3,3}, EvalBootstrap(ct, 2, 20) whenever the level
@@ -105,6 +107,7 @@ def test_bitonic_sort_test(built):
 
 @pytest.mark.parametrize("prog,count", [("KWayMaskingTest", 4), ("KWaySortUtilsTest", 11), ("KWayEvalUtilsTest", 6),
                                         ("KWaySorterTest", 7)])
+@pytest.mark.slow
 def test_kway_unit_tests(built, prog, count):
     """tests/k-way/{Masking,SortUtils,EvalUtils,Sorter}Test.cpp as-is against the
     engine's k-way module (SorterTest's DISABLED_Run2345Sorter stays disabled,
@@ -113,6 +116,7 @@ def test_kway_unit_tests(built, prog, count):
     assert rc == 0 and f"{count} tests ran, 0 failed" in out, out[-3000:]
 
 
+@pytest.mark.slow
 def test_kway_sort_test(built):
     """tests/KWaySortTest.cpp as-is: KWayAdapter<512> (k = 2, M = 9: 45 network
     stages) at ring 2^10 with full-slot bootstrapping ({5,5}) under

@@ -52,6 +52,7 @@ def test_main_rejects_missing_files(tmp_path):
     assert r.returncode == 1 and "Could not deserialize cryptocontext file" in r.stderr
 
 
+@pytest.mark.slow
 def test_fherma_flow_oracle(tmp_path, oracle_lib):
     out = flow(tmp_path, "oracle", 12, 44)
     assert "level 42" in out  # rank 29 (CompositeSign(4,3,3)) + placement 13
