@@ -179,21 +179,32 @@ class PhaseTimer {
         if (m_on) {
             m_cc->Synchronize();
             m_t = std::chrono::steady_clock::now();
+            m_s = m_cc->GetOpStats();
         }
     }
     void mark(const char* what) {
         if (!m_on) return;
+        std::lock_guard<std::mutex> g(m_mu);  // lanes on host threads mark too
         m_cc->Synchronize();
         auto now = std::chrono::steady_clock::now();
-        std::fprintf(stderr, "PHASE %-28s %8.3f ms\n", what,
-                     std::chrono::duration<double, std::milli>(now - m_t).count());
+        const auto st = m_cc->GetOpStats();
+        // op counts since the last mark: key switches, rescales, ct x ct
+        // tensors, automorphisms and NTT limb-transforms
+        std::fprintf(stderr, "PHASE %-36s %8.3f ms  ks %4llu  rs %4llu  tensor %4llu  aut %4llu  ntt %6llu\n",
+                     what, std::chrono::duration<double, std::milli>(now - m_t).count(),
+                     (unsigned long long)(st.keyswitch - m_s.keyswitch), (unsigned long long)(st.rescale - m_s.rescale),
+                     (unsigned long long)(st.tensor - m_s.tensor), (unsigned long long)(st.automorph - m_s.automorph),
+                     (unsigned long long)(st.ntt_limbs - m_s.ntt_limbs));
         m_t = now;
+        m_s = st;
     }
 
   private:
     CryptoContext<DCRTPoly> m_cc;
     bool m_on = false;
+    std::mutex m_mu;
     std::chrono::steady_clock::time_point m_t;
+    CryptoContextImpl<DCRTPoly>::OpStats m_s;
 };
 }  // namespace sfhe
 
@@ -362,6 +373,7 @@ class DirectSort : public SortBase<N> {
         m_cc->ForkLanes(lanes);
         sfhe::parallelLanes(m_cc, lanes, L.B, [&](int b) {
             auto shifted = vecRotsOpt(pre, L.P, L.S, L.npRank, b);
+            ph.mark("  rank batch: vecRotsOpt");
             auto dup = input_array->Clone();
             dup->SetSlots(L.S);
             if (b == 0 && offsetSelf) {
@@ -373,6 +385,7 @@ class DirectSort : public SortBase<N> {
                 dup = m_cc->EvalAdd(dup, off);
             }
             parts[b] = comp.compare(m_cc, dup, shifted, SignFunc, Cfg);
+            ph.mark("  rank batch: compare");
         });
         m_cc->JoinLanes();
         for (int b = 0; b < L.B; ++b) m_cc->EvalAddInPlace(rank, parts[b]);
@@ -437,17 +450,21 @@ class DirectSort : public SortBase<N> {
             // (r - rank_r - c) / 2N  in (-1, 1/2)
             auto z = m_cc->EvalMult(m_cc->EvalSub(indexMinusRank, chk), zmul / N / 2);
             if (rebase) z = m_cc->EvalAdd(z, zadd);
+            ph.mark("  place batch: z");
             auto hit = m_cc->EvalChebyshevSeriesPS(z, sincCoeffs, -1, 1);
             // the rebased series may be shorter (tiny tail terms dropped) and so
             // shallower: consume exactly the reference's PS depth (level tables)
             const uint32_t psLevel = z->GetLevel() + lbcrypto::ChebyshevPSDepth(
                 (uint32_t)selectDoubledSincCoefficients<N>().size() - 1);
             if (hit->GetLevel() < psLevel) hit = m_cc->AdjustLevel(hit, psLevel);
+            ph.mark("  place batch: sinc PS");
             auto masked = m_cc->EvalMult(hit, input_array);
             std::vector<int> amounts(L.npPlace);
             for (int i = 0; i < L.npPlace; ++i) amounts[i] = i;
             auto maskedRot = rot.rotateMany(masked, amounts);
+            ph.mark("  place batch: mask + baby rotations");
             parts[b] = blindRotationOptN(maskedRot, L.S, L.npPlace, b, L.P);
+            ph.mark("  place batch: blind rotation");
         });
         m_cc->JoinLanes();
         for (int b = 0; b < L.B; ++b) m_cc->EvalAddInPlace(output, parts[b]);

@@ -34,6 +34,8 @@
 // (24 for {5, 5}), as OpenFHE's FLEXIBLEAUTO bootstrapping with a uniform
 // ternary secret; EvalBootstrap(ct, 2, p) is meta-bootstrapping (Bossuat et
 // al.): the residual ct - BTS(ct) bootstrapped again at 2^p and added back.
+#include <chrono>
+#include <cstdio>
 #include <algorithm>
 #include <cmath>
 #include <complex>
@@ -375,6 +377,25 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::BootstrapOnce(const Ciphertext
 
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalBootstrap(const Ciphertext<DCRTPoly>& ct, uint32_t numIterations,
                                                                uint32_t precision) {
+    // SFHE_BOOT_TRACE=1 (diagnostics): device-synchronised wall time of every
+    // bootstrap on stderr ("BOOT <ms> ms level a -> b"), for attributing a
+    // k-way sort's time (tools/kway_run.py)
+    static const bool trace = std::getenv("SFHE_BOOT_TRACE") != nullptr;
+    if (trace) {
+        Synchronize();
+        const auto t0 = std::chrono::steady_clock::now();
+        auto out = bootstrapIters(ct, numIterations, precision);
+        Synchronize();
+        std::fprintf(stderr, "BOOT %.3f ms level %u -> %u\n",
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(),
+                     ct->GetLevel(), out->GetLevel());
+        return out;
+    }
+    return bootstrapIters(ct, numIterations, precision);
+}
+
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::bootstrapIters(const Ciphertext<DCRTPoly>& ct,
+                                                                 uint32_t numIterations, uint32_t precision) {
     if (numIterations <= 1) return BootstrapOnce(ct, 1.0, 1.0);
     // meta-bootstrapping: out = BTS(ct) + BTS((ct - BTS(ct)) 2^p) 2^-p; the
     // residual is formed at the deeper of the two levels

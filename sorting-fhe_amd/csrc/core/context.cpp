@@ -306,7 +306,7 @@ class SfheInternal {
             const char* v = std::getenv("SFHE_LAZY");
             return !v || *v != '0';
         }();
-        return on;
+        return on && s->lazyHold == 0;
     }
     static bool isLazy(const Ct& c) { return c && (c->def || c->pend); }
     static uint32_t ctEll(const SfheContextState* s, const CiphertextImpl<DCRTPoly>& c) {
@@ -392,30 +392,23 @@ class SfheInternal {
         const uint32_t ell = s->ellOf(level) + 1;
         const sfp_limbs m = s->qmap(ell);
         Ct out = newPendingCt(cc, level, std::max(a->slots, b->slots));
+        // out = w_0 x_0 + w_1 x_1 for both polynomials in one launch: w = 1,
+        // or the lift's integer for a canonical operand; -w for a subtrahend
         const uint64_t* x0[2];
         const uint64_t* x1[2];
-        DeviceBufferPtr lifted;
+        std::vector<u64> w(2 * (size_t)m.count);
         for (int i = 0; i < 2; ++i) {
             const Ct& c = *lz[i];
             x0[i] = c->c0;
             x1[i] = c->c1;
-            if (!liftIdx[i]) continue;
-            const size_t pw = s->polyWords(level - 1);
-            lifted = s->alloc(2 * pw);
-            auto k = constResidues(s, s->preScale(level) / c->scale, ell);
-            sfp_mul_const(s->dev, lifted->ptr, c->c0, k.data(), m);
-            sfp_mul_const(s->dev, lifted->ptr + pw, c->c1, k.data(), m);
-            x0[i] = lifted->ptr;
-            x1[i] = lifted->ptr + pw;
-            s->countBytes(4.0 * ell * s->n * 8);
+            const std::vector<u64> k = liftIdx[i] ? constResidues(s, s->preScale(level) / c->scale, ell)
+                                                  : std::vector<u64>(m.count, 1);
+            for (uint32_t r = 0; r < m.count; ++r) {
+                const u64 q = s->primes[s->qprime(r)];
+                w[(size_t)i * m.count + r] = (sub && i == 1) ? (k[r] ? q - k[r] : 0) : k[r];
+            }
         }
-        if (sub) {
-            sfp_sub(s->dev, out->c0, x0[0], x0[1], m);
-            sfp_sub(s->dev, out->c1, x1[0], x1[1], m);
-        } else {
-            sfp_add(s->dev, out->c0, x0[0], x0[1], m);
-            sfp_add(s->dev, out->c1, x1[0], x1[1], m);
-        }
+        sfp_lin_wsum_multi(s->dev, out->c0, 0, (size_t)(out->c1 - out->c0), x0, x1, 2, w.data(), 1, m);
         s->stats.add++;
         s->countBytes(6.0 * ell * s->n * 8);
         return out;
@@ -1106,8 +1099,14 @@ struct DeferredConstMult : DeferredOp {
         }
         const size_t pw = s->polyWords(level);
         auto out = s->alloc(2 * pw);
-        sfp_mul_const(s->dev, out->ptr, c0, k.data(), s->qmap(s->ellOf(level)));
-        sfp_mul_const(s->dev, out->ptr + pw, c1, k.data(), s->qmap(s->ellOf(level)));
+        if ((size_t)(c1 - c0) == pw) {  // both polynomials in one launch
+            std::vector<uint64_t> kk(k);
+            kk.insert(kk.end(), k.begin(), k.end());
+            sfp_mul_const(s->dev, out->ptr, c0, kk.data(), SfheInternal::both(s, s->ellOf(level)));
+        } else {
+            sfp_mul_const(s->dev, out->ptr, c0, k.data(), s->qmap(s->ellOf(level)));
+            sfp_mul_const(s->dev, out->ptr + pw, c1, k.data(), s->qmap(s->ellOf(level)));
+        }
         SfheInternal::adoptPending(ct, out, out->ptr, out->ptr + pw);
     }
 };

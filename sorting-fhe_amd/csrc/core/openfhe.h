@@ -408,6 +408,8 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
     // the values scaled by inFactor on the way in and outFactor on the way out
     uint32_t GetBootstrapDepth(const std::vector<uint32_t>& levelBudget, uint32_t slots = 0) const;
     Ciphertext<DCRTPoly> BootstrapOnce(const Ciphertext<DCRTPoly>& ct, double inFactor, double outFactor);
+    // EvalBootstrap's passes (meta-bootstrapping for numIterations >= 2)
+    Ciphertext<DCRTPoly> bootstrapIters(const Ciphertext<DCRTPoly>& ct, uint32_t numIterations, uint32_t precision);
 
     // ---------------- engine extensions (not OpenFHE) ----------------
     SfheContextState* state() const { return st.get(); }

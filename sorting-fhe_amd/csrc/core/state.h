@@ -124,6 +124,9 @@ struct SfheContextState {
     // graphOwned[p] = true while a DeviceBuffer still holds p
     bool capturing = false;
     uint64_t captureEpoch = 0, epochCount = 0;  // id of the open capture (0: none)
+    // >0: products inside the current region are formed canonically (lazy
+    // rescaling held off; the Chebyshev PS evaluator, see chebyshev.cpp)
+    uint32_t lazyHold = 0;
     std::set<uint64_t> abandonedEpochs;         // captures that were abandoned (their work never ran)
     std::vector<std::pair<uint64_t*, size_t>> capAllocs;
     std::unordered_map<uint64_t*, bool> graphOwned;

@@ -45,6 +45,8 @@ PROGRAMS = {
     "DirectSortNTest": (["tests/DirectSortNTest.cpp"], True, False),
     "SincTest": (["tests/SincTest.cpp"], False, False),
     "DirectSortBenchmark": (["benchmarks/DirectSortBenchmark.cpp"], False, False),
+    "SincBenchmark": (["benchmarks/SincBenchmark.cpp"], False, False),
+    "RotationBenchmark": (["benchmarks/RotationBenchmark.cpp"], False, False),
     "CompareTest": (["tests/CompareTest.cpp"], False, False),
     "SignTest": (["tests/SignTest.cpp"], False, False),
     "RotationTest": (["tests/RotationTest.cpp"], True, False),

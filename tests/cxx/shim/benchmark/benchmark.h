@@ -18,7 +18,7 @@ enum TimeUnit { kNanosecond, kMicrosecond, kMillisecond, kSecond };
 
 class State {
   public:
-    explicit State(int iters) : left_(iters), total_(iters) {}
+    explicit State(int iters, long long arg = 0) : left_(iters), total_(iters), arg_(arg) {}
     struct Iter {
         State* s;
         bool operator!=(const Iter&) const { return s->left_ > 0; }
@@ -29,9 +29,11 @@ class State {
     Iter end() { return Iter{this}; }
     std::map<std::string, double> counters;
     int iterations() const { return total_; }
+    long long range(int) const { return arg_; }
 
   private:
     int left_, total_;
+    long long arg_;
 };
 
 template <class T>
@@ -47,6 +49,15 @@ struct Bench {
     Bench* Unit(TimeUnit) { return this; }
     Bench* UseRealTime() { return this; }
     Bench* Iterations(int) { return this; }
+    Bench* Arg(long long a) {
+        args.push_back(a);
+        return this;
+    }
+    Bench* DenseRange(long long lo, long long hi, long long step = 1) {
+        for (long long a = lo; a <= hi; a += step) args.push_back(a);
+        return this;
+    }
+    std::vector<long long> args;  // empty: one run without an argument
 };
 inline std::vector<Bench*>& all() {
     static std::vector<Bench*> v;
@@ -67,18 +78,24 @@ inline int run(int argc, char** argv) {
         if (!std::strcmp(argv[i], "--benchmark_list_tests")) list = true;
     }
     for (auto* b : all()) {
-        if (!filter.empty() && !std::regex_search(b->name, std::regex(filter))) continue;
-        if (list) {
-            std::printf("%s\n", b->name.c_str());
-            continue;
+        std::vector<std::pair<std::string, long long>> runs;
+        if (b->args.empty()) runs.emplace_back(b->name, 0);
+        for (long long a : b->args) runs.emplace_back(b->name + "/" + std::to_string(a), a);
+        for (auto& r : runs) {
+            if (!filter.empty() && !std::regex_search(r.first, std::regex(filter))) continue;
+            if (list) {
+                std::printf("%s\n", r.first.c_str());
+                continue;
+            }
+            State st(iters, r.second);
+            auto t0 = std::chrono::steady_clock::now();
+            b->fn(st);
+            const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            std::printf("%-28s %12.3f ms/iter  (%d iterations)", r.first.c_str(), ms / iters, iters);
+            for (auto& kv : st.counters) std::printf("  %s=%g", kv.first.c_str(), kv.second);
+            std::printf("\n");
+            std::fflush(stdout);
         }
-        State st(iters);
-        auto t0 = std::chrono::steady_clock::now();
-        b->fn(st);
-        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-        std::printf("%-28s %12.3f ms/iter  (%d iterations)", b->name.c_str(), ms / iters, iters);
-        for (auto& kv : st.counters) std::printf("  %s=%g", kv.first.c_str(), kv.second);
-        std::printf("\n");
     }
     return 0;
 }

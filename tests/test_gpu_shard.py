@@ -36,9 +36,11 @@ def test_sharded_sort_bitexact_hip(hip_lib):
     assert np.array_equal(ref["sort"], ora["sort"])
 
 
-@pytest.mark.parametrize("N,logn,world", [(64, 15, 3), (128, 16, 4)])
+@pytest.mark.parametrize("N,logn,world", [(64, 15, 3), (128, 16, 4), (256, 17, 2), (256, 17, 3), (256, 17, 4)])
 def test_sharded_sort_large_bitexact_hip(hip_lib, N, logn, world):
-    """Larger rings and limb counts (31 Q limbs at N=128), more ranks."""
+    """Larger rings and limb counts (31 Q limbs at N=128), more ranks, and
+    BASELINE config 5's sort itself (DirectSort<256> at ring 2^17, 35 Q
+    limbs) at W = 2, 3, 4."""
     depth, rots = sfhe.direct_sort_params(N, "hip")
     kw = dict(mult_depth=depth, ring_dim=1 << logn, batch_size=N, rotations=rots, seed=4099)
     ref = sort_program(sfhe.Engine("hip", **kw), N)

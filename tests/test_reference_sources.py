@@ -126,3 +126,29 @@ def test_kway_sort_test(built):
     assert out.count(" == End stage ") == 45
     err = float(re.search(r"Maximum error: ([0-9.e+-]+)", out).group(1))
     assert err < 1e-3, err
+
+
+def test_direct_sort_ntest_small_oracle(built):
+    """tests/DirectSortNTest.cpp, N = 4 and 8 on the oracle: rotationIndexCheckN
+    on exact and noisy ranks passes; ConstructRank / SortTest run out of levels
+    (CompositeSign(3, 6, 3) against getSizeParameters' budget for the default
+    sign config) and fail with the depth exception, as they do in the
+    reference (tests/test_gpu_reference_sources.py runs every N)."""
+    rc, out = run(built[("DirectSortNTest", "oracle")], "--gtest_filter=*/0.*:*/1.*")
+    for i in (0, 1):
+        for t in ("RotationIndexCheck", "RotationIndexCheckWithNoise"):
+            assert f"[       OK ] DirectSort/DirectSortTestFixture/{i}.{t}\n" in out, out[-3000:]
+        for t in ("ConstructRank", "SortTest"):
+            assert f"[  FAILED  ] DirectSort/DirectSortTestFixture/{i}.{t}\n" in out, out[-3000:]
+    assert out.count("no levels left") == 4 and "Mismatch at index" not in out, out[-3000:]
+
+
+def test_rotation_and_sinc_benchmarks_oracle(built):
+    """benchmarks/RotationBenchmark.cpp (rotation chains at ring 2^12) and
+    benchmarks/SincBenchmark.cpp compile unchanged and run on the oracle."""
+    rc, out = run(built[("RotationBenchmark", "oracle")], "--benchmark_filter=BM_(Fast)?Rotations/(1|2|14)$")
+    assert rc == 0, out[-2000:]
+    for name in ["BM_Rotations/1", "BM_Rotations/14", "BM_FastRotations/2"]:
+        assert re.search(re.escape(name) + r"\s+[0-9.]+ ms", out), out[-2000:]
+    rc, out = run(built[("SincBenchmark", "oracle")])
+    assert rc == 0 and "BM_ScaledSinc " in out and "BM_ScaledSincJ" in out, out[-2000:]

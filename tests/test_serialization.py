@@ -61,12 +61,22 @@ def test_fherma_flow_oracle(tmp_path, oracle_lib):
 @pytest.mark.gpu
 def test_fherma_flow_config_json(tmp_path, hip_lib):
     """src/config.json: ring 2^17, depth 44, scale 40, batch 128, its rotation
-    indexes; main.cpp sorts with CompositeSign(4,3,3) (src/sort.h:93).  At
-    scale 40 that sign's error grows with the ring: the C oracle on the same
-    flow gives 5.5e-4 (2^12), 6.2e-3 (2^14), 2.9e-2 (2^15); the product at
-    2^17 measured 3.45e-2.  The gate is the reference's DirectSortTest
-    tolerance scaled to that trend (0.05), the level the exact one."""
-    out = flow(tmp_path, "hip", 17, 44, tol=0.05)
+    indexes; main.cpp sorts with CompositeSign(4,3,3) (src/sort.h:93).
+
+    Error attribution: the noise-free slot simulation of the
+    same sort (oracle/slotsim.py, (4,3,3) at N=128) is 9.8e-7, so all of
+    round 2's 3.45e-2 was CKKS noise -- the self comparison x_r - x_r sits at
+    the sign's steepest point, and CompositeSign<4>'s g4 is steeper there
+    than g3, so its rank error was ~30x the (3,dg,df) configs'.  With the
+    self comparison moved to the saturated region (constructRank's offset)
+    the product measures 9.9e-6; gate 1e-4.
+
+    Level 42 of depth 44: the rank takes 29 levels (2 + 3 g4 at 5 each + 3
+    f4 at 4 each: CompositeSign<4>'s degree-27 / degree-15 stages) and the
+    placement 13 (the 1/2N scaling 1, the doubled sinc's PS depth 10 for
+    N=128, the product with the input 1, the blind rotation's masks 1), so
+    config.json's depth leaves two levels unused."""
+    out = flow(tmp_path, "hip", 17, 44, tol=1e-4)
     assert "level 42" in out
 
 

@@ -77,14 +77,17 @@ def test_sharded_ops_bitexact_oracle(oracle_lib, world):
         compare(ref, outs[r])
 
 
-def test_sharded_sort_bitexact_oracle(oracle_lib):
-    N = 8
+@pytest.mark.parametrize("N,logn,world", [(8, 12, 2), (64, 13, 2), (64, 13, 3), (64, 13, 4)])
+def test_sharded_sort_bitexact_oracle(oracle_lib, N, logn, world):
+    """Whole DirectSort<N> limb-sharded over W thread ranks.  At W = 3, 4 the
+    sort's last levels hold fewer limbs than ranks (ranks without a limb
+    idle through those ops and still receive every broadcast)."""
     depth, rots = sfhe.direct_sort_params(N, "oracle")
-    kw = dict(mult_depth=depth, ring_dim=1 << 12, batch_size=N, rotations=rots, seed=777)
+    kw = dict(mult_depth=depth, ring_dim=1 << logn, batch_size=N, rotations=rots, seed=777)
     ref = sort_program(sfhe.Engine("oracle", **kw), N)
     assert np.max(np.abs(ref["dec"][:N] - np.sort(slotsim.input_vector(N)))) < 0.01
-    outs = sfhe.run_sharded_threads("oracle", 2, lambda e: sort_program(e, N), **kw)
-    for r in range(2):
+    outs = sfhe.run_sharded_threads("oracle", world, lambda e: sort_program(e, N), **kw)
+    for r in range(world):
         compare(ref, outs[r])
 
 
@@ -158,15 +161,15 @@ dist.destroy_process_group()
 """
 
 
-def test_sharded_sort_gloo_two_processes(oracle_lib, tmp_path):
-    """A whole DirectSort<8> limb-sharded over two PROCESSES (one per
+@pytest.mark.parametrize("N,logn", [(8, 12), (64, 13)])
+def test_sharded_sort_gloo_two_processes(oracle_lib, tmp_path, N, logn):
+    """A whole DirectSort<N> limb-sharded over two PROCESSES (one per
     'GPU', gloo host transport): every exchange of a real sharded sort
     (ModUp / ModDown all-gathers, rescale broadcasts) crosses a process
     boundary; both ranks' results are bit-identical to the unsharded sort."""
     import socket
-    N = 8
     depth, rots = sfhe.direct_sort_params(N, "oracle")
-    kw = dict(mult_depth=depth, ring_dim=1 << 12, batch_size=N, rotations=rots, seed=777)
+    kw = dict(mult_depth=depth, ring_dim=1 << logn, batch_size=N, rotations=rots, seed=777)
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]

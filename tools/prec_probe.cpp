@@ -8,6 +8,8 @@
 //   prec_probe h|h2 N logn [secure] [seed]   sort_hybrid / sort_hybrid2 (:894-1062, :1233-1389)
 //   prec_probe h1x N logn [secure] [seed]    sort_hybrid1 without taps (decrypting a tap settles
 //                                            a lazily rescaled ciphertext, so taps change the noise)
+//   prec_probe h2s N logn [secure] [seed]    hybrid II's scaled-sinc stage: input noise vs the
+//                                            noise the series adds, binned by |x|
 //
 // Engine knobs under test are read from the environment by the library.
 #include <algorithm>
@@ -102,14 +104,81 @@ std::vector<double> inputVector(int N, unsigned seed) {
     return x;
 }
 
+// f = c0/2 + sum_k c_k T_k(x) (the Chebyshev-series convention of EvalChebyshevSeriesPS), Clenshaw
+double chebEval(const std::vector<double>& c, double x) {
+    long double b1 = 0, b2 = 0;
+    for (size_t k = c.size() - 1; k >= 1; --k) {
+        long double b0 = c[k] + 2.0L * x * b1 - b2;
+        b2 = b1;
+        b1 = b0;
+    }
+    return (double)(c[0] / 2.0L + x * b1 - b2);
+}
+
+// hybrid II's series stage for batch 0, rotation 0 (reference sort_algo.h:1249-1308):
+// d = i/N - rank_j/N on the N x N matrix, then the scaled-sinc series.  Its
+// error splits into what the input noise explains (p(decrypted d) - p(exact d))
+// and what the series adds (decrypted output - p(decrypted d)); the same series
+// on a fresh encryption of the exact d at the same level isolates the series'
+// own noise from the rank's.
+template <int N>
+int seriesStage(Probe& P, CryptoContext<DCRTPoly>& cc, KeyPair<DCRTPoly>& kp, DirectSort<N>& ds,
+                std::shared_ptr<Encryption>& enc, Ciphertext<DCRTPoly> rank, Ciphertext<DCRTPoly> ct,
+                const Vec& rankExact, const Vec& sorted) {
+    const size_t S = (size_t)N * N;
+    const auto& co = selectCoefficients<N>();
+    std::printf("    series degree %zu\n", co.size() - 1);
+    auto rk = rank->Clone();
+    rk->SetSlots((uint32_t)S);
+    auto r = cc->EvalMult(rk, 1.0 / N);
+    Vec sub(S), dE(S);
+    for (size_t i = 0; i < (size_t)N; ++i)
+        for (size_t j = 0; j < (size_t)N; ++j) sub[i * N + j] = (double)i / N;
+    for (size_t s = 0; s < S; ++s) dE[s] = sub[s] - rankExact[s % N] / N;
+    auto d = cc->EvalSub(cc->MakeCKKSPackedPlaintext(sub, 1, r->GetLevel(), nullptr, (uint32_t)S), r);
+    Vec dD = P.dec(d);
+    P.report("d = i/N - rank/N", d, dD, dE, nullptr);
+    auto series = [&](const Ciphertext<DCRTPoly>& in, const Vec& inD, const char* name) {
+        auto o = cc->EvalChebyshevSeriesPS(in, co, -1, 1);
+        Vec oE(S), oL(S);
+        for (size_t s = 0; s < S; ++s) {
+            oE[s] = chebEval(co, dE[s]);
+            oL[s] = chebEval(co, inD[s]);
+        }
+        Vec oD = P.dec(o);
+        P.report(name, o, oD, oE, &oL);
+        const double edges[] = {0.0, 0.25, 0.5, 0.75, 0.9, 0.97, 1.01};
+        for (int bI = 0; bI + 1 < 7; ++bI) {
+            double mAdd = 0, mIn = 0;
+            for (size_t s = 0; s < S; ++s) {
+                const double a = std::fabs(dE[s]);
+                if (a < edges[bI] || a >= edges[bI + 1]) continue;
+                mAdd = std::max(mAdd, std::fabs(oD[s] - oL[s]));
+                mIn = std::max(mIn, std::fabs(oL[s] - oE[s]));
+            }
+            std::printf("      |x| in [%.2f, %.2f): added max %.3e   input-explained max %.3e\n", edges[bI],
+                        edges[bI + 1], mAdd, mIn);
+        }
+    };
+    series(d, dD, "sinc series on d");
+    auto fresh = cc->Encrypt(kp.publicKey, cc->MakeCKKSPackedPlaintext(dE, 1, d->GetLevel(), nullptr, (uint32_t)S));
+    series(fresh, P.dec(fresh), "sinc series on fresh exact d");
+    auto out = ds.rotationIndexCheckHybrid2(rank, ct, kp.secretKey);
+    Vec oD = P.dec(out);
+    oD.resize(N);
+    P.report("rotationIndexCheckHybrid2", out, oD, sorted, nullptr);
+    return 0;
+}
+
 template <int N>
 int run(const std::string& mode, int logn, bool secure, unsigned seed) {
     CCParams<CryptoContextCKKSRNS> params;
     std::vector<int> rots;
     uint32_t depth;
-    if (mode == "h1" || mode == "h1x" || mode == "h" || mode == "h2") {
+    if (mode == "h1" || mode == "h1x" || mode == "h" || mode == "h2" || mode == "h2s") {
         const sfhe::SizeParams* hp = mode == "h" ? sfhe::hybridParams(N, 0)
-                                     : mode == "h2" ? sfhe::hybridParams(N, 2) : sfhe::hybrid1Params(N);
+                                     : (mode == "h2" || mode == "h2s") ? sfhe::hybridParams(N, 2)
+                                                                       : sfhe::hybrid1Params(N);
         depth = hp->multDepth;
         rots = hp->rotations;
         params.SetBatchSize(N);
@@ -214,6 +283,8 @@ int run(const std::string& mode, int logn, bool secure, unsigned seed) {
         P.report("sort (placement)", out, P.dec(out), sorted, nullptr);
         return 0;
     }
+
+    if (mode == "h2s") return seriesStage<N>(P, cc, kp, ds, enc, rank, ct, rankExact, sorted);
 
     // ---- rotationIndexCheckHybrid1 with taps (N <= 256: one batch, M = N) ----
     const size_t M = N, S = (size_t)N * N;
