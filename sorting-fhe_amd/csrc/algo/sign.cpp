@@ -9,6 +9,7 @@
 #include "sign.h"
 
 #include <cmath>
+#include <map>
 #include <vector>
 
 using namespace lbcrypto;
@@ -20,23 +21,64 @@ using Ct = Ciphertext<DCRTPoly>;
 // sum_{i} c[i] x^(2i+1) for c.size() == 2^(k-1) odd coefficients, depth k:
 //   P(x) = A(x) + B(x) * x^(2^(k-1)),  A,B of half the degree.
 // pw[j] holds x^(2^(j+1)) (x^2, x^4, x^8, ...).
-Ct oddPoly(const CryptoContext<DCRTPoly>& cc, const Ct& x, const std::vector<Ct>& pw,
-           const double* c, size_t cnt) {
-    if (cnt == 1) return cc->EvalMult(x, c[0]);
-    size_t half = cnt / 2;
-    Ct lo = oddPoly(cc, x, pw, c, half);
-    Ct hi = oddPoly(cc, x, pw, c + half, half);
-    size_t j = 0;
-    while ((size_t)2 << j < 2 * half) ++j;  // x^(2*half) = pw[j]
-    return cc->EvalAdd(lo, cc->EvalMult(hi, pw[j]));
-}
+//
+// Every term lands directly at the level its sum works at, so no partial sum
+// is level-adjusted: B is formed at the level just above the product's, A at
+// the product's level, and a coefficient times x at whatever level it is
+// wanted, as one weighted sum that folds the scale into its integer weight
+// (one rescale, like EvalMult(x, c), but at any level below x's).  Only a
+// power x^(2^j) may need aligning, once per level (memo).  Degree 7: 10
+// rescales instead of 12 (4 coefficient products, 5 ciphertext products, x^2
+// aligned once); same depth and polynomial.
+struct OddPoly {
+    const CryptoContext<DCRTPoly>& cc;
+    const Ct& x;
+    const std::vector<Ct>& pw;
+    std::map<std::pair<size_t, uint32_t>, Ct> aligned;
+
+    // c x at level `at` (> x's level)
+    Ct constAt(double c, uint32_t at) {
+        cc->Settle(x);
+        const std::vector<const uint64_t*> i0{x->c0}, i1{x->c1};
+        const std::vector<double> w{c}, sc{x->scale};
+        return cc->LinearWSumRescale(i0, i1, w, at - 1, x->GetSlots(), &sc);
+    }
+    const Ct& power(size_t j, uint32_t level) {
+        if (pw[j]->GetLevel() >= level) return pw[j];
+        auto key = std::make_pair(j, level);
+        auto it = aligned.find(key);
+        if (it != aligned.end()) return it->second;
+        return aligned[key] = cc->AdjustLevel(pw[j], level);
+    }
+    static size_t powIndex(size_t half) {
+        size_t j = 0;
+        while ((size_t)2 << j < 2 * half) ++j;  // x^(2*half) = pw[j]
+        return j;
+    }
+    // level eval(c, cnt, 0) reaches
+    uint32_t natural(size_t cnt) const {
+        if (cnt == 1) return x->GetLevel() + 1;
+        const size_t half = cnt / 2;
+        return std::max(natural(half), pw[powIndex(half)]->GetLevel()) + 1;
+    }
+    Ct eval(const double* c, size_t cnt, uint32_t want) {
+        if (cnt == 1) return constAt(c[0], std::max(x->GetLevel() + 1, want));
+        const size_t half = cnt / 2, j = powIndex(half);
+        const uint32_t Lp = std::max(std::max(natural(half), pw[j]->GetLevel()) + 1, want);
+        Ct hi = eval(c + half, half, Lp - 1);
+        Ct prod = cc->EvalMult(hi, power(j, Lp - 1));
+        Ct lo = eval(c, half, Lp);
+        return cc->EvalAdd(lo, prod);
+    }
+};
 
 Ct oddPolyFull(const CryptoContext<DCRTPoly>& cc, const Ct& x, const std::vector<double>& c) {
     // even powers x^2, x^4, ... up to x^(cnt)
     std::vector<Ct> pw;
     pw.push_back(cc->EvalSquare(x));
     for (size_t p = 4; p < 2 * c.size(); p *= 2) pw.push_back(cc->EvalSquare(pw.back()));
-    return oddPoly(cc, x, pw, c.data(), c.size());
+    OddPoly op{cc, x, pw, {}};
+    return op.eval(c.data(), c.size(), 0);
 }
 
 template <int n>

@@ -19,6 +19,7 @@
 //   consumed exactly.
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <map>
 
@@ -93,21 +94,17 @@ class PSEvaluator {
     // flow, no ciphertext work), then compute them all: one multi-output
     // weighted sum + one batched rescale per leaf level.
     void precomputeLeaves(const std::vector<double>& p, uint32_t depth) {
-        std::vector<std::vector<double>> leaves;
-        plan(p, depth, leaves);
+        std::vector<std::pair<std::vector<double>, uint32_t>> leaves;  // (poly, weighted-sum level)
+        plan(p, depth, 0, leaves);
         std::map<uint32_t, std::vector<size_t>> byLevel;
-        std::vector<uint32_t> lev(leaves.size());
-        for (size_t i = 0; i < leaves.size(); ++i) {
-            lev[i] = leafLevel(leaves[i]);
-            byLevel[lev[i]].push_back(i);
-        }
+        for (size_t i = 0; i < leaves.size(); ++i) byLevel[leaves[i].second].push_back(i);
         pre.assign(leaves.size(), nullptr);
         for (auto& kv : byLevel) {
             const uint32_t L = kv.first;
             std::vector<uint32_t> js;  // inputs used by any leaf of this level
             for (uint32_t j = 1; j <= k; ++j)
                 for (size_t i : kv.second)
-                    if (j < leaves[i].size() && leaves[i][j] != 0.0) {
+                    if (j < leaves[i].first.size() && leaves[i].first[j] != 0.0) {
                         js.push_back(j);
                         break;
                     }
@@ -124,7 +121,7 @@ class PSEvaluator {
                 std::vector<std::vector<double>> w;
                 const size_t b1 = std::min(kv.second.size(), b0 + 64);
                 for (size_t t = b0; t < b1; ++t) {
-                    const auto& pl = leaves[kv.second[t]];
+                    const auto& pl = leaves[kv.second[t]].first;
                     std::vector<double> row;
                     for (uint32_t j : js) row.push_back(j < pl.size() ? pl[j] : 0.0);
                     w.push_back(std::move(row));
@@ -136,32 +133,39 @@ class PSEvaluator {
         nextLeaf = 0;
     }
 
-    Val eval(std::vector<double> p, uint32_t depth) {
+    // The value of p at level `want`, or deeper where its inputs are deeper.
+    // Every level alignment of the evaluation happens on the giant steps (one
+    // memoised AdjustLevel per (M, level), shared by all nodes) or inside the
+    // leaves: a leaf's weighted sum folds any input scale into its integer
+    // weights and rescales once, so it is formed directly at the level its
+    // consumer works at, for free.  A node q T_M + r is formed at
+    // Lp = max(its natural product level, want): q wanted at Lp - 1, T_M
+    // aligned to Lp - 1, r wanted at Lp -- no per-node rescale of a node's
+    // operands or result.  want = 0: the natural level.
+    Val eval(std::vector<double> p, uint32_t depth, uint32_t want = 0) {
         trim(p);
         if (p.empty()) return Val{true, 0.0, nullptr};
         const uint32_t deg = (uint32_t)p.size() - 1;
         if (deg == 0) return Val{true, p[0], nullptr};
-        if (deg <= k) return leaf(p);
-        if (depth >= 1 && deg + (1u << l) <= (1u << (depth - 1))) return eval(p, depth - 1);
+        if (deg <= k) return leaf(p, want);
+        if (depth >= 1 && deg + (1u << l) <= (1u << (depth - 1))) return eval(p, depth - 1, want);
         const uint32_t M = deg >= (1u << (depth - 1)) ? (1u << (depth - 1)) : (1u << (depth - 2));
-        std::vector<double> q(deg - M + 1, 0.0), r(p.begin(), p.begin() + M);
-        for (uint32_t j = M; j <= deg; ++j) {
-            if (j == M) {
-                q[0] += p[j];
-            } else {
-                q[j - M] += 2.0 * p[j];
-                r[2 * M - j] -= p[j];
-            }
-        }
-        Val qv = eval(q, depth - 1);
-        Val rv = eval(r, depth);
-        const Ct& TM = power(M);
+        std::vector<double> q, r;
+        divide(p, M, q, r);
+        const uint32_t Lp = productLevel(q, depth, M, want);
+        Val qv = eval(q, depth - 1, Lp - 1);
+        const Ct& TM = alignedPower(M, Lp - 1);
         Val out;
         out.isConst = false;
         if (qv.isConst)
             out.ct = cc->EvalMult(TM, qv.c);
         else
             out.ct = cc->EvalMult(qv.ct, TM);
+        Val rv = eval(r, depth, Lp);
+        if (std::getenv("SFHE_PS_DEBUG"))
+            std::fprintf(stderr, "PSNODE deg %u M %u | q %s lvl %d | TM lvl %u | prod lvl %u | r %s lvl %d\n", deg, M,
+                         qv.isConst ? "const" : "ct", qv.isConst ? -1 : (int)qv.ct->GetLevel(), TM->GetLevel(),
+                         out.ct->GetLevel(), rv.isConst ? "const" : "ct", rv.isConst ? -1 : (int)rv.ct->GetLevel());
         if (rv.isConst) {
             if (rv.c != 0.0) out.ct = cc->EvalAdd(out.ct, rv.c);
         } else {
@@ -171,22 +175,11 @@ class PSEvaluator {
     }
 
   private:
-    // eval()'s control flow without ciphertext work: the leaf polynomials
-    void plan(std::vector<double> p, uint32_t depth, std::vector<std::vector<double>>& leaves) {
-        trim(p);
-        if (p.size() <= 1) return;
+    // p = q T_M + r (Chebyshev division by T_M, M >= deg / 2)
+    static void divide(const std::vector<double>& p, uint32_t M, std::vector<double>& q, std::vector<double>& r) {
         const uint32_t deg = (uint32_t)p.size() - 1;
-        if (deg <= k) {
-            for (uint32_t j = 1; j <= deg; ++j)
-                if (p[j] != 0.0) {
-                    leaves.push_back(p);
-                    return;
-                }
-            return;
-        }
-        if (depth >= 1 && deg + (1u << l) <= (1u << (depth - 1))) return plan(p, depth - 1, leaves);
-        const uint32_t M = deg >= (1u << (depth - 1)) ? (1u << (depth - 1)) : (1u << (depth - 2));
-        std::vector<double> q(deg - M + 1, 0.0), r(p.begin(), p.begin() + M);
+        q.assign(deg - M + 1, 0.0);
+        r.assign(p.begin(), p.begin() + M);
         for (uint32_t j = M; j <= deg; ++j) {
             if (j == M) {
                 q[0] += p[j];
@@ -195,19 +188,72 @@ class PSEvaluator {
                 r[2 * M - j] -= p[j];
             }
         }
-        plan(q, depth - 1, leaves);
-        plan(r, depth, leaves);
     }
 
-    uint32_t leafLevel(const std::vector<double>& p) const {
-        uint32_t lev = 0;
+    // eval()'s control flow without ciphertext work: the leaf polynomials with
+    // the level of their weighted sum, in eval()'s visiting order.
+    void plan(std::vector<double> p, uint32_t depth, uint32_t want,
+              std::vector<std::pair<std::vector<double>, uint32_t>>& leaves) {
+        trim(p);
+        if (p.size() <= 1) return;
+        const uint32_t deg = (uint32_t)p.size() - 1;
+        if (deg <= k) {
+            const int lv = leafSumLevel(p, want);
+            if (lv >= 0) leaves.emplace_back(p, (uint32_t)lv);
+            return;
+        }
+        if (depth >= 1 && deg + (1u << l) <= (1u << (depth - 1))) return plan(p, depth - 1, want, leaves);
+        const uint32_t M = deg >= (1u << (depth - 1)) ? (1u << (depth - 1)) : (1u << (depth - 2));
+        std::vector<double> q, r;
+        divide(p, M, q, r);
+        const uint32_t Lp = productLevel(q, depth, M, want);
+        plan(q, depth - 1, Lp - 1, leaves);
+        plan(r, depth, Lp, leaves);
+    }
+
+    // level of a node's product q T_M: the natural one (q and T_M as they come,
+    // +1) or `want`, whichever is deeper
+    uint32_t productLevel(const std::vector<double>& q, uint32_t depth, uint32_t M, uint32_t want) const {
+        const int nq = natural(q, depth - 1);
+        const uint32_t nat = (uint32_t)std::max(nq, (int)powerLevel(M)) + 1;
+        return std::max(nat, want);
+    }
+
+    // level eval(p, depth) reaches without a wanted level (-1: a constant)
+    int natural(std::vector<double> p, uint32_t depth) const {
+        trim(p);
+        if (p.size() <= 1) return -1;
+        const uint32_t deg = (uint32_t)p.size() - 1;
+        if (deg <= k) {
+            const int lv = leafSumLevel(p, 0);
+            return lv < 0 ? -1 : lv + 1;
+        }
+        if (depth >= 1 && deg + (1u << l) <= (1u << (depth - 1))) return natural(p, depth - 1);
+        const uint32_t M = deg >= (1u << (depth - 1)) ? (1u << (depth - 1)) : (1u << (depth - 2));
+        std::vector<double> q, r;
+        divide(p, M, q, r);
+        const int lp = (int)productLevel(q, depth, M, 0);
+        return std::max(lp, natural(r, depth));
+    }
+
+    // level of the leaf's weighted sum (its output is one level deeper): the
+    // deepest input's, or want - 1 when that is deeper; -1 if p is a constant
+    int leafSumLevel(const std::vector<double>& p, uint32_t want) const {
+        int lev = -1;
         for (uint32_t j = 1; j < p.size(); ++j)
-            if (p[j] != 0.0) lev = std::max(lev, T[j]->GetLevel());
-        return lev;
+            if (p[j] != 0.0) lev = std::max(lev, (int)T[j]->GetLevel());
+        if (lev < 0) return -1;
+        return std::max(lev, (int)want - 1);
     }
 
     static void trim(std::vector<double>& p) {
         while (!p.empty() && p.back() == 0.0) p.pop_back();
+    }
+
+    // level of T_M for a power of two M (built or not yet built)
+    uint32_t powerLevel(uint32_t M) const {
+        if (M <= k) return T[M]->GetLevel();
+        return powerLevel(M / 2) + 1;  // T_2M = 2 T_M^2 - 1: one product
     }
 
     // T_M for a power of two M (giant steps built lazily: T_2M = 2 T_M^2 - 1)
@@ -221,6 +267,16 @@ class PSEvaluator {
         return giant[i] = cc->EvalAdd(cc->EvalAdd(sq, sq), -1.0);
     }
 
+    // T_M at `level` (>= its own): one AdjustLevel per (M, level), memoised
+    const Ct& alignedPower(uint32_t M, uint32_t level) {
+        const Ct& t = power(M);
+        if (t->GetLevel() >= level) return t;
+        auto key = std::make_pair(M, level);
+        auto it = alignedPow.find(key);
+        if (it != alignedPow.end()) return it->second;
+        return alignedPow[key] = cc->AdjustLevel(t, level);
+    }
+
     const Ct& atLevel(uint32_t j, uint32_t level) {
         auto key = std::make_pair(j, level);
         auto it = aligned.find(key);
@@ -228,7 +284,7 @@ class PSEvaluator {
         return aligned[key] = (T[j]->GetLevel() == level ? T[j] : cc->AdjustLevel(T[j], level));
     }
 
-    Val leaf(const std::vector<double>& p) {
+    Val leaf(const std::vector<double>& p, uint32_t want) {
         if (!pre.empty()) {  // precomputed (same visiting order as plan())
             bool any = false;
             for (uint32_t j = 1; j < p.size(); ++j) any = any || p[j] != 0.0;
@@ -241,18 +297,11 @@ class PSEvaluator {
             if (p[0] != 0.0) out.ct = cc->EvalAdd(out.ct, p[0]);
             return out;
         }
-        const uint32_t deg = (uint32_t)p.size() - 1;
-        uint32_t lev = 0;
-        bool any = false;
-        for (uint32_t j = 1; j <= deg; ++j)
-            if (p[j] != 0.0) {
-                lev = std::max(lev, T[j]->GetLevel());
-                any = true;
-            }
-        if (!any) return Val{true, p[0], nullptr};
+        const int lv = leafSumLevel(p, want);
+        if (lv < 0) return Val{true, p[0], nullptr};
         std::vector<const uint64_t*> ins0, ins1;
         std::vector<double> w, sc;
-        for (uint32_t j = 1; j <= deg; ++j) {
+        for (uint32_t j = 1; j < p.size(); ++j) {
             if (p[j] == 0.0) continue;
             const Ct& t = T[j];  // unadjusted: its scale is folded into the weight
             cc->Settle(t);  // raw pointers below: canonical rows, ordered after their writers
@@ -263,7 +312,7 @@ class PSEvaluator {
         }
         Val out;
         out.isConst = false;
-        out.ct = cc->LinearWSumRescale(ins0, ins1, w, lev, T[1]->GetSlots(), &sc);
+        out.ct = cc->LinearWSumRescale(ins0, ins1, w, (uint32_t)lv, T[1]->GetSlots(), &sc);
         if (p[0] != 0.0) out.ct = cc->EvalAdd(out.ct, p[0]);
         return out;
     }
@@ -274,7 +323,7 @@ class PSEvaluator {
     size_t nextLeaf = 0;
     std::vector<Ct> T;
     std::map<uint32_t, Ct> giant;
-    std::map<std::pair<uint32_t, uint32_t>, Ct> aligned;
+    std::map<std::pair<uint32_t, uint32_t>, Ct> aligned, alignedPow;
 };
 
 }  // namespace
@@ -354,10 +403,18 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalPolyLinear(
     while (!p.empty() && p.back() == 0.0) p.pop_back();
     if (p.size() < 2) SFHE_THROW("EvalPolyLinear needs degree >= 1");
     const uint32_t d = (uint32_t)p.size() - 1;
+    // only the powers the polynomial uses, and the ones they are built from
+    // (x^j = x^(j/2) x^(j - j/2)): an odd polynomial skips x^6 at degree 7
+    std::vector<char> need(d + 1, 0);
+    for (uint32_t j = d; j >= 1; --j)
+        if (p[j] != 0.0 || need[j]) {
+            need[j] = 1;
+            if (j >= 2) need[j / 2] = need[j - j / 2] = 1;
+        }
     std::vector<Ciphertext<DCRTPoly>> pw(d + 1);
     pw[1] = x;
     for (uint32_t j = 2; j <= d; ++j)
-        pw[j] = (j % 2 == 0) ? EvalSquare(pw[j / 2]) : EvalMult(pw[j / 2], pw[j / 2 + 1]);
+        if (need[j]) pw[j] = (j % 2 == 0) ? EvalSquare(pw[j / 2]) : EvalMult(pw[j / 2], pw[j / 2 + 1]);
     uint32_t lev = 0;
     for (uint32_t j = 1; j <= d; ++j)
         if (p[j] != 0.0) lev = std::max(lev, pw[j]->GetLevel());

@@ -101,7 +101,10 @@ def test_precision_attribution():
     print(f"default {base}\nno self offset {no_off}\nno lazy rescaling {no_lazy}\nno sinc rebase {no_reb}")
     assert base["rank"] < 5e-6 and base["sort"] < 8e-5       # measured 1.1e-6 / 2.6e-5
     assert no_off["rank"] > 20 * base["rank"]                 # ~1e-4: the self term's sign gain
-    assert no_lazy["sort"] > 1.15 * base["sort"]              # unrescaled sums (measured 3.2e-5, 1.25x)
+    # lazy rescaling moves the sort's error by less than its run-to-run
+    # spread here (2.6e-5 .. 4.4e-5 across op orders); it matters for hybrid1
+    # (test_hybrid1.py's 1.8e-6 gate).  Both stay inside the gate:
+    assert no_lazy["rank"] < 5e-6 and no_lazy["sort"] < 8e-5
     assert no_reb["sort"] > 20 * base["sort"]                 # giant steps at +-1 on the hits
 
 
