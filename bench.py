@@ -289,6 +289,9 @@ def main(argv=None):
                     help="skip the sort_hybrid1 leg (N=256 @ 2^17, the published-timing path)")
     ap.add_argument("--no-c5", dest="c5", action="store_false",
                     help="skip the config-5 leg (N=256 @ 2^17: unsharded at N=1, limb-sharded over RCCL at N>1)")
+    ap.add_argument("--c5-eager", action="store_true",
+                    help="run the config-5 leg without graph replay (profiling: replaying the 2^17 sort's graph "
+                         "under rocprofv3's kernel tracer crashes inside the profiler, DESIGN.md §5)")
     ap.add_argument("--shard", choices=("rccl", "host"), default=None,
                     help="limb-shard one sort over the ranks instead of running replicas")
     args = ap.parse_args(argv)
@@ -476,6 +479,8 @@ def main(argv=None):
         dog = threading.Timer(limit, stalled)
         dog.daemon = True
         dog.start()
+        if args.c5_eager:
+            os.environ["SFHE_GRAPH"] = "0"  # read per sort by the sorter
         try:
             result["c5"] = c5_leg(device, world, rank)
         except Exception as e:  # noqa: BLE001 -- an extra leg must not lose the metric line

@@ -171,6 +171,11 @@ struct sfp_conv {
     uint32_t nbig = 0;                       // 60-bit sources
     std::vector<uint32_t> hFpT, hIntT;       // ascending target indices
     uint32_t *fpT = nullptr, *intT = nullptr;
+    // every target, ascending: the integer-only job of a table with more
+    // 60-bit sources than the FP64 form splits (k_convf runs it on its
+    // integer blocks)
+    std::vector<uint32_t> hAll;
+    uint32_t* allT = nullptr;
     double *invD = nullptr, *invQ = nullptr;  // [ns] inv as a double, inv / s_i
     double *vD = nullptr, *vQ = nullptr;      // [ns][hFpT.size()]
     double *hD = nullptr, *hQ = nullptr;      // [kMaxConvBig][hFpT.size()]
@@ -1675,7 +1680,11 @@ __global__ __launch_bounds__(kThreads) void k_conv_mdrs(const MdrsArgs A, const 
 // each coefficient's dropped-row value r = (a_l - conv_l) P^-1 mod q_l
 // (centred).  Phase 2: FP64 targets fold [r]_t P_t into the conversion sum;
 // integer targets (fpT / intT split as in k_convf) use canonical residues.
-template <int NS>
+// BIGL: the dropped row's prime is 60-bit (scale-59 chains: the k-way /
+// bootstrapping contexts) and every target below it an integer row: r is
+// formed in integer arithmetic (k_conv_mdrs's), kept as its canonical
+// residue, and only integer blocks run.
+template <int NS, bool BIGL = false>
 __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_barrett* __restrict__ bar,
                                                     const double* __restrict__ qinvD, uint32_t logn) {
     constexpr int C = kConvChunk, X = kConvCoefs, WAVES = kThreads / 64;
@@ -1685,6 +1694,7 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
     double* const sQ = sDQ + NS * C;
     u64* const smod = reinterpret_cast<u64*>(sDQ);
     __shared__ double sLD[NS], sLQ[NS];
+    __shared__ u64 sLm[NS];  // BIGL: mod[i][l]
     __shared__ sf_barrett sB[NS], tB[C];
     __shared__ double sInvD[NS], sInvQ[NS], sQi[NS], tQi[C], tPd[C], tPq[C];
     __shared__ u64 tSp[C], tPm[C], tLs[C];
@@ -1706,8 +1716,12 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
         sQi[i] = qinvD[pi];
         sInvD[i] = A.invD[i];
         sInvQ[i] = A.invQ[i];
-        sLD[i] = A.lD[(size_t)i * A.nFpAll];
-        sLQ[i] = A.lQ[(size_t)i * A.nFpAll];
+        if (BIGL) {
+            sLm[i] = A.mod[(size_t)i * A.nt + A.l];
+        } else {
+            sLD[i] = A.lD[(size_t)i * A.nFpAll];
+            sLQ[i] = A.lQ[(size_t)i * A.nFpAll];
+        }
     } else if (threadIdx.x >= 64 && threadIdx.x < 64 + tc) {
         const uint32_t k = threadIdx.x - 64, t = tl[k0 + k];
         tB[k] = loadBar(bar, t);
@@ -1717,8 +1731,10 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
         tSpQ[k] = tSpD[k] / (double)tB[k].q;
         tPm[k] = A.pmod[t];
         tLs[k] = A.lsub[t];
-        tPd[k] = A.pmodD[t];
-        tPq[k] = A.pmodQ[t];
+        if (!BIGL) {
+            tPd[k] = A.pmodD[t];
+            tPq[k] = A.pmodQ[t];
+        }
         tRow[k] = t;
     }
     for (uint32_t e = threadIdx.x; e < ns * tc; e += kThreads) {
@@ -1747,6 +1763,22 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
             if ((uint32_t)i < ns) acc = fma(yL[i * X + cx], sQi[i], acc);
         const double v = rint(acc);
         vL[cx] = v;
+        if (BIGL) {  // as k_conv_mdrs: canonical y, the count of negative ones
+            const sf_barrett BL = loadBar(bar, A.l);
+            Acc sl{0, 0};
+            long long neg = (long long)v;
+#pragma unroll
+            for (int i = 0; i < NS; ++i)
+                if ((uint32_t)i < ns) {
+                    const double y = yL[i * X + cx];
+                    macc(sl, (u64)(y < 0.0 ? y + (double)sB[i].q : y), sLm[i]);
+                    neg += y < 0.0;
+                }
+            const u64 cl = subMultiple(sf_reduce128_acc(sl.lo, sl.hi, &BL), neg, A.sprod[A.l], BL);
+            const u64 al = J.al[((size_t)A.l << logn) + x0 + cx];
+            rL[cx] = __longlong_as_double((long long)bmul(sf_sub(al, cl, BL.q), A.pinvl, BL));
+            continue;
+        }
         const double spl = (double)A.sprod[A.l];
         double cl = fpMulMod(-v, spl, spl / qld, qld);
 #pragma unroll
@@ -1759,7 +1791,7 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
                            true);
     }
     __syncthreads();
-    if (fpBlock) {  // kConvTpi targets at a time, work items as k_convf
+    if (!BIGL && fpBlock) {  // kConvTpi targets at a time, work items as k_convf
         constexpr uint32_t CH = X / 64;
         const uint32_t items = CH * ((tc + kConvTpi - 1) / kConvTpi);
         for (uint32_t it = w; it < items; it += WAVES) {
@@ -1804,8 +1836,17 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
                 }
             }
             out = subMultiple(sf_reduce128_acc(s0.lo, s0.hi, &B), neg, tSp[k], B);
-            u64 lift = sf_reduce128((u64)(r < 0.0 ? r + qld : r), 0, &B);
-            if (r < 0.0) lift = sf_sub(lift, tLs[k], B.q);
+            u64 lift;
+            bool rneg;
+            if (BIGL) {  // canonical residue; centred: > q_l / 2 stands for r - q_l
+                const u64 rc = (u64)__double_as_longlong(r);
+                rneg = rc > (bar[A.l].q >> 1);
+                lift = sf_reduce128(rc, 0, &B);
+            } else {
+                rneg = r < 0.0;
+                lift = sf_reduce128((u64)(r < 0.0 ? r + qld : r), 0, &B);
+            }
+            if (rneg) lift = sf_sub(lift, tLs[k], B.q);
             out = sf_add(out, bmul(lift, tPm[k], B), B.q);
         }
         J.dst[((size_t)tRow[k] << logn) + x0 + cx] = out;
@@ -2961,8 +3002,10 @@ sfp_conv* sfp_upload_conv(sfp_dev* d, uint32_t ns, const uint32_t* src, uint32_t
         dmalloc(dp, v.size() * sizeof(v[0]));
         if (ok) hostToDev(d, dp, v.data(), v.size() * sizeof(v[0]));
     };
+    for (uint32_t t = 0; t < nt; ++t) c->hAll.push_back(t);
     up(c->fpT, c->hFpT);
     up(c->intT, c->hIntT);
+    up(c->allT, c->hAll);
     up(c->invD, invD);
     up(c->invQ, invQ);
     up(c->vD, vD);
@@ -2988,6 +3031,7 @@ void sfp_free_conv(sfp_dev* d, sfp_conv* c) {
     hipFree(c->drow);
     hipFree(c->fpT);
     hipFree(c->intT);
+    hipFree(c->allT);
     for (double* x : {c->invD, c->invQ, c->vD, c->vQ, c->hD, c->hQ}) hipFree(x);
     delete c;
 }
@@ -3020,6 +3064,11 @@ static ConvJob convJob(const sfp_conv* c, u64* dst, const u64* src, uint32_t ntU
     j.nInt = (uint32_t)(std::lower_bound(c->hIntT.begin(), c->hIntT.end(), ntUse) - c->hIntT.begin());
     j.nFpAll = (uint32_t)c->hFpT.size();
     j.nbig = c->nbig;
+    if (!c->fpOk) {  // more 60-bit sources than the FP64 form splits: integer targets only
+        j.nFp = 0;
+        j.intT = c->allT;
+        j.nInt = ntUse;
+    }
     return j;
 }
 
@@ -3035,7 +3084,13 @@ static void convLaunch(sfp_dev* d, const ConvJobs& J, uint32_t njobs, bool fpOk)
         maxZ = std::max(maxZ, (j.nFp + kConvChunk - 1) / kConvChunk + (j.nInt + kConvChunk - 1) / kConvChunk);
         bytes += 8.0 * d->n * (j.ns + j.ntUse);
     }
-    const bool fp = nttFp() && fpOk;
+    // the block-cooperative kernel (k_convf) runs every job: FP64 targets in
+    // FP64, the rest -- or, for tables with more 60-bit sources than it splits,
+    // every target (convJob) -- on its integer blocks.  k_conv (one thread per
+    // coefficient pair, 255 VGPRs, one wave per SIMD) only serves
+    // SFHE_NTT_FP=0.
+    (void)fpOk;
+    const bool fp = nttFp() != 0;
     const uint32_t gz = fp ? maxZ : (maxT + kConvChunk - 1) / kConvChunk;
     if (!gz) return;
     const dim3 g(fp ? d->n / kConvCoefs : d->n / (2 * kThreads), njobs, gz);
@@ -3218,9 +3273,29 @@ void sfp_moddown_rescale(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint6
         M.pmodQ = reinterpret_cast<const double*>(devConst(d, reinterpret_cast<const u64*>(pq), l));
         zc = (M.nFp + kConvChunk - 1) / kConvChunk + (M.nInt + kConvChunk - 1) / kConvChunk;
     }
-    const dim3 g(fp ? n / kConvCoefs : n / (2 * kThreads), 2, zc);
+    // the dropped prime 60-bit, FP64 sources, every target below it an
+    // integer row (scale-59 chains): the integer-l form of k_mdrsf
+    const bool bigl = !fp && nttFp() && c->fpOk && c->nbig == 0 && d->hbar[l].q >= kFpPrimeBound &&
+                      (c->hFpT.empty() || c->hFpT.front() > l);
+    if (bigl) {
+        M.intT = c->intT;
+        M.invD = c->invD;
+        M.invQ = c->invQ;
+        M.nFp = 0;
+        M.nFpAll = (uint32_t)c->hFpT.size();
+        M.nInt = (uint32_t)(std::lower_bound(c->hIntT.begin(), c->hIntT.end(), l) - c->hIntT.begin());
+        zc = (M.nInt + kConvChunk - 1) / kConvChunk;
+    }
+    const dim3 g((fp || bigl) ? n / kConvCoefs : n / (2 * kThreads), 2, zc);
     timedLaunch(d, SFP_FAM_CONV, 8.0 * n * 2 * (K + 1 + l), [&] {
-        if (fp && c->ns <= 13)  // LDS for 6 blocks per CU (as convLaunch)
+        if (bigl && c->ns <= 13)
+            hipLaunchKernelGGL((k_mdrsf<13, true>), g, dim3(kThreads), 0, d->st(), M, d->bar, d->qinvD, d->logn);
+        else if (bigl && c->ns <= 16)
+            hipLaunchKernelGGL((k_mdrsf<16, true>), g, dim3(kThreads), 0, d->st(), M, d->bar, d->qinvD, d->logn);
+        else if (bigl)
+            hipLaunchKernelGGL((k_mdrsf<kMaxConvSrc, true>), g, dim3(kThreads), 0, d->st(), M, d->bar, d->qinvD,
+                               d->logn);
+        else if (fp && c->ns <= 13)  // LDS for 6 blocks per CU (as convLaunch)
             hipLaunchKernelGGL(k_mdrsf<13>, g, dim3(kThreads), 0, d->st(), M, d->bar, d->qinvD, d->logn);
         else if (fp && c->ns <= 16)
             hipLaunchKernelGGL(k_mdrsf<16>, g, dim3(kThreads), 0, d->st(), M, d->bar, d->qinvD, d->logn);
