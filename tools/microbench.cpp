@@ -34,6 +34,9 @@ static void printTrace(sfp_dev* d) {
 
 template <class F>
 static double timeIt(sfp_dev* d, int iters, F&& f) {
+    // MB_REPS caps the repetitions (PMC passes serialise every dispatch)
+    static const int cap = std::getenv("MB_REPS") ? std::atoi(std::getenv("MB_REPS")) : 0;
+    if (cap > 0 && iters > cap) iters = cap;
     f();
     sfp_sync(d);
     auto t0 = std::chrono::high_resolution_clock::now();
@@ -120,6 +123,7 @@ int main(int argc, char** argv) {
         auto ct = cc->Encrypt(cc->KeyGen().publicKey, cc->MakeCKKSPackedPlaintext(std::vector<double>(256, 0.5)));
         cc->EvalMultKeyGen(cc->KeyGen().secretKey);
         auto sq = cc->EvalMult(ct, ct);  // builds the modup tables of the top level
+        cc->Settle(sq);                  // (a lazy product relinearises when settled)
         (void)sq;
         convs = s->modupConv.at(ell);
     }
