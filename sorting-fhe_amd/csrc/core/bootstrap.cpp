@@ -299,10 +299,9 @@ Ciphertext<DCRTPoly> applyGroup(CryptoContextImpl<DCRTPoly>* cc, Group& gr, uint
 
 Ciphertext<DCRTPoly> evalMod(CryptoContextImpl<DCRTPoly>* cc, const BootstrapPrecomp& b, Ciphertext<DCRTPoly> y) {
     auto c = cc->EvalChebyshevSeriesPS(y, b.cheb, -1.0, 1.0);
-    for (uint32_t i = 0; i < kDoubleAngles; ++i) {
-        auto sq = cc->EvalSquare(c);
-        c = cc->EvalAdd(cc->EvalAdd(sq, sq), -1.0);
-    }
+    // cos 2t = 2 cos^2 t - 1, the factor 2 on an operand so the product's
+    // rescale rounding enters once per angle doubling, not twice (chebyshev.cpp)
+    for (uint32_t i = 0; i < kDoubleAngles; ++i) c = cc->EvalAdd(cc->EvalMult(cc->EvalAdd(c, c), c), -1.0);
     return c;
 }
 

@@ -78,14 +78,16 @@ class PSEvaluator {
         : cc(cc), l(l), k(1u << l), D(D) {
         T.resize(k + 1);
         T[1] = y;
+        // T_2a = 2 T_a^2 - 1, T_2a+1 = 2 T_a T_a+1 - T_1, the factor 2 taken on
+        // an operand: doubling the product after its rescale would double the
+        // rescale's rounding error too, and at the extrema of T_a (|T_a| = 1,
+        // where the error of each doubling already grows 4x) that is what
+        // the series' error is made of.  (A lazily rescaled product gets the
+        // same by adding before its rescale; the series holds those off.)
         for (uint32_t j = 2; j <= k; ++j) {
-            Ct prod;
-            if (j % 2 == 0)
-                prod = cc->EvalSquare(T[j / 2]);
-            else
-                prod = cc->EvalMult(T[j / 2], T[j / 2 + 1]);
-            Ct two = cc->EvalAdd(prod, prod);
-            T[j] = (j % 2 == 0) ? cc->EvalAdd(two, -1.0) : cc->EvalSub(two, atLevel(1, two->GetLevel()));
+            const Ct& a = T[j / 2];
+            Ct prod = cc->EvalMult(doubled(j / 2), j % 2 == 0 ? a : T[j / 2 + 1]);
+            T[j] = (j % 2 == 0) ? cc->EvalAdd(prod, -1.0) : cc->EvalSub(prod, atLevel(1, prod->GetLevel()));
         }
         giant[l] = T[k];
     }
@@ -214,6 +216,7 @@ class PSEvaluator {
     // level of a node's product q T_M: the natural one (q and T_M as they come,
     // +1) or `want`, whichever is deeper
     uint32_t productLevel(const std::vector<double>& q, uint32_t depth, uint32_t M, uint32_t want) const {
+        if (naturalOnly()) want = 0;
         const int nq = natural(q, depth - 1);
         const uint32_t nat = (uint32_t)std::max(nq, (int)powerLevel(M)) + 1;
         return std::max(nat, want);
@@ -239,11 +242,22 @@ class PSEvaluator {
     // level of the leaf's weighted sum (its output is one level deeper): the
     // deepest input's, or want - 1 when that is deeper; -1 if p is a constant
     int leafSumLevel(const std::vector<double>& p, uint32_t want) const {
+        if (naturalOnly()) want = 0;
         int lev = -1;
         for (uint32_t j = 1; j < p.size(); ++j)
             if (p[j] != 0.0) lev = std::max(lev, (int)T[j]->GetLevel());
         if (lev < 0) return -1;
         return std::max(lev, (int)want - 1);
+    }
+
+    // SFHE_PS_NATURAL=1: every node and leaf at its natural level, the sums
+    // aligning the shallower operand (the pre-targeting plan; noise probe)
+    static bool naturalOnly() {
+        static const bool on = [] {
+            const char* v = std::getenv("SFHE_PS_NATURAL");
+            return v && *v == '1';
+        }();
+        return on;
     }
 
     static void trim(std::vector<double>& p) {
@@ -263,8 +277,15 @@ class PSEvaluator {
         auto it = giant.find(i);
         if (it != giant.end()) return it->second;
         const Ct& half = power(M / 2);
-        Ct sq = cc->EvalSquare(half);
-        return giant[i] = cc->EvalAdd(cc->EvalAdd(sq, sq), -1.0);
+        const Ct twice = cc->EvalAdd(half, half);  // 2 T_M before the rescale, as above
+        return giant[i] = cc->EvalAdd(cc->EvalMult(twice, half), -1.0);
+    }
+
+    // 2 T_j, memoised (an odd T_j+1's product reuses T_j's)
+    const Ct& doubled(uint32_t j) {
+        auto it = twice.find(j);
+        if (it != twice.end()) return it->second;
+        return twice[j] = cc->EvalAdd(T[j], T[j]);
     }
 
     // T_M at `level` (>= its own): one AdjustLevel per (M, level), memoised
@@ -324,6 +345,7 @@ class PSEvaluator {
     std::vector<Ct> T;
     std::map<uint32_t, Ct> giant;
     std::map<std::pair<uint32_t, uint32_t>, Ct> aligned, alignedPow;
+    std::map<uint32_t, Ct> twice;
 };
 
 }  // namespace

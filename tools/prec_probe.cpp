@@ -10,6 +10,7 @@
 //                                            a lazily rescaled ciphertext, so taps change the noise)
 //   prec_probe h2s N logn [secure] [seed]    hybrid II's scaled-sinc stage: input noise vs the
 //                                            noise the series adds, binned by |x|
+//   prec_probe sinc N logn [0] [seed]        SincTest's encrypted doubled-sinc series alone
 //
 // Engine knobs under test are read from the environment by the library.
 #include <algorithm>
@@ -438,6 +439,43 @@ int run(const std::string& mode, int logn, bool secure, unsigned seed) {
     return 0;
 }
 
+// tests/SincTest.cpp's encrypted experiment (depth 15, default scales, a
+// uniform grid on [-1, 1] over every slot): the doubled-sinc series' error,
+// split at |x| < 1/(2N) (the hit, an extremum of every giant step)
+template <int N>
+int sincSeries(int logn, unsigned seed) {
+    CCParams<CryptoContextCKKSRNS> params;
+    params.SetSecurityLevel(HEStd_NotSet);
+    params.SetRingDim(1u << logn);
+    params.SetMultiplicativeDepth(15);
+    params.SetSeed(seed);
+    auto cc = GenCryptoContext(params);
+    cc->Enable(PKE);
+    cc->Enable(KEYSWITCH);
+    cc->Enable(LEVELEDSHE);
+    cc->Enable(ADVANCEDSHE);
+    auto kp = cc->KeyGen();
+    cc->EvalMultKeyGen(kp.secretKey);
+    Probe P{cc, kp.secretKey};
+    const auto& coeffs = selectDoubledSincCoefficients<N>();
+    const size_t slots = (1u << logn) / 2;
+    Vec x(slots), f(slots);
+    for (size_t i = 0; i < slots; ++i) {
+        x[i] = -1.0 + 2.0 * (double)i / (double)(slots - 1);
+        f[i] = Sinc<2 * N>::doubled_sinc(x[i]);
+    }
+    auto pt = cc->MakeCKKSPackedPlaintext(x);
+    auto ct = cc->Encrypt(kp.publicKey, pt);
+    auto out = cc->EvalChebyshevSeriesPS(ct, coeffs, -1.0, 1.0);
+    Vec d = P.dec(out);
+    double m0, r0, m1, r1;
+    P.stat(d, f, [&](size_t i) { return std::fabs(x[i]) < 0.5 / N; }, m0, r0);
+    P.stat(d, f, [&](size_t i) { return std::fabs(x[i]) >= 0.5 / N; }, m1, r1);
+    std::printf("sinc N=%d degree %zu ring 2^%d level %u | hit max %.3e rms %.3e | rest max %.3e rms %.3e\n", N,
+                coeffs.size() - 1, logn, out->GetLevel(), m0, r0, m1, r1);
+    return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -450,6 +488,13 @@ int main(int argc, char** argv) {
     bool secure = argc > 4 && std::atoi(argv[4]);
     unsigned seed = argc > 5 ? (unsigned)std::atoi(argv[5]) : 20251205u + N;
     std::cout.setstate(std::ios::failbit);  // the sort's progress prints
+    if (mode == "sinc") switch (N) {
+            case 32: return sincSeries<32>(logn, seed);
+            case 64: return sincSeries<64>(logn, seed);
+            case 128: return sincSeries<128>(logn, seed);
+            case 256: return sincSeries<256>(logn, seed);
+            default: std::fprintf(stderr, "sinc: N in {32, 64, 128, 256}\n"); return 2;
+        }
     switch (N) {
         case 8: return run<8>(mode, logn, secure, seed);
         case 64: return run<64>(mode, logn, secure, seed);
