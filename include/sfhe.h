@@ -136,6 +136,10 @@ int sfhe_eval_mult_plain(sfhe_ctx* c, const sfhe_ct* a, const double* values, si
 int sfhe_eval_mult(sfhe_ctx* c, const sfhe_ct* a, const sfhe_ct* b, sfhe_ct** out);
 /* EvalRotate (rotation.h:224) */
 int sfhe_eval_rotate(sfhe_ctx* c, const sfhe_ct* a, int32_t r, sfhe_ct** out);
+/* sum_k EvalRotate(a[k], r[k]) with one shared ModDown (engine extension:
+ * output aggregation of the giant steps of vecRotsOpt / blindRotationOptN,
+ * src/sort_algo.h:342-364, 561-584, which sum individually rotated terms) */
+int sfhe_eval_rotate_sum(sfhe_ctx* c, const sfhe_ct* const* a, const int32_t* r, size_t count, sfhe_ct** out);
 /* CKKS bootstrapping (OpenFHE's EvalBootstrapSetup + EvalBootstrapKeyGen and
  * EvalBootstrap, as src/k-way/EvalUtils.cpp:57-86 and src/sort_algo.h:1437
  * call them): setup for ciphertexts of `slots` slots with the level budget

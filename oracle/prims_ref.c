@@ -263,6 +263,12 @@ void sfp_mac_plain2(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint64_t* 
     sfp_mac_plain(d, out0, a0, b, nin, m);
     sfp_mac_plain(d, out1, a1, b, nin, m);
 }
+
+void sfp_mac_plain_multi(sfp_dev* d, uint64_t* const* out0, uint64_t* const* out1, const uint64_t* const* a0,
+                         const uint64_t* const* a1, const uint64_t* const* b, uint32_t nin, uint32_t nout,
+                         sfp_limbs m) {
+    for (uint32_t g = 0; g < nout; ++g) sfp_mac_plain2(d, out0[g], out1[g], a0, a1, b + (size_t)g * nin, nin, m);
+}
 void sfp_mac_plain(sfp_dev* d, uint64_t* out, const uint64_t* const* a, const uint64_t* const* b,
                    uint32_t nin, sfp_limbs m) {
     LOOP_LIMBS({
@@ -478,10 +484,29 @@ void sfp_ks_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ex
     sfp_ks_inner_fold(d, acc0, acc1, ext, ext_stride, key, beta, ell, K, Lq, NULL, NULL, 0);
 }
 
+static void ks_inner_rows(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
+                          size_t ext_stride, const uint64_t* key, uint32_t beta, uint32_t ell,
+                          uint32_t K, uint32_t Lq, const uint64_t* fold0, const uint64_t* fold1,
+                          uint64_t fold_k, int accum);
+
 void sfp_ks_inner_fold(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
                        size_t ext_stride, const uint64_t* key, uint32_t beta, uint32_t ell,
                        uint32_t K, uint32_t Lq, const uint64_t* fold0, const uint64_t* fold1,
                        uint64_t fold_k) {
+    ks_inner_rows(d, acc0, acc1, ext, ext_stride, key, beta, ell, K, Lq, fold0, fold1, fold_k, 0);
+}
+
+void sfp_ks_inner_acc(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
+                      size_t ext_stride, const uint64_t* key, uint32_t beta, uint32_t ell, uint32_t K,
+                      uint32_t Lq) {
+    ks_inner_rows(d, acc0, acc1, ext, ext_stride, key, beta, ell, K, Lq, NULL, NULL, 0, 1);
+}
+
+// acc (+)= sum_j ext_j * key_j (mod q) per ext limb (sfp_ks_inner / _fold / _acc)
+static void ks_inner_rows(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
+                          size_t ext_stride, const uint64_t* key, uint32_t beta, uint32_t ell,
+                          uint32_t K, uint32_t Lq, const uint64_t* fold0, const uint64_t* fold1,
+                          uint64_t fold_k, int accum) {
     const uint32_t n = d->n, rows = ell + K, NP = Lq + K;
 #pragma omp parallel for schedule(static)
     for (uint32_t t = 0; t < rows; ++t) {
@@ -499,6 +524,10 @@ void sfp_ks_inner_fold(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_
             if (fold0 && t == ell - 1) {
                 s0 += (u128)fold0[(size_t)t * n + x] * fold_k;
                 s1 += (u128)fold1[(size_t)t * n + x] * fold_k;
+            }
+            if (accum) {
+                s0 += acc0[(size_t)t * n + x];
+                s1 += acc1[(size_t)t * n + x];
             }
             acc0[(size_t)t * n + x] = (u64)(s0 % q);
             acc1[(size_t)t * n + x] = (u64)(s1 % q);
@@ -651,7 +680,7 @@ void sfp_rescale_rows(sfp_dev* d, uint64_t* out, const uint64_t* in, const uint6
 
 void sfp_ks_inner_map(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
                       size_t ext_stride, const uint64_t* key, uint32_t beta, sfp_limbs pm,
-                      uint32_t keyQ, uint32_t key_rows) {
+                      uint32_t keyQ, uint32_t key_rows, int accum) {
     const uint32_t n = d->n;
 #pragma omp parallel for schedule(static)
     for (uint32_t t = 0; t < pm.count; ++t) {
@@ -665,6 +694,10 @@ void sfp_ks_inner_map(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t
                 const u64* ka = kb + (size_t)key_rows * n;
                 s0 += (u128)e * kb[(size_t)kr * n + x];
                 s1 += (u128)e * ka[(size_t)kr * n + x];
+            }
+            if (accum) {
+                s0 += acc0[(size_t)t * n + x];
+                s1 += acc1[(size_t)t * n + x];
             }
             acc0[(size_t)t * n + x] = (u64)(s0 % q);
             acc1[(size_t)t * n + x] = (u64)(s1 % q);

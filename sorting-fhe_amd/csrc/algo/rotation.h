@@ -169,6 +169,29 @@ class RotationComposer {
         return out;
     }
 
+    // sum_k rotate(in_k, rotations_k), the value of EvalAddMany over rotate():
+    // each term's steps but the last are applied as rotate() would, and the
+    // last steps of all terms share one ModDown (EvalRotateSum).
+    Ciphertext<DCRTPoly> rotateSum(const std::vector<Ciphertext<DCRTPoly>>& in,
+                                   const std::vector<int>& rotations) {
+        std::vector<Ciphertext<DCRTPoly>> pre;
+        std::vector<int32_t> last;
+        for (size_t k = 0; k < in.size(); ++k) {
+            const int r = rotations[k], slots = (int)in[k]->GetSlots();
+            if (r % slots == 0 || m_keys.count(r)) {
+                pre.push_back(in[k]);
+                last.push_back(r % slots == 0 ? 0 : r);
+                continue;
+            }
+            const auto steps = m_decomposer.decompose(r, slots, m_algo);
+            Ciphertext<DCRTPoly> x = in[k];
+            for (size_t i = 0; i + 1 < steps.size(); ++i) x = m_cc->EvalRotate(x, steps[i].stepSize);
+            pre.push_back(x);
+            last.push_back(steps.empty() ? 0 : steps.back().stepSize);
+        }
+        return m_cc->EvalRotateSum(pre, last);
+    }
+
     const std::set<int>& getRotationCalls() const { return rotation_calls; }
     void clearRotationCalls() { rotation_calls.clear(); }
 

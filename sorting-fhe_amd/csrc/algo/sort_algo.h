@@ -328,22 +328,28 @@ class DirectSort : public SortBase<N> {
         return v;
     }
 
+    // The giant steps' rotations is*P + j*np are applied as one rotation by
+    // is*P of the sum over j of rotations by j*np (rotations are linear), and
+    // that sum shares one ModDown (rotateSum, output aggregation): per batch
+    // P/np key switches with one ModDown instead of up to 2 P/np of each.
     Ciphertext<DCRTPoly> vecRotsOpt(const std::vector<Ciphertext<DCRTPoly>>& pre,
                                     int num_partition, int num_slots, int np, int is) {
-        std::vector<Ciphertext<DCRTPoly>> giants;
+        std::vector<std::vector<Plaintext>> masks;
+        std::vector<int> steps;
         for (int j = 0; j < num_partition / np; ++j) {
             const int shift = is * num_partition + j * np;
-            auto& masks = maskMemo({0, is, j, (int)pre[0]->GetLevel(), num_slots}, [&](auto& v) {
+            masks.push_back(maskMemo({0, is, j, (int)pre[0]->GetLevel(), num_slots}, [&](auto& v) {
                 for (int i = 0; i < np; ++i)
                     v.push_back(m_cc->MakeCKKSPackedPlaintext(
                         vectorRotate(generateMaskVector(num_slots, np * j + i), -shift), 1,
                         pre[i]->GetLevel(), nullptr, num_slots));
-            });
-            auto T = m_cc->EvalMultAddPlain(pre, masks);
-            T->SetSlots(num_slots);
-            giants.push_back(rot.rotate(T, shift));
+            }));
+            steps.push_back(j * np);
         }
-        return m_cc->EvalAddMany(giants);
+        // T_j = sum_i pre_i * mask_{np j + i} for every j at once (each pre_i read once)
+        auto giants = m_cc->EvalMultAddPlainMany(pre, masks);
+        for (auto& T : giants) T->SetSlots(num_slots);
+        return rot.rotate(rot.rotateSum(giants, steps), is * num_partition);
     }
 
     Ciphertext<DCRTPoly> constructRank(const Ciphertext<DCRTPoly>& input_array, SignFunc SignFunc,
@@ -398,22 +404,25 @@ class DirectSort : public SortBase<N> {
         return m_cc->EvalSub(rank, offsetSelf ? 1.0 : 0.5);
     }
 
-    // Rotates partition k = np*i + j of the masked inputs left by ib*P + k.
+    // Rotates partition k = np*i + j of the masked inputs left by ib*P + k
+    // (giant steps summed as in vecRotsOpt: one rotation by ib*P of a
+    // rotateSum over i*np).
     Ciphertext<DCRTPoly> blindRotationOptN(const std::vector<Ciphertext<DCRTPoly>>& masked_inputs,
                                            int num_slots, int np, int ib, int num_partition) {
-        std::vector<Ciphertext<DCRTPoly>> giants;
+        std::vector<std::vector<Plaintext>> masks;
+        std::vector<int> steps;
         for (int i = 0; i < (num_slots / N) / np; ++i) {
-            auto& masks = maskMemo({1, 0, i, (int)masked_inputs[0]->GetLevel(), num_slots}, [&](auto& v) {
+            masks.push_back(maskMemo({1, 0, i, (int)masked_inputs[0]->GetLevel(), num_slots}, [&](auto& v) {
                 for (int j = 0; j < np; ++j)
                     v.push_back(m_cc->MakeCKKSPackedPlaintext(
                         vectorRotate(generateMaskVectorN(num_slots, np * i + j), j), 1,
                         masked_inputs[j]->GetLevel(), nullptr, num_slots));
-            });
-            auto tmp = m_cc->EvalMultAddPlain(masked_inputs, masks);
-            giants.push_back(rot.rotate(tmp, ib * num_partition + i * np));
+            }));
+            steps.push_back(i * np);
         }
+        const auto giants = m_cc->EvalMultAddPlainMany(masked_inputs, masks);
         auto result = this->getZero()->Clone();
-        m_cc->EvalAddInPlace(result, m_cc->EvalAddMany(giants));
+        m_cc->EvalAddInPlace(result, rot.rotate(rot.rotateSum(giants, steps), ib * num_partition));
         return result;
     }
 
@@ -657,16 +666,18 @@ class DirectSort : public SortBase<N> {
                                             int np, int ib) {
         (void)ib;
         std::vector<Ciphertext<DCRTPoly>> giants;
+        std::vector<int> steps;
         for (int i = 0; i < (num_slots / N / 2) / np; ++i) {
             auto& masks = maskMemo({9, 0, i, (int)masked_inputs[0]->GetLevel(), num_slots}, [&](auto& v) {
                 for (int j = 0; j < np; ++j)
                     v.push_back(m_cc->MakeCKKSPackedPlaintext(vectorRotate(generateMaskVector2N(num_slots, np * i + j), j),
                                                               1, masked_inputs[j]->GetLevel(), nullptr, num_slots));
             });
-            giants.push_back(rot.rotate(m_cc->EvalMultAddPlain(masked_inputs, masks), i * np));
+            giants.push_back(m_cc->EvalMultAddPlain(masked_inputs, masks));
+            steps.push_back(i * np);
         }
         auto result = this->getZero()->Clone();
-        m_cc->EvalAddInPlace(result, m_cc->EvalAddMany(giants));
+        m_cc->EvalAddInPlace(result, rot.rotateSum(giants, steps));
         return result;
     }
 

@@ -349,6 +349,15 @@ int sfhe_eval_rotate(sfhe_ctx* c, const sfhe_ct* a, int32_t r, sfhe_ct** out) {
     REQUIRE(c && a && out, "null argument");
     return guard([&] { *out = wrap(c->cc->EvalRotate(a->ct, r)); });
 }
+int sfhe_eval_rotate_sum(sfhe_ctx* c, const sfhe_ct* const* a, const int32_t* r, size_t count, sfhe_ct** out) {
+    REQUIRE(c && a && r && out && count, "null argument");
+    for (size_t k = 0; k < count; ++k) REQUIRE(a[k], "null argument");
+    return guard([&] {
+        std::vector<Ciphertext<DCRTPoly>> v;
+        for (size_t k = 0; k < count; ++k) v.push_back(a[k]->ct);
+        *out = wrap(c->cc->EvalRotateSum(v, std::vector<int32_t>(r, r + count)));
+    });
+}
 int sfhe_bootstrap_setup(sfhe_ctx* c, uint32_t budget_c2s, uint32_t budget_s2c, uint32_t slots) {
     REQUIRE(c, "null argument");
     REQUIRE(c->keys.secretKey, "sfhe_keygen must be called first");

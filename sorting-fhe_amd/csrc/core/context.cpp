@@ -605,12 +605,24 @@ class SfheInternal {
     static void innerModDownShard(SfheContextState* s, const uint64_t* ext, size_t stride, uint32_t beta,
                                   uint32_t ell, const DeviceBufferPtr& key, uint64_t* out0, uint64_t* out1,
                                   int add0, int add1) {
-        const uint32_t n = s->n, K = s->K, lr = s->rows(ell), lp = s->prows();
-        const sfp_limbs em = s->extmap(ell);
-        const size_t aw = (size_t)em.count * n;
+        const size_t aw = (size_t)s->extmap(ell).count * s->n;
         auto acc = s->alloc(2 * aw);
-        sfp_ks_inner_map(s->dev, acc->ptr, acc->ptr + aw, ext, stride, key->ptr, beta, em, s->rows(s->Lq),
-                         s->rows(s->Lq) + lp);
+        innerShard(s, acc->ptr, ext, stride, beta, ell, key, 0);
+        modDownShard(s, acc->ptr, ell, out0, out1, add0, add1);
+    }
+    // the local key inner product into acc (2 polys of extmap(ell) rows), accumulated when accum
+    static void innerShard(SfheContextState* s, uint64_t* acc, const uint64_t* ext, size_t stride, uint32_t beta,
+                           uint32_t ell, const DeviceBufferPtr& key, int accum) {
+        const sfp_limbs em = s->extmap(ell);
+        const size_t aw = (size_t)em.count * s->n;
+        sfp_ks_inner_map(s->dev, acc, acc + aw, ext, stride, key->ptr, beta, em, s->rows(s->Lq),
+                         s->rows(s->Lq) + s->prows(), accum);
+    }
+    // ModDown of the local accumulators (their P rows are destroyed)
+    static void modDownShard(SfheContextState* s, uint64_t* acc, uint32_t ell, uint64_t* out0, uint64_t* out1,
+                             int add0, int add1) {
+        const uint32_t n = s->n, K = s->K, lr = s->rows(ell), lp = s->prows();
+        const size_t aw = (size_t)s->extmap(ell).count * n;
         // P rows: coefficient form, exchanged (both polys in one all-gather)
         const uint32_t per = (K + s->world - 1) / s->world;
         auto send = s->alloc((size_t)2 * per * n);
@@ -618,7 +630,7 @@ class SfheInternal {
         for (int p = 0; p < 2; ++p) {
             if (!lp) break;
             uint64_t* dst = send->ptr + (size_t)p * per * n;
-            sfp_d2d(s->dev, dst, acc->ptr + p * aw + (size_t)lr * n, (size_t)lp * n * 8);
+            sfp_d2d(s->dev, dst, acc + p * aw + (size_t)lr * n, (size_t)lp * n * 8);
             sfp_ntt(s->dev, dst, pm, 1);
         }
         auto all = s->alloc((size_t)2 * per * s->world * n);
@@ -638,7 +650,7 @@ class SfheInternal {
         for (int p = 0; p < 2; ++p) {
             sfp_conv_apply_centered(s->dev, conv->ptr, natP->ptr + (size_t)p * K * n, s->moddownConvShard, lr);
             sfp_ntt(s->dev, conv->ptr, s->qmap(ell), 0);
-            sfp_sub(s->dev, conv->ptr, acc->ptr + p * aw, conv->ptr, s->qmap(ell));
+            sfp_sub(s->dev, conv->ptr, acc + p * aw, conv->ptr, s->qmap(ell));
             sfp_mul_const(s->dev, conv->ptr, conv->ptr, pinv.data(), s->qmap(ell));
             if (adds[p])
                 sfp_add(s->dev, outs[p], outs[p], conv->ptr, s->qmap(ell));
@@ -2117,6 +2129,70 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMultAddPlain(
     return SfheInternal::traced(this, SfheInternal::rescale(this, t0, t1, level, slots), "EvalMultAddPlain");
 }
 
+std::vector<Ciphertext<DCRTPoly>> CryptoContextImpl<DCRTPoly>::EvalMultAddPlainMany(
+    const std::vector<Ciphertext<DCRTPoly>>& a, const std::vector<std::vector<Plaintext>>& p) {
+    OpLock g(st.get());
+    SfheContextState* s = st.get();
+    std::vector<Ciphertext<DCRTPoly>> out;
+    if (a.empty() || p.empty()) SFHE_THROW("operand count mismatch");
+    for (const auto& pg : p)
+        if (pg.size() != a.size()) SFHE_THROW("operand count mismatch");
+    if (a.size() > SFP_MAX_MACM_IN || p.size() == 1) {
+        for (const auto& pg : p) out.push_back(EvalMultAddPlain(a, pg));
+        return out;
+    }
+    SfheInternal::depsv(s, a);
+    uint32_t level = 0, slots = 0;
+    for (const auto& c : a) {
+        level = std::max(level, c->level);
+        slots = std::max(slots, c->slots);
+    }
+    for (const auto& pg : p)
+        for (const auto& pt : pg) slots = std::max(slots, pt->slots);
+    const uint32_t ell = s->ellOf(level), nin = (uint32_t)a.size(), G = (uint32_t)p.size();
+    if (ell < 2) SFHE_THROW("no levels left (multiplicative depth exhausted)");
+    std::vector<Ciphertext<DCRTPoly>> al(nin);
+    std::vector<const uint64_t*> x0(nin), x1(nin), m;
+    for (uint32_t j = 0; j < nin; ++j) {
+        al[j] = SfheInternal::adjust(this, a[j], level);
+        SfheInternal::deps(s, {&al[j]});
+        x0[j] = al[j]->c0;
+        x1[j] = al[j]->c1;
+    }
+    for (const auto& pg : p)
+        for (const auto& pt : pg) m.push_back(SfheInternal::encoded(this, pt, level));
+    const size_t pw = s->polyWords(level);
+    std::vector<DeviceBufferPtr> bufs(G);
+    std::vector<uint64_t*> o0(G), o1(G);
+    for (uint32_t k = 0; k < G; ++k) {
+        bufs[k] = s->alloc(2 * pw);
+        o0[k] = bufs[k]->ptr;
+        o1[k] = bufs[k]->ptr + pw;
+    }
+    const uint32_t per = std::min<uint32_t>(SFP_MAX_MACM_OUT, SFP_MAX_MACM_PT / nin);
+    for (uint32_t k = 0; k < G; k += per)
+        sfp_mac_plain_multi(s->dev, o0.data() + k, o1.data() + k, x0.data(), x1.data(), m.data() + (size_t)k * nin,
+                            nin, std::min(per, G - k), st->qmap(ell));
+    s->stats.ptmult += (uint64_t)nin * G;
+    s->countBytes((2.0 * nin + (double)G * nin + 2.0 * G) * ell * s->n * 8);
+    // lazy rescaling: the sums stay pending, as EvalMultAddPlain's deferred form would give them to their consumer
+    const bool pend = SfheInternal::lazy(s);
+    for (uint32_t k = 0; k < G; ++k) {
+        if (pend) {
+            auto ct = std::make_shared<CiphertextImpl<DCRTPoly>>();
+            ct->cc = shared_from_this();
+            ct->level = level + 1;
+            ct->slots = slots;
+            SfheInternal::adoptPending(*ct, bufs[k], o0[k], o1[k]);
+            out.push_back(ct);
+        } else {
+            out.push_back(SfheInternal::traced(this, SfheInternal::rescale(this, o0[k], o1[k], level, slots),
+                                               "EvalMultAddPlainMany"));
+        }
+    }
+    return out;
+}
+
 // ============================================================================
 // rotations
 
@@ -2218,6 +2294,92 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalFastRotation(
     s->stats.automorph++;
     s->countBytes((3.0 * ell + 2.0 * pre->beta * (ell + s->K)) * s->n * 8);
     return SfheInternal::traced(this, out, "EvalFastRotation");
+}
+
+// Output aggregation: the terms' key switches share the accumulator in the
+// extended basis (sfp_ks_inner_acc) and one ModDown, so a sum of R rotations
+// costs R ModUps and one ModDown instead of R of each.  Terms with a rotation
+// of a multiple of the slot count are added as they are.  SFHE_ROTSUM=0
+// (diagnostic) sums individual EvalRotates.
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotateSum(const std::vector<Ciphertext<DCRTPoly>>& a,
+                                                                const std::vector<int32_t>& r) {
+    OpLock g(st.get());
+    SfheContextState* s = st.get();
+    if (a.empty() || a.size() != r.size()) SFHE_THROW("EvalRotateSum: operand count mismatch");
+    static const bool off = [] {
+        const char* v = std::getenv("SFHE_ROTSUM");
+        return v && *v == '0';
+    }();
+    std::vector<size_t> rot, ident;
+    for (size_t k = 0; k < a.size(); ++k) (GaloisForRotation(r[k]) == 1 ? ident : rot).push_back(k);
+    const bool pend = !rot.empty() && SfheInternal::lazy(s) && SfheInternal::isLazy(a[rot[0]]);
+    bool agg = !off && rot.size() >= 2;
+    for (size_t k : rot)
+        agg = agg && a[k]->level == a[rot[0]]->level &&
+              (SfheInternal::lazy(s) && SfheInternal::isLazy(a[k])) == pend;
+    if (!agg) {
+        std::vector<Ciphertext<DCRTPoly>> terms;
+        for (size_t k = 0; k < a.size(); ++k) terms.push_back(EvalRotate(a[k], r[k]));
+        return EvalAddMany(terms);
+    }
+    std::vector<const DeviceBufferPtr*> keys;
+    for (size_t k : rot) {
+        auto it = s->rotKeys.find(GaloisForRotation(r[k]));
+        if (it == s->rotKeys.end())
+            SFHE_THROW("EvalKey for rotation " + std::to_string(r[k]) + " is not found");
+        keys.push_back(&it->second);
+    }
+    // pending products rotate before their rescale, as in EvalRotate
+    uint32_t slots = 0;
+    for (size_t k : rot) {
+        if (pend) {
+            SfheInternal::materialize(*a[k], true);
+            s->dep(a[k]->buf.get());
+        } else {
+            SfheInternal::deps(s, {&a[k]});
+        }
+        slots = std::max(slots, a[k]->slots);
+    }
+    const uint32_t level = a[rot[0]]->level, ell = SfheInternal::ctEll(s, *a[rot[0]]);
+    const uint32_t n = s->n, K = s->K, beta = (ell + s->alpha - 1) / s->alpha;
+    const bool shard = s->world > 1;  // local rows; the exchanges inside modupShard / modDownShard
+    const size_t stride = (size_t)(shard ? s->extmap(ell).count : ell + K) * n;
+    auto out = pend ? SfheInternal::newPendingCt(this, level, slots) : SfheInternal::newCt(this, level, slots);
+    auto t = s->alloc((size_t)s->rows(ell) * n);
+    auto c0 = s->alloc((size_t)s->rows(ell) * n);
+    auto ext = s->alloc(stride * beta);
+    auto scratch = s->alloc((size_t)ell * n);
+    auto acc = s->alloc(2 * stride);
+    for (size_t i = 0; i < rot.size(); ++i) {
+        const Ciphertext<DCRTPoly>& x = a[rot[i]];
+        const uint32_t gal = GaloisForRotation(r[rot[i]]);
+        // c0' = sum sigma_k(c0_k) (+ the shared ModDown below)
+        sfp_automorph(s->dev, i ? c0->ptr : out->c0, x->c0, gal, st->qmap(ell));
+        if (i) sfp_add(s->dev, out->c0, out->c0, c0->ptr, st->qmap(ell));
+        sfp_automorph(s->dev, t->ptr, x->c1, gal, st->qmap(ell));
+        if (shard) {
+            SfheInternal::modupShard(s, ext->ptr, t->ptr, ell);
+            SfheInternal::innerShard(s, acc->ptr, ext->ptr, stride, beta, ell, *keys[i], i ? 1 : 0);
+        } else {
+            sfp_modup(s->dev, ext->ptr, t->ptr, ell, K, s->Lq, s->alpha, SfheInternal::modupConv(this, ell).data(),
+                      scratch->ptr);
+            (i ? sfp_ks_inner_acc : sfp_ks_inner)(s->dev, acc->ptr, acc->ptr + stride, ext->ptr, stride,
+                                                   (*keys[i])->ptr, beta, ell, K, s->Lq);
+        }
+        s->stats.automorph++;
+        s->stats.keyswitch++;
+        s->countBytes((5.0 * ell + 2.0 * beta * (ell + K)) * n * 8);
+    }
+    if (shard) {
+        SfheInternal::modDownShard(s, acc->ptr, ell, out->c0, out->c1, 1, 0);
+    } else {
+        auto md = s->alloc((size_t)2 * ell * n);
+        sfp_moddown2(s->dev, out->c0, out->c1, acc->ptr, stride, ell, K, s->Lq, s->moddownConv,
+                     s->pInvModQ.data(), 1, 0, md->ptr);
+    }
+    Ciphertext<DCRTPoly> res = SfheInternal::traced(this, out, "EvalRotateSum");
+    for (size_t k : ident) res = EvalAdd(res, a[k]);
+    return res;
 }
 
 // ============================================================================

@@ -350,6 +350,10 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
     // level as summing the individually rescaled EvalMult(a_i, p_i)).
     Ciphertext<DCRTPoly> EvalMultAddPlain(const std::vector<Ciphertext<DCRTPoly>>& a,
                                           const std::vector<Plaintext>& p);
+    // Engine extension: EvalMultAddPlain(a, p[g]) for every g, each input
+    // read once for all the sums (vecRotsOpt's and the blind rotations' giant steps).
+    std::vector<Ciphertext<DCRTPoly>> EvalMultAddPlainMany(const std::vector<Ciphertext<DCRTPoly>>& a,
+                                                           const std::vector<std::vector<Plaintext>>& p);
 
     // rotations
     Ciphertext<DCRTPoly> EvalRotate(const Ciphertext<DCRTPoly>& a, int32_t r);
@@ -359,6 +363,12 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
     std::shared_ptr<FastRotationPrecomp> EvalFastRotationPrecompute(const Ciphertext<DCRTPoly>& a);
     Ciphertext<DCRTPoly> EvalFastRotation(const Ciphertext<DCRTPoly>& a, int32_t r, uint32_t m,
                                           const std::shared_ptr<FastRotationPrecomp>& pre);
+    // Engine extension: sum_k EvalRotate(a_k, r_k) with the key switches'
+    // inner products summed in the extended basis Q*P and ONE ModDown (output
+    // aggregation).  The same value as EvalAddMany of the rotations, with one
+    // ModDown rounding instead of one per term.  Every r_k needs its own key.
+    Ciphertext<DCRTPoly> EvalRotateSum(const std::vector<Ciphertext<DCRTPoly>>& a,
+                                       const std::vector<int32_t>& r);
 
     // polynomial evaluation (chebyshev.cpp)
     Ciphertext<DCRTPoly> EvalChebyshevSeriesPS(const Ciphertext<DCRTPoly>& x,

@@ -1203,6 +1203,54 @@ __global__ __launch_bounds__(kThreads) void k_mac_plain2(u64* __restrict__ out0,
     }
 }
 
+// sfp_mac_plain_multi: every thread keeps its two coefficients of all nin
+// inputs (both polys) in registers and forms the nout sums from them, so each
+// input row is read once instead of once per sum.
+struct MacMultiArgs {
+    const u64* a[SFP_MAX_MACM_IN];
+    const u64* c[SFP_MAX_MACM_IN];
+    const u64* b[SFP_MAX_MACM_PT];
+    u64* o0[SFP_MAX_MACM_OUT];
+    u64* o1[SFP_MAX_MACM_OUT];
+};
+template <int NI>
+__global__ __launch_bounds__(kThreads) void k_mac_plain_multi(const MacMultiArgs A, uint32_t nin, uint32_t nout,
+                                                              sfp_limbs m, const sf_barrett* __restrict__ bar,
+                                                              uint32_t logn) {
+    const size_t pairs = ((size_t)m.count << logn) >> 1;
+    for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < pairs;
+         i += (size_t)gridDim.x * kThreads) {
+        const size_t e = 2 * i;
+        const sf_barrett B = loadBar(bar, primeOf(m, (uint32_t)(e >> logn)));
+        ulonglong2 xa[NI], xc[NI];
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+            if ((uint32_t)j < nin) {
+                xa[j] = *reinterpret_cast<const ulonglong2*>(A.a[j] + e);
+                xc[j] = *reinterpret_cast<const ulonglong2*>(A.c[j] + e);
+            }
+        for (uint32_t g = 0; g < nout; ++g) {
+            Acc x0{0, 0}, y0{0, 0}, x1{0, 0}, y1{0, 0};
+#pragma unroll
+            for (int j = 0; j < NI; ++j)
+                if ((uint32_t)j < nin) {
+                    const ulonglong2 p = *reinterpret_cast<const ulonglong2*>(A.b[g * nin + j] + e);
+                    macc(x0, xa[j].x, p.x);
+                    macc(y0, xa[j].y, p.y);
+                    macc(x1, xc[j].x, p.x);
+                    macc(y1, xc[j].y, p.y);
+                }
+            ulonglong2 o0, o1;
+            o0.x = sf_reduce128_acc(x0.lo, x0.hi, &B);
+            o0.y = sf_reduce128_acc(y0.lo, y0.hi, &B);
+            o1.x = sf_reduce128_acc(x1.lo, x1.hi, &B);
+            o1.y = sf_reduce128_acc(y1.lo, y1.hi, &B);
+            *reinterpret_cast<ulonglong2*>(A.o0[g] + e) = o0;
+            *reinterpret_cast<ulonglong2*>(A.o1[g] + e) = o1;
+        }
+    }
+}
+
 __global__ __launch_bounds__(kThreads) void k_mac_plain(u64* __restrict__ out, PtrList2 ab,
                                                         uint32_t nin, sfp_limbs m,
                                                         const sf_barrett* __restrict__ bar,
@@ -1862,7 +1910,8 @@ __global__ __launch_bounds__(kThreads) void k_ks_inner(u64* __restrict__ acc0, u
                                                        sfp_limbs pm, uint32_t keyQ, uint32_t keyRows,
                                                        const u64* __restrict__ fold0,
                                                        const u64* __restrict__ fold1, u64 foldK,
-                                                       const sf_barrett* __restrict__ bar, uint32_t logn) {
+                                                       const sf_barrett* __restrict__ bar, uint32_t logn,
+                                                       int accum) {
     // two coefficients per thread: 16-byte loads of every ext / key row
     const uint32_t ell = pm.split, NP = keyRows;
     const size_t pairs = ((size_t)pm.count << logn) >> 1;
@@ -1898,6 +1947,14 @@ __global__ __launch_bounds__(kThreads) void k_ks_inner(u64* __restrict__ acc0, u
         o0.y = sf_reduce128_acc(s0b.lo, s0b.hi, &B);
         o1.x = sf_reduce128_acc(s1.lo, s1.hi, &B);
         o1.y = sf_reduce128_acc(s1b.lo, s1b.hi, &B);
+        if (accum) {  // sfp_ks_inner_acc: acc += the inner product
+            const ulonglong2 p0 = *reinterpret_cast<const ulonglong2*>(acc0 + e);
+            const ulonglong2 p1 = *reinterpret_cast<const ulonglong2*>(acc1 + e);
+            o0.x = sf_add(o0.x, p0.x, B.q);
+            o0.y = sf_add(o0.y, p0.y, B.q);
+            o1.x = sf_add(o1.x, p1.x, B.q);
+            o1.y = sf_add(o1.y, p1.y, B.q);
+        }
         *reinterpret_cast<ulonglong2*>(acc0 + e) = o0;
         *reinterpret_cast<ulonglong2*>(acc1 + e) = o1;
     }
@@ -2780,6 +2837,35 @@ void sfp_mac_plain2(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint64_t* 
     checkLaunch(d, "mac_plain2");
 }
 
+void sfp_mac_plain_multi(sfp_dev* d, uint64_t* const* out0, uint64_t* const* out1, const uint64_t* const* a0,
+                         const uint64_t* const* a1, const uint64_t* const* b, uint32_t nin, uint32_t nout,
+                         sfp_limbs m) {
+    if (!m.count || !nin || !nout) return;
+    if (!limbsOk(d, m, "mac_plain_multi")) return;
+    if (nin > SFP_MAX_MACM_IN || nout > SFP_MAX_MACM_OUT || nin * nout > SFP_MAX_MACM_PT) {
+        record(d, "mac_plain_multi", hipErrorInvalidValue);
+        return;
+    }
+    MacMultiArgs A{};
+    for (uint32_t j = 0; j < nin; ++j) {
+        A.a[j] = a0[j];
+        A.c[j] = a1[j];
+    }
+    for (uint32_t g = 0; g < nout; ++g) {
+        A.o0[g] = out0[g];
+        A.o1[g] = out1[g];
+        for (uint32_t j = 0; j < nin; ++j) A.b[g * nin + j] = b[(size_t)g * nin + j];
+    }
+    const size_t total = (size_t)m.count * d->n;
+    if (nin <= 8)
+        hipLaunchKernelGGL(k_mac_plain_multi<8>, dim3(ewGrid(total / 2)), dim3(kThreads), 0, d->st(), A, nin, nout, m,
+                           d->bar, d->logn);
+    else
+        hipLaunchKernelGGL(k_mac_plain_multi<SFP_MAX_MACM_IN>, dim3(ewGrid(total / 2)), dim3(kThreads), 0, d->st(), A,
+                           nin, nout, m, d->bar, d->logn);
+    checkLaunch(d, "mac_plain_multi");
+}
+
 void sfp_mac_plain(sfp_dev* d, uint64_t* out, const uint64_t* const* a, const uint64_t* const* b,
                    uint32_t nin, sfp_limbs m) {
     if (!limbsOk(d, m, "mac_plain")) return;
@@ -3175,9 +3261,21 @@ void sfp_ks_inner_fold(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_
     timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + 2.0), [&] {
         hipLaunchKernelGGL(k_ks_inner, dim3(ewGrid(total / 2)), dim3(kThreads), 0, d->st(), acc0, acc1, ext,
                            extStride, key, beta, sfp_limbs{ell + K, ell, Lq, 0, 1}, Lq, Lq + K, fold0, fold1,
-                           foldK, d->bar, d->logn);
+                           foldK, d->bar, d->logn, 0);
     });
     checkLaunch(d, "ks_inner");
+}
+
+void sfp_ks_inner_acc(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext, size_t extStride,
+                      const uint64_t* key, uint32_t beta, uint32_t ell, uint32_t K, uint32_t Lq) {
+    const size_t total = (size_t)(ell + K) * d->n;
+    // reads beta ext rows + 2*beta key rows + 2 accumulator rows, writes 2, per limb
+    timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + 4.0), [&] {
+        hipLaunchKernelGGL(k_ks_inner, dim3(ewGrid(total / 2)), dim3(kThreads), 0, d->st(), acc0, acc1, ext,
+                           extStride, key, beta, sfp_limbs{ell + K, ell, Lq, 0, 1}, Lq, Lq + K, (const u64*)nullptr,
+                           (const u64*)nullptr, (u64)0, d->bar, d->logn, 1);
+    });
+    checkLaunch(d, "ks_inner_acc");
 }
 
 void sfp_moddown2(sfp_dev* d, uint64_t* out0, uint64_t* out1, uint64_t* acc, size_t accStride,
@@ -3395,13 +3493,14 @@ void sfp_rescale_rows(sfp_dev* d, uint64_t* out, const uint64_t* in, const uint6
 }
 
 void sfp_ks_inner_map(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext, size_t extStride,
-                      const uint64_t* key, uint32_t beta, sfp_limbs pm, uint32_t keyQ, uint32_t keyRows) {
+                      const uint64_t* key, uint32_t beta, sfp_limbs pm, uint32_t keyQ, uint32_t keyRows,
+                      int accum) {
     if (!pm.count || !limbsOk(d, pm, "ks_inner_map")) return;
     const size_t total = (size_t)pm.count * d->n;
-    timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + 2.0), [&] {
+    timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + (accum ? 4.0 : 2.0)), [&] {
         hipLaunchKernelGGL(k_ks_inner, dim3(ewGrid(total / 2)), dim3(kThreads), 0, d->st(), acc0, acc1, ext, extStride,
                            key, beta, pm, keyQ, keyRows, (const u64*)nullptr, (const u64*)nullptr, (u64)0, d->bar,
-                           d->logn);
+                           d->logn, accum);
     });
     checkLaunch(d, "ks_inner_map");
 }

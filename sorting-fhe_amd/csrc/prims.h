@@ -119,6 +119,16 @@ void sfp_mac_plain(sfp_dev* d, uint64_t* out, const uint64_t* const* a, const ui
 // out0 = sum_j a0[j] * b[j], out1 = sum_j a1[j] * b[j]  (nin <= SFP_MAX_WSUM).
 void sfp_mac_plain2(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint64_t* const* a0,
                     const uint64_t* const* a1, const uint64_t* const* b, uint32_t nin, sfp_limbs m);
+// Several such sums over the same inputs (vecRotsOpt's giant steps: each
+// input read once for all of them):
+//   out0[g] = sum_j a0[j] * b[g*nin + j],  out1[g] = sum_j a1[j] * b[g*nin + j]  (g < nout)
+// nin <= SFP_MAX_MACM_IN, nout <= SFP_MAX_MACM_OUT, nout * nin <= SFP_MAX_MACM_PT.
+#define SFP_MAX_MACM_IN 16
+#define SFP_MAX_MACM_OUT 32
+#define SFP_MAX_MACM_PT 128
+void sfp_mac_plain_multi(sfp_dev* d, uint64_t* const* out0, uint64_t* const* out1, const uint64_t* const* a0,
+                         const uint64_t* const* a1, const uint64_t* const* b, uint32_t nin, uint32_t nout,
+                         sfp_limbs m);
 
 // ---- automorphism ----------------------------------------------------------
 // out = sigma_g(in) in the evaluation domain (g odd, < 2n); out != in.
@@ -185,6 +195,11 @@ void sfp_modup(sfp_dev* d, uint64_t* ext, const uint64_t* in, uint32_t ell, uint
 void sfp_ks_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
                   size_t ext_stride, const uint64_t* key, uint32_t beta, uint32_t ell, uint32_t K,
                   uint32_t Lq);
+// sfp_ks_inner accumulating: acc0 += sum_j ext_j * kb_j, acc1 += sum_j ext_j * ka_j
+// (the key switches of a rotation sum share one ModDown, EvalRotateSum).
+void sfp_ks_inner_acc(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
+                      size_t ext_stride, const uint64_t* key, uint32_t beta, uint32_t ell, uint32_t K,
+                      uint32_t Lq);
 
 // ModDown of both key-switch accumulators:
 //   out_p,i (+)= (acc_p,i - NTT(Conv_{P->Q}(INTT(acc_p,P)))_i) * pinv_i,
@@ -278,9 +293,10 @@ void sfp_rescale_rows(sfp_dev* d, uint64_t* out, const uint64_t* in, const uint6
 // prime map pm (pm.split Q rows then P rows); ext row t uses key row
 // t < pm.split ? t : keyQ + (t - pm.split) of each digit's [b rows][a rows]
 // block of key_rows rows.
+//   accum: acc (+)= the inner product (as sfp_ks_inner_acc)
 void sfp_ks_inner_map(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
                       size_t ext_stride, const uint64_t* key, uint32_t beta, sfp_limbs pm,
-                      uint32_t keyQ, uint32_t key_rows);
+                      uint32_t keyQ, uint32_t key_rows, int accum);
 
 // ---- graph capture (hipGraph) ---------------------------------------------------
 // Between sfp_capture_begin and sfp_capture_end every prim enqueued on lane 0

@@ -30,7 +30,7 @@ ABI_SYMBOLS = [
     "sfhe_sync", "sfhe_op_stats", "sfhe_encrypt", "sfhe_decrypt", "sfhe_ct_free",
     "sfhe_ct_clone", "sfhe_ct_info", "sfhe_ct_set_slots", "sfhe_ct_download", "sfhe_eval_add",
     "sfhe_eval_sub", "sfhe_eval_add_const", "sfhe_eval_mult_const", "sfhe_eval_mult_plain",
-    "sfhe_eval_mult", "sfhe_eval_rotate", "sfhe_eval_chebyshev", "sfhe_sign", "sfhe_compare",
+    "sfhe_eval_mult", "sfhe_eval_rotate", "sfhe_eval_rotate_sum", "sfhe_eval_chebyshev", "sfhe_sign", "sfhe_compare",
     "sfhe_direct_sort_params", "sfhe_doubled_sinc_coeffs", "sfhe_sorter_create",
     "sfhe_sorter_destroy", "sfhe_sorter_sort", "sfhe_sorter_rank", "sfhe_sorter_place",
     "sfhe_decompose", "sfhe_kernel_timing", "sfhe_kernel_timing_read",
@@ -107,6 +107,7 @@ _SIGS = {
     "sfhe_eval_mult_plain": (C.c_int, [_VP, _VP, _PD, _SZ, _U32, _PVP]),
     "sfhe_eval_mult": (C.c_int, [_VP, _VP, _VP, _PVP]),
     "sfhe_eval_rotate": (C.c_int, [_VP, _VP, C.c_int32, _PVP]),
+    "sfhe_eval_rotate_sum": (C.c_int, [_VP, C.POINTER(_VP), C.POINTER(C.c_int32), C.c_size_t, _PVP]),
     "sfhe_bootstrap_setup": (C.c_int, [_VP, _U32, _U32, _U32]),
     "sfhe_bootstrap_depth": (C.c_int, [_VP, _U32, _U32, _U32, _PU32]),
     "sfhe_bootstrap": (C.c_int, [_VP, _VP, _U32, _U32, _PVP]),
@@ -364,6 +365,12 @@ class Engine:
 
     def rotate(self, a, r: int):
         return self._new(self.lib.sfhe_eval_rotate, self.ctx, a.h, int(r))
+
+    def rotate_sum(self, cts, rots):
+        """sum_k rotate(cts[k], rots[k]) with one shared ModDown (EvalRotateSum)."""
+        hs = (_VP * len(cts))(*[c.h for c in cts])
+        rs = (C.c_int32 * len(rots))(*[int(r) for r in rots])
+        return self._new(self.lib.sfhe_eval_rotate_sum, self.ctx, hs, rs, len(cts))
 
     def bootstrap_setup(self, level_budget=(5, 5), slots: int = 0):
         """EvalBootstrapSetup + EvalBootstrapKeyGen for `slots`-slot ciphertexts."""

@@ -62,6 +62,31 @@ def test_rotation(oracle_lib, r):
     np.testing.assert_allclose(got, np.roll(x, -r), atol=1e-6)
 
 
+@pytest.mark.parametrize("lazy_product", [False, True])
+def test_rotate_sum(oracle_lib, lazy_product):
+    """EvalRotateSum (output aggregation: one ModDown for all terms) equals the
+    sum of the individual rotations, on canonical inputs and on lazily
+    rescaled products (the vecRotsOpt / blind-rotation giant steps)."""
+    rots = [1, 2, 3, 5, 8, 0, 15]
+    e = sfhe.Engine("oracle", mult_depth=3, ring_dim=1 << 12, batch_size=16,
+                    scaling_mod_size=50, rotations=[r for r in rots if r % 16])
+    rng = np.random.default_rng(11)
+    xs = [rng.uniform(-1, 1, 16) for _ in rots]
+    cts = [e.encrypt(x.tolist()) for x in xs]
+    if lazy_product:
+        cts = [e.mult_const(c, 0.5) for c in cts]
+        xs = [0.5 * x for x in xs]
+    got = e.rotate_sum(cts, rots)
+    ref = sum(np.roll(x, -r) for x, r in zip(xs, rots))
+    np.testing.assert_allclose(e.decrypt(got), ref, atol=1e-6)
+    sep = cts[0]
+    for c, r in zip(cts, rots):
+        t = e.rotate(c, r)
+        sep = t if c is cts[0] else e.add(sep, t)
+    assert got.level == sep.level
+    np.testing.assert_allclose(e.decrypt(got), e.decrypt(sep), atol=1e-6)
+
+
 def test_compare_reference_vectors(oracle_lib):
     """tests/CompareTest.cpp:13-63, verbatim parameters."""
     t = REF["compare_test"]
