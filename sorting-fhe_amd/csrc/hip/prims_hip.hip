@@ -326,6 +326,15 @@ __device__ __forceinline__ uint32_t ldsSw(uint32_t e) {
     const uint32_t x = e >> 5;
     return e ^ ((x ^ (x << 2)) & 31u);
 }
+// ldsSw is linear over GF(2): for index bits that do not overlap,
+// ldsSw(a | b) = ldsSw(a) ^ ldsSw(b).  A round's 2^B words of one thread sit at
+// e0 | j*h*C (COL) or e0 | j*h (ROW), where e0 has zeros in j's bits, so
+// their LDS slots are ldsSw(e0) ^ ldsSw(offset_j): one XOR per word, with
+// offset_j a compile-time constant in the unrolled rounds.
+template <bool COL>
+__device__ __forceinline__ uint32_t ldsOff(uint32_t jh, uint32_t C) {
+    return ldsSw(COL ? jh * C : jh);
+}
 
 struct NttTile {
     uint32_t logn, d;     // d = stages in this pass (logR or 8)
@@ -399,8 +408,9 @@ __device__ __forceinline__ void nttRound(u64* s, const NttTile& T, uint32_t S0, 
             }
         }
         u64 v[M];
+        const uint32_t a0 = ldsSw(nttLocal<COL>(T, st, ub));
 #pragma unroll
-        for (int j = 0; j < M; ++j) v[j] = s[ldsSw(nttLocal<COL>(T, st, ub + j * h))];
+        for (int j = 0; j < M; ++j) v[j] = s[a0 ^ ldsOff<COL>(j * h, T.C)];
         if (!INV) {
             // Harvey CT butterfly: in [0,4q) -> out [0,4q)
 #pragma unroll
@@ -434,7 +444,7 @@ __device__ __forceinline__ void nttRound(u64* s, const NttTile& T, uint32_t S0, 
             }
         }
 #pragma unroll
-        for (int j = 0; j < M; ++j) s[ldsSw(nttLocal<COL>(T, st, ub + j * h))] = v[j];
+        for (int j = 0; j < M; ++j) s[a0 ^ ldsOff<COL>(j * h, T.C)] = v[j];
     }
 }
 
@@ -468,6 +478,16 @@ __device__ __forceinline__ double fpMulMod(double y, double w, double wq, double
     return fma(-qq, q, hi) + lo;
 }
 
+// Exact u64 <-> double for integers below 2^52 (residues of primes < 2^42):
+// the value rides in the mantissa of 2^52 + x, two VALU operations each
+// instead of the generic 64-bit conversions' four to six.
+__device__ __forceinline__ double u2d(u64 x) {
+    return __longlong_as_double((long long)(x | 0x4330000000000000ull)) - 4503599627370496.0;
+}
+__device__ __forceinline__ u64 d2u(double v) {
+    return (u64)__double_as_longlong(v + 4503599627370496.0) & 0x000FFFFFFFFFFFFFull;
+}
+
 // |v| < 2^52 -> [0, q)
 __device__ __forceinline__ double fpReduce(double v, double q, double qinv) {
     double r = fma(-rint(v * qinv), q, v);
@@ -491,13 +511,17 @@ __device__ __forceinline__ void nttRoundFP(double* s, const NttTile& T, uint32_t
     const uint32_t logh = d - k0 - B;
     const uint32_t h = 1u << logh;
     const uint32_t span = D >> k0;
+    // COL columns per tile: TILE >> 8 when the pass's stage count is the
+    // compile-time 8 (then the index math and every slot offset fold)
+    const uint32_t Cc = (COL && DC == 8) ? (uint32_t)(TILE >> 8) : T.C;
+    const uint32_t logCc = (COL && DC == 8) ? (uint32_t)__builtin_ctz(TILE >> 8) : T.logC;
 #pragma unroll
     for (int gi = 0; gi < GPT; ++gi) {
         const uint32_t gid = threadIdx.x + gi * (TILE >> LE);
         uint32_t st, lo, hi;
         if (COL) {
-            st = gid & (T.C - 1);
-            const uint32_t rest = gid >> T.logC;
+            st = gid & (Cc - 1);
+            const uint32_t rest = gid >> logCc;
             lo = rest & (h - 1);
             hi = rest >> logh;
         } else {
@@ -528,8 +552,9 @@ __device__ __forceinline__ void nttRoundFP(double* s, const NttTile& T, uint32_t
             }
         }
         double v[M];
+        const uint32_t a0 = ldsSw(COL ? ub * Cc + st : st * 256u + ub);
 #pragma unroll
-        for (int j = 0; j < M; ++j) v[j] = s[ldsSw(nttLocal<COL>(T, st, ub + j * h))];
+        for (int j = 0; j < M; ++j) v[j] = s[a0 ^ ldsOff<COL>(j * h, Cc)];
         if (!INV) {
 #pragma unroll
             for (int t = 0; t < B; ++t) {
@@ -559,7 +584,7 @@ __device__ __forceinline__ void nttRoundFP(double* s, const NttTile& T, uint32_t
             }
         }
 #pragma unroll
-        for (int j = 0; j < M; ++j) s[ldsSw(nttLocal<COL>(T, st, ub + j * h))] = v[j];
+        for (int j = 0; j < M; ++j) s[a0 ^ ldsOff<COL>(j * h, Cc)] = v[j];
     }
 }
 
@@ -745,8 +770,8 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_b
             }
         }
         if (fp) {
-            s[ldsSw(e)] = __double_as_longlong((double)x.x);
-            s[ldsSw(e + 1)] = __double_as_longlong((double)x.y);
+            s[ldsSw(e)] = __double_as_longlong(u2d(x.x));
+            s[ldsSw(e + 1)] = __double_as_longlong(u2d(x.y));
         } else {
             s[ldsSw(e)] = x.x;
             s[ldsSw(e + 1)] = x.y;
@@ -821,8 +846,8 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_b
                 a0 = fpMulMod(a0, ninvD[prime], ninvQ[prime], qd);
                 a1 = fpMulMod(a1, ninvD[prime], ninvQ[prime], qd);
             }
-            x.x = (u64)fpReduce(a0, qd, qi);
-            x.y = (u64)fpReduce(a1, qd, qi);
+            x.x = d2u(fpReduce(a0, qd, qi));
+            x.y = d2u(fpReduce(a1, qd, qi));
         } else if (!FIRST) {  // finish the lazy ranges: forward [0,4q), inverse [0,2q) -> [0,q)
             if (scale) {
                 x.x = sf_mul_shoup_lazy(x.x, ni, niS, q);
@@ -1136,8 +1161,8 @@ __global__ __launch_bounds__(kThreads) void k_lin_wsum_multi(u64* __restrict__ o
         for (int o = 0; o < kWsumChunk; ++o) {
             if ((uint32_t)o < oc) {
                 u64* dst = out + (size_t)(o0 + o) * outStride + off;
-                dst[0] = (u64)fpReduce(f0[o], qd, qi);
-                dst[polyStride] = (u64)fpReduce(f1[o], qd, qi);
+                dst[0] = d2u(fpReduce(f0[o], qd, qi));
+                dst[polyStride] = d2u(fpReduce(f1[o], qd, qi));
             }
         }
         return;
