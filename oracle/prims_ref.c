@@ -487,26 +487,32 @@ void sfp_ks_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ex
 static void ks_inner_rows(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
                           size_t ext_stride, const uint64_t* key, uint32_t beta, uint32_t ell,
                           uint32_t K, uint32_t Lq, const uint64_t* fold0, const uint64_t* fold1,
-                          uint64_t fold_k, int accum);
+                          uint64_t fold_k, int accum, const uint64_t* pm);
+
+void sfp_ks_inner_mul(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
+                      size_t ext_stride, const uint64_t* key, uint32_t beta, uint32_t ell, uint32_t K,
+                      uint32_t Lq, const uint64_t* pm, int accum) {
+    ks_inner_rows(d, acc0, acc1, ext, ext_stride, key, beta, ell, K, Lq, NULL, NULL, 0, accum, pm);
+}
 
 void sfp_ks_inner_fold(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
                        size_t ext_stride, const uint64_t* key, uint32_t beta, uint32_t ell,
                        uint32_t K, uint32_t Lq, const uint64_t* fold0, const uint64_t* fold1,
                        uint64_t fold_k) {
-    ks_inner_rows(d, acc0, acc1, ext, ext_stride, key, beta, ell, K, Lq, fold0, fold1, fold_k, 0);
+    ks_inner_rows(d, acc0, acc1, ext, ext_stride, key, beta, ell, K, Lq, fold0, fold1, fold_k, 0, NULL);
 }
 
 void sfp_ks_inner_acc(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
                       size_t ext_stride, const uint64_t* key, uint32_t beta, uint32_t ell, uint32_t K,
                       uint32_t Lq) {
-    ks_inner_rows(d, acc0, acc1, ext, ext_stride, key, beta, ell, K, Lq, NULL, NULL, 0, 1);
+    ks_inner_rows(d, acc0, acc1, ext, ext_stride, key, beta, ell, K, Lq, NULL, NULL, 0, 1, NULL);
 }
 
 // acc (+)= sum_j ext_j * key_j (mod q) per ext limb (sfp_ks_inner / _fold / _acc)
 static void ks_inner_rows(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
                           size_t ext_stride, const uint64_t* key, uint32_t beta, uint32_t ell,
                           uint32_t K, uint32_t Lq, const uint64_t* fold0, const uint64_t* fold1,
-                          uint64_t fold_k, int accum) {
+                          uint64_t fold_k, int accum, const uint64_t* pm) {
     const uint32_t n = d->n, rows = ell + K, NP = Lq + K;
 #pragma omp parallel for schedule(static)
     for (uint32_t t = 0; t < rows; ++t) {
@@ -525,9 +531,14 @@ static void ks_inner_rows(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint
                 s0 += (u128)fold0[(size_t)t * n + x] * fold_k;
                 s1 += (u128)fold1[(size_t)t * n + x] * fold_k;
             }
+            if (pm) {  /* (sum mod q) * pm mod q */
+                const u64 m = pm[(size_t)t * n + x];
+                s0 = (u128)(u64)(s0 % q) * m;
+                s1 = (u128)(u64)(s1 % q) * m;
+            }
             if (accum) {
-                s0 += acc0[(size_t)t * n + x];
-                s1 += acc1[(size_t)t * n + x];
+                s0 = (u128)(u64)(s0 % q) + acc0[(size_t)t * n + x];
+                s1 = (u128)(u64)(s1 % q) + acc1[(size_t)t * n + x];
             }
             acc0[(size_t)t * n + x] = (u64)(s0 % q);
             acc1[(size_t)t * n + x] = (u64)(s1 % q);

@@ -268,6 +268,23 @@ Ciphertext<DCRTPoly> applyGroup(CryptoContextImpl<DCRTPoly>* cc, Group& gr, uint
         }
         gr.level = level;
     }
+    // double hoisting: one ModUp per input, one ModDown per group
+    // (EvalRotMultAddHoisted); SFHE_BOOT_HOIST=0 keeps a ModDown per rotation
+    static const bool hoistDown = [] {
+        const char* v = std::getenv("SFHE_BOOT_HOIST");
+        return !v || *v != '0';
+    }();
+    if (hoistDown) {
+        std::vector<std::vector<std::pair<int32_t, Plaintext>>> terms(in.size());
+        for (size_t t = 0; t < in.size(); ++t)
+            for (const auto& [k, v] : gr.diags) {
+                (void)v;
+                terms[t].emplace_back(k ? signedOffset(k, S) : 0, t == 0 ? gr.pts.at(k) : gr.ptsIm.at(k));
+            }
+        auto out = cc->EvalRotMultAddHoisted(in, terms);
+        out->SetSlots(S);
+        return out;
+    }
     std::vector<Ciphertext<DCRTPoly>> cts;
     std::vector<Plaintext> pts;
     for (size_t t = 0; t < in.size(); ++t) {

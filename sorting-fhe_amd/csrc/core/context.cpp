@@ -1029,6 +1029,31 @@ class SfheInternal {
         return buf->ptr;
     }
 
+    // pt at `level` over the extended basis: its ell q rows then the K P rows
+    // (evaluation domain), cached on the plaintext beside its q-row encodings
+    static const uint64_t* encodedExt(CC* cc, const Plaintext& pt, uint32_t level) {
+        SfheContextState* s = cc->st.get();
+        if (s->world > 1) SFHE_THROW("internal: extended-basis encodings are unsharded");
+        std::lock_guard<std::mutex> g(pt->encMutex);
+        const uint32_t key = level | 0x40000000u;
+        auto stale = [&](const DeviceBufferPtr& b) { return b->capEpoch && s->abandonedEpochs.count(b->capEpoch); };
+        auto it = pt->encoded.find(key);
+        if (it != pt->encoded.end() && stale(it->second)) {
+            pt->encoded.erase(it);
+            it = pt->encoded.end();
+        }
+        if (it != pt->encoded.end()) return ready(s, it->second.get());
+        const uint32_t ell = s->ellOf(level);
+        const sfp_limbs m{ell + s->K, ell, s->Lq};
+        auto buf = s->alloc((size_t)m.count * s->n);
+        encodeRows(s, pt, level, buf->ptr, m);
+        sfp_ntt(s->dev, buf->ptr, m, 0);
+        buf->ready = sfp_event_record(s->dev);
+        buf->readyEpoch = s->capturing ? s->captureEpoch : 0;
+        pt->encoded[key] = buf;
+        return buf->ptr;
+    }
+
     // a canonical ciphertext over existing rows (deferred ops keep the rows
     // they were given pinned, never the caller's possibly reassigned handle)
     static Ct view(CC* cc, const DeviceBufferPtr& buf, uint64_t* c0, uint64_t* c1, uint32_t level, double scale,
@@ -2134,7 +2159,8 @@ std::vector<Ciphertext<DCRTPoly>> CryptoContextImpl<DCRTPoly>::EvalMultAddPlainM
     OpLock g(st.get());
     SfheContextState* s = st.get();
     std::vector<Ciphertext<DCRTPoly>> out;
-    if (a.empty() || p.empty()) SFHE_THROW("operand count mismatch");
+    if (p.empty()) return out;  // no sums (the caller's EvalAddMany then fails as the reference's does)
+    if (a.empty()) SFHE_THROW("operand count mismatch");
     for (const auto& pg : p)
         if (pg.size() != a.size()) SFHE_THROW("operand count mismatch");
     if (a.size() > SFP_MAX_MACM_IN || p.size() == 1) {
@@ -2305,7 +2331,8 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotateSum(const std::vecto
                                                                 const std::vector<int32_t>& r) {
     OpLock g(st.get());
     SfheContextState* s = st.get();
-    if (a.empty() || a.size() != r.size()) SFHE_THROW("EvalRotateSum: operand count mismatch");
+    if (a.empty()) return EvalAddMany(a);  // the reference's error for an empty sum
+    if (a.size() != r.size()) SFHE_THROW("EvalRotateSum: operand count mismatch");
     static const bool off = [] {
         const char* v = std::getenv("SFHE_ROTSUM");
         return v && *v == '0';
@@ -2380,6 +2407,104 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotateSum(const std::vecto
     Ciphertext<DCRTPoly> res = SfheInternal::traced(this, out, "EvalRotateSum");
     for (size_t k : ident) res = EvalAdd(res, a[k]);
     return res;
+}
+
+// Double hoisting (Bossuat et al.'s hoisted ModDown): with acc_k the
+// extended-basis inner product of rotation k, p (.) ModDown(acc_k) and
+// ModDown(p_ext (.) acc_k) are the same value up to the ModDown rounding, so
+// sum_k p_k (.) Rot_k(a) = sum_k p_k (.) sigma_k(c0) + ModDown(sum_k p_k,ext (.) acc_k)
+// takes one ModDown for the whole sum; the diagonal's rounding is also no
+// longer multiplied by p_k.  Unsharded contexts (bootstrapping's linear maps).
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotMultAddHoisted(
+    const std::vector<Ciphertext<DCRTPoly>>& a,
+    const std::vector<std::vector<std::pair<int32_t, Plaintext>>>& terms) {
+    OpLock g(st.get());
+    SfheContextState* s = st.get();
+    if (a.empty() || a.size() != terms.size()) SFHE_THROW("EvalRotMultAddHoisted: operand count mismatch");
+    if (s->world > 1) SFHE_THROW("EvalRotMultAddHoisted: sharded contexts are not supported");
+    SfheInternal::depsv(s, a);
+    const uint32_t level = a[0]->level;
+    uint32_t slots = 0;
+    for (size_t t = 0; t < a.size(); ++t) {
+        if (a[t]->level != level) SFHE_THROW("EvalRotMultAddHoisted: inputs at different levels");
+        slots = std::max(slots, a[t]->slots);
+        for (const auto& tk : terms[t]) slots = std::max(slots, tk.second->slots);
+    }
+    const uint32_t ell = s->ellOf(level), n = s->n, K = s->K;
+    if (ell < 2) SFHE_THROW("no levels left (multiplicative depth exhausted)");
+    const uint32_t beta = (ell + s->alpha - 1) / s->alpha;
+    const size_t stride = (size_t)(ell + K) * n, pw = s->polyWords(level);
+    const sfp_limbs q = s->qmap(ell);
+    auto prod = s->alloc(2 * pw);  // the product sum before its rescale
+    uint64_t* t0 = prod->ptr;
+    uint64_t* t1 = t0 + pw;
+    auto acc = s->alloc(2 * stride);
+    bool accOn = false;
+    std::vector<DeviceBufferPtr> keep;
+    std::vector<const uint64_t*> x0, m0, x1, m1;  // c0 terms; c1 terms of the unrotated diagonals
+    for (size_t t = 0; t < a.size(); ++t) {
+        DeviceBufferPtr ext;
+        for (const auto& [r, pt] : terms[t]) {
+            const uint64_t* m = SfheInternal::encoded(this, pt, level);
+            const uint32_t gal = GaloisForRotation(r);
+            if (gal == 1) {
+                x0.push_back(a[t]->c0);
+                m0.push_back(m);
+                x1.push_back(a[t]->c1);
+                m1.push_back(m);
+                continue;
+            }
+            auto it = s->rotKeys.find(gal);
+            if (it == s->rotKeys.end())
+                SFHE_THROW("EvalKey for rotation " + std::to_string(r) + " is not found");
+            if (!ext) {  // the input's ModUp, shared by its rotations
+                ext = s->alloc(stride * beta);
+                auto scratch = s->alloc((size_t)ell * n);
+                sfp_modup(s->dev, ext->ptr, a[t]->c1, ell, K, s->Lq, s->alpha,
+                          SfheInternal::modupConv(this, ell).data(), scratch->ptr);
+            }
+            auto rc0 = s->alloc(pw);
+            sfp_automorph(s->dev, rc0->ptr, a[t]->c0, gal, q);
+            x0.push_back(rc0->ptr);
+            m0.push_back(m);
+            keep.push_back(rc0);
+            auto rext = s->alloc(stride * beta);
+            const uint32_t rows = beta * (ell + K);
+            sfp_automorph(s->dev, rext->ptr, ext->ptr, gal, sfp_limbs{rows, rows, 0, 0});
+            sfp_ks_inner_mul(s->dev, acc->ptr, acc->ptr + stride, rext->ptr, stride, it->second->ptr, beta, ell, K,
+                             s->Lq, SfheInternal::encodedExt(this, pt, level), accOn ? 1 : 0);
+            accOn = true;
+            s->stats.keyswitch++;
+            s->stats.automorph++;
+            s->countBytes((3.0 * ell + (2.0 * beta + 5.0) * (ell + K)) * n * 8);
+        }
+    }
+    auto macInto = [&](uint64_t* out, const std::vector<const uint64_t*>& x, const std::vector<const uint64_t*>& m) {
+        if (x.empty()) {
+            sfp_zero(s->dev, out, pw * 8);
+            return;
+        }
+        for (size_t done = 0; done < x.size(); done += SFP_MAX_WSUM) {
+            const uint32_t take = (uint32_t)std::min<size_t>(SFP_MAX_WSUM, x.size() - done);
+            if (done == 0) {
+                sfp_mac_plain(s->dev, out, x.data(), m.data(), take, q);
+            } else {
+                auto part = s->alloc(pw);
+                sfp_mac_plain(s->dev, part->ptr, x.data() + done, m.data() + done, take, q);
+                sfp_add(s->dev, out, out, part->ptr, q);
+            }
+        }
+    };
+    macInto(t0, x0, m0);
+    macInto(t1, x1, m1);
+    s->stats.ptmult += x0.size() + x1.size();
+    s->countBytes((2.0 * x0.size() + 2.0 * x1.size() + 2.0) * ell * n * 8);
+    if (accOn) {
+        auto scratch = s->alloc((size_t)2 * ell * n);
+        sfp_moddown2(s->dev, t0, t1, acc->ptr, stride, ell, K, s->Lq, s->moddownConv, s->pInvModQ.data(), 1, 1,
+                     scratch->ptr);
+    }
+    return SfheInternal::traced(this, SfheInternal::rescale(this, t0, t1, level, slots), "EvalRotMultAddHoisted");
 }
 
 // ============================================================================

@@ -369,6 +369,13 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
     // ModDown rounding instead of one per term.  Every r_k needs its own key.
     Ciphertext<DCRTPoly> EvalRotateSum(const std::vector<Ciphertext<DCRTPoly>>& a,
                                        const std::vector<int32_t>& r);
+    // Engine extension (double hoisting): sum_t sum_k p_tk (.) EvalRotate(a_t, r_tk), then one
+    // rescale -- EvalMultAddPlain over hoisted rotations.  Each input's rotations share one
+    // ModUp; every key-switched term is multiplied by its plaintext in the extended basis Q*P
+    // and the whole sum takes ONE ModDown (one per rotation otherwise).
+    Ciphertext<DCRTPoly> EvalRotMultAddHoisted(
+        const std::vector<Ciphertext<DCRTPoly>>& a,
+        const std::vector<std::vector<std::pair<int32_t, Plaintext>>>& terms);
 
     // polynomial evaluation (chebyshev.cpp)
     Ciphertext<DCRTPoly> EvalChebyshevSeriesPS(const Ciphertext<DCRTPoly>& x,

@@ -1936,7 +1936,7 @@ __global__ __launch_bounds__(kThreads) void k_ks_inner(u64* __restrict__ acc0, u
                                                        const u64* __restrict__ fold0,
                                                        const u64* __restrict__ fold1, u64 foldK,
                                                        const sf_barrett* __restrict__ bar, uint32_t logn,
-                                                       int accum) {
+                                                       int accum, const u64* __restrict__ pmul) {
     // two coefficients per thread: 16-byte loads of every ext / key row
     const uint32_t ell = pm.split, NP = keyRows;
     const size_t pairs = ((size_t)pm.count << logn) >> 1;
@@ -1972,6 +1972,13 @@ __global__ __launch_bounds__(kThreads) void k_ks_inner(u64* __restrict__ acc0, u
         o0.y = sf_reduce128_acc(s0b.lo, s0b.hi, &B);
         o1.x = sf_reduce128_acc(s1.lo, s1.hi, &B);
         o1.y = sf_reduce128_acc(s1b.lo, s1b.hi, &B);
+        if (pmul) {  // sfp_ks_inner_mul: times a plaintext in the extended basis
+            const ulonglong2 m = *reinterpret_cast<const ulonglong2*>(pmul + e);
+            o0.x = bmul(o0.x, m.x, B);
+            o0.y = bmul(o0.y, m.y, B);
+            o1.x = bmul(o1.x, m.x, B);
+            o1.y = bmul(o1.y, m.y, B);
+        }
         if (accum) {  // sfp_ks_inner_acc: acc += the inner product
             const ulonglong2 p0 = *reinterpret_cast<const ulonglong2*>(acc0 + e);
             const ulonglong2 p1 = *reinterpret_cast<const ulonglong2*>(acc1 + e);
@@ -3286,7 +3293,7 @@ void sfp_ks_inner_fold(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_
     timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + 2.0), [&] {
         hipLaunchKernelGGL(k_ks_inner, dim3(ewGrid(total / 2)), dim3(kThreads), 0, d->st(), acc0, acc1, ext,
                            extStride, key, beta, sfp_limbs{ell + K, ell, Lq, 0, 1}, Lq, Lq + K, fold0, fold1,
-                           foldK, d->bar, d->logn, 0);
+                           foldK, d->bar, d->logn, 0, (const u64*)nullptr);
     });
     checkLaunch(d, "ks_inner");
 }
@@ -3298,9 +3305,22 @@ void sfp_ks_inner_acc(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t
     timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + 4.0), [&] {
         hipLaunchKernelGGL(k_ks_inner, dim3(ewGrid(total / 2)), dim3(kThreads), 0, d->st(), acc0, acc1, ext,
                            extStride, key, beta, sfp_limbs{ell + K, ell, Lq, 0, 1}, Lq, Lq + K, (const u64*)nullptr,
-                           (const u64*)nullptr, (u64)0, d->bar, d->logn, 1);
+                           (const u64*)nullptr, (u64)0, d->bar, d->logn, 1, (const u64*)nullptr);
     });
     checkLaunch(d, "ks_inner_acc");
+}
+
+void sfp_ks_inner_mul(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext, size_t extStride,
+                      const uint64_t* key, uint32_t beta, uint32_t ell, uint32_t K, uint32_t Lq, const uint64_t* pm,
+                      int accum) {
+    const size_t total = (size_t)(ell + K) * d->n;
+    // reads beta ext rows + 2*beta key rows + the plaintext row (+ 2 accumulator rows), writes 2, per limb
+    timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + (accum ? 5.0 : 3.0)), [&] {
+        hipLaunchKernelGGL(k_ks_inner, dim3(ewGrid(total / 2)), dim3(kThreads), 0, d->st(), acc0, acc1, ext,
+                           extStride, key, beta, sfp_limbs{ell + K, ell, Lq, 0, 1}, Lq, Lq + K, (const u64*)nullptr,
+                           (const u64*)nullptr, (u64)0, d->bar, d->logn, accum, pm);
+    });
+    checkLaunch(d, "ks_inner_mul");
 }
 
 void sfp_moddown2(sfp_dev* d, uint64_t* out0, uint64_t* out1, uint64_t* acc, size_t accStride,
@@ -3525,7 +3545,7 @@ void sfp_ks_inner_map(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t
     timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + (accum ? 4.0 : 2.0)), [&] {
         hipLaunchKernelGGL(k_ks_inner, dim3(ewGrid(total / 2)), dim3(kThreads), 0, d->st(), acc0, acc1, ext, extStride,
                            key, beta, pm, keyQ, keyRows, (const u64*)nullptr, (const u64*)nullptr, (u64)0, d->bar,
-                           d->logn, accum);
+                           d->logn, accum, (const u64*)nullptr);
     });
     checkLaunch(d, "ks_inner_map");
 }

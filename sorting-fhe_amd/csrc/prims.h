@@ -195,6 +195,14 @@ void sfp_modup(sfp_dev* d, uint64_t* ext, const uint64_t* in, uint32_t ell, uint
 void sfp_ks_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
                   size_t ext_stride, const uint64_t* key, uint32_t beta, uint32_t ell, uint32_t K,
                   uint32_t Lq);
+// Key inner product times a plaintext in the extended basis, accumulated
+// (double hoisting: a hoisted rotation's product with a diagonal before its
+// ModDown, EvalRotMultAddHoisted):
+//   acc_p (+)= pm (.) sum_j ext_j * key_p,j   per ext limb, pm: ell+K rows
+//   (the plaintext's q rows then its P rows, evaluation domain).
+void sfp_ks_inner_mul(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
+                      size_t ext_stride, const uint64_t* key, uint32_t beta, uint32_t ell, uint32_t K,
+                      uint32_t Lq, const uint64_t* pm, int accum);
 // sfp_ks_inner accumulating: acc0 += sum_j ext_j * kb_j, acc1 += sum_j ext_j * ka_j
 // (the key switches of a rotation sum share one ModDown, EvalRotateSum).
 void sfp_ks_inner_acc(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
