@@ -346,9 +346,11 @@ class DirectSort : public SortBase<N> {
             }));
             steps.push_back(j * np);
         }
-        // T_j = sum_i pre_i * mask_{np j + i} for every j at once (each pre_i read once)
-        auto giants = m_cc->EvalMultAddPlainMany(pre, masks);
-        for (auto& T : giants) T->SetSlots(num_slots);
+        std::vector<Ciphertext<DCRTPoly>> giants;
+        for (const auto& m : masks) {  // T_j = sum_i pre_i * mask_{np j + i}
+            giants.push_back(m_cc->EvalMultAddPlain(pre, m));
+            giants.back()->SetSlots(num_slots);
+        }
         return rot.rotate(rot.rotateSum(giants, steps), is * num_partition);
     }
 
@@ -420,7 +422,8 @@ class DirectSort : public SortBase<N> {
             }));
             steps.push_back(i * np);
         }
-        const auto giants = m_cc->EvalMultAddPlainMany(masked_inputs, masks);
+        std::vector<Ciphertext<DCRTPoly>> giants;
+        for (const auto& m : masks) giants.push_back(m_cc->EvalMultAddPlain(masked_inputs, m));
         auto result = this->getZero()->Clone();
         m_cc->EvalAddInPlace(result, rot.rotate(rot.rotateSum(giants, steps), ib * num_partition));
         return result;

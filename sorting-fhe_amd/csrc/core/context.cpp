@@ -2154,71 +2154,6 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMultAddPlain(
     return SfheInternal::traced(this, SfheInternal::rescale(this, t0, t1, level, slots), "EvalMultAddPlain");
 }
 
-std::vector<Ciphertext<DCRTPoly>> CryptoContextImpl<DCRTPoly>::EvalMultAddPlainMany(
-    const std::vector<Ciphertext<DCRTPoly>>& a, const std::vector<std::vector<Plaintext>>& p) {
-    OpLock g(st.get());
-    SfheContextState* s = st.get();
-    std::vector<Ciphertext<DCRTPoly>> out;
-    if (p.empty()) return out;  // no sums (the caller's EvalAddMany then fails as the reference's does)
-    if (a.empty()) SFHE_THROW("operand count mismatch");
-    for (const auto& pg : p)
-        if (pg.size() != a.size()) SFHE_THROW("operand count mismatch");
-    if (a.size() > SFP_MAX_MACM_IN || p.size() == 1) {
-        for (const auto& pg : p) out.push_back(EvalMultAddPlain(a, pg));
-        return out;
-    }
-    SfheInternal::depsv(s, a);
-    uint32_t level = 0, slots = 0;
-    for (const auto& c : a) {
-        level = std::max(level, c->level);
-        slots = std::max(slots, c->slots);
-    }
-    for (const auto& pg : p)
-        for (const auto& pt : pg) slots = std::max(slots, pt->slots);
-    const uint32_t ell = s->ellOf(level), nin = (uint32_t)a.size(), G = (uint32_t)p.size();
-    if (ell < 2) SFHE_THROW("no levels left (multiplicative depth exhausted)");
-    std::vector<Ciphertext<DCRTPoly>> al(nin);
-    std::vector<const uint64_t*> x0(nin), x1(nin), m;
-    for (uint32_t j = 0; j < nin; ++j) {
-        al[j] = SfheInternal::adjust(this, a[j], level);
-        SfheInternal::deps(s, {&al[j]});
-        x0[j] = al[j]->c0;
-        x1[j] = al[j]->c1;
-    }
-    for (const auto& pg : p)
-        for (const auto& pt : pg) m.push_back(SfheInternal::encoded(this, pt, level));
-    const size_t pw = s->polyWords(level);
-    std::vector<DeviceBufferPtr> bufs(G);
-    std::vector<uint64_t*> o0(G), o1(G);
-    for (uint32_t k = 0; k < G; ++k) {
-        bufs[k] = s->alloc(2 * pw);
-        o0[k] = bufs[k]->ptr;
-        o1[k] = bufs[k]->ptr + pw;
-    }
-    const uint32_t per = std::min<uint32_t>(SFP_MAX_MACM_OUT, SFP_MAX_MACM_PT / nin);
-    for (uint32_t k = 0; k < G; k += per)
-        sfp_mac_plain_multi(s->dev, o0.data() + k, o1.data() + k, x0.data(), x1.data(), m.data() + (size_t)k * nin,
-                            nin, std::min(per, G - k), st->qmap(ell));
-    s->stats.ptmult += (uint64_t)nin * G;
-    s->countBytes((2.0 * nin + (double)G * nin + 2.0 * G) * ell * s->n * 8);
-    // lazy rescaling: the sums stay pending, as EvalMultAddPlain's deferred form would give them to their consumer
-    const bool pend = SfheInternal::lazy(s);
-    for (uint32_t k = 0; k < G; ++k) {
-        if (pend) {
-            auto ct = std::make_shared<CiphertextImpl<DCRTPoly>>();
-            ct->cc = shared_from_this();
-            ct->level = level + 1;
-            ct->slots = slots;
-            SfheInternal::adoptPending(*ct, bufs[k], o0[k], o1[k]);
-            out.push_back(ct);
-        } else {
-            out.push_back(SfheInternal::traced(this, SfheInternal::rescale(this, o0[k], o1[k], level, slots),
-                                               "EvalMultAddPlainMany"));
-        }
-    }
-    return out;
-}
-
 // ============================================================================
 // rotations
 

@@ -350,10 +350,6 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
     // level as summing the individually rescaled EvalMult(a_i, p_i)).
     Ciphertext<DCRTPoly> EvalMultAddPlain(const std::vector<Ciphertext<DCRTPoly>>& a,
                                           const std::vector<Plaintext>& p);
-    // Engine extension: EvalMultAddPlain(a, p[g]) for every g, each input
-    // read once for all the sums (vecRotsOpt's and the blind rotations' giant steps).
-    std::vector<Ciphertext<DCRTPoly>> EvalMultAddPlainMany(const std::vector<Ciphertext<DCRTPoly>>& a,
-                                                           const std::vector<std::vector<Plaintext>>& p);
 
     // rotations
     Ciphertext<DCRTPoly> EvalRotate(const Ciphertext<DCRTPoly>& a, int32_t r);

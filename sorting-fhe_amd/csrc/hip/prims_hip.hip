@@ -1228,54 +1228,6 @@ __global__ __launch_bounds__(kThreads) void k_mac_plain2(u64* __restrict__ out0,
     }
 }
 
-// sfp_mac_plain_multi: every thread keeps its two coefficients of all nin
-// inputs (both polys) in registers and forms the nout sums from them, so each
-// input row is read once instead of once per sum.
-struct MacMultiArgs {
-    const u64* a[SFP_MAX_MACM_IN];
-    const u64* c[SFP_MAX_MACM_IN];
-    const u64* b[SFP_MAX_MACM_PT];
-    u64* o0[SFP_MAX_MACM_OUT];
-    u64* o1[SFP_MAX_MACM_OUT];
-};
-template <int NI>
-__global__ __launch_bounds__(kThreads) void k_mac_plain_multi(const MacMultiArgs A, uint32_t nin, uint32_t nout,
-                                                              sfp_limbs m, const sf_barrett* __restrict__ bar,
-                                                              uint32_t logn) {
-    const size_t pairs = ((size_t)m.count << logn) >> 1;
-    for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < pairs;
-         i += (size_t)gridDim.x * kThreads) {
-        const size_t e = 2 * i;
-        const sf_barrett B = loadBar(bar, primeOf(m, (uint32_t)(e >> logn)));
-        ulonglong2 xa[NI], xc[NI];
-#pragma unroll
-        for (int j = 0; j < NI; ++j)
-            if ((uint32_t)j < nin) {
-                xa[j] = *reinterpret_cast<const ulonglong2*>(A.a[j] + e);
-                xc[j] = *reinterpret_cast<const ulonglong2*>(A.c[j] + e);
-            }
-        for (uint32_t g = 0; g < nout; ++g) {
-            Acc x0{0, 0}, y0{0, 0}, x1{0, 0}, y1{0, 0};
-#pragma unroll
-            for (int j = 0; j < NI; ++j)
-                if ((uint32_t)j < nin) {
-                    const ulonglong2 p = *reinterpret_cast<const ulonglong2*>(A.b[g * nin + j] + e);
-                    macc(x0, xa[j].x, p.x);
-                    macc(y0, xa[j].y, p.y);
-                    macc(x1, xc[j].x, p.x);
-                    macc(y1, xc[j].y, p.y);
-                }
-            ulonglong2 o0, o1;
-            o0.x = sf_reduce128_acc(x0.lo, x0.hi, &B);
-            o0.y = sf_reduce128_acc(y0.lo, y0.hi, &B);
-            o1.x = sf_reduce128_acc(x1.lo, x1.hi, &B);
-            o1.y = sf_reduce128_acc(y1.lo, y1.hi, &B);
-            *reinterpret_cast<ulonglong2*>(A.o0[g] + e) = o0;
-            *reinterpret_cast<ulonglong2*>(A.o1[g] + e) = o1;
-        }
-    }
-}
-
 __global__ __launch_bounds__(kThreads) void k_mac_plain(u64* __restrict__ out, PtrList2 ab,
                                                         uint32_t nin, sfp_limbs m,
                                                         const sf_barrett* __restrict__ bar,
@@ -2867,35 +2819,6 @@ void sfp_mac_plain2(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint64_t* 
     hipLaunchKernelGGL(k_mac_plain2, dim3(ewGrid(total / 2)), dim3(kThreads), 0, d->st(), out0, out1, L, nin, m,
                        d->bar, d->logn);
     checkLaunch(d, "mac_plain2");
-}
-
-void sfp_mac_plain_multi(sfp_dev* d, uint64_t* const* out0, uint64_t* const* out1, const uint64_t* const* a0,
-                         const uint64_t* const* a1, const uint64_t* const* b, uint32_t nin, uint32_t nout,
-                         sfp_limbs m) {
-    if (!m.count || !nin || !nout) return;
-    if (!limbsOk(d, m, "mac_plain_multi")) return;
-    if (nin > SFP_MAX_MACM_IN || nout > SFP_MAX_MACM_OUT || nin * nout > SFP_MAX_MACM_PT) {
-        record(d, "mac_plain_multi", hipErrorInvalidValue);
-        return;
-    }
-    MacMultiArgs A{};
-    for (uint32_t j = 0; j < nin; ++j) {
-        A.a[j] = a0[j];
-        A.c[j] = a1[j];
-    }
-    for (uint32_t g = 0; g < nout; ++g) {
-        A.o0[g] = out0[g];
-        A.o1[g] = out1[g];
-        for (uint32_t j = 0; j < nin; ++j) A.b[g * nin + j] = b[(size_t)g * nin + j];
-    }
-    const size_t total = (size_t)m.count * d->n;
-    if (nin <= 8)
-        hipLaunchKernelGGL(k_mac_plain_multi<8>, dim3(ewGrid(total / 2)), dim3(kThreads), 0, d->st(), A, nin, nout, m,
-                           d->bar, d->logn);
-    else
-        hipLaunchKernelGGL(k_mac_plain_multi<SFP_MAX_MACM_IN>, dim3(ewGrid(total / 2)), dim3(kThreads), 0, d->st(), A,
-                           nin, nout, m, d->bar, d->logn);
-    checkLaunch(d, "mac_plain_multi");
 }
 
 void sfp_mac_plain(sfp_dev* d, uint64_t* out, const uint64_t* const* a, const uint64_t* const* b,

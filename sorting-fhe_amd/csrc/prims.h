@@ -119,16 +119,6 @@ void sfp_mac_plain(sfp_dev* d, uint64_t* out, const uint64_t* const* a, const ui
 // out0 = sum_j a0[j] * b[j], out1 = sum_j a1[j] * b[j]  (nin <= SFP_MAX_WSUM).
 void sfp_mac_plain2(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint64_t* const* a0,
                     const uint64_t* const* a1, const uint64_t* const* b, uint32_t nin, sfp_limbs m);
-// Several such sums over the same inputs (vecRotsOpt's giant steps: each
-// input read once for all of them):
-//   out0[g] = sum_j a0[j] * b[g*nin + j],  out1[g] = sum_j a1[j] * b[g*nin + j]  (g < nout)
-// nin <= SFP_MAX_MACM_IN, nout <= SFP_MAX_MACM_OUT, nout * nin <= SFP_MAX_MACM_PT.
-#define SFP_MAX_MACM_IN 16
-#define SFP_MAX_MACM_OUT 32
-#define SFP_MAX_MACM_PT 128
-void sfp_mac_plain_multi(sfp_dev* d, uint64_t* const* out0, uint64_t* const* out1, const uint64_t* const* a0,
-                         const uint64_t* const* a1, const uint64_t* const* b, uint32_t nin, uint32_t nout,
-                         sfp_limbs m);
 
 // ---- automorphism ----------------------------------------------------------
 // out = sigma_g(in) in the evaluation domain (g odd, < 2n); out != in.
