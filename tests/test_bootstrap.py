@@ -84,6 +84,32 @@ def test_meta_bootstrap_input_deeper_than_output(oracle_lib):
     assert np.max(np.abs(np.array(e.decrypt(out))[:4] - x)) < 2.0 ** -25
 
 
+def test_double_hoisting_matches_per_rotation_moddown(oracle_lib):
+    """The linear maps' double hoisting (one ModDown per CoeffsToSlots /
+    SlotsToCoeffs group, EvalRotMultAddHoisted) against SFHE_BOOT_HOIST=0 (a
+    ModDown per rotation), each in its own process (the knob is read once):
+    both decrypt to the input within the bootstrap bound and to each other."""
+    import ast
+    import os
+    import subprocess
+    import sys
+    code = ("import sys, numpy as np; sys.path[:0] = sys.argv[1:3]; import sfhe; "
+            "from test_bootstrap import boot_engine, bootstrap_error; "
+            "e = boot_engine('oracle', 12, 8, 30, (2, 2)); out, err = bootstrap_error(e, 8); "
+            "print(repr((float(err), [float(v) for v in np.array(e.decrypt(out))[:8]])))")
+    here = os.path.dirname(os.path.abspath(__file__))
+    py = os.path.join(os.path.dirname(here), "sorting-fhe_amd", "python")
+    res = {}
+    for knob in ("1", "0"):
+        env = dict(os.environ, SFHE_BOOT_HOIST=knob)
+        r = subprocess.run([sys.executable, "-c", code, here, py], env=env, capture_output=True, text=True,
+                           timeout=600, check=True)
+        res[knob] = ast.literal_eval(r.stdout.strip().splitlines()[-1])
+    for knob, (err, _) in res.items():
+        assert err < 2.0 ** -20, (knob, err)
+    np.testing.assert_allclose(res["1"][1], res["0"][1], atol=2.0 ** -20)
+
+
 def test_bootstrap_errors(oracle_lib):
     e = sfhe.Engine("oracle", mult_depth=30, ring_dim=1 << 12, batch_size=8, seed=5)
     e.set_quiet(True)
