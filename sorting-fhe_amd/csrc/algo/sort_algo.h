@@ -786,7 +786,12 @@ class DirectSort : public SortBase<N> {
             m_graph.reset();
             auto g = std::make_unique<Graph>();
             g->key = key;
-            g->in = input_array->Clone();  // sorter-owned input buffer (eager copy)
+            // sorter-owned input buffer (eager copy) in canonical form: a lazy
+            // product's pending rows would be rescaled into a new buffer
+            // INSIDE the graph, and replays would then ignore the copied-in input
+            m_cc->Settle(input_array);
+            g->in = input_array->Clone();
+            m_cc->Settle(g->in);
             if (!m_cc->BeginCapture()) {
                 m_graphOff = true;
                 return sortEager(input_array, SignFunc, Cfg);

@@ -313,6 +313,29 @@ class SfheInternal {
         return s->ellOf(c.level) + (c.pend ? 1u : 0u);
     }
     static void materialize(CiphertextImpl<DCRTPoly>& c, bool pendingOk) {
+        SfheContextState* s = c.cc->state();
+        if (c.undo && !(s->capturing && s->captureEpoch == c.undo->epoch)) {
+            if (s->abandonedEpochs.count(c.undo->epoch)) {  // the capture's work never ran
+                c.def = c.undo->def;
+                c.buf = c.undo->buf;
+                c.c0 = c.undo->c0;
+                c.c1 = c.undo->c1;
+                c.pend = c.undo->pend;
+                c.scale = c.undo->scale;
+            }
+            c.undo.reset();
+        }
+        if (s->capturing && !c.undo && (c.def || (c.pend && !pendingOk))) {
+            auto u = std::make_shared<CiphertextImpl<DCRTPoly>::CaptureUndo>();
+            u->epoch = s->captureEpoch;
+            u->def = c.def;
+            u->buf = c.buf;
+            u->c0 = c.c0;
+            u->c1 = c.c1;
+            u->pend = c.pend;
+            u->scale = c.scale;
+            c.undo = std::move(u);
+        }
         if (c.def) {
             std::shared_ptr<DeferredOp> d = std::move(c.def);
             c.def.reset();
@@ -2207,6 +2230,10 @@ std::shared_ptr<FastRotationPrecomp> CryptoContextImpl<DCRTPoly>::EvalFastRotati
     pre->level = a->level;
     pre->pend = pend;
     pre->beta = (ell + s->alpha - 1) / s->alpha;
+    if (pend) {
+        pre->pinBuf = a->buf;
+        pre->pinC0 = a->c0;
+    }
     if (s->world > 1) {
         pre->stride = (size_t)s->extmap(ell).count * s->n;
         pre->ext = s->alloc(pre->stride * pre->beta);
@@ -2226,20 +2253,23 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalFastRotation(
     const Ciphertext<DCRTPoly>& a, int32_t r, uint32_t, const std::shared_ptr<FastRotationPrecomp>& pre) {
     OpLock g(st.get());
     SfheContextState* s = st.get();
-    if (pre && pre->pend) {  // the precomputation took a's unrescaled rows: so does the rotation
-        SfheInternal::materialize(*a, true);
-        s->dep(a->buf.get());
+    // A pending precomputation rotates the unrescaled rows it pinned (the
+    // shared ciphertext may have been settled since: same value, other form).
+    const bool pinned = pre && pre->pend;
+    if (pinned) {
+        s->dep(pre->pinBuf.get());
     } else {
         SfheInternal::deps(s, {&a});
     }
     uint32_t gal = GaloisForRotation(r);
     if (gal == 1) return a->Clone();
-    if (!pre || pre->level != a->level || pre->pend != a->pend)
+    if (!pre || pre->level != a->level)
         SFHE_THROW("fast-rotation precomputation does not match");
     auto it = s->rotKeys.find(gal);
     if (it == s->rotKeys.end())
         SFHE_THROW("EvalKey for rotation " + std::to_string(r) + " is not found");
-    const uint32_t ell = SfheInternal::ctEll(s, *a);
+    const uint32_t ell = pinned ? s->ellOf(pre->level) + 1 : SfheInternal::ctEll(s, *a);
+    const uint64_t* c0in = pinned ? pre->pinC0 : a->c0;
     // sigma commutes with the (coefficient-wise) base extension, so rotating
     // the extended digits equals extending the rotated c1.
     auto ext = s->alloc(pre->stride * pre->beta);
@@ -2248,7 +2278,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalFastRotation(
     sfp_automorph(s->dev, ext->ptr, pre->ext->ptr, gal, sfp_limbs{rows, rows, 0, 0});
     auto out = pre->pend ? SfheInternal::newPendingCt(this, a->level, a->slots)
                          : SfheInternal::newCt(this, a->level, a->slots);
-    sfp_automorph(s->dev, out->c0, a->c0, gal, st->qmap(ell));
+    sfp_automorph(s->dev, out->c0, c0in, gal, st->qmap(ell));
     SfheInternal::innerAndModDown(this, ext->ptr, pre->stride, pre->beta, ell, it->second,
                                   out->c0, out->c1, 1, 0);
     s->stats.keyswitch++;
@@ -2815,6 +2845,9 @@ void CryptoContextImpl<DCRTPoly>::CopyCiphertextInto(const Ciphertext<DCRTPoly>&
                                                      const Ciphertext<DCRTPoly>& src) {
     OpLock lk(st.get());
     SfheContextState* s = st.get();
+    // the destination's rows are what a graph reads: settling a lazy one would
+    // move it to a new buffer the graph never sees
+    if (dst->def || dst->pend || dst->undo) SFHE_THROW("CopyCiphertextInto: the destination is a lazy product");
     SfheInternal::deps(s, {&dst, &src});
     if (dst->level != src->level) SFHE_THROW("CopyCiphertextInto: level mismatch");
     const size_t bytes = s->polyWords(src->level) * 8;

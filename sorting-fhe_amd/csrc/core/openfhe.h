@@ -215,6 +215,19 @@ class CiphertextImpl<DCRTPoly> {
     //    rescale that settles the result.
     std::shared_ptr<DeferredOp> def;
     bool pend = false;
+    // The form this ciphertext had before a graph capture computed or settled
+    // it: the captured work only runs on replay, so if that
+    // capture is abandoned the ciphertext returns to this form and is
+    // recomputed eagerly by its next consumer.
+    struct CaptureUndo {
+        uint64_t epoch = 0;
+        std::shared_ptr<DeferredOp> def;
+        DeviceBufferPtr buf;
+        uint64_t *c0 = nullptr, *c1 = nullptr;
+        bool pend = false;
+        double scale = 1.0;
+    };
+    std::shared_ptr<CaptureUndo> undo;
 };
 
 // Key pairs carry a random 64-bit tag (OpenFHE's keyTag): evaluation keys,
@@ -245,6 +258,10 @@ struct FastRotationPrecomp {
     bool pend = false;  // taken of the ciphertext's unrescaled rows (one limb more)
     uint32_t beta = 0;
     size_t stride = 0;
+    // pending precomputations pin the c0 rows they were taken with: another
+    // consumer may settle (rescale) the shared ciphertext before the rotations
+    DeviceBufferPtr pinBuf;
+    const uint64_t* pinC0 = nullptr;
 };
 
 struct SfheContextState;  // parameters, tables, keys, pools (context.cpp)

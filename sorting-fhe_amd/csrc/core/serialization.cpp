@@ -8,9 +8,10 @@
 // chain (the chain is re-derived on load and must match); key and
 // ciphertext records carry their key pair's tag, then their device words,
 // whose counts are checked against the context's sizes before anything is
-// allocated.  A key record binds to a context of its fingerprint holding no
-// key pair yet (newest first), else to the one holding its own key pair; a
-// ciphertext record the other way round (openfhe.h, Serialize*Key).
+// allocated.  A key record binds to the context this thread deserialized
+// last when its fingerprint matches, else to a context of its fingerprint
+// holding no key pair yet (newest first), else to the one holding its own key
+// pair; a ciphertext record the other way round (openfhe.h, Serialize*Key).
 #include <algorithm>
 #include <cstring>
 #include <mutex>
@@ -31,8 +32,24 @@ std::vector<std::weak_ptr<CryptoContextImpl<DCRTPoly>>> g_registry;
 // to: a context holding that key pair, or one holding none yet (which the
 // record then claims), in the order `keysFirst` gives; newest first within
 // each.  Never a context of another key pair.
+// The context the calling thread deserialized last: the key records of one
+// load (src/sort.h:31-74 reads the context, then its keys) bind to it first,
+// so another live context with the same parameters -- keyless, or holding the
+// same key pair -- never receives part of that load.
+thread_local std::weak_ptr<CryptoContextImpl<DCRTPoly>> t_loaded;
+
 CryptoContext<DCRTPoly> findContext(uint64_t fp, uint64_t tag, bool freshFirst) {
     std::lock_guard<std::mutex> g(g_regMu);
+    if (auto cc = t_loaded.lock()) {
+        if (cc->Fingerprint() == fp) {
+            SfheContextState* s = cc->state();
+            if (freshFirst && s->keyTag == 0) {
+                s->keyTag = tag;
+                return cc;
+            }
+            if (tag && s->keyTag == tag) return cc;
+        }
+    }
     for (int pass = 0; pass < 2; ++pass) {
         const bool wantFresh = (pass == 0) == freshFirst;
         for (auto it = g_registry.rbegin(); it != g_registry.rend(); ++it)
@@ -199,6 +216,7 @@ bool Serial::Deserialize(CryptoContext<DCRTPoly>& cc, std::istream& is, SerType:
         return false;
     }
     cc = c;
+    t_loaded = c;
     return true;
 }
 

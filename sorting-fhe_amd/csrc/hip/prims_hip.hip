@@ -2589,6 +2589,8 @@ sfp_graph* sfp_capture_end(sfp_dev* d) {
     sfp_graph* g = d->capture;
     if (!g) return nullptr;
     d->cur = 0;
+    // test knob (read per capture): abandon this capture as if it had failed
+    if (const char* f = std::getenv("SFHE_CAPTURE_FORCE_FAIL"); f && *f == '1') captureFail(d, "forced (SFHE_CAPTURE_FORCE_FAIL)");
     const hipError_t e = hipStreamEndCapture(d->streams[0], &g->g);
     d->capture = nullptr;
     if (e != hipSuccess || g->failed || !g->g) {

@@ -11,6 +11,11 @@ and the test suite only read the committed JSON.  Extracted:
       coefficients (src/sign.cpp:9-158)
     - CompareTest inputs / expected outputs / tolerance (tests/CompareTest.cpp:13-63)
     - DecomposeTest key set and numbers (tests/DecomposeTest.cpp:10-13, :64-75)
+* hybrid1_published.json
+    - the reference's only published outputs: sort_hybrid1 per N (summary
+      and each of the 10 trials: ring, depth, sign configuration, time, max /
+      average error, result level) from comparison/experimental_results/
+      ours_hybrid1/{total_results.txt, trials/trial_*/size_*.txt}
 * derived_expectations.json (computed here, recorded with their derivation):
     - the Chebyshev-PS depth table of the reference's OpenFHE (SURVEY a-12 iv)
     - Decomposer NAF(127) = {64, 64, -1} recorded in SURVEY 8(c) from the
@@ -88,6 +93,37 @@ def decompose_test():
     return {"N": 128, "keys": keys, "numbers": numbers, "wrap": 128}
 
 
+def hybrid1_published():
+    base = "comparison/experimental_results/ours_hybrid1"
+    total = read(base + "/total_results.txt")
+    out = {}
+    for blk in total.split("Results for N = ")[1:]:
+        N = int(re.match(r"(\d+)", blk).group(1))
+        g = lambda pat: re.search(pat, blk).group(1)
+        cfg = nums(g(r"CompositeSign\(([^)]*)\)"))
+        out[str(N)] = {"ring_dim": int(g(r"Ring Dimension\s*:\s*(\d+)")),
+                       "mult_depth": int(g(r"Multiplicative Depth:\s*(\d+)")),
+                       "scaling_mod_size": int(g(r"Scaling Mod Size\s*:\s*(\d+)")),
+                       "sign": cfg,
+                       "avg_time_s": float(g(r"Average Time\s*:\s*([\d.]+)s")),
+                       "max_err_log2": float(g(r"Max Error \(log2\):\s*(-?[\d.]+)")),
+                       "avg_err_log2": float(g(r"Average Error \(log2\):\s*(-?[\d.]+)")),
+                       "trials": []}
+    for t in range(1, 11):
+        for N in out:
+            txt = read(f"{base}/trials/trial_{t}/size_{N}.txt")
+            m = re.search(r"Maximum error: ([-\d.e+]+) \(log2: (-?[\d.]+)\)", txt)
+            a = re.search(r"Average error: ([-\d.e+]+) \(log2: (-?[\d.]+)\)", txt)
+            out[N]["trials"].append({
+                "trial": t,
+                "time_ms": int(re.search(r"Execution time: (\d+) ms", txt).group(1)),
+                "max_err": float(m.group(1)), "max_err_log2": float(m.group(2)),
+                "avg_err": float(a.group(1)), "avg_err_log2": float(a.group(2)),
+                "level": int(re.search(r"Result Level: (\d+)", txt).group(1))})
+    return {"_source": f"extracted from /root/reference/{base} by tests/golden/make_golden.py (data only)",
+            "by_N": out}
+
+
 def main():
     ref = {
         "_source": "extracted from /root/reference by tests/golden/make_golden.py (data only)",
@@ -98,6 +134,8 @@ def main():
     }
     with open(os.path.join(HERE, "reference_params.json"), "w") as f:
         json.dump(ref, f, indent=1)
+    with open(os.path.join(HERE, "hybrid1_published.json"), "w") as f:
+        json.dump(hybrid1_published(), f, indent=1)
     derived = {
         "_source": "derived expectations (see SURVEY.md a-12 (iv) and 8(c))",
         "chebyshev_ps_depth_table": [[5, 3], [13, 4], [27, 5], [59, 6], [119, 7], [247, 8],

@@ -68,3 +68,34 @@ def test_graph_pool_steady(monkeypatch):
         sizes.append(e.pool_bytes())
     assert s.graph_nodes() > 0
     assert sizes[-1] == sizes[3], sizes
+
+
+@pytest.mark.parametrize("force_fail", [False, True])
+def test_graph_lazy_inputs(force_fail, monkeypatch):
+    """ADVICE r3 (high / medium): sorts of inputs that are lazy products
+    (EvalMult(ct, 1.0): deferred, rescaled by their first consumer).  Three
+    different arrays through one sorter -- eager, captured, replayed -- must
+    each come back sorted; with the capture forced to fail
+    (SFHE_CAPTURE_FORCE_FAIL=1) the sorter falls back to eager sorts and the
+    results are the same values."""
+    N, logn = 64, 14
+    depth, rots = sfhe.direct_sort_params(N, "hip")
+    e = sfhe.Engine("hip", mult_depth=depth + 1, ring_dim=1 << logn, batch_size=N, rotations=rots,
+                    seed=20251205 + N)
+    e.set_quiet(True)
+    cfg = slotsim.default_sign_config(N)
+    s = e.sorter(N)
+    monkeypatch.setenv("SFHE_GRAPH", "1")
+    rng = np.random.default_rng(5)
+    for i in range(3):
+        y = rng.permutation(N) / N + i * 0.3 / N
+        lazy = e.mult_const(e.encrypt(y.tolist()), 1.0)
+        if i == 1 and force_fail:
+            monkeypatch.setenv("SFHE_CAPTURE_FORCE_FAIL", "1")
+        out = s.sort(lazy, *cfg)
+        monkeypatch.delenv("SFHE_CAPTURE_FORCE_FAIL", raising=False)
+        err = float(np.max(np.abs(np.array(e.decrypt(out))[:N] - np.sort(y))))
+        print(f"input {i}: max err {err:.3g}, graph nodes {s.graph_nodes()}")
+        assert err < 1e-3, (i, err)
+        if i >= 1:
+            assert (s.graph_nodes() > 0) == (not force_fail)

@@ -128,6 +128,19 @@ def test_direct_sort_h1_test(hip_lib):
     assert len(errs) == 7 and max(errs) < 0.01
 
 
+def test_direct_sort_h1_test_large(hip_lib):
+    """tests/DirectSortH1Test.cpp as-is, the two largest sizes: N = 512 and
+    1024 (depth 53 / 56, CompositeSign(3,4,2) / (3,5,2)), which the reference
+    publishes at 2^-18.51 and 2^-17.85."""
+    rc, out = run(exe("DirectSortH1Test"), "--gtest_filter=*/7.*:*/8.*", timeout=600)
+    errs = [float(x) for x in re.findall(r"Maximum error: ([0-9.e+-]+)", out)]
+    times = [int(x) for x in re.findall(r"Execution time: (\d+) ms", out)]
+    print("max errors:", errs, "\nexecution ms:", times)
+    assert rc == 0, out[-4000:]
+    assert "2 tests ran, 0 failed" in out
+    assert len(errs) == 2 and max(errs) < 0.01
+
+
 def test_bitonic_sort_test(hip_lib):
     """tests/BitonicSortTest.cpp as-is: BitonicSort<4> at ring 2^12, depth 58,
     two meta-bootstraps (EvalBootstrap(ct, 2, 20)); max error < 1, none > 0.1."""

@@ -95,3 +95,53 @@ def test_hybrid1_directsorth1test_config(hip_lib, N, tol, exact_tol):
     assert err < 0.01
     assert err < exact_tol
     assert np.max(np.abs(got - sim)) < tol
+
+
+def _published():
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "hybrid1_published.json")) as f:
+        return json.load(f)["by_N"]
+
+
+def test_published_fixture_matches_params(oracle_lib):
+    """The published runs used the depths and sign configurations this engine
+    takes for DirectSortH1Test (hybrid1_params / default_sign_config)."""
+    pub = _published()
+    assert sorted(int(n) for n in pub) == SIZES
+    for N in SIZES:
+        p = pub[str(N)]
+        assert p["ring_dim"] == 1 << 17 and p["scaling_mod_size"] == 40
+        assert p["mult_depth"] == sfhe.hybrid1_params(N, "oracle")[0], N
+        assert tuple(p["sign"]) == tuple(slotsim.default_sign_config(N)), N
+        assert all(t["level"] == p["mult_depth"] for t in p["trials"])
+
+
+# Engine max error / the largest of the reference's 10 published trials,
+# allowed per N (VERDICT r3 item 2).  1.25 everywhere the engine is at or below
+# the reference; DESIGN.md §2 attributes any N listed with a larger factor.
+HYBRID1_RATIO = {N: 1.25 for N in SIZES}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", SIZES)
+def test_hybrid1_published_outputs(hip_lib, N):
+    """sort_hybrid1 at DirectSortH1Test's configuration (ring 2^17,
+    HEStd_128_classic, its depth / keys / sign configuration) against every
+    output the reference publishes (comparison/experimental_results/
+    ours_hybrid1/total_results.txt:1-224 and trials/trial_*/size_*.txt, 10
+    trials per N, extracted to tests/golden/hybrid1_published.json): final
+    level == depth (the reference's Result Level), and the max error within
+    HYBRID1_RATIO[N] x the largest published trial error."""
+    pub = _published()[str(N)]
+    e, x, out, depth = run_hybrid1("hip", N, 17, secure=True)
+    got = np.array(e.decrypt(out))[:N]
+    err = float(np.max(np.abs(got - np.sort(x))))
+    pmax = max(t["max_err"] for t in pub["trials"])
+    pmin = min(t["max_err"] for t in pub["trials"])
+    sim, _ = slotsim.sort_hybrid1(x, N, 1 << 17)
+    floor = float(np.max(np.abs(sim - np.sort(x))))
+    print(f"hybrid1 N={N}: max err {err:.3g} (log2 {np.log2(err):.2f}); published {pmin:.3g}..{pmax:.3g} "
+          f"(log2 {pub['max_err_log2']:.2f}); slotsim floor {floor:.3g}; ratio {err / pmax:.2f}")
+    assert out.level == depth == pub["mult_depth"]
+    assert err <= HYBRID1_RATIO[N] * pmax, (N, err, pmax)

@@ -99,3 +99,28 @@ def test_c_abi_save_load_roundtrip(tmp_path, oracle_lib):
     assert np.allclose(got, np.roll(x * x, -1), atol=1e-4)
     with pytest.raises(sfhe.SfheError, match="cannot open"):
         sfhe.Engine.load(str(tmp_path / "missing"), "oracle")
+
+
+def test_load_binds_every_record_to_the_loaded_context(tmp_path, oracle_lib):
+    """with another keyless context of the same parameters alive
+    (and the writer, holding the same key pair, too), every key record of one
+    sfhe_load -- public, secret, relinearisation and rotation keys -- and the
+    ciphertext loaded after it bind to the context that load deserialized."""
+    import numpy as np
+    import sfhe
+    kw = dict(mult_depth=4, ring_dim=1 << 12, batch_size=8, seed=9)
+    e = sfhe.Engine("oracle", rotations=[1], **kw)
+    e.set_quiet(True)
+    x = np.array([0.5, -0.25, 0.125, 0.75, 0.1, 0.2, 0.3, 0.4])
+    e.save(str(tmp_path))
+    e.save_ct(e.encrypt(x.tolist()), str(tmp_path / "ct.bin"))
+    blank = sfhe.Engine("oracle", keygen=False, **kw)  # same fingerprint, no key pair
+    f = sfhe.Engine.load(str(tmp_path), "oracle")
+    f.set_quiet(True)
+    ct = f.load_ct(str(tmp_path / "ct.bin"))
+    got = np.array(f.decrypt(f.rotate(f.mult(ct, ct), 1)))[:8]
+    assert np.allclose(got, np.roll(x * x, -1), atol=1e-4)
+    # the keyless bystander received nothing: it cannot decrypt or rotate
+    with pytest.raises(sfhe.SfheError):
+        blank.decrypt(blank.encrypt(x.tolist()))
+    del blank, e
