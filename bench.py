@@ -7,14 +7,19 @@ encrypted array (reference src/sort_algo.h:752-774, timed like
 tests/DirectSortTest.cpp:129-136) at the metric configuration of
 BASELINE.json: N=256, ring 2^16, depth 34, CompositeSign(3,4,2), scale 40.
 
-Multi-GPU: one process per GPU.  Default: every rank sorts its own array
-(independent replicas, no data-path collective) -> weak scaling; value =
-comparisons/s of the whole job = world * N^2 * K / max-over-ranks(time).
-``--shard rccl``: the ranks limb-shard ONE sort (rank r holds
-the RNS limbs i % world == r; RCCL all-gather at ModUp / ModDown, broadcast at
-rescale) -> strong scaling; value = N^2 * K / max-over-ranks(time).
-``--shard host`` runs the same over the gloo host transport (a rehearsal of
-the sharded bench on one GPU: SFHE_BENCH_DEVICE=0 puts every rank on it).
+Multi-GPU (one process per GPU; BASELINE north_star: "encrypted-sort
+wall-clock ... at 1, 2, 4 and 8 MI355X"): at N > 1 the headline is the
+wall-clock of ONE metric sort limb-sharded over the ranks (SURVEY §8(e):
+rank r holds the RNS limbs i % N == r above the replicated tail; RCCL
+all-gather at ModUp / ModDown, broadcast at rescale, the whole sort one
+hipGraph with its collectives) -> scaling "strong", value = N^2 * K / max-
+over-ranks(time).  The ranks' independent replica sorts (each GPU its own
+array, no data-path collective) are measured first and reported as the
+extra field ``replicas``; should the sharded leg fail or stall, the line
+carries the replica throughput as the headline and says so.
+``--replicas`` makes the replicas the headline (weak scaling);
+``--shard host`` runs the sharded sort over the gloo host transport (a
+rehearsal on one GPU: SFHE_BENCH_DEVICE=0 puts every rank on it).
 
 Extra fields: ``roofline`` (dominant kernel family: HIP events around each of
 its launches during one profiling sort after the timed region, lanes
@@ -274,6 +279,58 @@ def pmc_traffic(family: str):
     return j.get("families", {}).get(family, {}).get("traffic_over_algorithmic")
 
 
+def shard_spec(mode: str, rank: int, world: int):
+    """Engine(shard=...) argument of the limb-sharded sort: an RCCL
+    communicator (rank 0's unique id broadcast over torch.distributed) or the
+    gloo host transport."""
+    if mode == "rccl":
+        import torch.distributed as dist
+        uid = [sfhe.comm_uid("hip") if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        return ("rccl", rank, world, uid[0])
+    return ("host", rank, world, sfhe.GlooComm())
+
+
+def replica_leg(make_engine, spec, world, steps, warmup):
+    """Every rank sorts its own array on its own GPU (no data-path
+    collective): the job's throughput, world * N^2 per sort time.  Measured
+    with the same barrier / max-over-ranks timing as the headline."""
+    N, cfg = spec["N"], spec["cfg"]
+    eng = make_engine()
+    eng.set_quiet(True)
+    sorter = eng.sorter(N)
+    ct = eng.encrypt(input_vector(N).tolist())
+    holder = {}
+
+    def step():
+        holder["out"] = sorter.sort(ct, *cfg)
+
+    dt = timed_steps(step, eng.sync, world, steps, warmup)
+    nodes = sorter.graph_nodes()
+    holder.clear()
+    del sorter, ct
+    eng.close()
+    return {"value": world * N * N * steps / dt, "unit": "cmp/s", "ms_per_step": dt / steps * 1e3,
+            "scaling": "weak", "parallelism": f"replicas x{world}", "graph_nodes": nodes,
+            "note": "each rank sorts its own array (independent replicas, no data-path collective)"}
+
+
+def fallback_line(replicas, spec, world, args, why):
+    """The metric line when the sharded headline could not be measured: the
+    replica throughput, labelled as such."""
+    N = spec["N"]
+    return {"metric": "encrypted rank-sort homomorphic comparisons/s (N^2 per DirectSort<N>::sort)",
+            "value": replicas["value"], "unit": "cmp/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": replicas["ms_per_step"],
+            "sort_seconds": replicas["ms_per_step"] / 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u64 (RNS residues, 40/60-bit primes)",
+            "data": "synthetic: seeded permutation of {k/N}, CKKS-encrypted",
+            "config": {"workload": args.workload, "N": N, "ring_dim": 1 << spec["logn"],
+                       "mult_depth": spec["depth"], "sign": list(spec["cfg"]), "scale_bits": 40,
+                       "secure": spec["secure"], "parallelism": f"replicas x{world}"},
+            "replicas": replicas, "sharded_error": why}
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -293,7 +350,9 @@ def main(argv=None):
                     help="run the config-5 leg without graph replay (profiling: replaying the 2^17 sort's graph "
                          "under rocprofv3's kernel tracer crashes inside the profiler, DESIGN.md §5)")
     ap.add_argument("--shard", choices=("rccl", "host"), default=None,
-                    help="limb-shard one sort over the ranks instead of running replicas")
+                    help="transport of the limb-sharded headline sort at N > 1 (default rccl)")
+    ap.add_argument("--replicas", action="store_true",
+                    help="at N > 1, make the independent replica sorts the headline (weak scaling)")
     args = ap.parse_args(argv)
 
     world, rank, local = dist_init()
@@ -304,18 +363,42 @@ def main(argv=None):
     cfg = sign_config(N)
 
     device = int(os.environ.get("SFHE_BENCH_DEVICE", local))
+    mode = None if (world == 1 or args.replicas) else (args.shard or "rccl")
+    spec = dict(N=N, logn=logn, secure=secure, depth=depth, rots=rots, cfg=cfg)
+    replicas = None
+    if mode:  # the safe number first: every rank sorts its own array
+        replicas = replica_leg(lambda: sfhe.Engine("hip", mult_depth=depth, ring_dim=1 << logn, batch_size=N,
+                                                   secure=secure, rotations=rots, seed=20251205 + N + 7919 * rank,
+                                                   device=device),
+                               spec, world, args.steps, args.warmup)
     shard, seed = None, 20251205 + N + 7919 * rank
-    if args.shard and world > 1:
-        import torch.distributed as dist
+    if mode:
         seed = 20251205 + N  # every rank builds the same keys
-        if args.shard == "rccl":
-            uid = [sfhe.comm_uid("hip") if rank == 0 else None]
-            dist.broadcast_object_list(uid, src=0)
-            shard = ("rccl", rank, world, uid[0])
-        else:
-            shard = ("host", rank, world, sfhe.GlooComm())
-    eng = sfhe.Engine("hip", mult_depth=depth, ring_dim=1 << logn, batch_size=N, secure=secure,
-                      rotations=rots, seed=seed, device=device, shard=shard)
+        shard = shard_spec(mode, rank, world)
+    limit = float(os.environ.get("SFHE_SHARD_TIMEOUT", "600"))
+    dog = None
+    if mode:  # a stalled collective: report the replicas, then fail loudly
+        import threading
+
+        def stalled():
+            if rank == 0:
+                print(json.dumps(fallback_line(replicas, spec, world, args, f"sharded leg stalled after {limit:.0f} s")),
+                      flush=True)
+            sys.stderr.write(f"bench: sharded leg stalled after {limit:.0f} s\n")
+            sys.stderr.flush()
+            os._exit(2)
+        dog = threading.Timer(limit, stalled)
+        dog.daemon = True
+        dog.start()
+    try:
+        eng = sfhe.Engine("hip", mult_depth=depth, ring_dim=1 << logn, batch_size=N, secure=secure,
+                          rotations=rots, seed=seed, device=device, shard=shard)
+    except Exception as e:  # noqa: BLE001 -- the sharded context could not be built
+        if not mode:
+            raise
+        if rank == 0:
+            print(json.dumps(fallback_line(replicas, spec, world, args, f"sharded context: {e}")), flush=True)
+        sys.exit(3)
     eng.set_quiet(True)
     sorter = eng.sorter(N)
     x = input_vector(N)
@@ -337,6 +420,7 @@ def main(argv=None):
     cold_ms = (time.perf_counter() - t0) * 1e3
 
     dt = timed_steps(step, eng.sync, world, args.steps, args.warmup)
+    tail = eng.shard_tail()
 
     # profiling leg (after the timed region): one sort with the lanes
     # serialised on one stream and every launch of each family bracketed by
@@ -455,7 +539,8 @@ def main(argv=None):
         "data": "synthetic: seeded permutation of {k/N}, CKKS-encrypted",
         "config": {"workload": args.workload, "N": N, "ring_dim": 1 << logn, "mult_depth": depth,
                    "sign": list(cfg), "scale_bits": 40, "secure": secure,
-                   "parallelism": f"limb-shard x{world} ({args.shard})" if shard else f"replicas x{world}"},
+                   "parallelism": (f"limb-shard x{world} ({mode}; replicated tail <= {tail} limbs)" if shard
+                                   else f"replicas x{world}")},
         "algorithmic_gb_per_sort": stats["algo_bytes"] / 1e9,
         "graph": {"replayed": graph_nodes > 0, "nodes": graph_nodes,
                   "note": "timed steps replay the sort as one hipGraph (captured during warmup; "
@@ -465,27 +550,31 @@ def main(argv=None):
         "trials": trials,
         "cpu_baseline": None,
     }
-    if args.c5 and not shard:
+    if replicas:
+        result["replicas"] = replicas
+    if dog:
+        dog.cancel()
+    if args.c5 and (world == 1 or mode == "rccl"):
         import threading
 
-        def stalled():  # the collective path hung: report what was measured, then fail loudly
+        def c5_stalled():  # the collective path hung: report what was measured, then fail loudly
             if rank == 0:
-                result["c5"] = {"error": f"timeout after {limit:.0f} s (collective stalled)"}
+                result["c5"] = {"error": f"timeout after {c5_limit:.0f} s (collective stalled)"}
                 print(json.dumps(result), flush=True)
-            sys.stderr.write(f"bench: c5 leg stalled after {limit:.0f} s\n")
+            sys.stderr.write(f"bench: c5 leg stalled after {c5_limit:.0f} s\n")
             sys.stderr.flush()
             os._exit(2)
-        limit = float(os.environ.get("SFHE_C5_TIMEOUT", "240"))
-        dog = threading.Timer(limit, stalled)
-        dog.daemon = True
-        dog.start()
+        c5_limit = float(os.environ.get("SFHE_C5_TIMEOUT", "240"))
+        c5_dog = threading.Timer(c5_limit, c5_stalled)
+        c5_dog.daemon = True
+        c5_dog.start()
         if args.c5_eager:
             os.environ["SFHE_GRAPH"] = "0"  # read per sort by the sorter
         try:
             result["c5"] = c5_leg(device, world, rank)
         except Exception as e:  # noqa: BLE001 -- an extra leg must not lose the metric line
             result["c5"] = {"error": str(e)}
-        dog.cancel()
+        c5_dog.cancel()
     if rank == 0 and world == 1 and args.hybrid1:
         try:
             result["hybrid1"] = hybrid1_leg(device)

@@ -267,15 +267,20 @@ int sfhe_decompose(uint32_t N, const int32_t* keys, size_t nkeys, int32_t rotati
 /* ---- limb sharding (no reference counterpart: the reference
  * runs one process on one device) -------------------------------------------
  * One process per GPU; rank r of W holds the RNS limbs q_i / p_k with
- * i % W == r / k % W == r.  Key generation and encryption run on every limb
- * (setup); evaluation runs on the local limbs only, with three exchanges: the
- * ModUp input (all-gather of the coefficient-form Q limbs), the ModDown P
- * limbs (all-gather) and a rescale's dropped limb (broadcast by its owner).
+ * i % W == r / k % W == r of every ciphertext level with more than the
+ * replicated-tail limb count (SFHE_SHARD_TAIL, default 16; below it every
+ * rank holds and computes every limb, without exchanges).  Key generation
+ * and encryption run on every limb (setup) and every rank keeps whole
+ * switching keys; evaluation runs on the local limbs only, with three
+ * exchanges: the ModUp input (all-gather of the coefficient-form Q limbs),
+ * the ModDown P limbs (all-gather) and a rescale's dropped limb (broadcast by
+ * its owner), plus one all-gather where a ciphertext enters the tail.
  * Decryption and sfhe_ct_download all-gather the limbs.  Every rank makes
  * the same calls in the same order (they are collective); results are
  * bit-identical to the unsharded context.  Call once per context, after
  * sfhe_context_create and before sfhe_keygen, with the same params and seed
- * on every rank. */
+ * on every rank.  RCCL-sharded sorts are captured into hipGraphs with their
+ * collectives; a one-rank RCCL communicator takes the sharded path too. */
 /* 128-byte RCCL unique id (one rank; shared out of band).  SFHE_ENOTIMPL on
  * a backend without RCCL (the CPU oracle). */
 int sfhe_comm_uid(uint8_t uid[128]);
@@ -287,6 +292,8 @@ typedef void (*sfhe_allgather_fn)(void* user, const void* send, void* recv, size
 typedef void (*sfhe_bcast_fn)(void* user, void* buf, size_t bytes, int root);
 int sfhe_shard_host(sfhe_ctx* c, int rank, int world, sfhe_allgather_fn ag, sfhe_bcast_fn bc,
                     void* user);
+/* The replicated-tail limb count of a sharded context (0: unsharded). */
+int sfhe_shard_tail(const sfhe_ctx* c, uint32_t* limbs);
 
 #ifdef __cplusplus
 }

@@ -634,6 +634,7 @@ void sfp_comm_set_host(sfp_dev* d, int rank, int world, sfp_host_allgather_fn ag
     d->bc = bc;
     d->user = user;
 }
+int sfp_comm_capturable(sfp_dev* d) { (void)d; return 0; /* no graphs in the oracle */ }
 void sfp_allgather(sfp_dev* d, const void* send, void* recv, size_t bytes) {
     if (d->world <= 1 || !d->ag) {
         if (send != recv) memmove(recv, send, bytes);
@@ -689,7 +690,7 @@ void sfp_ks_inner_map(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t
     const uint32_t n = d->n;
 #pragma omp parallel for schedule(static)
     for (uint32_t t = 0; t < pm.count; ++t) {
-        const uint32_t kr = t < pm.split ? t : keyQ + (t - pm.split);
+        const uint32_t kr = keyQ == SFP_KEY_ROW_BY_PRIME ? pidx(pm, t) : (t < pm.split ? t : keyQ + (t - pm.split));
         const u64 q = d->q[pidx(pm, t)];
         for (uint32_t x = 0; x < n; ++x) {
             u128 s0 = 0, s1 = 0;

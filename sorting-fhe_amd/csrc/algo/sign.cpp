@@ -38,8 +38,10 @@ struct OddPoly {
 
     // c x at level `at` (> x's level)
     Ct constAt(double c, uint32_t at) {
-        cc->Settle(x);
-        const std::vector<const uint64_t*> i0{x->c0}, i1{x->c1};
+        const uint64_t *r0, *r1;
+        std::vector<DeviceBufferPtr> keep;
+        cc->RowsAt(x, at - 1, &r0, &r1, keep);  // settled (and gathered into a replicated tail)
+        const std::vector<const uint64_t*> i0{r0}, i1{r1};
         const std::vector<double> w{c}, sc{x->scale};
         return cc->LinearWSumRescale(i0, i1, w, at - 1, x->GetSlots(), &sc);
     }

@@ -727,8 +727,9 @@ class DirectSort : public SortBase<N> {
     // generates and encodes the masks); the second is captured into a graph
     // over a sorter-owned copy of the input; from then on a sort is: copy the
     // caller's input into that buffer, launch the graph, clone its result.
-    // Debug sorts (PRINT_PT decrypts) and sharded contexts stay eager;
-    // SFHE_GRAPH=0 disables graphs.
+    // Debug sorts (PRINT_PT decrypts) stay eager, and so do contexts sharded
+    // over a host transport (BeginCapture refuses them); RCCL-sharded sorts
+    // capture their collectives into the graph.  SFHE_GRAPH=0 disables graphs.
     struct GraphKey {
         uint32_t level = 0, slots = 0;
         int func = -1, n = 0, dg = 0, df = 0;
@@ -764,7 +765,7 @@ class DirectSort : public SortBase<N> {
     Ciphertext<DCRTPoly> sort(const Ciphertext<DCRTPoly>& input_array, SignFunc SignFunc,
                               SignConfig& Cfg) override {
         const bool debug = dynamic_cast<const DebugEncryption*>(m_enc.get()) != nullptr;
-        if (debug || m_graphOff || !graphsEnabled() || m_cc->ShardWorld() > 1)
+        if (debug || m_graphOff || !graphsEnabled())
             return sortEager(input_array, SignFunc, Cfg);
         GraphKey key;
         key.level = input_array->GetLevel();

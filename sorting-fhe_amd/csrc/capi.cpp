@@ -724,7 +724,7 @@ int sfhe_decompose(uint32_t N, const int32_t* keys, size_t nkeys, int32_t rotati
 int sfhe_debug_decrypt_coeffs(sfhe_ctx* c, const sfhe_ct* ct, double* out, size_t cap) {
     REQUIRE(c && ct && out, "null argument");
     REQUIRE(c->keys.secretKey, "no secret key");
-    REQUIRE(c->cc->ShardWorld() == 1, "debug decrypt needs an unsharded context");
+    REQUIRE(!c->cc->IsSharded(), "debug decrypt needs an unsharded context");
     const size_t n = c->cc->GetRingDimension();
     REQUIRE(cap >= n, "output buffer too small");
     return guard([&] {
@@ -796,14 +796,16 @@ int sfhe_shard_rccl(sfhe_ctx* c, int rank, int world, const uint8_t uid[128]) {
     REQUIRE(c && uid, "null argument");
     REQUIRE(world >= 1 && rank >= 0 && rank < world, "bad rank / world");
     REQUIRE(!c->keys.secretKey, "shard the context before sfhe_keygen");
-    REQUIRE(c->cc->ShardWorld() == 1, "context already sharded");
+    REQUIRE(!c->cc->IsSharded(), "context already sharded");
     return guard([&] {
         auto* s = c->cc->state();
         if (sfp_comm_init_rccl(s->dev, rank, world, uid) != 0) {
             const char* e = sfp_last_error(s->dev);
             throw OpenFHEException(std::string("device error: RCCL communicator: ") + (e ? e : "init failed"));
         }
-        c->cc->EnableSharding(rank, world);
+        // a one-rank communicator runs the sharded path too: its all-gathers
+        // and broadcasts go through RCCL (single-GPU validation)
+        c->cc->EnableSharding(rank, world, true);
     });
 }
 
@@ -811,11 +813,17 @@ int sfhe_shard_host(sfhe_ctx* c, int rank, int world, sfhe_allgather_fn ag, sfhe
     REQUIRE(c && ag && bc, "null argument");
     REQUIRE(world >= 1 && rank >= 0 && rank < world, "bad rank / world");
     REQUIRE(!c->keys.secretKey, "shard the context before sfhe_keygen");
-    REQUIRE(c->cc->ShardWorld() == 1, "context already sharded");
+    REQUIRE(!c->cc->IsSharded(), "context already sharded");
     return guard([&] {
         c->cc->EnableSharding(rank, world);
         sfp_comm_set_host(c->cc->state()->dev, rank, world, ag, bc, user);
     });
+}
+
+int sfhe_shard_tail(const sfhe_ctx* c, uint32_t* limbs) {
+    REQUIRE(c && limbs, "null argument");
+    *limbs = c->cc->ShardTailLimbs();
+    return SFHE_OK;
 }
 
 }  // extern "C"

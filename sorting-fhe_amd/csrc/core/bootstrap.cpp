@@ -197,7 +197,7 @@ void CryptoContextImpl<DCRTPoly>::EvalBootstrapSetup(std::vector<uint32_t> level
                                                      uint32_t slots, uint32_t) {
     OpLock g(st.get());
     SfheContextState* s = st.get();
-    if (s->world > 1) SFHE_THROW("bootstrapping a limb-sharded context is not supported");
+    if (s->sharded) SFHE_THROW("bootstrapping a limb-sharded context is not supported");
     if (!slots) slots = s->n / 2;
     if (slots > s->n / 2 || (slots & (slots - 1))) SFHE_THROW("EvalBootstrapSetup: slots must be a power of two <= n/2");
     if (levelBudget.size() != 2 || !levelBudget[0] || !levelBudget[1])

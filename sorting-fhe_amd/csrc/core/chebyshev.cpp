@@ -112,11 +112,13 @@ class PSEvaluator {
                     }
             std::vector<const uint64_t*> ins0, ins1;
             std::vector<double> sc;
+            std::vector<DeviceBufferPtr> keep;
             for (uint32_t j : js) {
                 const Ct& t = T[j];  // its first ellOf(L) rows; its scale is folded into the weights
-                cc->Settle(t);  // raw rows below: a lazy product's rescale first
-                ins0.push_back(t->c0);
-                ins1.push_back(t->c1);
+                const uint64_t *r0, *r1;
+                cc->RowsAt(t, L, &r0, &r1, keep);  // raw rows below: settled (and gathered into a replicated tail)
+                ins0.push_back(r0);
+                ins1.push_back(r1);
                 sc.push_back(t->scale);
             }
             for (size_t b0 = 0; b0 < kv.second.size(); b0 += 64) {
@@ -322,12 +324,14 @@ class PSEvaluator {
         if (lv < 0) return Val{true, p[0], nullptr};
         std::vector<const uint64_t*> ins0, ins1;
         std::vector<double> w, sc;
+        std::vector<DeviceBufferPtr> keep;
         for (uint32_t j = 1; j < p.size(); ++j) {
             if (p[j] == 0.0) continue;
             const Ct& t = T[j];  // unadjusted: its scale is folded into the weight
-            cc->Settle(t);  // raw pointers below: canonical rows, ordered after their writers
-            ins0.push_back(t->c0);
-            ins1.push_back(t->c1);
+            const uint64_t *r0, *r1;
+            cc->RowsAt(t, (uint32_t)lv, &r0, &r1, keep);  // raw pointers below: canonical rows, ordered after their writers
+            ins0.push_back(r0);
+            ins1.push_back(r1);
             w.push_back(p[j]);
             sc.push_back(t->scale);
         }
@@ -444,11 +448,13 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalPolyLinear(
     // weight (no level adjustment, no extra rounding)
     std::vector<const uint64_t*> i0, i1;
     std::vector<double> w, sc;
+    std::vector<DeviceBufferPtr> keep;
     for (uint32_t j = 1; j <= d; ++j) {
         if (p[j] == 0.0) continue;
-        Settle(pw[j]);  // raw rows below
-        i0.push_back(pw[j]->c0);
-        i1.push_back(pw[j]->c1);
+        const uint64_t *r0, *r1;
+        RowsAt(pw[j], lev, &r0, &r1, keep);  // raw rows below
+        i0.push_back(r0);
+        i1.push_back(r1);
         w.push_back(p[j]);
         sc.push_back(pw[j]->scale);
     }

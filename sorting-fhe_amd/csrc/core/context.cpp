@@ -351,7 +351,7 @@ class SfheInternal {
         const uint32_t ell = ctEll(s, c);
         const size_t pw = s->polyWords(c.level);
         auto out = s->alloc(2 * pw);
-        if (s->world > 1)  // the dropped row's owner broadcasts it
+        if (s->shardAt(ell))  // the dropped row's owner broadcasts it
             rescaleShard(s, out->ptr, c.c0, ell, 2, (size_t)(c.c1 - c.c0), pw);
         else
             sfp_rescale(s->dev, out->ptr, c.c0, ell, s->qInvTable[ell].data(), 2, (size_t)(c.c1 - c.c0), pw);
@@ -420,14 +420,20 @@ class SfheInternal {
         const uint64_t* x0[2];
         const uint64_t* x1[2];
         std::vector<u64> w(2 * (size_t)m.count);
+        DeviceBufferPtr gathered;  // a sharded operand read at a replicated (tail) limb count
         for (int i = 0; i < 2; ++i) {
             const Ct& c = *lz[i];
             x0[i] = c->c0;
             x1[i] = c->c1;
+            if (liftIdx[i] && s->shardAt(s->ellOf(c->level)) && !s->shardAt(ell)) {
+                gathered = gatherRows(s, c->c0, c->c1, ell);
+                x0[i] = gathered->ptr;
+                x1[i] = gathered->ptr + (size_t)ell * s->n;
+            }
             const std::vector<u64> k = liftIdx[i] ? constResidues(s, s->preScale(level) / c->scale, ell)
                                                   : std::vector<u64>(m.count, 1);
             for (uint32_t r = 0; r < m.count; ++r) {
-                const u64 q = s->primes[s->qprime(r)];
+                const u64 q = s->primes[s->qprime(r, ell)];
                 w[(size_t)i * m.count + r] = (sub && i == 1) ? (k[r] ? q - k[r] : 0) : k[r];
             }
         }
@@ -473,7 +479,7 @@ class SfheInternal {
     // residues of round(v) modulo the primes of the local rows of ell limbs
     static std::vector<u64> constResidues(SfheContextState* s, double v, uint32_t ell) {
         std::vector<u64> k(s->rows(ell));
-        for (uint32_t i = 0; i < k.size(); ++i) k[i] = residueOf(v, s->primes[s->qprime(i)]);
+        for (uint32_t i = 0; i < k.size(); ++i) k[i] = residueOf(v, s->primes[s->qprime(i, ell)]);
         return k;
     }
 
@@ -485,7 +491,7 @@ class SfheInternal {
         if (ell < 2) SFHE_THROW("no levels left to rescale (multiplicative depth exhausted)");
         Ct out = newCt(cc, level + 1, slots);
         if (c1 - c0 < 0) SFHE_THROW("internal: layout");
-        if (s->world > 1)
+        if (s->shardAt(ell))
             rescaleShard(s, out->c0, c0, ell, 2, (size_t)(c1 - c0), (size_t)(out->c1 - out->c0));
         else
             sfp_rescale(s->dev, out->c0, c0, ell, s->qInvTable[ell].data(), 2, (size_t)(c1 - c0),
@@ -510,6 +516,12 @@ class SfheInternal {
         auto k = constResidues(s, K, ell);
         s->stats.constmult++;
         s->countBytes(4.0 * ell * s->n * 8);
+        if (s->shardAt(s->ellOf(ct->level)) && !s->shardAt(ell)) {
+            // from dealt rows into the replicated tail: every row of the kept limbs first
+            auto full = gatherRows(s, ct->c0, ct->c1, ell);
+            auto v = view(cc, full, full->ptr, full->ptr + (size_t)ell * s->n, ct->level, ct->scale, ct->slots);
+            return mulRescale(cc, v, mid, k.data(), nullptr, ct->slots);
+        }
         return mulRescale(cc, ct, mid, k.data(), nullptr, ct->slots);
     }
 
@@ -530,7 +542,7 @@ class SfheInternal {
         SfheContextState* s = cc->st.get();
         const uint32_t ell = s->ellOf(level);
         if (ell < 2) SFHE_THROW("no levels left to rescale (multiplicative depth exhausted)");
-        if (!fusedRescale() || s->world > 1) {
+        if (!fusedRescale() || s->shardAt(ell)) {
             const size_t pw = s->polyWords(level);
             auto tmp = s->alloc(2 * pw);
             uint64_t* t0 = tmp->ptr;
@@ -576,15 +588,36 @@ class SfheInternal {
         return r;
     }
 
-    // coefficient-form rows of every limb of `local` (rows(ell) local rows,
-    // evaluation domain) in natural order into `nat` (ell rows)
+    // Every row of the first `ell` limbs of a ciphertext dealt over the ranks
+    // (c0 / c1: its local rows, a prefix of which are those limbs'), in
+    // natural order on every rank: 2 * ell rows, c0 then c1.  One all-gather.
+    static DeviceBufferPtr gatherRows(SfheContextState* s, const uint64_t* c0, const uint64_t* c1, uint32_t ell) {
+        const uint32_t n = s->n, lr = s->owned(ell);
+        const uint32_t per = (ell + s->world - 1) / s->world;
+        auto send = s->alloc((size_t)2 * per * n);
+        if (lr) {
+            sfp_d2d(s->dev, send->ptr, c0, (size_t)lr * n * 8);
+            sfp_d2d(s->dev, send->ptr + (size_t)per * n, c1, (size_t)lr * n * 8);
+        }
+        auto all = s->alloc((size_t)2 * per * s->world * n);
+        sfp_allgather(s->dev, send->ptr, all->ptr, (size_t)2 * per * n * 8);
+        auto full = s->alloc((size_t)2 * ell * n);
+        for (uint32_t p = 0; p < 2; ++p) {
+            auto idx = naturalOrder(s, ell, per, 2, p);
+            sfp_gather_rows(s->dev, full->ptr + (size_t)p * ell * n, all->ptr, idx.data(), ell);
+        }
+        return full;
+    }
+
+    // coefficient-form rows of every limb of `local` (this rank's dealt rows
+    // of ell limbs, evaluation domain) in natural order into `nat` (ell rows)
     static void gatherCoeff(SfheContextState* s, uint64_t* nat, const uint64_t* local, uint32_t ell) {
-        const uint32_t n = s->n, per = (ell + s->world - 1) / s->world, lr = s->rows(ell);
+        const uint32_t n = s->n, per = (ell + s->world - 1) / s->world, lr = s->owned(ell);
         auto send = s->alloc((size_t)per * n);
         auto all = s->alloc((size_t)per * s->world * n);
         if (lr) {
             sfp_d2d(s->dev, send->ptr, local, (size_t)lr * n * 8);
-            sfp_ntt(s->dev, send->ptr, s->qmap(ell), 1);
+            sfp_ntt(s->dev, send->ptr, s->shardMap(ell), 1);
         }
         sfp_allgather(s->dev, send->ptr, all->ptr, (size_t)per * n * 8);
         auto idx = naturalOrder(s, ell, per);
@@ -600,8 +633,8 @@ class SfheInternal {
         std::vector<sfp_conv*> v;
         const uint32_t beta = (ell + s->alpha - 1) / s->alpha;
         std::vector<uint32_t> dst;
-        for (uint32_t i = 0; i < s->rows(ell); ++i) dst.push_back(s->qprime(i));
-        for (uint32_t k = 0; k < s->prows(); ++k) dst.push_back(s->Lq + s->rank + k * s->world);
+        for (uint32_t i = 0; i < s->owned(ell); ++i) dst.push_back(s->qprimeShard(i));
+        for (uint32_t k = 0; k < s->owned(s->K); ++k) dst.push_back(s->Lq + s->rank + k * s->world);
         for (uint32_t j = 0; j < beta; ++j) {
             std::vector<uint32_t> src;
             for (uint32_t i = j * s->alpha; i < std::min((j + 1) * s->alpha, ell); ++i) src.push_back(i);
@@ -610,7 +643,7 @@ class SfheInternal {
         return s->modupConvShard[ell] = v;
     }
 
-    // ModUp of the local rows of d (ell limbs): beta blocks of extmap(ell) rows
+    // ModUp of the local rows of d (ell limbs, dealt): beta blocks of extmap(ell) rows
     static void modupShard(SfheContextState* s, uint64_t* ext, const uint64_t* d, uint32_t ell) {
         const uint32_t n = s->n, beta = (ell + s->alpha - 1) / s->alpha;
         const sfp_limbs em = s->extmap(ell);
@@ -633,18 +666,21 @@ class SfheInternal {
         innerShard(s, acc->ptr, ext, stride, beta, ell, key, 0);
         modDownShard(s, acc->ptr, ell, out0, out1, add0, add1);
     }
-    // the local key inner product into acc (2 polys of extmap(ell) rows), accumulated when accum
+    // The local key inner product into acc (2 polys of extmap(ell) rows),
+    // accumulated when accum.  Every rank keeps whole switching keys (they
+    // fit HBM many times over, and the replicated tail needs every row): a
+    // local ext row reads the key row of its own prime.
     static void innerShard(SfheContextState* s, uint64_t* acc, const uint64_t* ext, size_t stride, uint32_t beta,
                            uint32_t ell, const DeviceBufferPtr& key, int accum) {
         const sfp_limbs em = s->extmap(ell);
         const size_t aw = (size_t)em.count * s->n;
-        sfp_ks_inner_map(s->dev, acc, acc + aw, ext, stride, key->ptr, beta, em, s->rows(s->Lq),
-                         s->rows(s->Lq) + s->prows(), accum);
+        sfp_ks_inner_map(s->dev, acc, acc + aw, ext, stride, key->ptr, beta, em, SFP_KEY_ROW_BY_PRIME,
+                         s->Lq + s->K, accum);
     }
     // ModDown of the local accumulators (their P rows are destroyed)
     static void modDownShard(SfheContextState* s, uint64_t* acc, uint32_t ell, uint64_t* out0, uint64_t* out1,
                              int add0, int add1) {
-        const uint32_t n = s->n, K = s->K, lr = s->rows(ell), lp = s->prows();
+        const uint32_t n = s->n, K = s->K, lr = s->owned(ell), lp = s->owned(K);
         const size_t aw = (size_t)s->extmap(ell).count * n;
         // P rows: coefficient form, exchanged (both polys in one all-gather)
         const uint32_t per = (K + s->world - 1) / s->world;
@@ -666,17 +702,18 @@ class SfheInternal {
         if (!lr) return;
         // (acc_Q - NTT(Conv_centred(P rows))) * P^-1  (+ out)
         std::vector<u64> pinv(lr);
-        for (uint32_t i = 0; i < lr; ++i) pinv[i] = s->pInvModQ[s->qprime(i)];
+        for (uint32_t i = 0; i < lr; ++i) pinv[i] = s->pInvModQ[s->qprimeShard(i)];
         auto conv = s->alloc((size_t)lr * n);
         uint64_t* outs[2] = {out0, out1};
         const int adds[2] = {add0, add1};
+        const sfp_limbs qm = s->shardMap(ell);
         for (int p = 0; p < 2; ++p) {
             sfp_conv_apply_centered(s->dev, conv->ptr, natP->ptr + (size_t)p * K * n, s->moddownConvShard, lr);
-            sfp_ntt(s->dev, conv->ptr, s->qmap(ell), 0);
-            sfp_sub(s->dev, conv->ptr, acc + p * aw, conv->ptr, s->qmap(ell));
-            sfp_mul_const(s->dev, conv->ptr, conv->ptr, pinv.data(), s->qmap(ell));
+            sfp_ntt(s->dev, conv->ptr, qm, 0);
+            sfp_sub(s->dev, conv->ptr, acc + p * aw, conv->ptr, qm);
+            sfp_mul_const(s->dev, conv->ptr, conv->ptr, pinv.data(), qm);
             if (adds[p])
-                sfp_add(s->dev, outs[p], outs[p], conv->ptr, s->qmap(ell));
+                sfp_add(s->dev, outs[p], outs[p], conv->ptr, qm);
             else
                 sfp_d2d(s->dev, outs[p], conv->ptr, (size_t)lr * n * 8);
         }
@@ -694,74 +731,67 @@ class SfheInternal {
         s->countBytes((3.0 * ell + 2.0 * beta * (ell + s->K)) * s->n * 8);
     }
 
-    // rescale of npoly polys (local rows of ell limbs) by q_{ell-1}: its owner
-    // broadcasts the dropped row in coefficient form
+    // Rescale of npoly polys (this rank's dealt rows of ell limbs) by
+    // q_{ell-1}: its owner broadcasts the dropped row in coefficient form.
+    // When ell - 1 limbs fall in the replicated tail every rank then gathers
+    // every row of the result (out: ell - 1 rows per poly).
     static void rescaleShard(SfheContextState* s, uint64_t* out, const uint64_t* in, uint32_t ell, uint32_t npoly,
                              size_t inStride, size_t outStride) {
         const uint32_t n = s->n, drop = ell - 1, owner = drop % s->world;
         auto last = s->alloc((size_t)npoly * n);
         if ((uint32_t)s->rank == owner) {
-            const uint32_t lr = s->rows(ell);
+            const uint32_t lr = s->owned(ell);
             for (uint32_t p = 0; p < npoly; ++p)
                 sfp_d2d(s->dev, last->ptr + (size_t)p * n, in + p * inStride + (size_t)(lr - 1) * n, (size_t)n * 8);
             for (uint32_t p = 0; p < npoly; ++p)
                 sfp_ntt(s->dev, last->ptr + (size_t)p * n, sfp_limbs{1, 1, 0, drop, 1}, 1);
         }
         sfp_bcast(s->dev, last->ptr, (size_t)npoly * n * 8, (int)owner);
-        const uint32_t lo = s->rows(ell - 1);
+        const uint32_t lo = s->owned(ell - 1);
         std::vector<u64> qlinv(lo);
-        for (uint32_t i = 0; i < lo; ++i) qlinv[i] = s->qInvTable[ell][s->qprime(i)];
-        sfp_rescale_rows(s->dev, out, in, last->ptr, drop, s->qmap(ell - 1), qlinv.data(), npoly, inStride,
-                         outStride, n);
+        for (uint32_t i = 0; i < lo; ++i) qlinv[i] = s->qInvTable[ell][s->qprimeShard(i)];
+        if (s->shardAt(ell - 1)) {
+            sfp_rescale_rows(s->dev, out, in, last->ptr, drop, s->shardMap(ell - 1), qlinv.data(), npoly, inStride,
+                             outStride, n);
+            return;
+        }
+        // into the replicated tail: this rank's rows of the result, then an all-gather
+        const uint32_t per = (ell - 1 + s->world - 1) / s->world;
+        auto mine = s->alloc((size_t)npoly * per * n);
+        sfp_rescale_rows(s->dev, mine->ptr, in, last->ptr, drop, s->shardMap(ell - 1), qlinv.data(), npoly, inStride,
+                         (size_t)per * n, n);
+        auto all = s->alloc((size_t)npoly * per * s->world * n);
+        sfp_allgather(s->dev, mine->ptr, all->ptr, (size_t)npoly * per * n * 8);
+        for (uint32_t p = 0; p < npoly; ++p) {
+            auto idx = naturalOrder(s, ell - 1, per, npoly, p);
+            sfp_gather_rows(s->dev, out + p * outStride, all->ptr, idx.data(), ell - 1);
+        }
     }
 
     // this rank's rows of a ciphertext computed on every row (FullScope)
     static Ct localize(CC* cc, const Ct& full) {
         SfheContextState* s = cc->st.get();
-        if (s->world == 1) return full;
-        const uint32_t ell = s->ellOf(full->level), lr = s->rows(ell);
+        const uint32_t ell = s->ellOf(full->level);
+        if (!s->shardAt(ell)) return full;
+        const uint32_t lr = s->rows(ell);
         Ct out = newCt(cc, full->level, full->slots);
         out->scale = full->scale;
         std::vector<uint32_t> idx(lr);
-        for (uint32_t i = 0; i < lr; ++i) idx[i] = s->qprime(i);
+        for (uint32_t i = 0; i < lr; ++i) idx[i] = s->qprimeShard(i);
         sfp_gather_rows(s->dev, out->c0, full->c0, idx.data(), lr);
         sfp_gather_rows(s->dev, out->c1, full->c1, idx.data(), lr);
         return out;
     }
 
-    // every row of a sharded ciphertext, in natural order (2 * ell rows:
-    // c0 then c1), on every rank
+    // every row of a ciphertext in natural order (2 * ell rows: c0 then c1),
+    // on every rank (a collective when its rows are dealt)
     static DeviceBufferPtr gatherFull(SfheContextState* s, const Ct& a) {
-        const uint32_t n = s->n, ell = s->ellOf(a->level), lr = s->rows(ell);
-        const uint32_t per = (ell + s->world - 1) / s->world;
-        auto send = s->alloc((size_t)2 * per * n);
-        if (lr) {
-            sfp_d2d(s->dev, send->ptr, a->c0, (size_t)lr * n * 8);
-            sfp_d2d(s->dev, send->ptr + (size_t)per * n, a->c1, (size_t)lr * n * 8);
-        }
-        auto all = s->alloc((size_t)2 * per * s->world * n);
-        sfp_allgather(s->dev, send->ptr, all->ptr, (size_t)2 * per * n * 8);
-        auto full = s->alloc((size_t)2 * ell * n);
-        for (uint32_t p = 0; p < 2; ++p) {
-            auto idx = naturalOrder(s, ell, per, 2, p);
-            sfp_gather_rows(s->dev, full->ptr + (size_t)p * ell * n, all->ptr, idx.data(), ell);
-        }
+        const uint32_t ell = s->ellOf(a->level);
+        if (s->shardAt(ell)) return gatherRows(s, a->c0, a->c1, ell);
+        auto full = s->alloc((size_t)2 * ell * s->n);
+        sfp_d2d(s->dev, full->ptr, a->c0, (size_t)ell * s->n * 8);
+        sfp_d2d(s->dev, full->ptr + (size_t)ell * s->n, a->c1, (size_t)ell * s->n * 8);
         return full;
-    }
-
-    // this rank's rows of a switching key built on every row: per digit,
-    // [b rows][a rows] of (local Q rows, local P rows)
-    static DeviceBufferPtr localizeKey(SfheContextState* s, const DeviceBufferPtr& full) {
-        if (s->world == 1) return full;
-        const uint32_t n = s->n, NP = s->Lq + s->K, lq = s->rows(s->Lq), lp = s->prows();
-        std::vector<uint32_t> idx;
-        for (uint32_t i = 0; i < lq; ++i) idx.push_back(s->qprime(i));
-        for (uint32_t k = 0; k < lp; ++k) idx.push_back(s->Lq + s->rank + k * s->world);
-        const uint32_t R = lq + lp;
-        auto key = s->alloc((size_t)s->dnum * 2 * R * n);
-        for (uint32_t h = 0; h < 2 * s->dnum; ++h)
-            sfp_gather_rows(s->dev, key->ptr + (size_t)h * R * n, full->ptr + (size_t)h * NP * n, idx.data(), R);
-        return key;
     }
 
     // Hybrid key switch of d (ell limbs, evaluation domain) with `key`; the
@@ -769,7 +799,7 @@ class SfheInternal {
     static void keySwitch(CC* cc, const uint64_t* d, uint32_t ell, const DeviceBufferPtr& key,
                           uint64_t* out0, uint64_t* out1, int add0, int add1) {
         SfheContextState* s = cc->st.get();
-        if (s->world > 1) return keySwitchShard(cc, d, ell, key, out0, out1, add0, add1);
+        if (s->shardAt(ell)) return keySwitchShard(cc, d, ell, key, out0, out1, add0, add1);
         const uint32_t n = s->n, K = s->K;
         const uint32_t beta = (ell + s->alpha - 1) / s->alpha;
         const size_t stride = (size_t)(ell + K) * n;
@@ -791,7 +821,7 @@ class SfheInternal {
         SfheContextState* s = cc->st.get();
         const uint32_t ell = s->ellOf(level);
         if (ell < 2) SFHE_THROW("no levels left to rescale (multiplicative depth exhausted)");
-        if (s->world > 1) {
+        if (s->shardAt(ell)) {
             keySwitchShard(cc, d2, ell, s->relinKey, d0, d1, 1, 1);
             return rescale(cc, d0, d1, level, slots);
         }
@@ -823,7 +853,7 @@ class SfheInternal {
                                 uint32_t ell, const DeviceBufferPtr& key, uint64_t* out0,
                                 uint64_t* out1, int add0, int add1) {
         SfheContextState* s = cc->st.get();
-        if (s->world > 1) return innerModDownShard(s, ext, stride, beta, ell, key, out0, out1, add0, add1);
+        if (s->shardAt(ell)) return innerModDownShard(s, ext, stride, beta, ell, key, out0, out1, add0, add1);
         const uint32_t n = s->n, K = s->K;
         const size_t accStride = (size_t)(ell + K) * n;
         auto acc = s->alloc(2 * accStride);
@@ -883,13 +913,9 @@ class SfheInternal {
     // switching key from s' (device, Lq+K limbs, eval domain) to s
     static DeviceBufferPtr genSwitchKey(CC* cc, const uint64_t* sPrime, const uint64_t* sk) {
         SfheContextState* s = cc->st.get();
-        if (s->world > 1) {
-            DeviceBufferPtr full;
-            {
-                FullScope fs(s);
-                full = genSwitchKey(cc, sPrime, sk);
-            }
-            return localizeKey(s, full);
+        if (s->sharded) {  // every rank builds (and keeps) the whole key: same seed, same words
+            FullScope fs(s);
+            return genSwitchKey(cc, sPrime, sk);
         }
         const uint32_t n = s->n, NP = s->Lq + s->K;
         const sfp_limbs all{NP, NP, 0};
@@ -1056,7 +1082,7 @@ class SfheInternal {
     // (evaluation domain), cached on the plaintext beside its q-row encodings
     static const uint64_t* encodedExt(CC* cc, const Plaintext& pt, uint32_t level) {
         SfheContextState* s = cc->st.get();
-        if (s->world > 1) SFHE_THROW("internal: extended-basis encodings are unsharded");
+        if (s->shardAt(s->ellOf(level))) SFHE_THROW("internal: extended-basis encodings are unsharded");
         std::lock_guard<std::mutex> g(pt->encMutex);
         const uint32_t key = level | 0x40000000u;
         auto stale = [&](const DeviceBufferPtr& b) { return b->capEpoch && s->abandonedEpochs.count(b->capEpoch); };
@@ -1467,7 +1493,7 @@ void CryptoContextImpl<DCRTPoly>::Synchronize() {
 }
 
 // a sharded context issues its collectives in program order on one lane
-int CryptoContextImpl<DCRTPoly>::LaneCount() const { return st->world > 1 ? 1 : sfp_lanes(st->dev); }
+int CryptoContextImpl<DCRTPoly>::LaneCount() const { return st->sharded ? 1 : sfp_lanes(st->dev); }
 
 void CryptoContextImpl<DCRTPoly>::ForkLanes(int count) {
     OpLock g(st.get());
@@ -1672,7 +1698,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::Encrypt(const PublicKey<DCRTPo
     OpLock g(st.get());
     SfheContextState* s = st.get();
     if (!pk) SFHE_THROW("null public key");
-    if (s->world > 1) {  // encrypt every row, keep this rank's
+    if (s->sharded) {  // encrypt every row, keep this rank's
         Ciphertext<DCRTPoly> full;
         {
             FullScope fs(s);
@@ -1732,7 +1758,7 @@ void CryptoContextImpl<DCRTPoly>::Decrypt(const PrivateKey<DCRTPoly>& sk,
     SfheInternal::deps(st.get(), {&ct});
     SfheContextState* s = st.get();
     if (!sk) SFHE_THROW("null secret key");
-    if (s->world > 1) {  // every rank gathers the rows and decrypts
+    if (s->sharded) {  // every rank gathers the rows and decrypts
         auto full = SfheInternal::gatherFull(s, ct);
         FullScope fs(s);
         auto fc = std::make_shared<CiphertextImpl<DCRTPoly>>(*ct);
@@ -2234,7 +2260,7 @@ std::shared_ptr<FastRotationPrecomp> CryptoContextImpl<DCRTPoly>::EvalFastRotati
         pre->pinBuf = a->buf;
         pre->pinC0 = a->c0;
     }
-    if (s->world > 1) {
+    if (s->shardAt(ell)) {
         pre->stride = (size_t)s->extmap(ell).count * s->n;
         pre->ext = s->alloc(pre->stride * pre->beta);
         SfheInternal::modupShard(s, pre->ext->ptr, a->c1, ell);
@@ -2334,7 +2360,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotateSum(const std::vecto
     }
     const uint32_t level = a[rot[0]]->level, ell = SfheInternal::ctEll(s, *a[rot[0]]);
     const uint32_t n = s->n, K = s->K, beta = (ell + s->alpha - 1) / s->alpha;
-    const bool shard = s->world > 1;  // local rows; the exchanges inside modupShard / modDownShard
+    const bool shard = s->shardAt(ell);  // local rows; the exchanges inside modupShard / modDownShard
     const size_t stride = (size_t)(shard ? s->extmap(ell).count : ell + K) * n;
     auto out = pend ? SfheInternal::newPendingCt(this, level, slots) : SfheInternal::newCt(this, level, slots);
     auto t = s->alloc((size_t)s->rows(ell) * n);
@@ -2386,7 +2412,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotMultAddHoisted(
     OpLock g(st.get());
     SfheContextState* s = st.get();
     if (a.empty() || a.size() != terms.size()) SFHE_THROW("EvalRotMultAddHoisted: operand count mismatch");
-    if (s->world > 1) SFHE_THROW("EvalRotMultAddHoisted: sharded contexts are not supported");
+    if (s->sharded) SFHE_THROW("EvalRotMultAddHoisted: sharded contexts are not supported");
     SfheInternal::depsv(s, a);
     const uint32_t level = a[0]->level;
     uint32_t slots = 0;
@@ -2495,7 +2521,7 @@ void weightResidues(const SfheContextState* s, double w, uint32_t level, uint32_
         v = ((u128)(u64)hi << 64) + (u128)(u64)(a - std::ldexp(hi, 64));
     }
     for (uint32_t i = 0; i < s->rows(ell); ++i) {  // the local rows' primes
-        const u64 q = s->primes[s->qprime(i)];
+        const u64 q = s->primes[s->qprime(i, ell)];
         const u64 m = (u64)(v % q);
         kk.push_back(neg ? (m ? q - m : 0) : m);
     }
@@ -2525,7 +2551,7 @@ std::vector<Ciphertext<DCRTPoly>> CryptoContextImpl<DCRTPoly>::LinearWSumRescale
     // one rescale of all 2 * nout polynomials; the results share one buffer
     const size_t qw = s->polyWords(level + 1);
     auto res = s->alloc((size_t)nout * 2 * qw);
-    if (s->world > 1)
+    if (s->shardAt(ell))
         SfheInternal::rescaleShard(s, res->ptr, sums->ptr, ell, 2 * nout, pw, qw);
     else
         sfp_rescale(s->dev, res->ptr, sums->ptr, ell, s->qInvTable[ell].data(), 2 * nout, pw, qw);
@@ -2628,7 +2654,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::ModRaise(const Ciphertext<DCRT
     OpLock g(st.get());
     SfheInternal::deps(st.get(), {&a});
     SfheContextState* s = st.get();
-    if (s->world > 1) SFHE_THROW("bootstrapping a limb-sharded context is not supported");
+    if (s->sharded) SFHE_THROW("bootstrapping a limb-sharded context is not supported");
     if (s->ellOf(a->level) != 1) SFHE_THROW("ModRaise needs a ciphertext at the last level (one limb)");
     const uint32_t n = s->n;
     // coefficient form of both single-limb polys, then their centred lift to
@@ -2683,33 +2709,59 @@ void CryptoContextImpl<DCRTPoly>::EvalConjugateKeyGen(const PrivateKey<DCRTPoly>
 // ============================================================================
 // limb sharding
 
-void CryptoContextImpl<DCRTPoly>::EnableSharding(int rank, int world) {
+void CryptoContextImpl<DCRTPoly>::EnableSharding(int rank, int world, bool shardAtOne) {
     OpLock g(st.get());
     SfheContextState* s = st.get();
     if (world < 1 || rank < 0 || rank >= world) SFHE_THROW("EnableSharding: bad rank / world");
     if (s->relinKey || !s->rotKeys.empty()) SFHE_THROW("EnableSharding must precede the key generation");
-    if (s->world > 1) SFHE_THROW("EnableSharding: already sharded");
+    if (s->sharded) SFHE_THROW("EnableSharding: already sharded");
     s->rank = rank;
     s->world = world;
     s->ptCache.clear();
     s->ptCacheBytes = 0;
-    if (world == 1) return;
+    if (world == 1 && !shardAtOne) return;
+    s->sharded = true;
+    // replicated tail: levels of at most SFHE_SHARD_TAIL Q limbs (default 16)
+    // run on every rank without exchanges
+    const char* t = std::getenv("SFHE_SHARD_TAIL");
+    s->tailLimbs = t && *t ? (uint32_t)std::atoi(t) : 16u;
     // P -> this rank's Q rows (targets in local row order; a level's rows are a prefix)
     std::vector<uint32_t> src, dst;
     for (uint32_t k = 0; k < s->K; ++k) src.push_back(s->Lq + k);
-    for (uint32_t i = 0; i < s->rows(s->Lq); ++i) dst.push_back(s->qprime(i));
+    for (uint32_t i = 0; i < s->owned(s->Lq); ++i) dst.push_back(s->qprimeShard(i));
     s->moddownConvShard = dst.empty() ? nullptr : SfheInternal::makeConv(s, src, dst);
 }
 
+uint32_t CryptoContextImpl<DCRTPoly>::ShardTailLimbs() const { return st->sharded ? st->tailLimbs : 0; }
+
 int CryptoContextImpl<DCRTPoly>::ShardRank() const { return st->rank; }
 int CryptoContextImpl<DCRTPoly>::ShardWorld() const { return st->world; }
+bool CryptoContextImpl<DCRTPoly>::IsSharded() const { return st->sharded; }
+
+void CryptoContextImpl<DCRTPoly>::RowsAt(const Ciphertext<DCRTPoly>& ct, uint32_t level, const uint64_t** c0,
+                                         const uint64_t** c1, std::vector<DeviceBufferPtr>& keep) {
+    OpLock g(st.get());
+    SfheContextState* s = st.get();
+    SfheInternal::deps(s, {&ct});
+    const uint32_t ell = s->ellOf(level);
+    if (level < ct->level) SFHE_THROW("RowsAt: a ciphertext's rows cannot be read at a higher limb count");
+    if (s->shardAt(s->ellOf(ct->level)) && !s->shardAt(ell)) {
+        auto full = SfheInternal::gatherRows(s, ct->c0, ct->c1, ell);
+        *c0 = full->ptr;
+        *c1 = full->ptr + (size_t)ell * s->n;
+        keep.push_back(std::move(full));
+        return;
+    }
+    *c0 = ct->c0;
+    *c1 = ct->c1;
+}
 
 void CryptoContextImpl<DCRTPoly>::DownloadRows(const Ciphertext<DCRTPoly>& ct, uint64_t* out) {
     OpLock g(st.get());
     SfheInternal::deps(st.get(), {&ct});
     SfheContextState* s = st.get();
     const size_t words = (size_t)s->ellOf(ct->level) * s->n;
-    if (s->world > 1) {  // collective: every rank receives every row
+    if (s->sharded) {  // collective: every rank receives every row
         auto full = SfheInternal::gatherFull(s, ct);
         sfp_d2h(s->dev, out, full->ptr, 2 * words * 8);
     } else {
@@ -2751,7 +2803,8 @@ bool CryptoContextImpl<DCRTPoly>::BeginCapture() {
     SfheContextState* s = st.get();
     if (s->capturing) SFHE_THROW("BeginCapture: a capture is already open");
     if (s->forkedLanes) SFHE_THROW("BeginCapture inside a lane region");
-    if (s->world > 1) return false;  // collectives stay eager (host transports synchronise)
+    // a host transport synchronises (no capture); RCCL collectives are captured
+    if (s->sharded && !sfp_comm_capturable(s->dev)) return false;
     sfp_sync(s->dev);
     if (sfp_capture_begin(s->dev) != 0) {
         std::fprintf(stderr, "sfhe: this backend cannot capture graphs (%s); sorting eagerly\n", sfp_backend_name());

@@ -475,12 +475,24 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
     // read on other lanes only after the join.
     int LaneCount() const;
     // Limb sharding (engine extension): this process holds the
-    // RNS limbs i with i % world == rank of every ciphertext and key; call
-    // before key generation, with the device communicator set up (C ABI
-    // sfhe_comm_*).  Results are bit-identical to the unsharded context.
-    void EnableSharding(int rank, int world);
+    // RNS limbs i with i % world == rank of every ciphertext; levels with at
+    // most ShardTailLimbs() limbs run replicated on every rank (SFHE_SHARD_TAIL,
+    // default 16); every rank keeps whole switching keys.  Call before key
+    // generation, with the device communicator set up (C ABI sfhe_comm_*).
+    // shardAtOne: a one-rank communicator still takes the sharded code path
+    // (single-GPU validation of the exchanges).  Results are bit-identical
+    // to the unsharded context.
+    void EnableSharding(int rank, int world, bool shardAtOne = false);
     int ShardRank() const;
     int ShardWorld() const;
+    bool IsSharded() const;
+    uint32_t ShardTailLimbs() const;
+    // Engine internal (raw-row consumers: the weighted sums): ct's (c0, c1)
+    // rows, Settle()d, as valid at `level`'s limb count -- gathered into a
+    // buffer appended to `keep` when ct's rows are dealt over the ranks but
+    // that count falls in the replicated tail.
+    void RowsAt(const Ciphertext<DCRTPoly>& ct, uint32_t level, const uint64_t** c0, const uint64_t** c1,
+                std::vector<DeviceBufferPtr>& keep);
     // raw residues [c0 rows][c1 rows] of every limb, natural order (collective when sharded)
     void DownloadRows(const Ciphertext<DCRTPoly>& ct, uint64_t* out);
     void ForkLanes(int count);

@@ -100,7 +100,7 @@ bool binaryOnly(SerType::Kind k) {
 
 SfheContextState* unsharded(const CryptoContext<DCRTPoly>& cc) {
     SfheContextState* s = cc->state();
-    if (s->world > 1) SFHE_THROW("serialization of a limb-sharded context is not supported");
+    if (s->sharded) SFHE_THROW("serialization of a limb-sharded context is not supported");
     return s;
 }
 

@@ -137,10 +137,17 @@ struct SfheContextState {
 
     // limb sharding (one process per GPU): this rank holds Q limb i and P
     // limb k iff i % world == rank / k % world == rank, in increasing order,
-    // so a ciphertext's local rows at any level are a prefix of its rows at
-    // level 0 and rescaling drops at most the last local row.
+    // so a ciphertext's local rows at any sharded level are a prefix of its
+    // rows at level 0 and rescaling drops at most the last local row.
+    // Tail replication: at levels with at most tailLimbs Q limbs every rank
+    // holds and computes every row (no exchanges).  The
+    // representation of a row set is a function of its limb count alone.
+    // sharded is also set by a one-rank RCCL communicator: the sharded code
+    // path (exchanges through RCCL) at W = 1, for single-GPU validation.
     int rank = 0, world = 1;
-    bool fullScope = false;  // inside FullScope: world/rank read 1/0 (setup work on every row)
+    bool sharded = false;
+    uint32_t tailLimbs = 0;
+    bool fullScope = false;  // inside FullScope: unsharded (setup work on every row)
     std::vector<DeviceBufferPtr> scopeKeep;  // uncached encodings alive until the scope ends
     std::map<uint32_t, std::vector<sfp_conv*>> modupConvShard;  // ell -> per digit (owned targets)
     sfp_conv* moddownConvShard = nullptr;                        // P -> owned Q rows
@@ -155,15 +162,22 @@ struct SfheContextState {
     uint32_t owned(uint32_t count) const {
         return (uint32_t)rank < count ? (count - rank + world - 1) / world : 0;
     }
-    uint32_t rows(uint32_t ell) const { return owned(ell); }  // local Q rows at ell limbs
-    uint32_t prows() const { return owned(K); }                // local P rows
-    uint32_t qprime(uint32_t i) const { return rank + i * world; }  // prime of local Q row i
-    sfp_limbs qmap(uint32_t ell) const {
-        return sfp_limbs{rows(ell), rows(ell), 0, (uint32_t)rank, (uint32_t)world};
+    // rows of ell limbs are dealt over the ranks (else every rank holds all)
+    bool shardAt(uint32_t ell) const { return sharded && ell > tailLimbs; }
+    uint32_t rows(uint32_t ell) const { return shardAt(ell) ? owned(ell) : ell; }  // local Q rows at ell limbs
+    uint32_t prows(uint32_t ell) const { return shardAt(ell) ? owned(K) : K; }     // local P rows beside them
+    // prime of local Q row i at ell limbs
+    uint32_t qprime(uint32_t i, uint32_t ell) const { return shardAt(ell) ? rank + i * world : i; }
+    uint32_t qprimeShard(uint32_t i) const { return rank + i * world; }
+    sfp_limbs shardMap(uint32_t ell) const {  // this rank's dealt rows of ell limbs
+        return sfp_limbs{owned(ell), owned(ell), 0, (uint32_t)rank, (uint32_t)world};
     }
+    sfp_limbs qmap(uint32_t ell) const { return shardAt(ell) ? shardMap(ell) : sfp_limbs{ell, ell, 0, 0, 1}; }
     // local ext rows: the Q rows of ell limbs, then the P rows
     sfp_limbs extmap(uint32_t ell) const {
-        return sfp_limbs{rows(ell) + prows(), rows(ell), Lq + (uint32_t)rank, (uint32_t)rank, (uint32_t)world};
+        return shardAt(ell) ? sfp_limbs{owned(ell) + owned(K), owned(ell), Lq + (uint32_t)rank, (uint32_t)rank,
+                                        (uint32_t)world}
+                            : sfp_limbs{ell + K, ell, Lq, 0, 1};
     }
     size_t polyWords(uint32_t level) const { return (size_t)rows(ellOf(level)) * n; }
     uint64_t nextSeed() { return seed ^ (0x9E3779B97F4A7C15ULL * (seedCounter++)); }
@@ -177,14 +191,17 @@ struct SfheContextState {
 // rows, and plaintext encodings are not cached (they would have the full rows).
 class FullScope {
   public:
-    explicit FullScope(SfheContextState* s) : s_(s), rank_(s->rank), world_(s->world), was_(s->fullScope) {
+    explicit FullScope(SfheContextState* s)
+        : s_(s), rank_(s->rank), world_(s->world), sharded_(s->sharded), was_(s->fullScope) {
         s->rank = 0;
         s->world = 1;
+        s->sharded = false;
         s->fullScope = true;
     }
     ~FullScope() {
         s_->rank = rank_;
         s_->world = world_;
+        s_->sharded = sharded_;
         s_->fullScope = was_;
         if (!was_) s_->scopeKeep.clear();  // later users of the blocks are stream-ordered after
     }
@@ -192,7 +209,7 @@ class FullScope {
   private:
     SfheContextState* s_;
     int rank_, world_;
-    bool was_;
+    bool sharded_, was_;
 };
 
 // Serialises host-side use of a context and routes the calling thread's

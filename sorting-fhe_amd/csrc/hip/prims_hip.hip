@@ -1880,7 +1880,8 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
 
 // key inner product over ext rows t < ell+K
 // ext row t (prime primeOf(pm, t)) uses key row t < pm.split ? t : keyQ +
-// (t - pm.split) of each digit's [b rows][a rows] block of keyRows rows.
+// (t - pm.split) of each digit's [b rows][a rows] block of keyRows rows, or
+// the row of its prime when keyQ == SFP_KEY_ROW_BY_PRIME (a whole key).
 __global__ __launch_bounds__(kThreads) void k_ks_inner(u64* __restrict__ acc0, u64* __restrict__ acc1,
                                                        const u64* __restrict__ ext, size_t extStride,
                                                        const u64* __restrict__ key, uint32_t beta,
@@ -1898,8 +1899,9 @@ __global__ __launch_bounds__(kThreads) void k_ks_inner(u64* __restrict__ acc0, u
         const size_t e = 2 * i;
         const uint32_t t = (uint32_t)(e >> logn);
         const uint32_t x = (uint32_t)(e & (n - 1));
-        const uint32_t kr = t < ell ? t : keyQ + (t - ell);
-        const sf_barrett B = loadBar(bar, primeOf(pm, t));
+        const uint32_t pr = primeOf(pm, t);
+        const uint32_t kr = keyQ == SFP_KEY_ROW_BY_PRIME ? pr : (t < ell ? t : keyQ + (t - ell));
+        const sf_barrett B = loadBar(bar, pr);
         Acc s0{0, 0}, s0b{0, 0}, s1{0, 0}, s1b{0, 0};
         for (uint32_t j = 0; j < beta; ++j) {
             const ulonglong2 ev = *reinterpret_cast<const ulonglong2*>(ext + j * extStride + e);
@@ -3518,8 +3520,10 @@ static void ncclCheck(sfp_dev* d, const char* what, ncclResult_t r) {
     if (d->err.empty()) d->err = std::string(what) + ": " + rcclApi().errorString(r);
 }
 
+int sfp_comm_capturable(sfp_dev* d) { return d->nccl || !d->hostAg ? 1 : 0; }
+
 void sfp_allgather(sfp_dev* d, const void* send, void* recv, size_t bytes) {
-    if (d->world == 1) {
+    if (d->world == 1 && !d->nccl) {
         if (send != recv) sfp_d2d(d, recv, send, bytes);
         return;
     }
@@ -3538,7 +3542,7 @@ void sfp_allgather(sfp_dev* d, const void* send, void* recv, size_t bytes) {
 }
 
 void sfp_bcast(sfp_dev* d, void* buf, size_t bytes, int root) {
-    if (d->world == 1) return;
+    if (d->world == 1 && !d->nccl) return;
     if (d->nccl) {
         ncclCheck(d, "ncclBroadcast", rcclApi().broadcast(buf, buf, bytes, ncclUint8, root, d->nccl, d->st()));
         return;

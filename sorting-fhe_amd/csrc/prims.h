@@ -272,6 +272,9 @@ int sfp_comm_uid(void* uid128);
 int sfp_comm_init_rccl(sfp_dev* d, int rank, int world, const void* uid128);
 void sfp_comm_set_host(sfp_dev* d, int rank, int world, sfp_host_allgather_fn ag, sfp_host_bcast_fn bc,
                        void* user);
+// 1 when the collectives can be recorded into a graph (RCCL, or no
+// communicator at all); 0 for a host transport (it synchronises)
+int sfp_comm_capturable(sfp_dev* d);
 // recv = world blocks of `bytes`, rank-major (recv may contain send in place)
 void sfp_allgather(sfp_dev* d, const void* send, void* recv, size_t bytes);
 void sfp_bcast(sfp_dev* d, void* buf, size_t bytes, int root);
@@ -290,8 +293,10 @@ void sfp_rescale_rows(sfp_dev* d, uint64_t* out, const uint64_t* in, const uint6
 // Key inner product with explicit maps (limb sharding): ext rows follow the
 // prime map pm (pm.split Q rows then P rows); ext row t uses key row
 // t < pm.split ? t : keyQ + (t - pm.split) of each digit's [b rows][a rows]
-// block of key_rows rows.
+// block of key_rows rows -- or, with keyQ == SFP_KEY_ROW_BY_PRIME, the key row
+// of its prime (a whole key, key_rows = Lq + K: row r is prime r).
 //   accum: acc (+)= the inner product (as sfp_ks_inner_acc)
+#define SFP_KEY_ROW_BY_PRIME 0xFFFFFFFFu
 void sfp_ks_inner_map(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
                       size_t ext_stride, const uint64_t* key, uint32_t beta, sfp_limbs pm,
                       uint32_t keyQ, uint32_t key_rows, int accum);

@@ -41,7 +41,7 @@ ABI_SYMBOLS = [
     "sfhe_bootstrap_setup", "sfhe_bootstrap_depth", "sfhe_bootstrap",
     "sfhe_sorter_sort_bitonic", "sfhe_kway_sort", "sfhe_kway_params",
     "sfhe_save", "sfhe_load", "sfhe_ct_save", "sfhe_ct_load",
-    "sfhe_kway_create", "sfhe_kway_run", "sfhe_kway_destroy",
+    "sfhe_kway_create", "sfhe_kway_run", "sfhe_kway_destroy", "sfhe_shard_tail",
 ]
 
 
@@ -147,6 +147,7 @@ _SIGS = {
     "sfhe_pool_bytes": (C.c_int, [_VP, _PU64]),
     "sfhe_shard_rccl": (C.c_int, [_VP, C.c_int, C.c_int, _VP]),
     "sfhe_shard_host": (C.c_int, [_VP, C.c_int, C.c_int, _AG, _BC, _VP]),
+    "sfhe_shard_tail": (C.c_int, [_VP, _PU32]),
 }
 
 _libs: dict = {}
@@ -274,6 +275,12 @@ class Engine:
         bc = _BC(lambda _u, buf, nb, root: comm.bcast(rank, buf, nb, root))
         self._chk(self.lib.sfhe_shard_host(self.ctx, rank, world, ag, bc, None))
         self._comm_refs = (ag, bc, comm)  # the library keeps the raw pointers
+
+    def shard_tail(self) -> int:
+        """Replicated-tail limb count of a sharded context (0: unsharded)."""
+        v = C.c_uint32()
+        self._chk(self.lib.sfhe_shard_tail(self.ctx, C.byref(v)))
+        return v.value
 
     # -- context --
     def rotate_keygen(self, idx: Sequence[int]):

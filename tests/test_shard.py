@@ -68,8 +68,13 @@ def compare(ref, got):
         assert bad == 0, f"{k}: {bad} of {v.size} values differ"
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_ops_bitexact_oracle(oracle_lib, world):
+@pytest.mark.parametrize("world,tail", [(2, 0), (3, 0), (2, 3), (3, 4), (3, 16)])
+def test_sharded_ops_bitexact_oracle(oracle_lib, world, tail, monkeypatch):
+    """tail: SFHE_SHARD_TAIL, the limb count at and below which every rank
+    holds every row (0: dealt at every level; 3 / 4: the program crosses into
+    the replicated tail -- rescales, level adjustments, lifts and weighted-sum
+    inputs gathered there; 16: replicated throughout)."""
+    monkeypatch.setenv("SFHE_SHARD_TAIL", str(tail))
     ref = ops_program(sfhe.Engine("oracle", **OPS_KW))
     assert ref["levels"].max() == OPS_KW["mult_depth"]  # "deep" reached the last level
     outs = sfhe.run_sharded_threads("oracle", world, ops_program, **OPS_KW)
@@ -77,11 +82,11 @@ def test_sharded_ops_bitexact_oracle(oracle_lib, world):
         compare(ref, outs[r])
 
 
-@pytest.mark.parametrize("N,logn,world", [(8, 12, 2), (64, 13, 2), (64, 13, 3), (64, 13, 4)])
+@pytest.mark.parametrize("N,logn,world", [(8, 12, 2), (64, 13, 2), (64, 13, 3), (64, 13, 4), (8, 12, 8)])
 def test_sharded_sort_bitexact_oracle(oracle_lib, N, logn, world):
-    """Whole DirectSort<N> limb-sharded over W thread ranks.  At W = 3, 4 the
-    sort's last levels hold fewer limbs than ranks (ranks without a limb
-    idle through those ops and still receive every broadcast)."""
+    """Whole DirectSort<N> limb-sharded over W thread ranks (the default
+    replicated tail of 16 limbs: the rank's first levels are dealt, the
+    placement replicated).  W = 8: 3-4 dealt rows per rank above the tail."""
     depth, rots = sfhe.direct_sort_params(N, "oracle")
     kw = dict(mult_depth=depth, ring_dim=1 << logn, batch_size=N, rotations=rots, seed=777)
     ref = sort_program(sfhe.Engine("oracle", **kw), N)
@@ -128,7 +133,8 @@ def test_sharded_ops_gloo_two_processes(oracle_lib, tmp_path):
     path = str(tmp_path / "rank")
     code = GLOO_SCRIPT.format(py=os.path.join(ROOT, "sorting-fhe_amd", "python"), root=ROOT,
                               tests=os.path.join(ROOT, "tests"), port=port, path=path)
-    env = dict(os.environ, OMP_NUM_THREADS="4")
+    # dealt rows above 3 limbs, the replicated tail below: both across processes
+    env = dict(os.environ, OMP_NUM_THREADS="4", SFHE_SHARD_TAIL="3")
     procs = [subprocess.Popen([sys.executable, "-c", code, str(r)], env=env) for r in range(2)]
     try:
         for p in procs:
