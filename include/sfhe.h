@@ -90,6 +90,9 @@ int sfhe_sync(sfhe_ctx* c);
 /* counts[9]: keyswitch, rescale, tensor, ptmult, constmult, add, automorph,
  * ntt_limbs, wsum_terms; bytes: algorithmic HBM bytes (SURVEY §8(d) model). */
 int sfhe_op_stats(sfhe_ctx* c, uint64_t* counts, double* bytes, int reset);
+/* Plaintext encodings done on the device (sfp_encode) and on the host since
+ * the last sfhe_op_stats reset. */
+int sfhe_encode_counts(sfhe_ctx* c, uint64_t* device, uint64_t* host);
 /* Device memory held by the context's buffer pool (live and free blocks). */
 int sfhe_pool_bytes(sfhe_ctx* c, uint64_t* bytes);
 /* Live kernel timing (bench roofline; no reference counterpart): kernel

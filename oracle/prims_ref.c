@@ -45,6 +45,9 @@ struct sfp_dev {
     sfp_host_allgather_fn ag;
     sfp_host_bcast_fn bc;
     void* user;
+    /* the host encoder's tables (sfp_encode) */
+    u64* enc_rot;
+    double* enc_ksi;
 };
 
 struct sfp_conv {
@@ -111,6 +114,7 @@ void sfp_destroy(sfp_dev* d) {
     if (!d) return;
     free(d->q); free(d->psi); free(d->ipsi); free(d->psiS); free(d->ipsiS);
     free(d->ninv); free(d->ninvS);
+    free(d->enc_rot); free(d->enc_ksi);
     free(d);
 }
 
@@ -617,6 +621,64 @@ void sfp_load_i64(sfp_dev* d, uint64_t* p, const int64_t* c, sfp_limbs m) {
         u64 a = v < 0 ? (u64)(-(v + 1)) + 1 : (u64)v;
         u64 r = a % q;
         p[o + x] = (v < 0 && r) ? q - r : r;
+    })
+}
+
+/* ---- CKKS encoding (sfp_encode): the host encoder's special inverse FFT
+ * (csrc/core/encoder.cpp fftSpecialInv) restated in C, then round and reduce
+ * as sfp_load_i64.  Built with -ffp-contract=off: no fused multiply-add. */
+void sfp_encode_setup(sfp_dev* d, const uint64_t* rot, const double* ksi) {
+    free(d->enc_rot);
+    free(d->enc_ksi);
+    d->enc_rot = (u64*)malloc((size_t)d->n / 2 * 8);
+    d->enc_ksi = (double*)malloc((size_t)(2 * d->n + 1) * 16);
+    memcpy(d->enc_rot, rot, (size_t)d->n / 2 * 8);
+    memcpy(d->enc_ksi, ksi, (size_t)(2 * d->n + 1) * 16);
+}
+
+void sfp_encode(sfp_dev* d, uint64_t* p, const double* vals, uint32_t nvals, int real, uint32_t slots,
+                double scale, sfp_limbs m, uint64_t* scratch) {
+    const uint32_t n = d->n, S = slots;
+    const u64 M = 2ull * n;
+    double* v = (double*)scratch; /* S (re, im) pairs */
+    for (uint32_t i = 0; i < S; ++i) {
+        v[2 * i] = i < nvals ? (real ? vals[i] : vals[2 * i]) : 0.0;
+        v[2 * i + 1] = i < nvals && !real ? vals[2 * i + 1] : 0.0;
+    }
+    for (uint32_t len = S; len >= 1; len >>= 1) {
+        const uint32_t lenh = len >> 1;
+        const u64 lenq = (u64)len << 2;
+        for (uint32_t i = 0; i < S; i += len)
+            for (uint32_t j = 0; j < lenh; ++j) {
+                const u64 idx = (lenq - (d->enc_rot[j] % lenq)) * M / lenq;
+                double* a = v + 2 * (size_t)(i + j);
+                double* b = v + 2 * (size_t)(i + j + lenh);
+                const double kr = d->enc_ksi[2 * idx], ki = d->enc_ksi[2 * idx + 1];
+                const double ur = a[0] + b[0], ui = a[1] + b[1];
+                const double dr = a[0] - b[0], di = a[1] - b[1];
+                a[0] = ur;
+                a[1] = ui;
+                b[0] = dr * kr - di * ki;
+                b[1] = dr * ki + di * kr;
+            }
+        if (len == 1) break;
+    }
+    uint32_t logS = 0;
+    while ((1u << logS) < S) ++logS;
+    const uint32_t half = n / 2, gap = half / S;
+    LOOP_LIMBS({
+        const uint32_t xi = x < half ? x : x - half;
+        int64_t c = 0;
+        if (xi % gap == 0) {
+            const uint32_t i = xi / gap;
+            uint32_t r = 0;
+            for (uint32_t b = 0; b < logS; ++b) r |= ((i >> b) & 1u) << (logS - 1 - b);
+            const double u = v[2 * (size_t)r + (x < half ? 0 : 1)] / (double)S;
+            c = (int64_t)nearbyint(u * scale);
+        }
+        u64 a = c < 0 ? (u64)(-(c + 1)) + 1 : (u64)c;
+        u64 rr = a % q;
+        p[o + x] = (c < 0 && rr) ? q - rr : rr;
     })
 }
 

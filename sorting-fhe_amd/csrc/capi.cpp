@@ -268,6 +268,14 @@ int sfhe_op_stats(sfhe_ctx* c, uint64_t* counts, double* bytes, int reset) {
     return SFHE_OK;
 }
 
+int sfhe_encode_counts(sfhe_ctx* c, uint64_t* device, uint64_t* host) {
+    REQUIRE(c && device && host, "null argument");
+    auto s = c->cc->GetOpStats();
+    *device = s.dev_encodes;
+    *host = s.host_encodes;
+    return SFHE_OK;
+}
+
 int sfhe_encrypt(sfhe_ctx* c, const double* v, size_t len, uint32_t slots, uint32_t level,
                  sfhe_ct** out) {
     REQUIRE(c && out && (v || !len), "null argument");

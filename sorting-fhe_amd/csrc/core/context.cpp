@@ -987,6 +987,33 @@ class SfheInternal {
     // at scale / 2^shift and the residues multiplied by 2^shift mod q_i.
     static void encodeRows(SfheContextState* s, const Plaintext& pt, uint32_t level, uint64_t* dst,
                            sfp_limbs m, std::vector<int64_t>* keep = nullptr) {
+        // On the device (sfp_encode: the same FFT, bit for bit, no host
+        // synchronisation) unless the values could need the encoder's 2^shift
+        // range extension, or a trace wants the host coefficients.
+        // SFHE_HOST_ENCODE=1 (read per call) encodes on the host.
+        double mx = 0.0;
+        bool real = true;
+        for (const auto& c : pt->values) {
+            mx = std::max(mx, std::max(std::fabs(c.real()), std::fabs(c.imag())));
+            real = real && c.imag() == 0.0;
+        }
+        const char* he = std::getenv("SFHE_HOST_ENCODE");
+        const bool host = (he && *he == '1') || keep || !(mx * s->scale[level] < 2.0e18) ||
+                          (pt->slots & (pt->slots - 1)) || pt->values.size() > pt->slots;
+        if (!host) {
+            std::vector<double> v;
+            v.reserve(pt->values.size() * (real ? 1 : 2));
+            for (const auto& c : pt->values) {
+                v.push_back(c.real());
+                if (!real) v.push_back(c.imag());
+            }
+            auto scr = s->alloc((size_t)2 * pt->slots);
+            sfp_encode(s->dev, dst, v.data(), (uint32_t)pt->values.size(), real ? 1 : 0, pt->slots, s->scale[level],
+                       m, scr->ptr);
+            s->stats.dev_encodes++;
+            return;
+        }
+        s->stats.host_encodes++;
         std::vector<int64_t> local;
         std::vector<int64_t>& coeffs = keep ? *keep : local;
         const int shift = ckks_encode(pt->values, pt->slots, s->n, s->scale[level], coeffs);
@@ -1056,8 +1083,9 @@ class SfheInternal {
         std::vector<int64_t> coeffs;
         const size_t pw = s->polyWords(level);
         auto buf = s->alloc(pw);
-        encodeRows(s, pt, level, buf->ptr, s->qmap(ell), &coeffs);
-        if (std::getenv("SFHE_TRACE")) {
+        static const bool trace = std::getenv("SFHE_TRACE") != nullptr;
+        encodeRows(s, pt, level, buf->ptr, s->qmap(ell), trace ? &coeffs : nullptr);
+        if (trace) {
             uint64_t f = 1469598103934665603ull;
             for (int64_t v : coeffs) f = (f ^ (uint64_t)v) * 1099511628211ull;
             std::vector<u64> h(pw);
@@ -1422,6 +1450,12 @@ CryptoContextImpl<DCRTPoly>::CryptoContextImpl(const CCParams<CryptoContextCKKSR
     t.n_inv_shoup = ninvS.data();
     s.dev = sfp_create(p.GetDevice(), &t);
     if (!s.dev) SFHE_THROW(std::string("device backend '") + sfp_backend_name() + "' failed to initialise");
+    {  // the device encoder works from the host encoder's own tables
+        const uint64_t* rot = nullptr;
+        const double* ksi = nullptr;
+        ckks_encoder_tables(s.n, &rot, &ksi);
+        sfp_encode_setup(s.dev, rot, ksi);
+    }
 
     if (s.ext) {
         s.extIdx = s.Lq + s.K;

@@ -98,6 +98,12 @@ void fftSpecial(std::complex<double>* v, uint32_t size, const FFTTables& t) {
 
 }  // namespace
 
+void ckks_encoder_tables(uint32_t n, const uint64_t** rot, const double** ksi) {
+    const FFTTables& t = tables(n);
+    *rot = t.rot.data();
+    *ksi = reinterpret_cast<const double*>(t.ksi.data());  // (re, im) pairs: std::complex layout
+}
+
 int ckks_encode(const std::vector<std::complex<double>>& vals, uint32_t slots, uint32_t n,
                 double scale, std::vector<int64_t>& coeffs) {
     const FFTTables& t = tables(n);

@@ -504,6 +504,7 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
     struct OpStats {
         uint64_t keyswitch = 0, rescale = 0, tensor = 0, ptmult = 0, constmult = 0, add = 0,
                  automorph = 0, ntt_limbs = 0, wsum_terms = 0;
+        uint64_t dev_encodes = 0, host_encodes = 0;  // plaintext encodings on the device / host
         double algo_bytes = 0.0;  // SURVEY.md §8(d) byte model
         uint64_t pool_bytes = 0;  // device memory held by the context's pool (live + free blocks)
     };

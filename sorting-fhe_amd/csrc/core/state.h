@@ -242,5 +242,8 @@ int ckks_encode(const std::vector<std::complex<double>>& v, uint32_t slots, uint
                 double scale, std::vector<int64_t>& coeffs);
 void ckks_decode(const std::vector<double>& coeffs, uint32_t slots, uint32_t n,
                  std::vector<std::complex<double>>& out);
+// the encoder's tables (rot[j] = 5^j mod 2n, ksi[k] = exp(2 pi i k / 2n) as
+// (re, im) pairs), for the device encoder (sfp_encode_setup)
+void ckks_encoder_tables(uint32_t n, const uint64_t** rot, const double** ksi);
 
 }  // namespace lbcrypto

@@ -155,6 +155,9 @@ struct sfp_dev {
     size_t scrWords[SFP_MAX_LANES] = {};
     std::vector<void*> retired;
     sfp_graph* capture = nullptr;  // open capture (sfp_capture_begin)
+    // device CKKS encoder (sfp_encode): the host encoder's tables
+    u64* encRot = nullptr;         // [n/2] 5^j mod 2n
+    double2* encKsi = nullptr;     // [2n+1] exp(2 pi i k / 2n)
 };
 
 struct sfp_conv {
@@ -2301,6 +2304,8 @@ void sfp_destroy(sfp_dev* d) {
     hipHostFree(d->bounce);
     hipFree(d->cpool);
     hipFree(d->cpoolOld);
+    hipFree(d->encRot);
+    hipFree(d->encKsi);
     for (u64* p : d->scr) hipFree(p);
     for (void* p : d->retired) hipFree(p);
     for (int l = 0; l < d->nLanes; ++l) hipStreamDestroy(d->streams[l]);
@@ -3410,6 +3415,138 @@ void sfp_load_i64(sfp_dev* d, uint64_t* p, const int64_t* c, sfp_limbs m) {
 }
 
 
+
+// ---- CKKS encoding on the device (the sort's in-loop masks) ----------------
+// The host encoder's special inverse FFT (core/encoder.cpp fftSpecialInv),
+// operation for operation: the same stage order, the same integer twiddle
+// index, u = a + b and w = (a - b) * ksi with the complex product formed as
+// (re re - im im, re im + im re) with no fused multiply-add, the bit
+// reversal, the division by the size, then round(u * scale) and the residues
+// -- so the result equals ckks_encode + sfp_load_i64 bit for bit (the host's
+// doubles are IEEE-754 too, and its compiler does not contract either).
+// Stages whose butterflies span more than kEncTile values run one kernel per
+// stage over the whole vector; the rest run in LDS, one tile per block.
+constexpr uint32_t kEncTile = 2048;  // complex values per LDS tile (32 KB)
+
+__device__ __forceinline__ void encButterfly(double2& a, double2& b, uint32_t j, uint32_t len, const u64* rot,
+                                             const double2* ksi, u64 M) {
+#pragma clang fp contract(off)
+    const u64 lenq = (u64)len << 2;
+    const u64 idx = (lenq - (rot[j] & (lenq - 1))) * (M / lenq);  // == (lenq - rot % lenq) * M / lenq
+    const double2 k = ksi[idx];
+    const double2 u = make_double2(a.x + b.x, a.y + b.y);
+    const double dre = a.x - b.x, dim = a.y - b.y;
+    const double wre = dre * k.x - dim * k.y;
+    const double wim = dre * k.y + dim * k.x;
+    a = u;
+    b = make_double2(wre, wim);
+}
+
+// v = the values zero-padded to S (real: imaginary parts 0)
+__global__ __launch_bounds__(kThreads) void k_enc_load(double2* __restrict__ v, const double* __restrict__ vals,
+                                                       uint32_t nvals, int real, uint32_t S) {
+    for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < S; i += gridDim.x * kThreads) {
+        double2 x = make_double2(0.0, 0.0);
+        if (i < nvals) x = real ? make_double2(vals[i], 0.0) : make_double2(vals[2 * i], vals[2 * i + 1]);
+        v[i] = x;
+    }
+}
+
+// one stage of butterfly span `len` over the whole vector
+__global__ __launch_bounds__(kThreads) void k_enc_stage(double2* __restrict__ v, uint32_t S, uint32_t len,
+                                                        const u64* __restrict__ rot,
+                                                        const double2* __restrict__ ksi, u64 M) {
+    const uint32_t lenh = len >> 1;
+    for (uint32_t t = blockIdx.x * kThreads + threadIdx.x; t < S / 2; t += gridDim.x * kThreads) {
+        const uint32_t j = t % lenh, i = (t / lenh) * len;
+        double2 a = v[i + j], b = v[i + j + lenh];
+        encButterfly(a, b, j, len, rot, ksi, M);
+        v[i + j] = a;
+        v[i + j + lenh] = b;
+    }
+}
+
+// the stages of span T, T/2, ..., 2 on one T-value tile per block, in LDS
+__global__ __launch_bounds__(kThreads) void k_enc_tile(double2* __restrict__ v, uint32_t T,
+                                                       const u64* __restrict__ rot, const double2* __restrict__ ksi,
+                                                       u64 M) {
+    __shared__ double2 sh[kEncTile];
+    double2* g = v + (size_t)blockIdx.x * T;
+    for (uint32_t i = threadIdx.x; i < T; i += kThreads) sh[i] = g[i];
+    __syncthreads();
+    for (uint32_t len = T; len >= 2; len >>= 1) {
+        const uint32_t lenh = len >> 1;
+        for (uint32_t t = threadIdx.x; t < T / 2; t += kThreads) {
+            const uint32_t j = t % lenh, i = (t / lenh) * len;
+            double2 a = sh[i + j], b = sh[i + j + lenh];
+            encButterfly(a, b, j, len, rot, ksi, M);
+            sh[i + j] = a;
+            sh[i + j + lenh] = b;
+        }
+        __syncthreads();
+    }
+    for (uint32_t i = threadIdx.x; i < T; i += kThreads) g[i] = sh[i];
+}
+
+// coefficient x of the sparse packing (gap = n/2S): the bit-reversed value,
+// divided by S, times the scale, rounded; its residue in every row of m
+__global__ __launch_bounds__(kThreads) void k_enc_round(u64* __restrict__ p, const double2* __restrict__ v,
+                                                        uint32_t logS, double scale, sfp_limbs m,
+                                                        const sf_barrett* __restrict__ bar, uint32_t logn) {
+#pragma clang fp contract(off)
+    const uint32_t n = 1u << logn, half = n >> 1, gap = half >> logS;
+    for (uint32_t x = blockIdx.x * kThreads + threadIdx.x; x < n; x += gridDim.x * kThreads) {
+        const uint32_t xi = x < half ? x : x - half;
+        int64_t c = 0;
+        if ((xi & (gap - 1)) == 0) {
+            const uint32_t i = xi / gap;
+            const uint32_t r = logS ? (__brev(i) >> (32 - logS)) : 0u;
+            const double2 u = v[r];
+            const double q = (x < half ? u.x : u.y) / (double)(1u << logS);
+            c = (int64_t)rint(q * scale);
+        }
+        const u64 a = c < 0 ? (u64)(-(c + 1)) + 1 : (u64)c;
+        for (uint32_t limb = 0; limb < m.count; ++limb) {
+            const sf_barrett B = loadBar(bar, primeOf(m, limb));
+            const u64 res = sf_reduce128(a, 0, &B);
+            p[((size_t)limb << logn) + x] = (c < 0 && res) ? B.q - res : res;
+        }
+    }
+}
+
+void sfp_encode_setup(sfp_dev* d, const uint64_t* rot, const double* ksi) {
+    if (!d->encRot && (hipMalloc((void**)&d->encRot, (size_t)d->n / 2 * 8) != hipSuccess ||
+                       hipMalloc((void**)&d->encKsi, (size_t)(2 * d->n + 1) * sizeof(double2)) != hipSuccess)) {
+        hipGetLastError();
+        return record(d, "encode tables", hipErrorOutOfMemory);
+    }
+    hostToDev(d, d->encRot, rot, (size_t)d->n / 2 * 8);
+    hostToDev(d, d->encKsi, ksi, (size_t)(2 * d->n + 1) * sizeof(double2));
+}
+
+void sfp_encode(sfp_dev* d, uint64_t* dst, const double* vals, uint32_t nvals, int real, uint32_t slots,
+                double scale, sfp_limbs m, uint64_t* scratch) {
+    if (!limbsOk(d, m, "encode")) return;
+    if (!d->encRot || !slots || (slots & (slots - 1)) || slots > d->n / 2 || nvals > slots) {
+        record(d, "encode (tables not set up, or a bad slot count)", hipErrorInvalidValue);
+        return;
+    }
+    const u64 M = 2ull * d->n;
+    double2* v = reinterpret_cast<double2*>(scratch);
+    const double* dv = nvals ? (const double*)ringPut(d, vals, (size_t)nvals * (real ? 8 : 16)) : nullptr;
+    hipLaunchKernelGGL(k_enc_load, dim3(gridFor(slots, kThreads)), dim3(kThreads), 0, d->st(), v, dv, nvals, real,
+                       slots);
+    const uint32_t T = std::min(slots, kEncTile);
+    for (uint32_t len = slots; len > T; len >>= 1)
+        hipLaunchKernelGGL(k_enc_stage, dim3(gridFor(slots / 2, kThreads)), dim3(kThreads), 0, d->st(), v, slots, len,
+                           d->encRot, d->encKsi, M);
+    if (T >= 2)
+        hipLaunchKernelGGL(k_enc_tile, dim3(slots / T), dim3(kThreads), 0, d->st(), v, T, d->encRot, d->encKsi, M);
+    const uint32_t logS = (uint32_t)__builtin_ctz(slots);
+    hipLaunchKernelGGL(k_enc_round, dim3(ewGrid(d->n)), dim3(kThreads), 0, d->st(), dst, v, logS, scale, m, d->bar,
+                       d->logn);
+    checkLaunch(d, "encode");
+}
 
 // ---- limb sharding ----
 // dst row i = src row rows[i]

@@ -240,6 +240,22 @@ void sfp_sample_uniform(sfp_dev* d, uint64_t* p, sfp_limbs m, uint64_t seed);
 // Load signed coefficients (same for every limb) reduced mod each prime.
 void sfp_load_i64(sfp_dev* d, uint64_t* p, const int64_t* coeffs, sfp_limbs m);
 
+// ---- CKKS encoding on the device ------------------------------------------------
+// The host encoder's tables, uploaded once per device: rot[j] = 5^j mod 2n
+// (j < n/2) and ksi[k] = exp(2 pi i k / 2n) as (re, im) pairs (k <= 2n).
+void sfp_encode_setup(sfp_dev* d, const uint64_t* rot, const double* ksi);
+// p (rows of map m, COEFFICIENT domain) = the residues of the encoding of
+// `nvals` slot values (host array: doubles when `real`, else (re, im) pairs)
+// zero-padded to `slots`: the special inverse FFT, packed sparsely (gap
+// n / (2 slots)), each coefficient round(u * scale).  Bit-identical to the
+// host encoder (core/encoder.cpp ckks_encode) followed by sfp_load_i64,
+// provided no coefficient needs the encoder's 2^shift range extension (the
+// caller checks |value| * scale < 2e18).  No host synchronisation (the values
+// travel through the argument ring), so it may run inside a graph capture.
+// scratch: 2 * slots words.
+void sfp_encode(sfp_dev* d, uint64_t* p, const double* vals, uint32_t nvals, int real, uint32_t slots,
+                double scale, sfp_limbs m, uint64_t* scratch);
+
 // ---- lanes: independent in-order queues (HIP streams) ----------------------------
 // Every prim launches on the current lane.  Work on different lanes may run
 // concurrently; order it with events.  The oracle has one synchronous lane

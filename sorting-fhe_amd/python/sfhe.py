@@ -42,6 +42,7 @@ ABI_SYMBOLS = [
     "sfhe_sorter_sort_bitonic", "sfhe_kway_sort", "sfhe_kway_params",
     "sfhe_save", "sfhe_load", "sfhe_ct_save", "sfhe_ct_load",
     "sfhe_kway_create", "sfhe_kway_run", "sfhe_kway_destroy", "sfhe_shard_tail",
+    "sfhe_encode_counts",
 ]
 
 
@@ -148,6 +149,7 @@ _SIGS = {
     "sfhe_shard_rccl": (C.c_int, [_VP, C.c_int, C.c_int, _VP]),
     "sfhe_shard_host": (C.c_int, [_VP, C.c_int, C.c_int, _AG, _BC, _VP]),
     "sfhe_shard_tail": (C.c_int, [_VP, _PU32]),
+    "sfhe_encode_counts": (C.c_int, [_VP, _PU64, _PU64]),
 }
 
 _libs: dict = {}
@@ -318,6 +320,12 @@ class Engine:
         d = dict(zip(keys, list(c)))
         d["algo_bytes"] = b.value
         return d
+
+    def encode_counts(self):
+        """(device, host) plaintext encodings since the last op_stats reset."""
+        d, h = C.c_uint64(), C.c_uint64()
+        self._chk(self.lib.sfhe_encode_counts(self.ctx, C.byref(d), C.byref(h)))
+        return d.value, h.value
 
     def pool_bytes(self) -> int:
         v = C.c_uint64()
