@@ -624,6 +624,16 @@ void sfp_load_i64(sfp_dev* d, uint64_t* p, const int64_t* c, sfp_limbs m) {
     })
 }
 
+/* no fused ModUp + inner product: the host layer runs sfp_modup + sfp_ks_inner* */
+int sfp_modup_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* in, uint32_t ell, uint32_t K,
+                    uint32_t Lq, uint32_t alpha, const sfp_conv* const* convs, const uint64_t* key,
+                    const uint64_t* fold0, const uint64_t* fold1, uint64_t fold_k, int accum, uint64_t* ext,
+                    uint64_t* scratch) {
+    (void)d; (void)acc0; (void)acc1; (void)in; (void)ell; (void)K; (void)Lq; (void)alpha; (void)convs;
+    (void)key; (void)fold0; (void)fold1; (void)fold_k; (void)accum; (void)ext; (void)scratch;
+    return -1;
+}
+
 /* ---- CKKS encoding (sfp_encode): the host encoder's special inverse FFT
  * (csrc/core/encoder.cpp fftSpecialInv) restated in C, then round and reduce
  * as sfp_load_i64.  Built with -ffp-contract=off: no fused multiply-add. */

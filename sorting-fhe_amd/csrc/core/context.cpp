@@ -794,6 +794,32 @@ class SfheInternal {
         return full;
     }
 
+    // ModUp of d (ell limbs, evaluation domain, unsharded rows) and the key
+    // inner product into acc (two polys of ell+K rows, (ell+K)*n apart):
+    // accumulated when accum, + foldK * (fold0, fold1) on row ell-1 when
+    // fold0.  One fused pass where the backend has it (sfp_modup_inner: the
+    // extended digits never round-trip through HBM), else ModUp + inner product.
+    static void modupInner(CC* cc, uint64_t* acc, const uint64_t* d, uint32_t ell, const DeviceBufferPtr& key,
+                           const uint64_t* fold0, const uint64_t* fold1, u64 foldK, int accum) {
+        SfheContextState* s = cc->st.get();
+        const uint32_t n = s->n, K = s->K;
+        const uint32_t beta = (ell + s->alpha - 1) / s->alpha;
+        const size_t stride = (size_t)(ell + K) * n;
+        auto ext = s->alloc(stride * beta);
+        auto scratch = s->alloc((size_t)ell * n);
+        auto& convs = modupConv(cc, ell);
+        if (sfp_modup_inner(s->dev, acc, acc + stride, d, ell, K, s->Lq, s->alpha, convs.data(), key->ptr, fold0,
+                            fold1, foldK, accum, ext->ptr, scratch->ptr) == 0)
+            return;
+        sfp_modup(s->dev, ext->ptr, d, ell, K, s->Lq, s->alpha, convs.data(), scratch->ptr);
+        if (fold0)
+            sfp_ks_inner_fold(s->dev, acc, acc + stride, ext->ptr, stride, key->ptr, beta, ell, K, s->Lq, fold0, fold1,
+                              foldK);
+        else
+            (accum ? sfp_ks_inner_acc : sfp_ks_inner)(s->dev, acc, acc + stride, ext->ptr, stride, key->ptr, beta,
+                                                       ell, K, s->Lq);
+    }
+
     // Hybrid key switch of d (ell limbs, evaluation domain) with `key`; the
     // result goes to (out0, out1) (ell limbs each), added when add0 / add1.
     static void keySwitch(CC* cc, const uint64_t* d, uint32_t ell, const DeviceBufferPtr& key,
@@ -803,11 +829,11 @@ class SfheInternal {
         const uint32_t n = s->n, K = s->K;
         const uint32_t beta = (ell + s->alpha - 1) / s->alpha;
         const size_t stride = (size_t)(ell + K) * n;
-        auto ext = s->alloc(stride * beta);
-        auto scratch = s->alloc((size_t)ell * n);
-        auto& convs = modupConv(cc, ell);
-        sfp_modup(s->dev, ext->ptr, d, ell, K, s->Lq, s->alpha, convs.data(), scratch->ptr);
-        innerAndModDown(cc, ext->ptr, stride, beta, ell, key, out0, out1, add0, add1);
+        auto acc = s->alloc(2 * stride);
+        modupInner(cc, acc->ptr, d, ell, key, nullptr, nullptr, 0, 0);
+        auto md = s->alloc((size_t)2 * ell * n);
+        sfp_moddown2(s->dev, out0, out1, acc->ptr, stride, ell, K, s->Lq, s->moddownConv, s->pInvModQ.data(), add0,
+                     add1, md->ptr);
         s->stats.keyswitch++;
         // (3 l + 2 beta (l+K)) B
         s->countBytes((3.0 * ell + 2.0 * beta * (ell + K)) * n * 8);
@@ -828,15 +854,8 @@ class SfheInternal {
         const uint32_t n = s->n, K = s->K;
         const uint32_t beta = (ell + s->alpha - 1) / s->alpha;
         const size_t stride = (size_t)(ell + K) * n;
-        auto ext = s->alloc(stride * beta);
-        {
-            auto scratch = s->alloc((size_t)ell * n);
-            auto& convs = modupConv(cc, ell);
-            sfp_modup(s->dev, ext->ptr, d2, ell, K, s->Lq, s->alpha, convs.data(), scratch->ptr);
-        }
         auto acc = s->alloc(2 * stride);
-        sfp_ks_inner_fold(s->dev, acc->ptr, acc->ptr + stride, ext->ptr, stride, s->relinKey->ptr, beta,
-                          ell, K, s->Lq, d0, d1, s->pModQ[ell - 1]);
+        modupInner(cc, acc->ptr, d2, ell, s->relinKey, d0, d1, s->pModQ[ell - 1], 0);
         Ct out = newCt(cc, level + 1, slots);
         auto scratch = s->alloc((size_t)2 * (ell - 1) * n);
         sfp_moddown_rescale(s->dev, out->c0, out->c1, d0, d1, acc->ptr, stride, ell, K, s->Lq,
@@ -2399,8 +2418,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotateSum(const std::vecto
     auto out = pend ? SfheInternal::newPendingCt(this, level, slots) : SfheInternal::newCt(this, level, slots);
     auto t = s->alloc((size_t)s->rows(ell) * n);
     auto c0 = s->alloc((size_t)s->rows(ell) * n);
-    auto ext = s->alloc(stride * beta);
-    auto scratch = s->alloc((size_t)ell * n);
+    auto ext = shard ? s->alloc(stride * beta) : nullptr;  // (the unsharded ModUp allocates its own)
     auto acc = s->alloc(2 * stride);
     for (size_t i = 0; i < rot.size(); ++i) {
         const Ciphertext<DCRTPoly>& x = a[rot[i]];
@@ -2413,10 +2431,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotateSum(const std::vecto
             SfheInternal::modupShard(s, ext->ptr, t->ptr, ell);
             SfheInternal::innerShard(s, acc->ptr, ext->ptr, stride, beta, ell, *keys[i], i ? 1 : 0);
         } else {
-            sfp_modup(s->dev, ext->ptr, t->ptr, ell, K, s->Lq, s->alpha, SfheInternal::modupConv(this, ell).data(),
-                      scratch->ptr);
-            (i ? sfp_ks_inner_acc : sfp_ks_inner)(s->dev, acc->ptr, acc->ptr + stride, ext->ptr, stride,
-                                                   (*keys[i])->ptr, beta, ell, K, s->Lq);
+            SfheInternal::modupInner(this, acc->ptr, t->ptr, ell, *keys[i], nullptr, nullptr, 0, i ? 1 : 0);
         }
         s->stats.automorph++;
         s->stats.keyswitch++;

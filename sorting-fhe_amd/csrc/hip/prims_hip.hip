@@ -988,6 +988,200 @@ __global__ __launch_bounds__(kNttSmallThreads) void k_ntt_small(const RowGroup G
 
 enum EwOp { EW_ADD, EW_SUB, EW_NEG, EW_MUL, EW_MULADD, EW_MULC, EW_ADDC };
 
+// ---- ModUp's last NTT pass fused with the key inner product ----------------
+// (sfp_modup_inner).  Block (tile, t) owns row-tile `tile` of extended-basis
+// limb t.  For every digit j it takes that limb's canonical evaluation-domain
+// tile -- the forward ROW pass of the COL-pass output in ext_j, or the input
+// row itself where t is one of digit j's own limbs -- multiplies it by digit
+// j's two key rows and accumulates 128-bit sums; after the last digit the
+// sums (+ the relinearisation fold, + the previous accumulator) are reduced
+// into acc rows t.  The same integers as the ROW pass writing ext followed by
+// k_ks_inner, without the ext round trip through HBM and the extra launch.
+struct KsArgs {
+    const u64* in;        // ell rows, evaluation domain (the digits' own limbs)
+    const u64* ext;       // beta blocks of ell+K rows: COL-pass output of the other limbs
+    long long extStride;  // words between digit blocks
+    const u64* key;       // beta digits of [b rows][a rows], keyRows rows each
+    uint32_t keyRows, keyQ;  // ext limb t uses key row t < ell ? t : keyQ + (t - ell)
+    u64* acc0;
+    u64* acc1;
+    const u64* fold0;  // t == ell - 1: + foldK * fold_p (sfp_ks_inner_fold)
+    const u64* fold1;
+    u64 foldK;
+    uint32_t ell, Lq, alpha, beta;
+    int accum;  // acc += the inner product
+};
+
+template <int LE, int TILE>
+__global__ __launch_bounds__(TILE >> LE) void k_ntt_ks(const KsArgs A, const sf_barrett* __restrict__ bar,
+                                                     const u64* __restrict__ tw, const u64* __restrict__ twS,
+                                                     uint32_t logn, const double* __restrict__ twD,
+                                                     const double* __restrict__ qinvD, int useFp) {
+    __shared__ u64 s[TILE];
+    constexpr int NT = TILE >> LE;       // threads
+    constexpr int NPAIR = (1 << LE) / 2;  // 16-byte pairs per thread
+    const uint32_t n = 1u << logn;
+    const uint32_t logR = logn - 8;
+    const uint32_t t = blockIdx.y;
+    const uint32_t prime = t < A.ell ? t : A.Lq + (t - A.ell);
+    const sf_barrett B = loadBar(bar, prime);
+    const u64 q = B.q;
+    const bool fp = useFp && q < kFpPrimeBound;
+    NttTile T;
+    T.logn = logn;
+    T.d = 8u;
+    T.logC = 0;
+    T.C = 1;
+    const uint32_t tile = (gridDim.x & 7) ? blockIdx.x : (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    T.c0 = 0;
+    T.r0 = tile * (TILE / 256);
+    const uint32_t S0 = logR;
+    const u64* gw = fp ? reinterpret_cast<const u64*>(twD) + (size_t)prime * n : tw + (size_t)prime * n;
+    const u64* gx = twS + (size_t)prime * n;
+    constexpr bool kPfBuild = LE == 2;
+    constexpr int kPfRounds = 4;
+    double PW[kPfBuild ? kPfRounds * 3 : 1];
+    if constexpr (kPfBuild) {
+        if (fp) {
+            const double* gd = reinterpret_cast<const double*>(gw);
+#pragma unroll
+            for (int r = 0; r < kPfRounds; ++r) {
+                const uint32_t k0 = 2 * r, logh = 8 - k0 - 2;
+                const uint32_t lo = threadIdx.x & ((1u << logh) - 1);
+                const uint32_t rest = threadIdx.x >> logh;
+                const uint32_t hi = rest & ((1u << k0) - 1);
+                const uint32_t st = rest >> k0;
+                const uint32_t x0 = nttGlobal<false>(T, st, hi * (256u >> k0) + lo);
+#pragma unroll
+                for (int tt = 0; tt < 2; ++tt) {
+                    const uint32_t tb = twIndex<false>(T, S0, k0 + tt, x0);
+#pragma unroll
+                    for (int qd = 0; qd < (1 << tt); ++qd) PW[3 * r + (1 << tt) - 1 + qd] = gd[tb + qd];
+                }
+            }
+        }
+    }
+    const double qd = (double)q, qi = qinvD[prime];
+    const uint32_t kr = t < A.ell ? t : A.keyQ + (t - A.ell);
+    const size_t rowOff = (size_t)T.r0 * 256;
+    Acc a0[2 * NPAIR], a1[2 * NPAIR];
+#pragma unroll
+    for (int w = 0; w < 2 * NPAIR; ++w) a0[w] = a1[w] = Acc{0, 0};
+    for (uint32_t j = 0; j < A.beta; ++j) {
+        const bool own = t < A.ell && t >= j * A.alpha && t < min((j + 1) * A.alpha, A.ell);
+        u64 v[2 * NPAIR];
+        if (own) {
+            const u64* src = A.in + (size_t)t * n + rowOff;
+#pragma unroll
+            for (int k = 0; k < NPAIR; ++k) {
+                const uint32_t e = 2 * (threadIdx.x + k * NT);
+                const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(src + e);
+                v[2 * k] = x.x;
+                v[2 * k + 1] = x.y;
+            }
+        } else {
+            const u64* src = A.ext + j * A.extStride + (size_t)t * n + rowOff;
+            __syncthreads();  // the previous digit's readers are done with s
+#pragma unroll
+            for (int k = 0; k < NPAIR; ++k) {
+                const uint32_t e = 2 * (threadIdx.x + k * NT);
+                const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(src + e);
+                if (fp) {
+                    s[ldsSw(e)] = __double_as_longlong(u2d(x.x));
+                    s[ldsSw(e + 1)] = __double_as_longlong(u2d(x.y));
+                } else {
+                    s[ldsSw(e)] = x.x;
+                    s[ldsSw(e + 1)] = x.y;
+                }
+            }
+            __syncthreads();
+            bool done = false;
+            if constexpr (kPfBuild) {
+                if (fp) {
+#pragma unroll
+                    for (int r = 0; r < kPfRounds; ++r) {
+                        nttRoundFP<false, false, 2, 2, TILE, true, 8>(reinterpret_cast<double*>(s), T, S0, 2 * r,
+                                                                      qd, nullptr, qi, PW + 3 * r);
+                        __syncthreads();
+                    }
+                    done = true;
+                }
+            }
+            if (!done) {
+                const uint32_t nr = (8 + LE - 1) / LE;
+                for (uint32_t r = 0; r < nr; ++r) {
+                    const uint32_t k0 = LE * r;
+                    const int b = (int)min((uint32_t)LE, 8u - k0);
+                    if (fp)
+                        nttRoundDynFP<false, false, LE, TILE>(b, reinterpret_cast<double*>(s), T, S0, k0, qd,
+                                                              reinterpret_cast<const double*>(gw), qi);
+                    else
+                        nttRoundDyn<false, false, LE, TILE>(b, s, T, S0, k0, q, gw, gx);
+                    __syncthreads();
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < NPAIR; ++k) {
+                const uint32_t e = 2 * (threadIdx.x + k * NT);
+                u64 x0 = s[ldsSw(e)], x1 = s[ldsSw(e + 1)];
+                if (fp) {  // canonical [0, q), as the ROW pass stores it
+                    x0 = d2u(fpReduce(__longlong_as_double(x0), qd, qi));
+                    x1 = d2u(fpReduce(__longlong_as_double(x1), qd, qi));
+                } else {  // forward lazy range [0, 4q) -> [0, q)
+                    x0 = x0 >= 2 * q ? x0 - 2 * q : x0;
+                    x1 = x1 >= 2 * q ? x1 - 2 * q : x1;
+                    x0 = x0 >= q ? x0 - q : x0;
+                    x1 = x1 >= q ? x1 - q : x1;
+                }
+                v[2 * k] = x0;
+                v[2 * k + 1] = x1;
+            }
+        }
+        const u64* kb = A.key + (size_t)j * 2 * A.keyRows * n + (size_t)kr * n + rowOff;
+        const u64* ka = kb + (size_t)A.keyRows * n;
+#pragma unroll
+        for (int k = 0; k < NPAIR; ++k) {
+            const uint32_t e = 2 * (threadIdx.x + k * NT);
+            const ulonglong2 b2 = *reinterpret_cast<const ulonglong2*>(kb + e);
+            const ulonglong2 a2 = *reinterpret_cast<const ulonglong2*>(ka + e);
+            macc(a0[2 * k], v[2 * k], b2.x);
+            macc(a0[2 * k + 1], v[2 * k + 1], b2.y);
+            macc(a1[2 * k], v[2 * k], a2.x);
+            macc(a1[2 * k + 1], v[2 * k + 1], a2.y);
+        }
+    }
+    const bool fold = A.fold0 && t == A.ell - 1;
+    u64* o0 = A.acc0 + (size_t)t * n + rowOff;
+    u64* o1 = A.acc1 + (size_t)t * n + rowOff;
+#pragma unroll
+    for (int k = 0; k < NPAIR; ++k) {
+        const uint32_t e = 2 * (threadIdx.x + k * NT);
+        if (fold) {  // + P * d_l (sfp_ks_inner_fold)
+            const ulonglong2 f0 = *reinterpret_cast<const ulonglong2*>(A.fold0 + rowOff + e);
+            const ulonglong2 f1 = *reinterpret_cast<const ulonglong2*>(A.fold1 + rowOff + e);
+            macc(a0[2 * k], f0.x, A.foldK);
+            macc(a0[2 * k + 1], f0.y, A.foldK);
+            macc(a1[2 * k], f1.x, A.foldK);
+            macc(a1[2 * k + 1], f1.y, A.foldK);
+        }
+        ulonglong2 r0, r1;
+        r0.x = sf_reduce128_acc(a0[2 * k].lo, a0[2 * k].hi, &B);
+        r0.y = sf_reduce128_acc(a0[2 * k + 1].lo, a0[2 * k + 1].hi, &B);
+        r1.x = sf_reduce128_acc(a1[2 * k].lo, a1[2 * k].hi, &B);
+        r1.y = sf_reduce128_acc(a1[2 * k + 1].lo, a1[2 * k + 1].hi, &B);
+        if (A.accum) {
+            const ulonglong2 p0 = *reinterpret_cast<const ulonglong2*>(o0 + e);
+            const ulonglong2 p1 = *reinterpret_cast<const ulonglong2*>(o1 + e);
+            r0.x = sf_add(r0.x, p0.x, q);
+            r0.y = sf_add(r0.y, p0.y, q);
+            r1.x = sf_add(r1.x, p1.x, q);
+            r1.y = sf_add(r1.y, p1.y, q);
+        }
+        *reinterpret_cast<ulonglong2*>(o0 + e) = r0;
+        *reinterpret_cast<ulonglong2*>(o1 + e) = r1;
+    }
+}
+
 struct ConstArgs {
     u64 k[SFP_MAX_LIMBS];
 };
@@ -2416,12 +2610,17 @@ static RowGroup rowsOf(uint32_t P, uint32_t R, sfp_limbs pm) {
     return G;
 }
 
-// Both passes of a (batched) NTT over the rows of G.
-static void nttRows(sfp_dev* d, const RowGroup& G, int inverse) {
+// Both passes of a (batched) NTT over the rows of G (firstOnly: only the first
+// pass -- the forward COL pass -- whose output a fused second pass consumes).
+static void nttRows(sfp_dev* d, const RowGroup& G, int inverse, bool firstOnly = false) {
     const uint32_t rows = G.P * G.R;
     if (!rows || !limbsOk(d, G.pm, "ntt")) return;
     if (G.lift && G.liftPrime >= d->np) return (void)limbsOk(d, sfp_limbs{1, 1, G.liftPrime, G.liftPrime}, "ntt lift");
     const double bytes = 16.0 * rows * d->n;
+    if (firstOnly && (d->n <= (uint32_t)kNttTile || inverse)) {
+        record(d, "ntt (first pass alone: forward, rings above one tile only)", hipErrorInvalidValue);
+        return;
+    }
     if (d->n <= (uint32_t)kNttTile) {  // small rings: one single-pass block per row
         timedLaunch(d, SFP_FAM_NTT, bytes, [&] {
             if (inverse)
@@ -2460,7 +2659,9 @@ static void nttRows(sfp_dev* d, const RowGroup& G, int inverse) {
     const bool t1k = rows <= t1kRows && d->n <= smallTile * 128u;
     const dim3 g(d->n / (t1k ? smallTile : (uint32_t)kNttTile), rows);
     const bool small = rows < (uint32_t)kNttSmallRows;
+    int npass = 0;
     auto pass = [&](auto kern, int threads) {
+        if (firstOnly && npass++ > 0) return;
         timedLaunch(d, SFP_FAM_NTT, bytes, [&] {
             hipLaunchKernelGGL(kern, g, dim3(threads), 0, d->st(), G, d->bar, tw, twS, d->ninv,
                                d->ninvS, d->logn, twD, d->qinvD, d->ninvD, d->ninvQ, nttFp());
@@ -3204,6 +3405,72 @@ void sfp_modup(sfp_dev* d, uint64_t* ext, const uint64_t* in, uint32_t ell, uint
     B.skipEll = ell;
     B.alpha = alpha;
     nttRows(d, B, 0);
+}
+
+int sfp_modup_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* in, uint32_t ell, uint32_t K,
+                    uint32_t Lq, uint32_t alpha, const sfp_conv* const* convs, const uint64_t* key,
+                    const uint64_t* fold0, const uint64_t* fold1, uint64_t foldK, int accum, uint64_t* ext,
+                    uint64_t* scr) {
+    static const bool on = [] {  // SFHE_KS_FUSE=0: the unfused sequence (A/B)
+        const char* v = std::getenv("SFHE_KS_FUSE");
+        return !v || *v != '0';
+    }();
+    const uint32_t n = d->n;
+    const uint32_t beta = (ell + alpha - 1) / alpha;
+    if (!on || n <= (uint32_t)kNttTile) return -1;  // the caller runs sfp_modup + sfp_ks_inner*
+    const long long stride = (long long)(ell + K) * n;
+    if (beta > (uint32_t)kMaxConvJobs || ell + K > SFP_MAX_LIMBS || (fold0 && (!fold1 || ell < 1))) {
+        record(d, "modup_inner (too many digits / limbs)", hipErrorInvalidValue);
+        return 0;
+    }
+    // INTT of every input row (the digits' own rows are read from `in` by the fused pass)
+    RowGroup A = rowsOf(1, ell, sfp_limbs{ell, ell, 0, 0});
+    A.src = RowPtr{in, 0, (long long)n};
+    A.dst = RowPtr{scr, 0, (long long)n};
+    nttRows(d, A, 1);
+    ConvJobs J;
+    bool fpOk = true;
+    for (uint32_t j = 0; j < beta; ++j) {
+        J.j[j] = convJob(convs[j], ext + j * stride, scr + (size_t)j * alpha * n, convs[j]->nt, 0);
+        fpOk = fpOk && convs[j]->fpOk;
+    }
+    convLaunch(d, J, beta, fpOk);
+    // the forward COL pass of every converted row; the ROW pass runs fused below
+    RowGroup B = rowsOf(beta, ell + K, sfp_limbs{ell + K, ell, Lq, 0});
+    B.src = B.dst = RowPtr{ext, stride, (long long)n};
+    B.skipEll = ell;
+    B.alpha = alpha;
+    nttRows(d, B, 0, true);
+    KsArgs a;
+    a.in = in;
+    a.ext = ext;
+    a.extStride = stride;
+    a.key = key;
+    a.keyRows = Lq + K;
+    a.keyQ = Lq;
+    a.acc0 = acc0;
+    a.acc1 = acc1;
+    a.fold0 = fold0;
+    a.fold1 = fold1;
+    a.foldK = foldK;
+    a.ell = ell;
+    a.Lq = Lq;
+    a.alpha = alpha;
+    a.beta = beta;
+    a.accum = accum;
+    const uint32_t rows = ell + K;
+    const size_t total = (size_t)rows * n;
+    const bool t1k = rows <= 64 && n <= 1024u * 128u;
+    timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + (accum ? 4.0 : 2.0)), [&] {
+        if (t1k)
+            hipLaunchKernelGGL((k_ntt_ks<2, 1024>), dim3(n / 1024, rows), dim3(1024 >> 2), 0, d->st(), a, d->bar,
+                               d->psi, d->psiS, d->logn, d->psiD, d->qinvD, nttFp());
+        else
+            hipLaunchKernelGGL((k_ntt_ks<2, kNttTile>), dim3(n / kNttTile, rows), dim3(kNttTile >> 2), 0, d->st(),
+                               a, d->bar, d->psi, d->psiS, d->logn, d->psiD, d->qinvD, nttFp());
+    });
+    checkLaunch(d, "ntt_ks");
+    return 0;
 }
 
 void sfp_ks_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,

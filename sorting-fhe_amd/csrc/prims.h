@@ -178,6 +178,18 @@ void sfp_conv_apply_centered(sfp_dev* d, uint64_t* dst, const uint64_t* src, con
 void sfp_modup(sfp_dev* d, uint64_t* ext, const uint64_t* in, uint32_t ell, uint32_t K,
                uint32_t Lq, uint32_t alpha, const sfp_conv* const* convs, uint64_t* scratch);
 
+// ModUp fused with the key inner product (one key switch's ModUp + inner
+// product without the extended digits' round trip through HBM): the same
+// acc0 / acc1 as sfp_modup followed by sfp_ks_inner_fold (fold0 != NULL),
+// sfp_ks_inner_acc (accum) or sfp_ks_inner.  ext: beta * (ell+K) * n words
+// of scratch (the COL-pass intermediate), scr: ell * n words.  Returns -1
+// (and does nothing) where the backend has no fused form -- rings of one NTT
+// tile, SFHE_KS_FUSE=0, the oracle -- and the caller runs the unfused prims.
+int sfp_modup_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* in, uint32_t ell, uint32_t K,
+                    uint32_t Lq, uint32_t alpha, const sfp_conv* const* convs, const uint64_t* key,
+                    const uint64_t* fold0, const uint64_t* fold1, uint64_t fold_k, int accum, uint64_t* ext,
+                    uint64_t* scratch);
+
 // Key inner product:  acc0 = sum_j ext_j * kb_j,  acc1 = sum_j ext_j * ka_j
 //   ext  : beta extended polys, each (ell+K) limbs, stride ext_stride.
 //   key  : beta digits, each [b rows (Lq+K)][a rows (Lq+K)]; ext limb t maps to
