@@ -568,7 +568,8 @@ static void moddown1(sfp_dev* d, uint64_t* out, uint64_t* acc, uint32_t ell, uin
 
 void sfp_moddown2(sfp_dev* d, uint64_t* out0, uint64_t* out1, uint64_t* acc, size_t acc_stride,
                   uint32_t ell, uint32_t K, uint32_t Lq, const sfp_conv* c, const uint64_t* pinv,
-                  int add0, int add1, uint64_t* scratch) {
+                  int add0, int add1, uint64_t* scratch, int row_done) {
+    (void)row_done; /* never set: the oracle has no sfp_modup_inner */
     moddown1(d, out0, acc, ell, K, Lq, c, pinv, add0, scratch);
     moddown1(d, out1, acc + acc_stride, ell, K, Lq, c, pinv, add1, scratch + (size_t)ell * d->n);
 }
@@ -579,9 +580,10 @@ void sfp_moddown2(sfp_dev* d, uint64_t* out0, uint64_t* out1, uint64_t* acc, siz
 void sfp_moddown_rescale(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint64_t* d0,
                          const uint64_t* d1, uint64_t* acc, size_t acc_stride, uint32_t ell,
                          uint32_t K, uint32_t Lq, const sfp_conv* c, const uint64_t* pinv,
-                         const uint64_t* pmod, const uint64_t* qlinv, uint64_t* scratch) {
+                         const uint64_t* pmod, const uint64_t* qlinv, uint64_t* scratch, int row_done) {
     const uint32_t n = d->n, l = ell - 1;
     (void)pmod;
+    (void)row_done; /* never set: the oracle has no sfp_modup_inner */
     u64* s = (u64*)malloc((size_t)ell * n * 8);
     for (int p = 0; p < 2; ++p) {
         const u64* dp = p ? d1 : d0;
@@ -627,10 +629,10 @@ void sfp_load_i64(sfp_dev* d, uint64_t* p, const int64_t* c, sfp_limbs m) {
 /* no fused ModUp + inner product: the host layer runs sfp_modup + sfp_ks_inner* */
 int sfp_modup_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* in, uint32_t ell, uint32_t K,
                     uint32_t Lq, uint32_t alpha, const sfp_conv* const* convs, const uint64_t* key,
-                    const uint64_t* fold0, const uint64_t* fold1, uint64_t fold_k, int accum, uint64_t* ext,
-                    uint64_t* scratch) {
+                    const uint64_t* fold0, const uint64_t* fold1, uint64_t fold_k, int accum, uint32_t inv_from,
+                    uint64_t* ext, uint64_t* scratch) {
     (void)d; (void)acc0; (void)acc1; (void)in; (void)ell; (void)K; (void)Lq; (void)alpha; (void)convs;
-    (void)key; (void)fold0; (void)fold1; (void)fold_k; (void)accum; (void)ext; (void)scratch;
+    (void)key; (void)fold0; (void)fold1; (void)fold_k; (void)accum; (void)inv_from; (void)ext; (void)scratch;
     return -1;
 }
 

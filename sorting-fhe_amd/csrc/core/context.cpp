@@ -798,9 +798,13 @@ class SfheInternal {
     // inner product into acc (two polys of ell+K rows, (ell+K)*n apart):
     // accumulated when accum, + foldK * (fold0, fold1) on row ell-1 when
     // fold0.  One fused pass where the backend has it (sfp_modup_inner: the
-    // extended digits never round-trip through HBM), else ModUp + inner product.
-    static void modupInner(CC* cc, uint64_t* acc, const uint64_t* d, uint32_t ell, const DeviceBufferPtr& key,
-                           const uint64_t* fold0, const uint64_t* fold1, u64 foldK, int accum) {
+    // extended digits never round-trip through HBM), else ModUp + inner
+    // product.  invFrom: rows t >= invFrom may leave after the first pass of
+    // the ModDown's inverse NTT; returns whether they did (the ModDown's
+    // row_done).
+    static int modupInner(CC* cc, uint64_t* acc, const uint64_t* d, uint32_t ell, const DeviceBufferPtr& key,
+                          const uint64_t* fold0, const uint64_t* fold1, u64 foldK, int accum,
+                          uint32_t invFrom = ~0u) {
         SfheContextState* s = cc->st.get();
         const uint32_t n = s->n, K = s->K;
         const uint32_t beta = (ell + s->alpha - 1) / s->alpha;
@@ -809,8 +813,8 @@ class SfheInternal {
         auto scratch = s->alloc((size_t)ell * n);
         auto& convs = modupConv(cc, ell);
         if (sfp_modup_inner(s->dev, acc, acc + stride, d, ell, K, s->Lq, s->alpha, convs.data(), key->ptr, fold0,
-                            fold1, foldK, accum, ext->ptr, scratch->ptr) == 0)
-            return;
+                            fold1, foldK, accum, invFrom, ext->ptr, scratch->ptr) == 0)
+            return invFrom != ~0u;
         sfp_modup(s->dev, ext->ptr, d, ell, K, s->Lq, s->alpha, convs.data(), scratch->ptr);
         if (fold0)
             sfp_ks_inner_fold(s->dev, acc, acc + stride, ext->ptr, stride, key->ptr, beta, ell, K, s->Lq, fold0, fold1,
@@ -818,6 +822,7 @@ class SfheInternal {
         else
             (accum ? sfp_ks_inner_acc : sfp_ks_inner)(s->dev, acc, acc + stride, ext->ptr, stride, key->ptr, beta,
                                                        ell, K, s->Lq);
+        return 0;
     }
 
     // Hybrid key switch of d (ell limbs, evaluation domain) with `key`; the
@@ -830,10 +835,10 @@ class SfheInternal {
         const uint32_t beta = (ell + s->alpha - 1) / s->alpha;
         const size_t stride = (size_t)(ell + K) * n;
         auto acc = s->alloc(2 * stride);
-        modupInner(cc, acc->ptr, d, ell, key, nullptr, nullptr, 0, 0);
+        const int rowDone = modupInner(cc, acc->ptr, d, ell, key, nullptr, nullptr, 0, 0, ell);
         auto md = s->alloc((size_t)2 * ell * n);
         sfp_moddown2(s->dev, out0, out1, acc->ptr, stride, ell, K, s->Lq, s->moddownConv, s->pInvModQ.data(), add0,
-                     add1, md->ptr);
+                     add1, md->ptr, rowDone);
         s->stats.keyswitch++;
         // (3 l + 2 beta (l+K)) B
         s->countBytes((3.0 * ell + 2.0 * beta * (ell + K)) * n * 8);
@@ -855,12 +860,12 @@ class SfheInternal {
         const uint32_t beta = (ell + s->alpha - 1) / s->alpha;
         const size_t stride = (size_t)(ell + K) * n;
         auto acc = s->alloc(2 * stride);
-        modupInner(cc, acc->ptr, d2, ell, s->relinKey, d0, d1, s->pModQ[ell - 1], 0);
+        const int rowDone = modupInner(cc, acc->ptr, d2, ell, s->relinKey, d0, d1, s->pModQ[ell - 1], 0, ell - 1);
         Ct out = newCt(cc, level + 1, slots);
         auto scratch = s->alloc((size_t)2 * (ell - 1) * n);
         sfp_moddown_rescale(s->dev, out->c0, out->c1, d0, d1, acc->ptr, stride, ell, K, s->Lq,
                             s->moddownConv, s->pInvModQ.data(), s->pModQ.data(),
-                            s->qInvTable[ell].data(), scratch->ptr);
+                            s->qInvTable[ell].data(), scratch->ptr, rowDone);
         s->stats.keyswitch++;
         s->stats.rescale++;
         s->countBytes((3.0 * ell + 2.0 * beta * (ell + K)) * n * 8);
@@ -880,7 +885,7 @@ class SfheInternal {
                      s->Lq);
         auto scratch = s->alloc((size_t)2 * ell * n);
         sfp_moddown2(s->dev, out0, out1, acc->ptr, accStride, ell, K, s->Lq, s->moddownConv,
-                     s->pInvModQ.data(), add0, add1, scratch->ptr);
+                     s->pInvModQ.data(), add0, add1, scratch->ptr, 0);
     }
 
     static std::vector<sfp_conv*>& modupConv(CC* cc, uint32_t ell) {
@@ -2420,6 +2425,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotateSum(const std::vecto
     auto c0 = s->alloc((size_t)s->rows(ell) * n);
     auto ext = shard ? s->alloc(stride * beta) : nullptr;  // (the unsharded ModUp allocates its own)
     auto acc = s->alloc(2 * stride);
+    int rowDone = 0;
     for (size_t i = 0; i < rot.size(); ++i) {
         const Ciphertext<DCRTPoly>& x = a[rot[i]];
         const uint32_t gal = GaloisForRotation(r[rot[i]]);
@@ -2431,7 +2437,9 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotateSum(const std::vecto
             SfheInternal::modupShard(s, ext->ptr, t->ptr, ell);
             SfheInternal::innerShard(s, acc->ptr, ext->ptr, stride, beta, ell, *keys[i], i ? 1 : 0);
         } else {
-            SfheInternal::modupInner(this, acc->ptr, t->ptr, ell, *keys[i], nullptr, nullptr, 0, i ? 1 : 0);
+            // the last term's pass also runs the ModDown's first inverse pass on the P rows
+            rowDone = SfheInternal::modupInner(this, acc->ptr, t->ptr, ell, *keys[i], nullptr, nullptr, 0, i ? 1 : 0,
+                                               i + 1 == rot.size() ? ell : ~0u);
         }
         s->stats.automorph++;
         s->stats.keyswitch++;
@@ -2442,7 +2450,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotateSum(const std::vecto
     } else {
         auto md = s->alloc((size_t)2 * ell * n);
         sfp_moddown2(s->dev, out->c0, out->c1, acc->ptr, stride, ell, K, s->Lq, s->moddownConv,
-                     s->pInvModQ.data(), 1, 0, md->ptr);
+                     s->pInvModQ.data(), 1, 0, md->ptr, rowDone);
     }
     Ciphertext<DCRTPoly> res = SfheInternal::traced(this, out, "EvalRotateSum");
     for (size_t k : ident) res = EvalAdd(res, a[k]);
@@ -2542,7 +2550,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotMultAddHoisted(
     if (accOn) {
         auto scratch = s->alloc((size_t)2 * ell * n);
         sfp_moddown2(s->dev, t0, t1, acc->ptr, stride, ell, K, s->Lq, s->moddownConv, s->pInvModQ.data(), 1, 1,
-                     scratch->ptr);
+                     scratch->ptr, 0);
     }
     return SfheInternal::traced(this, SfheInternal::rescale(this, t0, t1, level, slots), "EvalRotMultAddHoisted");
 }

@@ -1010,6 +1010,12 @@ struct KsArgs {
     u64 foldK;
     uint32_t ell, Lq, alpha, beta;
     int accum;  // acc += the inner product
+    // rows t >= invFrom (the P limbs, and for a ModDown fused with its rescale
+    // the dropped q limb too) leave after the first pass of ModDown's inverse
+    // NTT (its ROW pass), which the ModDown then skips; ~0u: none
+    uint32_t invFrom;
+    const u64 *itw, *itwS;
+    const double* itwD;
 };
 
 template <int LE, int TILE>
@@ -1153,6 +1159,8 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt_ks(const KsArgs A, const sf_
     const bool fold = A.fold0 && t == A.ell - 1;
     u64* o0 = A.acc0 + (size_t)t * n + rowOff;
     u64* o1 = A.acc1 + (size_t)t * n + rowOff;
+    const bool inv = t >= A.invFrom;
+    ulonglong2 r[2][NPAIR];
 #pragma unroll
     for (int k = 0; k < NPAIR; ++k) {
         const uint32_t e = 2 * (threadIdx.x + k * NT);
@@ -1177,8 +1185,57 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt_ks(const KsArgs A, const sf_
             r1.x = sf_add(r1.x, p1.x, q);
             r1.y = sf_add(r1.y, p1.y, q);
         }
-        *reinterpret_cast<ulonglong2*>(o0 + e) = r0;
-        *reinterpret_cast<ulonglong2*>(o1 + e) = r1;
+        r[0][k] = r0;
+        r[1][k] = r1;
+        if (!inv) {
+            *reinterpret_cast<ulonglong2*>(o0 + e) = r0;
+            *reinterpret_cast<ulonglong2*>(o1 + e) = r1;
+        }
+    }
+    if (!inv) return;
+    // ModDown's inverse ROW pass on both accumulators' tiles (as k_ntt's first
+    // inverse pass: FP64 rows leave canonical, integer rows in [0, 2q))
+    const u64* iw = fp ? reinterpret_cast<const u64*>(A.itwD) + (size_t)prime * n : A.itw + (size_t)prime * n;
+    const u64* ix = A.itwS + (size_t)prime * n;
+    for (int p = 0; p < 2; ++p) {
+        __syncthreads();  // s is free (the last digit's readers, or the previous poly's writers)
+#pragma unroll
+        for (int k = 0; k < NPAIR; ++k) {
+            const uint32_t e = 2 * (threadIdx.x + k * NT);
+            if (fp) {
+                s[ldsSw(e)] = __double_as_longlong(u2d(r[p][k].x));
+                s[ldsSw(e + 1)] = __double_as_longlong(u2d(r[p][k].y));
+            } else {
+                s[ldsSw(e)] = r[p][k].x;
+                s[ldsSw(e + 1)] = r[p][k].y;
+            }
+        }
+        __syncthreads();
+        const uint32_t nr = (8 + LE - 1) / LE;
+        for (uint32_t ri = 0; ri < nr; ++ri) {
+            const uint32_t rr = nr - 1 - ri;
+            const uint32_t k0 = LE * rr;
+            const int b = (int)min((uint32_t)LE, 8u - k0);
+            if (fp)
+                nttRoundDynFP<true, false, LE, TILE>(b, reinterpret_cast<double*>(s), T, S0, k0, qd,
+                                                     reinterpret_cast<const double*>(iw), qi);
+            else
+                nttRoundDyn<true, false, LE, TILE>(b, s, T, S0, k0, q, iw, ix);
+            __syncthreads();
+        }
+        u64* o = p ? o1 : o0;
+#pragma unroll
+        for (int k = 0; k < NPAIR; ++k) {
+            const uint32_t e = 2 * (threadIdx.x + k * NT);
+            ulonglong2 x;
+            x.x = s[ldsSw(e)];
+            x.y = s[ldsSw(e + 1)];
+            if (fp) {
+                x.x = d2u(fpReduce(__longlong_as_double(x.x), qd, qi));
+                x.y = d2u(fpReduce(__longlong_as_double(x.y), qd, qi));
+            }
+            *reinterpret_cast<ulonglong2*>(o + e) = x;
+        }
     }
 }
 
@@ -2610,15 +2667,16 @@ static RowGroup rowsOf(uint32_t P, uint32_t R, sfp_limbs pm) {
     return G;
 }
 
-// Both passes of a (batched) NTT over the rows of G (firstOnly: only the first
-// pass -- the forward COL pass -- whose output a fused second pass consumes).
-static void nttRows(sfp_dev* d, const RowGroup& G, int inverse, bool firstOnly = false) {
+// Both passes of a (batched) NTT over the rows of G -- or only the first
+// (passes == 1: its output feeds a fused second pass, k_ntt_ks) or only the
+// second (passes == 2: a fused kernel ran the first).
+static void nttRows(sfp_dev* d, const RowGroup& G, int inverse, int passes = 3) {
     const uint32_t rows = G.P * G.R;
     if (!rows || !limbsOk(d, G.pm, "ntt")) return;
     if (G.lift && G.liftPrime >= d->np) return (void)limbsOk(d, sfp_limbs{1, 1, G.liftPrime, G.liftPrime}, "ntt lift");
     const double bytes = 16.0 * rows * d->n;
-    if (firstOnly && (d->n <= (uint32_t)kNttTile || inverse)) {
-        record(d, "ntt (first pass alone: forward, rings above one tile only)", hipErrorInvalidValue);
+    if (passes != 3 && d->n <= (uint32_t)kNttTile) {
+        record(d, "ntt (a single pass: rings above one tile only)", hipErrorInvalidValue);
         return;
     }
     if (d->n <= (uint32_t)kNttTile) {  // small rings: one single-pass block per row
@@ -2661,7 +2719,7 @@ static void nttRows(sfp_dev* d, const RowGroup& G, int inverse, bool firstOnly =
     const bool small = rows < (uint32_t)kNttSmallRows;
     int npass = 0;
     auto pass = [&](auto kern, int threads) {
-        if (firstOnly && npass++ > 0) return;
+        if (!((passes >> npass++) & 1)) return;
         timedLaunch(d, SFP_FAM_NTT, bytes, [&] {
             hipLaunchKernelGGL(kern, g, dim3(threads), 0, d->st(), G, d->bar, tw, twS, d->ninv,
                                d->ninvS, d->logn, twD, d->qinvD, d->ninvD, d->ninvQ, nttFp());
@@ -3409,8 +3467,8 @@ void sfp_modup(sfp_dev* d, uint64_t* ext, const uint64_t* in, uint32_t ell, uint
 
 int sfp_modup_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* in, uint32_t ell, uint32_t K,
                     uint32_t Lq, uint32_t alpha, const sfp_conv* const* convs, const uint64_t* key,
-                    const uint64_t* fold0, const uint64_t* fold1, uint64_t foldK, int accum, uint64_t* ext,
-                    uint64_t* scr) {
+                    const uint64_t* fold0, const uint64_t* fold1, uint64_t foldK, int accum, uint32_t invFrom,
+                    uint64_t* ext, uint64_t* scr) {
     static const bool on = [] {  // SFHE_KS_FUSE=0: the unfused sequence (A/B)
         const char* v = std::getenv("SFHE_KS_FUSE");
         return !v || *v != '0';
@@ -3440,7 +3498,7 @@ int sfp_modup_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* 
     B.src = B.dst = RowPtr{ext, stride, (long long)n};
     B.skipEll = ell;
     B.alpha = alpha;
-    nttRows(d, B, 0, true);
+    nttRows(d, B, 0, 1);
     KsArgs a;
     a.in = in;
     a.ext = ext;
@@ -3458,6 +3516,10 @@ int sfp_modup_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* 
     a.alpha = alpha;
     a.beta = beta;
     a.accum = accum;
+    a.invFrom = invFrom;
+    a.itw = d->ipsi;
+    a.itwS = d->ipsiS;
+    a.itwD = d->ipsiD;
     const uint32_t rows = ell + K;
     const size_t total = (size_t)rows * n;
     const bool t1k = rows <= 64 && n <= 1024u * 128u;
@@ -3524,7 +3586,7 @@ void sfp_ks_inner_mul(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t
 
 void sfp_moddown2(sfp_dev* d, uint64_t* out0, uint64_t* out1, uint64_t* acc, size_t accStride,
                   uint32_t ell, uint32_t K, uint32_t Lq, const sfp_conv* c, const uint64_t* pinv,
-                  int add0, int add1, uint64_t* scr) {
+                  int add0, int add1, uint64_t* scr, int rowDone) {
     const uint32_t n = d->n;
     if (ell > SFP_MAX_LIMBS) {
         record(d, "moddown (too many limbs)", hipErrorInvalidValue);
@@ -3533,7 +3595,7 @@ void sfp_moddown2(sfp_dev* d, uint64_t* out0, uint64_t* out1, uint64_t* acc, siz
     u64* pRows = acc + (size_t)ell * n;
     RowGroup A = rowsOf(2, K, sfp_limbs{K, 0, Lq, 0});
     A.src = A.dst = RowPtr{pRows, (long long)accStride, (long long)n};
-    nttRows(d, A, 1);
+    nttRows(d, A, 1, rowDone ? 2 : 3);
     ConvJobs J;
     J.j[0] = convJob(c, scr, pRows, ell, 1);
     J.j[1] = convJob(c, scr + (size_t)ell * n, pRows + accStride, ell, 1);
@@ -3554,7 +3616,7 @@ void sfp_moddown2(sfp_dev* d, uint64_t* out0, uint64_t* out1, uint64_t* acc, siz
 void sfp_moddown_rescale(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint64_t* d0,
                          const uint64_t* d1, uint64_t* acc, size_t accStride, uint32_t ell,
                          uint32_t K, uint32_t Lq, const sfp_conv* c, const uint64_t* pinv,
-                         const uint64_t* pmod, const uint64_t* qlinv, uint64_t* scr) {
+                         const uint64_t* pmod, const uint64_t* qlinv, uint64_t* scr, int rowDone) {
     const uint32_t n = d->n, l = ell - 1;
     if (ell < 2 || ell > SFP_MAX_LIMBS || !c || c->ns > (uint32_t)kMaxConvSrc || c->nt < ell ||
         !limbsOk(d, sfp_limbs{K + 1, 1, Lq, l}, "moddown_rescale")) {
@@ -3564,7 +3626,7 @@ void sfp_moddown_rescale(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint6
     // INTT of rows [l, ell+K) of both accumulators: the dropped q row and the P rows
     RowGroup A = rowsOf(2, K + 1, sfp_limbs{K + 1, 1, Lq, l});
     A.src = A.dst = RowPtr{acc + (size_t)l * n, (long long)accStride, (long long)n};
-    nttRows(d, A, 1);
+    nttRows(d, A, 1, rowDone ? 2 : 3);
     // conversion + the dropped row's lift
     MdrsArgs M;
     for (int p = 0; p < 2; ++p) {

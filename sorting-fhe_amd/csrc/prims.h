@@ -181,14 +181,17 @@ void sfp_modup(sfp_dev* d, uint64_t* ext, const uint64_t* in, uint32_t ell, uint
 // ModUp fused with the key inner product (one key switch's ModUp + inner
 // product without the extended digits' round trip through HBM): the same
 // acc0 / acc1 as sfp_modup followed by sfp_ks_inner_fold (fold0 != NULL),
-// sfp_ks_inner_acc (accum) or sfp_ks_inner.  ext: beta * (ell+K) * n words
-// of scratch (the COL-pass intermediate), scr: ell * n words.  Returns -1
-// (and does nothing) where the backend has no fused form -- rings of one NTT
-// tile, SFHE_KS_FUSE=0, the oracle -- and the caller runs the unfused prims.
+// sfp_ks_inner_acc (accum) or sfp_ks_inner -- except that the rows
+// t >= inv_from (the P rows: ell; with the dropped q row: ell - 1; UINT32_MAX:
+// none) leave after the first (ROW) pass of ModDown's inverse NTT, so the
+// ModDown that follows is called with row_done = 1.  ext: beta * (ell+K) * n
+// words of scratch (the COL-pass intermediate), scr: ell * n words.  Returns
+// -1 (and does nothing) where the backend has no fused form -- rings of one
+// NTT tile, SFHE_KS_FUSE=0, the oracle -- and the caller runs the unfused prims.
 int sfp_modup_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* in, uint32_t ell, uint32_t K,
                     uint32_t Lq, uint32_t alpha, const sfp_conv* const* convs, const uint64_t* key,
-                    const uint64_t* fold0, const uint64_t* fold1, uint64_t fold_k, int accum, uint64_t* ext,
-                    uint64_t* scratch);
+                    const uint64_t* fold0, const uint64_t* fold1, uint64_t fold_k, int accum, uint32_t inv_from,
+                    uint64_t* ext, uint64_t* scratch);
 
 // Key inner product:  acc0 = sum_j ext_j * kb_j,  acc1 = sum_j ext_j * ka_j
 //   ext  : beta extended polys, each (ell+K) limbs, stride ext_stride.
@@ -218,9 +221,11 @@ void sfp_ks_inner_acc(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t
 //         acc_1 = acc + acc_stride; their P rows are destroyed.
 //   add0/add1: accumulate into out0/out1 instead of overwriting.
 //   pinv: host array ell of P^{-1} mod q_i.  scratch: 2*ell*n words.
+//   row_done: the P rows already had their inverse NTT's first pass
+//   (sfp_modup_inner with inv_from = ell).
 void sfp_moddown2(sfp_dev* d, uint64_t* out0, uint64_t* out1, uint64_t* acc, size_t acc_stride,
                   uint32_t ell, uint32_t K, uint32_t Lq, const sfp_conv* c, const uint64_t* pinv,
-                  int add0, int add1, uint64_t* scratch);
+                  int add0, int add1, uint64_t* scratch, int row_done);
 
 // sfp_ks_inner that also folds the relinearised polys' last q row into the
 // accumulators: acc_p,l += fold_k * fold_p,l  (l = ell-1, fold_k = P mod q_l),
@@ -239,11 +244,12 @@ void sfp_ks_inner_fold(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_
 // the conversion, and out_i = (acc_i - NTT(conv_i + P [r]_i)) (P q_l)^-1
 // + d_i q_l^-1 needs one NTT instead of two.
 //   pinv[i] = P^-1, pmod[i] = P mod q_i (i < ell);  qlinv[i] = q_l^-1 mod q_i
-//   (i < l).  acc is destroyed.  scratch: 2*l*n words.
+//   (i < l).  acc is destroyed.  scratch: 2*l*n words.  row_done: rows
+//   [l, ell+K) already had their inverse NTT's first pass (inv_from = l).
 void sfp_moddown_rescale(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint64_t* d0,
                          const uint64_t* d1, uint64_t* acc, size_t acc_stride, uint32_t ell,
                          uint32_t K, uint32_t Lq, const sfp_conv* c, const uint64_t* pinv,
-                         const uint64_t* pmod, const uint64_t* qlinv, uint64_t* scratch);
+                         const uint64_t* pmod, const uint64_t* qlinv, uint64_t* scratch, int row_done);
 
 // ---- sampling (counter-based, deterministic) ------------------------------------
 // Uniform residues mod each limb's prime: value for (limb, i) is derived from

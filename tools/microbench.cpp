@@ -141,7 +141,7 @@ int main(int argc, char** argv) {
     });
     const double md = timeIt(d, 30, [&] {
         sfp_moddown2(d, out, out + (size_t)ell * n, acc, stride, ell, K, s->Lq, s->moddownConv,
-                     s->pInvModQ.data(), 1, 1, scr);
+                     s->pInvModQ.data(), 1, 1, scr, 0);
     });
     const double rs = timeIt(d, 30, [&] {
         sfp_rescale(d, out, buf, ell, s->qInvTable[ell].data(), 2, (size_t)ell * n, (size_t)(ell - 1) * n);
