@@ -90,6 +90,10 @@ int sfhe_sync(sfhe_ctx* c);
 /* counts[9]: keyswitch, rescale, tensor, ptmult, constmult, add, automorph,
  * ntt_limbs, wsum_terms; bytes: algorithmic HBM bytes (SURVEY §8(d) model). */
 int sfhe_op_stats(sfhe_ctx* c, uint64_t* counts, double* bytes, int reset);
+/* Bootstrap shapes (input level, iterations, precision) replayed from a
+ * captured hipGraph so far (the first call of a shape runs eagerly, the
+ * second is captured). */
+int sfhe_bootstrap_graphs(sfhe_ctx* c, uint64_t* count);
 /* Plaintext encodings done on the device (sfp_encode) and on the host since
  * the last sfhe_op_stats reset. */
 int sfhe_encode_counts(sfhe_ctx* c, uint64_t* device, uint64_t* host);

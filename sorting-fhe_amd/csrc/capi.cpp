@@ -268,6 +268,12 @@ int sfhe_op_stats(sfhe_ctx* c, uint64_t* counts, double* bytes, int reset) {
     return SFHE_OK;
 }
 
+int sfhe_bootstrap_graphs(sfhe_ctx* c, uint64_t* count) {
+    REQUIRE(c && count, "null argument");
+    *count = c->cc->BootstrapGraphs();
+    return SFHE_OK;
+}
+
 int sfhe_encode_counts(sfhe_ctx* c, uint64_t* device, uint64_t* host) {
     REQUIRE(c && device && host, "null argument");
     auto s = c->cc->GetOpStats();

@@ -99,6 +99,18 @@ struct Group {
 using boot::Group;
 
 struct BootstrapPrecomp {
+    // hipGraph replay of EvalBootstrap (BASELINE config 4): the op sequence of
+    // a bootstrap depends only on (input level, iterations, precision), so the
+    // first call of a shape runs eagerly (it encodes the diagonals), the
+    // second is captured over a graph-owned input buffer, later calls copy
+    // their input in and replay
+    struct Replay {
+        int uses = 0;
+        bool off = false;
+        std::shared_ptr<CryptoContextImpl<DCRTPoly>::CapturedGraph> g;
+        Ciphertext<DCRTPoly> in, out;
+    };
+    std::map<std::tuple<uint32_t, uint32_t, uint32_t>, Replay> replays;
     uint32_t slots = 0, gap = 0;
     std::vector<Group> c2s, s2c;        // in application order
     std::map<double, Group> s2cFirst;   // s2c[0] with the output factor folded in, per factor
@@ -400,14 +412,66 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalBootstrap(const Ciphertext
     if (trace) {
         Synchronize();
         const auto t0 = std::chrono::steady_clock::now();
-        auto out = bootstrapIters(ct, numIterations, precision);
+        auto out = bootstrapReplay(ct, numIterations, precision);
         Synchronize();
         std::fprintf(stderr, "BOOT %.3f ms level %u -> %u\n",
                      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(),
                      ct->GetLevel(), out->GetLevel());
         return out;
     }
-    return bootstrapIters(ct, numIterations, precision);
+    return bootstrapReplay(ct, numIterations, precision);
+}
+
+// EvalBootstrap through its captured graph where it can be (see
+// BootstrapPrecomp::Replay): not inside another capture (its launches are then
+// part of that graph), a lane region, or with SFHE_GRAPH=0.
+Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::bootstrapReplay(const Ciphertext<DCRTPoly>& ct,
+                                                                  uint32_t numIterations, uint32_t precision) {
+    SfheContextState* s = st.get();
+    OpLock lk(s);
+    auto it = s->boot.find(ct->GetSlots());
+    const char* gv = std::getenv("SFHE_GRAPH");
+    if (it == s->boot.end() || (gv && *gv == '0') || s->capturing || s->forkedLanes)
+        return bootstrapIters(ct, numIterations, precision);
+    BootstrapPrecomp::Replay& r = it->second->replays[std::make_tuple(ct->GetLevel(), numIterations, precision)];
+    if (r.off || r.uses++ == 0) return bootstrapIters(ct, numIterations, precision);
+    if (!r.g) {  // second call of this shape: capture
+        Settle(ct);  // the graph reads canonical rows (a lazy input's rescale stays outside)
+        r.in = ct->Clone();
+        Settle(r.in);
+        if (!BeginCapture()) {
+            r.off = true;
+            return bootstrapIters(ct, numIterations, precision);
+        }
+        Ciphertext<DCRTPoly> out;
+        try {
+            out = bootstrapIters(r.in, numIterations, precision);
+        } catch (...) {
+            EndCapture(nullptr);
+            r.off = true;
+            throw;
+        }
+        r.g = EndCapture(out);
+        if (!r.g) {
+            r.off = true;
+            r.in.reset();
+            return bootstrapIters(ct, numIterations, precision);
+        }
+        r.out = out;
+    } else {
+        CopyCiphertextInto(r.in, ct);
+    }
+    Launch(r.g);
+    auto res = r.out->Clone();
+    res->SetSlots(r.out->GetSlots());
+    return res;
+}
+
+size_t CryptoContextImpl<DCRTPoly>::BootstrapGraphs() const {
+    size_t k = 0;
+    for (const auto& [slots, b] : st->boot)
+        for (const auto& [key, r] : b->replays) k += r.g ? 1 : 0;
+    return k;
 }
 
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::bootstrapIters(const Ciphertext<DCRTPoly>& ct,

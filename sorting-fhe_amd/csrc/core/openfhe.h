@@ -440,6 +440,11 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
     Ciphertext<DCRTPoly> BootstrapOnce(const Ciphertext<DCRTPoly>& ct, double inFactor, double outFactor);
     // EvalBootstrap's passes (meta-bootstrapping for numIterations >= 2)
     Ciphertext<DCRTPoly> bootstrapIters(const Ciphertext<DCRTPoly>& ct, uint32_t numIterations, uint32_t precision);
+    // ... replayed from a hipGraph captured per (input level, iterations,
+    // precision) after the first eager call of that shape (bootstrap.cpp)
+    Ciphertext<DCRTPoly> bootstrapReplay(const Ciphertext<DCRTPoly>& ct, uint32_t numIterations, uint32_t precision);
+    // bootstrap shapes replayed from a captured graph so far
+    size_t BootstrapGraphs() const;
 
     // ---------------- engine extensions (not OpenFHE) ----------------
     SfheContextState* state() const { return st.get(); }

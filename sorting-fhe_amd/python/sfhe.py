@@ -42,7 +42,7 @@ ABI_SYMBOLS = [
     "sfhe_sorter_sort_bitonic", "sfhe_kway_sort", "sfhe_kway_params",
     "sfhe_save", "sfhe_load", "sfhe_ct_save", "sfhe_ct_load",
     "sfhe_kway_create", "sfhe_kway_run", "sfhe_kway_destroy", "sfhe_shard_tail",
-    "sfhe_encode_counts",
+    "sfhe_encode_counts", "sfhe_bootstrap_graphs",
 ]
 
 
@@ -150,6 +150,7 @@ _SIGS = {
     "sfhe_shard_host": (C.c_int, [_VP, C.c_int, C.c_int, _AG, _BC, _VP]),
     "sfhe_shard_tail": (C.c_int, [_VP, _PU32]),
     "sfhe_encode_counts": (C.c_int, [_VP, _PU64, _PU64]),
+    "sfhe_bootstrap_graphs": (C.c_int, [_VP, _PU64]),
 }
 
 _libs: dict = {}
@@ -394,6 +395,12 @@ class Engine:
     def bootstrap_depth(self, level_budget=(5, 5), slots: int = 0) -> int:
         v = C.c_uint32()
         self._chk(self.lib.sfhe_bootstrap_depth(self.ctx, level_budget[0], level_budget[1], slots, C.byref(v)))
+        return v.value
+
+    def bootstrap_graphs(self) -> int:
+        """Bootstrap shapes replayed from a captured hipGraph so far."""
+        v = C.c_uint64()
+        self._chk(self.lib.sfhe_bootstrap_graphs(self.ctx, C.byref(v)))
         return v.value
 
     def bootstrap(self, a, iterations: int = 1, precision: int = 0):

@@ -149,3 +149,31 @@ def test_bootstrap_ring17(hip_lib, S, budget, depth, iters, secure, bound):
     print(f"bootstrap 2^17 S={S} {budget} x{iters}: {dt * 1e3:.0f} ms, max err {err:.3g} (log2 {np.log2(err):.1f})")
     assert out.level == e.bootstrap_depth(budget, S)
     assert err < bound
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("iters", [1, 2])
+def test_bootstrap_graph_replay(hip_lib, monkeypatch, iters):
+    """EvalBootstrap replays a captured hipGraph (BASELINE config 4's
+    "hipGraph capture"): the first bootstrap of a shape (input level,
+    iterations, precision) runs eagerly, the second is captured, later ones
+    copy their input into the graph and replay -- each bit-identical to the
+    eager bootstrap of the same input, and a fresh input through the graph
+    decrypts within the bootstrap bound."""
+    monkeypatch.setenv("SFHE_GRAPH", "1")
+    S = 16
+    e = boot_engine("hip", 14, S, 40, (2, 2))
+    rng = np.random.default_rng(3)
+    x = rng.uniform(-1, 1, S)
+    ct = e.mult_const(e.encrypt(x.tolist()), 1.0)
+    outs = [e.bootstrap(ct, iters).download() for _ in range(3)]  # eager, captured, replayed
+    assert e.bootstrap_graphs() == 1
+    monkeypatch.setenv("SFHE_GRAPH", "0")
+    eager = e.bootstrap(ct, iters).download()
+    for o in outs:
+        assert np.array_equal(o, eager)
+    monkeypatch.setenv("SFHE_GRAPH", "1")
+    y = rng.uniform(-1, 1, S)
+    out = e.bootstrap(e.mult_const(e.encrypt(y.tolist()), 1.0), iters)
+    err = float(np.max(np.abs(np.array(e.decrypt(out))[:S] - y)))
+    assert err < (2.0 ** -15 if iters == 1 else 2.0 ** -25), err
