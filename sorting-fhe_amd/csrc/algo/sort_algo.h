@@ -306,8 +306,8 @@ class DirectSort : public SortBase<N> {
         if (v.empty()) return {};
         const long n = (long)v.size();
         long s = ((r % n) + n) % n;
-        std::vector<double> out(v.size());
-        for (long i = 0; i < n; ++i) out[i] = v[(i + s) % n];
+        std::vector<double> out(v.size());  // out[i] = v[(i + s) mod n]
+        std::rotate_copy(v.begin(), v.begin() + s, v.end(), out.begin());
         return out;
     }
 

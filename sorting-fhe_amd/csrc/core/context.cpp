@@ -1076,14 +1076,17 @@ class SfheInternal {
         uint64_t h = 1469598103934665603ull;
         if (s->ptCacheOn) {
             auto mix = [&](uint64_t x) { h = (h ^ x) * 1099511628211ull; };
-            for (auto& c : pt->values) {
-                uint64_t b[2];
-                double re = c.real(), im = c.imag();
-                std::memcpy(&b[0], &re, 8);
-                std::memcpy(&b[1], &im, 8);
-                mix(b[0]);
-                mix(b[1]);
-            }
+            // four independent FNV lanes over the values' words (one serial
+            // multiply chain per word was the cold sort's largest host cost
+            // after the encoding moved to the device), folded at the end
+            const uint64_t* wv = reinterpret_cast<const uint64_t*>(pt->values.data());
+            const size_t nw = 2 * pt->values.size();
+            uint64_t ln[4] = {h, h ^ 1, h ^ 2, h ^ 3};
+            size_t i = 0;
+            for (; i + 4 <= nw; i += 4)
+                for (int k = 0; k < 4; ++k) ln[k] = (ln[k] ^ wv[i + k]) * 1099511628211ull;
+            for (; i < nw; ++i) ln[0] = (ln[0] ^ wv[i]) * 1099511628211ull;
+            for (int k = 0; k < 4; ++k) mix(ln[k]);
             mix(pt->slots);
             mix(level);
             mix(pt->values.size());
