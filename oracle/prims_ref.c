@@ -636,6 +636,18 @@ int sfp_modup_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* 
     return -1;
 }
 
+/* no fused tensor + relinearisation + rescale: the host layer runs the prims */
+int sfp_mult_relin_rescale(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint64_t* a0, const uint64_t* a1,
+                           const uint64_t* b0, const uint64_t* b1, uint32_t ell, uint32_t K, uint32_t Lq,
+                           uint32_t alpha, const sfp_conv* const* convs, const uint64_t* key, const sfp_conv* c,
+                           const uint64_t* pinv, const uint64_t* pmod, const uint64_t* qlinv, uint64_t* acc,
+                           uint64_t* ext, uint64_t* scratch) {
+    (void)d; (void)out0; (void)out1; (void)a0; (void)a1; (void)b0; (void)b1; (void)ell; (void)K; (void)Lq;
+    (void)alpha; (void)convs; (void)key; (void)c; (void)pinv; (void)pmod; (void)qlinv; (void)acc; (void)ext;
+    (void)scratch;
+    return -1;
+}
+
 /* ---- CKKS encoding (sfp_encode): the host encoder's special inverse FFT
  * (csrc/core/encoder.cpp fftSpecialInv) restated in C, then round and reduce
  * as sfp_load_i64.  Built with -ffp-contract=off: no fused multiply-add. */

@@ -873,6 +873,43 @@ class SfheInternal {
         return out;
     }
 
+    // EvalMult(ct, ct)'s whole canonical tail from the aligned operands
+    // (a0, a1), (b0, b1) at `level`: one fused pass chain where the backend
+    // has it (sfp_mult_relin_rescale: the tensor is formed inside the key
+    // switch's passes, never written out), else the tensor then relinRescale.
+    static Ct multRelinRescale(CC* cc, const uint64_t* a0, const uint64_t* a1, const uint64_t* b0,
+                               const uint64_t* b1, uint32_t level, uint32_t slots) {
+        SfheContextState* s = cc->st.get();
+        const uint32_t ell = s->ellOf(level);
+        if (ell < 2) SFHE_THROW("no levels left to rescale (multiplicative depth exhausted)");
+        const size_t pw = s->polyWords(level);
+        if (!s->shardAt(ell)) {
+            const uint32_t n = s->n, K = s->K, beta = (ell + s->alpha - 1) / s->alpha;
+            const size_t stride = (size_t)(ell + K) * n;
+            Ct out = newCt(cc, level + 1, slots);
+            auto acc = s->alloc(2 * stride);
+            auto ext = s->alloc(stride * beta);
+            auto scratch = s->alloc((size_t)2 * ell * n);
+            auto& convs = modupConv(cc, ell);
+            if (sfp_mult_relin_rescale(s->dev, out->c0, out->c1, a0, a1, b0, b1, ell, K, s->Lq, s->alpha,
+                                       convs.data(), s->relinKey->ptr, s->moddownConv, s->pInvModQ.data(),
+                                       s->pModQ.data(), s->qInvTable[ell].data(), acc->ptr, ext->ptr,
+                                       scratch->ptr) == 0) {
+                s->stats.keyswitch++;
+                s->stats.rescale++;
+                s->countBytes((3.0 * ell + 2.0 * beta * (ell + K)) * n * 8);
+                s->countBytes(4.0 * ell * n * 8);
+                return out;
+            }
+        }
+        auto t = s->alloc(3 * pw);
+        uint64_t* d0 = t->ptr;
+        uint64_t* d1 = d0 + pw;
+        uint64_t* d2 = d1 + pw;
+        sfp_tensor(s->dev, d0, d1, d2, a0, a1, b0, b1, s->qmap(ell));
+        return relinRescale(cc, d0, d1, d2, level, slots);
+    }
+
     static void innerAndModDown(CC* cc, const uint64_t* ext, size_t stride, uint32_t beta,
                                 uint32_t ell, const DeviceBufferPtr& key, uint64_t* out0,
                                 uint64_t* out1, int add0, int add1) {
@@ -1312,21 +1349,27 @@ struct DeferredMacPlain : DeferredOp {
     }
 };
 
-// EvalMult(ct, ct): tensor done; relinearisation (+ rescale) deferred
+// EvalMult(ct, ct): the tensor, relinearisation and rescale deferred to the
+// first consumer (the canonical form runs them as one fused chain,
+// multRelinRescale; the pending form needs the tensor's rows)
 struct DeferredRelin : DeferredOp {
-    DeviceBufferPtr t;  // d0, d1, d2 (polyWords(level) apart)
+    DeviceBufferPtr pa, pb;  // the aligned operands' rows, pinned
+    const uint64_t *a0, *a1, *b0, *b1;
     uint32_t level, slots;
     void run(CCI* cc, CtI& ct, bool pending) override {
         SfheContextState* s = cc->state();
-        s->dep(t.get());
+        s->dep(pa.get());
+        s->dep(pb.get());
+        if (!pending) {
+            SfheInternal::adopt(ct, SfheInternal::multRelinRescale(cc, a0, a1, b0, b1, level, slots));
+            return;
+        }
         const size_t pw = s->polyWords(level);
+        auto t = s->alloc(3 * pw);
         uint64_t* d0 = t->ptr;
         uint64_t* d1 = d0 + pw;
         uint64_t* d2 = d1 + pw;
-        if (!pending) {
-            SfheInternal::adopt(ct, SfheInternal::relinRescale(cc, d0, d1, d2, level, slots));
-            return;
-        }
+        sfp_tensor(s->dev, d0, d1, d2, a0, a1, b0, b1, s->qmap(s->ellOf(level)));
         SfheInternal::keySwitch(cc, d2, s->ellOf(level), s->relinKey, d0, d1, 1, 1);
         SfheInternal::adoptPending(ct, t, d0, d1);
     }
@@ -2185,24 +2228,29 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMult(const Ciphertext<DCRT
     const uint32_t ell = s->ellOf(a->level);
     if (ell < 2) SFHE_THROW("no levels left (multiplicative depth exhausted)");
     const size_t pw = s->polyWords(a->level);
-    auto t = s->alloc(3 * pw);
-    uint64_t* d0 = t->ptr;
-    uint64_t* d1 = d0 + pw;
-    uint64_t* d2 = d1 + pw;
-    sfp_tensor(s->dev, d0, d1, d2, a->c0, a->c1, b->c0, b->c1, st->qmap(ell));
     s->stats.tensor++;
     s->countBytes(7.0 * ell * s->n * 8);
     const uint32_t slots = std::max(a->slots, b->slots);
     if (SfheInternal::lazy(s) && SfheInternal::fusedRescale()) {
         auto op = std::make_shared<DeferredRelin>();
-        op->t = t;
+        op->pa = a->buf;
+        op->pb = b->buf;
+        op->a0 = a->c0;
+        op->a1 = a->c1;
+        op->b0 = b->c0;
+        op->b1 = b->c1;
         op->level = a->level;
         op->slots = slots;
         return SfheInternal::deferredCt(this, a->level + 1, slots, op);
     }
     if (SfheInternal::fusedRescale())
-        return SfheInternal::traced(this, SfheInternal::relinRescale(this, d0, d1, d2, a->level, slots),
-                                    "EvalMult");
+        return SfheInternal::traced(
+            this, SfheInternal::multRelinRescale(this, a->c0, a->c1, b->c0, b->c1, a->level, slots), "EvalMult");
+    auto t = s->alloc(3 * pw);
+    uint64_t* d0 = t->ptr;
+    uint64_t* d1 = d0 + pw;
+    uint64_t* d2 = d1 + pw;
+    sfp_tensor(s->dev, d0, d1, d2, a->c0, a->c1, b->c0, b->c1, st->qmap(ell));
     SfheInternal::keySwitch(this, d2, ell, s->relinKey, d0, d1, 1, 1);
     return SfheInternal::traced(this, SfheInternal::rescale(this, d0, d1, a->level, slots), "EvalMult");
 }

@@ -625,6 +625,11 @@ struct RowGroup {
     uint32_t lift, liftPrime;
     uint32_t epi, addMask;  // addMask bit p: accumulate into eout for polynomial p
     RowPtr eadd;            // epi with eadd.base: eout += eadd * k2_i
+    // epi with tA0: eadd is the tensor product of (tA0, tA1) and (tB0, tB1)
+    // formed here (row i, n words per row): a0 b0 for polynomial 0, a0 b1 +
+    // a1 b0 for polynomial 1 (sfp_mult_relin_rescale: the tensor is never
+    // written out)
+    const u64 *tA0, *tA1, *tB0, *tB1;
     // multipliers (a rescale fused with the product before it):
     //   pre / preK: the first pass reads src * pre (elementwise) or src * preK_i
     //   emul / emK: the epilogue uses ein * emul or ein * emK_i in place of ein
@@ -830,11 +835,13 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_b
     const u64* ein = epi ? rowAt(G.ein, pp, ii) : nullptr;
     const u64 ek = epi ? G.k[ii] : 0, ekS = epi ? G.kS[ii] : 0;
     const u64* ead = epi && G.eadd.base ? rowAt(G.eadd, pp, ii) : nullptr;
-    const u64 ek2 = ead ? G.k2[ii] : 0, ek2S = ead ? G.k2S[ii] : 0;
+    const bool tens = epi && G.tA0;
+    const u64 ek2 = (ead || tens) ? G.k2[ii] : 0, ek2S = (ead || tens) ? G.k2S[ii] : 0;
     const u64* emul = epi && G.emul.base ? rowAt(G.emul, pp, ii) : nullptr;
     const bool emK = epi && G.emK;
     const u64 emk = emK ? G.emK[ii] : 0, emkS = emK ? G.emKS[ii] : 0;
-    const sf_barrett EB = emul ? loadBar(bar, prime) : sf_barrett{};
+    const sf_barrett EB = (emul || tens) ? loadBar(bar, prime) : sf_barrett{};
+    const size_t trow = (size_t)ii << logn;
 #pragma unroll
     for (int k = 0; k < (1 << LE) / 2; ++k) {
         const uint32_t e = 2 * (threadIdx.x + k * (TILE >> LE));
@@ -880,8 +887,28 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_b
                 x.x = sf_add(x.x, o.x, q);
                 x.y = sf_add(x.y, o.y, q);
             }
-            if (ead) {
-                const ulonglong2 o = *reinterpret_cast<const ulonglong2*>(ead + g);
+            if (ead || tens) {
+                ulonglong2 o;
+                if (tens) {  // the tensor product's polynomial pp at (row ii, g)
+                    const ulonglong2 a0 = *reinterpret_cast<const ulonglong2*>(G.tA0 + trow + g);
+                    const ulonglong2 b0 = *reinterpret_cast<const ulonglong2*>(G.tB0 + trow + g);
+                    if (pp == 0) {
+                        o.x = bmul(a0.x, b0.x, EB);
+                        o.y = bmul(a0.y, b0.y, EB);
+                    } else {
+                        const ulonglong2 a1 = *reinterpret_cast<const ulonglong2*>(G.tA1 + trow + g);
+                        const ulonglong2 b1 = *reinterpret_cast<const ulonglong2*>(G.tB1 + trow + g);
+                        Acc t{0, 0}, u{0, 0};
+                        macc(t, a0.x, b1.x);
+                        macc(t, a1.x, b0.x);
+                        macc(u, a0.y, b1.y);
+                        macc(u, a1.y, b0.y);
+                        o.x = sf_reduce128_acc(t.lo, t.hi, &EB);
+                        o.y = sf_reduce128_acc(u.lo, u.hi, &EB);
+                    }
+                } else {
+                    o = *reinterpret_cast<const ulonglong2*>(ead + g);
+                }
                 x.x = sf_add(x.x, sf_mul_shoup(o.x, ek2, ek2S, q), q);
                 x.y = sf_add(x.y, sf_mul_shoup(o.y, ek2, ek2S, q), q);
             }
@@ -999,6 +1026,7 @@ enum EwOp { EW_ADD, EW_SUB, EW_NEG, EW_MUL, EW_MULADD, EW_MULC, EW_ADDC };
 // k_ks_inner, without the ext round trip through HBM and the extra launch.
 struct KsArgs {
     const u64* in;        // ell rows, evaluation domain (the digits' own limbs)
+    const u64* inMul;     // non-null: the own limbs are in (.) inMul (a relinearised tensor's d2 = a1 b1)
     const u64* ext;       // beta blocks of ell+K rows: COL-pass output of the other limbs
     long long extStride;  // words between digit blocks
     const u64* key;       // beta digits of [b rows][a rows], keyRows rows each
@@ -1008,6 +1036,9 @@ struct KsArgs {
     const u64* fold0;  // t == ell - 1: + foldK * fold_p (sfp_ks_inner_fold)
     const u64* fold1;
     u64 foldK;
+    // non-null: the fold rows are the tensor's d0 = a0 b0, d1 = a0 b1 + a1 b0
+    // at row ell - 1, formed here (fold0 / fold1 unused)
+    const u64 *fa0, *fa1, *fb0, *fb1;
     uint32_t ell, Lq, alpha, beta;
     int accum;  // acc += the inner product
     // rows t >= invFrom (the P limbs, and for a ModDown fused with its rescale
@@ -1078,10 +1109,16 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt_ks(const KsArgs A, const sf_
         u64 v[2 * NPAIR];
         if (own) {
             const u64* src = A.in + (size_t)t * n + rowOff;
+            const u64* mul = A.inMul ? A.inMul + (size_t)t * n + rowOff : nullptr;
 #pragma unroll
             for (int k = 0; k < NPAIR; ++k) {
                 const uint32_t e = 2 * (threadIdx.x + k * NT);
-                const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(src + e);
+                ulonglong2 x = *reinterpret_cast<const ulonglong2*>(src + e);
+                if (mul) {
+                    const ulonglong2 m = *reinterpret_cast<const ulonglong2*>(mul + e);
+                    x.x = bmul(x.x, m.x, B);
+                    x.y = bmul(x.y, m.y, B);
+                }
                 v[2 * k] = x.x;
                 v[2 * k + 1] = x.y;
             }
@@ -1156,7 +1193,7 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt_ks(const KsArgs A, const sf_
             macc(a1[2 * k + 1], v[2 * k + 1], a2.y);
         }
     }
-    const bool fold = A.fold0 && t == A.ell - 1;
+    const bool fold = (A.fold0 || A.fa0) && t == A.ell - 1;
     u64* o0 = A.acc0 + (size_t)t * n + rowOff;
     u64* o1 = A.acc1 + (size_t)t * n + rowOff;
     const bool inv = t >= A.invFrom;
@@ -1165,8 +1202,26 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt_ks(const KsArgs A, const sf_
     for (int k = 0; k < NPAIR; ++k) {
         const uint32_t e = 2 * (threadIdx.x + k * NT);
         if (fold) {  // + P * d_l (sfp_ks_inner_fold)
-            const ulonglong2 f0 = *reinterpret_cast<const ulonglong2*>(A.fold0 + rowOff + e);
-            const ulonglong2 f1 = *reinterpret_cast<const ulonglong2*>(A.fold1 + rowOff + e);
+            ulonglong2 f0, f1;
+            if (A.fa0) {  // d0 = a0 b0, d1 = a0 b1 + a1 b0 at row l (canonical, as k_tensor writes them)
+                const size_t ro = (size_t)t * n + rowOff + e;
+                const ulonglong2 x0 = *reinterpret_cast<const ulonglong2*>(A.fa0 + ro);
+                const ulonglong2 x1 = *reinterpret_cast<const ulonglong2*>(A.fa1 + ro);
+                const ulonglong2 y0 = *reinterpret_cast<const ulonglong2*>(A.fb0 + ro);
+                const ulonglong2 y1 = *reinterpret_cast<const ulonglong2*>(A.fb1 + ro);
+                Acc tt{0, 0}, uu{0, 0};
+                macc(tt, x0.x, y1.x);
+                macc(tt, x1.x, y0.x);
+                macc(uu, x0.y, y1.y);
+                macc(uu, x1.y, y0.y);
+                f0.x = bmul(x0.x, y0.x, B);
+                f0.y = bmul(x0.y, y0.y, B);
+                f1.x = sf_reduce128_acc(tt.lo, tt.hi, &B);
+                f1.y = sf_reduce128_acc(uu.lo, uu.hi, &B);
+            } else {
+                f0 = *reinterpret_cast<const ulonglong2*>(A.fold0 + (size_t)t * n + rowOff + e);
+                f1 = *reinterpret_cast<const ulonglong2*>(A.fold1 + (size_t)t * n + rowOff + e);
+            }
             macc(a0[2 * k], f0.x, A.foldK);
             macc(a0[2 * k + 1], f0.y, A.foldK);
             macc(a1[2 * k], f1.x, A.foldK);
@@ -3465,26 +3520,31 @@ void sfp_modup(sfp_dev* d, uint64_t* ext, const uint64_t* in, uint32_t ell, uint
     nttRows(d, B, 0);
 }
 
-int sfp_modup_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* in, uint32_t ell, uint32_t K,
-                    uint32_t Lq, uint32_t alpha, const sfp_conv* const* convs, const uint64_t* key,
-                    const uint64_t* fold0, const uint64_t* fold1, uint64_t foldK, int accum, uint32_t invFrom,
-                    uint64_t* ext, uint64_t* scr) {
-    static const bool on = [] {  // SFHE_KS_FUSE=0: the unfused sequence (A/B)
+static bool ksFuse() {  // SFHE_KS_FUSE=0: the unfused sequences (A/B)
+    static const bool on = [] {
         const char* v = std::getenv("SFHE_KS_FUSE");
         return !v || *v != '0';
     }();
+    return on;
+}
+
+// The fused ModUp + key inner product (sfp_modup_inner / sfp_mult_relin_rescale):
+// INTT of the input (in, or in (.) inMul: a tensor's d2 = a1 b1 formed in the
+// first pass), the digits' conversions, the forward COL pass, then k_ntt_ks.
+// T[4] (a0, a1, b0, b1) non-null: the fold rows are the tensor's d0 / d1.
+static void modupInnerCore(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* in, const uint64_t* inMul,
+                           uint32_t ell, uint32_t K, uint32_t Lq, uint32_t alpha, const sfp_conv* const* convs,
+                           const uint64_t* key, const uint64_t* fold0, const uint64_t* fold1,
+                           const uint64_t* const* T, uint64_t foldK, int accum, uint32_t invFrom, uint64_t* ext,
+                           uint64_t* scr) {
     const uint32_t n = d->n;
     const uint32_t beta = (ell + alpha - 1) / alpha;
-    if (!on || n <= (uint32_t)kNttTile) return -1;  // the caller runs sfp_modup + sfp_ks_inner*
     const long long stride = (long long)(ell + K) * n;
-    if (beta > (uint32_t)kMaxConvJobs || ell + K > SFP_MAX_LIMBS || (fold0 && (!fold1 || ell < 1))) {
-        record(d, "modup_inner (too many digits / limbs)", hipErrorInvalidValue);
-        return 0;
-    }
     // INTT of every input row (the digits' own rows are read from `in` by the fused pass)
     RowGroup A = rowsOf(1, ell, sfp_limbs{ell, ell, 0, 0});
     A.src = RowPtr{in, 0, (long long)n};
     A.dst = RowPtr{scr, 0, (long long)n};
+    if (inMul) A.pre = RowPtr{inMul, 0, (long long)n};
     nttRows(d, A, 1);
     ConvJobs J;
     bool fpOk = true;
@@ -3500,7 +3560,9 @@ int sfp_modup_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* 
     B.alpha = alpha;
     nttRows(d, B, 0, 1);
     KsArgs a;
+    std::memset(&a, 0, sizeof a);
     a.in = in;
+    a.inMul = inMul;
     a.ext = ext;
     a.extStride = stride;
     a.key = key;
@@ -3510,6 +3572,12 @@ int sfp_modup_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* 
     a.acc1 = acc1;
     a.fold0 = fold0;
     a.fold1 = fold1;
+    if (T) {
+        a.fa0 = T[0];
+        a.fa1 = T[1];
+        a.fb0 = T[2];
+        a.fb1 = T[3];
+    }
     a.foldK = foldK;
     a.ell = ell;
     a.Lq = Lq;
@@ -3532,6 +3600,20 @@ int sfp_modup_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* 
                                a, d->bar, d->psi, d->psiS, d->logn, d->psiD, d->qinvD, nttFp());
     });
     checkLaunch(d, "ntt_ks");
+}
+
+int sfp_modup_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* in, uint32_t ell, uint32_t K,
+                    uint32_t Lq, uint32_t alpha, const sfp_conv* const* convs, const uint64_t* key,
+                    const uint64_t* fold0, const uint64_t* fold1, uint64_t foldK, int accum, uint32_t invFrom,
+                    uint64_t* ext, uint64_t* scr) {
+    const uint32_t beta = (ell + alpha - 1) / alpha;
+    if (!ksFuse() || d->n <= (uint32_t)kNttTile) return -1;  // the caller runs sfp_modup + sfp_ks_inner*
+    if (beta > (uint32_t)kMaxConvJobs || ell + K > SFP_MAX_LIMBS || (fold0 && (!fold1 || ell < 1))) {
+        record(d, "modup_inner (too many digits / limbs)", hipErrorInvalidValue);
+        return 0;
+    }
+    modupInnerCore(d, acc0, acc1, in, nullptr, ell, K, Lq, alpha, convs, key, fold0, fold1, nullptr, foldK, accum,
+                   invFrom, ext, scr);
     return 0;
 }
 
@@ -3613,10 +3695,12 @@ void sfp_moddown2(sfp_dev* d, uint64_t* out0, uint64_t* out1, uint64_t* acc, siz
     nttRows(d, B, 0);
 }
 
-void sfp_moddown_rescale(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint64_t* d0,
-                         const uint64_t* d1, uint64_t* acc, size_t accStride, uint32_t ell,
-                         uint32_t K, uint32_t Lq, const sfp_conv* c, const uint64_t* pinv,
-                         const uint64_t* pmod, const uint64_t* qlinv, uint64_t* scr, int rowDone) {
+// sfp_moddown_rescale; T[4] (a0, a1, b0, b1) non-null: d0 / d1 are the
+// tensor of (a0, a1) and (b0, b1), formed in the final pass's epilogue
+static void moddownRescaleCore(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint64_t* d0, const uint64_t* d1,
+                               const uint64_t* const* T, uint64_t* acc, size_t accStride, uint32_t ell, uint32_t K,
+                               uint32_t Lq, const sfp_conv* c, const uint64_t* pinv, const uint64_t* pmod,
+                               const uint64_t* qlinv, uint64_t* scr, int rowDone) {
     const uint32_t n = d->n, l = ell - 1;
     if (ell < 2 || ell > SFP_MAX_LIMBS || !c || c->ns > (uint32_t)kMaxConvSrc || c->nt < ell ||
         !limbsOk(d, sfp_limbs{K + 1, 1, Lq, l}, "moddown_rescale")) {
@@ -3715,12 +3799,48 @@ void sfp_moddown_rescale(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint6
     B.epi = 1;
     B.ein = RowPtr{acc, (long long)accStride, (long long)n};
     B.eout = RowPtr{out0, (long long)(out1 - out0), (long long)n};
-    B.eadd = RowPtr{d0, (long long)(d1 - d0), (long long)n};
+    if (T) {
+        B.tA0 = T[0];
+        B.tA1 = T[1];
+        B.tB0 = T[2];
+        B.tB1 = T[3];
+    } else {
+        B.eadd = RowPtr{d0, (long long)(d1 - d0), (long long)n};
+    }
     B.k = devConst(d, k1, l);
     B.kS = devConst(d, k1S, l);
     B.k2 = devConst(d, qlinv, l);
     B.k2S = devConst(d, k2S, l);
     nttRows(d, B, 0);
+}
+
+void sfp_moddown_rescale(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint64_t* d0,
+                         const uint64_t* d1, uint64_t* acc, size_t accStride, uint32_t ell,
+                         uint32_t K, uint32_t Lq, const sfp_conv* c, const uint64_t* pinv,
+                         const uint64_t* pmod, const uint64_t* qlinv, uint64_t* scr, int rowDone) {
+    moddownRescaleCore(d, out0, out1, d0, d1, nullptr, acc, accStride, ell, K, Lq, c, pinv, pmod, qlinv, scr,
+                       rowDone);
+}
+
+int sfp_mult_relin_rescale(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint64_t* a0, const uint64_t* a1,
+                           const uint64_t* b0, const uint64_t* b1, uint32_t ell, uint32_t K, uint32_t Lq,
+                           uint32_t alpha, const sfp_conv* const* convs, const uint64_t* key, const sfp_conv* c,
+                           const uint64_t* pinv, const uint64_t* pmod, const uint64_t* qlinv, uint64_t* acc,
+                           uint64_t* ext, uint64_t* scr) {
+    const uint32_t beta = (ell + alpha - 1) / alpha;
+    if (!ksFuse() || d->n <= (uint32_t)kNttTile) return -1;
+    if (ell < 2 || beta > (uint32_t)kMaxConvJobs || ell + K > SFP_MAX_LIMBS) {
+        record(d, "mult_relin_rescale (too many digits / limbs)", hipErrorInvalidValue);
+        return 0;
+    }
+    const uint64_t* T[4] = {a0, a1, b0, b1};
+    // d2 = a1 b1 in the ModUp's first pass and the own digits; d0, d1 at row
+    // ell - 1 in the inner product's fold, the rest in the ModDown's epilogue
+    modupInnerCore(d, acc, acc + (size_t)(ell + K) * d->n, a1, b1, ell, K, Lq, alpha, convs, key, nullptr, nullptr,
+                   T, pmod[ell - 1], 0, ell - 1, ext, scr);
+    moddownRescaleCore(d, out0, out1, nullptr, nullptr, T, acc, (size_t)(ell + K) * d->n, ell, K, Lq, c, pinv, pmod,
+                       qlinv, scr, 1);
+    return 0;
 }
 
 // ---- sampling ----

@@ -251,6 +251,20 @@ void sfp_moddown_rescale(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint6
                          uint32_t K, uint32_t Lq, const sfp_conv* c, const uint64_t* pinv,
                          const uint64_t* pmod, const uint64_t* qlinv, uint64_t* scratch, int row_done);
 
+// EvalMult(ct, ct) end to end from its operands (a0, a1) and (b0, b1) (ell
+// rows each, evaluation domain): the tensor, the relinearisation with `key`
+// and the rescale -- bit-identical to sfp_tensor followed by sfp_modup +
+// sfp_ks_inner_fold (fold_k = pmod[ell-1]) + sfp_moddown_rescale, with the
+// tensor's three products formed inside those passes (never written out).
+// out0 / out1: ell - 1 rows.  acc: 2 (ell+K) n words, ext: beta (ell+K) n,
+// scratch: 2 ell n.  Returns -1 (nothing done) where the backend has no fused
+// form (the caller runs the unfused prims).
+int sfp_mult_relin_rescale(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint64_t* a0, const uint64_t* a1,
+                           const uint64_t* b0, const uint64_t* b1, uint32_t ell, uint32_t K, uint32_t Lq,
+                           uint32_t alpha, const sfp_conv* const* convs, const uint64_t* key, const sfp_conv* c,
+                           const uint64_t* pinv, const uint64_t* pmod, const uint64_t* qlinv, uint64_t* acc,
+                           uint64_t* ext, uint64_t* scratch);
+
 // ---- sampling (counter-based, deterministic) ------------------------------------
 // Uniform residues mod each limb's prime: value for (limb, i) is derived from
 // splitmix64(seed, stream-id = prime index, i); identical on every backend.
