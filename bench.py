@@ -9,11 +9,14 @@ BASELINE.json: N=256, ring 2^16, depth 34, CompositeSign(3,4,2), scale 40.
 
 Multi-GPU (one process per GPU; BASELINE north_star: "encrypted-sort
 wall-clock ... at 1, 2, 4 and 8 MI355X"): at N > 1 the headline is the
-wall-clock of ONE metric sort limb-sharded over the ranks (SURVEY §8(e):
-rank r holds the RNS limbs i % N == r above the replicated tail; RCCL
-all-gather at ModUp / ModDown, broadcast at rescale, the whole sort one
-hipGraph with its collectives) -> scaling "strong", value = N^2 * K / max-
-over-ranks(time).  The ranks' independent replica sorts (each GPU its own
+wall-clock of ONE metric sort over all ranks -> scaling "strong", value =
+N^2 * K / max-over-ranks(time).  The ranks form G = 2 batch groups (``--split``;
+the sort's two independent batches per phase, one per group, parts
+all-gathered over RCCL) of N/G ranks, and each group limb-shards its batch
+(in-group rank r holds the RNS limbs i % (N/G) == r above the
+replicated tail; RCCL all-gather at ModUp / ModDown, broadcast at rescale).
+The whole sort is one hipGraph with its collectives.  ``--split 1``: limb
+sharding over all N ranks.  The ranks' independent replica sorts (each GPU its own
 array, no data-path collective) are measured first and reported as the
 extra field ``replicas``; should the sharded leg fail or stall, the line
 carries the replica throughput as the headline and says so.
@@ -219,29 +222,25 @@ def kway_leg(device, k=2, M=10, logn=17):
             "stages": M + M * (M - 1) // 2 * ((k + 1) // 2)}
 
 
-def c5_leg(device, world=1, rank=0, steps=2):
+def c5_leg(device, world=1, rank=0, steps=2, groups=1):
     """BASELINE config 5's sort: DirectSort<256> at ring 2^17 (DirectSortTest's
     ring, HEStd_128_classic, ~40 limbs).  world == 1: one GPU, unsharded (the
-    reference point).  world > 1: the ranks LIMB-SHARD one sort over RCCL
-    (SURVEY §8(e)): per-sort wall-clock at W GPUs.  Run after the replica
+    reference point).  world > 1: the ranks split one sort's batches over
+    `groups` groups and limb-shard each group's share over RCCL (SURVEY
+    §8(e)): per-sort wall-clock at W GPUs.  Run after the replica
     measurement, as an extra field; a watchdog (SFHE_C5_TIMEOUT s, default
     240) prints the line without it and exits with status 2 if the collective
     path stalls."""
     import numpy as np
     N, logn, secure = WORKLOADS["directsort_n256_2e17"]
     depth, rots = sfhe.direct_sort_params(N, "hip")
-    shard = None
+    shard = grp = None
     transport = os.environ.get("SFHE_C5_TRANSPORT", "rccl")  # "host": gloo rehearsal (ranks may share a GPU)
-    if world > 1 and transport == "host":
-        shard = ("host", rank, world, sfhe.GlooComm())
-    elif world > 1:
-        import torch.distributed as dist
-        uid = [sfhe.comm_uid("hip") if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        shard = ("rccl", rank, world, uid[0])
+    if world > 1:
+        shard, grp = comm_spec(transport, rank, world, groups)
     t0 = time.perf_counter()
     eng = sfhe.Engine("hip", mult_depth=depth, ring_dim=1 << logn, batch_size=N, secure=secure,
-                      rotations=rots, seed=20251205 + N, device=device, shard=shard)
+                      rotations=rots, seed=20251205 + N, device=device, shard=shard, groups=grp)
     eng.set_quiet(True)
     setup_s = time.perf_counter() - t0
     x = input_vector(N)
@@ -256,7 +255,8 @@ def c5_leg(device, world=1, rank=0, steps=2):
     dt = timed_steps(step, eng.sync, world, steps, 1)
     err = float(np.max(np.abs(np.array(eng.decrypt(holder["out"]))[:N] - np.sort(x))))
     return {"workload": f"DirectSort<{N}> @ ring 2^{logn} (HEStd_128_classic, depth {depth})",
-            "parallelism": f"limb-shard x{world} ({transport})" if world > 1 else "1 GPU, unsharded",
+            "parallelism": parallelism(world, groups, transport, eng.shard_tail()) if world > 1
+            else "1 GPU, unsharded",
             "ms_per_sort": dt / steps * 1e3, "setup_s": setup_s, "max_err": err, "level": holder["out"].level}
 
 
@@ -279,16 +279,45 @@ def pmc_traffic(family: str):
     return j.get("families", {}).get(family, {}).get("traffic_over_algorithmic")
 
 
-def shard_spec(mode: str, rank: int, world: int):
-    """Engine(shard=...) argument of the limb-sharded sort: an RCCL
-    communicator (rank 0's unique id broadcast over torch.distributed) or the
-    gloo host transport."""
-    if mode == "rccl":
-        import torch.distributed as dist
-        uid = [sfhe.comm_uid("hip") if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        return ("rccl", rank, world, uid[0])
-    return ("host", rank, world, sfhe.GlooComm())
+def comm_spec(mode: str, rank: int, world: int, groups: int):
+    """Engine(shard=..., groups=...) arguments of the multi-GPU sort: `groups`
+    batch groups of world // groups ranks (rank = group * per + r), each group
+    limb-sharded over its own communicator when per > 1, and a group
+    communicator per in-group rank r joining the groups (sfhe_groups_*).
+    RCCL: each communicator's unique id made by one of its members and shared
+    with all_gather_object; host: gloo subgroups.  Collective over all ranks."""
+    import torch.distributed as dist
+    per = world // groups
+    g, r = divmod(rank, per)
+    if mode == "host":
+        limb = [dist.new_group(list(range(h * per, (h + 1) * per))) for h in range(groups)]
+        cross = [dist.new_group([h * per + j for h in range(groups)]) for j in range(per)]
+        shard = ("host", r, per, sfhe.GlooComm(limb[g])) if per > 1 else None
+        grp = ("host", g, groups, sfhe.GlooComm(cross[r])) if groups > 1 else None
+        return shard, grp
+    mine = {}
+    if per > 1 and r == 0:
+        mine[f"limb{g}"] = sfhe.comm_uid("hip")
+    if groups > 1 and g == 0:
+        mine[f"cross{r}"] = sfhe.comm_uid("hip")
+    every = [None] * world
+    dist.all_gather_object(every, mine)
+    uids = {}
+    for m in every:
+        uids.update(m)
+    shard = ("rccl", r, per, uids[f"limb{g}"]) if per > 1 else None
+    grp = ("rccl", g, groups, uids[f"cross{r}"]) if groups > 1 else None
+    return shard, grp
+
+
+def parallelism(world: int, groups: int, mode: str, tail: int) -> str:
+    per = world // groups
+    parts = []
+    if groups > 1:
+        parts.append(f"batch-split x{groups}")
+    if per > 1:
+        parts.append(f"limb-shard x{per} (replicated tail <= {tail} limbs)")
+    return " * ".join(parts) + f" over {mode}"
 
 
 def replica_leg(make_engine, spec, world, steps, warmup):
@@ -350,7 +379,10 @@ def main(argv=None):
                     help="run the config-5 leg without graph replay (profiling: replaying the 2^17 sort's graph "
                          "under rocprofv3's kernel tracer crashes inside the profiler, DESIGN.md §5)")
     ap.add_argument("--shard", choices=("rccl", "host"), default=None,
-                    help="transport of the limb-sharded headline sort at N > 1 (default rccl)")
+                    help="transport of the multi-GPU headline sort at N > 1 (default rccl)")
+    ap.add_argument("--split", type=int, default=None,
+                    help="batch groups of the multi-GPU sort (default 2 when N is even, else 1; "
+                         "1 = limb sharding over all ranks)")
     ap.add_argument("--replicas", action="store_true",
                     help="at N > 1, make the independent replica sorts the headline (weak scaling)")
     args = ap.parse_args(argv)
@@ -371,10 +403,14 @@ def main(argv=None):
                                                    secure=secure, rotations=rots, seed=20251205 + N + 7919 * rank,
                                                    device=device),
                                spec, world, args.steps, args.warmup)
-    shard, seed = None, 20251205 + N + 7919 * rank
+    groups = args.split if args.split else (2 if world % 2 == 0 else 1)
+    if world % groups:
+        raise SystemExit(f"--split {groups} does not divide --gpus {world}")
+    shard = grp = None
+    seed = 20251205 + N + 7919 * rank
     if mode:
         seed = 20251205 + N  # every rank builds the same keys
-        shard = shard_spec(mode, rank, world)
+        shard, grp = comm_spec(mode, rank, world, groups)
     limit = float(os.environ.get("SFHE_SHARD_TIMEOUT", "600"))
     dog = None
     if mode:  # a stalled collective: report the replicas, then fail loudly
@@ -392,7 +428,7 @@ def main(argv=None):
         dog.start()
     try:
         eng = sfhe.Engine("hip", mult_depth=depth, ring_dim=1 << logn, batch_size=N, secure=secure,
-                          rotations=rots, seed=seed, device=device, shard=shard)
+                          rotations=rots, seed=seed, device=device, shard=shard, groups=grp)
     except Exception as e:  # noqa: BLE001 -- the sharded context could not be built
         if not mode:
             raise
@@ -521,7 +557,7 @@ def main(argv=None):
     }
 
     sort_s = dt / args.steps
-    sorts = 1 if shard else world  # concurrent sorts in the job
+    sorts = 1 if mode else world  # concurrent sorts in the job
     value = sorts * N * N * args.steps / dt
     result = {
         "metric": "encrypted rank-sort homomorphic comparisons/s (N^2 per DirectSort<N>::sort)",
@@ -533,13 +569,13 @@ def main(argv=None):
         "ms_per_step": sort_s * 1e3,
         "sort_seconds": sort_s,
         "higher_is_better": True,
-        "scaling": "strong" if shard else "weak",
+        "scaling": "strong" if mode else "weak",
         "vs_baseline": None,
         "dtype": "u64 (RNS residues, 40/60-bit primes)",
         "data": "synthetic: seeded permutation of {k/N}, CKKS-encrypted",
         "config": {"workload": args.workload, "N": N, "ring_dim": 1 << logn, "mult_depth": depth,
                    "sign": list(cfg), "scale_bits": 40, "secure": secure,
-                   "parallelism": (f"limb-shard x{world} ({mode}; replicated tail <= {tail} limbs)" if shard
+                   "parallelism": (parallelism(world, groups, mode, tail) if mode
                                    else f"replicas x{world}")},
         "algorithmic_gb_per_sort": stats["algo_bytes"] / 1e9,
         "graph": {"replayed": graph_nodes > 0, "nodes": graph_nodes,
@@ -571,7 +607,7 @@ def main(argv=None):
         if args.c5_eager:
             os.environ["SFHE_GRAPH"] = "0"  # read per sort by the sorter
         try:
-            result["c5"] = c5_leg(device, world, rank)
+            result["c5"] = c5_leg(device, world, rank, groups=groups)
         except Exception as e:  # noqa: BLE001 -- an extra leg must not lose the metric line
             result["c5"] = {"error": str(e)}
         c5_dog.cancel()

@@ -302,6 +302,23 @@ int sfhe_shard_host(sfhe_ctx* c, int rank, int world, sfhe_allgather_fn ag, sfhe
 /* The replicated-tail limb count of a sharded context (0: unsharded). */
 int sfhe_shard_tail(const sfhe_ctx* c, uint32_t* limbs);
 
+/* ---- batch groups (no reference counterpart) ------------------------------
+ * DirectSort's rank and placement phases each run B independent batches
+ * (reference src/sort_algo.h:438-492, 713-742, the OpenMP batch loop).  With
+ * G batch groups, the ranks form G groups of W/G (each group limb-sharded
+ * over its own communicator, or one unsharded rank); group g runs the
+ * batches b with b % G == g and every part is all-gathered over a second
+ * communicator joining the ranks that hold the same rows in different groups
+ * (in-group rank r of every group).  Every rank ends with the same,
+ * bit-identical result as the unsplit sort.  B not a multiple of G: every
+ * group runs every batch; one group (groups == 1) runs every batch and
+ * still routes each part through the communicator (single-GPU validation of
+ * the collective).  Call before sfhe_keygen, with the same params and
+ * seed on every rank; the calls are collective like the sharded ones. */
+int sfhe_groups_rccl(sfhe_ctx* c, int group, int groups, const uint8_t uid[128]);
+int sfhe_groups_host(sfhe_ctx* c, int group, int groups, sfhe_allgather_fn ag, void* user);
+int sfhe_groups(const sfhe_ctx* c, int* group, int* groups);
+
 #ifdef __cplusplus
 }
 #endif

@@ -45,6 +45,10 @@ struct sfp_dev {
     sfp_host_allgather_fn ag;
     sfp_host_bcast_fn bc;
     void* user;
+    /* batch groups (sfp_group_*): rank grank of gworld, host all-gather */
+    int grank, gworld;
+    sfp_host_allgather_fn gag;
+    void* guser;
     /* the host encoder's tables (sfp_encode) */
     u64* enc_rot;
     double* enc_ksi;
@@ -79,6 +83,7 @@ sfp_dev* sfp_create(int device, const sfp_tables* t) {
     (void)device;
     sfp_dev* d = (sfp_dev*)calloc(1, sizeof(sfp_dev));
     d->world = 1;
+    d->gworld = 1;
     d->logn = t->logn;
     d->n = 1u << t->logn;
     d->np = t->nprimes;
@@ -729,6 +734,26 @@ void sfp_allgather(sfp_dev* d, const void* send, void* recv, size_t bytes) {
     void* tmp = malloc(bytes ? bytes : 1); /* send may alias recv */
     memcpy(tmp, send, bytes);
     d->ag(d->user, tmp, recv, bytes);
+    free(tmp);
+}
+int sfp_group_init_rccl(sfp_dev* d, int group, int groups, const void* uid128) {
+    (void)d; (void)group; (void)groups; (void)uid128;
+    return -1; /* no RCCL in the oracle */
+}
+void sfp_group_set_host(sfp_dev* d, int group, int groups, sfp_host_allgather_fn ag, void* user) {
+    d->grank = group;
+    d->gworld = groups;
+    d->gag = ag;
+    d->guser = user;
+}
+void sfp_group_allgather(sfp_dev* d, const void* send, void* recv, size_t bytes) {
+    if (d->gworld <= 1 || !d->gag) {
+        if (send != recv) memmove(recv, send, bytes);
+        return;
+    }
+    void* tmp = malloc(bytes ? bytes : 1);
+    memcpy(tmp, send, bytes);
+    d->gag(d->guser, tmp, recv, bytes);
     free(tmp);
 }
 void sfp_bcast(sfp_dev* d, void* buf, size_t bytes, int root) {

@@ -151,6 +151,40 @@ void parallelLanes(const CryptoContext<DCRTPoly>& cc, int lanes, int count, F&& 
     if (err) std::rethrow_exception(err);
 }
 
+// The batches of one sort phase over the context's batch groups (DESIGN.md
+// §7): group g of G runs the batches b with b % G == g; gatherParts then
+// all-gathers every part over the group communicator, so each rank holds all
+// B parts and sums them exactly as an unsplit sort.  The parts are settled
+// (canonical) on every path, split or not, so the sums are bit-identical.
+// B not a multiple of G: every group runs every batch (no split).  A
+// one-group communicator (BatchGather at G = 1) still routes every part
+// through the collective: single-GPU validation.
+struct BatchSplit {
+    int G = 1, g = 0;
+    bool gather = false;
+    std::vector<int> mine;
+    BatchSplit(const CryptoContext<DCRTPoly>& cc, int B) {
+        if (cc->BatchGroups() > 1 && B % cc->BatchGroups() == 0) {
+            G = cc->BatchGroups();
+            g = cc->BatchGroup();
+            gather = true;
+        } else if (cc->BatchGroups() == 1) {
+            gather = cc->BatchGather();
+        }
+        for (int b = g; b < B; b += G) mine.push_back(b);
+    }
+    void gatherParts(const CryptoContext<DCRTPoly>& cc, std::vector<Ciphertext<DCRTPoly>>& parts) const {
+        if (!gather) {
+            for (auto& p : parts) cc->Settle(p);
+            return;
+        }
+        for (size_t k = 0; k < parts.size() / G; ++k) {
+            auto all = cc->GatherGroups(parts[k * G + g]);
+            for (int h = 0; h < G; ++h) parts[k * G + h] = all[h];
+        }
+    }
+};
+
 // Placement evaluates the doubled sinc in the rebased variable (on unless
 // SFHE_SINC_REBASE=0; see rotationIndexCheckN).
 inline bool sincRebase() {
@@ -375,11 +409,14 @@ class DirectSort : public SortBase<N> {
         // final correction is -1 instead of the reference's -1/2 (:503-504).
         // Same rank up to the sign's approximation error; DESIGN.md §2.
         const bool offsetSelf = sfhe::selfOffset();
-        // the batches are independent: each runs on its own lane (stream)
+        // the batches are independent: each runs on its own lane (stream),
+        // and over batch groups on its own GPU group
         std::vector<Ciphertext<DCRTPoly>> parts(L.B);
-        const int lanes = std::min(L.B, m_cc->LaneCount());
+        const sfhe::BatchSplit split(m_cc, L.B);
+        const int lanes = std::min((int)split.mine.size(), m_cc->LaneCount());
         m_cc->ForkLanes(lanes);
-        sfhe::parallelLanes(m_cc, lanes, L.B, [&](int b) {
+        sfhe::parallelLanes(m_cc, lanes, (int)split.mine.size(), [&](int i) {
+            const int b = split.mine[i];
             auto shifted = vecRotsOpt(pre, L.P, L.S, L.npRank, b);
             ph.mark("  rank batch: vecRotsOpt");
             auto dup = input_array->Clone();
@@ -396,6 +433,7 @@ class DirectSort : public SortBase<N> {
             ph.mark("  rank batch: compare");
         });
         m_cc->JoinLanes();
+        split.gatherParts(m_cc, parts);
         for (int b = 0; b < L.B; ++b) m_cc->EvalAddInPlace(rank, parts[b]);
         ph.mark("rank: batches (vecRotsOpt+compare)");
         // sum the P partitions (period N inside S slots)
@@ -452,9 +490,11 @@ class DirectSort : public SortBase<N> {
                                         : selectDoubledSincCoefficients<N>();
         const double zmul = rebase ? 4.0 / 3.0 : 1.0, zadd = rebase ? 1.0 / 3.0 : 0.0;
         std::vector<Ciphertext<DCRTPoly>> parts(L.B);
-        const int lanes = std::min(L.B, m_cc->LaneCount());
+        const sfhe::BatchSplit split(m_cc, L.B);
+        const int lanes = std::min((int)split.mine.size(), m_cc->LaneCount());
         m_cc->ForkLanes(lanes);
-        sfhe::parallelLanes(m_cc, lanes, L.B, [&](int b) {
+        sfhe::parallelLanes(m_cc, lanes, (int)split.mine.size(), [&](int i) {
+            const int b = split.mine[i];
             Plaintext chk = maskMemo({3, b, 0, (int)indexMinusRank->GetLevel(), L.S}, [&](auto& v) {
                 v.push_back(m_cc->MakeCKKSPackedPlaintext(generateCheckingVectorN(L.S, b * L.P), 1,
                                                           indexMinusRank->GetLevel(), nullptr, L.S));
@@ -479,6 +519,7 @@ class DirectSort : public SortBase<N> {
             ph.mark("  place batch: blind rotation");
         });
         m_cc->JoinLanes();
+        split.gatherParts(m_cc, parts);
         for (int b = 0; b < L.B; ++b) m_cc->EvalAddInPlace(output, parts[b]);
         ph.mark("place: batches (sinc PS+mask+blind rotation)");
         for (int s = L.S / 2; s >= N; s /= 2) m_cc->EvalAddInPlace(output, rot.rotate(output, s));

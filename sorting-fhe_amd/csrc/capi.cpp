@@ -840,4 +840,40 @@ int sfhe_shard_tail(const sfhe_ctx* c, uint32_t* limbs) {
     return SFHE_OK;
 }
 
+// ---- batch groups ----
+int sfhe_groups_rccl(sfhe_ctx* c, int group, int groups, const uint8_t uid[128]) {
+    REQUIRE(c && uid, "null argument");
+    REQUIRE(groups >= 1 && group >= 0 && group < groups, "bad group / groups");
+    REQUIRE(!c->keys.secretKey, "set the batch groups before sfhe_keygen");
+    REQUIRE(c->cc->BatchGroups() == 1, "batch groups already set");
+    return guard([&] {
+        auto* s = c->cc->state();
+        if (sfp_group_init_rccl(s->dev, group, groups, uid) != 0) {
+            const char* e = sfp_last_error(s->dev);
+            throw OpenFHEException(std::string("device error: RCCL group communicator: ") +
+                                   (e ? e : "init failed"));
+        }
+        // a one-group communicator still gathers every part (through RCCL)
+        c->cc->EnableBatchGroups(group, groups, true);
+    });
+}
+
+int sfhe_groups_host(sfhe_ctx* c, int group, int groups, sfhe_allgather_fn ag, void* user) {
+    REQUIRE(c && ag, "null argument");
+    REQUIRE(groups >= 1 && group >= 0 && group < groups, "bad group / groups");
+    REQUIRE(!c->keys.secretKey, "set the batch groups before sfhe_keygen");
+    REQUIRE(c->cc->BatchGroups() == 1, "batch groups already set");
+    return guard([&] {
+        c->cc->EnableBatchGroups(group, groups, true);
+        sfp_group_set_host(c->cc->state()->dev, group, groups, ag, user);
+    });
+}
+
+int sfhe_groups(const sfhe_ctx* c, int* group, int* groups) {
+    REQUIRE(c && group && groups, "null argument");
+    *group = c->cc->BatchGroup();
+    *groups = c->cc->BatchGroups();
+    return SFHE_OK;
+}
+
 }  // extern "C"

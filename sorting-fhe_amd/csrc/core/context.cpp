@@ -2842,6 +2842,45 @@ void CryptoContextImpl<DCRTPoly>::EnableSharding(int rank, int world, bool shard
 
 uint32_t CryptoContextImpl<DCRTPoly>::ShardTailLimbs() const { return st->sharded ? st->tailLimbs : 0; }
 
+void CryptoContextImpl<DCRTPoly>::EnableBatchGroups(int group, int groups, bool gatherAtOne) {
+    OpLock g(st.get());
+    if (groups < 1 || group < 0 || group >= groups) SFHE_THROW("EnableBatchGroups: bad group / groups");
+    if (st->capturing) SFHE_THROW("EnableBatchGroups inside a capture");
+    st->bgroup = group;
+    st->bgroups = groups;
+    st->bgatherAtOne = gatherAtOne;
+}
+bool CryptoContextImpl<DCRTPoly>::BatchGather() const { return st->bgroups > 1 || st->bgatherAtOne; }
+int CryptoContextImpl<DCRTPoly>::BatchGroup() const { return st->bgroup; }
+int CryptoContextImpl<DCRTPoly>::BatchGroups() const { return st->bgroups; }
+
+std::vector<Ciphertext<DCRTPoly>> CryptoContextImpl<DCRTPoly>::GatherGroups(const Ciphertext<DCRTPoly>& ct) {
+    OpLock g(st.get());
+    SfheContextState* s = st.get();
+    if (!ct) SFHE_THROW("GatherGroups: null ciphertext");
+    SfheInternal::deps(s, {&ct});
+    const size_t pw = s->polyWords(ct->level);
+    const size_t G = (size_t)s->bgroups;
+    // [c0 rows][c1 rows] of this group, then every group's, group-major
+    auto recv = s->alloc(G * 2 * pw);
+    uint64_t* mine = recv->ptr + (size_t)s->bgroup * 2 * pw;
+    sfp_d2d(s->dev, mine, ct->c0, pw * 8);
+    sfp_d2d(s->dev, mine + pw, ct->c1, pw * 8);
+    sfp_group_allgather(s->dev, mine, recv->ptr, 2 * pw * 8);
+    std::vector<Ciphertext<DCRTPoly>> out(G);
+    for (size_t i = 0; i < G; ++i) {
+        auto c = std::make_shared<CiphertextImpl<DCRTPoly>>(*ct);
+        c->buf = recv;
+        c->c0 = recv->ptr + i * 2 * pw;
+        c->c1 = c->c0 + pw;
+        c->def.reset();
+        c->pend = false;
+        c->undo.reset();
+        out[i] = c;
+    }
+    return out;
+}
+
 int CryptoContextImpl<DCRTPoly>::ShardRank() const { return st->rank; }
 int CryptoContextImpl<DCRTPoly>::ShardWorld() const { return st->world; }
 bool CryptoContextImpl<DCRTPoly>::IsSharded() const { return st->sharded; }
@@ -2912,7 +2951,7 @@ bool CryptoContextImpl<DCRTPoly>::BeginCapture() {
     if (s->capturing) SFHE_THROW("BeginCapture: a capture is already open");
     if (s->forkedLanes) SFHE_THROW("BeginCapture inside a lane region");
     // a host transport synchronises (no capture); RCCL collectives are captured
-    if (s->sharded && !sfp_comm_capturable(s->dev)) return false;
+    if ((s->sharded || s->bgroups > 1 || s->bgatherAtOne) && !sfp_comm_capturable(s->dev)) return false;
     sfp_sync(s->dev);
     if (sfp_capture_begin(s->dev) != 0) {
         std::fprintf(stderr, "sfhe: this backend cannot capture graphs (%s); sorting eagerly\n", sfp_backend_name());

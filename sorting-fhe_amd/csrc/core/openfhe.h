@@ -492,6 +492,20 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
     int ShardWorld() const;
     bool IsSharded() const;
     uint32_t ShardTailLimbs() const;
+    // Batch groups (engine extension): the sort's independent
+    // batches are split over `groups` GPU groups, this rank in group `group`
+    // (each group limb-sharded or not).  The device's group communicator
+    // (C ABI sfhe_groups_*) joins the ranks holding the same rows of
+    // different groups.  GatherGroups(ct) settles ct and all-gathers it over
+    // that communicator: every group's ciphertext, group order (collective:
+    // every rank calls it in the same program order).
+    // gatherAtOne: a one-group communicator still routes the parts through
+    // GatherGroups (single-GPU validation of the collective, as shardAtOne).
+    void EnableBatchGroups(int group, int groups, bool gatherAtOne = false);
+    int BatchGroup() const;
+    int BatchGroups() const;
+    bool BatchGather() const;  // groups > 1, or gatherAtOne
+    std::vector<Ciphertext<DCRTPoly>> GatherGroups(const Ciphertext<DCRTPoly>& ct);
     // Engine internal (raw-row consumers: the weighted sums): ct's (c0, c1)
     // rows, Settle()d, as valid at `level`'s limb count -- gathered into a
     // buffer appended to `keep` when ct's rows are dealt over the ranks but

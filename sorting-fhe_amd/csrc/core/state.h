@@ -145,6 +145,9 @@ struct SfheContextState {
     // sharded is also set by a one-rank RCCL communicator: the sharded code
     // path (exchanges through RCCL) at W = 1, for single-GPU validation.
     int rank = 0, world = 1;
+    // batch groups (EnableBatchGroups): this rank is in group bgroup of bgroups
+    int bgroup = 0, bgroups = 1;
+    bool bgatherAtOne = false;  // a one-group communicator still gathers (validation)
     bool sharded = false;
     uint32_t tailLimbs = 0;
     bool fullScope = false;  // inside FullScope: unsharded (setup work on every row)

@@ -149,6 +149,11 @@ struct sfp_dev {
     sfp_host_allgather_fn hostAg = nullptr;
     sfp_host_bcast_fn hostBc = nullptr;
     void* hostUser = nullptr;
+    // batch groups (sfp_group_*): rank grank of gworld
+    int grank = 0, gworld = 1;
+    ncclComm_t gnccl = nullptr;
+    sfp_host_allgather_fn gHostAg = nullptr;
+    void* gHostUser = nullptr;
     // per-lane scratch (scratch()), and buffers retired by its growth
     std::mutex scrMu;
     u64* scr[SFP_MAX_LANES] = {};
@@ -2591,6 +2596,7 @@ void sfp_destroy(sfp_dev* d) {
     if (!d) return;
     syncAll(d);
     if (d->nccl) rcclApi().commDestroy(d->nccl);
+    if (d->gnccl) rcclApi().commDestroy(d->gnccl);
     for (sfp_event* e : d->evFree) {
         hipEventDestroy(e->e);
         delete e;
@@ -4069,26 +4075,70 @@ int sfp_comm_uid(void* uid128) {
     return rcclApi().getUniqueId(reinterpret_cast<ncclUniqueId*>(uid128)) == ncclSuccess ? 0 : -1;
 }
 
-int sfp_comm_init_rccl(sfp_dev* d, int rank, int world, const void* uid128) {
+static void ncclCheck(sfp_dev* d, const char* what, ncclResult_t r);
+
+static ncclComm_t rcclInit(sfp_dev* d, int rank, int world, const void* uid128) {
     ncclUniqueId id;
     std::memcpy(&id, uid128, sizeof id);
     SFP_CHECK(hipSetDevice(d->device));
     if (!rcclApi().ok) {
         std::lock_guard<std::mutex> g(d->mu);
         if (d->err.empty()) d->err = "RCCL library (librccl.so.1) not found";
-        return -1;
+        return nullptr;
     }
     ncclComm_t c = nullptr;
     const ncclResult_t r = rcclApi().commInitRank(&c, world, id, rank);
     if (r != ncclSuccess) {
         std::lock_guard<std::mutex> g(d->mu);
         if (d->err.empty()) d->err = std::string("ncclCommInitRank: ") + rcclApi().errorString(r);
-        return -1;
+        return nullptr;
     }
+    return c;
+}
+
+int sfp_comm_init_rccl(sfp_dev* d, int rank, int world, const void* uid128) {
+    ncclComm_t c = rcclInit(d, rank, world, uid128);
+    if (!c) return -1;
     d->nccl = c;
     d->rank = rank;
     d->world = world;
     return 0;
+}
+
+int sfp_group_init_rccl(sfp_dev* d, int group, int groups, const void* uid128) {
+    ncclComm_t c = rcclInit(d, group, groups, uid128);
+    if (!c) return -1;
+    d->gnccl = c;
+    d->grank = group;
+    d->gworld = groups;
+    return 0;
+}
+
+void sfp_group_set_host(sfp_dev* d, int group, int groups, sfp_host_allgather_fn ag, void* user) {
+    d->grank = group;
+    d->gworld = groups;
+    d->gHostAg = ag;
+    d->gHostUser = user;
+}
+
+void sfp_group_allgather(sfp_dev* d, const void* send, void* recv, size_t bytes) {
+    if (d->gnccl) {
+        ncclCheck(d, "ncclAllGather (groups)",
+                  rcclApi().allGather(send, recv, bytes, ncclUint8, d->gnccl, d->st()));
+        return;
+    }
+    if (d->gworld == 1) {
+        if (send != recv) sfp_d2d(d, recv, send, bytes);
+        return;
+    }
+    if (!d->gHostAg) {
+        record(d, "group allgather (no communicator)", hipErrorInvalidValue);
+        return;
+    }
+    std::vector<char> hs(bytes), hr(bytes * d->gworld);
+    devToHost(d, hs.data(), send, bytes);
+    d->gHostAg(d->gHostUser, hs.data(), hr.data(), bytes);
+    hostToDev(d, recv, hr.data(), hr.size());
 }
 
 void sfp_comm_set_host(sfp_dev* d, int rank, int world, sfp_host_allgather_fn ag, sfp_host_bcast_fn bc,
@@ -4106,7 +4156,7 @@ static void ncclCheck(sfp_dev* d, const char* what, ncclResult_t r) {
     if (d->err.empty()) d->err = std::string(what) + ": " + rcclApi().errorString(r);
 }
 
-int sfp_comm_capturable(sfp_dev* d) { return d->nccl || !d->hostAg ? 1 : 0; }
+int sfp_comm_capturable(sfp_dev* d) { return (d->nccl || !d->hostAg) && (d->gnccl || !d->gHostAg) ? 1 : 0; }
 
 void sfp_allgather(sfp_dev* d, const void* send, void* recv, size_t bytes) {
     if (d->world == 1 && !d->nccl) {

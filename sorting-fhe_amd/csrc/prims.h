@@ -327,6 +327,15 @@ int sfp_comm_capturable(sfp_dev* d);
 void sfp_allgather(sfp_dev* d, const void* send, void* recv, size_t bytes);
 void sfp_bcast(sfp_dev* d, void* buf, size_t bytes, int root);
 
+// Batch groups (the sort's independent batches split over GPU groups,
+// DESIGN.md §7): a second communicator joining the ranks that hold the same
+// rows of different batches -- rank `group` of `groups`.  Only an all-gather;
+// same transports and ordering as above.
+int sfp_group_init_rccl(sfp_dev* d, int group, int groups, const void* uid128);
+void sfp_group_set_host(sfp_dev* d, int group, int groups, sfp_host_allgather_fn ag, void* user);
+// recv = groups blocks of `bytes`, group-major (recv may contain send in place)
+void sfp_group_allgather(sfp_dev* d, const void* send, void* recv, size_t bytes);
+
 // dst row i = src row rows[i] (count rows of n words; rows: host array)
 void sfp_gather_rows(sfp_dev* d, uint64_t* dst, const uint64_t* src, const uint32_t* rows, uint32_t count);
 

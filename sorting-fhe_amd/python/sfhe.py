@@ -42,6 +42,7 @@ ABI_SYMBOLS = [
     "sfhe_sorter_sort_bitonic", "sfhe_kway_sort", "sfhe_kway_params",
     "sfhe_save", "sfhe_load", "sfhe_ct_save", "sfhe_ct_load",
     "sfhe_kway_create", "sfhe_kway_run", "sfhe_kway_destroy", "sfhe_shard_tail",
+    "sfhe_groups_rccl", "sfhe_groups_host", "sfhe_groups",
     "sfhe_encode_counts", "sfhe_bootstrap_graphs",
 ]
 
@@ -149,6 +150,9 @@ _SIGS = {
     "sfhe_shard_rccl": (C.c_int, [_VP, C.c_int, C.c_int, _VP]),
     "sfhe_shard_host": (C.c_int, [_VP, C.c_int, C.c_int, _AG, _BC, _VP]),
     "sfhe_shard_tail": (C.c_int, [_VP, _PU32]),
+    "sfhe_groups_rccl": (C.c_int, [_VP, C.c_int, C.c_int, _VP]),
+    "sfhe_groups_host": (C.c_int, [_VP, C.c_int, C.c_int, _AG, _VP]),
+    "sfhe_groups": (C.c_int, [_VP, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "sfhe_encode_counts": (C.c_int, [_VP, _PU64, _PU64]),
     "sfhe_bootstrap_graphs": (C.c_int, [_VP, _PU64]),
 }
@@ -192,9 +196,11 @@ class Engine:
                  batch_size: int = 0, scaling_mod_size: int = 40, first_mod_size: int = 60,
                  secure: bool = False, num_large_digits: int = 0, seed: int = 0x5EED5EED2025,
                  device: int = 0, rotations: Sequence[int] = (), keygen: bool = True,
-                 scaling: str = "FLEXIBLEAUTOEXT", shard=None):
+                 scaling: str = "FLEXIBLEAUTOEXT", shard=None, groups=None):
         """shard: None, ("rccl", rank, world, uid) or ("host", rank, world, comm)
-        (limb sharding, include/sfhe.h; every rank passes the same params)."""
+        (limb sharding, include/sfhe.h; every rank passes the same params).
+        groups: None, ("rccl", group, groups, uid) or ("host", group, groups,
+        comm): the sort's batches split over batch groups (sfhe_groups_*)."""
         self.lib = load(backend)
         self.backend = backend
         p = Params()
@@ -220,6 +226,14 @@ class Engine:
                 self.shard_host(rank, world, arg)
             else:
                 raise ValueError(f"unknown shard transport {kind!r}")
+        if groups is not None:
+            kind, g, G, arg = groups
+            if kind == "rccl":
+                self.groups_rccl(g, G, arg)
+            elif kind == "host":
+                self.groups_host(g, G, arg)
+            else:
+                raise ValueError(f"unknown group transport {kind!r}")
         if keygen:
             self._chk(self.lib.sfhe_keygen(self.ctx))
             if rotations:
@@ -278,6 +292,22 @@ class Engine:
         bc = _BC(lambda _u, buf, nb, root: comm.bcast(rank, buf, nb, root))
         self._chk(self.lib.sfhe_shard_host(self.ctx, rank, world, ag, bc, None))
         self._comm_refs = (ag, bc, comm)  # the library keeps the raw pointers
+
+    def groups_rccl(self, group: int, groups: int, uid: bytes):
+        buf = (C.c_uint8 * 128).from_buffer_copy(bytes(uid))
+        self._chk(self.lib.sfhe_groups_rccl(self.ctx, group, groups, buf))
+
+    def groups_host(self, group: int, groups: int, comm):
+        """comm: as shard_host's (only its allgather is used)."""
+        ag = _AG(lambda _u, send, recv, nb: comm.allgather(group, send, recv, nb))
+        self._chk(self.lib.sfhe_groups_host(self.ctx, group, groups, ag, None))
+        self._group_refs = (ag, comm)
+
+    def groups(self):
+        """(group, groups) of the batch split ((0, 1): unsplit)."""
+        g, G = C.c_int(), C.c_int()
+        self._chk(self.lib.sfhe_groups(self.ctx, C.byref(g), C.byref(G)))
+        return g.value, G.value
 
     def shard_tail(self) -> int:
         """Replicated-tail limb count of a sharded context (0: unsharded)."""
@@ -686,9 +716,45 @@ class GlooComm:
     def bcast(self, rank, buf, nbytes, root):
         import torch
         t = torch.frombuffer(bytearray(C.string_at(buf, nbytes)), dtype=torch.uint8)
-        self.dist.broadcast(t, src=root, group=self.group)
+        # root is a rank of this communicator; torch wants the global rank
+        src = root if self.group is None else self.dist.get_global_rank(self.group, root)
+        self.dist.broadcast(t, src=src, group=self.group)
         if rank != root:
             C.memmove(buf, t.numpy().ctypes.data, nbytes)
+
+
+def run_split_threads(backend: str, world: int, groups: int, fn, **engine_kw):
+    """Run fn(engine) on `world` thread ranks split into `groups` batch groups
+    of world // groups ranks (rank = group * (world // groups) + r); each
+    group limb-sharded over its own ThreadComm when it has more than one
+    rank.  Returns the per-rank results (rank order)."""
+    import threading
+    per = world // groups
+    if per * groups != world:
+        raise ValueError("world must be a multiple of groups")
+    limb = [ThreadComm(per) for _ in range(groups)]
+    grp = [ThreadComm(groups) for _ in range(per)]
+    outs, errs = [None] * world, []
+
+    def body(rank):
+        g, r = divmod(rank, per)
+        try:
+            shard = ("host", r, per, limb[g]) if per > 1 else None
+            e = Engine(backend, shard=shard, groups=("host", g, groups, grp[r]), **engine_kw)
+            outs[rank] = fn(e)
+        except BaseException as ex:  # unblock the other ranks
+            errs.append(ex)
+            for c in limb + grp:
+                c.bar.abort()
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if errs:
+        raise errs[0]
+    return outs
 
 
 def run_sharded_threads(backend: str, world: int, fn, **engine_kw):

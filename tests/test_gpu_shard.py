@@ -57,6 +57,21 @@ def test_sharded_sort_large_bitexact_hip(hip_lib, N, logn, world):
         compare(ref, outs[r])
 
 
+@pytest.mark.parametrize("N,logn,world,groups", [(256, 16, 2, 2), (256, 16, 8, 2), (256, 17, 4, 2)])
+def test_batch_split_sort_bitexact_hip(hip_lib, N, logn, world, groups):
+    """The bench's multi-GPU layout as thread ranks on this GPU: two batch
+    groups (each runs one of the sort's two batches per phase; parts
+    all-gathered over the host transport), each group limb-sharded over
+    world // groups ranks -- the metric sort at W = 2 (split only) and W = 8
+    (2 x 4), config 5's at W = 4 -- bit-identical to the unsplit sort."""
+    depth, rots = sfhe.direct_sort_params(N, "hip")
+    kw = dict(mult_depth=depth, ring_dim=1 << logn, batch_size=N, rotations=rots, seed=4099)
+    ref = sort_program(sfhe.Engine("hip", **kw), N)
+    outs = sfhe.run_split_threads("hip", world, groups, lambda e: sort_program(e, N), **kw)
+    for r in range(world):
+        compare(ref, outs[r])
+
+
 RCCL_SCRIPT = r"""
 import os, sys
 sys.path.insert(0, {py!r}); sys.path.insert(0, {tests!r})
@@ -84,8 +99,10 @@ x = slotsim.input_vector(N)
 ref = sfhe.Engine("hip", **kw); ref.set_quiet(True)
 want = ref.sorter(N).sort(ref.encrypt(x.tolist()), *cfg).download()
 ref.close()
-uid = sfhe.comm_uid("hip")
-e = sfhe.Engine("hip", shard=("rccl", 0, 1, uid), **kw); e.set_quiet(True)
+uid, uid2 = sfhe.comm_uid("hip"), sfhe.comm_uid("hip")
+# and a one-group batch communicator: every part of both phases through ncclAllGather
+e = sfhe.Engine("hip", shard=("rccl", 0, 1, uid), groups=("rccl", 0, 1, uid2), **kw); e.set_quiet(True)
+assert e.groups() == (0, 1)
 s = e.sorter(N)
 ct = e.encrypt(x.tolist())
 outs = [s.sort(ct, *cfg) for _ in range(3)]   # eager, captured, replayed
@@ -107,7 +124,9 @@ print("RCCL graph OK")
 def test_rccl_single_rank_communicator(hip_lib, N, logn, tail):
     """sfhe_comm_uid + sfhe_shard_rccl (ncclCommInitRank) on one rank: the
     context takes the sharded code path with every exchange an RCCL call
-    (ncclAllGather / ncclBroadcast, not the one-rank device copy).  The op
+    (ncclAllGather / ncclBroadcast, not the one-rank device copy); the sort
+    also has a one-group batch communicator (sfhe_groups_rccl) through which
+    every batch part is all-gathered.  The op
     program, then DirectSort<N> sorted eagerly, captured into a hipGraph
     WITH its RCCL collectives, and replayed -- all bit-identical to the
     unsharded sort.  Own process: RCCL's threads and the HIP runtime are torn

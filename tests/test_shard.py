@@ -195,3 +195,44 @@ def test_sharded_sort_gloo_two_processes(oracle_lib, tmp_path, N, logn):
     for r in range(2):
         z = np.load(f"{path}{r}.npz")
         compare(ref, {k: z[k] for k in z.files})
+
+
+@pytest.mark.parametrize("world,groups", [(1, 1), (2, 2), (4, 2)])
+def test_batch_split_sort_bitexact_oracle(oracle_lib, world, groups):
+    """DirectSort<64> @ 2^12 has B = 2 batches in both phases (P = 32): with
+    two batch groups each group runs one batch and all-gathers the parts
+    (sfhe_groups_host); W = 4 also limb-shards each group over two ranks.
+    Every rank's result is bit-identical to the unsplit sort.  (1, 1): one
+    group that still gathers every part through its communicator."""
+    N, logn = 64, 12
+    depth, rots = sfhe.direct_sort_params(N, "oracle")
+    kw = dict(mult_depth=depth, ring_dim=1 << logn, batch_size=N, rotations=rots, seed=777)
+
+    def prog(e):
+        e.op_stats(reset=True)
+        out = sort_program(e, N)
+        return out, e.op_stats()["tensor"]
+
+    ref, ref_tensors = prog(sfhe.Engine("oracle", **kw))
+    assert np.max(np.abs(ref["dec"][:N] - np.sort(slotsim.input_vector(N)))) < 0.01
+    outs = sfhe.run_split_threads("oracle", world, groups, prog, **kw)
+    for r in range(world):
+        compare(ref, outs[r][0])
+        if groups > 1:  # one of the two batches per rank: about half the ct x ct products
+            assert outs[r][1] < 0.6 * ref_tensors, (outs[r][1], ref_tensors)
+
+
+def test_batch_groups_arguments(oracle_lib):
+    e = sfhe.Engine("oracle", keygen=False, mult_depth=2, ring_dim=1 << 12)
+    assert e.groups() == (0, 1)
+    with pytest.raises(sfhe.SfheError):
+        e.groups_host(2, 2, sfhe.ThreadComm(2))  # group outside the groups
+    e.groups_host(1, 2, sfhe.ThreadComm(2))
+    assert e.groups() == (1, 2)
+    with pytest.raises(sfhe.SfheError):
+        e.groups_host(0, 2, sfhe.ThreadComm(2))  # already set
+    e2 = sfhe.Engine("oracle", mult_depth=2, ring_dim=1 << 12)
+    with pytest.raises(sfhe.SfheError):  # after key generation
+        e2.groups_host(0, 2, sfhe.ThreadComm(2))
+    with pytest.raises(sfhe.SfheError):  # the oracle has no RCCL
+        e2.groups_rccl(0, 2, bytes(128))
