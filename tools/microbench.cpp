@@ -127,6 +127,9 @@ int main(int argc, char** argv) {
         (void)sq;
         convs = s->modupConv.at(ell);
     }
+    // the conversion family's algorithmic bytes from here on (tools/pmc_traffic.py
+    // pairs them with the last CONV_ALGO launches of the PMC passes)
+    sfp_prof_set(d, SFP_FAM_CONV, 1);
     const double mu = timeIt(d, 30, [&] {
         sfp_modup(d, ext, buf, ell, K, s->Lq, s->alpha, convs.data(), scr);
     });
@@ -146,6 +149,18 @@ int main(int argc, char** argv) {
     const double rs = timeIt(d, 30, [&] {
         sfp_rescale(d, out, buf, ell, s->qInvTable[ell].data(), 2, (size_t)ell * n, (size_t)(ell - 1) * n);
     });
+    // the fused key-switch chains (ModUp + inner product in one pass family;
+    // tensor + relinearisation + rescale without the tensor in HBM)
+    const double mi = timeIt(d, 30, [&] {
+        sfp_modup_inner(d, acc, acc + stride, buf, ell, K, s->Lq, s->alpha, convs.data(), s->relinKey->ptr,
+                        nullptr, nullptr, 0, 0, ~0u, ext, scr);
+    });
+    const size_t pw = (size_t)ell * n;
+    const double mr = timeIt(d, 30, [&] {
+        sfp_mult_relin_rescale(d, out, out + pw, buf, buf + pw, buf + 2 * pw, buf + 3 * pw, ell, K, s->Lq,
+                               s->alpha, convs.data(), s->relinKey->ptr, s->moddownConv, s->pInvModQ.data(),
+                               s->pModQ.data(), s->qInvTable[ell].data(), acc, ext, scr);
+    });
     const double B = 8.0 * n;
     std::printf("modup   ell=%u beta=%u: %8.2f us  (%.1f GB/s on ell + beta(ell+K) rows)\n", ell, beta,
                 mu, (ell + beta * (ell + K)) * B / mu / 1e3);
@@ -153,6 +168,15 @@ int main(int argc, char** argv) {
     std::printf("moddown2            : %8.2f us  (%.1f GB/s on 2(ell+K) + 2 ell rows)\n", md,
                 (2.0 * (ell + K) + 2.0 * ell) * B / md / 1e3);
     std::printf("rescale x2 polys    : %8.2f us  (%.1f GB/s on 4 ell rows)\n", rs, 4.0 * ell * B / rs / 1e3);
+    std::printf("modup_inner (fused) : %8.2f us  (modup + ks_inner: %.2f us)\n", mi, mu + ki);
+    std::printf("mult_relin_rescale  : %8.2f us\n", mr);
+    {
+        uint64_t launches = 0, timed = 0;
+        double ms = 0, bytes = 0;
+        sfp_prof_read(d, SFP_FAM_CONV, &launches, &timed, &ms, &bytes);
+        sfp_prof_set(d, SFP_FAM_CONV, 0);
+        std::printf("CONV_ALGO launches=%llu bytes=%.0f ms=%.3f\n", (unsigned long long)launches, bytes, ms);
+    }
     const char* e = sfp_last_error(d);
     if (e) std::printf("ERROR: %s\n", e);
     return e ? 1 : 0;

@@ -32,8 +32,8 @@ def main():
     segs.append(cur)
     big = [s for s in segs if len(s) > 1000]
     seg = sorted(big, key=len)[len(big) // 2]
-    ys = [r[3] for r in seg if "k_ntt" in r[2]]
-    dur = [(r[1] - r[0]) / 1e3 for r in seg if "k_ntt" in r[2]]
+    ys = [r[3] for r in seg if "k_ntt<" in r[2]]  # not k_ntt_ks (the fused key inner product)
+    dur = [(r[1] - r[0]) / 1e3 for r in seg if "k_ntt<" in r[2]]
     print(f"segment of {len(seg)} kernels: {len(ys)} NTT passes")
     print(f"rows per pass: mean {statistics.mean(ys):.1f}, median {statistics.median(ys)}, "
           f"row-weighted mean {sum(y * y for y in ys) / sum(ys):.1f}")

@@ -28,6 +28,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def family(name: str):
     s = name.split("(")[0].replace("void ", "")
+    if s.startswith("k_ntt_ks"):  # the fused ModUp ROW pass + key inner product
+        return "ks_inner"
     if s.startswith("k_ntt"):
         return "ntt"
     if s.startswith("k_conv") or s.startswith("k_mdrs"):
@@ -61,7 +63,16 @@ def main():
     ap.add_argument("write_csv")
     ap.add_argument("--n", type=int, default=65536)
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--mb-log", default=None,
+                    help="microbench stdout: its CONV_ALGO line gives the conversion launches' algorithmic bytes")
     a = ap.parse_args()
+    conv_algo = None
+    if a.mb_log:
+        with open(a.mb_log) as f:
+            for line in f:
+                m = re.match(r"CONV_ALGO launches=(\d+) bytes=([\d.e+]+)", line)
+                if m:
+                    conv_algo = (int(m.group(1)), float(m.group(2)))
     fe = load(a.fetch_csv, "FETCH_SIZE")
     wr = load(a.write_csv, "WRITE_SIZE")
     acc = collections.defaultdict(lambda: {"launches": 0, "fetch": 0.0, "write": 0.0, "algo": 0.0})
@@ -78,6 +89,9 @@ def main():
     out = {}
     for fam in fam_f:
         F, W = fam_f[fam], fam_w.get(fam, [])
+        if fam == "conv" and conv_algo:  # the launches the microbench's byte count covers: the last L
+            L = conv_algo[0]
+            F, W = F[-L:], W[-L:]
         k = min(len(F), len(W))
         fetch = sum(v for _, _, v in F[:k]) * 1024 * 2
         write = sum(v for _, _, v in W[:k]) * 1024
@@ -87,6 +101,9 @@ def main():
             algo = sum(16.0 * ntt_rows(nm, g, a.n) * a.n for nm, g, _ in F[:k])
             entry["algorithmic_bytes_per_launch"] = algo / k
             entry["traffic_over_algorithmic"] = (fetch + write) / algo
+        if fam == "conv" and conv_algo and k == conv_algo[0]:
+            entry["algorithmic_bytes_per_launch"] = conv_algo[1] / k
+            entry["traffic_over_algorithmic"] = (fetch + write) / conv_algo[1]
         out[fam] = entry
     src = os.path.join(ROOT, "sorting-fhe_amd", "csrc", "hip", "prims_hip.hip")
     with open(src, "rb") as f:

@@ -33,7 +33,7 @@ def main():
         agg[k][0] += 1
         agg[k][1] += dur
         total += dur
-        if k.startswith("k_ntt"):
+        if k.startswith("k_ntt<"):
             agg[k][2] += gy * a.n * 16.0  # one pass reads and writes every coefficient once
     print(f"{'kernel':34s} {'calls':>8s} {'total ms':>10s} {'avg us':>8s} {'share':>6s} {'GB/s':>8s}")
     for k, (c, d, b) in sorted(agg.items(), key=lambda kv: -kv[1][1])[: a.top]:
