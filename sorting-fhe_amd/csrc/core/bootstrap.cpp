@@ -205,6 +205,10 @@ void dbg(CryptoContextImpl<DCRTPoly>* cc, const BootstrapPrecomp& b, const char*
 
 }  // namespace
 
+double CryptoContextImpl<DCRTPoly>::BootstrapOverflowBound() { return kOverflowBound + 1.0; }
+uint32_t CryptoContextImpl<DCRTPoly>::BootstrapDoubleAngles() { return kDoubleAngles; }
+uint32_t CryptoContextImpl<DCRTPoly>::BootstrapChebDegree() { return kChebDegree; }
+
 void CryptoContextImpl<DCRTPoly>::EvalBootstrapSetup(std::vector<uint32_t> levelBudget, std::vector<uint32_t>,
                                                      uint32_t slots, uint32_t) {
     OpLock g(st.get());
@@ -224,9 +228,16 @@ void CryptoContextImpl<DCRTPoly>::EvalBootstrapSetup(std::vector<uint32_t> level
     b->c2s = groupStages(c2sStages, levelBudget[0], slots);
     b->s2c = groupStages(s2cStages, levelBudget[1], slots);
     // C2S scale: 1/S of the inverse FFT, 1/gap of the trace, the raised
-    // ciphertext's scale label Delta_0 / q_0, and 1/2 for the re/im split
+    // ciphertext's scale label Delta_0 / q_0, and 1/2 for the re/im split --
+    // about 1/n in all, spread evenly over the groups.  Every C2S product
+    // multiplies the raised values m + q_0 I, whose I part is ~2^24 times the
+    // message, by diagonals quantised at the level's scale: diagonals of
+    // magnitude 2^-e lose e bits of that quantisation's relative precision,
+    // and the error is amplified by I / m at the output.  The whole 1/n on
+    // the first group cost 2^-16 at ring 2^15 (tools/boot_probe).
     const double q0 = (double)s->primes[0];
-    scaleMap(b->c2s.front().diags, cd(s->scale[0] / (q0 * b->gap * slots * 2.0)));
+    const double c2sScale = s->scale[0] / (q0 * b->gap * slots * 2.0);
+    for (auto& gr : b->c2s) scaleMap(gr.diags, cd(std::pow(c2sScale, 1.0 / (double)b->c2s.size())));
     std::set<int32_t> rot;
     for (const auto* gs : {&b->c2s, &b->s2c})
         for (const auto& gr : *gs)
@@ -354,19 +365,23 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::BootstrapOnce(const Ciphertext
     const double deltaL = s->scale[s->L];
     const int preScaleBits =
         std::max(0, kTargetBits - (int)std::lround(std::log2((double)s->primes[0] / deltaL)));
+    auto tap = [&](const char* what, const Ciphertext<DCRTPoly>& c, const DiagMap* m) {
+        dbg(this, b, what, c);
+        if (bootTap) bootTap(what, c, m);
+    };
     auto low = AdjustLevelScaled(ct, s->L, inFactor * std::ldexp(1.0, -preScaleBits));
-    dbg(this, b, "low", low);
+    tap("low", low, nullptr);
     auto raised = ModRaise(low);
     raised->SetSlots(S);
-    dbg(this, b, "raised", raised);
+    tap("raised", raised, nullptr);
     // 3: sparse trace
     for (uint32_t t = S; t < s->n / 2; t <<= 1) raised = EvalAdd(raised, EvalRotate(raised, (int32_t)t));
-    dbg(this, b, "traced", raised);
+    tap("traced", raised, nullptr);
     // 4: CoeffsToSlots (h = u / 2 in bit-reversed order)
     Ciphertext<DCRTPoly> h = raised;
     for (auto& gr : b.c2s) {
         h = applyGroup(this, gr, S, {h}, false);
-        dbg(this, b, "c2s", h);
+        tap("c2s", h, &gr.diags);
     }
     // 5: real and imaginary halves
     auto hc = EvalConjugate(h);
@@ -377,12 +392,12 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::BootstrapOnce(const Ciphertext
     auto yre = EvalMult(re, 1.0 / Kb);
     Plaintext negi = MakeCKKSPackedPlaintext(std::vector<cd>(S, cd(0.0, -1.0 / Kb)), 1, imi->GetLevel(), nullptr, S);
     auto yim = EvalMult(imi, negi);
-    dbg(this, b, "re", re);
-    dbg(this, b, "yim", yim);
+    tap("yre", yre, nullptr);
+    tap("yim", yim, nullptr);
     auto wre = evalMod(this, b, yre);
     auto wim = evalMod(this, b, yim);
-    dbg(this, b, "wre", wre);
-    dbg(this, b, "wim", wim);
+    tap("wre", wre, nullptr);
+    tap("wim", wim, nullptr);
     // 7: SlotsToCoeffs of w_re + i w_im, times q_0 2^k outFactor / (2 pi Delta_L)
     const double cOut = (double)s->primes[0] * std::ldexp(1.0, preScaleBits) * outFactor / (2.0 * M_PI * deltaL);
     // the first S2C group with cOut folded into its diagonals (one copy per
@@ -395,10 +410,10 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::BootstrapOnce(const Ciphertext
         fit = b.s2cFirst.emplace(cOut, std::move(g0)).first;
     }
     auto out = applyGroup(this, fit->second, S, {wre, wim}, true);
-    dbg(this, b, "s2c", out);
+    tap("s2c", out, &fit->second.diags);
     for (size_t g = 1; g < b.s2c.size(); ++g) {
         out = applyGroup(this, b.s2c[g], S, {out}, false);
-        dbg(this, b, "s2c", out);
+        tap("s2c", out, &b.s2c[g].diags);
     }
     return out;
 }
@@ -431,7 +446,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::bootstrapReplay(const Cipherte
     OpLock lk(s);
     auto it = s->boot.find(ct->GetSlots());
     const char* gv = std::getenv("SFHE_GRAPH");
-    if (it == s->boot.end() || (gv && *gv == '0') || s->capturing || s->forkedLanes)
+    if (it == s->boot.end() || (gv && *gv == '0') || s->capturing || s->forkedLanes || bootTap)
         return bootstrapIters(ct, numIterations, precision);
     BootstrapPrecomp::Replay& r = it->second->replays[std::make_tuple(ct->GetLevel(), numIterations, precision)];
     if (r.off || r.uses++ == 0) return bootstrapIters(ct, numIterations, precision);

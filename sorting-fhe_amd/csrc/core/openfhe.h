@@ -445,6 +445,22 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
     Ciphertext<DCRTPoly> bootstrapReplay(const Ciphertext<DCRTPoly>& ct, uint32_t numIterations, uint32_t precision);
     // bootstrap shapes replayed from a captured graph so far
     size_t BootstrapGraphs() const;
+    // Diagnostics (tools/prec_probe boot; not for production): called after
+    // every bootstrapping stage of BootstrapOnce with the stage's output and,
+    // for the linear stages (CoeffsToSlots / SlotsToCoeffs groups), the slot
+    // map applied: out[p] = sum_k v_k[p] in[(p + k) mod S] (the first
+    // SlotsToCoeffs group takes in = re + i im).  Stages: "low", "raised",
+    // "traced", "c2s", "yre", "yim", "wre", "wim", "s2c".  Bootstraps run
+    // eagerly while a tap is set.
+    using BootstrapSlotMap = std::map<uint32_t, std::vector<std::complex<double>>>;
+    using BootstrapTap =
+        std::function<void(const char* stage, const Ciphertext<DCRTPoly>& ct, const BootstrapSlotMap* map)>;
+    void SetBootstrapTap(BootstrapTap tap) { bootTap = std::move(tap); }
+    // K + 1 of EvalMod's input scaling (y = x / (K + 1)) and the number of
+    // double angles (diagnostics)
+    static double BootstrapOverflowBound();
+    static uint32_t BootstrapDoubleAngles();
+    static uint32_t BootstrapChebDegree();
 
     // ---------------- engine extensions (not OpenFHE) ----------------
     SfheContextState* state() const { return st.get(); }
@@ -551,6 +567,7 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
   private:
     std::unique_ptr<SfheContextState> st;
     uint32_t enabled = 0;
+    BootstrapTap bootTap;
     friend class SfheInternal;
 };
 
