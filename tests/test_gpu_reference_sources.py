@@ -18,10 +18,27 @@ BUILD = os.path.join(HERE, "cxx", "build")
 pytestmark = pytest.mark.gpu
 
 
+CSRC = os.path.join(os.path.dirname(HERE), "sorting-fhe_amd", "csrc")
+
+
+def _newest_header() -> float:
+    t = 0.0
+    for d, _, fs in os.walk(CSRC):
+        for f in fs:
+            if f.endswith(".h"):
+                t = max(t, os.path.getmtime(os.path.join(d, f)))
+    return t
+
+
 def exe(name):
     p = os.path.join(BUILD, name + "_hip")
     if not os.access(p, os.X_OK):
         pytest.skip(f"{name}_hip not built (tests/cxx/reference_harness.py runs where the reference is)")
+    # the programs compile the engine's headers (sort_algo.h, openfhe.h,
+    # state.h) into themselves: one built before a header change disagrees
+    # with the library on object layouts, which corrupts memory at run time
+    assert os.path.getmtime(p) >= _newest_header(), (
+        f"{name}_hip is older than the engine headers: rebuild it (python tests/cxx/reference_harness.py)")
     return p
 
 
