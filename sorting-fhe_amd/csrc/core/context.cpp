@@ -1742,6 +1742,10 @@ void CryptoContextImpl<DCRTPoly>::EvalMultKeyGen(const PrivateKey<DCRTPoly>& sk)
     sfp_mul(s->dev, s2->ptr, sk->s->ptr, sk->s->ptr, sfp_limbs{NP, NP, 0});
     s->relinKey = SfheInternal::genSwitchKey(this, s2->ptr, sk->s->ptr);
     s->keyTag = sk->tag;
+    // every level's ModUp conversion tables now, as OpenFHE precomputes its
+    // CRT tables with the context: built lazily, each upload drained the
+    // device inside the first sort
+    for (uint32_t ell = 1; ell <= s->Lq; ++ell) SfheInternal::modupConv(this, ell);
 }
 
 void CryptoContextImpl<DCRTPoly>::EvalRotateKeyGen(const PrivateKey<DCRTPoly>& sk,

@@ -140,7 +140,16 @@ struct sfp_dev {
     u64* cpool = nullptr;
     u64* cpoolOld = nullptr;  // the retired generation (devConst)
     size_t cpoolCap = 0, cpoolOff = 0;
-    std::unordered_map<uint64_t, std::vector<std::pair<std::vector<u64>, size_t>>> cmap;
+    // contents -> pool offset; a miss is uploaded on the lane that made it
+    // (stream-ordered, no drain), and another lane's first hit waits for
+    // that upload's event
+    struct ConstEntry {
+        std::vector<u64> v;
+        size_t off;
+        int lane;
+        hipEvent_t ev;
+    };
+    std::unordered_map<uint64_t, std::vector<ConstEntry>> cmap;
     std::mutex mu;
     std::string err;
     // limb sharding: this process is rank `rank` of `world`
@@ -2400,6 +2409,27 @@ static const u64* arenaPut(sfp_dev* d, const void* src, size_t bytes) {
     return dv;
 }
 
+// Host bytes -> device address dst through the pinned ring, ordered on the
+// current lane (ringPut's rules: the region is reused after a full drain).
+static void ringUpload(sfp_dev* d, void* dst, const void* src, size_t bytes) {
+    const size_t span = (bytes + 255) & ~(size_t)255;
+    if (d->ringOff + span > d->ringCap) {
+        syncAll(d);
+        d->ringOff = 0;
+    }
+    char* h = d->hring + d->ringOff;
+    std::memcpy(h, src, bytes);
+    devCopy(d, dst, h, bytes);
+    d->ringOff += span;
+}
+
+static void constClear(sfp_dev* d) {
+    for (auto& kv : d->cmap)
+        for (auto& e : kv.second)
+            if (e.ev) hipEventDestroy(e.ev);
+    d->cmap.clear();
+}
+
 static void* ringPut(sfp_dev* d, const void* src, size_t bytes) {
     if (d->capture) return const_cast<u64*>(arenaPut(d, src, bytes));
     const size_t span = (bytes + 255) & ~(size_t)255;  // keep entries 256-B aligned
@@ -2453,7 +2483,16 @@ static const u64* devConst(sfp_dev* d, const u64* v, size_t count) {
     }
     auto& bucket = d->cmap[h];
     for (auto& e : bucket)
-        if (e.first.size() == count && std::equal(v, v + count, e.first.begin())) return d->cpool + e.second;
+        if (e.v.size() == count && std::equal(v, v + count, e.v.begin())) {
+            if (e.ev && e.lane != d->cur) {  // uploaded on another lane: order after it
+                SFP_CHECK(hipStreamWaitEvent(d->st(), e.ev, 0));
+                if (hipEventQuery(e.ev) == hipSuccess) {  // done: later hits need no wait
+                    hipEventDestroy(e.ev);
+                    e.ev = nullptr;
+                }
+            }
+            return d->cpool + e.off;
+        }
     const size_t words = (count + 1) & ~(size_t)1;  // keep 16-B alignment
     if (!d->cpool || d->cpoolOff + words > d->cpoolCap) {
         // Two generations: the full pool is retired, not overwritten, so
@@ -2467,13 +2506,20 @@ static const u64* devConst(sfp_dev* d, const u64* v, size_t count) {
         }
         std::swap(d->cpool, d->cpoolOld);
         if (!d->cpool) SFP_CHECK(hipMalloc((void**)&d->cpool, d->cpoolCap * 8));
-        d->cmap.clear();
+        constClear(d);
         d->cpoolOff = 0;
     }
     const size_t off = d->cpoolOff;
     d->cpoolOff += words;
-    hostToDev(d, d->cpool + off, v, count * 8);
-    d->cmap[h].push_back({std::vector<u64>(v, v + count), off});
+    // through the pinned ring on this lane's stream: a miss no longer drains
+    // the device (the cold sort's first use of every per-level constant)
+    ringUpload(d, d->cpool + off, v, count * 8);
+    hipEvent_t ev = nullptr;
+    if (d->nLanes > 1 && !d->serial) {
+        SFP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        SFP_CHECK(hipEventRecord(ev, d->st()));
+    }
+    d->cmap[h].push_back({std::vector<u64>(v, v + count), off, d->cur, ev});
     return d->cpool + off;
 }
 
@@ -2603,6 +2649,7 @@ void sfp_destroy(sfp_dev* d) {
     }
     for (auto& f : d->prof) profFlush(d, f);
     for (hipEvent_t e : d->evPool) hipEventDestroy(e);
+    constClear(d);
     hipFree(d->bar);
     hipFree(d->psi);
     hipFree(d->psiS);
