@@ -99,6 +99,9 @@ int sfhe_bootstrap_graphs(sfhe_ctx* c, uint64_t* count);
 int sfhe_encode_counts(sfhe_ctx* c, uint64_t* device, uint64_t* host);
 /* Device memory held by the context's buffer pool (live and free blocks). */
 int sfhe_pool_bytes(sfhe_ctx* c, uint64_t* bytes);
+/* Engine contexts alive in this process (diagnostics: after every
+ * sfhe_context_destroy of a process's contexts it is back to 0). */
+int sfhe_live_contexts(void);
 /* Live kernel timing (bench roofline; no reference counterpart): kernel
  * families SFHE_KFAM_*; every `period`-th launch of the family is bracketed
  * by HIP events on the context's stream (period 0 = off; resets counters).

@@ -790,6 +790,8 @@ int sfhe_context_primes(sfhe_ctx* c, uint64_t* out, size_t cap, size_t* count) {
     return SFHE_OK;
 }
 
+int sfhe_live_contexts(void) { return CryptoContextImpl<DCRTPoly>::LiveContexts(); }
+
 int sfhe_pool_bytes(sfhe_ctx* c, uint64_t* bytes) {
     REQUIRE(c && bytes, "null argument");
     *bytes = c->cc->GetOpStats().pool_bytes;

@@ -474,12 +474,34 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::bootstrapReplay(const Cipherte
         }
         r.out = out;
     } else {
+        r.in->cc = shared_from_this();
         CopyCiphertextInto(r.in, ct);
     }
+    // the replay's ciphertexts are the context's own: bound to it only while
+    // in use (a stored strong reference would be a cycle that keeps every
+    // context with a replayed bootstrap, and its device memory, alive)
+    struct Unbind {
+        BootstrapPrecomp::Replay& r;
+        ~Unbind() {
+            r.in->cc.reset();
+            r.out->cc.reset();
+        }
+    } unbind{r};
+    r.out->cc = shared_from_this();
     Launch(r.g);
     auto res = r.out->Clone();
     res->SetSlots(r.out->GetSlots());
     return res;
+}
+
+void CryptoContextImpl<DCRTPoly>::releaseBootstrapGraphs() {
+    for (auto& [slots, b] : st->boot)
+        for (auto& [shape, r] : b->replays) {
+            if (r.g) ReleaseGraph(*r.g);
+            r.g.reset();
+            r.in.reset();
+            r.out.reset();
+        }
 }
 
 size_t CryptoContextImpl<DCRTPoly>::BootstrapGraphs() const {

@@ -10,6 +10,7 @@
 //
 // All polynomial work is enqueued through csrc/prims.h.
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -1379,6 +1380,10 @@ struct DeferredRelin : DeferredOp {
 // ============================================================================
 // context construction
 
+// contexts alive in this process (diagnostics: sfhe_live_contexts)
+static std::atomic<int> g_liveContexts{0};
+int CryptoContextImpl<DCRTPoly>::LiveContexts() { return g_liveContexts.load(); }
+
 CryptoContextImpl<DCRTPoly>::CryptoContextImpl(const CCParams<CryptoContextCKKSRNS>& p)
     : st(new SfheContextState) {
     SfheContextState& s = *st;
@@ -1556,13 +1561,16 @@ CryptoContextImpl<DCRTPoly>::CryptoContextImpl(const CCParams<CryptoContextCKKSR
         for (uint32_t i = 0; i + 1 < ell; ++i)
             s.qInvTable[ell].push_back(invmod(ql % s.primes[i], s.primes[i]));
     }
+    g_liveContexts.fetch_add(1);
 }
 
 CryptoContextImpl<DCRTPoly>::~CryptoContextImpl() {
     if (!st) return;
+    g_liveContexts.fetch_sub(1);
     st->relinKey.reset();
     st->rotKeys.clear();
     st->ptCache.clear();
+    releaseBootstrapGraphs();  // the replay graphs' blocks back to the pool first
     st->boot.clear();  // its diagonal encodings return blocks to the pool below
     for (auto& kv : st->modupConv)
         for (auto* c : kv.second) sfp_free_conv(st->dev, c);
@@ -2934,20 +2942,28 @@ struct CryptoContextImpl<DCRTPoly>::CapturedGraph {
     ~CapturedGraph() {
         keep.reset();
         auto c = cc.lock();
-        if (!c) return;  // the context is gone: its pool and device went with it
-        SfheContextState* s = c->state();
-        OpLock lk(s);
-        sfp_graph_destroy(s->dev, g);  // drains the device first
-        std::lock_guard<std::mutex> pg(s->poolMu);
-        for (auto& o : owned) {
-            auto it = s->graphOwned.find(o.first);
-            if (it == s->graphOwned.end()) continue;
-            const bool live = it->second;
-            s->graphOwned.erase(it);
-            if (!live) s->freeList[0][o.second].push_back(o.first);  // else its holder frees it
-        }
+        if (!c) return;  // the context is gone (or releasing it: ReleaseGraph ran)
+        c->ReleaseGraph(*this);
     }
 };
+
+void CryptoContextImpl<DCRTPoly>::ReleaseGraph(CapturedGraph& cg) {
+    SfheContextState* s = st.get();
+    OpLock lk(s);
+    cg.keep.reset();
+    if (cg.g) sfp_graph_destroy(s->dev, cg.g);  // drains the device first
+    cg.g = nullptr;
+    std::lock_guard<std::mutex> pg(s->poolMu);
+    for (auto& o : cg.owned) {
+        auto it = s->graphOwned.find(o.first);
+        if (it == s->graphOwned.end()) continue;
+        const bool live = it->second;
+        s->graphOwned.erase(it);
+        if (!live) s->freeList[0][o.second].push_back(o.first);  // else its holder frees it
+    }
+    cg.owned.clear();
+    cg.cc.reset();
+}
 
 bool CryptoContextImpl<DCRTPoly>::BeginCapture() {
     OpLock g(st.get());

@@ -557,6 +557,15 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
     bool BeginCapture();
     std::shared_ptr<CapturedGraph> EndCapture(const Ciphertext<DCRTPoly>& keep);
     void Launch(const std::shared_ptr<CapturedGraph>& g);
+    // Engine internal: destroy g's executable graph and hand its pool blocks
+    // back now (a graph the context itself holds, at context destruction,
+    // when its weak context reference no longer locks)
+    void ReleaseGraph(CapturedGraph& g);
+    // contexts alive in this process (diagnostics: a context kept alive by a
+    // reference cycle keeps its device memory)
+    static int LiveContexts();
+    // ... for every bootstrap replay graph (bootstrap.cpp)
+    void releaseBootstrapGraphs();
     size_t GraphNodes(const std::shared_ptr<CapturedGraph>& g) const;
     // the graph's NTT kernels replayed alone (sfp_graph_family_time)
     bool GraphNttTime(const std::shared_ptr<CapturedGraph>& g, int reps, double* ms, uint64_t* launches,

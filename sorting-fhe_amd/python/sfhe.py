@@ -34,7 +34,7 @@ ABI_SYMBOLS = [
     "sfhe_direct_sort_params", "sfhe_doubled_sinc_coeffs", "sfhe_sorter_create",
     "sfhe_sorter_destroy", "sfhe_sorter_sort", "sfhe_sorter_rank", "sfhe_sorter_place",
     "sfhe_decompose", "sfhe_kernel_timing", "sfhe_kernel_timing_read",
-    "sfhe_comm_uid", "sfhe_shard_rccl", "sfhe_shard_host", "sfhe_pool_bytes",
+    "sfhe_comm_uid", "sfhe_shard_rccl", "sfhe_shard_host", "sfhe_pool_bytes", "sfhe_live_contexts",
     "sfhe_serialize_lanes", "sfhe_sorter_graph_nodes", "sfhe_sorter_create_rot",
     "sfhe_sorter_sort_hybrid1", "sfhe_hybrid1_params", "sfhe_sorter_graph_ntt_time",
     "sfhe_sorter_sort_hybrid", "sfhe_hybrid_params", "sfhe_sorter_place_2n",
@@ -147,6 +147,7 @@ _SIGS = {
     "sfhe_decompose": (C.c_int, [_U32, _PI32, _SZ, C.c_int32, C.c_int32, C.c_int, _PI32, _PI32, _SZ, _PSZ]),
     "sfhe_comm_uid": (C.c_int, [_VP]),
     "sfhe_pool_bytes": (C.c_int, [_VP, _PU64]),
+    "sfhe_live_contexts": (C.c_int, []),
     "sfhe_shard_rccl": (C.c_int, [_VP, C.c_int, C.c_int, _VP]),
     "sfhe_shard_host": (C.c_int, [_VP, C.c_int, C.c_int, _AG, _BC, _VP]),
     "sfhe_shard_tail": (C.c_int, [_VP, _PU32]),
@@ -658,6 +659,11 @@ def decompose(N: int, keys: Sequence[int], rotation: int, wrapN: int, algo: int,
 
 
 # ---- limb-sharding transports ------------------------------------------------
+
+def live_contexts(backend: str = "hip") -> int:
+    """Engine contexts alive in this process (sfhe_live_contexts)."""
+    return load(backend).sfhe_live_contexts()
+
 
 def comm_uid(backend: str = "hip"):
     """128-byte RCCL unique id (bytes), or None where the backend has no RCCL."""

@@ -36,6 +36,20 @@ def bootstrap_error(e, S, iterations=1, levels_used=3, seed=1):
     return out, float(np.max(np.abs(got - x)))
 
 
+def test_contexts_are_released(oracle_lib):
+    """Closing an engine destroys its context after a sort and a bootstrap
+    (sfhe_live_contexts; the GPU test covers the graph-replayed bootstrap)."""
+    import gc
+    live = sfhe.live_contexts("oracle")
+    e = boot_engine("oracle", 12, 8, 30, (2, 2))
+    out, err = bootstrap_error(e, 8)
+    assert sfhe.live_contexts("oracle") == live + 1
+    del out
+    e.close()
+    gc.collect()
+    assert sfhe.live_contexts("oracle") == live
+
+
 def test_bootstrap_depth_model(oracle_lib):
     """levelBudget[0] + 1 + PS depth of the degree-89 cosine (7) + 6 double
     angles + levelBudget[1], each budget capped at log2(slots)."""
@@ -177,3 +191,12 @@ def test_bootstrap_graph_replay(hip_lib, monkeypatch, iters):
     out = e.bootstrap(e.mult_const(e.encrypt(y.tolist()), 1.0), iters)
     err = float(np.max(np.abs(np.array(e.decrypt(out))[:S] - y)))
     assert err < (2.0 ** -15 if iters == 1 else 2.0 ** -25), err
+    # the replay graph and its ciphertexts belong to the context: closing the
+    # engine destroys the context (no reference cycle keeping it, and its
+    # device memory, alive -- KWaySort2Test runs nine contexts in a process)
+    import gc
+    live = sfhe.live_contexts("hip")
+    del ct, out
+    e.close()
+    gc.collect()
+    assert sfhe.live_contexts("hip") == live - 1
