@@ -210,6 +210,10 @@ static void ntt_inv(const sfp_dev* d, u64* a, uint32_t p) {
     for (uint32_t j = 0; j < n; ++j) a[j] = shoup(a[j], d->ninv[p], d->ninvS[p], q);
 }
 
+void sfp_ntt_batch(sfp_dev* d, uint64_t* p, size_t stride, uint32_t count, sfp_limbs m, int inverse) {
+    for (uint32_t b = 0; b < count; ++b) sfp_ntt(d, p + (size_t)b * stride, m, inverse);
+}
+
 void sfp_ntt(sfp_dev* d, uint64_t* p, sfp_limbs m, int inverse) {
 #pragma omp parallel for schedule(static)
     for (uint32_t i = 0; i < m.count; ++i) {
@@ -663,6 +667,15 @@ void sfp_encode_setup(sfp_dev* d, const uint64_t* rot, const double* ksi) {
     d->enc_ksi = (double*)malloc((size_t)(2 * d->n + 1) * 16);
     memcpy(d->enc_rot, rot, (size_t)d->n / 2 * 8);
     memcpy(d->enc_ksi, ksi, (size_t)(2 * d->n + 1) * 16);
+}
+
+void sfp_encode(sfp_dev* d, uint64_t* p, const double* vals, uint32_t nvals, int real, uint32_t slots,
+                double scale, sfp_limbs m, uint64_t* scratch);
+void sfp_encode_batch(sfp_dev* d, uint64_t* dst, size_t dstStride, const double* vals, uint32_t nvals,
+                      uint32_t count, int real, uint32_t slots, double scale, sfp_limbs m, uint64_t* scratch) {
+    for (uint32_t b = 0; b < count; ++b)
+        sfp_encode(d, dst + (size_t)b * dstStride, vals + (size_t)b * nvals * (real ? 1 : 2), nvals, real, slots,
+                   scale, m, scratch);
 }
 
 void sfp_encode(sfp_dev* d, uint64_t* p, const double* vals, uint32_t nvals, int real, uint32_t slots,

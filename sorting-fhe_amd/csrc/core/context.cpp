@@ -146,7 +146,7 @@ u64 residueOf(double x, u64 q) {
 
 DeviceBuffer::~DeviceBuffer() {
     if (ready) sfp_event_free(st->dev, ready);
-    if (!ptr) return;
+    if (!ptr || parent) return;  // a view: the parent block returns to the pool with its last view
     std::lock_guard<std::mutex> g(st->poolMu);
     if (!st->graphOwned.empty()) {
         auto it = st->graphOwned.find(ptr);
@@ -1090,6 +1090,75 @@ class SfheInternal {
         }
     }
 
+    // an encoding made inside an abandoned capture never ran: it is remade
+    static bool staleEnc(SfheContextState* s, const DeviceBufferPtr& b) {
+        return b->capEpoch && s->abandonedEpochs.count(b->capEpoch);
+    }
+
+    // the context-level cache key of (values, slots, level): four independent
+    // FNV lanes over the values' words (one serial multiply chain per word
+    // was the cold sort's largest host cost after the encoding moved to the
+    // device), folded at the end
+    static uint64_t encHash(const Plaintext& pt, uint32_t level) {
+        uint64_t h = 1469598103934665603ull;
+        auto mix = [&](uint64_t x) { h = (h ^ x) * 1099511628211ull; };
+        const uint64_t* wv = reinterpret_cast<const uint64_t*>(pt->values.data());
+        const size_t nw = 2 * pt->values.size();
+        uint64_t ln[4] = {h, h ^ 1, h ^ 2, h ^ 3};
+        size_t i = 0;
+        for (; i + 4 <= nw; i += 4)
+            for (int k = 0; k < 4; ++k) ln[k] = (ln[k] ^ wv[i + k]) * 1099511628211ull;
+        for (; i < nw; ++i) ln[0] = (ln[0] ^ wv[i]) * 1099511628211ull;
+        for (int k = 0; k < 4; ++k) mix(ln[k]);
+        mix(pt->slots);
+        mix(level);
+        mix(pt->values.size());
+        return h;
+    }
+
+    // pt's existing encoding at `level` (its own, or an identical plaintext's
+    // from the context cache, then adopted), or nullptr; h: the cache key
+    // (computed when the cache is on)
+    static DeviceBuffer* findEncoding(SfheContextState* s, const Plaintext& pt, uint32_t level, uint64_t& h) {
+        auto it = pt->encoded.find(level);
+        if (it != pt->encoded.end() && staleEnc(s, it->second)) {
+            pt->encoded.erase(it);
+            it = pt->encoded.end();
+        }
+        if (it != pt->encoded.end()) return it->second.get();
+        h = 0;
+        if (!s->ptCacheOn) return nullptr;
+        h = encHash(pt, level);
+        auto ci = s->ptCache.find(h);
+        if (ci == s->ptCache.end()) return nullptr;
+        auto& v = ci->second;
+        for (auto e = v.begin(); e != v.end();)
+            if (staleEnc(s, e->buf)) {
+                s->ptCacheBytes -= e->buf->words * 8;
+                e = v.erase(e);
+            } else {
+                ++e;
+            }
+        for (auto& e : v)
+            if (e.slots == pt->slots && e.values == pt->values) {
+                pt->encoded[level] = e.buf;
+                return e.buf.get();
+            }
+        return nullptr;
+    }
+
+    // a new encoding of pt at `level` (its evaluation-domain rows in buf)
+    static void keepEncoding(SfheContextState* s, const Plaintext& pt, uint32_t level, uint64_t h,
+                             const DeviceBufferPtr& buf) {
+        buf->ready = sfp_event_record(s->dev);
+        buf->readyEpoch = s->capturing ? s->captureEpoch : 0;
+        pt->encoded[level] = buf;
+        if (s->ptCacheOn && s->ptCacheBytes + buf->words * 8 <= s->ptCacheLimit) {
+            s->ptCache[h].push_back(PtCacheEntry{pt->values, pt->slots, buf});
+            s->ptCacheBytes += buf->words * 8;
+        }
+    }
+
     static const uint64_t* encoded(CC* cc, const Plaintext& pt, uint32_t level) {
         SfheContextState* s = cc->st.get();
         std::lock_guard<std::mutex> g(pt->encMutex);
@@ -1102,49 +1171,8 @@ class SfheInternal {
             s->scopeKeep.push_back(buf);
             return buf->ptr;
         }
-        // an encoding made inside an abandoned capture never ran: make it again
-        auto stale = [&](const DeviceBufferPtr& b) { return b->capEpoch && s->abandonedEpochs.count(b->capEpoch); };
-        auto it = pt->encoded.find(level);
-        if (it != pt->encoded.end() && stale(it->second)) {
-            pt->encoded.erase(it);
-            it = pt->encoded.end();
-        }
-        if (it != pt->encoded.end()) return ready(s, it->second.get());
-        // context-level cache: identical (values, slots, level) encode identically
-        uint64_t h = 1469598103934665603ull;
-        if (s->ptCacheOn) {
-            auto mix = [&](uint64_t x) { h = (h ^ x) * 1099511628211ull; };
-            // four independent FNV lanes over the values' words (one serial
-            // multiply chain per word was the cold sort's largest host cost
-            // after the encoding moved to the device), folded at the end
-            const uint64_t* wv = reinterpret_cast<const uint64_t*>(pt->values.data());
-            const size_t nw = 2 * pt->values.size();
-            uint64_t ln[4] = {h, h ^ 1, h ^ 2, h ^ 3};
-            size_t i = 0;
-            for (; i + 4 <= nw; i += 4)
-                for (int k = 0; k < 4; ++k) ln[k] = (ln[k] ^ wv[i + k]) * 1099511628211ull;
-            for (; i < nw; ++i) ln[0] = (ln[0] ^ wv[i]) * 1099511628211ull;
-            for (int k = 0; k < 4; ++k) mix(ln[k]);
-            mix(pt->slots);
-            mix(level);
-            mix(pt->values.size());
-            auto ci = s->ptCache.find(h);
-            if (ci != s->ptCache.end()) {
-                auto& v = ci->second;
-                for (auto e = v.begin(); e != v.end();)
-                    if (stale(e->buf)) {
-                        s->ptCacheBytes -= e->buf->words * 8;
-                        e = v.erase(e);
-                    } else {
-                        ++e;
-                    }
-                for (auto& e : v)
-                    if (e.slots == pt->slots && e.values == pt->values) {
-                        pt->encoded[level] = e.buf;
-                        return ready(s, e.buf.get());
-                    }
-            }
-        }
+        uint64_t h = 0;
+        if (DeviceBuffer* b = findEncoding(s, pt, level, h)) return ready(s, b);
         std::vector<int64_t> coeffs;
         const size_t pw = s->polyWords(level);
         auto buf = s->alloc(pw);
@@ -1153,22 +1181,86 @@ class SfheInternal {
         if (trace) {
             uint64_t f = 1469598103934665603ull;
             for (int64_t v : coeffs) f = (f ^ (uint64_t)v) * 1099511628211ull;
-            std::vector<u64> h(pw);
-            sfp_d2h(s->dev, h.data(), buf->ptr, h.size() * 8);
-            uint64_t g = 1469598103934665603ull;
-            for (u64 v : h) g = (g ^ v) * 1099511628211ull;
+            std::vector<u64> hv(pw);
+            sfp_d2h(s->dev, hv.data(), buf->ptr, hv.size() * 8);
+            uint64_t gg = 1469598103934665603ull;
+            for (u64 v : hv) gg = (gg ^ v) * 1099511628211ull;
             std::fprintf(stderr, "ENCODE slots=%u level=%u coeffs=%016llx loaded=%016llx\n", pt->slots,
-                         level, (unsigned long long)f, (unsigned long long)g);
+                         level, (unsigned long long)f, (unsigned long long)gg);
         }
         sfp_ntt(s->dev, buf->ptr, s->qmap(ell), 0);
-        buf->ready = sfp_event_record(s->dev);
-        buf->readyEpoch = s->capturing ? s->captureEpoch : 0;
-        pt->encoded[level] = buf;
-        if (s->ptCacheOn && s->ptCacheBytes + pw * 8 <= s->ptCacheLimit) {
-            s->ptCache[h].push_back(PtCacheEntry{pt->values, pt->slots, buf});
-            s->ptCacheBytes += pw * 8;
-        }
+        keepEncoding(s, pt, level, h, buf);
         return buf->ptr;
+    }
+
+    // Every not-yet-encoded plaintext of `pts` at `level` (one slot count,
+    // value count and real-ness: the sort's masks of one giant step) encoded
+    // in ONE batch -- one launch per encoder stage and one NTT launch pair
+    // for all of them -- into views of one pool block.  The same values as
+    // encoded() one at a time (sfp_encode_batch is sfp_encode per batch
+    // member); the cold sort's mask encodings were ~10 launches each.
+    static void encodeBatch(CC* cc, const std::vector<Plaintext>& pts, uint32_t level) {
+        SfheContextState* s = cc->st.get();
+        if (pts.size() < 2 || s->fullScope) return;
+        static const bool trace = std::getenv("SFHE_TRACE") != nullptr;
+        const char* he = std::getenv("SFHE_HOST_ENCODE");
+        if (trace || (he && *he == '1')) return;
+        const uint32_t ell = s->ellOf(level);
+        const size_t pw = s->polyWords(level);
+        struct Miss {
+            Plaintext pt;
+            uint64_t h;
+        };
+        std::vector<Miss> miss;
+        bool real0 = true;
+        for (const auto& pt : pts) {
+            if (!pt) continue;
+            std::lock_guard<std::mutex> g(pt->encMutex);
+            uint64_t h = 0;
+            if (findEncoding(s, pt, level, h)) continue;
+            bool dup = false;  // the same plaintext twice in the list
+            for (auto& m : miss) dup = dup || m.pt == pt;
+            if (dup) continue;
+            double mx = 0.0;
+            bool real = true;
+            for (const auto& c : pt->values) {
+                mx = std::max(mx, std::max(std::fabs(c.real()), std::fabs(c.imag())));
+                real = real && c.imag() == 0.0;
+            }
+            // the device path of encodeRows, and the shape of the first miss
+            if (!(mx * s->scale[level] < 2.0e18) || (pt->slots & (pt->slots - 1)) ||
+                pt->values.size() > pt->slots)
+                continue;
+            if (!miss.empty() && (pt->slots != miss[0].pt->slots ||
+                                  pt->values.size() != miss[0].pt->values.size() || real != real0))
+                continue;
+            if (miss.empty()) real0 = real;
+            miss.push_back({pt, h});
+        }
+        if (miss.size() < 2) return;
+        const uint32_t count = (uint32_t)miss.size(), slots = miss[0].pt->slots;
+        const uint32_t nvals = (uint32_t)miss[0].pt->values.size();
+        std::vector<double> vals;
+        vals.reserve((size_t)count * nvals * (real0 ? 1 : 2));
+        for (auto& m : miss)
+            for (const auto& c : m.pt->values) {
+                vals.push_back(c.real());
+                if (!real0) vals.push_back(c.imag());
+            }
+        auto block = s->alloc((size_t)count * pw);
+        auto scr = s->alloc((size_t)count * 2 * slots);
+        sfp_encode_batch(s->dev, block->ptr, pw, vals.data(), nvals, count, real0 ? 1 : 0, slots, s->scale[level],
+                         s->qmap(ell), scr->ptr);
+        sfp_ntt_batch(s->dev, block->ptr, pw, count, s->qmap(ell), 0);
+        s->stats.dev_encodes += count;
+        for (uint32_t b = 0; b < count; ++b) {
+            auto view = std::make_shared<DeviceBuffer>(s, block->ptr + (size_t)b * pw, pw, block->lane, block->region);
+            view->parent = block;
+            view->seq = block->seq;
+            view->capEpoch = block->capEpoch;
+            std::lock_guard<std::mutex> g(miss[b].pt->encMutex);
+            keepEncoding(s, miss[b].pt, level, miss[b].h, view);
+        }
     }
 
     // pt at `level` over the extended basis: its ell q rows then the K P rows
@@ -1324,6 +1416,7 @@ struct DeferredMacPlain : DeferredOp {
         SfheContextState* s = cc->state();
         for (auto& b : pins) s->dep(b.get());
         std::vector<const uint64_t*> m;
+        SfheInternal::encodeBatch(cc, pts, level);
         for (auto& p : pts) m.push_back(SfheInternal::encoded(cc, p, level));
         const uint32_t ell = s->ellOf(level);
         const size_t pw = s->polyWords(level);
@@ -2303,6 +2396,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMultAddPlain(
         s->countBytes((3.0 * a.size() + 2.0) * ell * s->n * 8);
         return SfheInternal::deferredCt(this, level + 1, slots, op);
     }
+    SfheInternal::encodeBatch(this, p, level);
     for (size_t i = 0; i < a.size(); ++i) m.push_back(SfheInternal::encoded(this, p[i], level));
     const size_t pw = s->polyWords(level);
     auto tmp = s->alloc(2 * pw);

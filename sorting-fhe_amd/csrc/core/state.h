@@ -28,6 +28,7 @@ class DeviceBuffer {
     sfp_event* ready = nullptr;    // shared encodings: end of the producing work
     uint64_t readyEpoch = 0;       // capture epoch `ready` was recorded in (0: none)
     uint64_t capEpoch = 0;         // capture epoch it was allocated in (0: none)
+    std::shared_ptr<DeviceBuffer> parent;  // a view into parent's block (batched encodings)
 };
 
 struct BootstrapPrecomp;  // bootstrap.cpp

@@ -2894,6 +2894,13 @@ void sfp_ntt(sfp_dev* d, uint64_t* p, sfp_limbs m, int inverse) {
     nttRows(d, G, inverse);
 }
 
+void sfp_ntt_batch(sfp_dev* d, uint64_t* p, size_t stride, uint32_t count, sfp_limbs m, int inverse) {
+    if (!count) return;
+    RowGroup G = rowsOf(count, m.count, m);
+    G.src = G.dst = RowPtr{p, (long long)stride, (long long)d->n};
+    nttRows(d, G, inverse);
+}
+
 // Developer hook (SFHE_NTT_TRACE builds): per-kernel phase clocks since the
 // last call, [variant INV*2+COL][phase 0..5, 7 = blocks]; -1 otherwise.
 extern "C" int sfp_ntt_trace(sfp_dev* d, unsigned long long* out32) {
@@ -3947,6 +3954,9 @@ __device__ __forceinline__ void encButterfly(double2& a, double2& b, uint32_t j,
 // v = the values zero-padded to S (real: imaginary parts 0)
 __global__ __launch_bounds__(kThreads) void k_enc_load(double2* __restrict__ v, const double* __restrict__ vals,
                                                        uint32_t nvals, int real, uint32_t S) {
+    // batch b = blockIdx.y: its own S values and nvals inputs
+    v += (size_t)blockIdx.y * S;
+    if (vals) vals += (size_t)blockIdx.y * nvals * (real ? 1 : 2);
     for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < S; i += gridDim.x * kThreads) {
         double2 x = make_double2(0.0, 0.0);
         if (i < nvals) x = real ? make_double2(vals[i], 0.0) : make_double2(vals[2 * i], vals[2 * i + 1]);
@@ -3958,6 +3968,7 @@ __global__ __launch_bounds__(kThreads) void k_enc_load(double2* __restrict__ v, 
 __global__ __launch_bounds__(kThreads) void k_enc_stage(double2* __restrict__ v, uint32_t S, uint32_t len,
                                                         const u64* __restrict__ rot,
                                                         const double2* __restrict__ ksi, u64 M) {
+    v += (size_t)blockIdx.y * S;
     const uint32_t lenh = len >> 1;
     for (uint32_t t = blockIdx.x * kThreads + threadIdx.x; t < S / 2; t += gridDim.x * kThreads) {
         const uint32_t j = t % lenh, i = (t / lenh) * len;
@@ -3973,7 +3984,7 @@ __global__ __launch_bounds__(kThreads) void k_enc_tile(double2* __restrict__ v, 
                                                        const u64* __restrict__ rot, const double2* __restrict__ ksi,
                                                        u64 M) {
     __shared__ double2 sh[kEncTile];
-    double2* g = v + (size_t)blockIdx.x * T;
+    double2* g = v + (size_t)blockIdx.y * gridDim.x * T + (size_t)blockIdx.x * T;
     for (uint32_t i = threadIdx.x; i < T; i += kThreads) sh[i] = g[i];
     __syncthreads();
     for (uint32_t len = T; len >= 2; len >>= 1) {
@@ -3994,9 +4005,12 @@ __global__ __launch_bounds__(kThreads) void k_enc_tile(double2* __restrict__ v, 
 // divided by S, times the scale, rounded; its residue in every row of m
 __global__ __launch_bounds__(kThreads) void k_enc_round(u64* __restrict__ p, const double2* __restrict__ v,
                                                         uint32_t logS, double scale, sfp_limbs m,
-                                                        const sf_barrett* __restrict__ bar, uint32_t logn) {
+                                                        const sf_barrett* __restrict__ bar, uint32_t logn,
+                                                        size_t pStride) {
 #pragma clang fp contract(off)
     const uint32_t n = 1u << logn, half = n >> 1, gap = half >> logS;
+    p += (size_t)blockIdx.y * pStride;
+    v += (size_t)blockIdx.y << logS;
     for (uint32_t x = blockIdx.x * kThreads + threadIdx.x; x < n; x += gridDim.x * kThreads) {
         const uint32_t xi = x < half ? x : x - half;
         int64_t c = 0;
@@ -4026,28 +4040,36 @@ void sfp_encode_setup(sfp_dev* d, const uint64_t* rot, const double* ksi) {
     hostToDev(d, d->encKsi, ksi, (size_t)(2 * d->n + 1) * sizeof(double2));
 }
 
-void sfp_encode(sfp_dev* d, uint64_t* dst, const double* vals, uint32_t nvals, int real, uint32_t slots,
-                double scale, sfp_limbs m, uint64_t* scratch) {
+void sfp_encode_batch(sfp_dev* d, uint64_t* dst, size_t dstStride, const double* vals, uint32_t nvals,
+                      uint32_t count, int real, uint32_t slots, double scale, sfp_limbs m, uint64_t* scratch) {
+    if (!count) return;
     if (!limbsOk(d, m, "encode")) return;
-    if (!d->encRot || !slots || (slots & (slots - 1)) || slots > d->n / 2 || nvals > slots) {
-        record(d, "encode (tables not set up, or a bad slot count)", hipErrorInvalidValue);
+    if (!d->encRot || !slots || (slots & (slots - 1)) || slots > d->n / 2 || nvals > slots || count > 65535u) {
+        record(d, "encode (tables not set up, or a bad slot / batch count)", hipErrorInvalidValue);
         return;
     }
     const u64 M = 2ull * d->n;
     double2* v = reinterpret_cast<double2*>(scratch);
-    const double* dv = nvals ? (const double*)ringPut(d, vals, (size_t)nvals * (real ? 8 : 16)) : nullptr;
-    hipLaunchKernelGGL(k_enc_load, dim3(gridFor(slots, kThreads)), dim3(kThreads), 0, d->st(), v, dv, nvals, real,
-                       slots);
+    const double* dv =
+        nvals ? (const double*)ringPut(d, vals, (size_t)count * nvals * (real ? 8 : 16)) : nullptr;
+    hipLaunchKernelGGL(k_enc_load, dim3(gridFor(slots, kThreads), count), dim3(kThreads), 0, d->st(), v, dv, nvals,
+                       real, slots);
     const uint32_t T = std::min(slots, kEncTile);
     for (uint32_t len = slots; len > T; len >>= 1)
-        hipLaunchKernelGGL(k_enc_stage, dim3(gridFor(slots / 2, kThreads)), dim3(kThreads), 0, d->st(), v, slots, len,
-                           d->encRot, d->encKsi, M);
+        hipLaunchKernelGGL(k_enc_stage, dim3(gridFor(slots / 2, kThreads), count), dim3(kThreads), 0, d->st(), v,
+                           slots, len, d->encRot, d->encKsi, M);
     if (T >= 2)
-        hipLaunchKernelGGL(k_enc_tile, dim3(slots / T), dim3(kThreads), 0, d->st(), v, T, d->encRot, d->encKsi, M);
+        hipLaunchKernelGGL(k_enc_tile, dim3(slots / T, count), dim3(kThreads), 0, d->st(), v, T, d->encRot,
+                           d->encKsi, M);
     const uint32_t logS = (uint32_t)__builtin_ctz(slots);
-    hipLaunchKernelGGL(k_enc_round, dim3(ewGrid(d->n)), dim3(kThreads), 0, d->st(), dst, v, logS, scale, m, d->bar,
-                       d->logn);
+    hipLaunchKernelGGL(k_enc_round, dim3(ewGrid(d->n), count), dim3(kThreads), 0, d->st(), dst, v, logS, scale, m,
+                       d->bar, d->logn, dstStride);
     checkLaunch(d, "encode");
+}
+
+void sfp_encode(sfp_dev* d, uint64_t* dst, const double* vals, uint32_t nvals, int real, uint32_t slots,
+                double scale, sfp_limbs m, uint64_t* scratch) {
+    sfp_encode_batch(d, dst, 0, vals, nvals, 1, real, slots, scale, m, scratch);
 }
 
 // ---- limb sharding ----

@@ -287,6 +287,13 @@ void sfp_encode_setup(sfp_dev* d, const uint64_t* rot, const double* ksi);
 // scratch: 2 * slots words.
 void sfp_encode(sfp_dev* d, uint64_t* p, const double* vals, uint32_t nvals, int real, uint32_t slots,
                 double scale, sfp_limbs m, uint64_t* scratch);
+// `count` encodings at once (one slot count, value count and real-ness):
+// rows dst + b * dstStride <- the encoding of vals + b * nvals (* 2 when
+// complex), each as sfp_encode; scratch: count * 2 * slots words
+void sfp_encode_batch(sfp_dev* d, uint64_t* dst, size_t dstStride, const double* vals, uint32_t nvals,
+                      uint32_t count, int real, uint32_t slots, double scale, sfp_limbs m, uint64_t* scratch);
+// sfp_ntt of `count` row sets p + b * stride (each the rows of map m), one launch per pass
+void sfp_ntt_batch(sfp_dev* d, uint64_t* p, size_t stride, uint32_t count, sfp_limbs m, int inverse);
 
 // ---- lanes: independent in-order queues (HIP streams) ----------------------------
 // Every prim launches on the current lane.  Work on different lanes may run

@@ -79,3 +79,36 @@ def test_device_encoding_bitexact_hip(hip_lib, monkeypatch, logn):
     """The HIP kernels, up to the metric ring (2^16: 32768-slot masks, four
     global stages then 2048-value LDS tiles) and 2^17."""
     check("hip", logn, monkeypatch, 1 << (logn - 1))
+
+
+def sort_encodings(backend, monkeypatch, logn, N):
+    """A DirectSort<N>'s downloaded result with every mask encoded on the
+    host, and with the masks of each giant step encoded as one device batch
+    (sfp_encode_batch / sfp_ntt_batch, core/context.cpp encodeBatch)."""
+    from oracle import slotsim
+    depth, rots = sfhe.direct_sort_params(N, backend)
+    kw = dict(mult_depth=depth, ring_dim=1 << logn, batch_size=N, rotations=rots, seed=99)
+    out = {}
+    for host in (True, False):
+        monkeypatch.setenv("SFHE_HOST_ENCODE", "1" if host else "0")
+        e = sfhe.Engine(backend, **kw)
+        e.set_quiet(True)
+        e.set_plaintext_cache(False)
+        e.op_stats(reset=True)
+        r = e.sorter(N).sort(e.encrypt(slotsim.input_vector(N).tolist()), *slotsim.default_sign_config(N))
+        out[host] = (r.download(), e.encode_counts())
+        e.close()
+    (h, (hd, hh)), (d, (dd, dh)) = out[True], out[False]
+    assert hd == 0 and dh == 0 and dd == hh > 0, (hd, hh, dd, dh)
+    assert np.array_equal(h, d)
+
+
+def test_batched_mask_encodings_bitexact_oracle(oracle_lib, monkeypatch):
+    sort_encodings("oracle", monkeypatch, 12, 8)
+
+
+@pytest.mark.gpu
+def test_batched_mask_encodings_bitexact_hip(hip_lib, monkeypatch):
+    """The metric sort's masks (16 per giant step, 32768 slots): batched on
+    the device, bit-identical to the host encoder."""
+    sort_encodings("hip", monkeypatch, 16, 256)
