@@ -10,6 +10,7 @@
 #include <tuple>
 #include <memory>
 #include <mutex>
+#include <thread>
 
 #include "comparison.h"
 
@@ -68,9 +69,10 @@ const std::vector<double>& cached(int N, bool doubled) {
 std::vector<double> rebase(const std::vector<double>& c, double lo, double hi) {
     const size_t D = c.size() - 1;
     // p at the D+1 Chebyshev nodes of y (Clenshaw in long double), then the
-    // discrete Chebyshev transform: exact for a degree-D polynomial
+    // discrete Chebyshev transform: exact for a degree-D polynomial.  O(D^2)
+    // in long double: over the host's cores (the cold sort paid it serially)
     std::vector<long double> pv(D + 1);
-    for (size_t j = 0; j <= D; ++j) {
+    lbcrypto::ParallelFor(D + 1, [&](size_t j) {
         const long double y = std::cos((long double)M_PI * ((long double)j + 0.5L) / (long double)(D + 1));
         const long double z = (long double)lo + (y + 1.0L) * ((long double)hi - (long double)lo) / 2.0L;
         long double b1 = 0, b2 = 0;
@@ -80,14 +82,13 @@ std::vector<double> rebase(const std::vector<double>& c, double lo, double hi) {
             b1 = b0;
         }
         pv[j] = z * b1 - b2 + 0.5L * (long double)c[0];
-    }
+    });
     // cos(pi k (2j+1) / (2(D+1))) depends on k(2j+1) mod 4(D+1)
     const size_t P = 4 * (D + 1);
     std::vector<long double> ctab(P);
     for (size_t m = 0; m < P; ++m) ctab[m] = std::cos((long double)M_PI * (long double)m / (2.0L * (D + 1)));
     std::vector<double> d(D + 1);
-    double mx = 0;
-    for (size_t k = 0; k <= D; ++k) {
+    lbcrypto::ParallelFor(D + 1, [&](size_t k) {
         long double acc = 0;
         size_t idx = k % P;
         const size_t step = (2 * k) % P;
@@ -97,8 +98,9 @@ std::vector<double> rebase(const std::vector<double>& c, double lo, double hi) {
             if (idx >= P) idx -= P;
         }
         d[k] = (double)(acc * 2.0L / (long double)(D + 1));
-        mx = std::max(mx, std::fabs(d[k]));
-    }
+    });
+    double mx = 0;
+    for (double v : d) mx = std::max(mx, std::fabs(v));
     for (double& v : d)
         if (std::fabs(v) < 1e-12 * mx) v = 0.0;
     while (d.size() > 1 && d.back() == 0.0) d.pop_back();

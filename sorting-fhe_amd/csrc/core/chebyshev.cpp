@@ -43,13 +43,14 @@ std::vector<double> EvalChebyshevCoefficients(std::function<double(double)> func
     const double piByDeg = M_PI / (double)degree;
     std::vector<double> fx(degree);
     for (uint32_t j = 0; j < degree; ++j) fx[j] = func(std::cos(piByDeg * (j + 0.5)) * bMinusA + bPlusA);
+    // O(degree^2) (the sinc tables interpolate at degree 13011): over the cores
     // cos(pi * i * (2j+1) / (2 d)) depends only on i*(2j+1) mod 4d
     const uint64_t P = 4ull * degree;
     std::vector<double> ctab(P);
     for (uint64_t m = 0; m < P; ++m) ctab[m] = std::cos(M_PI * (double)m / (2.0 * degree));
     std::vector<double> c(degree, 0.0);
     const double mult = 2.0 / (double)degree;
-    for (uint32_t i = 0; i < degree; ++i) {
+    ParallelFor(degree, [&](size_t i) {
         double acc = 0.0;
         uint64_t step = (2ull * i) % P, idx = i % P;
         for (uint32_t j = 0; j < degree; ++j) {
@@ -58,7 +59,7 @@ std::vector<double> EvalChebyshevCoefficients(std::function<double(double)> func
             if (idx >= P) idx -= P;
         }
         c[i] = acc * mult;
-    }
+    });
     return c;
 }
 

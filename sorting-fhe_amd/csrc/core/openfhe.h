@@ -20,6 +20,7 @@
 //    exactly (DirectSortTest asserts final level == multDepth).
 #pragma once
 
+#include <algorithm>
 #include <complex>
 #include <fstream>
 #include <cstdint>
@@ -31,6 +32,7 @@
 #include <set>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "prims.h"
@@ -630,6 +632,24 @@ class CryptoContextFactory {
 
 // OpenFHE math/chebyshev.h: Chebyshev interpolation coefficients (c0/2
 // convention) of f on [a,b] at `degree` Chebyshev nodes.
+// body(i) for i < count over the host's cores (engine utility for the
+// O(degree^2) coefficient transforms: each index is computed alone, so the
+// results do not depend on the thread count)
+template <class F>
+void ParallelFor(size_t count, F&& body) {
+    const size_t T = std::max<size_t>(1, std::min<size_t>(std::thread::hardware_concurrency(), 16));
+    if (T == 1 || count < 64) {
+        for (size_t i = 0; i < count; ++i) body(i);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (size_t t = 0; t < T; ++t)
+        th.emplace_back([&, t] {
+            for (size_t i = t; i < count; i += T) body(i);
+        });
+    for (auto& x : th) x.join();
+}
+
 std::vector<double> EvalChebyshevCoefficients(std::function<double(double)> func, double a,
                                               double b, uint32_t degree);
 
