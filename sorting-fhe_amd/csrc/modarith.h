@@ -59,7 +59,10 @@ typedef struct {
 
 // Reduce a 128-bit value z to [0, q).  Precondition: z < 2^(b+63) so that
 // z >> (b-1) fits a word; the estimate never overshoots, and the final loop
-// runs at most 2 + z / 2^(2b) times (one or two for a single product).
+// runs at most 2 + z / 2^(2b) times (one or two for a single product, ~18
+// for the widest lazy sum of products).  The loop is capped: operands that
+// break the precondition (non-canonical residues) give a wrong result in
+// bounded time instead of ~2^24 iterations per word on the GPU.
 SF_HD u64 sf_reduce128(u64 zlo, u64 zhi, const sf_barrett* m) {
     const uint32_t b = m->b;
     // x = z >> (b-1)
@@ -69,7 +72,7 @@ SF_HD u64 sf_reduce128(u64 zlo, u64 zhi, const sf_barrett* m) {
     u64 phi = sf_mulhi(x, m->mu);
     u64 qhat = (phi << (63 - b)) | (plo >> (b + 1));
     u64 r = zlo - qhat * m->q;
-    while (r >= m->q) r -= m->q;
+    for (int it = 0; r >= m->q && it < 64; ++it) r -= m->q;
     return r;
 }
 

@@ -156,8 +156,11 @@ int main(int argc, char** argv) {
                         nullptr, nullptr, 0, 0, ~0u, ext, scr);
     });
     const size_t pw = (size_t)ell * n;
+    // four canonical operand polynomials (residues of each row's own prime)
+    auto* ops = (uint64_t*)sfp_alloc(d, 4 * pw * 8);
+    for (int k = 0; k < 4; ++k) sfp_sample_uniform(d, ops + k * pw, sfp_limbs{ell, ell, 0, 0}, 21 + k);
     const double mr = timeIt(d, 30, [&] {
-        sfp_mult_relin_rescale(d, out, out + pw, buf, buf + pw, buf + 2 * pw, buf + 3 * pw, ell, K, s->Lq,
+        sfp_mult_relin_rescale(d, out, out + pw, ops, ops + pw, ops + 2 * pw, ops + 3 * pw, ell, K, s->Lq,
                                s->alpha, convs.data(), s->relinKey->ptr, s->moddownConv, s->pInvModQ.data(),
                                s->pModQ.data(), s->qInvTable[ell].data(), acc, ext, scr);
     });
