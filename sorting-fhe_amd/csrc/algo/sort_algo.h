@@ -414,7 +414,7 @@ class DirectSort : public SortBase<N> {
         std::vector<Ciphertext<DCRTPoly>> parts(L.B);
         const sfhe::BatchSplit split(m_cc, L.B);
         const int lanes = std::min((int)split.mine.size(), m_cc->LaneCount());
-        m_cc->ForkLanes(lanes);
+        if (lanes > 1) m_cc->ForkLanes(lanes);  // (one batch: no region, the PS may open its own)
         sfhe::parallelLanes(m_cc, lanes, (int)split.mine.size(), [&](int i) {
             const int b = split.mine[i];
             auto shifted = vecRotsOpt(pre, L.P, L.S, L.npRank, b);
@@ -492,7 +492,7 @@ class DirectSort : public SortBase<N> {
         std::vector<Ciphertext<DCRTPoly>> parts(L.B);
         const sfhe::BatchSplit split(m_cc, L.B);
         const int lanes = std::min((int)split.mine.size(), m_cc->LaneCount());
-        m_cc->ForkLanes(lanes);
+        if (lanes > 1) m_cc->ForkLanes(lanes);  // (one batch: no region, the PS may open its own)
         sfhe::parallelLanes(m_cc, lanes, (int)split.mine.size(), [&](int i) {
             const int b = split.mine[i];
             Plaintext chk = maskMemo({3, b, 0, (int)indexMinusRank->GetLevel(), L.S}, [&](auto& v) {

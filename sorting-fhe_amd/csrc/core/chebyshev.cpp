@@ -147,18 +147,25 @@ class PSEvaluator {
     // Lp = max(its natural product level, want): q wanted at Lp - 1, T_M
     // aligned to Lp - 1, r wanted at Lp -- no per-node rescale of a node's
     // operands or result.  want = 0: the natural level.
-    Val eval(std::vector<double> p, uint32_t depth, uint32_t want = 0) {
+    //
+    // Lanes (SFHE_PS_LANES, a sort phase that runs one batch per GPU): a
+    // node's q and r subtrees are independent, so q goes to lane + span/2 and
+    // r stays on `lane` until the span is used up; the engine orders every
+    // cross-lane read after its writer.  Same operations, same values.
+    Val eval(std::vector<double> p, uint32_t depth, uint32_t want = 0, int lane = 0, int span = 1) {
         trim(p);
         if (p.empty()) return Val{true, 0.0, nullptr};
         const uint32_t deg = (uint32_t)p.size() - 1;
         if (deg == 0) return Val{true, p[0], nullptr};
         if (deg <= k) return leaf(p, want);
-        if (depth >= 1 && deg + (1u << l) <= (1u << (depth - 1))) return eval(p, depth - 1, want);
+        if (depth >= 1 && deg + (1u << l) <= (1u << (depth - 1))) return eval(p, depth - 1, want, lane, span);
         const uint32_t M = deg >= (1u << (depth - 1)) ? (1u << (depth - 1)) : (1u << (depth - 2));
         std::vector<double> q, r;
         divide(p, M, q, r);
         const uint32_t Lp = productLevel(q, depth, M, want);
-        Val qv = eval(q, depth - 1, Lp - 1);
+        const int half = span / 2;
+        if (half) cc->SetLane(lane + half);
+        Val qv = eval(q, depth - 1, Lp - 1, half ? lane + half : lane, half ? half : 1);
         const Ct& TM = alignedPower(M, Lp - 1);
         Val out;
         out.isConst = false;
@@ -166,7 +173,8 @@ class PSEvaluator {
             out.ct = cc->EvalMult(TM, qv.c);
         else
             out.ct = cc->EvalMult(qv.ct, TM);
-        Val rv = eval(r, depth, Lp);
+        if (half) cc->SetLane(lane);
+        Val rv = eval(r, depth, Lp, lane, half ? half : 1);
         if (std::getenv("SFHE_PS_DEBUG"))
             std::fprintf(stderr, "PSNODE deg %u M %u | q %s lvl %d | TM lvl %u | prod lvl %u | r %s lvl %d\n", deg, M,
                          qv.isConst ? "const" : "ct", qv.isConst ? -1 : (int)qv.ct->GetLevel(), TM->GetLevel(),
@@ -403,10 +411,27 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalChebyshevSeriesPS(
     const uint32_t l = std::min(bestL, (uint32_t)(31 - __builtin_clz(std::max<uint32_t>(d, 2))));
     Ciphertext<DCRTPoly> out;
     {
+        // SFHE_PS_LANES=k: the recursion's independent subtrees on k lanes,
+        // when no lane region is open (a sort phase with one batch per GPU:
+        // config 3, or a batch-split rank) and the context is not limb-sharded
+        static const int psLanes = [] {
+            const char* v = std::getenv("SFHE_PS_LANES");
+            return v ? std::atoi(v) : 0;
+        }();
+        int lanes = 1;
+        if (psLanes > 1 && !st->forkedLanes && d >= 64) {
+            lanes = std::min(psLanes, LaneCount());
+            lanes = lanes >= 4 ? 4 : (lanes >= 2 ? 2 : 1);
+        }
+        if (lanes > 1) ForkLanes(lanes);
         PSEvaluator ps(this, y, l, D);
         static const bool batched = std::getenv("SFHE_PS_UNBATCHED") == nullptr;
         if (batched) ps.precomputeLeaves(p, D);
-        auto v = ps.eval(p, D);
+        auto v = ps.eval(p, D, 0, 0, lanes);
+        if (lanes > 1) {
+            SetLane(0);
+            JoinLanes();
+        }
         out = v.isConst ? EvalAdd(EvalMult(y, 0.0), v.c) : v.ct;
     }
     const uint32_t target = y->GetLevel() + D;
