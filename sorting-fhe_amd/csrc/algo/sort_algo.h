@@ -361,6 +361,30 @@ class DirectSort : public SortBase<N> {
         if (v.empty()) build(v);
         return v;
     }
+    // The memo entries of `keys`, `count` masks each, mask i of entry k made
+    // by make(k, i); the missing ones built over the host's cores (the cold
+    // sort's mask generation: 128 vectors of 32768 slots per giant-step
+    // phase at the metric config).  Entries are filled in place, so the map
+    // is not modified while the threads run.
+    template <class F>
+    std::vector<const std::vector<Plaintext>*> maskMemoMany(const std::vector<std::array<int, 5>>& keys, int count,
+                                                            F&& make) {
+        std::lock_guard<std::mutex> g(m_masksMu);
+        std::vector<std::vector<Plaintext>*> vs;
+        std::vector<std::pair<size_t, int>> todo;
+        for (size_t k = 0; k < keys.size(); ++k) {
+            auto& v = m_masks[keys[k]];
+            if (v.empty()) {
+                v.resize(count);
+                for (int i = 0; i < count; ++i) todo.emplace_back(k, i);
+            }
+            vs.push_back(&v);
+        }
+        lbcrypto::ParallelFor(
+            todo.size(), [&](size_t t) { (*vs[todo[t].first])[todo[t].second] = make(todo[t].first, todo[t].second); },
+            2);
+        return {vs.begin(), vs.end()};
+    }
 
     // The giant steps' rotations is*P + j*np are applied as one rotation by
     // is*P of the sum over j of rotations by j*np (rotations are linear), and
@@ -368,21 +392,20 @@ class DirectSort : public SortBase<N> {
     // P/np key switches with one ModDown instead of up to 2 P/np of each.
     Ciphertext<DCRTPoly> vecRotsOpt(const std::vector<Ciphertext<DCRTPoly>>& pre,
                                     int num_partition, int num_slots, int np, int is) {
-        std::vector<std::vector<Plaintext>> masks;
+        std::vector<std::array<int, 5>> keys;
         std::vector<int> steps;
         for (int j = 0; j < num_partition / np; ++j) {
-            const int shift = is * num_partition + j * np;
-            masks.push_back(maskMemo({0, is, j, (int)pre[0]->GetLevel(), num_slots}, [&](auto& v) {
-                for (int i = 0; i < np; ++i)
-                    v.push_back(m_cc->MakeCKKSPackedPlaintext(
-                        vectorRotate(generateMaskVector(num_slots, np * j + i), -shift), 1,
-                        pre[i]->GetLevel(), nullptr, num_slots));
-            }));
+            keys.push_back({0, is, j, (int)pre[0]->GetLevel(), num_slots});
             steps.push_back(j * np);
         }
+        const auto masks = maskMemoMany(keys, np, [&](size_t j, int i) {
+            const int shift = is * num_partition + (int)j * np;
+            return m_cc->MakeCKKSPackedPlaintext(vectorRotate(generateMaskVector(num_slots, np * (int)j + i), -shift),
+                                                 1, pre[i]->GetLevel(), nullptr, num_slots);
+        });
         std::vector<Ciphertext<DCRTPoly>> giants;
-        for (const auto& m : masks) {  // T_j = sum_i pre_i * mask_{np j + i}
-            giants.push_back(m_cc->EvalMultAddPlain(pre, m));
+        for (const auto* m : masks) {  // T_j = sum_i pre_i * mask_{np j + i}
+            giants.push_back(m_cc->EvalMultAddPlain(pre, *m));
             giants.back()->SetSlots(num_slots);
         }
         return rot.rotate(rot.rotateSum(giants, steps), is * num_partition);
@@ -449,19 +472,18 @@ class DirectSort : public SortBase<N> {
     // rotateSum over i*np).
     Ciphertext<DCRTPoly> blindRotationOptN(const std::vector<Ciphertext<DCRTPoly>>& masked_inputs,
                                            int num_slots, int np, int ib, int num_partition) {
-        std::vector<std::vector<Plaintext>> masks;
+        std::vector<std::array<int, 5>> keys;
         std::vector<int> steps;
         for (int i = 0; i < (num_slots / N) / np; ++i) {
-            masks.push_back(maskMemo({1, 0, i, (int)masked_inputs[0]->GetLevel(), num_slots}, [&](auto& v) {
-                for (int j = 0; j < np; ++j)
-                    v.push_back(m_cc->MakeCKKSPackedPlaintext(
-                        vectorRotate(generateMaskVectorN(num_slots, np * i + j), j), 1,
-                        masked_inputs[j]->GetLevel(), nullptr, num_slots));
-            }));
+            keys.push_back({1, 0, i, (int)masked_inputs[0]->GetLevel(), num_slots});
             steps.push_back(i * np);
         }
+        const auto masks = maskMemoMany(keys, np, [&](size_t i, int j) {
+            return m_cc->MakeCKKSPackedPlaintext(vectorRotate(generateMaskVectorN(num_slots, np * (int)i + j), j), 1,
+                                                 masked_inputs[j]->GetLevel(), nullptr, num_slots);
+        });
         std::vector<Ciphertext<DCRTPoly>> giants;
-        for (const auto& m : masks) giants.push_back(m_cc->EvalMultAddPlain(masked_inputs, m));
+        for (const auto* m : masks) giants.push_back(m_cc->EvalMultAddPlain(masked_inputs, *m));
         auto result = this->getZero()->Clone();
         m_cc->EvalAddInPlace(result, rot.rotate(rot.rotateSum(giants, steps), ib * num_partition));
         return result;

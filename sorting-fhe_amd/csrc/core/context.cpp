@@ -1119,7 +1119,8 @@ class SfheInternal {
     // pt's existing encoding at `level` (its own, or an identical plaintext's
     // from the context cache, then adopted), or nullptr; h: the cache key
     // (computed when the cache is on)
-    static DeviceBuffer* findEncoding(SfheContextState* s, const Plaintext& pt, uint32_t level, uint64_t& h) {
+    static DeviceBuffer* findEncoding(SfheContextState* s, const Plaintext& pt, uint32_t level, uint64_t& h,
+                                      const uint64_t* hashed = nullptr) {
         auto it = pt->encoded.find(level);
         if (it != pt->encoded.end() && staleEnc(s, it->second)) {
             pt->encoded.erase(it);
@@ -1128,7 +1129,7 @@ class SfheInternal {
         if (it != pt->encoded.end()) return it->second.get();
         h = 0;
         if (!s->ptCacheOn) return nullptr;
-        h = encHash(pt, level);
+        h = hashed ? *hashed : encHash(pt, level);
         auto ci = s->ptCache.find(h);
         if (ci == s->ptCache.end()) return nullptr;
         auto& v = ci->second;
@@ -1213,20 +1214,41 @@ class SfheInternal {
         };
         std::vector<Miss> miss;
         bool real0 = true;
-        for (const auto& pt : pts) {
-            if (!pt) continue;
-            std::lock_guard<std::mutex> g(pt->encMutex);
-            uint64_t h = 0;
-            if (findEncoding(s, pt, level, h)) continue;
-            bool dup = false;  // the same plaintext twice in the list
-            for (auto& m : miss) dup = dup || m.pt == pt;
-            if (dup) continue;
+        // the cache keys and value ranges of every plaintext over the host's
+        // cores (each a pass over 2 * slots words)
+        std::vector<uint64_t> hs(pts.size(), 0);
+        std::vector<double> mxs(pts.size(), 0.0);
+        std::vector<char> reals(pts.size(), 1), scanned(pts.size(), 0);
+        auto scan = [&](size_t i) {
+            if (s->ptCacheOn) hs[i] = encHash(pts[i], level);
             double mx = 0.0;
             bool real = true;
-            for (const auto& c : pt->values) {
+            for (const auto& c : pts[i]->values) {
                 mx = std::max(mx, std::max(std::fabs(c.real()), std::fabs(c.imag())));
                 real = real && c.imag() == 0.0;
             }
+            mxs[i] = mx;
+            reals[i] = real;
+            scanned[i] = 1;
+        };
+        ParallelFor(
+            pts.size(),
+            [&](size_t i) {
+                if (pts[i] && !pts[i]->encoded.count(level)) scan(i);  // (encoded ones: no pass at all)
+            },
+            2);
+        for (size_t pi = 0; pi < pts.size(); ++pi) {
+            const auto& pt = pts[pi];
+            if (!pt) continue;
+            std::lock_guard<std::mutex> g(pt->encMutex);
+            uint64_t h = 0;
+            if (findEncoding(s, pt, level, h, scanned[pi] && s->ptCacheOn ? &hs[pi] : nullptr)) continue;
+            if (!scanned[pi]) scan(pi);  // its own encoding was stale (an abandoned capture's)
+            bool dup = false;  // the same plaintext twice in the list
+            for (auto& m : miss) dup = dup || m.pt == pt;
+            if (dup) continue;
+            const double mx = mxs[pi];
+            const bool real = reals[pi] != 0;
             // the device path of encodeRows, and the shape of the first miss
             if (!(mx * s->scale[level] < 2.0e18) || (pt->slots & (pt->slots - 1)) ||
                 pt->values.size() > pt->slots)

@@ -636,9 +636,9 @@ class CryptoContextFactory {
 // O(degree^2) coefficient transforms: each index is computed alone, so the
 // results do not depend on the thread count)
 template <class F>
-void ParallelFor(size_t count, F&& body) {
-    const size_t T = std::max<size_t>(1, std::min<size_t>(std::thread::hardware_concurrency(), 16));
-    if (T == 1 || count < 64) {
+void ParallelFor(size_t count, F&& body, size_t minCount = 64) {
+    const size_t T = std::max<size_t>(1, std::min<size_t>(std::min<size_t>(std::thread::hardware_concurrency(), 16), count));
+    if (T == 1 || count < minCount) {
         for (size_t i = 0; i < count; ++i) body(i);
         return;
     }
