@@ -381,8 +381,8 @@ def main(argv=None):
     ap.add_argument("--shard", choices=("rccl", "host"), default=None,
                     help="transport of the multi-GPU headline sort at N > 1 (default rccl)")
     ap.add_argument("--split", type=int, default=None,
-                    help="batch groups of the multi-GPU sort (default 2 when N is even, else 1; "
-                         "1 = limb sharding over all ranks)")
+                    help="batch groups of the multi-GPU sort (default 2 when N is even and the sort has an "
+                         "even batch count, else 1; 1 = limb sharding over all ranks)")
     ap.add_argument("--replicas", action="store_true",
                     help="at N > 1, make the independent replica sorts the headline (weak scaling)")
     args = ap.parse_args(argv)
@@ -403,7 +403,9 @@ def main(argv=None):
                                                    secure=secure, rotations=rots, seed=20251205 + N + 7919 * rank,
                                                    device=device),
                                spec, world, args.steps, args.warmup)
-    groups = args.split if args.split else (2 if world % 2 == 0 else 1)
+    # DirectSort's batches per phase (RankLayout: P = min(N, n/2/N) partitions, B = N/P)
+    batches = N // min(N, (1 << logn) // 2 // N)
+    groups = args.split if args.split else (2 if world % 2 == 0 and batches % 2 == 0 else 1)
     if world % groups:
         raise SystemExit(f"--split {groups} does not divide --gpus {world}")
     shard = grp = None
