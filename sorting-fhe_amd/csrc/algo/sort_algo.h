@@ -790,9 +790,10 @@ class DirectSort : public SortBase<N> {
     // generates and encodes the masks); the second is captured into a graph
     // over a sorter-owned copy of the input; from then on a sort is: copy the
     // caller's input into that buffer, launch the graph, clone its result.
-    // Debug sorts (PRINT_PT decrypts) stay eager, and so do contexts sharded
-    // over a host transport (BeginCapture refuses them); RCCL-sharded sorts
-    // capture their collectives into the graph.  SFHE_GRAPH=0 disables graphs.
+    // Debug sorts (PRINT_PT decrypts) replay two graphs with the decrypts
+    // between them (sortDebug); contexts sharded over a host transport run
+    // eagerly (BeginCapture refuses them); RCCL-sharded sorts capture their
+    // collectives into the graph.  SFHE_GRAPH=0 disables graphs.
     struct GraphKey {
         uint32_t level = 0, slots = 0;
         int func = -1, n = 0, dg = 0, df = 0;
@@ -817,18 +818,109 @@ class DirectSort : public SortBase<N> {
     }
 
   public:
-    ~DirectSort() override { m_graph.reset(); }
+    ~DirectSort() override {
+        m_graph.reset();
+        m_debugGraphs.reset();
+    }
     // nodes of the captured sort (0: none yet / eager)
-    size_t graphNodes() const { return m_graph ? m_cc->GraphNodes(m_graph->g) : 0; }
+    size_t graphNodes() const {
+        if (m_graph) return m_cc->GraphNodes(m_graph->g);
+        return m_debugGraphs ? m_cc->GraphNodes(m_debugGraphs->rank) + m_cc->GraphNodes(m_debugGraphs->place) : 0;
+    }
     // the captured sort's NTT kernels replayed alone (bench roofline)
     bool graphNttTime(int reps, double* ms, uint64_t* launches, double* bytes) {
         return m_graph && m_cc->GraphNttTime(m_graph->g, reps, ms, launches, bytes);
     }
 
+    // Debug sorts (DebugEncryption: PRINT_PT decrypts of the input, the rank
+    // and the output inside sort(), reference :755-770, as DirectSortTest
+    // times them) replay TWO graphs -- the rank and the placement -- with the
+    // three decrypts run eagerly between them, instead of running the whole
+    // sort eagerly.
+    struct DebugGraphs {
+        std::shared_ptr<CryptoContextImpl<DCRTPoly>::CapturedGraph> rank, place;
+        Ciphertext<DCRTPoly> in, rankOut, out;
+        GraphKey key;
+    };
+    std::unique_ptr<DebugGraphs> m_debugGraphs;
+
+    Ciphertext<DCRTPoly> sortDebug(const Ciphertext<DCRTPoly>& input_array, SignFunc SignFunc, SignConfig& Cfg,
+                                   const GraphKey& key) {
+        if (!(m_debugGraphs && m_debugGraphs->key == key)) {
+            if (!(m_warm && m_warmKey == key)) {  // first sort of this shape: eager, builds the masks
+                m_warm = true;
+                m_warmKey = key;
+                return sortEager(input_array, SignFunc, Cfg);
+            }
+            m_debugGraphs.reset();
+            auto g = std::make_unique<DebugGraphs>();
+            g->key = key;
+            m_cc->Settle(input_array);
+            g->in = input_array->Clone();
+            m_cc->Settle(g->in);
+            std::cout << "\n===== Direct Sort Input Array: \n";
+            PRINT_PT(m_enc, input_array);
+            auto capture = [&](auto&& body, Ciphertext<DCRTPoly>& out)
+                -> std::shared_ptr<CryptoContextImpl<DCRTPoly>::CapturedGraph> {
+                if (!m_cc->BeginCapture()) return nullptr;
+                try {
+                    out = body();
+                } catch (...) {
+                    m_cc->EndCapture(nullptr);
+                    m_graphOff = true;
+                    throw;
+                }
+                auto cg = m_cc->EndCapture(out);
+                if (cg) m_cc->Launch(cg);
+                return cg;
+            };
+            g->rank = capture([&] { return constructRank(g->in, SignFunc, Cfg); }, g->rankOut);
+            if (!g->rank) {  // (a capture that failed ran nothing: the rest eagerly)
+                m_graphOff = true;
+                auto r = constructRank(input_array, SignFunc, Cfg);
+                std::cout << "\n===== Constructed Rank: \n";
+                PRINT_PT(m_enc, r);
+                auto o = rotationIndexCheckN(r, input_array);
+                std::cout << "\n===== Final Output: \n";
+                PRINT_PT(m_enc, o);
+                std::cout << "Final Level: " << o->GetLevel() << std::endl;
+                return o;
+            }
+            std::cout << "\n===== Constructed Rank: \n";
+            PRINT_PT(m_enc, g->rankOut);
+            g->place = capture([&] { return rotationIndexCheckN(g->rankOut, g->in); }, g->out);
+            if (!g->place) {
+                m_graphOff = true;
+                auto o = rotationIndexCheckN(g->rankOut, input_array);
+                std::cout << "\n===== Final Output: \n";
+                PRINT_PT(m_enc, o);
+                std::cout << "Final Level: " << o->GetLevel() << std::endl;
+                return o;
+            }
+            m_debugGraphs = std::move(g);
+        } else {
+            if (m_debugGraphs->in != input_array) m_cc->CopyCiphertextInto(m_debugGraphs->in, input_array);
+            std::cout << "\n===== Direct Sort Input Array: \n";
+            PRINT_PT(m_enc, input_array);
+            m_cc->Launch(m_debugGraphs->rank);
+            std::cout << "\n===== Constructed Rank: \n";
+            PRINT_PT(m_enc, m_debugGraphs->rankOut);
+            m_cc->Launch(m_debugGraphs->place);
+        }
+        DebugGraphs& g = *m_debugGraphs;
+        std::cout << "\n===== Final Output: \n";
+        PRINT_PT(m_enc, g.out);
+        std::cout << "Final Level: " << g.out->GetLevel() << std::endl;
+        input_array->SetSlots(g.in->GetSlots());  // sort()'s side effect on its input (:711)
+        auto result = g.out->Clone();
+        result->SetSlots(g.out->GetSlots());
+        return result;
+    }
+
     Ciphertext<DCRTPoly> sort(const Ciphertext<DCRTPoly>& input_array, SignFunc SignFunc,
                               SignConfig& Cfg) override {
         const bool debug = dynamic_cast<const DebugEncryption*>(m_enc.get()) != nullptr;
-        if (debug || m_graphOff || !graphsEnabled())
+        if (m_graphOff || !graphsEnabled())
             return sortEager(input_array, SignFunc, Cfg);
         GraphKey key;
         key.level = input_array->GetLevel();
@@ -841,6 +933,7 @@ class DirectSort : public SortBase<N> {
         key.dg = Cfg.compos.dg;
         key.df = Cfg.compos.df;
         key.multDepth = Cfg.multDepth;
+        if (debug) return sortDebug(input_array, SignFunc, Cfg, key);
         if (!(m_graph && m_graph->key == key)) {
             if (!(m_warm && m_warmKey == key)) {  // first sort of this shape: eager, builds the masks
                 m_warm = true;

@@ -99,3 +99,37 @@ def test_graph_lazy_inputs(force_fail, monkeypatch):
         assert err < 1e-3, (i, err)
         if i >= 1:
             assert (s.graph_nodes() > 0) == (not force_fail)
+
+
+def test_debug_sort_graphs(capfd, monkeypatch):
+    """A debug sorter (DebugEncryption: the PRINT_PT decrypts of the input,
+    the rank and the output inside sort(), reference src/sort_algo.h:755-770,
+    as DirectSortTest times it) replays two graphs -- the rank and the
+    placement -- with the decrypts between them: outputs bit-identical to the
+    eager debug sort, and the printed decryptions the same text."""
+    N, logn = 64, 14
+    depth, rots = sfhe.direct_sort_params(N, "hip")
+    e = sfhe.Engine("hip", mult_depth=depth, ring_dim=1 << logn, batch_size=N, rotations=rots,
+                    seed=20251205 + N)
+    cfg = slotsim.default_sign_config(N)
+    s = e.sorter(N, debug=True)
+    ct = e.encrypt(slotsim.input_vector(N).tolist())
+    monkeypatch.setenv("SFHE_GRAPH", "1")
+    outs, texts = [], []
+    for _ in range(3):                   # eager, captured, replayed
+        capfd.readouterr()
+        outs.append(s.sort(ct, *cfg).download())
+        e.sync()
+        texts.append(capfd.readouterr().out)
+    nodes = s.graph_nodes()
+    assert nodes > 100, nodes
+    monkeypatch.setenv("SFHE_GRAPH", "0")
+    capfd.readouterr()
+    eager = s.sort(ct, *cfg).download()
+    e.sync()
+    eager_text = capfd.readouterr().out
+    assert "Constructed Rank" in eager_text and "Final Output" in eager_text
+    for o, t in zip(outs, texts):
+        assert np.array_equal(o, eager)
+        assert t == eager_text
+    print(f"debug sort: two graphs of {nodes} nodes, replay bit-identical to eager")
