@@ -129,7 +129,11 @@ def test_debug_sort_graphs(capfd, monkeypatch):
     e.sync()
     eager_text = capfd.readouterr().out
     assert "Constructed Rank" in eager_text and "Final Output" in eager_text
-    for o, t in zip(outs, texts):
+    for o in outs:
         assert np.array_equal(o, eager)
-        assert t == eager_text
+    # the captured and the replayed sort print what the eager one prints (the
+    # first sort's text differs: it sees its input at N slots, and sort()
+    # leaves the input at the layout's S slots, :711)
+    assert texts[1] == eager_text
+    assert texts[2] == eager_text
     print(f"debug sort: two graphs of {nodes} nodes, replay bit-identical to eager")
