@@ -877,25 +877,28 @@ class DirectSort : public SortBase<N> {
             g->rank = capture([&] { return constructRank(g->in, SignFunc, Cfg); }, g->rankOut);
             if (!g->rank) {  // (a capture that failed ran nothing: the rest eagerly)
                 m_graphOff = true;
-                auto r = constructRank(input_array, SignFunc, Cfg);
+                auto ctx_Rank = constructRank(input_array, SignFunc, Cfg);
                 std::cout << "\n===== Constructed Rank: \n";
-                PRINT_PT(m_enc, r);
-                auto o = rotationIndexCheckN(r, input_array);
+                PRINT_PT(m_enc, ctx_Rank);
+                auto output_array = rotationIndexCheckN(ctx_Rank, input_array);
                 std::cout << "\n===== Final Output: \n";
-                PRINT_PT(m_enc, o);
-                std::cout << "Final Level: " << o->GetLevel() << std::endl;
-                return o;
+                PRINT_PT(m_enc, output_array);
+                std::cout << "Final Level: " << output_array->GetLevel() << std::endl;
+                return output_array;
             }
-            std::cout << "\n===== Constructed Rank: \n";
-            PRINT_PT(m_enc, g->rankOut);
+            {
+                const auto& ctx_Rank = g->rankOut;  // (PRINT_PT prints the expression's name)
+                std::cout << "\n===== Constructed Rank: \n";
+                PRINT_PT(m_enc, ctx_Rank);
+            }
             g->place = capture([&] { return rotationIndexCheckN(g->rankOut, g->in); }, g->out);
             if (!g->place) {
                 m_graphOff = true;
-                auto o = rotationIndexCheckN(g->rankOut, input_array);
+                auto output_array = rotationIndexCheckN(g->rankOut, input_array);
                 std::cout << "\n===== Final Output: \n";
-                PRINT_PT(m_enc, o);
-                std::cout << "Final Level: " << o->GetLevel() << std::endl;
-                return o;
+                PRINT_PT(m_enc, output_array);
+                std::cout << "Final Level: " << output_array->GetLevel() << std::endl;
+                return output_array;
             }
             m_debugGraphs = std::move(g);
         } else {
@@ -903,14 +906,16 @@ class DirectSort : public SortBase<N> {
             std::cout << "\n===== Direct Sort Input Array: \n";
             PRINT_PT(m_enc, input_array);
             m_cc->Launch(m_debugGraphs->rank);
+            const auto& ctx_Rank = m_debugGraphs->rankOut;
             std::cout << "\n===== Constructed Rank: \n";
-            PRINT_PT(m_enc, m_debugGraphs->rankOut);
+            PRINT_PT(m_enc, ctx_Rank);
             m_cc->Launch(m_debugGraphs->place);
         }
         DebugGraphs& g = *m_debugGraphs;
+        const auto& output_array = g.out;
         std::cout << "\n===== Final Output: \n";
-        PRINT_PT(m_enc, g.out);
-        std::cout << "Final Level: " << g.out->GetLevel() << std::endl;
+        PRINT_PT(m_enc, output_array);
+        std::cout << "Final Level: " << output_array->GetLevel() << std::endl;
         input_array->SetSlots(g.in->GetSlots());  // sort()'s side effect on its input (:711)
         auto result = g.out->Clone();
         result->SetSlots(g.out->GetSlots());

@@ -694,8 +694,6 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_b
     const uint32_t pp = rid / G.R, ii = rid % G.R;
     if (G.skipEll && ii >= G.alpha * pp && ii < min(G.alpha * (pp + 1), G.skipEll)) return;
     const uint32_t prime = primeOf(G.pm, ii);
-    const u64 q = bar[prime].q;
-    const bool fp = useFp && q < kFpPrimeBound;  // uniform per block
     NttTile T;
     T.logn = logn;
     T.d = COL ? logR : 8u;
@@ -709,73 +707,114 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_b
     T.c0 = COL ? tile * T.C : 0u;
     T.r0 = COL ? 0u : tile * (TILE / 256);
     const uint32_t S0 = COL ? 0u : logR;
+    constexpr int NT = TILE >> LE, NPAIR = (1 << LE) / 2;
 
-    // the pass's twiddle table for this prime: FP64 values (W/q is formed in
-    // registers) or integer values with their Shoup companions
-    const u64* gw = fp ? reinterpret_cast<const u64*>(twD) + (size_t)prime * n : tw + (size_t)prime * n;
+    // Every global load the prologue needs is issued before the first wait:
+    // the tile (and its pre-multiplier / the epilogue's input row), both
+    // twiddle forms (the row's arithmetic is known only once q arrives), then
+    // the prime.  One HBM round trip instead of one per dependent step.
+    const u64* in = FIRST ? rowAt(G.src, pp, ii) : rowAt(G.dst, pp, ii);
+    const u64* pre = FIRST && G.pre.base ? rowAt(G.pre, pp, ii) : nullptr;
+    const bool epi = !FIRST && G.epi;
+    const u64* ein = epi ? rowAt(G.ein, pp, ii) : nullptr;
+    auto tileOff = [&](int k) -> size_t {
+        const uint32_t e = 2 * (threadIdx.x + k * NT);
+        return COL ? (size_t)(e >> T.logC) * 256 + T.c0 + (e & (T.C - 1)) : (size_t)T.r0 * 256 + e;
+    };
+    ulonglong2 xr[NPAIR], mr[NPAIR], er[NPAIR];
+#pragma unroll
+    for (int k = 0; k < NPAIR; ++k) xr[k] = *reinterpret_cast<const ulonglong2*>(in + tileOff(k));
+    if (pre) {
+#pragma unroll
+        for (int k = 0; k < NPAIR; ++k) mr[k] = *reinterpret_cast<const ulonglong2*>(pre + tileOff(k));
+    }
+    if (ein) {
+#pragma unroll
+        for (int k = 0; k < NPAIR; ++k) er[k] = *reinterpret_cast<const ulonglong2*>(ein + tileOff(k));
+    }
+    const u64* gwI = tw + (size_t)prime * n;
+    const u64* gwD = reinterpret_cast<const u64*>(twD) + (size_t)prime * n;
     const u64* gx = twS + (size_t)prime * n;
-    if (COL) {  // entries [1, 2^logR) -> LDS
-        for (uint32_t e = threadIdx.x; e < (1u << logR) - 1; e += (TILE >> LE)) {
-            tW[e] = gw[e + 1];
-            if (!fp) tX[e] = gx[e + 1];
+    // COL: twiddle entries [1, 2^logR) -> LDS (clamped indices: unconditional loads)
+    constexpr int kColPer = COL ? (int)((kNttColTw + NT - 1) / NT) : 1;
+    const uint32_t colTw = (1u << logR) - 1;
+    u64 cwI[kColPer], cwX[kColPer], cwD[kColPer];
+    if (COL) {
+#pragma unroll
+        for (int c = 0; c < kColPer; ++c) {
+            const uint32_t e = min(threadIdx.x + c * NT, colTw - 1) + 1;
+            cwI[c] = gwI[e];
+            cwX[c] = gx[e];
+            cwD[c] = gwD[e];
         }
     }
-    const u64* rw = COL ? tW : gw;
-    const u64* rx = COL ? tX : gx;
     // ROW pass, FP64 rows, one group per thread per round (LE = 2): every
     // round's twiddles are data-independent, so all 4 x 3 of them are loaded
     // here, in flight together with the tile, instead of one HBM latency per
-    // register round.
+    // register round (loaded for every row; integer rows ignore them)
     constexpr bool kPfBuild = !COL && LE == 2;
     constexpr int kPfRounds = 8 / 2;
-    const bool rowPf = kPfBuild && fp;
     double PW[kPfBuild ? kPfRounds * 3 : 1];
     if constexpr (kPfBuild) {
-        if (rowPf) {
-            const double* gd = reinterpret_cast<const double*>(gw);
-            const uint32_t gid = threadIdx.x;
+        const double* gd = reinterpret_cast<const double*>(gwD);
+        const uint32_t gid = threadIdx.x;
 #pragma unroll
-            for (int r = 0; r < kPfRounds; ++r) {
-                const uint32_t k0 = 2 * r, logh = 8 - k0 - 2;
-                const uint32_t lo = gid & ((1u << logh) - 1);
-                const uint32_t rest = gid >> logh;
-                const uint32_t hi = rest & ((1u << k0) - 1);
-                const uint32_t st = rest >> k0;
-                const uint32_t x0 = nttGlobal<false>(T, st, hi * (256u >> k0) + lo);
+        for (int r = 0; r < kPfRounds; ++r) {
+            const uint32_t k0 = 2 * r, logh = 8 - k0 - 2;
+            const uint32_t lo = gid & ((1u << logh) - 1);
+            const uint32_t rest = gid >> logh;
+            const uint32_t hi = rest & ((1u << k0) - 1);
+            const uint32_t st = rest >> k0;
+            const uint32_t x0 = nttGlobal<false>(T, st, hi * (256u >> k0) + lo);
 #pragma unroll
-                for (int t = 0; t < 2; ++t) {
-                    const uint32_t tb = twIndex<false>(T, S0, k0 + t, x0);
+            for (int t = 0; t < 2; ++t) {
+                const uint32_t tb = twIndex<false>(T, S0, k0 + t, x0);
 #pragma unroll
-                    for (int qd = 0; qd < (1 << t); ++qd) PW[3 * r + (1 << t) - 1 + qd] = gd[tb + qd];
-                }
+                for (int qd = 0; qd < (1 << t); ++qd) PW[3 * r + (1 << t) - 1 + qd] = gd[tb + qd];
             }
         }
     }
-
-    const u64* in = FIRST ? rowAt(G.src, pp, ii) : rowAt(G.dst, pp, ii);
-    u64* cp = nullptr;
-    if (FIRST && G.copy.base)
-        cp = G.copyByAlpha ? const_cast<u64*>(G.copy.base) + (ii / G.alpha) * G.copy.ps + ii * G.copy.is
-                           : rowAt(G.copy, pp, ii);
     sf_barrett LB{};
     u64 lsub = 0;
-    const u64* pre = FIRST && G.pre.base ? rowAt(G.pre, pp, ii) : nullptr;
     const bool preK = FIRST && G.preK;
     const u64 pk = preK ? G.preK[ii] : 0, pkS = preK ? G.preKS[ii] : 0;
     if (FIRST && (G.lift || pre)) LB = loadBar(bar, prime);
     if (FIRST && G.lift) lsub = G.liftSub[ii];
     const u64 lhalf = (FIRST && G.lift) ? (bar[G.liftPrime].q >> 1) : 0;
+    const u64 q = bar[prime].q;
+    const bool fp = useFp && q < kFpPrimeBound;  // uniform per block
+    const bool rowPf = kPfBuild && fp;
 
-    // global -> LDS, 16 B per lane; tile-linear word e is row-major (u, st)
+    // the pass's twiddle table for this prime: FP64 values (W/q is formed in
+    // registers) or integer values with their Shoup companions
+    const u64* gw = fp ? gwD : gwI;
+    if (COL) {
 #pragma unroll
-    for (int k = 0; k < (1 << LE) / 2; ++k) {
-        const uint32_t e = 2 * (threadIdx.x + k * (TILE >> LE));
-        const size_t g = COL ? (size_t)(e >> T.logC) * 256 + T.c0 + (e & (T.C - 1)) : (size_t)T.r0 * 256 + e;
-        ulonglong2 x = *reinterpret_cast<const ulonglong2*>(in + g);
+        for (int c = 0; c < kColPer; ++c) {
+            const uint32_t e = threadIdx.x + c * NT;
+            if (e < colTw) {
+                tW[e] = fp ? cwD[c] : cwI[c];
+                if (!fp) tX[e] = cwX[c];
+            }
+        }
+    }
+    const u64* rw = COL ? tW : gw;
+    const u64* rx = COL ? tX : gx;
+    u64* cp = nullptr;
+    if (FIRST && G.copy.base)
+        cp = G.copyByAlpha ? const_cast<u64*>(G.copy.base) + (ii / G.alpha) * G.copy.ps + ii * G.copy.is
+                           : rowAt(G.copy, pp, ii);
+
+    // tile -> LDS, 16 B per lane; tile-linear word e is row-major (u, st)
+#pragma unroll
+    for (int k = 0; k < NPAIR; ++k) {
+        const uint32_t e = 2 * (threadIdx.x + k * NT);
+        const size_t g = tileOff(k);
+        ulonglong2 x = xr[k];
         if (FIRST) {
             if (cp) *reinterpret_cast<ulonglong2*>(cp + g) = x;
             if (pre) {
-                const ulonglong2 m = *reinterpret_cast<const ulonglong2*>(pre + g);
+                const ulonglong2 m = mr[k];
                 x.x = bmul(x.x, m.x, LB);
                 x.y = bmul(x.y, m.y, LB);
             }
@@ -844,9 +883,7 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_b
     }
     const bool scale = INV && COL;
     const u64 ni = scale ? ninv[prime] : 0, niS = scale ? ninvS[prime] : 0;
-    const bool epi = !FIRST && G.epi;
     u64* out = epi ? rowAt(G.eout, pp, ii) : rowAt(G.dst, pp, ii);
-    const u64* ein = epi ? rowAt(G.ein, pp, ii) : nullptr;
     const u64 ek = epi ? G.k[ii] : 0, ekS = epi ? G.kS[ii] : 0;
     const u64* ead = epi && G.eadd.base ? rowAt(G.eadd, pp, ii) : nullptr;
     const bool tens = epi && G.tA0;
@@ -857,9 +894,9 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_b
     const sf_barrett EB = (emul || tens) ? loadBar(bar, prime) : sf_barrett{};
     const size_t trow = (size_t)ii << logn;
 #pragma unroll
-    for (int k = 0; k < (1 << LE) / 2; ++k) {
-        const uint32_t e = 2 * (threadIdx.x + k * (TILE >> LE));
-        const size_t g = COL ? (size_t)(e >> T.logC) * 256 + T.c0 + (e & (T.C - 1)) : (size_t)T.r0 * 256 + e;
+    for (int k = 0; k < NPAIR; ++k) {
+        const uint32_t e = 2 * (threadIdx.x + k * NT);
+        const size_t g = tileOff(k);
         ulonglong2 x;
         x.x = s[ldsSw(e)];
         x.y = s[ldsSw(e + 1)];
@@ -884,7 +921,7 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_b
             x.y = x.y >= q ? x.y - q : x.y;
         }
         if (epi) {
-            ulonglong2 a = *reinterpret_cast<const ulonglong2*>(ein + g);
+            ulonglong2 a = er[k];
             if (emul) {
                 const ulonglong2 m = *reinterpret_cast<const ulonglong2*>(emul + g);
                 a.x = bmul(a.x, m.x, EB);
@@ -1068,7 +1105,7 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt_ks(const KsArgs A, const sf_
                                                      const u64* __restrict__ tw, const u64* __restrict__ twS,
                                                      uint32_t logn, const double* __restrict__ twD,
                                                      const double* __restrict__ qinvD, int useFp) {
-    __shared__ u64 s[TILE];
+    __shared__ u64 s[2 * TILE];  // the second tile: acc1's inverse ROW pass (same rounds as acc0's)
     constexpr int NT = TILE >> LE;       // threads
     constexpr int NPAIR = (1 << LE) / 2;  // 16-byte pairs per thread
     const uint32_t n = 1u << logn;
@@ -1115,12 +1152,54 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt_ks(const KsArgs A, const sf_
     const double qd = (double)q, qi = qinvD[prime];
     const uint32_t kr = t < A.ell ? t : A.keyQ + (t - A.ell);
     const size_t rowOff = (size_t)T.r0 * 256;
+    const bool inv = t >= A.invFrom;
+    const u64* iw = fp ? reinterpret_cast<const u64*>(A.itwD) + (size_t)prime * n : A.itw + (size_t)prime * n;
+    const u64* ix = A.itwS + (size_t)prime * n;
+    // Register prefetches (the kernel runs at two waves per SIMD, so latency
+    // is hidden by loads in flight, not by other waves): the inverse pass's
+    // twiddles, the previous accumulator, and each digit's key rows below are
+    // issued before the work that precedes their use.
+    double PIW[kPfBuild ? kPfRounds * 3 : 1];
+    if constexpr (kPfBuild) {
+        if (fp && inv) {
+            const double* gd = reinterpret_cast<const double*>(iw);
+#pragma unroll
+            for (int r = 0; r < kPfRounds; ++r) {
+                const uint32_t k0 = 2 * r, logh = 8 - k0 - 2;
+                const uint32_t lo = threadIdx.x & ((1u << logh) - 1);
+                const uint32_t rest = threadIdx.x >> logh;
+                const uint32_t hi = rest & ((1u << k0) - 1);
+                const uint32_t st = rest >> k0;
+                const uint32_t x0 = nttGlobal<false>(T, st, hi * (256u >> k0) + lo);
+#pragma unroll
+                for (int tt = 0; tt < 2; ++tt) {
+                    const uint32_t tb = twIndex<false>(T, S0, k0 + tt, x0);
+#pragma unroll
+                    for (int qd2 = 0; qd2 < (1 << tt); ++qd2) PIW[3 * r + (1 << tt) - 1 + qd2] = gd[tb + qd2];
+                }
+            }
+        }
+    }
+    u64* o0 = A.acc0 + (size_t)t * n + rowOff;
+    u64* o1 = A.acc1 + (size_t)t * n + rowOff;
+    ulonglong2 prev[2][NPAIR];
+    if (A.accum) {
+#pragma unroll
+        for (int k = 0; k < NPAIR; ++k) {
+            const uint32_t e = 2 * (threadIdx.x + k * NT);
+            prev[0][k] = *reinterpret_cast<const ulonglong2*>(o0 + e);
+            prev[1][k] = *reinterpret_cast<const ulonglong2*>(o1 + e);
+        }
+    }
     Acc a0[2 * NPAIR], a1[2 * NPAIR];
 #pragma unroll
     for (int w = 0; w < 2 * NPAIR; ++w) a0[w] = a1[w] = Acc{0, 0};
     for (uint32_t j = 0; j < A.beta; ++j) {
         const bool own = t < A.ell && t >= j * A.alpha && t < min((j + 1) * A.alpha, A.ell);
         u64 v[2 * NPAIR];
+        const u64* kb = A.key + (size_t)j * 2 * A.keyRows * n + (size_t)kr * n + rowOff;
+        const u64* ka = kb + (size_t)A.keyRows * n;
+        ulonglong2 kb2[NPAIR], ka2[NPAIR];
         if (own) {
             const u64* src = A.in + (size_t)t * n + rowOff;
             const u64* mul = A.inMul ? A.inMul + (size_t)t * n + rowOff : nullptr;
@@ -1136,13 +1215,28 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt_ks(const KsArgs A, const sf_
                 v[2 * k] = x.x;
                 v[2 * k + 1] = x.y;
             }
+#pragma unroll
+            for (int k = 0; k < NPAIR; ++k) {
+                const uint32_t e = 2 * (threadIdx.x + k * NT);
+                kb2[k] = *reinterpret_cast<const ulonglong2*>(kb + e);
+                ka2[k] = *reinterpret_cast<const ulonglong2*>(ka + e);
+            }
         } else {
             const u64* src = A.ext + j * A.extStride + (size_t)t * n + rowOff;
+            ulonglong2 xs[NPAIR];
+#pragma unroll
+            for (int k = 0; k < NPAIR; ++k) xs[k] = *reinterpret_cast<const ulonglong2*>(src + 2 * (threadIdx.x + k * NT));
+#pragma unroll
+            for (int k = 0; k < NPAIR; ++k) {  // in flight during the ROW rounds
+                const uint32_t e = 2 * (threadIdx.x + k * NT);
+                kb2[k] = *reinterpret_cast<const ulonglong2*>(kb + e);
+                ka2[k] = *reinterpret_cast<const ulonglong2*>(ka + e);
+            }
             __syncthreads();  // the previous digit's readers are done with s
 #pragma unroll
             for (int k = 0; k < NPAIR; ++k) {
                 const uint32_t e = 2 * (threadIdx.x + k * NT);
-                const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(src + e);
+                const ulonglong2 x = xs[k];
                 if (fp) {
                     s[ldsSw(e)] = __double_as_longlong(u2d(x.x));
                     s[ldsSw(e + 1)] = __double_as_longlong(u2d(x.y));
@@ -1194,13 +1288,10 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt_ks(const KsArgs A, const sf_
                 v[2 * k + 1] = x1;
             }
         }
-        const u64* kb = A.key + (size_t)j * 2 * A.keyRows * n + (size_t)kr * n + rowOff;
-        const u64* ka = kb + (size_t)A.keyRows * n;
 #pragma unroll
         for (int k = 0; k < NPAIR; ++k) {
-            const uint32_t e = 2 * (threadIdx.x + k * NT);
-            const ulonglong2 b2 = *reinterpret_cast<const ulonglong2*>(kb + e);
-            const ulonglong2 a2 = *reinterpret_cast<const ulonglong2*>(ka + e);
+            const ulonglong2 b2 = kb2[k];
+            const ulonglong2 a2 = ka2[k];
             macc(a0[2 * k], v[2 * k], b2.x);
             macc(a0[2 * k + 1], v[2 * k + 1], b2.y);
             macc(a1[2 * k], v[2 * k], a2.x);
@@ -1208,10 +1299,7 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt_ks(const KsArgs A, const sf_
         }
     }
     const bool fold = (A.fold0 || A.fa0) && t == A.ell - 1;
-    u64* o0 = A.acc0 + (size_t)t * n + rowOff;
-    u64* o1 = A.acc1 + (size_t)t * n + rowOff;
-    const bool inv = t >= A.invFrom;
-    ulonglong2 r[2][NPAIR];
+    if (inv) __syncthreads();  // the last digit's readers are done with s
 #pragma unroll
     for (int k = 0; k < NPAIR; ++k) {
         const uint32_t e = 2 * (threadIdx.x + k * NT);
@@ -1247,58 +1335,72 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt_ks(const KsArgs A, const sf_
         r1.x = sf_reduce128_acc(a1[2 * k].lo, a1[2 * k].hi, &B);
         r1.y = sf_reduce128_acc(a1[2 * k + 1].lo, a1[2 * k + 1].hi, &B);
         if (A.accum) {
-            const ulonglong2 p0 = *reinterpret_cast<const ulonglong2*>(o0 + e);
-            const ulonglong2 p1 = *reinterpret_cast<const ulonglong2*>(o1 + e);
+            const ulonglong2 p0 = prev[0][k], p1 = prev[1][k];
             r0.x = sf_add(r0.x, p0.x, q);
             r0.y = sf_add(r0.y, p0.y, q);
             r1.x = sf_add(r1.x, p1.x, q);
             r1.y = sf_add(r1.y, p1.y, q);
         }
-        r[0][k] = r0;
-        r[1][k] = r1;
         if (!inv) {
             *reinterpret_cast<ulonglong2*>(o0 + e) = r0;
             *reinterpret_cast<ulonglong2*>(o1 + e) = r1;
+        } else if (fp) {
+            s[ldsSw(e)] = __double_as_longlong(u2d(r0.x));
+            s[ldsSw(e + 1)] = __double_as_longlong(u2d(r0.y));
+            s[TILE + ldsSw(e)] = __double_as_longlong(u2d(r1.x));
+            s[TILE + ldsSw(e + 1)] = __double_as_longlong(u2d(r1.y));
+        } else {
+            s[ldsSw(e)] = r0.x;
+            s[ldsSw(e + 1)] = r0.y;
+            s[TILE + ldsSw(e)] = r1.x;
+            s[TILE + ldsSw(e + 1)] = r1.y;
         }
     }
     if (!inv) return;
-    // ModDown's inverse ROW pass on both accumulators' tiles (as k_ntt's first
-    // inverse pass: FP64 rows leave canonical, integer rows in [0, 2q))
-    const u64* iw = fp ? reinterpret_cast<const u64*>(A.itwD) + (size_t)prime * n : A.itw + (size_t)prime * n;
-    const u64* ix = A.itwS + (size_t)prime * n;
-    for (int p = 0; p < 2; ++p) {
-        __syncthreads();  // s is free (the last digit's readers, or the previous poly's writers)
+    // ModDown's inverse ROW pass on both accumulators' tiles, round by round
+    // (as k_ntt's first inverse pass: FP64 rows leave canonical, integer rows
+    // in [0, 2q))
+    __syncthreads();
+    bool done = false;
+    if constexpr (kPfBuild) {
+        if (fp) {
 #pragma unroll
-        for (int k = 0; k < NPAIR; ++k) {
-            const uint32_t e = 2 * (threadIdx.x + k * NT);
-            if (fp) {
-                s[ldsSw(e)] = __double_as_longlong(u2d(r[p][k].x));
-                s[ldsSw(e + 1)] = __double_as_longlong(u2d(r[p][k].y));
-            } else {
-                s[ldsSw(e)] = r[p][k].x;
-                s[ldsSw(e + 1)] = r[p][k].y;
+            for (int ri = 0; ri < kPfRounds; ++ri) {
+                const int r = kPfRounds - 1 - ri;
+                nttRoundFP<true, false, 2, 2, TILE, true, 8>(reinterpret_cast<double*>(s), T, S0, 2 * r, qd, nullptr,
+                                                             qi, PIW + 3 * r);
+                nttRoundFP<true, false, 2, 2, TILE, true, 8>(reinterpret_cast<double*>(s + TILE), T, S0, 2 * r, qd,
+                                                             nullptr, qi, PIW + 3 * r);
+                __syncthreads();
             }
+            done = true;
         }
-        __syncthreads();
+    }
+    if (!done) {
         const uint32_t nr = (8 + LE - 1) / LE;
         for (uint32_t ri = 0; ri < nr; ++ri) {
             const uint32_t rr = nr - 1 - ri;
             const uint32_t k0 = LE * rr;
             const int b = (int)min((uint32_t)LE, 8u - k0);
-            if (fp)
-                nttRoundDynFP<true, false, LE, TILE>(b, reinterpret_cast<double*>(s), T, S0, k0, qd,
-                                                     reinterpret_cast<const double*>(iw), qi);
-            else
-                nttRoundDyn<true, false, LE, TILE>(b, s, T, S0, k0, q, iw, ix);
+            for (int p = 0; p < 2; ++p) {
+                if (fp)
+                    nttRoundDynFP<true, false, LE, TILE>(b, reinterpret_cast<double*>(s + p * TILE), T, S0, k0, qd,
+                                                         reinterpret_cast<const double*>(iw), qi);
+                else
+                    nttRoundDyn<true, false, LE, TILE>(b, s + p * TILE, T, S0, k0, q, iw, ix);
+            }
             __syncthreads();
         }
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
         u64* o = p ? o1 : o0;
 #pragma unroll
         for (int k = 0; k < NPAIR; ++k) {
             const uint32_t e = 2 * (threadIdx.x + k * NT);
             ulonglong2 x;
-            x.x = s[ldsSw(e)];
-            x.y = s[ldsSw(e + 1)];
+            x.x = s[p * TILE + ldsSw(e)];
+            x.y = s[p * TILE + ldsSw(e + 1)];
             if (fp) {
                 x.x = d2u(fpReduce(__longlong_as_double(x.x), qd, qi));
                 x.y = d2u(fpReduce(__longlong_as_double(x.y), qd, qi));
@@ -1532,7 +1634,24 @@ __global__ __launch_bounds__(kThreads) void k_mac_plain2(u64* __restrict__ out0,
         const size_t e = 2 * i;
         const sf_barrett B = loadBar(bar, primeOf(m, (uint32_t)(e >> logn)));
         Acc x0{0, 0}, y0{0, 0}, x1{0, 0}, y1{0, 0};
-        for (uint32_t j = 0; j < nin; ++j) {
+        uint32_t j = 0;
+        for (; j + 2 <= nin; j += 2) {  // two terms' six loads in flight together
+            const ulonglong2 p = *reinterpret_cast<const ulonglong2*>(L.b[j] + e);
+            const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(L.a[j] + e);
+            const ulonglong2 c = *reinterpret_cast<const ulonglong2*>(L.c[j] + e);
+            const ulonglong2 p2 = *reinterpret_cast<const ulonglong2*>(L.b[j + 1] + e);
+            const ulonglong2 a2 = *reinterpret_cast<const ulonglong2*>(L.a[j + 1] + e);
+            const ulonglong2 c2 = *reinterpret_cast<const ulonglong2*>(L.c[j + 1] + e);
+            macc(x0, a.x, p.x);
+            macc(y0, a.y, p.y);
+            macc(x1, c.x, p.x);
+            macc(y1, c.y, p.y);
+            macc(x0, a2.x, p2.x);
+            macc(y0, a2.y, p2.y);
+            macc(x1, c2.x, p2.x);
+            macc(y1, c2.y, p2.y);
+        }
+        if (j < nin) {
             const ulonglong2 p = *reinterpret_cast<const ulonglong2*>(L.b[j] + e);
             const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(L.a[j] + e);
             const ulonglong2 c = *reinterpret_cast<const ulonglong2*>(L.c[j] + e);
@@ -1768,6 +1887,9 @@ constexpr int kConvCoefs = SFHE_CONV_COEFS;
 #define SFHE_CONV_TPI 4
 #endif
 constexpr int kConvTpi = SFHE_CONV_TPI;  // FP64 targets per phase-2 iteration
+// phase-1 source words per thread (NS sources x kConvCoefs coefficients)
+template <int NS>
+constexpr int kConvPer = (NS * kConvCoefs + kThreads - 1) / kThreads;
 static_assert(kConvChunk % kConvTpi == 0 && kConvCoefs % 64 == 0 && kConvCoefs <= kThreads, "conversion block shape");
 
 template <int NS>
@@ -1799,6 +1921,14 @@ __global__ __launch_bounds__(kThreads) void k_convf(const ConvJobs J, const sf_b
     const uint32_t tc = min((uint32_t)C, cnt - k0);
     const uint32_t ns = c.ns;
     const uint32_t* tl = fpBlock ? c.fpT : c.intT;
+    // the block's source words are issued first (as k_mdrsf)
+    const uint32_t x0 = blockIdx.x * X, nsX = ns * X;
+    u64 sv[kConvPer<NS>];
+#pragma unroll
+    for (int k = 0; k < kConvPer<NS>; ++k) {
+        const uint32_t e = min(threadIdx.x + k * kThreads, nsX - 1);  // (unconditional: no branch between loads)
+        sv[k] = c.src[((size_t)(e / X) << logn) + x0 + e % X];
+    }
     if (threadIdx.x < ns) {
         const uint32_t i = threadIdx.x, pi = c.sidx[i];
         sB[i] = loadBar(bar, pi);
@@ -1834,12 +1964,15 @@ __global__ __launch_bounds__(kThreads) void k_convf(const ConvJobs J, const sf_b
             hQs[b * C + k] = c.hQ[(size_t)b * c.nFpAll + k0 + k];
         }
     __syncthreads();
-    const uint32_t x0 = blockIdx.x * X, lane = threadIdx.x % 64, w = threadIdx.x / 64;
+    const uint32_t lane = threadIdx.x % 64, w = threadIdx.x / 64;
     const bool cen = c.centered;
     // phase 1: y for every (source, coefficient) pair
-    for (uint32_t e = threadIdx.x; e < ns * X; e += kThreads) {
+#pragma unroll
+    for (int k = 0; k < kConvPer<NS>; ++k) {
+        const uint32_t e = threadIdx.x + k * kThreads;
+        if (e >= nsX) break;
         const uint32_t i = e / X, cx = e % X;
-        const u64 s = c.src[((size_t)i << logn) + x0 + cx];
+        const u64 s = sv[k];
         const sf_barrett B = sB[i];
         if (!fpBlock) {
             yL[i * X + cx] = bmul(s, sInv[i], B);
@@ -2058,6 +2191,17 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
     const uint32_t tc = min((uint32_t)C, cnt - k0);
     const uint32_t ns = A.ns;
     const uint32_t* tl = fpBlock ? A.fpT : A.intT;
+    // the block's source words and its dropped-row words are issued first, so
+    // their HBM latency overlaps the constant staging below (one round trip
+    // for the whole phase 1 instead of one per loop iteration)
+    const uint32_t x0 = blockIdx.x * X, nsX = ns * X;
+    u64 sv[kConvPer<NS>];
+#pragma unroll
+    for (int k = 0; k < kConvPer<NS>; ++k) {
+        const uint32_t e = min(threadIdx.x + k * kThreads, nsX - 1);  // (unconditional: no branch between loads)
+        sv[k] = J.src[((size_t)(e / X) << logn) + x0 + e % X];
+    }
+    const u64 alv = J.al[((size_t)A.l << logn) + x0 + threadIdx.x % X];
     if (threadIdx.x < ns) {
         const uint32_t i = threadIdx.x, pi = A.sidx[i];
         sB[i] = loadBar(bar, pi);
@@ -2095,15 +2239,19 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
         }
     }
     __syncthreads();
-    const uint32_t x0 = blockIdx.x * X, lane = threadIdx.x % 64, w = threadIdx.x / 64;
-    for (uint32_t e = threadIdx.x; e < ns * X; e += kThreads) {
-        const uint32_t i = e / X, cx = e % X;
-        const u64 s = J.src[((size_t)i << logn) + x0 + cx];
-        yL[i * X + cx] = fpSourceY(s, (double)sB[i].q, sInvD[i], sInvQ[i], sQi[i], true);
+    const uint32_t lane = threadIdx.x % 64, w = threadIdx.x / 64;
+#pragma unroll
+    for (int k = 0; k < kConvPer<NS>; ++k) {
+        const uint32_t e = threadIdx.x + k * kThreads;
+        if (e < nsX) {
+            const uint32_t i = e / X;
+            yL[e] = fpSourceY(sv[k], (double)sB[i].q, sInvD[i], sInvQ[i], sQi[i], true);
+        }
     }
     __syncthreads();
     const double qld = (double)bar[A.l].q;
-    for (uint32_t cx = threadIdx.x; cx < X; cx += kThreads) {  // the dropped row: r = (a_l - conv_l) * P^-1 mod q_l, centred
+    if (threadIdx.x < X) {  // the dropped row: r = (a_l - conv_l) * P^-1 mod q_l, centred
+        const uint32_t cx = threadIdx.x;
         // exact centred conversion: the overflow v (convOverflow), removed from every target
         double acc = 0.0;
 #pragma unroll
@@ -2123,20 +2271,18 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
                     neg += y < 0.0;
                 }
             const u64 cl = subMultiple(sf_reduce128_acc(sl.lo, sl.hi, &BL), neg, A.sprod[A.l], BL);
-            const u64 al = J.al[((size_t)A.l << logn) + x0 + cx];
-            rL[cx] = __longlong_as_double((long long)bmul(sf_sub(al, cl, BL.q), A.pinvl, BL));
-            continue;
-        }
+            rL[cx] = __longlong_as_double((long long)bmul(sf_sub(alv, cl, BL.q), A.pinvl, BL));
+        } else {
         const double spl = (double)A.sprod[A.l];
         double cl = fpMulMod(-v, spl, spl / qld, qld);
 #pragma unroll
         for (int i = 0; i < NS; ++i)
             if ((uint32_t)i < ns) cl += fpMulMod(yL[i * X + cx], sLD[i], sLQ[i], qld);
         const double qli = qinvD[A.l];
-        const u64 al = J.al[((size_t)A.l << logn) + x0 + cx];
         const double pl = (double)A.pinvl;
-        rL[cx] = fpSourceY((u64)fpReduce((double)al - fpReduce(cl, qld, qli), qld, qli), qld, pl, pl / qld, qli,
+        rL[cx] = fpSourceY((u64)fpReduce((double)alv - fpReduce(cl, qld, qli), qld, qli), qld, pl, pl / qld, qli,
                            true);
+        }
     }
     __syncthreads();
     if (!BIGL && fpBlock) {  // kConvTpi targets at a time, work items as k_convf
