@@ -156,3 +156,29 @@ def test_depth_exhaustion_is_an_error(oracle_lib):
     c2 = e.mult(c, c)
     with pytest.raises(sfhe.SfheError):
         e.mult(c2, c2)
+
+
+def test_debug_sort_repeats(oracle_lib, capfd):
+    """A debug sorter (DebugEncryption's PRINT_PT decrypts inside sort(),
+    src/sort_algo.h:755-770) sorted three times: on the oracle the graph
+    capture the second sort attempts is refused, the sorter falls back to
+    eager sorts (DirectSort::sortDebug), and every sort returns the same
+    ciphertext and prints the same sections; the second and third the same
+    text."""
+    N = 8
+    depth, rots = sfhe.direct_sort_params(N, "oracle")
+    e = sfhe.Engine("oracle", mult_depth=depth, ring_dim=1 << 12, batch_size=N, rotations=rots, seed=7)
+    s = e.sorter(N, debug=True)
+    x = slotsim.input_vector(N)
+    ct = e.encrypt(x.tolist())
+    cfg = slotsim.default_sign_config(N)
+    outs, texts = [], []
+    for _ in range(3):
+        capfd.readouterr()
+        outs.append(s.sort(ct, *cfg).download())
+        texts.append(capfd.readouterr().out)
+    for t in texts:
+        assert t.count("Constructed Rank") == 1 and t.count("Final Output") == 1
+    assert np.array_equal(outs[0], outs[1]) and np.array_equal(outs[1], outs[2])
+    assert texts[1] == texts[2]
+    np.testing.assert_allclose(np.array(e.decrypt(e.sorter(N).sort(ct, *cfg)))[:N], np.sort(x), atol=0.01)
