@@ -710,7 +710,7 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_b
     constexpr int NT = TILE >> LE, NPAIR = (1 << LE) / 2;
 
     // Every global load the prologue needs is issued before the first wait:
-    // the tile (and its pre-multiplier / the epilogue's input row), both
+    // the tile (and its pre-multiplier), both
     // twiddle forms (the row's arithmetic is known only once q arrives), then
     // the prime.  One HBM round trip instead of one per dependent step.
     const u64* in = FIRST ? rowAt(G.src, pp, ii) : rowAt(G.dst, pp, ii);
@@ -721,16 +721,12 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_b
         const uint32_t e = 2 * (threadIdx.x + k * NT);
         return COL ? (size_t)(e >> T.logC) * 256 + T.c0 + (e & (T.C - 1)) : (size_t)T.r0 * 256 + e;
     };
-    ulonglong2 xr[NPAIR], mr[NPAIR], er[NPAIR];
+    ulonglong2 xr[NPAIR], mr[NPAIR];
 #pragma unroll
     for (int k = 0; k < NPAIR; ++k) xr[k] = *reinterpret_cast<const ulonglong2*>(in + tileOff(k));
     if (pre) {
 #pragma unroll
         for (int k = 0; k < NPAIR; ++k) mr[k] = *reinterpret_cast<const ulonglong2*>(pre + tileOff(k));
-    }
-    if (ein) {
-#pragma unroll
-        for (int k = 0; k < NPAIR; ++k) er[k] = *reinterpret_cast<const ulonglong2*>(ein + tileOff(k));
     }
     const u64* gwI = tw + (size_t)prime * n;
     const u64* gwD = reinterpret_cast<const u64*>(twD) + (size_t)prime * n;
@@ -920,8 +916,8 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_b
             x.x = x.x >= q ? x.x - q : x.x;
             x.y = x.y >= q ? x.y - q : x.y;
         }
-        if (epi) {
-            ulonglong2 a = er[k];
+        if (epi) {  // (the input row is read here: loaded with the tile it cost a wave per SIMD)
+            ulonglong2 a = *reinterpret_cast<const ulonglong2*>(ein + g);
             if (emul) {
                 const ulonglong2 m = *reinterpret_cast<const ulonglong2*>(emul + g);
                 a.x = bmul(a.x, m.x, EB);
