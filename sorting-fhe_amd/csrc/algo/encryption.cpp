@@ -7,14 +7,18 @@ Ciphertext<DCRTPoly> Encryption::encryptInput(std::vector<double> input) {
     return m_cc->Encrypt(m_PublicKey, m_cc->MakeCKKSPackedPlaintext(input));
 }
 
-std::vector<double> DebugEncryption::getPlaintext(const Ciphertext<DCRTPoly>& ct,
-                                                  double threshold) const {
-    Plaintext pt;
-    m_cc->Decrypt(m_PrivateKey, ct, &pt);
+std::vector<double> DebugEncryption::realValues(const Plaintext& pt, double threshold) {
     std::vector<double> v = pt->GetRealPackedValue();
     for (double& x : v)
         if (std::fabs(x) < threshold) x = 0.0;
     return v;
+}
+
+std::vector<double> DebugEncryption::getPlaintext(const Ciphertext<DCRTPoly>& ct,
+                                                  double threshold) const {
+    Plaintext pt;
+    m_cc->Decrypt(m_PrivateKey, ct, &pt);
+    return realValues(pt, threshold);
 }
 
 Plaintext DebugEncryption::getDecrypt(const Ciphertext<DCRTPoly>& ct) const {

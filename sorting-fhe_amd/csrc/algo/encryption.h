@@ -18,12 +18,13 @@ using namespace lbcrypto;
 // Debug print of a ciphertext's decryption (compiled in when ENABLE_PRINT_PT
 // is defined, as the reference's default build does: CMakeLists.txt:63-66).
 #ifdef ENABLE_PRINT_PT
+// (one decryption serves both the values and the precision estimate)
 #define PRINT_PT(enc, ct)                                                              \
     do {                                                                               \
         if (dynamic_cast<const DebugEncryption*>((enc).get()) != nullptr) {            \
-            auto _pt = (enc)->getPlaintext((ct));                                      \
-            std::cout << _pt << ": " << #ct << " Level: " << (ct)->GetLevel()          \
-                      << ", LogPrecision: " << (enc)->getDecrypt((ct))->GetLogPrecision() \
+            const Plaintext _dp = (enc)->getDecrypt((ct));                             \
+            std::cout << DebugEncryption::realValues(_dp) << ": " << #ct << " Level: "  \
+                      << (ct)->GetLevel() << ", LogPrecision: " << _dp->GetLogPrecision() \
                       << "\n";                                                         \
         }                                                                              \
     } while (0)
@@ -62,6 +63,8 @@ class DebugEncryption : public Encryption {
     [[nodiscard]] std::vector<double> getPlaintext(const Ciphertext<DCRTPoly>& ct,
                                                    double threshold = 1e-10) const override;
     Plaintext getDecrypt(const Ciphertext<DCRTPoly>& ct) const override;
+    // a decryption's real slot values, |x| < threshold shown as 0 (getPlaintext's form)
+    static std::vector<double> realValues(const Plaintext& pt, double threshold = 1e-10);
 
   private:
     PrivateKey<DCRTPoly> m_PrivateKey;

@@ -64,8 +64,9 @@ void fftSpecialInv(std::complex<double>* v, uint32_t size, const FFTTables& t) {
         for (uint32_t i = 0; i < size; i += len) {
             uint32_t lenh = len >> 1;
             uint64_t lenq = (uint64_t)len << 2;
+            const uint64_t step = M / lenq;  // lenq divides M: the divisions are masks and a product
             for (uint32_t j = 0; j < lenh; ++j) {
-                uint64_t idx = (lenq - (t.rot[j] % lenq)) * M / lenq;
+                uint64_t idx = (lenq - (t.rot[j] & (lenq - 1))) * step;
                 std::complex<double> u = v[i + j] + v[i + j + lenh];
                 std::complex<double> w = (v[i + j] - v[i + j + lenh]) * t.ksi[idx];
                 v[i + j] = u;
@@ -85,8 +86,9 @@ void fftSpecial(std::complex<double>* v, uint32_t size, const FFTTables& t) {
         for (uint32_t i = 0; i < size; i += len) {
             uint32_t lenh = len >> 1;
             uint64_t lenq = (uint64_t)len << 2;
+            const uint64_t step = M / lenq;  // as fftSpecialInv
             for (uint32_t j = 0; j < lenh; ++j) {
-                uint64_t idx = (t.rot[j] % lenq) * M / lenq;
+                uint64_t idx = (t.rot[j] & (lenq - 1)) * step;
                 std::complex<double> u = v[i + j];
                 std::complex<double> w = v[i + j + lenh] * t.ksi[idx];
                 v[i + j] = u + w;
