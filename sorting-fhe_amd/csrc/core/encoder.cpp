@@ -82,20 +82,36 @@ void fftSpecialInv(std::complex<double>* v, uint32_t size, const FFTTables& t) {
 void fftSpecial(std::complex<double>* v, uint32_t size, const FFTTables& t) {
     const uint64_t M = 2ull * t.n;
     bitReverse(v, size);
-    for (uint32_t len = 2; len <= size; len <<= 1) {
-        for (uint32_t i = 0; i < size; i += len) {
-            uint32_t lenh = len >> 1;
-            uint64_t lenq = (uint64_t)len << 2;
-            const uint64_t step = M / lenq;  // as fftSpecialInv
-            for (uint32_t j = 0; j < lenh; ++j) {
+    // butterflies j0 <= j < j1 of every block of stage `len` in [lo, hi)
+    auto stage = [&](uint32_t len, uint32_t lo, uint32_t hi, uint32_t j0, uint32_t j1) {
+        const uint32_t lenh = len >> 1;
+        const uint64_t lenq = (uint64_t)len << 2;
+        const uint64_t step = M / lenq;  // as fftSpecialInv
+        for (uint32_t i = lo; i < hi; i += len)
+            for (uint32_t j = j0; j < j1; ++j) {
                 uint64_t idx = (t.rot[j] & (lenq - 1)) * step;
                 std::complex<double> u = v[i + j];
                 std::complex<double> w = v[i + j + lenh] * t.ksi[idx];
                 v[i + j] = u + w;
                 v[i + j + lenh] = u - w;
             }
+    };
+    // Large decodes (the debug prints' 32 768-slot decryptions) on 16 host
+    // threads: the stages inside blocks of size/16 run per block, the last
+    // four stages split each block's butterflies.  Every butterfly computes
+    // what the sequential loop computes, so the values are identical.
+    const uint32_t T = size >= 8192 ? 16 : 1, B = size / T;
+    if (T > 1) {
+        ParallelFor(T, [&](size_t b) {
+            for (uint32_t len = 2; len <= B; len <<= 1) stage(len, (uint32_t)b * B, (uint32_t)(b + 1) * B, 0, len >> 1);
+        }, 1);
+        for (uint32_t len = 2 * B; len <= size; len <<= 1) {
+            const uint32_t lenh = len >> 1, part = lenh / T;
+            ParallelFor(T, [&](size_t p) { stage(len, 0, size, (uint32_t)p * part, (uint32_t)(p + 1) * part); }, 1);
         }
+        return;
     }
+    for (uint32_t len = 2; len <= size; len <<= 1) stage(len, 0, size, 0, len >> 1);
 }
 
 }  // namespace
