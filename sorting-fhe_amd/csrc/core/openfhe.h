@@ -684,15 +684,20 @@ inline std::ostream& operator<<(std::ostream& os, const std::vector<double>& v) 
         for (size_t i = 0; i < v.size(); ++i) os << (i ? ", " : "") << v[i];
         return os << "]";
     }
-    std::string out;
-    out.reserve(v.size() * 14 + 2);
-    out += '[';
-    char b[64];
-    for (size_t i = 0; i < v.size(); ++i) {
-        if (i) out += ", ";
-        const auto r = std::to_chars(b, b + sizeof b, v[i], std::chars_format::general, 6);
-        out.append(b, r.ptr);
-    }
-    out += ']';
-    return os.write(out.data(), (std::streamsize)out.size());
+    // (long vectors: 16 slices formatted on host threads, written in order)
+    const size_t T = v.size() >= 4096 ? 16 : 1, per = (v.size() + T - 1) / T;
+    std::vector<std::string> parts(T);
+    lbcrypto::ParallelFor(T, [&](size_t p) {
+        std::string& out = parts[p];
+        out.reserve(per * 14 + 2);
+        char b[64];
+        for (size_t i = p * per; i < std::min(v.size(), (p + 1) * per); ++i) {
+            if (i) out += ", ";
+            const auto r = std::to_chars(b, b + sizeof b, v[i], std::chars_format::general, 6);
+            out.append(b, r.ptr);
+        }
+    }, 1);
+    os.put('[');
+    for (const auto& part : parts) os.write(part.data(), (std::streamsize)part.size());
+    return os.put(']');
 }
