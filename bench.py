@@ -442,9 +442,9 @@ def main(argv=None):
     x = input_vector(N)
     ct = eng.encrypt(x.tolist())  # input resident in HBM before timing
 
-    families = ("ntt", "conv", "ks_inner")
+    families = ("ntt", "conv", "ks_inner", "ntt_ks")
     kernel_name = {"ntt": "k_ntt (both passes, fwd+inv)", "conv": "k_convf / k_mdrsf",
-                   "ks_inner": "k_ks_inner"}
+                   "ks_inner": "k_ks_inner", "ntt_ks": "k_ntt_ks (ModUp ROW pass + key inner product)"}
 
     def step():
         out = sorter.sort(ct, *cfg)
@@ -463,8 +463,10 @@ def main(argv=None):
     # profiling leg (after the timed region): one sort with the lanes
     # serialised on one stream and every launch of each family bracketed by
     # HIP events on that stream -- per-launch durations as rocprofv3 measures
-    # them (no other lane's kernels inside a timed interval)
+    # them (no other lane's kernels inside a timed interval; the batches'
+    # stacked launches are timed as issued, a merged pair as one launch)
     graph_nodes = sorter.graph_nodes()
+    stk0 = eng.stack_stats()
     eng.sync()
     os.environ["SFHE_GRAPH"] = "0"  # per-launch timing needs the eager path
     eng.serialize_lanes(True)
@@ -476,6 +478,7 @@ def main(argv=None):
     eng.sync()
     serial_ms = (time.perf_counter() - t0) * 1e3
     stats = eng.op_stats()  # the SURVEY §8(d) byte model over one (eager) sort
+    stk1 = eng.stack_stats()
     kt = {fam: eng.kernel_timing_read(fam) for fam in families}
     for fam in families:
         eng.kernel_timing(fam, 0)
@@ -583,6 +586,9 @@ def main(argv=None):
         "graph": {"replayed": graph_nodes > 0, "nodes": graph_nodes,
                   "note": "timed steps replay the sort as one hipGraph (captured during warmup; "
                           "SFHE_GRAPH=0 runs them eagerly)"},
+        "stacked": {"merged_pairs_per_sort": stk1[0] - stk0[0], "alone_per_sort": stk1[1] - stk0[1],
+                    "note": "the batches' identical ops issued as one launch (prims.h sfp_stack_*); "
+                            "counted over the profiling sort's stacked regions (SFHE_STACK_BATCHES=0: off)"},
         "roofline": roofline,
         "kernels": kernels,
         "trials": trials,

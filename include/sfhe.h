@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define SFHE_ABI_VERSION 1
+#define SFHE_ABI_VERSION 2  /* bumped when a declaration or struct below changes */
 
 #define SFHE_OK 0
 #define SFHE_EINVAL (-1)   /* bad argument */
@@ -110,12 +110,17 @@ int sfhe_live_contexts(void);
 #define SFHE_KFAM_NTT 0
 #define SFHE_KFAM_CONV 1
 #define SFHE_KFAM_KSINNER 2
+#define SFHE_KFAM_NTTKS 3   /* k_ntt_ks: ModUp's ROW pass fused with the key inner product */
 int sfhe_kernel_timing(sfhe_ctx* c, uint32_t family, uint32_t period);
 int sfhe_kernel_timing_read(sfhe_ctx* c, uint32_t family, uint64_t* launches, uint64_t* timed,
                             double* ms, double* bytes);
 /* on != 0: all of the context's lanes (streams) issue on one stream, so timed
  * launches run alone, as under rocprofv3 (bench profiling leg; slower). */
 int sfhe_serialize_lanes(sfhe_ctx* c, int on);
+/* Stacked launches so far (no reference counterpart; prims.h sfp_stack_*):
+ * the sort's two batches issue their identical ops as one launch each --
+ * `merged` such pairs, `single` launches issued alone inside stacked regions. */
+int sfhe_stack_stats(sfhe_ctx* c, uint64_t* merged, uint64_t* single);
 
 /* ---- encryption ------------------------------------------------------------
  * Replaces Encryption::encryptInput (encryption.cpp:5-12, MakeCKKSPacked-

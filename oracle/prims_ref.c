@@ -149,6 +149,14 @@ int sfp_graph_family_time(sfp_dev* d, sfp_graph* g, uint32_t fam, int reps, doub
     return -1;
 }
 void sfp_serialize(sfp_dev* d, int on) { (void)d; (void)on; }
+/* one synchronous lane: nothing to stack */
+void sfp_stack_begin(sfp_dev* d) { (void)d; }
+void sfp_stack_end(sfp_dev* d) { (void)d; }
+void sfp_stack_stats(sfp_dev* d, uint64_t* merged, uint64_t* single) {
+    (void)d;
+    if (merged) *merged = 0;
+    if (single) *single = 0;
+}
 /* no graphs: the host layer runs every region eagerly */
 int sfp_capture_begin(sfp_dev* d) { (void)d; return -1; }
 void sfp_clear_error(sfp_dev* d) { (void)d; }

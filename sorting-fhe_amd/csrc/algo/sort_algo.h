@@ -185,6 +185,17 @@ struct BatchSplit {
     }
 };
 
+// The batches of a sort phase run the same op sequence on their lanes: as
+// stacked launches (one launch per op for both batches, ForkLanes(k, true))
+// unless SFHE_STACK_BATCHES=0 (then two streams that overlap on the device).
+inline bool stackBatches() {
+    static const bool on = [] {
+        const char* v = std::getenv("SFHE_STACK_BATCHES");
+        return !v || *v != '0';
+    }();
+    return on;
+}
+
 // Placement evaluates the doubled sinc in the rebased variable (on unless
 // SFHE_SINC_REBASE=0; see rotationIndexCheckN).
 inline bool sincRebase() {
@@ -437,7 +448,7 @@ class DirectSort : public SortBase<N> {
         std::vector<Ciphertext<DCRTPoly>> parts(L.B);
         const sfhe::BatchSplit split(m_cc, L.B);
         const int lanes = std::min((int)split.mine.size(), m_cc->LaneCount());
-        if (lanes > 1) m_cc->ForkLanes(lanes);  // (one batch: no region, the PS may open its own)
+        if (lanes > 1) m_cc->ForkLanes(lanes, sfhe::stackBatches());  // (one batch: no region, the PS may open its own)
         sfhe::parallelLanes(m_cc, lanes, (int)split.mine.size(), [&](int i) {
             const int b = split.mine[i];
             auto shifted = vecRotsOpt(pre, L.P, L.S, L.npRank, b);
@@ -514,7 +525,7 @@ class DirectSort : public SortBase<N> {
         std::vector<Ciphertext<DCRTPoly>> parts(L.B);
         const sfhe::BatchSplit split(m_cc, L.B);
         const int lanes = std::min((int)split.mine.size(), m_cc->LaneCount());
-        if (lanes > 1) m_cc->ForkLanes(lanes);  // (one batch: no region, the PS may open its own)
+        if (lanes > 1) m_cc->ForkLanes(lanes, sfhe::stackBatches());  // (one batch: no region, the PS may open its own)
         sfhe::parallelLanes(m_cc, lanes, (int)split.mine.size(), [&](int i) {
             const int b = split.mine[i];
             Plaintext chk = maskMemo({3, b, 0, (int)indexMinusRank->GetLevel(), L.S}, [&](auto& v) {
@@ -640,7 +651,7 @@ class DirectSort : public SortBase<N> {
         }
         std::vector<Ciphertext<DCRTPoly>> Masked(num_batch);
         const int lanes = std::min((int)num_batch, m_cc->LaneCount());
-        m_cc->ForkLanes(lanes);
+        m_cc->ForkLanes(lanes, sfhe::stackBatches());
         sfhe::parallelLanes(m_cc, lanes, (int)num_batch, [&](int bi) {
             const size_t b = (size_t)bi;
             // subMask_b[i M + j] = subScale (b M + i) (reference :1089-1098, :929-939)

@@ -772,6 +772,14 @@ int sfhe_serialize_lanes(sfhe_ctx* c, int on) {
     });
 }
 
+int sfhe_stack_stats(sfhe_ctx* c, uint64_t* merged, uint64_t* single) {
+    REQUIRE(c, "null context");
+    return guard([&] {
+        OpLock g(c->cc->state());
+        sfp_stack_stats(c->cc->state()->dev, merged, single);
+    });
+}
+
 int sfhe_kernel_timing_read(sfhe_ctx* c, uint32_t family, uint64_t* launches, uint64_t* timed,
                             double* ms, double* bytes) {
     REQUIRE(c, "null context");

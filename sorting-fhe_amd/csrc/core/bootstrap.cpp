@@ -464,6 +464,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::bootstrapReplay(const Cipherte
         } catch (...) {
             EndCapture(nullptr);
             r.off = true;
+            r.in.reset();  // (its cc would tie the context to its own replay table)
             throw;
         }
         r.g = EndCapture(out);

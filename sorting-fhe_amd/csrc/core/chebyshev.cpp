@@ -423,15 +423,24 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalChebyshevSeriesPS(
             lanes = std::min(psLanes, LaneCount());
             lanes = lanes >= 4 ? 4 : (lanes >= 2 ? 2 : 1);
         }
-        if (lanes > 1) ForkLanes(lanes);
+        // the lane region is closed on every exit, an exception included
+        struct LaneRegion {
+            CryptoContextImpl<DCRTPoly>* cc;
+            int lanes;
+            LaneRegion(CryptoContextImpl<DCRTPoly>* c, int k) : cc(c), lanes(k) {
+                if (lanes > 1) cc->ForkLanes(lanes);
+            }
+            ~LaneRegion() {
+                if (lanes > 1) {
+                    cc->SetLane(0);
+                    cc->JoinLanes();
+                }
+            }
+        } region(this, lanes);
         PSEvaluator ps(this, y, l, D);
         static const bool batched = std::getenv("SFHE_PS_UNBATCHED") == nullptr;
         if (batched) ps.precomputeLeaves(p, D);
         auto v = ps.eval(p, D, 0, 0, lanes);
-        if (lanes > 1) {
-            SetLane(0);
-            JoinLanes();
-        }
         out = v.isConst ? EvalAdd(EvalMult(y, 0.0), v.c) : v.ct;
     }
     const uint32_t target = y->GetLevel() + D;

@@ -1102,13 +1102,19 @@ class SfheInternal {
     static uint64_t encHash(const Plaintext& pt, uint32_t level) {
         uint64_t h = 1469598103934665603ull;
         auto mix = [&](uint64_t x) { h = (h ^ x) * 1099511628211ull; };
-        const uint64_t* wv = reinterpret_cast<const uint64_t*>(pt->values.data());
+        // the doubles' words are read with memcpy (no type-punned loads)
+        const char* wv = reinterpret_cast<const char*>(pt->values.data());
         const size_t nw = 2 * pt->values.size();
+        auto word = [wv](size_t i) {
+            uint64_t x;
+            std::memcpy(&x, wv + 8 * i, 8);
+            return x;
+        };
         uint64_t ln[4] = {h, h ^ 1, h ^ 2, h ^ 3};
         size_t i = 0;
         for (; i + 4 <= nw; i += 4)
-            for (int k = 0; k < 4; ++k) ln[k] = (ln[k] ^ wv[i + k]) * 1099511628211ull;
-        for (; i < nw; ++i) ln[0] = (ln[0] ^ wv[i]) * 1099511628211ull;
+            for (int k = 0; k < 4; ++k) ln[k] = (ln[k] ^ word(i + k)) * 1099511628211ull;
+        for (; i < nw; ++i) ln[0] = (ln[0] ^ word(i)) * 1099511628211ull;
         for (int k = 0; k < 4; ++k) mix(ln[k]);
         mix(pt->slots);
         mix(level);
@@ -1499,6 +1505,16 @@ struct DeferredRelin : DeferredOp {
 static std::atomic<int> g_liveContexts{0};
 int CryptoContextImpl<DCRTPoly>::LiveContexts() { return g_liveContexts.load(); }
 
+void SfheCheckLayout(uint64_t callerStamp) {
+    const uint64_t mine = SfheFacadeLayout();
+    if (callerStamp == mine) return;
+    char b[160];
+    std::snprintf(b, sizeof b, "caller stamp %016llx, library stamp %016llx (facade ABI version %d)",
+                  (unsigned long long)callerStamp, (unsigned long long)mine, SFHE_FACADE_ABI_VERSION);
+    SFHE_THROW(std::string("the engine headers this program was compiled against do not match the library's "
+                           "(object layouts differ; rebuild the program against the installed headers): ") + b);
+}
+
 CryptoContextImpl<DCRTPoly>::CryptoContextImpl(const CCParams<CryptoContextCKKSRNS>& p)
     : st(new SfheContextState) {
     SfheContextState& s = *st;
@@ -1722,7 +1738,7 @@ void CryptoContextImpl<DCRTPoly>::Synchronize() {
 // a sharded context issues its collectives in program order on one lane
 int CryptoContextImpl<DCRTPoly>::LaneCount() const { return st->sharded ? 1 : sfp_lanes(st->dev); }
 
-void CryptoContextImpl<DCRTPoly>::ForkLanes(int count) {
+void CryptoContextImpl<DCRTPoly>::ForkLanes(int count, bool stacked) {
     OpLock g(st.get());
     SfheContextState* s = st.get();
     if (s->forkedLanes) SFHE_THROW("ForkLanes: a lane region is already open");
@@ -1739,6 +1755,7 @@ void CryptoContextImpl<DCRTPoly>::ForkLanes(int count) {
     }
     s->forkedLanes = count;
     s->region = ++s->regionCount;
+    if (stacked && count > 1) sfp_stack_begin(s->dev);
 }
 
 void CryptoContextImpl<DCRTPoly>::SetLane(int lane) {
@@ -1762,6 +1779,7 @@ void CryptoContextImpl<DCRTPoly>::JoinLanes() {
                      (unsigned long long)s->regionDepWaits);
         s->regionDepWaits = 0;
     }
+    sfp_stack_end(s->dev);  // (a stacked region: its launches are issued now, on lane 0)
     for (int i = 1; i < s->forkedLanes; ++i) s->laneWait(0, i);
     sfp_set_lane(s->dev, 0);
     std::lock_guard<std::mutex> pg(s->poolMu);

@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <charconv>
 #include <complex>
+#include <cstddef>
 #include <locale>
 #include <fstream>
 #include <cstdint>
@@ -534,7 +535,10 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
                 std::vector<DeviceBufferPtr>& keep);
     // raw residues [c0 rows][c1 rows] of every limb, natural order (collective when sharded)
     void DownloadRows(const Ciphertext<DCRTPoly>& ct, uint64_t* out);
-    void ForkLanes(int count);
+    // stacked: the region's lanes are issued as stacked launches (prims.h
+    // sfp_stack_begin): identical ops of different lanes become one launch;
+    // JoinLanes issues them.  For lanes that run the same op sequence.
+    void ForkLanes(int count, bool stacked = false);
     void SetLane(int lane);
     void JoinLanes();
     // Plaintext-encoding cache across calls (default on); see DESIGN.md.
@@ -588,7 +592,62 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
 // their context by its parameter fingerprint, as OpenFHE's static key maps do).
 void RegisterCryptoContext(const CryptoContext<DCRTPoly>& cc);
 
+// ---------------------------------------------------------------------------
+// Layout stamp: the ABI handshake between a caller and the library.  Callers
+// compile the classes above into their own objects (inline accessors, field
+// reads, make_shared), so a caller built against headers other than the
+// library's reads and writes them at the wrong offsets: silent heap
+// corruption (two reference-harness programs built against older headers
+// aborted in malloc this way).  The stamp hashes the version, the
+// size and alignment of every class defined here, the offset of every public
+// field and the sizes of the standard-library types inside them (a different
+// libstdc++ ABI or _GLIBCXX_DEBUG changes those); GenCryptoContext hands the
+// caller's stamp to the library, which throws OpenFHEException on a mismatch.
+// SFHE_LAYOUT_SALT exists only for the test that builds a deliberately
+// mismatched caller (tests/test_abi_stamp.py).
+#define SFHE_FACADE_ABI_VERSION 5
+#ifndef SFHE_LAYOUT_SALT
+#define SFHE_LAYOUT_SALT 0
+#endif
+#pragma GCC diagnostic push
+#pragma GCC diagnostic ignored "-Winvalid-offsetof"
+inline uint64_t SfheFacadeLayout() {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&h](uint64_t x) { h = (h ^ x) * 1099511628211ull; };
+    using Ct = CiphertextImpl<DCRTPoly>;
+    using Pk = PublicKeyImpl<DCRTPoly>;
+    using Sk = PrivateKeyImpl<DCRTPoly>;
+    using Cc = CryptoContextImpl<DCRTPoly>;
+    const uint64_t v[] = {
+        SFHE_FACADE_ABI_VERSION, SFHE_LAYOUT_SALT,
+        sizeof(std::string), sizeof(std::mutex), sizeof(std::shared_ptr<int>), sizeof(std::vector<int>),
+        sizeof(std::map<int, int>), sizeof(std::set<int>), sizeof(std::function<void()>), sizeof(std::complex<double>),
+        sizeof(CCParams<CryptoContextCKKSRNS>), alignof(CCParams<CryptoContextCKKSRNS>),
+        sizeof(EncodingParamsImpl), sizeof(KeyPair<DCRTPoly>),
+        sizeof(PlaintextImpl), alignof(PlaintextImpl), offsetof(PlaintextImpl, values), offsetof(PlaintextImpl, slots),
+        offsetof(PlaintextImpl, level), offsetof(PlaintextImpl, length), offsetof(PlaintextImpl, logPrecision),
+        offsetof(PlaintextImpl, logError), offsetof(PlaintextImpl, realCache), offsetof(PlaintextImpl, encoded),
+        offsetof(PlaintextImpl, encMutex),
+        sizeof(Ct), alignof(Ct), offsetof(Ct, cc), offsetof(Ct, buf), offsetof(Ct, c0), offsetof(Ct, c1),
+        offsetof(Ct, level), offsetof(Ct, slots), offsetof(Ct, scale), offsetof(Ct, def), offsetof(Ct, pend),
+        offsetof(Ct, undo), sizeof(Ct::CaptureUndo),
+        sizeof(Pk), offsetof(Pk, b), offsetof(Pk, a), offsetof(Pk, cc), offsetof(Pk, tag),
+        sizeof(Sk), offsetof(Sk, s), offsetof(Sk, ternary), offsetof(Sk, cc), offsetof(Sk, tag),
+        sizeof(FastRotationPrecomp), offsetof(FastRotationPrecomp, ext), offsetof(FastRotationPrecomp, level),
+        offsetof(FastRotationPrecomp, pend), offsetof(FastRotationPrecomp, beta), offsetof(FastRotationPrecomp, stride),
+        offsetof(FastRotationPrecomp, pinBuf), offsetof(FastRotationPrecomp, pinC0),
+        sizeof(Cc), alignof(Cc), sizeof(Cc::OpStats), sizeof(Cc::BootstrapTap),
+    };
+    for (uint64_t x : v) mix(x);
+    return h;
+}
+#pragma GCC diagnostic pop
+// Library side: throws OpenFHEException unless callerStamp is the library's
+// own SfheFacadeLayout() (context.cpp).
+void SfheCheckLayout(uint64_t callerStamp);
+
 inline CryptoContext<DCRTPoly> GenCryptoContext(const CCParams<CryptoContextCKKSRNS>& p) {
+    SfheCheckLayout(SfheFacadeLayout());
     auto cc = std::make_shared<CryptoContextImpl<DCRTPoly>>(p);
     RegisterCryptoContext(cc);
     return cc;

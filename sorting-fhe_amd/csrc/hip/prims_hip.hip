@@ -22,7 +22,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <memory>
 #include <mutex>
+#include <unordered_set>
 #include <unordered_map>
 #include <string>
 #include <type_traits>
@@ -82,6 +85,22 @@ __device__ __forceinline__ void macc(Acc& a, u64 x, u64 y) {
 struct sfp_event {
     hipEvent_t e = nullptr;
     int lane = 0;
+    uint64_t recId = 0;  // inside a stacked region: id of its latest (deferred) record
+};
+
+// One deferred item of a stacked region (sfp_stack_begin): a launch, or an
+// event record / wait of a lane, issued in order by stackFlush.
+struct StackRec {
+    enum Kind : uint8_t { LAUNCH, EV_RECORD, EV_WAIT };
+    Kind kind = LAUNCH;
+    uint32_t cls = 0;  // merge class (STK_*; 0: always issued alone)
+    uint64_t key = 0;  // two heads of one class and key may become one launch
+    uint64_t id = 0;   // EV_RECORD: its id; EV_WAIT: the record it waits for (0: one before the region)
+    sfp_event* ev = nullptr;
+    uint32_t fam = ~0u;  // kernel family for live timing (sfp_prof_*), and its algorithmic bytes
+    double bytes = 0;
+    std::function<void(hipStream_t)> go;  // the launch on its own
+    std::shared_ptr<void> pay;            // class payload (what stackMerge reads of both)
 };
 
 // A captured graph and the device arena its launches read their small
@@ -107,7 +126,18 @@ struct sfp_dev {
     hipStream_t streams[SFP_MAX_LANES] = {};
     int nLanes = 1, cur = 0;
     bool serial = false;  // sfp_serialize: every lane on streams[0]
-    hipStream_t st() const { return streams[serial ? 0 : cur]; }
+    // stacked region (sfp_stack_begin): every lane's launches are recorded in
+    // stack[lane] and issued by stackFlush on streams[0]; uploads and other
+    // immediate stream work go to streams[0] directly (before the deferred
+    // launches that read them)
+    bool stackOn = false;
+    std::vector<StackRec> stack[SFP_MAX_LANES];
+    uint64_t recSeq = 0;
+    std::vector<sfp_event*> stackFreedEv;  // freed inside the region: reusable after the flush
+    uint64_t stkMerged = 0, stkSingle = 0;  // launches issued as merged pairs / alone
+    uint32_t stkFam = ~0u;  // timedLaunch's family while it records (stacked)
+    double stkBytes = 0;
+    hipStream_t st() const { return streams[(serial || stackOn) ? 0 : cur]; }
     std::vector<sfp_event*> evFree;
     std::mutex evMu;  // evFree: buffers release events from any host thread
     uint32_t n = 0, logn = 0, np = 0;
@@ -211,8 +241,30 @@ static void captureFail(sfp_dev* d, const char* why) {
     }
 }
 
+static void stackFlush(sfp_dev* d);
+
+// A launch on the current lane: issued now, or recorded for the stacked
+// region's flush (`launch` captures its arguments by value).
+static void issue(sfp_dev* d, std::function<void(hipStream_t)>&& launch) {
+    if (!d->stackOn) return launch(d->st());
+    StackRec r;
+    r.go = std::move(launch);
+    r.fam = d->stkFam;
+    r.bytes = d->stkBytes;
+    d->stack[d->cur].push_back(std::move(r));
+}
+static void issueRec(sfp_dev* d, StackRec&& r) {
+    if (!d->stackOn) return r.go(d->st());
+    r.fam = d->stkFam;
+    r.bytes = d->stkBytes;
+    d->stack[d->cur].push_back(std::move(r));
+}
+#define SFP_GO(kern, grid, block, ...) \
+    issue(d, [=](hipStream_t s_) { hipLaunchKernelGGL(kern, grid, block, 0, s_, __VA_ARGS__); })
+
 // Drain every lane (shared host-visible resources: ring, bounce, constant pool).
 static void syncAll(sfp_dev* d) {
+    stackFlush(d);
     if (d->capture) return captureFail(d, "host synchronisation inside the captured region");
     for (int i = 0; i < d->nLanes; ++i) {
         hipError_t e = hipStreamSynchronize(d->streams[i]);
@@ -231,7 +283,7 @@ static bool debugSync() {
 static void checkLaunch(sfp_dev* d, const char* k) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) record(d, k, e);
-    if (debugSync() && !d->capture) {
+    if (debugSync() && !d->capture && !d->stackOn) {
         e = hipStreamSynchronize(d->st());
         if (e != hipSuccess) record(d, k, e);
     }
@@ -281,6 +333,14 @@ static void profFlush(sfp_dev* d, sfp_dev::ProfFam& f) {
 template <class F>
 static void timedLaunch(sfp_dev* d, uint32_t fam, double bytes, F&& launch) {
     sfp_dev::ProfFam& f = d->prof[fam];
+    if (d->stackOn) {  // recorded: stackFlush times it as issued
+        d->stkFam = fam;
+        d->stkBytes = bytes;
+        launch();
+        d->stkFam = ~0u;
+        d->stkBytes = 0;
+        return;
+    }
     if (d->capture || !f.period || (f.seen++ % f.period) != 0) {
         launch();
         return;
@@ -653,6 +713,18 @@ struct RowGroup {
     const u64 *k, *kS, *k2, *k2S, *liftSub, *preK, *preKS, *emK, *emKS;
 };
 
+// Stacked launches (sfp_stack_begin): NG independent argument sets in one
+// launch, blockIdx.y < split -> set 0, the rest -> set 1 (rows renumbered
+// from 0).  Two lanes' identical ops (the sort's batches) become one launch
+// with the rows of both; NG = 1 is the ordinary launch.
+template <class T, int NG>
+struct ArgSet {
+    T a[NG];
+    uint32_t split;  // grid rows of set 0
+};
+template <int NG>
+using RowGroupSet = ArgSet<RowGroup, NG>;
+
 __device__ __forceinline__ u64* rowAt(const RowPtr& r, uint32_t p, uint32_t i) {
     return const_cast<u64*>(r.base) + p * r.ps + i * r.is;
 }
@@ -673,8 +745,8 @@ __device__ unsigned long long g_nttTrace[kTraceSlots][4][8];
 #define NTT_MARK(i)
 #endif
 
-template <bool INV, bool COL, int LE, int TILE>
-__global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_barrett* __restrict__ bar,
+template <bool INV, bool COL, int LE, int TILE, int NG = 1>
+__global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroupSet<NG> GS, const sf_barrett* __restrict__ bar,
                                                   const u64* __restrict__ tw, const u64* __restrict__ twS,
                                                   const u64* __restrict__ ninv,
                                                   const u64* __restrict__ ninvS, uint32_t logn,
@@ -690,7 +762,9 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroup G, const sf_b
     constexpr bool FIRST = (COL != INV);  // forward: COL first; inverse: ROW first
     const uint32_t n = 1u << logn;
     const uint32_t logR = logn - 8;
-    const uint32_t rid = blockIdx.y;
+    const uint32_t gsel = (NG > 1 && blockIdx.y >= GS.split) ? 1u : 0u;
+    const RowGroup& G = GS.a[gsel];
+    const uint32_t rid = blockIdx.y - (gsel ? GS.split : 0u);
     const uint32_t pp = rid / G.R, ii = rid % G.R;
     if (G.skipEll && ii >= G.alpha * pp && ii < min(G.alpha * (pp + 1), G.skipEll)) return;
     const uint32_t prime = primeOf(G.pm, ii);
@@ -1096,8 +1170,8 @@ struct KsArgs {
     const double* itwD;
 };
 
-template <int LE, int TILE>
-__global__ __launch_bounds__(TILE >> LE) void k_ntt_ks(const KsArgs A, const sf_barrett* __restrict__ bar,
+template <int LE, int TILE, int NG = 1>
+__global__ __launch_bounds__(TILE >> LE) void k_ntt_ks(const ArgSet<KsArgs, NG> AS, const sf_barrett* __restrict__ bar,
                                                      const u64* __restrict__ tw, const u64* __restrict__ twS,
                                                      uint32_t logn, const double* __restrict__ twD,
                                                      const double* __restrict__ qinvD, int useFp) {
@@ -1106,7 +1180,9 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt_ks(const KsArgs A, const sf_
     constexpr int NPAIR = (1 << LE) / 2;  // 16-byte pairs per thread
     const uint32_t n = 1u << logn;
     const uint32_t logR = logn - 8;
-    const uint32_t t = blockIdx.y;
+    const uint32_t asel = (NG > 1 && blockIdx.y >= AS.split) ? 1u : 0u;
+    const KsArgs& A = AS.a[asel];
+    const uint32_t t = blockIdx.y - (asel ? AS.split : 0u);
     const uint32_t prime = t < A.ell ? t : A.Lq + (t - A.ell);
     const sf_barrett B = loadBar(bar, prime);
     const u64 q = B.q;
@@ -2074,7 +2150,7 @@ struct MdrsJob {
     u64* dst;        // l rows
 };
 struct MdrsArgs {
-    MdrsJob j[2];
+    MdrsJob j[4];  // blockIdx.y: two polys, or two stacked launches' four
     const uint32_t* sidx;
     const u64 *inv, *mod, *sprod;  // the ModDown conversion table (targets 0..)
     const u64 *pmod, *lsub;        // P mod q_t, q_l mod q_t
@@ -2478,6 +2554,211 @@ __global__ __launch_bounds__(kThreads) void k_fill1(unsigned char* __restrict__ 
 // ============================================================================
 // host side
 
+// ============================================================================
+// Stacked launches (sfp_stack_begin / sfp_stack_end)
+//
+// Inside a stacked region every lane's launches, event records and event
+// waits are recorded per lane instead of issued.  stackFlush then issues them
+// all on streams[0]: each lane's items in that lane's order, a wait only after
+// the record it names, and -- whenever two lanes' next launches are the same
+// kernel over different rows (the sort's two batches run the same op
+// sequence, reference src/sort_algo.h:438-455, 713-742) -- those two as ONE
+// launch whose grid holds the rows of both (ArgSet<T, 2>), or whose job table
+// holds the jobs of both (conversions).  Per-row arithmetic is unchanged, so
+// results are bit-identical; the sort issues about half the launches.
+enum { STK_NONE = 0, STK_NTT = 1, STK_KS = 2, STK_CONV = 3, STK_MDRS = 4 };
+
+static uint64_t stkKey(const void* kern, uint32_t a, uint32_t b) {
+    uint64_t h = 1469598103934665603ull;
+    for (uint64_t x : {(uint64_t)(uintptr_t)kern, (uint64_t)a, (uint64_t)b}) h = (h ^ x) * 1099511628211ull;
+    return h;
+}
+
+using NttKern2 = void (*)(RowGroupSet<2>, const sf_barrett*, const u64*, const u64*, const u64*, const u64*,
+                          uint32_t, const double*, const double*, const double*, const double*, int);
+struct NttPay {
+    RowGroup G;
+    uint32_t rows;
+    dim3 g;
+    int threads, useFp;
+    NttKern2 k2;
+    const u64 *tw, *twS;
+    const double* twD;
+};
+using KsKern2 = void (*)(ArgSet<KsArgs, 2>, const sf_barrett*, const u64*, const u64*, uint32_t, const double*,
+                         const double*, int);
+struct KsPay {
+    KsArgs a;
+    uint32_t rows;
+    dim3 g;
+    int threads, useFp;
+    KsKern2 k2;
+};
+using ConvKern = void (*)(ConvJobs, const sf_barrett*, const double*, uint32_t);
+struct ConvPay {
+    ConvJobs J;
+    uint32_t njobs;
+    dim3 g;
+    ConvKern k;
+};
+struct MdrsPay {
+    MdrsArgs M;  // (memset before filling: compared bytewise outside its jobs)
+    dim3 g;
+    ConvKern k;  // (same signature with MdrsArgs: stored through MdrsKern)
+};
+using MdrsKern = void (*)(MdrsArgs, const sf_barrett*, const double*, uint32_t);
+
+// Issue the heads a and b (same class and key) as one launch on s; false if
+// their arguments cannot share one (the caller then issues them apart);
+// check: only report whether they can.
+static bool stackMerge(sfp_dev* d, const StackRec& a, const StackRec& b, hipStream_t s, bool check) {
+    switch (a.cls) {
+        case STK_NTT: {
+            const auto& A = *static_cast<const NttPay*>(a.pay.get());
+            const auto& B = *static_cast<const NttPay*>(b.pay.get());
+            if (!A.k2 || A.rows + B.rows > 65535u || A.g.x != B.g.x || A.useFp != B.useFp) return false;
+            if (check) return true;
+            RowGroupSet<2> GS;
+            GS.a[0] = A.G;
+            GS.a[1] = B.G;
+            GS.split = A.rows;
+            hipLaunchKernelGGL(A.k2, dim3(A.g.x, A.rows + B.rows), dim3(A.threads), 0, s, GS, d->bar, A.tw, A.twS,
+                               d->ninv, d->ninvS, d->logn, A.twD, d->qinvD, d->ninvD, d->ninvQ, A.useFp);
+            return true;
+        }
+        case STK_KS: {
+            const auto& A = *static_cast<const KsPay*>(a.pay.get());
+            const auto& B = *static_cast<const KsPay*>(b.pay.get());
+            if (!A.k2 || A.rows + B.rows > 65535u || A.g.x != B.g.x || A.useFp != B.useFp) return false;
+            if (check) return true;
+            ArgSet<KsArgs, 2> AS;
+            AS.a[0] = A.a;
+            AS.a[1] = B.a;
+            AS.split = A.rows;
+            hipLaunchKernelGGL(A.k2, dim3(A.g.x, A.rows + B.rows), dim3(A.threads), 0, s, AS, d->bar, d->psi,
+                               d->psiS, d->logn, d->psiD, d->qinvD, A.useFp);
+            return true;
+        }
+        case STK_CONV: {
+            const auto& A = *static_cast<const ConvPay*>(a.pay.get());
+            const auto& B = *static_cast<const ConvPay*>(b.pay.get());
+            if (A.k != B.k || A.njobs + B.njobs > (uint32_t)kMaxConvJobs || A.g.x != B.g.x) return false;
+            if (check) return true;
+            ConvJobs J = A.J;
+            for (uint32_t k = 0; k < B.njobs; ++k) J.j[A.njobs + k] = B.J.j[k];
+            hipLaunchKernelGGL(A.k, dim3(A.g.x, A.njobs + B.njobs, std::max(A.g.z, B.g.z)), dim3(kThreads), 0, s, J,
+                               d->bar, d->qinvD, d->logn);
+            return true;
+        }
+        case STK_MDRS: {
+            const auto& A = *static_cast<const MdrsPay*>(a.pay.get());
+            const auto& B = *static_cast<const MdrsPay*>(b.pay.get());
+            if (A.k != B.k || A.g.y + B.g.y > 4u || A.g.x != B.g.x || A.g.z != B.g.z) return false;
+            MdrsArgs x = A.M, y = B.M;
+            std::memset(x.j, 0, sizeof x.j);
+            std::memset(y.j, 0, sizeof y.j);
+            if (std::memcmp(&x, &y, sizeof x)) return false;  // another table / level
+            if (check) return true;
+            MdrsArgs M = A.M;
+            for (uint32_t k = 0; k < B.g.y; ++k) M.j[A.g.y + k] = B.M.j[k];
+            hipLaunchKernelGGL(reinterpret_cast<MdrsKern>(A.k), dim3(A.g.x, A.g.y + B.g.y, A.g.z), dim3(kThreads), 0,
+                               s, M, d->bar, d->qinvD, d->logn);
+            return true;
+        }
+        default:
+            return false;
+    }
+}
+
+// Issue one launch (or a merged pair) on s, bracketed by HIP events when its
+// family is being timed (sfp_prof_set) and this launch is a sampled one.
+template <class F>
+static void stackTimed(sfp_dev* d, hipStream_t s, uint32_t fam, double bytes, F&& go) {
+    if (fam >= SFP_FAM_COUNT || d->capture) return go();
+    sfp_dev::ProfFam& f = d->prof[fam];
+    if (!f.period || (f.seen++ % f.period) != 0) return go();
+    hipEvent_t a = takeEvent(d), b = takeEvent(d);
+    SFP_CHECK(hipEventRecord(a, s));
+    go();
+    SFP_CHECK(hipEventRecord(b, s));
+    f.pending.push_back({a, b});
+    f.timed++;
+    f.bytes += bytes;
+    if (f.pending.size() >= 8192) profFlush(d, f);
+}
+
+static void stackFlush(sfp_dev* d) {
+    if (!d->stackOn) return;
+    const hipStream_t s = d->streams[0];
+    const int L = d->nLanes;
+    size_t at[SFP_MAX_LANES] = {};
+    std::unordered_set<uint64_t> done;  // records issued so far
+    auto left = [&](int l) { return d->stack[l].size() - at[l]; };
+    auto head = [&](int l) -> StackRec& { return d->stack[l][at[l]]; };
+    auto blocked = [&](int l) {
+        const StackRec& r = head(l);
+        return r.kind == StackRec::EV_WAIT && r.id && !done.count(r.id);
+    };
+    for (;;) {
+        // records and satisfied waits first: they cost nothing and unblock
+        for (bool moved = true; moved;) {
+            moved = false;
+            for (int l = 0; l < L; ++l)
+                while (left(l) && head(l).kind != StackRec::LAUNCH && !blocked(l)) {
+                    const StackRec& r = head(l);
+                    if (r.kind == StackRec::EV_RECORD) {
+                        SFP_CHECK(hipEventRecord(r.ev->e, s));
+                        done.insert(r.id);
+                    } else if (!r.id) {  // an event recorded before the region
+                        SFP_CHECK(hipStreamWaitEvent(s, r.ev->e, 0));
+                    }  // (a record issued above: same stream, already ordered)
+                    ++at[l];
+                    moved = true;
+                }
+        }
+        int cand[SFP_MAX_LANES], nc = 0;
+        for (int l = 0; l < L; ++l)
+            if (left(l) && head(l).kind == StackRec::LAUNCH) cand[nc++] = l;
+        if (!nc) {
+            for (int l = 0; l < L; ++l)
+                if (left(l)) {  // a wait whose record never comes: issue the rest in lane order
+                    record(d, "stacked region: an event wait without its record", hipErrorInvalidValue);
+                    for (int k = 0; k < L; ++k)
+                        for (; left(k); ++at[k])
+                            if (head(k).kind == StackRec::LAUNCH) head(k).go(s);
+                    break;
+                }
+            break;
+        }
+        bool merged = false;
+        for (int i = 0; i < nc && !merged; ++i)
+            for (int j = i + 1; j < nc && !merged; ++j) {
+                const StackRec &a = head(cand[i]), &b = head(cand[j]);
+                if (a.cls && a.cls == b.cls && a.key == b.key && stackMerge(d, a, b, s, true)) {
+                    stackTimed(d, s, a.fam, a.bytes + b.bytes, [&] { stackMerge(d, a, b, s, false); });
+                    ++at[cand[i]];
+                    ++at[cand[j]];
+                    ++d->stkMerged;
+                    merged = true;
+                }
+            }
+        if (merged) continue;
+        // alone: the lane furthest behind (most items left) goes first, which
+        // realigns lanes whose sequences differ by an op (batch 0's offset)
+        int best = cand[0];
+        for (int i = 1; i < nc; ++i)
+            if (left(cand[i]) > left(best)) best = cand[i];
+        const StackRec& r = head(best);
+        stackTimed(d, s, r.fam, r.bytes, [&] { r.go(s); });
+        ++at[best];
+        ++d->stkSingle;
+    }
+    for (int l = 0; l < L; ++l) d->stack[l].clear();
+    std::lock_guard<std::mutex> g(d->evMu);
+    for (sfp_event* e : d->stackFreedEv) d->evFree.push_back(e);
+    d->stackFreedEv.clear();
+}
+
 static unsigned ewGrid(size_t work) {
     size_t g = (work + kThreads - 1) / kThreads;
     if (g > 256 * 16) g = 256 * 16;
@@ -2497,30 +2778,44 @@ static bool dmaCopy() {
     return on;
 }
 
-static void devCopy(sfp_dev* d, void* dst, const void* src, size_t b) {
+// immediate: issued on the stream now even inside a stacked region (host
+// uploads and downloads through the ring / bounce buffers: the deferred
+// launches that read an upload are issued after it on the same stream)
+static void devCopy(sfp_dev* d, void* dst, const void* src, size_t b, bool immediate = false) {
     if (!b) return;
     if (dmaCopy()) {
-        SFP_CHECK(hipMemcpyAsync(dst, src, b, hipMemcpyDefault, d->st()));
+        if (immediate || !d->stackOn)
+            SFP_CHECK(hipMemcpyAsync(dst, src, b, hipMemcpyDefault, d->st()));
+        else
+            issue(d, [=](hipStream_t s_) { hipMemcpyAsync(dst, src, b, hipMemcpyDefault, s_); });
         return;
     }
+    std::function<void(hipStream_t)> go;
     if ((((uintptr_t)dst | (uintptr_t)src | b) & 15) == 0) {
         const size_t cnt = b / 16;
-        hipLaunchKernelGGL(k_copy16, dim3(ewGrid(cnt)), dim3(kThreads), 0, d->st(), (ulonglong2*)dst,
-                           (const ulonglong2*)src, cnt);
+        go = [=](hipStream_t s_) {
+            hipLaunchKernelGGL(k_copy16, dim3(ewGrid(cnt)), dim3(kThreads), 0, s_, (ulonglong2*)dst,
+                               (const ulonglong2*)src, cnt);
+        };
     } else {
-        hipLaunchKernelGGL(k_copy1, dim3(ewGrid(b)), dim3(kThreads), 0, d->st(), (unsigned char*)dst,
-                           (const unsigned char*)src, b);
+        go = [=](hipStream_t s_) {
+            hipLaunchKernelGGL(k_copy1, dim3(ewGrid(b)), dim3(kThreads), 0, s_, (unsigned char*)dst,
+                               (const unsigned char*)src, b);
+        };
     }
+    if (immediate)
+        go(d->st());
+    else
+        issue(d, std::move(go));
     checkLaunch(d, "copy");
 }
 
 static void devZero(sfp_dev* d, void* dst, size_t b) {
     if (!b) return;
     if ((((uintptr_t)dst | b) & 15) == 0) {
-        hipLaunchKernelGGL(k_fill16, dim3(ewGrid(b / 16)), dim3(kThreads), 0, d->st(), (ulonglong2*)dst,
-                           b / 16);
+        SFP_GO(k_fill16, dim3(ewGrid(b / 16)), dim3(kThreads), (ulonglong2*)dst, b / 16);
     } else {
-        hipLaunchKernelGGL(k_fill1, dim3(ewGrid(b)), dim3(kThreads), 0, d->st(), (unsigned char*)dst, b);
+        SFP_GO(k_fill1, dim3(ewGrid(b)), dim3(kThreads), (unsigned char*)dst, b);
     }
     checkLaunch(d, "zero");
 }
@@ -2555,13 +2850,14 @@ static const u64* arenaPut(sfp_dev* d, const void* src, size_t bytes) {
 // current lane (ringPut's rules: the region is reused after a full drain).
 static void ringUpload(sfp_dev* d, void* dst, const void* src, size_t bytes) {
     const size_t span = (bytes + 255) & ~(size_t)255;
+    if (span > d->ringCap) return record(d, "argument ring: upload larger than the ring", hipErrorInvalidValue);
     if (d->ringOff + span > d->ringCap) {
         syncAll(d);
         d->ringOff = 0;
     }
     char* h = d->hring + d->ringOff;
     std::memcpy(h, src, bytes);
-    devCopy(d, dst, h, bytes);
+    devCopy(d, dst, h, bytes, true);
     d->ringOff += span;
 }
 
@@ -2575,6 +2871,10 @@ static void constClear(sfp_dev* d) {
 static void* ringPut(sfp_dev* d, const void* src, size_t bytes) {
     if (d->capture) return const_cast<u64*>(arenaPut(d, src, bytes));
     const size_t span = (bytes + 255) & ~(size_t)255;  // keep entries 256-B aligned
+    if (span > d->ringCap) {  // (would write past the pinned ring) -- callers chunk their uploads
+        record(d, "argument ring: upload larger than the ring", hipErrorInvalidValue);
+        return nullptr;
+    }
     if (d->ringOff + span > d->ringCap) {
         syncAll(d);
         d->ringOff = 0;
@@ -2582,7 +2882,7 @@ static void* ringPut(sfp_dev* d, const void* src, size_t bytes) {
     char* h = d->hring + d->ringOff;
     char* dv = d->dring + d->ringOff;
     std::memcpy(h, src, bytes);  // only the caller's bytes: src may end right there
-    devCopy(d, dv, h, bytes);
+    devCopy(d, dv, h, bytes, true);
     d->ringOff += span;
     return dv;
 }
@@ -2594,7 +2894,7 @@ static void hostToDev(sfp_dev* d, void* dst, const void* src, size_t b) {
     for (size_t off = 0; off < b; off += d->bounceCap) {
         const size_t c = b - off < d->bounceCap ? b - off : d->bounceCap;
         std::memcpy(d->bounce, (const char*)src + off, c);
-        devCopy(d, (char*)dst + off, d->bounce, c);
+        devCopy(d, (char*)dst + off, d->bounce, c, true);
         SFP_CHECK(hipStreamSynchronize(d->st()));
     }
 }
@@ -2604,7 +2904,7 @@ static void devToHost(sfp_dev* d, void* dst, const void* src, size_t b) {
     syncAll(d);
     for (size_t off = 0; off < b; off += d->bounceCap) {
         const size_t c = b - off < d->bounceCap ? b - off : d->bounceCap;
-        devCopy(d, d->bounce, (const char*)src + off, c);
+        devCopy(d, d->bounce, (const char*)src + off, c, true);
         SFP_CHECK(hipStreamSynchronize(d->st()));
         std::memcpy((char*)dst + off, d->bounce, c);
     }
@@ -2703,6 +3003,8 @@ sfp_dev* sfp_create(int device, const sfp_tables* t) {
               hipMalloc(&d->ipsiD, tn) == hipSuccess && hipMalloc(&d->qinvD, d->np * 8) == hipSuccess &&
               hipMalloc(&d->ninvD, d->np * 8) == hipSuccess && hipMalloc(&d->ninvQ, d->np * 8) == hipSuccess;
     d->ringCap = (size_t)16 << 20;
+    if (const char* v = std::getenv("SFHE_ARG_RING_MB"))  // (tests: force chunked uploads)
+        d->ringCap = (size_t)std::max(1, std::atoi(v)) << 20;
     d->bounceCap = (size_t)32 << 20;
     ok = ok &&
          hipHostMalloc((void**)&d->hring, d->ringCap, hipHostMallocMapped | hipHostMallocCoherent) ==
@@ -2862,21 +3164,61 @@ sfp_event* sfp_event_record(sfp_dev* d) {
         SFP_CHECK(hipEventCreateWithFlags(&e->e, hipEventDisableTiming));
     }
     e->lane = d->cur;
+    if (d->stackOn) {  // recorded at its place in the lane's sequence by stackFlush
+        StackRec r;
+        r.kind = StackRec::EV_RECORD;
+        r.ev = e;
+        r.id = e->recId = ++d->recSeq;
+        d->stack[d->cur].push_back(std::move(r));
+        return e;
+    }
+    e->recId = 0;
     SFP_CHECK(hipEventRecord(e->e, d->st()));
     return e;
 }
 void sfp_event_wait(sfp_dev* d, const sfp_event* e) {
-    if (e && e->lane != d->cur) SFP_CHECK(hipStreamWaitEvent(d->st(), e->e, 0));
+    if (!e || e->lane == d->cur) return;
+    if (d->stackOn) {
+        StackRec r;
+        r.kind = StackRec::EV_WAIT;
+        r.ev = const_cast<sfp_event*>(e);
+        r.id = e->recId;  // 0: a record made before the region (a real event already)
+        d->stack[d->cur].push_back(std::move(r));
+        return;
+    }
+    SFP_CHECK(hipStreamWaitEvent(d->st(), e->e, 0));
 }
 int sfp_event_done(sfp_dev* d, const sfp_event* e) {
     // a capture starts after every lane drained: earlier events are complete
     if (d->capture) return 1;
+    stackFlush(d);
     return !e || hipEventQuery(e->e) == hipSuccess;
 }
 void sfp_event_free(sfp_dev* d, sfp_event* e) {
     if (!e) return;
     std::lock_guard<std::mutex> g(d->evMu);
+    // inside a stacked region a deferred record or wait may still name it:
+    // reusable only after the flush
+    if (d->stackOn && e->recId) return d->stackFreedEv.push_back(e);
     d->evFree.push_back(e);  // re-recording later is safe: waits bind at enqueue time
+}
+
+void sfp_stack_begin(sfp_dev* d) {
+    if (d->stackOn) return;
+    static const bool on = [] {
+        const char* v = std::getenv("SFHE_STACK");
+        return !v || *v != '0';
+    }();
+    if (!on) return;
+    d->stackOn = true;
+}
+void sfp_stack_end(sfp_dev* d) {
+    stackFlush(d);
+    d->stackOn = false;
+}
+void sfp_stack_stats(sfp_dev* d, uint64_t* merged, uint64_t* single) {
+    if (merged) *merged = d->stkMerged;
+    if (single) *single = d->stkSingle;
 }
 void sfp_lane_wait(sfp_dev* d, int waiter, int waitee) {
     if (waiter == waitee) return;
@@ -2932,10 +3274,10 @@ static void nttRows(sfp_dev* d, const RowGroup& G, int inverse, int passes = 3) 
     if (d->n <= (uint32_t)kNttTile) {  // small rings: one single-pass block per row
         timedLaunch(d, SFP_FAM_NTT, bytes, [&] {
             if (inverse)
-                hipLaunchKernelGGL(k_ntt_small<true>, dim3(1, rows), dim3(kNttSmallThreads), 0, d->st(), G, d->bar,
+                SFP_GO(k_ntt_small<true>, dim3(1, rows), dim3(kNttSmallThreads), G, d->bar,
                                    d->ipsi, d->ipsiS, d->ninv, d->ninvS, d->logn);
             else
-                hipLaunchKernelGGL(k_ntt_small<false>, dim3(1, rows), dim3(kNttSmallThreads), 0, d->st(), G, d->bar,
+                SFP_GO(k_ntt_small<false>, dim3(1, rows), dim3(kNttSmallThreads), G, d->bar,
                                    d->psi, d->psiS, d->ninv, d->ninvS, d->logn);
         });
         checkLaunch(d, "ntt");
@@ -2968,11 +3310,35 @@ static void nttRows(sfp_dev* d, const RowGroup& G, int inverse, int passes = 3) 
     const dim3 g(d->n / (t1k ? smallTile : (uint32_t)kNttTile), rows);
     const bool small = rows < (uint32_t)kNttSmallRows;
     int npass = 0;
-    auto pass = [&](auto kern, int threads) {
+    // kern2: the same pass over two row groups (stacked launches), or null
+    auto pass = [&](auto kern, NttKern2 kern2, int threads) {
         if (!((passes >> npass++) & 1)) return;
         timedLaunch(d, SFP_FAM_NTT, bytes, [&] {
-            hipLaunchKernelGGL(kern, g, dim3(threads), 0, d->st(), G, d->bar, tw, twS, d->ninv,
-                               d->ninvS, d->logn, twD, d->qinvD, d->ninvD, d->ninvQ, nttFp());
+            RowGroupSet<1> GS;
+            GS.a[0] = G;
+            GS.split = rows;
+            const int fp = nttFp();
+            StackRec r;
+            r.go = [=](hipStream_t s_) {
+                hipLaunchKernelGGL(kern, g, dim3(threads), 0, s_, GS, d->bar, tw, twS, d->ninv, d->ninvS, d->logn,
+                                   twD, d->qinvD, d->ninvD, d->ninvQ, fp);
+            };
+            if (kern2 && d->stackOn) {
+                auto P = std::make_shared<NttPay>();
+                P->G = G;
+                P->rows = rows;
+                P->g = g;
+                P->threads = threads;
+                P->useFp = fp;
+                P->k2 = kern2;
+                P->tw = tw;
+                P->twS = twS;
+                P->twD = twD;
+                r.cls = STK_NTT;
+                r.key = stkKey((const void*)kern, g.x, (uint32_t)threads);
+                r.pay = std::move(P);
+            }
+            issueRec(d, std::move(r));
         });
     };
     static const int le = [] {  // SFHE_NTT_LE: register-round width experiments (2, 3, 4)
@@ -2985,18 +3351,18 @@ static void nttRows(sfp_dev* d, const RowGroup& G, int inverse, int passes = 3) 
         constexpr int ST = decltype(tileC)::value;
         if (smallLe == 3) {
             if (!inverse) {
-                pass(k_ntt<false, true, 3, ST>, ST >> 3);
-                pass(k_ntt<false, false, 3, ST>, ST >> 3);
+                pass(k_ntt<false, true, 3, ST>, NttKern2{}, ST >> 3);
+                pass(k_ntt<false, false, 3, ST>, NttKern2{}, ST >> 3);
             } else {
-                pass(k_ntt<true, false, 3, ST>, ST >> 3);
-                pass(k_ntt<true, true, 3, ST>, ST >> 3);
+                pass(k_ntt<true, false, 3, ST>, NttKern2{}, ST >> 3);
+                pass(k_ntt<true, true, 3, ST>, NttKern2{}, ST >> 3);
             }
         } else if (!inverse) {
-            pass(k_ntt<false, true, 2, ST>, ST >> 2);
-            pass(k_ntt<false, false, 2, ST>, ST >> 2);
+            pass(k_ntt<false, true, 2, ST>, k_ntt<false, true, 2, ST, 2>, ST >> 2);
+            pass(k_ntt<false, false, 2, ST>, k_ntt<false, false, 2, ST, 2>, ST >> 2);
         } else {
-            pass(k_ntt<true, false, 2, ST>, ST >> 2);
-            pass(k_ntt<true, true, 2, ST>, ST >> 2);
+            pass(k_ntt<true, false, 2, ST>, k_ntt<true, false, 2, ST, 2>, ST >> 2);
+            pass(k_ntt<true, true, 2, ST>, k_ntt<true, true, 2, ST, 2>, ST >> 2);
         }
     };
     if (t1k) {
@@ -3006,25 +3372,25 @@ static void nttRows(sfp_dev* d, const RowGroup& G, int inverse, int passes = 3) 
             smallPasses(std::integral_constant<int, 1024>{});
     } else if (!inverse) {
         if (L == 4) {
-            pass(k_ntt<false, true, 4, T>, T >> 4);
-            pass(k_ntt<false, false, 4, T>, T >> 4);
+            pass(k_ntt<false, true, 4, T>, NttKern2{}, T >> 4);
+            pass(k_ntt<false, false, 4, T>, NttKern2{}, T >> 4);
         } else if (L == 2) {
-            pass(k_ntt<false, true, 2, T>, T >> 2);
-            pass(k_ntt<false, false, 2, T>, T >> 2);
+            pass(k_ntt<false, true, 2, T>, k_ntt<false, true, 2, T, 2>, T >> 2);
+            pass(k_ntt<false, false, 2, T>, k_ntt<false, false, 2, T, 2>, T >> 2);
         } else {
-            pass(k_ntt<false, true, 3, T>, T >> 3);
-            pass(k_ntt<false, false, 3, T>, T >> 3);
+            pass(k_ntt<false, true, 3, T>, NttKern2{}, T >> 3);
+            pass(k_ntt<false, false, 3, T>, NttKern2{}, T >> 3);
         }
     } else {
         if (L == 4) {
-            pass(k_ntt<true, false, 4, T>, T >> 4);
-            pass(k_ntt<true, true, 4, T>, T >> 4);
+            pass(k_ntt<true, false, 4, T>, NttKern2{}, T >> 4);
+            pass(k_ntt<true, true, 4, T>, NttKern2{}, T >> 4);
         } else if (L == 2) {
-            pass(k_ntt<true, false, 2, T>, T >> 2);
-            pass(k_ntt<true, true, 2, T>, T >> 2);
+            pass(k_ntt<true, false, 2, T>, k_ntt<true, false, 2, T, 2>, T >> 2);
+            pass(k_ntt<true, true, 2, T>, k_ntt<true, true, 2, T, 2>, T >> 2);
         } else {
-            pass(k_ntt<true, false, 3, T>, T >> 3);
-            pass(k_ntt<true, true, 3, T>, T >> 3);
+            pass(k_ntt<true, false, 3, T>, NttKern2{}, T >> 3);
+            pass(k_ntt<true, true, 3, T>, NttKern2{}, T >> 3);
         }
     }
     checkLaunch(d, "ntt");
@@ -3111,6 +3477,7 @@ void sfp_clear_error(sfp_dev* d) {
 sfp_graph* sfp_capture_end(sfp_dev* d) {
     sfp_graph* g = d->capture;
     if (!g) return nullptr;
+    stackFlush(d);  // (a stacked region left open: its launches belong to the graph)
     d->cur = 0;
     // test knob (read per capture): abandon this capture as if it had failed
     if (const char* f = std::getenv("SFHE_CAPTURE_FORCE_FAIL"); f && *f == '1') captureFail(d, "forced (SFHE_CAPTURE_FORCE_FAIL)");
@@ -3148,7 +3515,8 @@ sfp_graph* sfp_capture_end(sfp_dev* d) {
 
 void sfp_graph_launch(sfp_dev* d, sfp_graph* g) {
     if (!g || !g->exec) return record(d, "graph_launch", hipErrorInvalidValue);
-    SFP_CHECK(hipGraphLaunch(g->exec, d->st()));
+    hipGraphExec_t ex = g->exec;
+    issue(d, [d, ex](hipStream_t s_) { SFP_CHECK(hipGraphLaunch(ex, s_)); });
 }
 
 size_t sfp_graph_nodes(const sfp_graph* g) { return g ? g->nodes : 0; }
@@ -3157,7 +3525,13 @@ int sfp_graph_family_time(sfp_dev* d, sfp_graph* g, uint32_t fam, int reps, doub
                           double* bytes) {
     if (!g || !g->g || fam != SFP_FAM_NTT || reps < 1 || d->capture) return -1;
     constexpr int T = kNttTile;
-    const void* fns[] = {(const void*)k_ntt<false, true, 2, T>, (const void*)k_ntt<false, false, 2, T>,
+    const void* fns[] = {(const void*)k_ntt<false, true, 2, T, 2>, (const void*)k_ntt<false, false, 2, T, 2>,
+                         (const void*)k_ntt<true, true, 2, T, 2>,  (const void*)k_ntt<true, false, 2, T, 2>,
+                         (const void*)k_ntt<false, true, 2, 1024, 2>, (const void*)k_ntt<false, false, 2, 1024, 2>,
+                         (const void*)k_ntt<true, true, 2, 1024, 2>,  (const void*)k_ntt<true, false, 2, 1024, 2>,
+                         (const void*)k_ntt<false, true, 2, 512, 2>, (const void*)k_ntt<false, false, 2, 512, 2>,
+                         (const void*)k_ntt<true, true, 2, 512, 2>,  (const void*)k_ntt<true, false, 2, 512, 2>,
+                         (const void*)k_ntt<false, true, 2, T>, (const void*)k_ntt<false, false, 2, T>,
                          (const void*)k_ntt<true, true, 2, T>,  (const void*)k_ntt<true, false, 2, T>,
                          (const void*)k_ntt<false, true, 3, T>, (const void*)k_ntt<false, false, 3, T>,
                          (const void*)k_ntt<true, true, 3, T>,  (const void*)k_ntt<true, false, 3, T>,
@@ -3253,7 +3627,7 @@ static void ew(sfp_dev* d, u64* out, const u64* a, const u64* b, const u64* c, s
     ConstArgs ka;
     if (k) std::memcpy(ka.k, k, m.count * 8);
     const size_t pairs = ((size_t)m.count * d->n) / 2;
-    hipLaunchKernelGGL(k_ew<OP>, dim3(ewGrid(pairs)), dim3(kThreads), 0, d->st(), out, a, b, c, m,
+    SFP_GO(k_ew<OP>, dim3(ewGrid(pairs)), dim3(kThreads), out, a, b, c, m,
                        d->bar, d->logn, ka);
     checkLaunch(d, "elementwise");
 }
@@ -3285,7 +3659,7 @@ void sfp_tensor(sfp_dev* d, uint64_t* d0, uint64_t* d1, uint64_t* d2, const uint
                 const uint64_t* a1, const uint64_t* b0, const uint64_t* b1, sfp_limbs m) {
     if (!limbsOk(d, m, "tensor")) return;
     const size_t total = (size_t)m.count * d->n;
-    hipLaunchKernelGGL(k_tensor, dim3(ewGrid(total / 2)), dim3(kThreads), 0, d->st(), d0, d1, d2, a0, a1,
+    SFP_GO(k_tensor, dim3(ewGrid(total / 2)), dim3(kThreads), d0, d1, d2, a0, a1,
                        b0, b1, m, d->bar, d->logn);
     checkLaunch(d, "tensor");
 }
@@ -3301,7 +3675,7 @@ void sfp_lin_wsum(sfp_dev* d, uint64_t* out, const uint64_t* const* ins, const u
     for (uint32_t j = 0; j < nin; ++j) pl.p[j] = ins[j];
     const u64* dk = (const u64*)ringPut(d, k, (size_t)nin * m.count * 8);
     const size_t total = (size_t)m.count * d->n;
-    hipLaunchKernelGGL(k_lin_wsum, dim3(ewGrid(total)), dim3(kThreads), 0, d->st(), out, pl, dk, nin,
+    SFP_GO(k_lin_wsum, dim3(ewGrid(total)), dim3(kThreads), out, pl, dk, nin,
                        m, d->bar, d->logn);
     checkLaunch(d, "lin_wsum");
 }
@@ -3321,7 +3695,7 @@ void sfp_lin_wsum_multi(sfp_dev* d, uint64_t* out, size_t outStride, size_t poly
     }
     const u64* dk = (const u64*)ringPut(d, k, (size_t)nout * nin * m.count * 8);
     const dim3 g((d->n / kThreads) * ((nout + kWsumChunk - 1) / kWsumChunk), m.count);
-    hipLaunchKernelGGL(k_lin_wsum_multi, g, dim3(kThreads), 0, d->st(), out, outStride, polyStride, pl, dk,
+    SFP_GO(k_lin_wsum_multi, g, dim3(kThreads), out, outStride, polyStride, pl, dk,
                        nin, nout, m, d->bar, d->logn, d->qinvD, (int)nttFp());
     checkLaunch(d, "lin_wsum_multi");
 }
@@ -3341,7 +3715,7 @@ void sfp_mac_plain2(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint64_t* 
         L.b[j] = b[j];
     }
     const size_t total = (size_t)m.count * d->n;
-    hipLaunchKernelGGL(k_mac_plain2, dim3(ewGrid(total / 2)), dim3(kThreads), 0, d->st(), out0, out1, L, nin, m,
+    SFP_GO(k_mac_plain2, dim3(ewGrid(total / 2)), dim3(kThreads), out0, out1, L, nin, m,
                        d->bar, d->logn);
     checkLaunch(d, "mac_plain2");
 }
@@ -3359,14 +3733,14 @@ void sfp_mac_plain(sfp_dev* d, uint64_t* out, const uint64_t* const* a, const ui
         pl.b[j] = b[j];
     }
     const size_t total = (size_t)m.count * d->n;
-    hipLaunchKernelGGL(k_mac_plain, dim3(ewGrid(total)), dim3(kThreads), 0, d->st(), out, pl, nin, m,
+    SFP_GO(k_mac_plain, dim3(ewGrid(total)), dim3(kThreads), out, pl, nin, m,
                        d->bar, d->logn);
     checkLaunch(d, "mac_plain");
 }
 
 void sfp_automorph(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t g, sfp_limbs m) {
     const size_t total = (size_t)m.count * d->n;
-    hipLaunchKernelGGL(k_automorph, dim3(ewGrid(total)), dim3(kThreads), 0, d->st(), out, in, g,
+    SFP_GO(k_automorph, dim3(ewGrid(total)), dim3(kThreads), out, in, g,
                        m.count, d->logn);
     checkLaunch(d, "automorph");
 }
@@ -3663,14 +4037,22 @@ static void convLaunch(sfp_dev* d, const ConvJobs& J, uint32_t njobs, bool fpOk)
     timedLaunch(d, SFP_FAM_CONV, bytes, [&] {
         // NS = 13 (ModDown's K P-rows, ModUp digits of <= 13 primes) sizes the
         // LDS for 6 blocks per CU instead of 5 (the loops keep their guards)
-        if (fp && maxS <= 13)
-            hipLaunchKernelGGL(k_convf<13>, g, dim3(kThreads), 0, d->st(), J, d->bar, d->qinvD, d->logn);
-        else if (fp && maxS <= 16)
-            hipLaunchKernelGGL(k_convf<16>, g, dim3(kThreads), 0, d->st(), J, d->bar, d->qinvD, d->logn);
-        else if (fp)
-            hipLaunchKernelGGL(k_convf<kMaxConvSrc>, g, dim3(kThreads), 0, d->st(), J, d->bar, d->qinvD, d->logn);
-        else
-            hipLaunchKernelGGL(k_conv, g, dim3(kThreads), 0, d->st(), J, d->bar, d->qinvD, d->logn);
+        ConvKern k = (fp && maxS <= 13) ? k_convf<13> : (fp && maxS <= 16) ? k_convf<16>
+                     : fp                ? k_convf<kMaxConvSrc>
+                                         : k_conv;
+        StackRec r;
+        r.go = [=](hipStream_t s_) { hipLaunchKernelGGL(k, g, dim3(kThreads), 0, s_, J, d->bar, d->qinvD, d->logn); };
+        if (d->stackOn) {
+            auto P = std::make_shared<ConvPay>();
+            P->J = J;
+            P->njobs = njobs;
+            P->g = g;
+            P->k = k;
+            r.cls = STK_CONV;
+            r.key = stkKey((const void*)k, g.x, 0);
+            r.pay = std::move(P);
+        }
+        issueRec(d, std::move(r));
     });
     checkLaunch(d, "conv");
 }
@@ -3793,13 +4175,32 @@ static void modupInnerCore(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uin
     const uint32_t rows = ell + K;
     const size_t total = (size_t)rows * n;
     const bool t1k = rows <= 64 && n <= 1024u * 128u;
-    timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + (accum ? 4.0 : 2.0)), [&] {
-        if (t1k)
-            hipLaunchKernelGGL((k_ntt_ks<2, 1024>), dim3(n / 1024, rows), dim3(1024 >> 2), 0, d->st(), a, d->bar,
-                               d->psi, d->psiS, d->logn, d->psiD, d->qinvD, nttFp());
-        else
-            hipLaunchKernelGGL((k_ntt_ks<2, kNttTile>), dim3(n / kNttTile, rows), dim3(kNttTile >> 2), 0, d->st(),
-                               a, d->bar, d->psi, d->psiS, d->logn, d->psiD, d->qinvD, nttFp());
+    timedLaunch(d, SFP_FAM_NTTKS, 8.0 * total * (3.0 * beta + (accum ? 4.0 : 2.0)), [&] {
+        ArgSet<KsArgs, 1> AS;
+        AS.a[0] = a;
+        AS.split = rows;
+        const int fp = nttFp();
+        const dim3 g(n / (t1k ? 1024u : (uint32_t)kNttTile), rows);
+        const int threads = (t1k ? 1024 : kNttTile) >> 2;
+        auto k1 = t1k ? k_ntt_ks<2, 1024> : k_ntt_ks<2, kNttTile>;
+        StackRec r;
+        r.go = [=](hipStream_t s_) {
+            hipLaunchKernelGGL(k1, g, dim3(threads), 0, s_, AS, d->bar, d->psi, d->psiS, d->logn, d->psiD, d->qinvD,
+                               fp);
+        };
+        if (d->stackOn) {
+            auto P = std::make_shared<KsPay>();
+            P->a = a;
+            P->rows = rows;
+            P->g = g;
+            P->threads = threads;
+            P->useFp = fp;
+            P->k2 = t1k ? k_ntt_ks<2, 1024, 2> : k_ntt_ks<2, kNttTile, 2>;
+            r.cls = STK_KS;
+            r.key = stkKey((const void*)k1, g.x, (uint32_t)threads);
+            r.pay = std::move(P);
+        }
+        issueRec(d, std::move(r));
     });
     checkLaunch(d, "ntt_ks");
 }
@@ -3836,7 +4237,7 @@ void sfp_ks_inner_fold(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_
     }
     // reads beta ext rows + 2*beta key rows, writes 2 accumulator rows, per limb
     timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + 2.0), [&] {
-        hipLaunchKernelGGL(k_ks_inner, dim3(ewGrid(total / 2)), dim3(kThreads), 0, d->st(), acc0, acc1, ext,
+        SFP_GO(k_ks_inner, dim3(ewGrid(total / 2)), dim3(kThreads), acc0, acc1, ext,
                            extStride, key, beta, sfp_limbs{ell + K, ell, Lq, 0, 1}, Lq, Lq + K, fold0, fold1,
                            foldK, d->bar, d->logn, 0, (const u64*)nullptr);
     });
@@ -3848,7 +4249,7 @@ void sfp_ks_inner_acc(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t
     const size_t total = (size_t)(ell + K) * d->n;
     // reads beta ext rows + 2*beta key rows + 2 accumulator rows, writes 2, per limb
     timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + 4.0), [&] {
-        hipLaunchKernelGGL(k_ks_inner, dim3(ewGrid(total / 2)), dim3(kThreads), 0, d->st(), acc0, acc1, ext,
+        SFP_GO(k_ks_inner, dim3(ewGrid(total / 2)), dim3(kThreads), acc0, acc1, ext,
                            extStride, key, beta, sfp_limbs{ell + K, ell, Lq, 0, 1}, Lq, Lq + K, (const u64*)nullptr,
                            (const u64*)nullptr, (u64)0, d->bar, d->logn, 1, (const u64*)nullptr);
     });
@@ -3861,7 +4262,7 @@ void sfp_ks_inner_mul(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t
     const size_t total = (size_t)(ell + K) * d->n;
     // reads beta ext rows + 2*beta key rows + the plaintext row (+ 2 accumulator rows), writes 2, per limb
     timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + (accum ? 5.0 : 3.0)), [&] {
-        hipLaunchKernelGGL(k_ks_inner, dim3(ewGrid(total / 2)), dim3(kThreads), 0, d->st(), acc0, acc1, ext,
+        SFP_GO(k_ks_inner, dim3(ewGrid(total / 2)), dim3(kThreads), acc0, acc1, ext,
                            extStride, key, beta, sfp_limbs{ell + K, ell, Lq, 0, 1}, Lq, Lq + K, (const u64*)nullptr,
                            (const u64*)nullptr, (u64)0, d->bar, d->logn, accum, pm);
     });
@@ -3915,6 +4316,7 @@ static void moddownRescaleCore(sfp_dev* d, uint64_t* out0, uint64_t* out1, const
     nttRows(d, A, 1, rowDone ? 2 : 3);
     // conversion + the dropped row's lift
     MdrsArgs M;
+    std::memset(&M, 0, sizeof M);  // (stacked launches compare it bytewise)
     for (int p = 0; p < 2; ++p) {
         const u64* ap = acc + (size_t)p * accStride;
         M.j[p] = MdrsJob{ap + (size_t)ell * n, ap, scr + (size_t)p * l * n};
@@ -3978,21 +4380,26 @@ static void moddownRescaleCore(sfp_dev* d, uint64_t* out0, uint64_t* out1, const
     }
     const dim3 g((fp || bigl) ? n / kConvCoefs : n / (2 * kThreads), 2, zc);
     timedLaunch(d, SFP_FAM_CONV, 8.0 * n * 2 * (K + 1 + l), [&] {
-        if (bigl && c->ns <= 13)
-            hipLaunchKernelGGL((k_mdrsf<13, true>), g, dim3(kThreads), 0, d->st(), M, d->bar, d->qinvD, d->logn);
-        else if (bigl && c->ns <= 16)
-            hipLaunchKernelGGL((k_mdrsf<16, true>), g, dim3(kThreads), 0, d->st(), M, d->bar, d->qinvD, d->logn);
-        else if (bigl)
-            hipLaunchKernelGGL((k_mdrsf<kMaxConvSrc, true>), g, dim3(kThreads), 0, d->st(), M, d->bar, d->qinvD,
-                               d->logn);
-        else if (fp && c->ns <= 13)  // LDS for 6 blocks per CU (as convLaunch)
-            hipLaunchKernelGGL(k_mdrsf<13>, g, dim3(kThreads), 0, d->st(), M, d->bar, d->qinvD, d->logn);
-        else if (fp && c->ns <= 16)
-            hipLaunchKernelGGL(k_mdrsf<16>, g, dim3(kThreads), 0, d->st(), M, d->bar, d->qinvD, d->logn);
-        else if (fp)
-            hipLaunchKernelGGL(k_mdrsf<kMaxConvSrc>, g, dim3(kThreads), 0, d->st(), M, d->bar, d->qinvD, d->logn);
-        else
-            hipLaunchKernelGGL(k_conv_mdrs, g, dim3(kThreads), 0, d->st(), M, d->bar, d->qinvD, d->logn);
+        // (fp: LDS for 6 blocks per CU at ns <= 13, as convLaunch)
+        MdrsKern k = (bigl && c->ns <= 13) ? k_mdrsf<13, true>
+                     : (bigl && c->ns <= 16) ? k_mdrsf<16, true>
+                     : bigl                  ? k_mdrsf<kMaxConvSrc, true>
+                     : (fp && c->ns <= 13)   ? k_mdrsf<13>
+                     : (fp && c->ns <= 16)   ? k_mdrsf<16>
+                     : fp                    ? k_mdrsf<kMaxConvSrc>
+                                             : k_conv_mdrs;
+        StackRec r;
+        r.go = [=](hipStream_t s_) { hipLaunchKernelGGL(k, g, dim3(kThreads), 0, s_, M, d->bar, d->qinvD, d->logn); };
+        if (d->stackOn) {
+            auto P = std::make_shared<MdrsPay>();
+            P->M = M;
+            P->g = g;
+            P->k = reinterpret_cast<ConvKern>(k);
+            r.cls = STK_MDRS;
+            r.key = stkKey((const void*)k, g.x, g.z);
+            r.pay = std::move(P);
+        }
+        issueRec(d, std::move(r));
     });
     checkLaunch(d, "conv_mdrs");
     // out_i = (acc_i - NTT(y_i)) (P q_l)^-1 + d_i q_l^-1
@@ -4049,7 +4456,7 @@ int sfp_mult_relin_rescale(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uin
 void sfp_sample_uniform(sfp_dev* d, uint64_t* p, sfp_limbs m, uint64_t seed) {
     if (!limbsOk(d, m, "uniform")) return;
     const size_t total = (size_t)m.count * d->n;
-    hipLaunchKernelGGL(k_uniform, dim3(ewGrid(total)), dim3(kThreads), 0, d->st(), p, m, seed, d->bar,
+    SFP_GO(k_uniform, dim3(ewGrid(total)), dim3(kThreads), p, m, seed, d->bar,
                        d->logn);
     checkLaunch(d, "uniform");
 }
@@ -4060,7 +4467,7 @@ void sfp_load_i64(sfp_dev* d, uint64_t* p, const int64_t* c, sfp_limbs m) {
     // reads the coefficients straight from it
     syncAll(d);
     std::memcpy(d->bounce, c, (size_t)d->n * 8);
-    hipLaunchKernelGGL(k_load_i64, dim3(ewGrid(d->n)), dim3(kThreads), 0, d->st(), p,
+    SFP_GO(k_load_i64, dim3(ewGrid(d->n)), dim3(kThreads), p,
                        (const int64_t*)d->bounce, m, d->bar, d->logn);
     checkLaunch(d, "load_i64");
 }
@@ -4190,21 +4597,32 @@ void sfp_encode_batch(sfp_dev* d, uint64_t* dst, size_t dstStride, const double*
         record(d, "encode (tables not set up, or a bad slot / batch count)", hipErrorInvalidValue);
         return;
     }
+    // the values travel through the argument ring: batches whose values
+    // exceed half of it are encoded in chunks (ringPut refuses an upload
+    // larger than the ring; a bootstrap's diagonals at 2^14+ slots are)
+    const size_t per = (size_t)nvals * (real ? 8 : 16);
+    const uint32_t chunk = per ? (uint32_t)std::max<size_t>(1, std::min<size_t>(count, d->ringCap / 2 / per)) : count;
+    if (chunk < count && !d->capture) {
+        for (uint32_t b0 = 0; b0 < count; b0 += chunk)
+            sfp_encode_batch(d, dst + (size_t)b0 * dstStride, dstStride, vals + (size_t)b0 * nvals * (real ? 1 : 2),
+                             nvals, std::min(chunk, count - b0), real, slots, scale, m, scratch);
+        return;
+    }
     const u64 M = 2ull * d->n;
     double2* v = reinterpret_cast<double2*>(scratch);
-    const double* dv =
-        nvals ? (const double*)ringPut(d, vals, (size_t)count * nvals * (real ? 8 : 16)) : nullptr;
-    hipLaunchKernelGGL(k_enc_load, dim3(gridFor(slots, kThreads), count), dim3(kThreads), 0, d->st(), v, dv, nvals,
+    const double* dv = nvals ? (const double*)ringPut(d, vals, (size_t)count * per) : nullptr;
+    if (nvals && !dv) return;
+    SFP_GO(k_enc_load, dim3(gridFor(slots, kThreads), count), dim3(kThreads), v, dv, nvals,
                        real, slots);
     const uint32_t T = std::min(slots, kEncTile);
     for (uint32_t len = slots; len > T; len >>= 1)
-        hipLaunchKernelGGL(k_enc_stage, dim3(gridFor(slots / 2, kThreads), count), dim3(kThreads), 0, d->st(), v,
+        SFP_GO(k_enc_stage, dim3(gridFor(slots / 2, kThreads), count), dim3(kThreads), v,
                            slots, len, d->encRot, d->encKsi, M);
     if (T >= 2)
-        hipLaunchKernelGGL(k_enc_tile, dim3(slots / T, count), dim3(kThreads), 0, d->st(), v, T, d->encRot,
+        SFP_GO(k_enc_tile, dim3(slots / T, count), dim3(kThreads), v, T, d->encRot,
                            d->encKsi, M);
     const uint32_t logS = (uint32_t)__builtin_ctz(slots);
-    hipLaunchKernelGGL(k_enc_round, dim3(ewGrid(d->n), count), dim3(kThreads), 0, d->st(), dst, v, logS, scale, m,
+    SFP_GO(k_enc_round, dim3(ewGrid(d->n), count), dim3(kThreads), dst, v, logS, scale, m,
                        d->bar, d->logn, dstStride);
     checkLaunch(d, "encode");
 }
@@ -4230,7 +4648,7 @@ void sfp_gather_rows(sfp_dev* d, uint64_t* dst, const uint64_t* src, const uint3
     if (!count) return;
     const uint32_t* dr = (const uint32_t*)ringPut(d, rows, (size_t)count * 4);
     const dim3 g(std::max(1u, std::min(64u, (d->n / 2) / kThreads)), count);
-    hipLaunchKernelGGL(k_gather_rows, g, dim3(kThreads), 0, d->st(), (ulonglong2*)dst, (const ulonglong2*)src, dr,
+    SFP_GO(k_gather_rows, g, dim3(kThreads), (ulonglong2*)dst, (const ulonglong2*)src, dr,
                        d->logn);
     checkLaunch(d, "gather_rows");
 }
@@ -4273,7 +4691,7 @@ void sfp_ks_inner_map(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t
     if (!pm.count || !limbsOk(d, pm, "ks_inner_map")) return;
     const size_t total = (size_t)pm.count * d->n;
     timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + (accum ? 4.0 : 2.0)), [&] {
-        hipLaunchKernelGGL(k_ks_inner, dim3(ewGrid(total / 2)), dim3(kThreads), 0, d->st(), acc0, acc1, ext, extStride,
+        SFP_GO(k_ks_inner, dim3(ewGrid(total / 2)), dim3(kThreads), acc0, acc1, ext, extStride,
                            key, beta, pm, keyQ, keyRows, (const u64*)nullptr, (const u64*)nullptr, (u64)0, d->bar,
                            d->logn, accum, (const u64*)nullptr);
     });
@@ -4334,6 +4752,7 @@ void sfp_group_set_host(sfp_dev* d, int group, int groups, sfp_host_allgather_fn
 
 void sfp_group_allgather(sfp_dev* d, const void* send, void* recv, size_t bytes) {
     if (d->gnccl) {
+        stackFlush(d);  // (collectives are issued in program order)
         ncclCheck(d, "ncclAllGather (groups)",
                   rcclApi().allGather(send, recv, bytes, ncclUint8, d->gnccl, d->st()));
         return;
@@ -4375,6 +4794,7 @@ void sfp_allgather(sfp_dev* d, const void* send, void* recv, size_t bytes) {
         return;
     }
     if (d->nccl) {
+        stackFlush(d);  // (collectives are issued in program order)
         ncclCheck(d, "ncclAllGather", rcclApi().allGather(send, recv, bytes, ncclUint8, d->nccl, d->st()));
         return;
     }
@@ -4391,6 +4811,7 @@ void sfp_allgather(sfp_dev* d, const void* send, void* recv, size_t bytes) {
 void sfp_bcast(sfp_dev* d, void* buf, size_t bytes, int root) {
     if (d->world == 1 && !d->nccl) return;
     if (d->nccl) {
+        stackFlush(d);  // (collectives are issued in program order)
         ncclCheck(d, "ncclBroadcast", rcclApi().broadcast(buf, buf, bytes, ncclUint8, root, d->nccl, d->st()));
         return;
     }

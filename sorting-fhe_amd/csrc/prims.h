@@ -313,6 +313,20 @@ void sfp_event_free(sfp_dev* d, sfp_event* e);
 // Lane `waiter` waits for everything enqueued so far on lane `waitee`.
 void sfp_lane_wait(sfp_dev* d, int waiter, int waitee);
 
+// ---- stacked launches ----------------------------------------------------------
+// Between sfp_stack_begin and sfp_stack_end the lanes' work is recorded per
+// lane and issued at the end (or at any host synchronisation) on lane 0's
+// stream: each lane's work in its own order, every event wait after its
+// record, and two lanes' next launches of the same kernel (NTT pass, fused
+// key-switch pass, base conversion, ModDown+rescale conversion) over
+// different rows merged into ONE launch -- the sort's batches, which run the
+// same op sequence on two lanes, take half the launches.  Results are
+// bit-identical.  No-op for the oracle, with serialised lanes, or with
+// SFHE_STACK=0.  sfp_stack_stats: launches issued merged (pairs) / alone.
+void sfp_stack_begin(sfp_dev* d);
+void sfp_stack_end(sfp_dev* d);
+void sfp_stack_stats(sfp_dev* d, uint64_t* merged, uint64_t* single);
+
 // ---- multi-process limb sharding (one process per GPU) --------------------------
 // Collectives over the ranks of a sharded context, ordered on the current
 // lane like every other primitive.  Two transports:
@@ -399,8 +413,11 @@ void sfp_graph_destroy(sfp_dev* d, sfp_graph* g);
 // single launches.  Algorithmic bytes per launch (minimum HBM traffic):
 //   NTT pass     16 B per coefficient (read + write once; twiddles excluded)
 //   CONV         8 B per source coefficient read + 8 B per target written
-//   KSINNER      8 B per ext / key / accumulator word touched
-enum { SFP_FAM_NTT = 0, SFP_FAM_CONV = 1, SFP_FAM_KSINNER = 2, SFP_FAM_COUNT = 3 };
+//   KSINNER      8 B per ext / key / accumulator word touched (k_ks_inner)
+//   NTTKS        the same for k_ntt_ks (ModUp's ROW pass fused with the inner product)
+// Inside a stacked region the launches are timed as issued (a merged pair is
+// one launch with the bytes of both).
+enum { SFP_FAM_NTT = 0, SFP_FAM_CONV = 1, SFP_FAM_KSINNER = 2, SFP_FAM_NTTKS = 3, SFP_FAM_COUNT = 4 };
 // Time every `period`-th launch of `fam` (0 = off); resets its counters.
 void sfp_prof_set(sfp_dev* d, uint32_t fam, uint32_t period);
 // Since the last sfp_prof_set: launches seen, launches timed, their summed

@@ -35,7 +35,7 @@ ABI_SYMBOLS = [
     "sfhe_sorter_destroy", "sfhe_sorter_sort", "sfhe_sorter_rank", "sfhe_sorter_place",
     "sfhe_decompose", "sfhe_kernel_timing", "sfhe_kernel_timing_read",
     "sfhe_comm_uid", "sfhe_shard_rccl", "sfhe_shard_host", "sfhe_pool_bytes", "sfhe_live_contexts",
-    "sfhe_serialize_lanes", "sfhe_sorter_graph_nodes", "sfhe_sorter_create_rot",
+    "sfhe_serialize_lanes", "sfhe_stack_stats", "sfhe_sorter_graph_nodes", "sfhe_sorter_create_rot",
     "sfhe_sorter_sort_hybrid1", "sfhe_hybrid1_params", "sfhe_sorter_graph_ntt_time",
     "sfhe_sorter_sort_hybrid", "sfhe_hybrid_params", "sfhe_sorter_place_2n",
     "sfhe_bootstrap_setup", "sfhe_bootstrap_depth", "sfhe_bootstrap",
@@ -143,6 +143,7 @@ _SIGS = {
     "sfhe_sorter_graph_ntt_time": (C.c_int, [_VP, C.c_int, _PD, _PU64, _PD]),
     "sfhe_kernel_timing": (C.c_int, [_VP, _U32, _U32]),
     "sfhe_serialize_lanes": (C.c_int, [_VP, C.c_int]),
+    "sfhe_stack_stats": (C.c_int, [_VP, _PU64, _PU64]),
     "sfhe_kernel_timing_read": (C.c_int, [_VP, _U32, _PU64, _PU64, _PD, _PD]),
     "sfhe_decompose": (C.c_int, [_U32, _PI32, _SZ, C.c_int32, C.c_int32, C.c_int, _PI32, _PI32, _SZ, _PSZ]),
     "sfhe_comm_uid": (C.c_int, [_VP]),
@@ -166,6 +167,9 @@ def lib_path(backend: str = "hip") -> str:
     return os.environ.get("SFHE_PRODUCT_LIB", PRODUCT_LIB) if backend == "hip" else ORACLE_LIB
 
 
+ABI_VERSION = 2  # include/sfhe.h SFHE_ABI_VERSION
+
+
 def load(backend: str = "hip"):
     """Load the engine library.  backend='hip' is the product (raises if the
     HIP build is absent); backend='oracle' is the CPU oracle (tests only)."""
@@ -181,6 +185,11 @@ def load(backend: str = "hip"):
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args
+    # the ctypes structures and signatures above are those of include/sfhe.h
+    # at SFHE_ABI_VERSION: refuse a library built from another version
+    if lib.sfhe_abi_version() != ABI_VERSION:
+        raise SfheError(f"{path}: C ABI version {lib.sfhe_abi_version()}, this binding speaks {ABI_VERSION} "
+                        "(rebuild the library or use the matching sfhe.py)")
     _libs[backend] = lib
     return lib
 
@@ -364,13 +373,19 @@ class Engine:
         self._chk(self.lib.sfhe_pool_bytes(self.ctx, C.byref(v)))
         return v.value
 
-    KFAM = {"ntt": 0, "conv": 1, "ks_inner": 2}
+    KFAM = {"ntt": 0, "conv": 1, "ks_inner": 2, "ntt_ks": 3}
 
     def kernel_timing(self, family: str, period: int = 1):
         self._chk(self.lib.sfhe_kernel_timing(self.ctx, self.KFAM[family], period))
 
     def serialize_lanes(self, on: bool = True):
         self._chk(self.lib.sfhe_serialize_lanes(self.ctx, int(on)))
+
+    def stack_stats(self):
+        """(merged pairs, launches alone) issued by stacked regions so far."""
+        m, s1 = C.c_uint64(), C.c_uint64()
+        self._chk(self.lib.sfhe_stack_stats(self.ctx, C.byref(m), C.byref(s1)))
+        return m.value, s1.value
 
     def kernel_timing_read(self, family: str) -> dict:
         la, ti = C.c_uint64(), C.c_uint64()

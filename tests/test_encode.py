@@ -112,3 +112,14 @@ def test_batched_mask_encodings_bitexact_hip(hip_lib, monkeypatch):
     """The metric sort's masks (16 per giant step, 32768 slots): batched on
     the device, bit-identical to the host encoder."""
     sort_encodings("hip", monkeypatch, 16, 256)
+
+
+@pytest.mark.gpu
+def test_batched_encodings_chunked_hip(hip_lib, monkeypatch):
+    """a batch whose values exceed the argument ring is
+    encoded in chunks (ringPut refuses oversize uploads instead of writing past
+    the pinned ring).  With a 1 MiB ring every giant step's 16 masks of 32768
+    slots (4 MiB of values) take several chunks; the sort stays bit-identical
+    to the host encoder."""
+    monkeypatch.setenv("SFHE_ARG_RING_MB", "1")
+    sort_encodings("hip", monkeypatch, 16, 256)
