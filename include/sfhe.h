@@ -309,6 +309,10 @@ int sfhe_shard_host(sfhe_ctx* c, int rank, int world, sfhe_allgather_fn ag, sfhe
                     void* user);
 /* The replicated-tail limb count of a sharded context (0: unsharded). */
 int sfhe_shard_tail(const sfhe_ctx* c, uint32_t* limbs);
+/* Rows per digit part of this rank's switching keys: num_q + num_p for whole
+ * keys; a sharded rank of world > 1 keeps only its slice (the replicated
+ * tail's Q rows, its own dealt Q rows, the P rows; SFHE_KEY_SLICE=0: whole). */
+int sfhe_key_rows(const sfhe_ctx* c, uint32_t* rows);
 
 /* ---- batch groups (no reference counterpart) ------------------------------
  * DirectSort's rank and placement phases each run B independent batches

@@ -52,7 +52,16 @@ struct sfp_dev {
     /* the host encoder's tables (sfp_encode) */
     u64* enc_rot;
     double* enc_ksi;
+    /* switching-key geometry (sfp_set_key_geom; rows == 0: whole keys) */
+    sfp_key_geom kg;
 };
+
+void sfp_set_key_geom(sfp_dev* d, const sfp_key_geom* g) {
+    if (g)
+        d->kg = *g;
+    else
+        memset(&d->kg, 0, sizeof d->kg);
+}
 
 struct sfp_conv {
     uint32_t ns, nt;
@@ -528,11 +537,12 @@ static void ks_inner_rows(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint
                           size_t ext_stride, const uint64_t* key, uint32_t beta, uint32_t ell,
                           uint32_t K, uint32_t Lq, const uint64_t* fold0, const uint64_t* fold1,
                           uint64_t fold_k, int accum, const uint64_t* pm) {
-    const uint32_t n = d->n, rows = ell + K, NP = Lq + K;
+    const uint32_t n = d->n, rows = ell + K, NP = d->kg.rows ? d->kg.rows : Lq + K;
+    const uint32_t pst = d->kg.rows ? d->kg.pstart : Lq;
 #pragma omp parallel for schedule(static)
     for (uint32_t t = 0; t < rows; ++t) {
-        const uint32_t kr = t < ell ? t : Lq + (t - ell);
-        const u64 q = d->q[kr];
+        const uint32_t kr = t < ell ? t : pst + (t - ell);  /* key row */
+        const u64 q = d->q[t < ell ? t : Lq + (t - ell)];
         for (uint32_t x = 0; x < n; ++x) {
             u128 s0 = 0, s1 = 0;
             for (uint32_t j = 0; j < beta; ++j) {
@@ -822,7 +832,8 @@ void sfp_ks_inner_map(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t
     const uint32_t n = d->n;
 #pragma omp parallel for schedule(static)
     for (uint32_t t = 0; t < pm.count; ++t) {
-        const uint32_t kr = keyQ == SFP_KEY_ROW_BY_PRIME ? pidx(pm, t) : (t < pm.split ? t : keyQ + (t - pm.split));
+        const uint32_t kr = keyQ == SFP_KEY_ROW_BY_PRIME ? sfp_key_row(&d->kg, pidx(pm, t))
+                                                         : (t < pm.split ? t : keyQ + (t - pm.split));
         const u64 q = d->q[pidx(pm, t)];
         for (uint32_t x = 0; x < n; ++x) {
             u128 s0 = 0, s1 = 0;

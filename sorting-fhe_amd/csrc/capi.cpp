@@ -850,6 +850,12 @@ int sfhe_shard_tail(const sfhe_ctx* c, uint32_t* limbs) {
     return SFHE_OK;
 }
 
+int sfhe_key_rows(const sfhe_ctx* c, uint32_t* rows) {
+    REQUIRE(c && rows, "null argument");
+    *rows = c->cc->SwitchKeyRows();
+    return SFHE_OK;
+}
+
 // ---- batch groups ----
 int sfhe_groups_rccl(sfhe_ctx* c, int group, int groups, const uint8_t uid[128]) {
     REQUIRE(c && uid, "null argument");

@@ -644,6 +644,28 @@ class SfheInternal {
         return s->modupConvShard[ell] = v;
     }
 
+    // This rank's slice of a whole switching key (sfp_key_geom): per digit
+    // and part, the tail Q rows, the rank's dealt Q rows above the tail and
+    // the P rows -- every row a replicated level or this rank's dealt rows
+    // read.
+    static DeviceBufferPtr sliceKey(SfheContextState* s, const DeviceBufferPtr& whole) {
+        const sfp_key_geom& g = s->kgeom;
+        const uint32_t n = s->n, NP = s->Lq + s->K;
+        std::vector<uint32_t> rows;
+        for (uint32_t p = 0; p < NP; ++p) {
+            const bool keep = p < g.tail || p >= s->Lq || p % g.world == (uint32_t)s->rank;
+            if (!keep) continue;
+            if (sfp_key_row(&g, p) != rows.size()) SFHE_THROW("internal: key slice row map");
+            rows.push_back(p);
+        }
+        if (rows.size() != g.rows) SFHE_THROW("internal: key slice size");
+        auto out = s->alloc((size_t)s->dnum * 2 * g.rows * n);
+        for (uint32_t part = 0; part < 2 * s->dnum; ++part)
+            sfp_gather_rows(s->dev, out->ptr + (size_t)part * g.rows * n, whole->ptr + (size_t)part * NP * n,
+                            rows.data(), g.rows);
+        return out;
+    }
+
     // ModUp of the local rows of d (ell limbs, dealt): beta blocks of extmap(ell) rows
     static void modupShard(SfheContextState* s, uint64_t* ext, const uint64_t* d, uint32_t ell) {
         const uint32_t n = s->n, beta = (ell + s->alpha - 1) / s->alpha;
@@ -668,15 +690,14 @@ class SfheInternal {
         modDownShard(s, acc->ptr, ell, out0, out1, add0, add1);
     }
     // The local key inner product into acc (2 polys of extmap(ell) rows),
-    // accumulated when accum.  Every rank keeps whole switching keys (they
-    // fit HBM many times over, and the replicated tail needs every row): a
-    // local ext row reads the key row of its own prime.
+    // accumulated when accum.  A local ext row reads the key row of its own
+    // prime (sfp_key_row: in this rank's key slice).
     static void innerShard(SfheContextState* s, uint64_t* acc, const uint64_t* ext, size_t stride, uint32_t beta,
                            uint32_t ell, const DeviceBufferPtr& key, int accum) {
         const sfp_limbs em = s->extmap(ell);
         const size_t aw = (size_t)em.count * s->n;
         sfp_ks_inner_map(s->dev, acc, acc + aw, ext, stride, key->ptr, beta, em, SFP_KEY_ROW_BY_PRIME,
-                         s->Lq + s->K, accum);
+                         s->keyRows(), accum);
     }
     // ModDown of the local accumulators (their P rows are destroyed)
     static void modDownShard(SfheContextState* s, uint64_t* acc, uint32_t ell, uint64_t* out0, uint64_t* out1,
@@ -975,9 +996,13 @@ class SfheInternal {
     // switching key from s' (device, Lq+K limbs, eval domain) to s
     static DeviceBufferPtr genSwitchKey(CC* cc, const uint64_t* sPrime, const uint64_t* sk) {
         SfheContextState* s = cc->st.get();
-        if (s->sharded) {  // every rank builds (and keeps) the whole key: same seed, same words
-            FullScope fs(s);
-            return genSwitchKey(cc, sPrime, sk);
+        if (s->sharded) {  // every rank builds the whole key (same seed, same words) ...
+            DeviceBufferPtr whole;
+            {
+                FullScope fs(s);
+                whole = genSwitchKey(cc, sPrime, sk);
+            }
+            return s->kgeom.rows ? sliceKey(s, whole) : whole;  // ... and keeps its slice
         }
         const uint32_t n = s->n, NP = s->Lq + s->K;
         const sfp_limbs all{NP, NP, 0};
@@ -2984,9 +3009,26 @@ void CryptoContextImpl<DCRTPoly>::EnableSharding(int rank, int world, bool shard
     for (uint32_t k = 0; k < s->K; ++k) src.push_back(s->Lq + k);
     for (uint32_t i = 0; i < s->owned(s->Lq); ++i) dst.push_back(s->qprimeShard(i));
     s->moddownConvShard = dst.empty() ? nullptr : SfheInternal::makeConv(s, src, dst);
+    // Sliced keys (each GPU stores only its slice of every
+    // evaluation key): rows of the replicated levels, of this rank's dealt
+    // primes and the P rows.  SFHE_KEY_SLICE=0 keeps whole keys.
+    const char* ks = std::getenv("SFHE_KEY_SLICE");
+    if (world > 1 && !(ks && *ks == '0')) {
+        sfp_key_geom& g = s->kgeom;
+        g.tail = std::min(s->tailLimbs, s->Lq);
+        g.world = (uint32_t)world;
+        g.lq = s->Lq;
+        g.first = g.tail + ((uint32_t)rank + world - g.tail % world) % world;
+        uint32_t high = 0;
+        for (uint32_t p = g.first; p < s->Lq; p += world) ++high;
+        g.pstart = g.tail + high;
+        g.rows = g.pstart + s->K;
+        sfp_set_key_geom(s->dev, &g);
+    }
 }
 
 uint32_t CryptoContextImpl<DCRTPoly>::ShardTailLimbs() const { return st->sharded ? st->tailLimbs : 0; }
+uint32_t CryptoContextImpl<DCRTPoly>::SwitchKeyRows() const { return st->keyRows(); }
 
 void CryptoContextImpl<DCRTPoly>::EnableBatchGroups(int group, int groups, bool gatherAtOne) {
     OpLock g(st.get());

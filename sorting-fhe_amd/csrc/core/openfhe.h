@@ -503,7 +503,8 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
     // Limb sharding (engine extension): this process holds the
     // RNS limbs i with i % world == rank of every ciphertext; levels with at
     // most ShardTailLimbs() limbs run replicated on every rank (SFHE_SHARD_TAIL,
-    // default 16); every rank keeps whole switching keys.  Call before key
+    // default 16); every rank keeps its slice of the switching keys (the rows
+    // of those levels, of its own dealt primes and the P rows).  Call before key
     // generation, with the device communicator set up (C ABI sfhe_comm_*).
     // shardAtOne: a one-rank communicator still takes the sharded code path
     // (single-GPU validation of the exchanges).  Results are bit-identical
@@ -513,6 +514,9 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
     int ShardWorld() const;
     bool IsSharded() const;
     uint32_t ShardTailLimbs() const;
+    // rows per digit part of this rank's switching keys: Lq + K for whole
+    // keys, fewer for a sliced key (sharded, world > 1; SFHE_KEY_SLICE=0: whole)
+    uint32_t SwitchKeyRows() const;
     // Batch groups (engine extension): the sort's independent
     // batches are split over `groups` GPU groups, this rank in group `group`
     // (each group limb-sharded or not).  The device's group communicator

@@ -153,6 +153,10 @@ struct SfheContextState {
     uint32_t tailLimbs = 0;
     bool fullScope = false;  // inside FullScope: unsharded (setup work on every row)
     std::vector<DeviceBufferPtr> scopeKeep;  // uncached encodings alive until the scope ends
+    // switching-key geometry: whole keys (rows 0), or this rank's slice of
+    // every key (sfp_key_geom; set by EnableSharding)
+    sfp_key_geom kgeom{};
+    uint32_t keyRows() const { return kgeom.rows ? kgeom.rows : Lq + K; }
     std::map<uint32_t, std::vector<sfp_conv*>> modupConvShard;  // ell -> per digit (owned targets)
     sfp_conv* moddownConvShard = nullptr;                        // P -> owned Q rows
 

@@ -135,6 +135,9 @@ struct sfp_dev {
     uint64_t recSeq = 0;
     std::vector<sfp_event*> stackFreedEv;  // freed inside the region: reusable after the flush
     uint64_t stkMerged = 0, stkSingle = 0;  // launches issued as merged pairs / alone
+    sfp_key_geom kg = {};          // switching-key geometry (sfp_set_key_geom; rows 0: whole keys)
+    uint64_t intMask[2] = {0, 0};  // prime p (< 128) runs integer NTT butterflies (nttRows)
+    bool intMaskSet = false;
     uint32_t stkFam = ~0u;  // timedLaunch's family while it records (stacked)
     double stkBytes = 0;
     hipStream_t st() const { return streams[(serial || stackOn) ? 0 : cur]; }
@@ -698,6 +701,9 @@ struct RowGroup {
     uint32_t skipEll;      // >0: skip rows alpha*p <= i < min(alpha*(p+1), skipEll) (ModUp own digit)
     uint32_t lift, liftPrime;
     uint32_t epi, addMask;  // addMask bit p: accumulate into eout for polynomial p
+    uint32_t primeMajor;    // grid row order: prime-major (rows of one prime adjacent) or poly-major
+    uint32_t maskOk;        // intMask valid (every prime index < 128)
+    uint64_t intMask[2];    // bit p: prime p runs the integer butterflies
     RowPtr eadd;            // epi with eadd.base: eout += eadd * k2_i
     // epi with tA0: eadd is the tensor product of (tA0, tA1) and (tB0, tB1)
     // formed here (row i, n words per row): a0 b0 for polynomial 0, a0 b1 +
@@ -717,11 +723,26 @@ struct RowGroup {
 // launch, blockIdx.y < split -> set 0, the rest -> set 1 (rows renumbered
 // from 0).  Two lanes' identical ops (the sort's batches) become one launch
 // with the rows of both; NG = 1 is the ordinary launch.
+// With `inter` (both sets of equal row count) the sets alternate instead:
+// grid row y is row y / 2 of set y % 2, so the two sets' rows of one prime
+// (one key row, one twiddle table) run side by side and share their L2 lines.
 template <class T, int NG>
 struct ArgSet {
     T a[NG];
     uint32_t split;  // grid rows of set 0
+    uint32_t inter;
 };
+template <class T, int NG>
+__device__ __forceinline__ uint32_t argSel(const ArgSet<T, NG>& S, uint32_t& row) {
+    const uint32_t y = blockIdx.y;
+    if (NG > 1 && S.inter) {
+        row = y >> 1;
+        return y & 1u;
+    }
+    const uint32_t sel = (NG > 1 && y >= S.split) ? 1u : 0u;
+    row = y - (sel ? S.split : 0u);
+    return sel;
+}
 template <int NG>
 using RowGroupSet = ArgSet<RowGroup, NG>;
 
@@ -762,12 +783,16 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroupSet<NG> GS, co
     constexpr bool FIRST = (COL != INV);  // forward: COL first; inverse: ROW first
     const uint32_t n = 1u << logn;
     const uint32_t logR = logn - 8;
-    const uint32_t gsel = (NG > 1 && blockIdx.y >= GS.split) ? 1u : 0u;
-    const RowGroup& G = GS.a[gsel];
-    const uint32_t rid = blockIdx.y - (gsel ? GS.split : 0u);
-    const uint32_t pp = rid / G.R, ii = rid % G.R;
+    uint32_t rid;
+    const RowGroup& G = GS.a[argSel(GS, rid)];
+    // prime-major rows (the default): the P polynomials' rows of one prime
+    // are adjacent in the grid, so their blocks share the twiddle lines in L2
+    const uint32_t pp = G.primeMajor ? rid % G.P : rid / G.R, ii = G.primeMajor ? rid / G.P : rid % G.R;
     if (G.skipEll && ii >= G.alpha * pp && ii < min(G.alpha * (pp + 1), G.skipEll)) return;
     const uint32_t prime = primeOf(G.pm, ii);
+    // the row's arithmetic from the host's prime mask (no dependent load):
+    // 1 FP64, 0 integer, -1 unknown (load both twiddle forms)
+    const int knownFp = G.maskOk ? (useFp && !((G.intMask[prime >> 6] >> (prime & 63)) & 1ull) ? 1 : 0) : -1;
     NttTile T;
     T.logn = logn;
     T.d = COL ? logR : 8u;
@@ -813,9 +838,11 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroupSet<NG> GS, co
 #pragma unroll
         for (int c = 0; c < kColPer; ++c) {
             const uint32_t e = min(threadIdx.x + c * NT, colTw - 1) + 1;
-            cwI[c] = gwI[e];
-            cwX[c] = gx[e];
-            cwD[c] = gwD[e];
+            if (knownFp != 0) cwD[c] = gwD[e];
+            if (knownFp != 1) {
+                cwI[c] = gwI[e];
+                cwX[c] = gx[e];
+            }
         }
     }
     // ROW pass, FP64 rows, one group per thread per round (LE = 2): every
@@ -825,7 +852,7 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroupSet<NG> GS, co
     constexpr bool kPfBuild = !COL && LE == 2;
     constexpr int kPfRounds = 8 / 2;
     double PW[kPfBuild ? kPfRounds * 3 : 1];
-    if constexpr (kPfBuild) {
+    if constexpr (kPfBuild) if (knownFp != 0) {
         const double* gd = reinterpret_cast<const double*>(gwD);
         const uint32_t gid = threadIdx.x;
 #pragma unroll
@@ -1180,9 +1207,8 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt_ks(const ArgSet<KsArgs, NG> 
     constexpr int NPAIR = (1 << LE) / 2;  // 16-byte pairs per thread
     const uint32_t n = 1u << logn;
     const uint32_t logR = logn - 8;
-    const uint32_t asel = (NG > 1 && blockIdx.y >= AS.split) ? 1u : 0u;
-    const KsArgs& A = AS.a[asel];
-    const uint32_t t = blockIdx.y - (asel ? AS.split : 0u);
+    uint32_t t;
+    const KsArgs& A = AS.a[argSel(AS, t)];
     const uint32_t prime = t < A.ell ? t : A.Lq + (t - A.ell);
     const sf_barrett B = loadBar(bar, prime);
     const u64 q = B.q;
@@ -1486,11 +1512,24 @@ struct ConstArgs {
     u64 k[SFP_MAX_LIMBS];
 };
 
-template <int OP>
-__global__ __launch_bounds__(kThreads) void k_ew(u64* __restrict__ out, const u64* __restrict__ a,
-                                                 const u64* __restrict__ b, const u64* __restrict__ c,
-                                                 sfp_limbs m, const sf_barrett* __restrict__ bar,
-                                                 uint32_t logn, ConstArgs k) {
+// Grid-stride kernels in arg-set form: set blockIdx.y of NG (a stacked pair
+// of launches runs both sets, grid.y = 2; each set loops over its own rows).
+struct EwArgs {
+    u64* out;
+    const u64 *a, *b, *c;
+    sfp_limbs m;
+    ConstArgs k;
+};
+template <int OP, int NG = 1>
+__global__ __launch_bounds__(kThreads) void k_ew(const ArgSet<EwArgs, NG> S, const sf_barrett* __restrict__ bar,
+                                                 uint32_t logn) {
+    const EwArgs& A = S.a[NG > 1 ? blockIdx.y : 0];
+    u64* __restrict__ out = A.out;
+    const u64* __restrict__ a = A.a;
+    const u64* __restrict__ b = A.b;
+    const u64* __restrict__ c = A.c;
+    const sfp_limbs m = A.m;
+    const ConstArgs& k = A.k;
     const size_t pairs = ((size_t)m.count << logn) >> 1;
     for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < pairs;
          i += (size_t)gridDim.x * kThreads) {
@@ -1571,10 +1610,22 @@ struct PtrList2 {
 };
 
 // out = sum_j ins[j] * k[j][limb]   (k: device array nin x count)
-__global__ __launch_bounds__(kThreads) void k_lin_wsum(u64* __restrict__ out, PtrList ins,
-                                                       const u64* __restrict__ k, uint32_t nin,
-                                                       sfp_limbs m, const sf_barrett* __restrict__ bar,
+struct WsumArgs {
+    u64* out;
+    PtrList ins;
+    const u64* k;
+    uint32_t nin;
+    sfp_limbs m;
+};
+template <int NG = 1>
+__global__ __launch_bounds__(kThreads) void k_lin_wsum(const ArgSet<WsumArgs, NG> S, const sf_barrett* __restrict__ bar,
                                                        uint32_t logn) {
+    const WsumArgs& A = S.a[NG > 1 ? blockIdx.y : 0];
+    u64* __restrict__ out = A.out;
+    const PtrList& ins = A.ins;
+    const u64* __restrict__ k = A.k;
+    const uint32_t nin = A.nin;
+    const sfp_limbs m = A.m;
     const size_t total = (size_t)m.count << logn;
     for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < total;
          i += (size_t)gridDim.x * kThreads) {
@@ -1757,8 +1808,18 @@ __global__ __launch_bounds__(kThreads) void k_mac_plain(u64* __restrict__ out, P
 }
 
 // out[k] = in[perm_g(k)] for every limb
-__global__ __launch_bounds__(kThreads) void k_automorph(u64* __restrict__ out, const u64* __restrict__ in,
-                                                        uint32_t g, uint32_t count, uint32_t logn) {
+struct AutArgs {
+    u64* out;
+    const u64* in;
+    uint32_t g, count;
+};
+template <int NG = 1>
+__global__ __launch_bounds__(kThreads) void k_automorph(const ArgSet<AutArgs, NG> S, const sf_barrett* __restrict__,
+                                                        uint32_t logn) {
+    const AutArgs& A = S.a[NG > 1 ? blockIdx.y : 0];
+    u64* __restrict__ out = A.out;
+    const u64* __restrict__ in = A.in;
+    const uint32_t g = A.g, count = A.count;
     const uint32_t n = 1u << logn;
     const size_t total = (size_t)count << logn;
     const u64 mask = 2ull * n - 1;
@@ -2419,18 +2480,48 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
     }
 }
 
+// prims.h sfp_key_row on the device
+__device__ __forceinline__ uint32_t keyRowOf(const sfp_key_geom& g, uint32_t p) {
+    if (!g.rows) return p;
+    return p < g.tail ? p : p < g.lq ? g.tail + (p - g.first) / g.world : g.pstart + (p - g.lq);
+}
+
 // key inner product over ext rows t < ell+K
 // ext row t (prime primeOf(pm, t)) uses key row t < pm.split ? t : keyQ +
 // (t - pm.split) of each digit's [b rows][a rows] block of keyRows rows, or
-// the row of its prime when keyQ == SFP_KEY_ROW_BY_PRIME (a whole key).
-__global__ __launch_bounds__(kThreads) void k_ks_inner(u64* __restrict__ acc0, u64* __restrict__ acc1,
-                                                       const u64* __restrict__ ext, size_t extStride,
-                                                       const u64* __restrict__ key, uint32_t beta,
-                                                       sfp_limbs pm, uint32_t keyQ, uint32_t keyRows,
-                                                       const u64* __restrict__ fold0,
-                                                       const u64* __restrict__ fold1, u64 foldK,
-                                                       const sf_barrett* __restrict__ bar, uint32_t logn,
-                                                       int accum, const u64* __restrict__ pmul) {
+// the row of its prime when keyQ == SFP_KEY_ROW_BY_PRIME (sfp_key_row: a
+// whole key, or this rank's slice of it).
+struct KsInnerArgs {
+    u64 *acc0, *acc1;
+    const u64* ext;
+    size_t extStride;
+    const u64* key;
+    uint32_t beta;
+    sfp_limbs pm;
+    uint32_t keyQ, keyRows;
+    const u64 *fold0, *fold1;
+    u64 foldK;
+    int accum;
+    const u64* pmul;
+    sfp_key_geom kg;
+};
+template <int NG = 1>
+__global__ __launch_bounds__(kThreads) void k_ks_inner(const ArgSet<KsInnerArgs, NG> S,
+                                                       const sf_barrett* __restrict__ bar, uint32_t logn) {
+    const KsInnerArgs& A = S.a[NG > 1 ? blockIdx.y : 0];
+    u64* __restrict__ acc0 = A.acc0;
+    u64* __restrict__ acc1 = A.acc1;
+    const u64* __restrict__ ext = A.ext;
+    const size_t extStride = A.extStride;
+    const u64* __restrict__ key = A.key;
+    const uint32_t beta = A.beta, keyQ = A.keyQ, keyRows = A.keyRows;
+    const sfp_limbs pm = A.pm;
+    const u64* __restrict__ fold0 = A.fold0;
+    const u64* __restrict__ fold1 = A.fold1;
+    const u64 foldK = A.foldK;
+    const int accum = A.accum;
+    const u64* __restrict__ pmul = A.pmul;
+    const sfp_key_geom& kg = A.kg;
     // two coefficients per thread: 16-byte loads of every ext / key row
     const uint32_t ell = pm.split, NP = keyRows;
     const size_t pairs = ((size_t)pm.count << logn) >> 1;
@@ -2441,7 +2532,7 @@ __global__ __launch_bounds__(kThreads) void k_ks_inner(u64* __restrict__ acc0, u
         const uint32_t t = (uint32_t)(e >> logn);
         const uint32_t x = (uint32_t)(e & (n - 1));
         const uint32_t pr = primeOf(pm, t);
-        const uint32_t kr = keyQ == SFP_KEY_ROW_BY_PRIME ? pr : (t < ell ? t : keyQ + (t - ell));
+        const uint32_t kr = keyQ == SFP_KEY_ROW_BY_PRIME ? keyRowOf(kg, pr) : (t < ell ? t : keyQ + (t - ell));
         const sf_barrett B = loadBar(bar, pr);
         Acc s0{0, 0}, s0b{0, 0}, s1{0, 0}, s1b{0, 0};
         for (uint32_t j = 0; j < beta; ++j) {
@@ -2566,7 +2657,7 @@ __global__ __launch_bounds__(kThreads) void k_fill1(unsigned char* __restrict__ 
 // launch whose grid holds the rows of both (ArgSet<T, 2>), or whose job table
 // holds the jobs of both (conversions).  Per-row arithmetic is unchanged, so
 // results are bit-identical; the sort issues about half the launches.
-enum { STK_NONE = 0, STK_NTT = 1, STK_KS = 2, STK_CONV = 3, STK_MDRS = 4 };
+enum { STK_NONE = 0, STK_NTT = 1, STK_KS = 2, STK_CONV = 3, STK_MDRS = 4, STK_Y = 5 };
 
 static uint64_t stkKey(const void* kern, uint32_t a, uint32_t b) {
     uint64_t h = 1469598103934665603ull;
@@ -2608,6 +2699,49 @@ struct MdrsPay {
 };
 using MdrsKern = void (*)(MdrsArgs, const sf_barrett*, const double*, uint32_t);
 
+// grid.y arg-set kernels (k_ew, k_automorph, k_lin_wsum, k_ks_inner): two
+// launches of one kernel become one with grid.y = 2 (the larger grid.x; each
+// set's grid-stride loop covers its own rows)
+struct YPayBase {
+    dim3 g;
+    virtual ~YPayBase() = default;
+    virtual void launch2(sfp_dev* d, hipStream_t s, const YPayBase& other) const = 0;
+};
+template <class Args>
+struct YPay : YPayBase {
+    Args a;
+    void (*k2)(ArgSet<Args, 2>, const sf_barrett*, uint32_t);
+    void launch2(sfp_dev* d, hipStream_t s, const YPayBase& other) const override {
+        const auto& o = static_cast<const YPay<Args>&>(other);
+        ArgSet<Args, 2> S;
+        S.a[0] = a;
+        S.a[1] = o.a;
+        S.split = 0;
+        S.inter = 0;
+        hipLaunchKernelGGL(k2, dim3(std::max(g.x, o.g.x), 2), dim3(kThreads), 0, s, S, d->bar, d->logn);
+    }
+};
+template <class Args>
+static void issueY(sfp_dev* d, void (*k1)(ArgSet<Args, 1>, const sf_barrett*, uint32_t),
+                   void (*k2)(ArgSet<Args, 2>, const sf_barrett*, uint32_t), dim3 g, const Args& a) {
+    ArgSet<Args, 1> S;
+    S.a[0] = a;
+    S.split = 0;
+    S.inter = 0;
+    StackRec r;
+    r.go = [=](hipStream_t s_) { hipLaunchKernelGGL(k1, g, dim3(kThreads), 0, s_, S, d->bar, d->logn); };
+    if (d->stackOn) {
+        auto P = std::make_shared<YPay<Args>>();
+        P->a = a;
+        P->k2 = k2;
+        P->g = g;
+        r.cls = STK_Y;
+        r.key = stkKey((const void*)k1, 0, 0);
+        r.pay = std::move(P);
+    }
+    issueRec(d, std::move(r));
+}
+
 // Issue the heads a and b (same class and key) as one launch on s; false if
 // their arguments cannot share one (the caller then issues them apart);
 // check: only report whether they can.
@@ -2622,6 +2756,7 @@ static bool stackMerge(sfp_dev* d, const StackRec& a, const StackRec& b, hipStre
             GS.a[0] = A.G;
             GS.a[1] = B.G;
             GS.split = A.rows;
+            GS.inter = A.rows == B.rows;
             hipLaunchKernelGGL(A.k2, dim3(A.g.x, A.rows + B.rows), dim3(A.threads), 0, s, GS, d->bar, A.tw, A.twS,
                                d->ninv, d->ninvS, d->logn, A.twD, d->qinvD, d->ninvD, d->ninvQ, A.useFp);
             return true;
@@ -2635,6 +2770,7 @@ static bool stackMerge(sfp_dev* d, const StackRec& a, const StackRec& b, hipStre
             AS.a[0] = A.a;
             AS.a[1] = B.a;
             AS.split = A.rows;
+            AS.inter = A.rows == B.rows;
             hipLaunchKernelGGL(A.k2, dim3(A.g.x, A.rows + B.rows), dim3(A.threads), 0, s, AS, d->bar, d->psi,
                                d->psiS, d->logn, d->psiD, d->qinvD, A.useFp);
             return true;
@@ -2663,6 +2799,11 @@ static bool stackMerge(sfp_dev* d, const StackRec& a, const StackRec& b, hipStre
             for (uint32_t k = 0; k < B.g.y; ++k) M.j[A.g.y + k] = B.M.j[k];
             hipLaunchKernelGGL(reinterpret_cast<MdrsKern>(A.k), dim3(A.g.x, A.g.y + B.g.y, A.g.z), dim3(kThreads), 0,
                                s, M, d->bar, d->qinvD, d->logn);
+            return true;
+        }
+        case STK_Y: {
+            if (check) return true;
+            static_cast<const YPayBase*>(a.pay.get())->launch2(d, s, *static_cast<const YPayBase*>(b.pay.get()));
             return true;
         }
         default:
@@ -3262,7 +3403,23 @@ static RowGroup rowsOf(uint32_t P, uint32_t R, sfp_limbs pm) {
 // Both passes of a (batched) NTT over the rows of G -- or only the first
 // (passes == 1: its output feeds a fused second pass, k_ntt_ks) or only the
 // second (passes == 2: a fused kernel ran the first).
-static void nttRows(sfp_dev* d, const RowGroup& G, int inverse, int passes = 3) {
+static int nttFp();
+static void nttRows(sfp_dev* d, const RowGroup& G0, int inverse, int passes = 3) {
+    RowGroup G = G0;
+    // SFHE_NTT_ROW_ORDER=0: poly-major grid rows (A/B knob)
+    static const uint32_t primeMajor = [] {
+        const char* v = std::getenv("SFHE_NTT_ROW_ORDER");
+        return (uint32_t)(!v || *v != '0');
+    }();
+    G.primeMajor = primeMajor;
+    if (!d->intMaskSet) {  // integer-arithmetic primes (60-bit, or every prime with SFHE_NTT_FP=0)
+        for (uint32_t p = 0; p < d->np && p < 128; ++p)
+            if (!nttFp() || d->hbar[p].q >= kFpPrimeBound) d->intMask[p >> 6] |= 1ull << (p & 63);
+        d->intMaskSet = true;
+    }
+    G.maskOk = d->np <= 128;
+    G.intMask[0] = d->intMask[0];
+    G.intMask[1] = d->intMask[1];
     const uint32_t rows = G.P * G.R;
     if (!rows || !limbsOk(d, G.pm, "ntt")) return;
     if (G.lift && G.liftPrime >= d->np) return (void)limbsOk(d, sfp_limbs{1, 1, G.liftPrime, G.liftPrime}, "ntt lift");
@@ -3317,6 +3474,7 @@ static void nttRows(sfp_dev* d, const RowGroup& G, int inverse, int passes = 3) 
             RowGroupSet<1> GS;
             GS.a[0] = G;
             GS.split = rows;
+            GS.inter = 0;
             const int fp = nttFp();
             StackRec r;
             r.go = [=](hipStream_t s_) {
@@ -3627,8 +3785,9 @@ static void ew(sfp_dev* d, u64* out, const u64* a, const u64* b, const u64* c, s
     ConstArgs ka;
     if (k) std::memcpy(ka.k, k, m.count * 8);
     const size_t pairs = ((size_t)m.count * d->n) / 2;
-    SFP_GO(k_ew<OP>, dim3(ewGrid(pairs)), dim3(kThreads), out, a, b, c, m,
-                       d->bar, d->logn, ka);
+    EwArgs A{out, a, b, c, m, {}};
+    A.k = ka;
+    issueY<EwArgs>(d, k_ew<OP, 1>, k_ew<OP, 2>, dim3(ewGrid(pairs)), A);
     checkLaunch(d, "elementwise");
 }
 
@@ -3675,8 +3834,7 @@ void sfp_lin_wsum(sfp_dev* d, uint64_t* out, const uint64_t* const* ins, const u
     for (uint32_t j = 0; j < nin; ++j) pl.p[j] = ins[j];
     const u64* dk = (const u64*)ringPut(d, k, (size_t)nin * m.count * 8);
     const size_t total = (size_t)m.count * d->n;
-    SFP_GO(k_lin_wsum, dim3(ewGrid(total)), dim3(kThreads), out, pl, dk, nin,
-                       m, d->bar, d->logn);
+    issueY<WsumArgs>(d, k_lin_wsum<1>, k_lin_wsum<2>, dim3(ewGrid(total)), WsumArgs{out, pl, dk, nin, m});
     checkLaunch(d, "lin_wsum");
 }
 
@@ -3740,8 +3898,7 @@ void sfp_mac_plain(sfp_dev* d, uint64_t* out, const uint64_t* const* a, const ui
 
 void sfp_automorph(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t g, sfp_limbs m) {
     const size_t total = (size_t)m.count * d->n;
-    SFP_GO(k_automorph, dim3(ewGrid(total)), dim3(kThreads), out, in, g,
-                       m.count, d->logn);
+    issueY<AutArgs>(d, k_automorph<1>, k_automorph<2>, dim3(ewGrid(total)), AutArgs{out, in, g, m.count});
     checkLaunch(d, "automorph");
 }
 
@@ -4150,8 +4307,8 @@ static void modupInnerCore(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uin
     a.ext = ext;
     a.extStride = stride;
     a.key = key;
-    a.keyRows = Lq + K;
-    a.keyQ = Lq;
+    a.keyRows = d->kg.rows ? d->kg.rows : Lq + K;  // (a sliced key: sfp_set_key_geom)
+    a.keyQ = d->kg.rows ? d->kg.pstart : Lq;
     a.acc0 = acc0;
     a.acc1 = acc1;
     a.fold0 = fold0;
@@ -4179,6 +4336,7 @@ static void modupInnerCore(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uin
         ArgSet<KsArgs, 1> AS;
         AS.a[0] = a;
         AS.split = rows;
+        AS.inter = 0;
         const int fp = nttFp();
         const dim3 g(n / (t1k ? 1024u : (uint32_t)kNttTile), rows);
         const int threads = (t1k ? 1024 : kNttTile) >> 2;
@@ -4230,6 +4388,7 @@ void sfp_ks_inner_fold(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_
                        size_t extStride, const uint64_t* key, uint32_t beta, uint32_t ell,
                        uint32_t K, uint32_t Lq, const uint64_t* fold0, const uint64_t* fold1,
                        uint64_t foldK) {
+    const uint32_t keyQ0 = d->kg.rows ? d->kg.pstart : Lq, keyRows0 = d->kg.rows ? d->kg.rows : Lq + K;
     const size_t total = (size_t)(ell + K) * d->n;
     if (fold0 && (!fold1 || ell < 1)) {
         record(d, "ks_inner_fold", hipErrorInvalidValue);
@@ -4237,21 +4396,20 @@ void sfp_ks_inner_fold(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_
     }
     // reads beta ext rows + 2*beta key rows, writes 2 accumulator rows, per limb
     timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + 2.0), [&] {
-        SFP_GO(k_ks_inner, dim3(ewGrid(total / 2)), dim3(kThreads), acc0, acc1, ext,
-                           extStride, key, beta, sfp_limbs{ell + K, ell, Lq, 0, 1}, Lq, Lq + K, fold0, fold1,
-                           foldK, d->bar, d->logn, 0, (const u64*)nullptr);
+        issueY<KsInnerArgs>(d, k_ks_inner<1>, k_ks_inner<2>, dim3(ewGrid(total / 2)),
+                                KsInnerArgs{acc0, acc1, ext, extStride, key, beta, sfp_limbs{ell + K, ell, Lq, 0, 1}, keyQ0, keyRows0, fold0, fold1, foldK, 0, (const u64*)nullptr, d->kg});
     });
     checkLaunch(d, "ks_inner");
 }
 
 void sfp_ks_inner_acc(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext, size_t extStride,
                       const uint64_t* key, uint32_t beta, uint32_t ell, uint32_t K, uint32_t Lq) {
+    const uint32_t keyQ0 = d->kg.rows ? d->kg.pstart : Lq, keyRows0 = d->kg.rows ? d->kg.rows : Lq + K;
     const size_t total = (size_t)(ell + K) * d->n;
     // reads beta ext rows + 2*beta key rows + 2 accumulator rows, writes 2, per limb
     timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + 4.0), [&] {
-        SFP_GO(k_ks_inner, dim3(ewGrid(total / 2)), dim3(kThreads), acc0, acc1, ext,
-                           extStride, key, beta, sfp_limbs{ell + K, ell, Lq, 0, 1}, Lq, Lq + K, (const u64*)nullptr,
-                           (const u64*)nullptr, (u64)0, d->bar, d->logn, 1, (const u64*)nullptr);
+        issueY<KsInnerArgs>(d, k_ks_inner<1>, k_ks_inner<2>, dim3(ewGrid(total / 2)),
+                                KsInnerArgs{acc0, acc1, ext, extStride, key, beta, sfp_limbs{ell + K, ell, Lq, 0, 1}, keyQ0, keyRows0, (const u64*)nullptr, (const u64*)nullptr, (u64)0, 1, (const u64*)nullptr, d->kg});
     });
     checkLaunch(d, "ks_inner_acc");
 }
@@ -4259,12 +4417,12 @@ void sfp_ks_inner_acc(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t
 void sfp_ks_inner_mul(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext, size_t extStride,
                       const uint64_t* key, uint32_t beta, uint32_t ell, uint32_t K, uint32_t Lq, const uint64_t* pm,
                       int accum) {
+    const uint32_t keyQ0 = d->kg.rows ? d->kg.pstart : Lq, keyRows0 = d->kg.rows ? d->kg.rows : Lq + K;
     const size_t total = (size_t)(ell + K) * d->n;
     // reads beta ext rows + 2*beta key rows + the plaintext row (+ 2 accumulator rows), writes 2, per limb
     timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + (accum ? 5.0 : 3.0)), [&] {
-        SFP_GO(k_ks_inner, dim3(ewGrid(total / 2)), dim3(kThreads), acc0, acc1, ext,
-                           extStride, key, beta, sfp_limbs{ell + K, ell, Lq, 0, 1}, Lq, Lq + K, (const u64*)nullptr,
-                           (const u64*)nullptr, (u64)0, d->bar, d->logn, accum, pm);
+        issueY<KsInnerArgs>(d, k_ks_inner<1>, k_ks_inner<2>, dim3(ewGrid(total / 2)),
+                                KsInnerArgs{acc0, acc1, ext, extStride, key, beta, sfp_limbs{ell + K, ell, Lq, 0, 1}, keyQ0, keyRows0, (const u64*)nullptr, (const u64*)nullptr, (u64)0, accum, pm, d->kg});
     });
     checkLaunch(d, "ks_inner_mul");
 }
@@ -4691,11 +4849,15 @@ void sfp_ks_inner_map(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t
     if (!pm.count || !limbsOk(d, pm, "ks_inner_map")) return;
     const size_t total = (size_t)pm.count * d->n;
     timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + (accum ? 4.0 : 2.0)), [&] {
-        SFP_GO(k_ks_inner, dim3(ewGrid(total / 2)), dim3(kThreads), acc0, acc1, ext, extStride,
-                           key, beta, pm, keyQ, keyRows, (const u64*)nullptr, (const u64*)nullptr, (u64)0, d->bar,
-                           d->logn, accum, (const u64*)nullptr);
+        issueY<KsInnerArgs>(d, k_ks_inner<1>, k_ks_inner<2>, dim3(ewGrid(total / 2)),
+                                KsInnerArgs{acc0, acc1, ext, extStride, key, beta, pm, keyQ, keyRows, (const u64*)nullptr, (const u64*)nullptr, (u64)0, accum, (const u64*)nullptr, d->kg});
     });
     checkLaunch(d, "ks_inner_map");
+}
+
+void sfp_set_key_geom(sfp_dev* d, const sfp_key_geom* g) {
+    stackFlush(d);  // (recorded launches keep the geometry they were issued with)
+    d->kg = g ? *g : sfp_key_geom{};
 }
 
 int sfp_comm_uid(void* uid128) {

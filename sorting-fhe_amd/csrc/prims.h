@@ -375,6 +375,24 @@ void sfp_rescale_rows(sfp_dev* d, uint64_t* out, const uint64_t* in, const uint6
 // of its prime (a whole key, key_rows = Lq + K: row r is prime r).
 //   accum: acc (+)= the inner product (as sfp_ks_inner_acc)
 #define SFP_KEY_ROW_BY_PRIME 0xFFFFFFFFu
+
+// Switching-key geometry (sliced keys).  By default a key digit
+// is [b rows][a rows] of Lq + K rows each, row r holding prime r.  A limb-
+// sharded rank keeps a slice: the `tail` Q rows of the replicated levels
+// (primes 0 .. tail-1), its own dealt Q primes >= tail (first, first + world,
+// ... < lq), then the K P rows, `rows` in all (pstart = rows - K):
+//   row(p) = p < tail ? p : p < lq ? tail + (p - first) / world : pstart + (p - lq)
+// Every key prim then reads that layout: ext row t < ell of a replicated level
+// reads row t, its P rows row pstart + (t - ell), and SFP_KEY_ROW_BY_PRIME
+// reads row(prime).  rows == 0: whole keys (the default).
+typedef struct {
+    uint32_t rows, pstart, tail, world, first, lq;
+} sfp_key_geom;
+void sfp_set_key_geom(sfp_dev* d, const sfp_key_geom* g);
+static inline uint32_t sfp_key_row(const sfp_key_geom* g, uint32_t p) {
+    if (!g->rows) return p;
+    return p < g->tail ? p : p < g->lq ? g->tail + (p - g->first) / g->world : g->pstart + (p - g->lq);
+}
 void sfp_ks_inner_map(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
                       size_t ext_stride, const uint64_t* key, uint32_t beta, sfp_limbs pm,
                       uint32_t keyQ, uint32_t key_rows, int accum);

@@ -41,7 +41,7 @@ ABI_SYMBOLS = [
     "sfhe_bootstrap_setup", "sfhe_bootstrap_depth", "sfhe_bootstrap",
     "sfhe_sorter_sort_bitonic", "sfhe_kway_sort", "sfhe_kway_params",
     "sfhe_save", "sfhe_load", "sfhe_ct_save", "sfhe_ct_load",
-    "sfhe_kway_create", "sfhe_kway_run", "sfhe_kway_destroy", "sfhe_shard_tail",
+    "sfhe_kway_create", "sfhe_kway_run", "sfhe_kway_destroy", "sfhe_shard_tail", "sfhe_key_rows",
     "sfhe_groups_rccl", "sfhe_groups_host", "sfhe_groups",
     "sfhe_encode_counts", "sfhe_bootstrap_graphs",
 ]
@@ -152,6 +152,7 @@ _SIGS = {
     "sfhe_shard_rccl": (C.c_int, [_VP, C.c_int, C.c_int, _VP]),
     "sfhe_shard_host": (C.c_int, [_VP, C.c_int, C.c_int, _AG, _BC, _VP]),
     "sfhe_shard_tail": (C.c_int, [_VP, _PU32]),
+    "sfhe_key_rows": (C.c_int, [_VP, _PU32]),
     "sfhe_groups_rccl": (C.c_int, [_VP, C.c_int, C.c_int, _VP]),
     "sfhe_groups_host": (C.c_int, [_VP, C.c_int, C.c_int, _AG, _VP]),
     "sfhe_groups": (C.c_int, [_VP, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
@@ -323,6 +324,12 @@ class Engine:
         """Replicated-tail limb count of a sharded context (0: unsharded)."""
         v = C.c_uint32()
         self._chk(self.lib.sfhe_shard_tail(self.ctx, C.byref(v)))
+        return v.value
+
+    def key_rows(self) -> int:
+        """Rows per digit part of this rank's switching keys (a slice when sharded)."""
+        v = C.c_uint32()
+        self._chk(self.lib.sfhe_key_rows(self.ctx, C.byref(v)))
         return v.value
 
     # -- context --

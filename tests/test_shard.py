@@ -236,3 +236,35 @@ def test_batch_groups_arguments(oracle_lib):
         e2.groups_host(0, 2, sfhe.ThreadComm(2))
     with pytest.raises(sfhe.SfheError):  # the oracle has no RCCL
         e2.groups_rccl(0, 2, bytes(128))
+
+
+@pytest.mark.parametrize("world,tail", [(3, 4), (2, 0), (4, 16)])
+def test_sliced_keys_oracle(oracle_lib, world, tail, monkeypatch):
+    """each rank keeps only its slice of every switching key --
+    the Q rows of the replicated tail, its own dealt Q rows above it and the P
+    rows (sfp_key_geom) -- and every op stays bit-identical to the unsharded
+    context (the sharded tests above run with sliced keys by default)."""
+    monkeypatch.setenv("SFHE_SHARD_TAIL", str(tail))
+    ref_e = sfhe.Engine("oracle", **OPS_KW)
+    info = ref_e.info()
+    nq, npr = info["num_q"], info["num_p"]
+    assert ref_e.key_rows() == nq + npr
+    ref = ops_program(ref_e)
+
+    def prog(e):
+        out = ops_program(e)
+        out["key_rows"] = np.array([e.key_rows()])
+        return out
+
+    outs = sfhe.run_sharded_threads("oracle", world, prog, **OPS_KW)
+    t = min(tail, nq)
+    for r in range(world):
+        want = t + sum(1 for p in range(t, nq) if p % world == r) + npr
+        assert int(outs[r].pop("key_rows")[0]) == want
+        assert want < nq + npr or t == nq  # (a tail over every limb: nothing to slice)
+        compare(ref, outs[r])
+    monkeypatch.setenv("SFHE_KEY_SLICE", "0")  # whole keys: the same residues
+    outs = sfhe.run_sharded_threads("oracle", world, prog, **OPS_KW)
+    for r in range(world):
+        assert int(outs[r].pop("key_rows")[0]) == nq + npr
+        compare(ref, outs[r])
