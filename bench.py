@@ -209,7 +209,7 @@ def kway_leg(device, k=2, M=10, logn=17):
     ct = eng.encrypt(x.tolist())
     sorter = eng.kway(k, M)
     ms = []
-    for _ in range(2):  # cold (encodes masks / diagonals), warm
+    for _ in range(3):  # cold (encodes masks / diagonals), captured into a hipGraph, replayed
         eng.sync()
         t0 = time.perf_counter()
         out = sorter.sort(ct, 3, 2, 5, depth)  # (3, d_f, d_g) as the test passes it
@@ -217,7 +217,9 @@ def kway_leg(device, k=2, M=10, logn=17):
         ms.append((time.perf_counter() - t0) * 1e3)
     err = float(np.max(np.abs(np.array(eng.decrypt(out))[:N] - np.sort(x))))
     return {"workload": f"k-way sort N={N} (k={k}, M={M}) @ ring 2^{logn}, depth {depth}, bootstrapping {budget}",
-            "ms": ms[-1], "ms_cold": ms[0],
+            "ms": ms[-1], "ms_cold": ms[0], "ms_capture": ms[1], "graph_nodes": sorter.graph_nodes(),
+            "note": "ms: the replay of the whole sort's hipGraph (stages + bootstraps); ms_capture: the "
+                    "second sort, which captures it",
             "bootstrap_keygen_s": setup_s, "level": out.level, "max_err": err,
             "stages": M + M * (M - 1) // 2 * ((k + 1) // 2)}
 
@@ -607,6 +609,11 @@ def main(argv=None):
         result["replicas"] = replicas
     if dog:
         dog.cancel()
+    def leg(name):  # progress on stderr (a crash inside a leg names it)
+        sys.stderr.write(f"bench: {name}\n")
+        sys.stderr.flush()
+
+    leg(f"timed region done: {dt / args.steps * 1e3:.2f} ms per sort")
     if args.c5 and (world == 1 or mode == "rccl"):
         import threading
 
@@ -623,6 +630,7 @@ def main(argv=None):
         c5_dog.start()
         if args.c5_eager:
             os.environ["SFHE_GRAPH"] = "0"  # read per sort by the sorter
+        leg("c5 leg")
         try:
             # config 5's sort has one batch per phase at 2^17: nothing to split,
             # so its ranks limb-shard over all N
@@ -631,16 +639,19 @@ def main(argv=None):
             result["c5"] = {"error": str(e)}
         c5_dog.cancel()
     if rank == 0 and world == 1 and args.hybrid1:
+        leg("hybrid1 leg")
         try:
             result["hybrid1"] = hybrid1_leg(device)
         except Exception as e:  # noqa: BLE001 -- an extra leg must not lose the metric line
             result["hybrid1"] = {"error": str(e)}
     if rank == 0 and world == 1 and args.kway:
+        leg("kway leg")
         try:
             result["kway"] = kway_leg(device)
         except Exception as e:  # noqa: BLE001
             result["kway"] = {"error": str(e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        leg("cpu baseline")
         try:
             result["cpu_baseline"] = cpu_baseline(N, logn, secure, depth, rots, cfg)
         except Exception as e:  # the oracle is optional on a box without its build

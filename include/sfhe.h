@@ -268,6 +268,10 @@ typedef struct sfhe_kway sfhe_kway;
 int sfhe_kway_create(sfhe_ctx* c, uint32_t N, int k, int M, sfhe_kway** out);
 int sfhe_kway_run(sfhe_kway* s, const sfhe_ct* in, int n, int dg, int df, uint32_t mult_depth, sfhe_ct** out);
 void sfhe_kway_destroy(sfhe_kway* s);
+/* Nodes of the handle's captured sort graph (0: none yet).  The first sort of
+ * a shape runs eagerly, the second is captured whole -- stages and the
+ * bootstraps between them -- and later sorts replay it (SFHE_GRAPH=0: eager). */
+int sfhe_kway_graph_nodes(const sfhe_kway* s, uint64_t* nodes);
 /* KWayAdapter<N>::getSizeParameters (kway_adapter.h:41-64): batch (next power
  * of two >= N), depth 40, first modulus 60 / scale 59 bits, level budget
  * {4,4} (N <= 128) or {5,5}, the +-2^i rotation keys below N. */

@@ -118,14 +118,22 @@ void Sorter::comparisonForSort2(Ct& ctxt, std::vector<std::vector<int>>& indices
     ctxt_comp2 = comp.compare(m_cc, ctxt, prev2, SignFunc::CompositeSign, Cfg);
 }
 
+int Sorter::stageCount() const { return (int)(m_M + m_M * (m_M - 1) / 2 * ((m_k + 1) / 2)); }
+
 void Sorter::sorter(Ct& ctxt, Ct& ctxt_out, SignConfig& Cfg) {
     assert((m_k == 2 || m_k == 3 || m_k == 5) && "Only k=2,3,5 is supported");
+    if (!runStages(ctxt, 0, stageCount(), Cfg)) return;
+    ctxt_out = ctxt;
+    std::cout << "Level of output: " << ctxt->GetLevel() << std::endl;
+    PRINT_PT(m_enc, ctxt_out);
+}
+
+bool Sorter::runStages(Ct& ctxt, int first, int last, SignConfig& Cfg) {
     constexpr bool verbose = false;
     const int depth = Cfg.multDepth;
     const long k = m_k;
-    const int stages = (int)(m_M + m_M * (m_M - 1) / 2 * ((m_k + 1) / 2));
     Ct fix, c1, c2;
-    for (int stage = 0; stage < stages; ++stage) {
+    for (int stage = first; stage < last; ++stage) {
         std::cout << " == stage " << stage << " == " << std::endl;
         const auto [m, logDist, slope] = sortType((int)m_k, (int)m_M, stage);
         const long shift = getRotateDistance(m_k, logDist, slope);
@@ -184,14 +192,12 @@ void Sorter::sorter(Ct& ctxt, Ct& ctxt_out, SignConfig& Cfg) {
             ctxt = m_cc->EvalAdd(two, fix);
         } else {
             std::cout << "[Sorter::Sorter] ERROR : no matching k & slope" << std::endl;
-            return;
+            return false;
         }
         std::cout << " == End stage " << stage << " == " << std::endl;
         if (std::getenv("SFHE_KWAY_DEBUG") && m_privateKey) debugWithSk(ctxt, 8, "stage " + std::to_string(stage));
     }
-    ctxt_out = ctxt;
-    std::cout << "Level of output: " << ctxt->GetLevel() << std::endl;
-    PRINT_PT(m_enc, ctxt_out);
+    return true;
 }
 
 }  // namespace kwaySort

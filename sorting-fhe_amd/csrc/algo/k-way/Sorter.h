@@ -58,6 +58,10 @@ class Sorter : public SortUtils {
 
     // the whole network (Sorter.cpp:284-404)
     void sorter(Ciphertext<DCRTPoly>& ctxt, Ciphertext<DCRTPoly>& ctxt_out, SignConfig& Cfg);
+    // engine extension: the network's stages [first, last) on ctxt (in place;
+    // false: no stage schedule for this k) -- the pieces KWayAdapter captures
+    int stageCount() const;
+    bool runStages(Ciphertext<DCRTPoly>& ctxt, int first, int last, SignConfig& Cfg);
 
   protected:
     // levels a stage of each sub-sorter size needs after its comparison

@@ -5,7 +5,10 @@
 
 #include <cassert>
 #include <cmath>
+#include <cstdlib>
+#include <algorithm>
 #include <memory>
+#include <vector>
 
 #include "k-way/Sorter.h"
 #include "key/privatekey-fwd.h"
@@ -43,16 +46,106 @@ class KWayAdapter : public SortBase<N> {
         parameters.SetMultiplicativeDepth(40);
     }
 
-    // (Not graph-captured, unlike DirectSort::sort: a captured graph pins
-    // every buffer it touches for its lifetime.  One hipGraph per stage was
-    // tried at N = 1024 @ 2^17: each stage is ~4.1 k nodes, and the capture
-    // of stage 17 failed on a host synchronisation -- the pool, whose blocks
-    // 16 captured stages now pinned, had to grow.)
+    // hipGraph replay (BASELINE config 4: "rotation / key-switch heavy,
+    // hipGraph capture"), as DirectSort::sort: the stage schedule (reference
+    // src/k-way/Sorter.cpp:284-400) and its bootstraps depend only on (N, k,
+    // M, the input's level and slots, the sign configuration), never on the
+    // data.  The first sort of a shape runs eagerly (it encodes the masks and
+    // bootstrapping diagonals); the second is captured -- every stage's
+    // comparisons, masked rotations and sub-sorters together with the
+    // bootstraps between them (a bootstrap inside a capture records its
+    // launches into the enclosing graph) -- as a chain of graphs of
+    // SFHE_KWAY_CHUNK stages each (default 14: four graphs of ~40 k nodes at
+    // N = 1024, where one graph of the whole sort, 159 k nodes, crashed the
+    // HIP runtime at instantiation), each reading the previous one's output;
+    // later sorts copy their input in and replay the chain.  A captured graph
+    // pins the pool blocks it touches, so a chunk pins one working set (one
+    // graph per stage pinned 55 and ran the pool out, round 3).  SFHE_GRAPH=0,
+    // or a capture that fails (a host synchronisation inside: a debug
+    // decrypt), runs eagerly.
     Ciphertext<DCRTPoly> sort(const Ciphertext<DCRTPoly>& input_array, SignFunc, SignConfig& Cfg) override {
-        return sortEager(input_array, Cfg);
+        const char* gv = std::getenv("SFHE_GRAPH");
+        if (m_graphOff || (gv && *gv == '0')) return sortEager(input_array, Cfg);
+        const Key key{input_array->GetLevel(), input_array->GetSlots(), Cfg.compos.n, Cfg.compos.dg, Cfg.compos.df,
+                      Cfg.multDepth};
+        if (!(m_graph && m_graph->key == key)) {
+            if (!(m_warm && m_warmKey == key)) {  // first sort of this shape: eager
+                m_warm = true;
+                m_warmKey = key;
+                return sortEager(input_array, Cfg);
+            }
+            m_graph.reset();
+            auto g = std::make_unique<Graph>();
+            g->key = key;
+            m_cc->Settle(input_array);
+            g->in = input_array->Clone();
+            m_cc->Settle(g->in);
+            const int stages = m_sorter->stageCount(), per = chunkStages();
+            Ciphertext<DCRTPoly> x = g->in;
+            for (int s0 = 0; s0 < stages; s0 += per) {
+                if (!m_cc->BeginCapture()) {
+                    m_graphOff = true;
+                    return sortEager(input_array, Cfg);
+                }
+                bool ok = false;
+                try {
+                    ok = m_sorter->runStages(x, s0, std::min(stages, s0 + per), Cfg);
+                } catch (...) {
+                    m_cc->EndCapture(nullptr);
+                    m_graphOff = true;
+                    throw;
+                }
+                auto cg = m_cc->EndCapture(ok ? x : nullptr);
+                if (!ok || !cg) {  // (an abandoned capture ran nothing: the whole sort again, eagerly)
+                    m_graphOff = true;
+                    return sortEager(input_array, Cfg);
+                }
+                m_cc->Launch(cg);  // (this chunk's work: the next capture reads its output)
+                g->chain.push_back(cg);
+            }
+            g->out = x;
+            m_graph = std::move(g);
+        } else {
+            if (m_graph->in != input_array) m_cc->CopyCiphertextInto(m_graph->in, input_array);
+            for (const auto& cg : m_graph->chain) m_cc->Launch(cg);
+        }
+        auto ctxt_out = m_graph->out->Clone();
+        ctxt_out->SetSlots(m_graph->out->GetSlots());
+        std::cout << "Level of output: " << ctxt_out->GetLevel() << std::endl;  // (Sorter::sorter's last prints)
+        PRINT_PT(m_enc, ctxt_out);
+        return ctxt_out;
     }
+    // nodes of the captured sort's graphs (0: none yet / eager)
+    size_t graphNodes() const {
+        size_t n = 0;
+        if (m_graph)
+            for (const auto& cg : m_graph->chain) n += m_cc->GraphNodes(cg);
+        return n;
+    }
+    ~KWayAdapter() override { m_graph.reset(); }
 
   private:
+    struct Key {
+        uint32_t level, slots;
+        int n, dg, df, depth;
+        bool operator==(const Key& o) const {
+            return level == o.level && slots == o.slots && n == o.n && dg == o.dg && df == o.df && depth == o.depth;
+        }
+    };
+    struct Graph {
+        std::vector<std::shared_ptr<CryptoContextImpl<DCRTPoly>::CapturedGraph>> chain;
+        Ciphertext<DCRTPoly> in, out;
+        Key key{};
+    };
+    static int chunkStages() {
+        const char* v = std::getenv("SFHE_KWAY_CHUNK");
+        const int c = v ? std::atoi(v) : 14;
+        return c > 0 ? c : 14;
+    }
+    std::unique_ptr<Graph> m_graph;
+    Key m_warmKey{};
+    bool m_warm = false, m_graphOff = false;
+
     Ciphertext<DCRTPoly> sortEager(const Ciphertext<DCRTPoly>& input_array, SignConfig& Cfg) {
         Ciphertext<DCRTPoly> in = input_array->Clone(), out;
         m_sorter->sorter(in, out, Cfg);

@@ -614,6 +614,7 @@ namespace {
 struct KWayBase {
     virtual ~KWayBase() = default;
     virtual Ct run(const Ct& in, SignConfig& cfg) = 0;
+    virtual size_t graphNodes() const = 0;
 };
 template <int N>
 struct KWayImpl : KWayBase {
@@ -622,6 +623,7 @@ struct KWayImpl : KWayBase {
         : a(c->cc, c->keys.publicKey, c->keys.secretKey,
             std::make_shared<Encryption>(c->cc, c->keys.publicKey), k, M) {}
     Ct run(const Ct& in, SignConfig& cfg) override { return a.sort(in, SignFunc::CompositeSign, cfg); }
+    size_t graphNodes() const override { return a.graphNodes(); }
 };
 std::unique_ptr<KWayBase> makeKWay(sfhe_ctx* c, uint32_t N, int k, int M) {
     switch (N) {
@@ -667,6 +669,12 @@ int sfhe_kway_run(sfhe_kway* s, const sfhe_ct* in, int n, int dg, int df, uint32
 }
 
 void sfhe_kway_destroy(sfhe_kway* s) { delete s; }
+
+int sfhe_kway_graph_nodes(const sfhe_kway* s, uint64_t* nodes) {
+    REQUIRE(s && nodes, "null argument");
+    *nodes = s->impl->graphNodes();
+    return SFHE_OK;
+}
 
 int sfhe_kway_params(uint32_t N, uint32_t* batch, uint32_t* mult_depth, uint32_t* budget_c2s, uint32_t* budget_s2c,
                      int32_t* rotations, size_t cap, size_t* count) {

@@ -136,8 +136,6 @@ struct sfp_dev {
     std::vector<sfp_event*> stackFreedEv;  // freed inside the region: reusable after the flush
     uint64_t stkMerged = 0, stkSingle = 0;  // launches issued as merged pairs / alone
     sfp_key_geom kg = {};          // switching-key geometry (sfp_set_key_geom; rows 0: whole keys)
-    uint64_t intMask[2] = {0, 0};  // prime p (< 128) runs integer NTT butterflies (nttRows)
-    bool intMaskSet = false;
     uint32_t stkFam = ~0u;  // timedLaunch's family while it records (stacked)
     double stkBytes = 0;
     hipStream_t st() const { return streams[(serial || stackOn) ? 0 : cur]; }
@@ -701,9 +699,6 @@ struct RowGroup {
     uint32_t skipEll;      // >0: skip rows alpha*p <= i < min(alpha*(p+1), skipEll) (ModUp own digit)
     uint32_t lift, liftPrime;
     uint32_t epi, addMask;  // addMask bit p: accumulate into eout for polynomial p
-    uint32_t primeMajor;    // grid row order: prime-major (rows of one prime adjacent) or poly-major
-    uint32_t maskOk;        // intMask valid (every prime index < 128)
-    uint64_t intMask[2];    // bit p: prime p runs the integer butterflies
     RowPtr eadd;            // epi with eadd.base: eout += eadd * k2_i
     // epi with tA0: eadd is the tensor product of (tA0, tA1) and (tB0, tB1)
     // formed here (row i, n words per row): a0 b0 for polynomial 0, a0 b1 +
@@ -785,14 +780,9 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroupSet<NG> GS, co
     const uint32_t logR = logn - 8;
     uint32_t rid;
     const RowGroup& G = GS.a[argSel(GS, rid)];
-    // prime-major rows (the default): the P polynomials' rows of one prime
-    // are adjacent in the grid, so their blocks share the twiddle lines in L2
-    const uint32_t pp = G.primeMajor ? rid % G.P : rid / G.R, ii = G.primeMajor ? rid / G.P : rid % G.R;
+    const uint32_t pp = rid / G.R, ii = rid % G.R;
     if (G.skipEll && ii >= G.alpha * pp && ii < min(G.alpha * (pp + 1), G.skipEll)) return;
     const uint32_t prime = primeOf(G.pm, ii);
-    // the row's arithmetic from the host's prime mask (no dependent load):
-    // 1 FP64, 0 integer, -1 unknown (load both twiddle forms)
-    const int knownFp = G.maskOk ? (useFp && !((G.intMask[prime >> 6] >> (prime & 63)) & 1ull) ? 1 : 0) : -1;
     NttTile T;
     T.logn = logn;
     T.d = COL ? logR : 8u;
@@ -838,11 +828,9 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroupSet<NG> GS, co
 #pragma unroll
         for (int c = 0; c < kColPer; ++c) {
             const uint32_t e = min(threadIdx.x + c * NT, colTw - 1) + 1;
-            if (knownFp != 0) cwD[c] = gwD[e];
-            if (knownFp != 1) {
-                cwI[c] = gwI[e];
-                cwX[c] = gx[e];
-            }
+            cwI[c] = gwI[e];
+            cwX[c] = gx[e];
+            cwD[c] = gwD[e];
         }
     }
     // ROW pass, FP64 rows, one group per thread per round (LE = 2): every
@@ -852,7 +840,7 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroupSet<NG> GS, co
     constexpr bool kPfBuild = !COL && LE == 2;
     constexpr int kPfRounds = 8 / 2;
     double PW[kPfBuild ? kPfRounds * 3 : 1];
-    if constexpr (kPfBuild) if (knownFp != 0) {
+    if constexpr (kPfBuild) {
         const double* gd = reinterpret_cast<const double*>(gwD);
         const uint32_t gid = threadIdx.x;
 #pragma unroll
@@ -3405,21 +3393,7 @@ static RowGroup rowsOf(uint32_t P, uint32_t R, sfp_limbs pm) {
 // second (passes == 2: a fused kernel ran the first).
 static int nttFp();
 static void nttRows(sfp_dev* d, const RowGroup& G0, int inverse, int passes = 3) {
-    RowGroup G = G0;
-    // SFHE_NTT_ROW_ORDER=0: poly-major grid rows (A/B knob)
-    static const uint32_t primeMajor = [] {
-        const char* v = std::getenv("SFHE_NTT_ROW_ORDER");
-        return (uint32_t)(!v || *v != '0');
-    }();
-    G.primeMajor = primeMajor;
-    if (!d->intMaskSet) {  // integer-arithmetic primes (60-bit, or every prime with SFHE_NTT_FP=0)
-        for (uint32_t p = 0; p < d->np && p < 128; ++p)
-            if (!nttFp() || d->hbar[p].q >= kFpPrimeBound) d->intMask[p >> 6] |= 1ull << (p & 63);
-        d->intMaskSet = true;
-    }
-    G.maskOk = d->np <= 128;
-    G.intMask[0] = d->intMask[0];
-    G.intMask[1] = d->intMask[1];
+    const RowGroup& G = G0;
     const uint32_t rows = G.P * G.R;
     if (!rows || !limbsOk(d, G.pm, "ntt")) return;
     if (G.lift && G.liftPrime >= d->np) return (void)limbsOk(d, sfp_limbs{1, 1, G.liftPrime, G.liftPrime}, "ntt lift");
@@ -3653,7 +3627,7 @@ sfp_graph* sfp_capture_end(sfp_dev* d) {
     if (hipGraphGetNodes(g->g, nullptr, &g->nodes) != hipSuccess) g->nodes = 0;
     static const size_t maxNodes = [] {  // SFHE_GRAPH_MAX_NODES: larger captures fall back to eager
         const char* v = std::getenv("SFHE_GRAPH_MAX_NODES");
-        return v ? (size_t)std::atoll(v) : (size_t)200000;
+        return v ? (size_t)std::atoll(v) : (size_t)600000;  // (the k-way sort: ~225 k)
     }();
     if (std::getenv("SFHE_GRAPH_DEBUG")) std::fprintf(stderr, "[sfhe] captured graph: %zu nodes\n", g->nodes);
     if (g->nodes > maxNodes) {

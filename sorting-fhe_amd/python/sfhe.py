@@ -41,7 +41,8 @@ ABI_SYMBOLS = [
     "sfhe_bootstrap_setup", "sfhe_bootstrap_depth", "sfhe_bootstrap",
     "sfhe_sorter_sort_bitonic", "sfhe_kway_sort", "sfhe_kway_params",
     "sfhe_save", "sfhe_load", "sfhe_ct_save", "sfhe_ct_load",
-    "sfhe_kway_create", "sfhe_kway_run", "sfhe_kway_destroy", "sfhe_shard_tail", "sfhe_key_rows",
+    "sfhe_kway_create", "sfhe_kway_run", "sfhe_kway_destroy", "sfhe_kway_graph_nodes", "sfhe_shard_tail",
+    "sfhe_key_rows",
     "sfhe_groups_rccl", "sfhe_groups_host", "sfhe_groups",
     "sfhe_encode_counts", "sfhe_bootstrap_graphs",
 ]
@@ -135,6 +136,7 @@ _SIGS = {
     "sfhe_kway_create": (C.c_int, [_VP, _U32, C.c_int, C.c_int, _PVP]),
     "sfhe_kway_run": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_int, _U32, _PVP]),
     "sfhe_kway_destroy": (None, [_VP]),
+    "sfhe_kway_graph_nodes": (C.c_int, [_VP, _PU64]),
     "sfhe_load": (C.c_int, [C.c_char_p, _PVP]),
     "sfhe_ct_save": (C.c_int, [_VP, _VP, C.c_char_p]),
     "sfhe_ct_load": (C.c_int, [_VP, C.c_char_p, _PVP]),
@@ -611,6 +613,12 @@ class KWay:
 
     def sort(self, ct: "Ct", n: int = 3, dg: int = 2, df: int = 2, mult_depth: int = 40) -> "Ct":
         return self.eng._new(self.eng.lib.sfhe_kway_run, self.h, ct.h, n, dg, df, mult_depth)
+
+    def graph_nodes(self) -> int:
+        """Nodes of the captured sort graph (0: none yet / eager)."""
+        v = C.c_uint64()
+        self.eng._chk(self.eng.lib.sfhe_kway_graph_nodes(self.h, C.byref(v)))
+        return v.value
 
 
 def kway_params(N: int, backend: str = "hip"):

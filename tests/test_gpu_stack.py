@@ -1,4 +1,5 @@
-"""Stacked launches (prims.h sfp_stack_*, DESIGN.md §4 "stacked batches"):
+"""Stacked launches (prims.h sfp_stack_*, DESIGN.md §4 "stacked batches";
+SFHE_STACK_BATCHES=1 -- off by default, two streams measured faster):
 the sort's batches run the same op sequence on their lanes; inside a stacked
 region their identical ops are issued as ONE launch each (NTT passes, fused
 key-switch passes, conversions, ModDown+rescale conversions), the rest in an
@@ -34,7 +35,8 @@ def sort_pair(N, logn):
 
 
 @pytest.mark.parametrize("N,logn,batches", [(128, 14, 2), (256, 15, 4)])
-def test_stacked_sort_bitexact(hip_lib, oracle_lib, N, logn, batches):
+def test_stacked_sort_bitexact(hip_lib, oracle_lib, N, logn, batches, monkeypatch):
+    monkeypatch.setenv("SFHE_STACK_BATCHES", "1")  # (off by default: DESIGN.md §4)
     res, x = sort_pair(N, logn)
     eo, _, (ref,) = res["oracle"]
     eh, sh, outs = res["hip"]

@@ -122,3 +122,36 @@ def test_kway_handle_oracle(oracle_lib):
     h = ctypes.c_void_p()
     assert e.lib.sfhe_kway_create(e.ctx, 12, 2, 3, ctypes.byref(h)) != sfhe.SFHE_OK
     assert "k^M" in e.lib.sfhe_last_error().decode()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,k,M,logn", [(8, 2, 3, 12), (27, 3, 3, 13)])
+def test_kway_graph_replay_hip(hip_lib, oracle_lib, N, k, M, logn):
+    """The k-way network as a hipGraph (BASELINE config 4): a persistent
+    adapter sorts eagerly, then captures the whole sort -- every stage's
+    comparisons, masked rotations and sub-sorters with the bootstraps between
+    them -- and replays it.  Eager, captured and replayed sorts are the
+    oracle's residues bit for bit; a new input through the replayed graph
+    sorts correctly."""
+    batch, depth, budget, rots = sfhe.kway_params(N, "hip")
+    kw = dict(mult_depth=depth, ring_dim=1 << logn, batch_size=batch, scaling_mod_size=59, rotations=rots,
+              seed=11)
+    x = np.random.default_rng(3).permutation(N) / N
+    ref = sfhe.Engine("oracle", **kw)
+    ref.set_quiet(True)
+    ref.bootstrap_setup(budget, batch)
+    want = ref.kway(k, M).sort(ref.encrypt(x.tolist()), 3, 2, 2, depth).download()
+    e = sfhe.Engine("hip", **kw)
+    e.set_quiet(True)
+    e.bootstrap_setup(budget, batch)
+    s = e.kway(k, M)
+    ct = e.encrypt(x.tolist())
+    outs = [s.sort(ct, 3, 2, 2, depth) for _ in range(3)]  # eager, captured, replayed
+    nodes = s.graph_nodes()
+    print(f"k-way N={N} (k={k}, M={M}) @ 2^{logn}: graph of {nodes} nodes")
+    assert nodes > 100
+    for i, o in enumerate(outs):
+        assert np.array_equal(o.download(), want), f"sort {i} differs from the oracle"
+    y = np.random.default_rng(4).permutation(N) / N
+    o = s.sort(e.encrypt(y.tolist()), 3, 2, 2, depth)
+    assert np.max(np.abs(np.array(e.decrypt(o))[:N] - np.sort(y))) < 0.01
