@@ -161,6 +161,13 @@ void sfp_serialize(sfp_dev* d, int on) { (void)d; (void)on; }
 /* one synchronous lane: nothing to stack */
 void sfp_stack_begin(sfp_dev* d) { (void)d; }
 void sfp_stack_end(sfp_dev* d) { (void)d; }
+int sfp_batch_begin(sfp_dev* d, uint32_t count) {
+    (void)d;
+    (void)count;
+    return 0;
+}
+void sfp_batch_lane(sfp_dev* d, uint32_t i) { (void)d; (void)i; }
+void sfp_batch_end(sfp_dev* d) { (void)d; }
 void sfp_stack_stats(sfp_dev* d, uint64_t* merged, uint64_t* single) {
     (void)d;
     if (merged) *merged = 0;

@@ -71,7 +71,18 @@ struct Val {
     bool isConst = true;
     double c = 0.0;
     Ct ct;
+    int node = -1;  // PSEvaluator::build: the value of node `node` once evaluated
 };
+
+// SFHE_PS_WAVES=0: the recursive evaluation order (every product in turn)
+// instead of the level-synchronous one (A/B knob; the same values)
+bool psWaves() {
+    static const bool on = [] {
+        const char* v = std::getenv("SFHE_PS_WAVES");
+        return !v || *v != '0';
+    }();
+    return on;
+}
 
 class PSEvaluator {
   public:
@@ -85,10 +96,25 @@ class PSEvaluator {
         // where the error of each doubling already grows 4x) that is what
         // the series' error is made of.  (A lazily rescaled product gets the
         // same by adding before its rescale; the series holds those off.)
-        for (uint32_t j = 2; j <= k; ++j) {
-            const Ct& a = T[j / 2];
-            Ct prod = cc->EvalMult(doubled(j / 2), j % 2 == 0 ? a : T[j / 2 + 1]);
-            T[j] = (j % 2 == 0) ? cc->EvalAdd(prod, -1.0) : cc->EvalSub(prod, atLevel(1, prod->GetLevel()));
+        // T_j for j in (2^i, 2^(i+1)] reads T_m with m <= 2^i only: each such
+        // range is one wave of independent products (EvalMultMany)
+        for (uint32_t half = 1; half < k; half *= 2) {
+            const uint32_t lo = half + 1, hi = std::min(k, 2 * half);
+            std::vector<Ct> as, bs;
+            for (uint32_t j = lo; j <= hi; ++j) {
+                as.push_back(doubled(j / 2));
+                bs.push_back(j % 2 == 0 ? T[j / 2] : T[j / 2 + 1]);
+            }
+            std::vector<Ct> prods;
+            if (psWaves()) {
+                prods = cc->EvalMultMany(as, bs);
+            } else {
+                for (size_t i = 0; i < as.size(); ++i) prods.push_back(cc->EvalMult(as[i], bs[i]));
+            }
+            for (uint32_t j = lo; j <= hi; ++j) {
+                const Ct& prod = prods[j - lo];
+                T[j] = (j % 2 == 0) ? cc->EvalAdd(prod, -1.0) : cc->EvalSub(prod, atLevel(1, prod->GetLevel()));
+            }
         }
         giant[l] = T[k];
     }
@@ -187,7 +213,98 @@ class PSEvaluator {
         return out;
     }
 
+    // ---- level-synchronous evaluation (the default) ----
+    // build() runs eval()'s recursion -- same levels, same leaves in the same
+    // visiting order -- but records each node q T_M + r instead of computing
+    // it; run() then evaluates the tree in waves: every node whose q is ready
+    // takes its product with the aligned giant step (the nodes of one (M, Lp)
+    // as ONE EvalMultMany: their launches merged), then every node whose
+    // product and r are ready takes its sum.  The same operations on the same
+    // operands as eval(), so the same values; the chain of dependent products
+    // shrinks from one per node (81 for the N = 256 doubled sinc) to the
+    // tree's height.
+    Val build(std::vector<double> p, uint32_t depth, uint32_t want = 0) {
+        trim(p);
+        if (p.empty()) return Val{true, 0.0, nullptr};
+        const uint32_t deg = (uint32_t)p.size() - 1;
+        if (deg == 0) return Val{true, p[0], nullptr};
+        if (deg <= k) return leaf(p, want);
+        if (depth >= 1 && deg + (1u << l) <= (1u << (depth - 1))) return build(p, depth - 1, want);
+        const uint32_t M = deg >= (1u << (depth - 1)) ? (1u << (depth - 1)) : (1u << (depth - 2));
+        std::vector<double> q, r;
+        divide(p, M, q, r);
+        const uint32_t Lp = productLevel(q, depth, M, want);
+        Node nd;
+        nd.q = build(q, depth - 1, Lp - 1);
+        nd.r = build(r, depth, Lp);
+        nd.M = M;
+        nd.Lp = Lp;
+        nodes.push_back(std::move(nd));
+        Val v;
+        v.isConst = false;
+        v.node = (int)nodes.size() - 1;
+        return v;
+    }
+
+    Val run(const Val& root) {
+        if (root.node < 0) return root;
+        auto ready = [&](const Val& v) { return v.isConst || v.node < 0 || nodes[v.node].hasOut; };
+        auto value = [&](const Val& v) -> const Ct& { return v.node < 0 ? v.ct : nodes[v.node].out; };
+        while (!nodes[root.node].hasOut) {
+            bool progress = false;
+            std::map<std::pair<uint32_t, uint32_t>, std::vector<size_t>> waves;  // (M, Lp) -> nodes
+            for (size_t i = 0; i < nodes.size(); ++i)
+                if (!nodes[i].hasProd && ready(nodes[i].q)) waves[{nodes[i].M, nodes[i].Lp}].push_back(i);
+            for (auto& w : waves) {
+                const Ct& TM = alignedPower(w.first.first, w.first.second - 1);
+                std::vector<Ct> as, bs;
+                std::vector<size_t> which;
+                for (size_t i : w.second) {
+                    Node& nd = nodes[i];
+                    if (nd.q.isConst) {
+                        nd.prod = cc->EvalMult(TM, nd.q.c);
+                        nd.hasProd = true;
+                        continue;
+                    }
+                    as.push_back(value(nd.q));
+                    bs.push_back(TM);
+                    which.push_back(i);
+                }
+                auto prods = cc->EvalMultMany(as, bs);
+                for (size_t t = 0; t < which.size(); ++t) {
+                    nodes[which[t]].prod = prods[t];
+                    nodes[which[t]].hasProd = true;
+                }
+                progress = true;
+            }
+            for (auto& nd : nodes) {
+                if (nd.hasOut || !nd.hasProd || !ready(nd.r)) continue;
+                if (nd.r.isConst)
+                    nd.out = nd.r.c != 0.0 ? cc->EvalAdd(nd.prod, nd.r.c) : nd.prod;
+                else
+                    nd.out = cc->EvalAdd(nd.prod, value(nd.r));
+                nd.hasOut = true;
+                nd.prod = nullptr;
+                progress = true;
+            }
+            if (!progress) SFHE_THROW("internal: Chebyshev wave evaluation stalled");
+        }
+        Val out;
+        out.isConst = false;
+        out.ct = nodes[root.node].out;
+        nodes.clear();
+        return out;
+    }
+
   private:
+    struct Node {
+        Val q, r;
+        uint32_t M = 0, Lp = 0;
+        Ct prod, out;
+        bool hasProd = false, hasOut = false;
+    };
+    std::vector<Node> nodes;
+
     // p = q T_M + r (Chebyshev division by T_M, M >= deg / 2)
     static void divide(const std::vector<double>& p, uint32_t M, std::vector<double>& q, std::vector<double>& r) {
         const uint32_t deg = (uint32_t)p.size() - 1;
@@ -440,7 +557,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalChebyshevSeriesPS(
         PSEvaluator ps(this, y, l, D);
         static const bool batched = std::getenv("SFHE_PS_UNBATCHED") == nullptr;
         if (batched) ps.precomputeLeaves(p, D);
-        auto v = ps.eval(p, D, 0, 0, lanes);
+        auto v = (lanes == 1 && psWaves()) ? ps.run(ps.build(p, D)) : ps.eval(p, D, 0, 0, lanes);
         out = v.isConst ? EvalAdd(EvalMult(y, 0.0), v.c) : v.ct;
     }
     const uint32_t target = y->GetLevel() + D;
@@ -474,8 +591,24 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalPolyLinear(
         }
     std::vector<Ciphertext<DCRTPoly>> pw(d + 1);
     pw[1] = x;
-    for (uint32_t j = 2; j <= d; ++j)
-        if (need[j]) pw[j] = (j % 2 == 0) ? EvalSquare(pw[j / 2]) : EvalMult(pw[j / 2], pw[j / 2 + 1]);
+    // x^j for j in (2^i, 2^(i+1)] reads powers <= 2^i only: one wave of
+    // independent products each (EvalMultMany; the same values)
+    for (uint32_t half = 1; half < d; half *= 2) {
+        std::vector<Ciphertext<DCRTPoly>> as, bs;
+        std::vector<uint32_t> js;
+        for (uint32_t j = half + 1; j <= std::min(d, 2 * half); ++j)
+            if (need[j]) {
+                as.push_back(pw[j / 2]);
+                bs.push_back(pw[j - j / 2]);
+                js.push_back(j);
+            }
+        if (psWaves()) {
+            auto prods = EvalMultMany(as, bs);
+            for (size_t t = 0; t < js.size(); ++t) pw[js[t]] = prods[t];
+        } else {
+            for (size_t t = 0; t < js.size(); ++t) pw[js[t]] = EvalMult(as[t], bs[t]);
+        }
+    }
     uint32_t lev = 0;
     for (uint32_t j = 1; j <= d; ++j)
         if (p[j] != 0.0) lev = std::max(lev, pw[j]->GetLevel());

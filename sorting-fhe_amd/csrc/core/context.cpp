@@ -932,6 +932,49 @@ class SfheInternal {
         return relinRescale(cc, d0, d1, d2, level, slots);
     }
 
+    // multRelinRescale of up to SFP_BATCH_MAX independent operand pairs at one
+    // level as ONE batched op (sfp_batch_*): each pair's fused chain is issued
+    // on its own virtual lane and the pairs' identical launches run merged.
+    // Every pair's buffers live until the batch is issued.  Pairs the backend
+    // cannot fuse run one by one (multRelinRescale: the same values).
+    static std::vector<Ct> multRelinRescaleMany(CC* cc, const std::vector<const CiphertextImpl<DCRTPoly>*>& a,
+                                                const std::vector<const CiphertextImpl<DCRTPoly>*>& b, uint32_t level,
+                                                const std::vector<uint32_t>& slots) {
+        SfheContextState* s = cc->st.get();
+        const size_t cnt = a.size();
+        const uint32_t ell = s->ellOf(level);
+        std::vector<Ct> out(cnt);
+        if (ell < 2) SFHE_THROW("no levels left to rescale (multiplicative depth exhausted)");
+        const uint32_t n = s->n, K = s->K, beta = (ell + s->alpha - 1) / s->alpha;
+        const size_t stride = (size_t)(ell + K) * n;
+        std::vector<DeviceBufferPtr> keep;
+        auto& convs = modupConv(cc, ell);
+        size_t done = 0;
+        if (!s->shardAt(ell) && sfp_batch_begin(s->dev, (uint32_t)cnt)) {
+            for (; done < cnt; ++done) {
+                out[done] = newCt(cc, level + 1, slots[done]);
+                auto acc = s->alloc(2 * stride);
+                auto ext = s->alloc(stride * beta);
+                auto scratch = s->alloc((size_t)2 * ell * n);
+                keep.insert(keep.end(), {acc, ext, scratch});
+                sfp_batch_lane(s->dev, (uint32_t)done);
+                if (sfp_mult_relin_rescale(s->dev, out[done]->c0, out[done]->c1, a[done]->c0, a[done]->c1,
+                                           b[done]->c0, b[done]->c1, ell, K, s->Lq, s->alpha, convs.data(),
+                                           s->relinKey->ptr, s->moddownConv, s->pInvModQ.data(), s->pModQ.data(),
+                                           s->qInvTable[ell].data(), acc->ptr, ext->ptr, scratch->ptr) != 0)
+                    break;  // (no fused form: nothing issued for this pair)
+                s->stats.keyswitch++;
+                s->stats.rescale++;
+                s->countBytes((3.0 * ell + 2.0 * beta * (ell + K)) * n * 8);
+                s->countBytes(4.0 * ell * n * 8);
+            }
+            sfp_batch_end(s->dev);
+        }
+        for (size_t i = done; i < cnt; ++i)
+            out[i] = multRelinRescale(cc, a[i]->c0, a[i]->c1, b[i]->c0, b[i]->c1, level, slots[i]);
+        return out;
+    }
+
     static void innerAndModDown(CC* cc, const uint64_t* ext, size_t stride, uint32_t beta,
                                 uint32_t ell, const DeviceBufferPtr& key, uint64_t* out0,
                                 uint64_t* out1, int add0, int add1) {
@@ -2427,6 +2470,47 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMult(const Ciphertext<DCRT
 
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalSquare(const Ciphertext<DCRTPoly>& a) {
     return EvalMult(a, a);
+}
+
+std::vector<Ciphertext<DCRTPoly>> CryptoContextImpl<DCRTPoly>::EvalMultMany(
+    const std::vector<Ciphertext<DCRTPoly>>& a0, const std::vector<Ciphertext<DCRTPoly>>& b0) {
+    OpLock g(st.get());
+    SfheContextState* s = st.get();
+    if (a0.size() != b0.size()) SFHE_THROW("operand count mismatch");
+    const size_t cnt = a0.size();
+    std::vector<Ciphertext<DCRTPoly>> out(cnt);
+    // the products are formed canonically (as a deferred product is when its
+    // consumer needs the canonical form: the same values); for consumers that
+    // would take a lazy product's pending rows, use EvalMult
+    if (cnt < 2 || !SfheInternal::fusedRescale()) {
+        for (size_t i = 0; i < cnt; ++i) out[i] = EvalMult(a0[i], b0[i]);
+        return out;
+    }
+    if (!s->relinKey) SFHE_THROW("EvalMultKeyGen must be called before EvalMult");
+    std::vector<Ciphertext<DCRTPoly>> A(a0), B(b0);
+    for (size_t i = 0; i < cnt; ++i) {
+        SfheInternal::deps(s, {&a0[i], &b0[i]});
+        SfheInternal::align(this, A[i], B[i]);
+        if (s->ellOf(A[i]->level) < 2) SFHE_THROW("no levels left (multiplicative depth exhausted)");
+        s->stats.tensor++;
+        s->countBytes(7.0 * s->ellOf(A[i]->level) * s->n * 8);
+    }
+    // runs of up to SFP_BATCH_MAX consecutive pairs at one level
+    for (size_t i = 0; i < cnt;) {
+        size_t j = i + 1;
+        while (j < cnt && j - i < SFP_BATCH_MAX && A[j]->level == A[i]->level) ++j;
+        std::vector<const CiphertextImpl<DCRTPoly>*> pa, pb;
+        std::vector<uint32_t> slots;
+        for (size_t k = i; k < j; ++k) {
+            pa.push_back(A[k].get());
+            pb.push_back(B[k].get());
+            slots.push_back(std::max(A[k]->slots, B[k]->slots));
+        }
+        auto r = SfheInternal::multRelinRescaleMany(this, pa, pb, A[i]->level, slots);
+        for (size_t k = i; k < j; ++k) out[k] = SfheInternal::traced(this, r[k - i], "EvalMult");
+        i = j;
+    }
+    return out;
 }
 
 Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMultAddPlain(

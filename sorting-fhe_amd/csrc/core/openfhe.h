@@ -368,6 +368,13 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
         return EvalMult(a, b);
     }
     Ciphertext<DCRTPoly> EvalSquare(const Ciphertext<DCRTPoly>& a);
+    // Engine extension: EvalMult(a_i, b_i) for independent pairs, each formed
+    // canonically (rescaled: the values a lazy product takes when its
+    // consumer needs the canonical form); pairs at one level run as batched
+    // ops (prims.h sfp_batch_*: their identical launches merged, up to four
+    // pairs per launch).
+    std::vector<Ciphertext<DCRTPoly>> EvalMultMany(const std::vector<Ciphertext<DCRTPoly>>& a,
+                                                   const std::vector<Ciphertext<DCRTPoly>>& b);
     // Engine extension: sum_i a_i * p_i with ONE rescale (same value and
     // level as summing the individually rescaled EvalMult(a_i, p_i)).
     Ciphertext<DCRTPoly> EvalMultAddPlain(const std::vector<Ciphertext<DCRTPoly>>& a,

@@ -132,13 +132,19 @@ struct sfp_dev {
     // launches that read them)
     bool stackOn = false;
     std::vector<StackRec> stack[SFP_MAX_LANES];
+    hipStream_t stackStream = nullptr;  // where the flush issues (null: streams[0])
+    bool batchOn = false;               // a batched op (sfp_batch_begin): lists 4 + i
+    int batchCur = 0;                   // the caller's lane (restored at sfp_batch_end)
     uint64_t recSeq = 0;
     std::vector<sfp_event*> stackFreedEv;  // freed inside the region: reusable after the flush
     uint64_t stkMerged = 0, stkSingle = 0;  // launches issued as merged pairs / alone
     sfp_key_geom kg = {};          // switching-key geometry (sfp_set_key_geom; rows 0: whole keys)
     uint32_t stkFam = ~0u;  // timedLaunch's family while it records (stacked)
     double stkBytes = 0;
-    hipStream_t st() const { return streams[(serial || stackOn) ? 0 : cur]; }
+    hipStream_t st() const {
+        if (batchOn) return stackStream;
+        return streams[(serial || stackOn) ? 0 : cur];
+    }
     std::vector<sfp_event*> evFree;
     std::mutex evMu;  // evFree: buffers release events from any host thread
     uint32_t n = 0, logn = 0, np = 0;
@@ -714,28 +720,35 @@ struct RowGroup {
     const u64 *k, *kS, *k2, *k2S, *liftSub, *preK, *preKS, *emK, *emKS;
 };
 
-// Stacked launches (sfp_stack_begin): NG independent argument sets in one
-// launch, blockIdx.y < split -> set 0, the rest -> set 1 (rows renumbered
-// from 0).  Two lanes' identical ops (the sort's batches) become one launch
-// with the rows of both; NG = 1 is the ordinary launch.
-// With `inter` (both sets of equal row count) the sets alternate instead:
-// grid row y is row y / 2 of set y % 2, so the two sets' rows of one prime
-// (one key row, one twiddle table) run side by side and share their L2 lines.
+// Merged launches (stacked regions, batched ops; sfp_stack_begin /
+// sfp_batch_begin): NG independent argument sets in one launch.  Set i owns
+// the grid rows [start[i], start[i+1]) (renumbered from 0); with `inter` (NG
+// sets of equal row counts) the sets alternate instead -- grid row y is row
+// y / NG of set y % NG -- so the sets' rows of one prime (one key row, one
+// twiddle table) run side by side and share their L2 lines.  NG = 1 is the
+// ordinary launch.
 template <class T, int NG>
 struct ArgSet {
     T a[NG];
-    uint32_t split;  // grid rows of set 0
+    uint32_t start[NG];  // start[0] = 0
     uint32_t inter;
 };
 template <class T, int NG>
 __device__ __forceinline__ uint32_t argSel(const ArgSet<T, NG>& S, uint32_t& row) {
     const uint32_t y = blockIdx.y;
-    if (NG > 1 && S.inter) {
-        row = y >> 1;
-        return y & 1u;
+    if (NG == 1) {
+        row = y;
+        return 0;
     }
-    const uint32_t sel = (NG > 1 && y >= S.split) ? 1u : 0u;
-    row = y - (sel ? S.split : 0u);
+    if (S.inter) {
+        row = y / NG;
+        return y % NG;
+    }
+    uint32_t sel = 0;
+#pragma unroll
+    for (int i = 1; i < NG; ++i)
+        if (y >= S.start[i]) sel = (uint32_t)i;
+    row = y - S.start[sel];
     return sel;
 }
 template <int NG>
@@ -2193,13 +2206,14 @@ __global__ __launch_bounds__(kThreads) void k_convf(const ConvJobs J, const sf_b
 // P-rows (as k_conv), the dropped row's coefficient r = (a_l - conv_l) P^-1
 // mod q_l, and for every kept target t < l:  y_t = conv_t + P_t [r]_t, with
 // [r]_t the centred lift of r (r > q_l/2 stands for r - q_l).
+constexpr int kMdrsJobs = 8;
 struct MdrsJob {
     const u64* src;  // K P-rows, coefficient domain
     const u64* al;   // accumulator row l, coefficient domain
     u64* dst;        // l rows
 };
 struct MdrsArgs {
-    MdrsJob j[4];  // blockIdx.y: two polys, or two stacked launches' four
+    MdrsJob j[kMdrsJobs];  // blockIdx.y: two polys, or the polys of up to four merged launches
     const uint32_t* sidx;
     const u64 *inv, *mod, *sprod;  // the ModDown conversion table (targets 0..)
     const u64 *pmod, *lsub;        // P mod q_t, q_l mod q_t
@@ -2653,25 +2667,31 @@ static uint64_t stkKey(const void* kern, uint32_t a, uint32_t b) {
     return h;
 }
 
-using NttKern2 = void (*)(RowGroupSet<2>, const sf_barrett*, const u64*, const u64*, const u64*, const u64*,
+template <int NG>
+using NttKernN = void (*)(RowGroupSet<NG>, const sf_barrett*, const u64*, const u64*, const u64*, const u64*,
                           uint32_t, const double*, const double*, const double*, const double*, int);
+using NttKern2 = NttKernN<2>;
+using NttKern4 = NttKernN<4>;
 struct NttPay {
     RowGroup G;
     uint32_t rows;
     dim3 g;
     int threads, useFp;
     NttKern2 k2;
+    NttKern4 k4;
     const u64 *tw, *twS;
     const double* twD;
 };
-using KsKern2 = void (*)(ArgSet<KsArgs, 2>, const sf_barrett*, const u64*, const u64*, uint32_t, const double*,
+template <int NG>
+using KsKernN = void (*)(ArgSet<KsArgs, NG>, const sf_barrett*, const u64*, const u64*, uint32_t, const double*,
                          const double*, int);
 struct KsPay {
     KsArgs a;
     uint32_t rows;
     dim3 g;
     int threads, useFp;
-    KsKern2 k2;
+    KsKernN<2> k2;
+    KsKernN<4> k4;
 };
 using ConvKern = void (*)(ConvJobs, const sf_barrett*, const double*, uint32_t);
 struct ConvPay {
@@ -2687,34 +2707,69 @@ struct MdrsPay {
 };
 using MdrsKern = void (*)(MdrsArgs, const sf_barrett*, const double*, uint32_t);
 
-// grid.y arg-set kernels (k_ew, k_automorph, k_lin_wsum, k_ks_inner): two
-// launches of one kernel become one with grid.y = 2 (the larger grid.x; each
-// set's grid-stride loop covers its own rows)
+// up to this many heads become one launch (the ArgSet<T, 4> kernels)
+constexpr int kMergeMax = 4;
+
+// The row-group kernels (k_ntt, k_ntt_ks): the heads' argument sets in one
+// ArgSet<T, NG> (NG = 2 or 4), rows concatenated -- or alternating when every
+// set has the same row count and fills the NG slots.
+template <class T, int NG, class F>
+static void launchSets(const T* const* a, const uint32_t* rows, int cnt, F&& launch) {
+    ArgSet<T, NG> S;
+    uint32_t total = 0;
+    bool equal = true;
+    for (int i = 0; i < NG; ++i) {
+        S.a[i] = *a[std::min(i, cnt - 1)];
+        S.start[i] = total;
+        if (i < cnt) {
+            total += rows[i];
+            equal = equal && rows[i] == rows[0];
+        }
+    }
+    S.inter = equal && cnt == NG;
+    launch(S, total);
+}
+
+// grid.y arg-set kernels (k_ew, k_automorph, k_lin_wsum, k_ks_inner): the
+// heads' sets with grid.y = their count (the largest grid.x; each set's
+// grid-stride loop covers its own rows)
 struct YPayBase {
     dim3 g;
     virtual ~YPayBase() = default;
-    virtual void launch2(sfp_dev* d, hipStream_t s, const YPayBase& other) const = 0;
+    virtual void launchMany(sfp_dev* d, hipStream_t s, const YPayBase* const* h, int cnt) const = 0;
 };
 template <class Args>
 struct YPay : YPayBase {
     Args a;
     void (*k2)(ArgSet<Args, 2>, const sf_barrett*, uint32_t);
-    void launch2(sfp_dev* d, hipStream_t s, const YPayBase& other) const override {
-        const auto& o = static_cast<const YPay<Args>&>(other);
-        ArgSet<Args, 2> S;
-        S.a[0] = a;
-        S.a[1] = o.a;
-        S.split = 0;
+    void (*k4)(ArgSet<Args, 4>, const sf_barrett*, uint32_t);
+    template <int NG, class K>
+    void go(sfp_dev* d, hipStream_t s, const YPayBase* const* h, int cnt, K k) const {
+        ArgSet<Args, NG> S;
+        uint32_t gx = 0;
+        for (int i = 0; i < NG; ++i) {
+            const auto& o = static_cast<const YPay<Args>&>(*h[std::min(i, cnt - 1)]);
+            S.a[i] = o.a;
+            S.start[i] = 0;
+            gx = std::max(gx, o.g.x);
+        }
         S.inter = 0;
-        hipLaunchKernelGGL(k2, dim3(std::max(g.x, o.g.x), 2), dim3(kThreads), 0, s, S, d->bar, d->logn);
+        hipLaunchKernelGGL(k, dim3(gx, cnt), dim3(kThreads), 0, s, S, d->bar, d->logn);
+    }
+    void launchMany(sfp_dev* d, hipStream_t s, const YPayBase* const* h, int cnt) const override {
+        if (cnt == 2)
+            go<2>(d, s, h, cnt, k2);
+        else
+            go<4>(d, s, h, cnt, k4);
     }
 };
 template <class Args>
 static void issueY(sfp_dev* d, void (*k1)(ArgSet<Args, 1>, const sf_barrett*, uint32_t),
-                   void (*k2)(ArgSet<Args, 2>, const sf_barrett*, uint32_t), dim3 g, const Args& a) {
+                   void (*k2)(ArgSet<Args, 2>, const sf_barrett*, uint32_t),
+                   void (*k4)(ArgSet<Args, 4>, const sf_barrett*, uint32_t), dim3 g, const Args& a) {
     ArgSet<Args, 1> S;
     S.a[0] = a;
-    S.split = 0;
+    S.start[0] = 0;
     S.inter = 0;
     StackRec r;
     r.go = [=](hipStream_t s_) { hipLaunchKernelGGL(k1, g, dim3(kThreads), 0, s_, S, d->bar, d->logn); };
@@ -2722,6 +2777,7 @@ static void issueY(sfp_dev* d, void (*k1)(ArgSet<Args, 1>, const sf_barrett*, ui
         auto P = std::make_shared<YPay<Args>>();
         P->a = a;
         P->k2 = k2;
+        P->k4 = k4;
         P->g = g;
         r.cls = STK_Y;
         r.key = stkKey((const void*)k1, 0, 0);
@@ -2730,68 +2786,119 @@ static void issueY(sfp_dev* d, void (*k1)(ArgSet<Args, 1>, const sf_barrett*, ui
     issueRec(d, std::move(r));
 }
 
-// Issue the heads a and b (same class and key) as one launch on s; false if
-// their arguments cannot share one (the caller then issues them apart);
-// check: only report whether they can.
-static bool stackMerge(sfp_dev* d, const StackRec& a, const StackRec& b, hipStream_t s, bool check) {
-    switch (a.cls) {
+// Issue the heads h[0..cnt) (2 <= cnt <= kMergeMax, one class and key) as one
+// launch on s; false if their arguments cannot share one (the caller then
+// issues them apart); check: only report whether they can.
+static bool stackMerge(sfp_dev* d, const StackRec* const* h, int cnt, hipStream_t s, bool check) {
+    auto pay = [&](int i) { return h[i]->pay.get(); };
+    switch (h[0]->cls) {
         case STK_NTT: {
-            const auto& A = *static_cast<const NttPay*>(a.pay.get());
-            const auto& B = *static_cast<const NttPay*>(b.pay.get());
-            if (!A.k2 || A.rows + B.rows > 65535u || A.g.x != B.g.x || A.useFp != B.useFp) return false;
+            const NttPay* P[kMergeMax];
+            const RowGroup* G[kMergeMax];
+            uint32_t rows[kMergeMax], total = 0;
+            for (int i = 0; i < cnt; ++i) {
+                P[i] = static_cast<const NttPay*>(pay(i));
+                G[i] = &P[i]->G;
+                rows[i] = P[i]->rows;
+                total += rows[i];
+                if (P[i]->g.x != P[0]->g.x || P[i]->useFp != P[0]->useFp) return false;
+            }
+            if (total > 65535u || !(cnt == 2 ? (bool)P[0]->k2 : (bool)P[0]->k4)) return false;
             if (check) return true;
-            RowGroupSet<2> GS;
-            GS.a[0] = A.G;
-            GS.a[1] = B.G;
-            GS.split = A.rows;
-            GS.inter = A.rows == B.rows;
-            hipLaunchKernelGGL(A.k2, dim3(A.g.x, A.rows + B.rows), dim3(A.threads), 0, s, GS, d->bar, A.tw, A.twS,
-                               d->ninv, d->ninvS, d->logn, A.twD, d->qinvD, d->ninvD, d->ninvQ, A.useFp);
+            const NttPay& A = *P[0];
+            auto launch = [&](const auto& S, uint32_t tot) {
+                using SetT = std::decay_t<decltype(S)>;
+                NttKernN<sizeof(SetT::a) / sizeof(RowGroup)> k;
+                if constexpr (sizeof(SetT::a) / sizeof(RowGroup) == 2)
+                    k = A.k2;
+                else
+                    k = A.k4;
+                hipLaunchKernelGGL(k, dim3(A.g.x, tot), dim3(A.threads), 0, s, S, d->bar, A.tw, A.twS, d->ninv,
+                                   d->ninvS, d->logn, A.twD, d->qinvD, d->ninvD, d->ninvQ, A.useFp);
+            };
+            if (cnt == 2)
+                launchSets<RowGroup, 2>(G, rows, cnt, launch);
+            else
+                launchSets<RowGroup, 4>(G, rows, cnt, launch);
             return true;
         }
         case STK_KS: {
-            const auto& A = *static_cast<const KsPay*>(a.pay.get());
-            const auto& B = *static_cast<const KsPay*>(b.pay.get());
-            if (!A.k2 || A.rows + B.rows > 65535u || A.g.x != B.g.x || A.useFp != B.useFp) return false;
+            const KsPay* P[kMergeMax];
+            const KsArgs* A[kMergeMax];
+            uint32_t rows[kMergeMax], total = 0;
+            for (int i = 0; i < cnt; ++i) {
+                P[i] = static_cast<const KsPay*>(pay(i));
+                A[i] = &P[i]->a;
+                rows[i] = P[i]->rows;
+                total += rows[i];
+                if (P[i]->g.x != P[0]->g.x || P[i]->useFp != P[0]->useFp) return false;
+            }
+            if (total > 65535u || !(cnt == 2 ? (bool)P[0]->k2 : (bool)P[0]->k4)) return false;
             if (check) return true;
-            ArgSet<KsArgs, 2> AS;
-            AS.a[0] = A.a;
-            AS.a[1] = B.a;
-            AS.split = A.rows;
-            AS.inter = A.rows == B.rows;
-            hipLaunchKernelGGL(A.k2, dim3(A.g.x, A.rows + B.rows), dim3(A.threads), 0, s, AS, d->bar, d->psi,
-                               d->psiS, d->logn, d->psiD, d->qinvD, A.useFp);
+            const KsPay& B = *P[0];
+            auto launch = [&](const auto& S, uint32_t tot) {
+                using SetT = std::decay_t<decltype(S)>;
+                KsKernN<sizeof(SetT::a) / sizeof(KsArgs)> k;
+                if constexpr (sizeof(SetT::a) / sizeof(KsArgs) == 2)
+                    k = B.k2;
+                else
+                    k = B.k4;
+                hipLaunchKernelGGL(k, dim3(B.g.x, tot), dim3(B.threads), 0, s, S, d->bar, d->psi, d->psiS, d->logn,
+                                   d->psiD, d->qinvD, B.useFp);
+            };
+            if (cnt == 2)
+                launchSets<KsArgs, 2>(A, rows, cnt, launch);
+            else
+                launchSets<KsArgs, 4>(A, rows, cnt, launch);
             return true;
         }
         case STK_CONV: {
-            const auto& A = *static_cast<const ConvPay*>(a.pay.get());
-            const auto& B = *static_cast<const ConvPay*>(b.pay.get());
-            if (A.k != B.k || A.njobs + B.njobs > (uint32_t)kMaxConvJobs || A.g.x != B.g.x) return false;
+            const ConvPay* P[kMergeMax];
+            uint32_t jobs = 0, gz = 0;
+            for (int i = 0; i < cnt; ++i) {
+                P[i] = static_cast<const ConvPay*>(pay(i));
+                if (P[i]->k != P[0]->k || P[i]->g.x != P[0]->g.x) return false;
+                jobs += P[i]->njobs;
+                gz = std::max(gz, P[i]->g.z);
+            }
+            if (jobs > (uint32_t)kMaxConvJobs) return false;
             if (check) return true;
-            ConvJobs J = A.J;
-            for (uint32_t k = 0; k < B.njobs; ++k) J.j[A.njobs + k] = B.J.j[k];
-            hipLaunchKernelGGL(A.k, dim3(A.g.x, A.njobs + B.njobs, std::max(A.g.z, B.g.z)), dim3(kThreads), 0, s, J,
-                               d->bar, d->qinvD, d->logn);
+            ConvJobs J;
+            uint32_t at = 0;
+            for (int i = 0; i < cnt; ++i)
+                for (uint32_t k = 0; k < P[i]->njobs; ++k) J.j[at++] = P[i]->J.j[k];
+            hipLaunchKernelGGL(P[0]->k, dim3(P[0]->g.x, jobs, gz), dim3(kThreads), 0, s, J, d->bar, d->qinvD,
+                               d->logn);
             return true;
         }
         case STK_MDRS: {
-            const auto& A = *static_cast<const MdrsPay*>(a.pay.get());
-            const auto& B = *static_cast<const MdrsPay*>(b.pay.get());
-            if (A.k != B.k || A.g.y + B.g.y > 4u || A.g.x != B.g.x || A.g.z != B.g.z) return false;
-            MdrsArgs x = A.M, y = B.M;
-            std::memset(x.j, 0, sizeof x.j);
-            std::memset(y.j, 0, sizeof y.j);
-            if (std::memcmp(&x, &y, sizeof x)) return false;  // another table / level
+            const MdrsPay* P[kMergeMax];
+            uint32_t jobs = 0;
+            MdrsArgs x0 = static_cast<const MdrsPay*>(pay(0))->M;
+            std::memset(x0.j, 0, sizeof x0.j);
+            for (int i = 0; i < cnt; ++i) {
+                P[i] = static_cast<const MdrsPay*>(pay(i));
+                if (P[i]->k != P[0]->k || P[i]->g.x != P[0]->g.x || P[i]->g.z != P[0]->g.z) return false;
+                MdrsArgs x = P[i]->M;
+                std::memset(x.j, 0, sizeof x.j);
+                if (std::memcmp(&x, &x0, sizeof x)) return false;  // another table / level
+                jobs += P[i]->g.y;
+            }
+            if (jobs > (uint32_t)kMdrsJobs) return false;
             if (check) return true;
-            MdrsArgs M = A.M;
-            for (uint32_t k = 0; k < B.g.y; ++k) M.j[A.g.y + k] = B.M.j[k];
-            hipLaunchKernelGGL(reinterpret_cast<MdrsKern>(A.k), dim3(A.g.x, A.g.y + B.g.y, A.g.z), dim3(kThreads), 0,
-                               s, M, d->bar, d->qinvD, d->logn);
+            MdrsArgs M = P[0]->M;
+            uint32_t at = 0;
+            for (int i = 0; i < cnt; ++i)
+                for (uint32_t k = 0; k < P[i]->g.y; ++k) M.j[at++] = P[i]->M.j[k];
+            hipLaunchKernelGGL(reinterpret_cast<MdrsKern>(P[0]->k), dim3(P[0]->g.x, jobs, P[0]->g.z), dim3(kThreads),
+                               0, s, M, d->bar, d->qinvD, d->logn);
             return true;
         }
         case STK_Y: {
             if (check) return true;
-            static_cast<const YPayBase*>(a.pay.get())->launch2(d, s, *static_cast<const YPayBase*>(b.pay.get()));
+            const YPayBase* Y[kMergeMax];
+            for (int i = 0; i < cnt; ++i) Y[i] = static_cast<const YPayBase*>(pay(i));
+            Y[0]->launchMany(d, s, Y, cnt);
             return true;
         }
         default:
@@ -2818,9 +2925,9 @@ static void stackTimed(sfp_dev* d, hipStream_t s, uint32_t fam, double bytes, F&
 
 static void stackFlush(sfp_dev* d) {
     if (!d->stackOn) return;
-    const hipStream_t s = d->streams[0];
-    const int L = d->nLanes;
-    size_t at[SFP_MAX_LANES] = {};
+    const hipStream_t s = d->stackStream ? d->stackStream : d->streams[0];
+    constexpr int L = SFP_MAX_LANES;
+    size_t at[L] = {};
     std::unordered_set<uint64_t> done;  // records issued so far
     auto left = [&](int l) { return d->stack[l].size() - at[l]; };
     auto head = [&](int l) -> StackRec& { return d->stack[l][at[l]]; };
@@ -2845,7 +2952,7 @@ static void stackFlush(sfp_dev* d) {
                     moved = true;
                 }
         }
-        int cand[SFP_MAX_LANES], nc = 0;
+        int cand[L], nc = 0;
         for (int l = 0; l < L; ++l)
             if (left(l) && head(l).kind == StackRec::LAUNCH) cand[nc++] = l;
         if (!nc) {
@@ -2859,27 +2966,46 @@ static void stackFlush(sfp_dev* d) {
                 }
             break;
         }
-        bool merged = false;
-        for (int i = 0; i < nc && !merged; ++i)
-            for (int j = i + 1; j < nc && !merged; ++j) {
-                const StackRec &a = head(cand[i]), &b = head(cand[j]);
-                if (a.cls && a.cls == b.cls && a.key == b.key && stackMerge(d, a, b, s, true)) {
-                    stackTimed(d, s, a.fam, a.bytes + b.bytes, [&] { stackMerge(d, a, b, s, false); });
-                    ++at[cand[i]];
-                    ++at[cand[j]];
-                    ++d->stkMerged;
-                    merged = true;
-                }
+        // the largest group of heads of one class and key (up to kMergeMax,
+        // lanes furthest behind first) becomes one launch
+        int best[kMergeMax], nb = 0;
+        for (int i = 0; i < nc; ++i) {
+            const StackRec& a = head(cand[i]);
+            if (!a.cls) continue;
+            int grp[kMergeMax], ng = 0;
+            for (int j = i; j < nc && ng < kMergeMax; ++j) {
+                const StackRec& b = head(cand[j]);
+                if (b.cls == a.cls && b.key == a.key) grp[ng++] = cand[j];
             }
-        if (merged) continue;
+            if (ng > nb) {
+                nb = ng;
+                std::copy(grp, grp + ng, best);
+            }
+        }
+        while (nb >= 2) {
+            const StackRec* hs[kMergeMax];
+            double bytes = 0;
+            for (int i = 0; i < nb; ++i) {
+                hs[i] = &head(best[i]);
+                bytes += hs[i]->bytes;
+            }
+            if (stackMerge(d, hs, nb, s, true)) {
+                stackTimed(d, s, hs[0]->fam, bytes, [&] { stackMerge(d, hs, nb, s, false); });
+                for (int i = 0; i < nb; ++i) ++at[best[i]];
+                ++d->stkMerged;
+                break;
+            }
+            --nb;  // (a group whose arguments do not fit one launch: try fewer)
+        }
+        if (nb >= 2) continue;
         // alone: the lane furthest behind (most items left) goes first, which
         // realigns lanes whose sequences differ by an op (batch 0's offset)
-        int best = cand[0];
+        int one = cand[0];
         for (int i = 1; i < nc; ++i)
-            if (left(cand[i]) > left(best)) best = cand[i];
-        const StackRec& r = head(best);
+            if (left(cand[i]) > left(one)) one = cand[i];
+        const StackRec& r = head(one);
         stackTimed(d, s, r.fam, r.bytes, [&] { r.go(s); });
-        ++at[best];
+        ++at[one];
         ++d->stkSingle;
     }
     for (int l = 0; l < L; ++l) d->stack[l].clear();
@@ -3334,6 +3460,7 @@ void sfp_event_free(sfp_dev* d, sfp_event* e) {
 
 void sfp_stack_begin(sfp_dev* d) {
     if (d->stackOn) return;
+    d->stackStream = nullptr;  // (lanes: the flush issues on lane 0)
     static const bool on = [] {
         const char* v = std::getenv("SFHE_STACK");
         return !v || *v != '0';
@@ -3342,8 +3469,40 @@ void sfp_stack_begin(sfp_dev* d) {
     d->stackOn = true;
 }
 void sfp_stack_end(sfp_dev* d) {
+    if (d->batchOn) return;  // (a batched op's region ends with sfp_batch_end)
     stackFlush(d);
     d->stackOn = false;
+}
+
+// Batched ops: `count` (<= SFP_BATCH_MAX) independent ops issued one after the
+// other by the host, each after sfp_batch_lane(i), are recorded on virtual
+// lanes and issued at sfp_batch_end on the caller's stream, identical
+// launches of the ops merged (up to four into one).  Inside a stacked lane
+// region (no nesting) or with serialised lanes the ops run as issued.
+int sfp_batch_begin(sfp_dev* d, uint32_t count) {
+    static const bool on = [] {
+        const char* v = std::getenv("SFHE_BATCH");
+        return !v || *v != '0';
+    }();
+    if (!on || d->stackOn || d->serial || count < 2 || count > SFP_BATCH_MAX ||
+        d->nLanes > SFP_MAX_LANES - SFP_BATCH_MAX)
+        return 0;
+    d->stackStream = d->st();
+    d->batchCur = d->cur;
+    d->batchOn = true;
+    d->stackOn = true;
+    return 1;
+}
+void sfp_batch_lane(sfp_dev* d, uint32_t i) {
+    if (d->batchOn) d->cur = (int)(SFP_MAX_LANES - SFP_BATCH_MAX + i);  // (its own list and scratch)
+}
+void sfp_batch_end(sfp_dev* d) {
+    if (!d->batchOn) return;
+    d->cur = d->batchCur;
+    stackFlush(d);
+    d->batchOn = false;
+    d->stackOn = false;
+    d->stackStream = nullptr;
 }
 void sfp_stack_stats(sfp_dev* d, uint64_t* merged, uint64_t* single) {
     if (merged) *merged = d->stkMerged;
@@ -3441,13 +3600,13 @@ static void nttRows(sfp_dev* d, const RowGroup& G0, int inverse, int passes = 3)
     const dim3 g(d->n / (t1k ? smallTile : (uint32_t)kNttTile), rows);
     const bool small = rows < (uint32_t)kNttSmallRows;
     int npass = 0;
-    // kern2: the same pass over two row groups (stacked launches), or null
-    auto pass = [&](auto kern, NttKern2 kern2, int threads) {
+    // kern2 / kern4: the same pass over two / four row groups (merged launches), or null
+    auto pass = [&](auto kern, NttKern2 kern2, NttKern4 kern4, int threads) {
         if (!((passes >> npass++) & 1)) return;
         timedLaunch(d, SFP_FAM_NTT, bytes, [&] {
             RowGroupSet<1> GS;
             GS.a[0] = G;
-            GS.split = rows;
+            GS.start[0] = 0;
             GS.inter = 0;
             const int fp = nttFp();
             StackRec r;
@@ -3463,6 +3622,7 @@ static void nttRows(sfp_dev* d, const RowGroup& G0, int inverse, int passes = 3)
                 P->threads = threads;
                 P->useFp = fp;
                 P->k2 = kern2;
+                P->k4 = kern4;
                 P->tw = tw;
                 P->twS = twS;
                 P->twD = twD;
@@ -3483,18 +3643,18 @@ static void nttRows(sfp_dev* d, const RowGroup& G0, int inverse, int passes = 3)
         constexpr int ST = decltype(tileC)::value;
         if (smallLe == 3) {
             if (!inverse) {
-                pass(k_ntt<false, true, 3, ST>, NttKern2{}, ST >> 3);
-                pass(k_ntt<false, false, 3, ST>, NttKern2{}, ST >> 3);
+                pass(k_ntt<false, true, 3, ST>, NttKern2{}, NttKern4{}, ST >> 3);
+                pass(k_ntt<false, false, 3, ST>, NttKern2{}, NttKern4{}, ST >> 3);
             } else {
-                pass(k_ntt<true, false, 3, ST>, NttKern2{}, ST >> 3);
-                pass(k_ntt<true, true, 3, ST>, NttKern2{}, ST >> 3);
+                pass(k_ntt<true, false, 3, ST>, NttKern2{}, NttKern4{}, ST >> 3);
+                pass(k_ntt<true, true, 3, ST>, NttKern2{}, NttKern4{}, ST >> 3);
             }
         } else if (!inverse) {
-            pass(k_ntt<false, true, 2, ST>, k_ntt<false, true, 2, ST, 2>, ST >> 2);
-            pass(k_ntt<false, false, 2, ST>, k_ntt<false, false, 2, ST, 2>, ST >> 2);
+            pass(k_ntt<false, true, 2, ST>, k_ntt<false, true, 2, ST, 2>, k_ntt<false, true, 2, ST, 4>, ST >> 2);
+            pass(k_ntt<false, false, 2, ST>, k_ntt<false, false, 2, ST, 2>, k_ntt<false, false, 2, ST, 4>, ST >> 2);
         } else {
-            pass(k_ntt<true, false, 2, ST>, k_ntt<true, false, 2, ST, 2>, ST >> 2);
-            pass(k_ntt<true, true, 2, ST>, k_ntt<true, true, 2, ST, 2>, ST >> 2);
+            pass(k_ntt<true, false, 2, ST>, k_ntt<true, false, 2, ST, 2>, k_ntt<true, false, 2, ST, 4>, ST >> 2);
+            pass(k_ntt<true, true, 2, ST>, k_ntt<true, true, 2, ST, 2>, k_ntt<true, true, 2, ST, 4>, ST >> 2);
         }
     };
     if (t1k) {
@@ -3504,25 +3664,25 @@ static void nttRows(sfp_dev* d, const RowGroup& G0, int inverse, int passes = 3)
             smallPasses(std::integral_constant<int, 1024>{});
     } else if (!inverse) {
         if (L == 4) {
-            pass(k_ntt<false, true, 4, T>, NttKern2{}, T >> 4);
-            pass(k_ntt<false, false, 4, T>, NttKern2{}, T >> 4);
+            pass(k_ntt<false, true, 4, T>, NttKern2{}, NttKern4{}, T >> 4);
+            pass(k_ntt<false, false, 4, T>, NttKern2{}, NttKern4{}, T >> 4);
         } else if (L == 2) {
-            pass(k_ntt<false, true, 2, T>, k_ntt<false, true, 2, T, 2>, T >> 2);
-            pass(k_ntt<false, false, 2, T>, k_ntt<false, false, 2, T, 2>, T >> 2);
+            pass(k_ntt<false, true, 2, T>, k_ntt<false, true, 2, T, 2>, k_ntt<false, true, 2, T, 4>, T >> 2);
+            pass(k_ntt<false, false, 2, T>, k_ntt<false, false, 2, T, 2>, k_ntt<false, false, 2, T, 4>, T >> 2);
         } else {
-            pass(k_ntt<false, true, 3, T>, NttKern2{}, T >> 3);
-            pass(k_ntt<false, false, 3, T>, NttKern2{}, T >> 3);
+            pass(k_ntt<false, true, 3, T>, NttKern2{}, NttKern4{}, T >> 3);
+            pass(k_ntt<false, false, 3, T>, NttKern2{}, NttKern4{}, T >> 3);
         }
     } else {
         if (L == 4) {
-            pass(k_ntt<true, false, 4, T>, NttKern2{}, T >> 4);
-            pass(k_ntt<true, true, 4, T>, NttKern2{}, T >> 4);
+            pass(k_ntt<true, false, 4, T>, NttKern2{}, NttKern4{}, T >> 4);
+            pass(k_ntt<true, true, 4, T>, NttKern2{}, NttKern4{}, T >> 4);
         } else if (L == 2) {
-            pass(k_ntt<true, false, 2, T>, k_ntt<true, false, 2, T, 2>, T >> 2);
-            pass(k_ntt<true, true, 2, T>, k_ntt<true, true, 2, T, 2>, T >> 2);
+            pass(k_ntt<true, false, 2, T>, k_ntt<true, false, 2, T, 2>, k_ntt<true, false, 2, T, 4>, T >> 2);
+            pass(k_ntt<true, true, 2, T>, k_ntt<true, true, 2, T, 2>, k_ntt<true, true, 2, T, 4>, T >> 2);
         } else {
-            pass(k_ntt<true, false, 3, T>, NttKern2{}, T >> 3);
-            pass(k_ntt<true, true, 3, T>, NttKern2{}, T >> 3);
+            pass(k_ntt<true, false, 3, T>, NttKern2{}, NttKern4{}, T >> 3);
+            pass(k_ntt<true, true, 3, T>, NttKern2{}, NttKern4{}, T >> 3);
         }
     }
     checkLaunch(d, "ntt");
@@ -3761,7 +3921,7 @@ static void ew(sfp_dev* d, u64* out, const u64* a, const u64* b, const u64* c, s
     const size_t pairs = ((size_t)m.count * d->n) / 2;
     EwArgs A{out, a, b, c, m, {}};
     A.k = ka;
-    issueY<EwArgs>(d, k_ew<OP, 1>, k_ew<OP, 2>, dim3(ewGrid(pairs)), A);
+    issueY<EwArgs>(d, k_ew<OP, 1>, k_ew<OP, 2>, k_ew<OP, 4>, dim3(ewGrid(pairs)), A);
     checkLaunch(d, "elementwise");
 }
 
@@ -3808,7 +3968,7 @@ void sfp_lin_wsum(sfp_dev* d, uint64_t* out, const uint64_t* const* ins, const u
     for (uint32_t j = 0; j < nin; ++j) pl.p[j] = ins[j];
     const u64* dk = (const u64*)ringPut(d, k, (size_t)nin * m.count * 8);
     const size_t total = (size_t)m.count * d->n;
-    issueY<WsumArgs>(d, k_lin_wsum<1>, k_lin_wsum<2>, dim3(ewGrid(total)), WsumArgs{out, pl, dk, nin, m});
+    issueY<WsumArgs>(d, k_lin_wsum<1>, k_lin_wsum<2>, k_lin_wsum<4>, dim3(ewGrid(total)), WsumArgs{out, pl, dk, nin, m});
     checkLaunch(d, "lin_wsum");
 }
 
@@ -3872,7 +4032,7 @@ void sfp_mac_plain(sfp_dev* d, uint64_t* out, const uint64_t* const* a, const ui
 
 void sfp_automorph(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t g, sfp_limbs m) {
     const size_t total = (size_t)m.count * d->n;
-    issueY<AutArgs>(d, k_automorph<1>, k_automorph<2>, dim3(ewGrid(total)), AutArgs{out, in, g, m.count});
+    issueY<AutArgs>(d, k_automorph<1>, k_automorph<2>, k_automorph<4>, dim3(ewGrid(total)), AutArgs{out, in, g, m.count});
     checkLaunch(d, "automorph");
 }
 
@@ -4309,7 +4469,7 @@ static void modupInnerCore(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uin
     timedLaunch(d, SFP_FAM_NTTKS, 8.0 * total * (3.0 * beta + (accum ? 4.0 : 2.0)), [&] {
         ArgSet<KsArgs, 1> AS;
         AS.a[0] = a;
-        AS.split = rows;
+        AS.start[0] = 0;
         AS.inter = 0;
         const int fp = nttFp();
         const dim3 g(n / (t1k ? 1024u : (uint32_t)kNttTile), rows);
@@ -4328,6 +4488,7 @@ static void modupInnerCore(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uin
             P->threads = threads;
             P->useFp = fp;
             P->k2 = t1k ? k_ntt_ks<2, 1024, 2> : k_ntt_ks<2, kNttTile, 2>;
+            P->k4 = t1k ? k_ntt_ks<2, 1024, 4> : k_ntt_ks<2, kNttTile, 4>;
             r.cls = STK_KS;
             r.key = stkKey((const void*)k1, g.x, (uint32_t)threads);
             r.pay = std::move(P);
@@ -4370,7 +4531,7 @@ void sfp_ks_inner_fold(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_
     }
     // reads beta ext rows + 2*beta key rows, writes 2 accumulator rows, per limb
     timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + 2.0), [&] {
-        issueY<KsInnerArgs>(d, k_ks_inner<1>, k_ks_inner<2>, dim3(ewGrid(total / 2)),
+        issueY<KsInnerArgs>(d, k_ks_inner<1>, k_ks_inner<2>, k_ks_inner<4>, dim3(ewGrid(total / 2)),
                                 KsInnerArgs{acc0, acc1, ext, extStride, key, beta, sfp_limbs{ell + K, ell, Lq, 0, 1}, keyQ0, keyRows0, fold0, fold1, foldK, 0, (const u64*)nullptr, d->kg});
     });
     checkLaunch(d, "ks_inner");
@@ -4382,7 +4543,7 @@ void sfp_ks_inner_acc(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t
     const size_t total = (size_t)(ell + K) * d->n;
     // reads beta ext rows + 2*beta key rows + 2 accumulator rows, writes 2, per limb
     timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + 4.0), [&] {
-        issueY<KsInnerArgs>(d, k_ks_inner<1>, k_ks_inner<2>, dim3(ewGrid(total / 2)),
+        issueY<KsInnerArgs>(d, k_ks_inner<1>, k_ks_inner<2>, k_ks_inner<4>, dim3(ewGrid(total / 2)),
                                 KsInnerArgs{acc0, acc1, ext, extStride, key, beta, sfp_limbs{ell + K, ell, Lq, 0, 1}, keyQ0, keyRows0, (const u64*)nullptr, (const u64*)nullptr, (u64)0, 1, (const u64*)nullptr, d->kg});
     });
     checkLaunch(d, "ks_inner_acc");
@@ -4395,7 +4556,7 @@ void sfp_ks_inner_mul(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t
     const size_t total = (size_t)(ell + K) * d->n;
     // reads beta ext rows + 2*beta key rows + the plaintext row (+ 2 accumulator rows), writes 2, per limb
     timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + (accum ? 5.0 : 3.0)), [&] {
-        issueY<KsInnerArgs>(d, k_ks_inner<1>, k_ks_inner<2>, dim3(ewGrid(total / 2)),
+        issueY<KsInnerArgs>(d, k_ks_inner<1>, k_ks_inner<2>, k_ks_inner<4>, dim3(ewGrid(total / 2)),
                                 KsInnerArgs{acc0, acc1, ext, extStride, key, beta, sfp_limbs{ell + K, ell, Lq, 0, 1}, keyQ0, keyRows0, (const u64*)nullptr, (const u64*)nullptr, (u64)0, accum, pm, d->kg});
     });
     checkLaunch(d, "ks_inner_mul");
@@ -4823,7 +4984,7 @@ void sfp_ks_inner_map(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t
     if (!pm.count || !limbsOk(d, pm, "ks_inner_map")) return;
     const size_t total = (size_t)pm.count * d->n;
     timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + (accum ? 4.0 : 2.0)), [&] {
-        issueY<KsInnerArgs>(d, k_ks_inner<1>, k_ks_inner<2>, dim3(ewGrid(total / 2)),
+        issueY<KsInnerArgs>(d, k_ks_inner<1>, k_ks_inner<2>, k_ks_inner<4>, dim3(ewGrid(total / 2)),
                                 KsInnerArgs{acc0, acc1, ext, extStride, key, beta, pm, keyQ, keyRows, (const u64*)nullptr, (const u64*)nullptr, (u64)0, accum, (const u64*)nullptr, d->kg});
     });
     checkLaunch(d, "ks_inner_map");

@@ -327,6 +327,20 @@ void sfp_stack_begin(sfp_dev* d);
 void sfp_stack_end(sfp_dev* d);
 void sfp_stack_stats(sfp_dev* d, uint64_t* merged, uint64_t* single);
 
+// Batched ops (the same mechanism for independent ops of ONE host lane: the
+// Chebyshev PS's products of one tree level, a polynomial's powers of one
+// depth).  sfp_batch_begin(d, count) returns 1 if batching is on; the host
+// then issues op i after sfp_batch_lane(d, i) and calls sfp_batch_end, which
+// issues everything on the caller's lane, up to four identical launches of
+// different ops merged into one.  The ops' buffers must stay allocated until
+// sfp_batch_end (their launches are issued there).  Returns 0 (the ops run as
+// issued) for the oracle, with SFHE_BATCH=0, inside a stacked lane region or
+// with serialised lanes.
+#define SFP_BATCH_MAX 4
+int sfp_batch_begin(sfp_dev* d, uint32_t count);
+void sfp_batch_lane(sfp_dev* d, uint32_t i);
+void sfp_batch_end(sfp_dev* d);
+
 // ---- multi-process limb sharding (one process per GPU) --------------------------
 // Collectives over the ranks of a sharded context, ordered on the current
 // lane like every other primitive.  Two transports:

@@ -182,3 +182,38 @@ def test_debug_sort_repeats(oracle_lib, capfd):
     assert np.array_equal(outs[0], outs[1]) and np.array_equal(outs[1], outs[2])
     assert texts[1] == texts[2]
     np.testing.assert_allclose(np.array(e.decrypt(e.sorter(N).sort(ct, *cfg)))[:N], np.sort(x), atol=0.01)
+
+
+WAVES_CHILD = r"""
+import hashlib, sys
+import sfhe
+from oracle import slotsim
+N = 16
+depth, rots = sfhe.direct_sort_params(N, "oracle")
+e = sfhe.Engine("oracle", mult_depth=depth, ring_dim=1 << 12, batch_size=N, rotations=rots, seed=5)
+e.set_quiet(True)
+o = e.sorter(N).sort(e.encrypt(slotsim.input_vector(N).tolist()), *slotsim.default_sign_config(N))
+e2 = sfhe.Engine("oracle", mult_depth=30, ring_dim=1 << 12, batch_size=8, scaling_mod_size=50, seed=6)
+s = e2.sign(e2.encrypt([0.3, -0.2, 0.05, -0.7]), 4, 3, 3)
+print(hashlib.sha256(o.download().tobytes() + s.download().tobytes()).hexdigest())
+"""
+
+
+def test_ps_waves_same_values(oracle_lib):
+    """The level-synchronous Chebyshev PS and polynomial powers (EvalMultMany
+    waves, the default) against the recursive order (SFHE_PS_WAVES=0): the
+    same operations on the same operands, so the same residues -- a whole
+    DirectSort<16> and a CompositeSign(4,3,3) (knob read once per process:
+    child processes)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([os.path.join(root, "sorting-fhe_amd", "python"), root]))
+    out = []
+    for w in ("1", "0"):
+        p = subprocess.run([sys.executable, "-c", WAVES_CHILD], env=dict(env, SFHE_PS_WAVES=w), capture_output=True,
+                           text=True, timeout=600)
+        assert p.returncode == 0, p.stderr[-2000:]
+        out.append(p.stdout.strip().splitlines()[-1])
+    assert out[0] == out[1]
