@@ -553,6 +553,18 @@ def main(argv=None):
         timing = ("HIP events around every launch of the family on the stream it runs on, during one "
                   f"profiling sort after the timed region with the lanes serialised ({serial_ms:.1f} ms)")
     achieved = r_bytes / (r_ms / 1e3) / 1e9 if r_ms else 0.0
+    # every family of the captured sort replayed alone the same way: where the
+    # sort's kernel time goes ("all" = every kernel node back to back, i.e.
+    # without the two lanes' overlap; the timed sort is shorter by that overlap)
+    graph_breakdown = None
+    if not os.environ.get("SFHE_NO_GRAPH_REPLAY"):
+        try:
+            graph_breakdown = {}
+            for f in ("ntt", "conv", "ntt_ks", "ks_inner", "other", "all"):
+                f_ms, f_n, _ = sorter.graph_family_time(f, reps=3)
+                graph_breakdown[f] = {"ms_per_sort": f_ms, "launches_per_sort": f_n}
+        except sfhe.SfheError:
+            graph_breakdown = None
     ratio = pmc_traffic(dom)
     roofline = {
         "bound": "hbm",
@@ -602,6 +614,7 @@ def main(argv=None):
                             "counted over the profiling sort's stacked regions (SFHE_STACK_BATCHES=0: off)"},
         "roofline": roofline,
         "kernels": kernels,
+        "graph_breakdown": graph_breakdown,
         "trials": trials,
         "cpu_baseline": None,
     }

@@ -111,6 +111,8 @@ int sfhe_live_contexts(void);
 #define SFHE_KFAM_CONV 1
 #define SFHE_KFAM_KSINNER 2
 #define SFHE_KFAM_NTTKS 3   /* k_ntt_ks: ModUp's ROW pass fused with the key inner product */
+#define SFHE_KFAM_OTHER 4   /* (graph timing only) every kernel of no family above */
+#define SFHE_KFAM_ALL 5     /* (graph timing only) every kernel */
 int sfhe_kernel_timing(sfhe_ctx* c, uint32_t family, uint32_t period);
 int sfhe_kernel_timing_read(sfhe_ctx* c, uint32_t family, uint64_t* launches, uint64_t* timed,
                             double* ms, double* bytes);
@@ -211,6 +213,11 @@ int sfhe_sorter_graph_nodes(const sfhe_sorter* s, uint64_t* nodes);
  * kernel time of one sort), *launches, *bytes (algorithmic: 16 B per
  * coefficient per pass).  SFHE_EINVAL-class error when no graph exists. */
 int sfhe_sorter_graph_ntt_time(sfhe_sorter* s, int reps, double* ms, uint64_t* launches, double* bytes);
+/* The same for any family SFHE_KFAM_* (OTHER: the kernels of no family, ALL:
+ * every kernel node -- the sort's kernel time without lane overlap); *bytes
+ * counts the NTT passes only. */
+int sfhe_sorter_graph_family_time(sfhe_sorter* s, uint32_t family, int reps, double* ms, uint64_t* launches,
+                                  double* bytes);
 /* DirectSort<N>::sort_hybrid1 (sort_algo.h:1213-1229): constructRank, then
  * rotationIndexCheckHybrid1 (:1067-1209, MEHP24 indicatorAdv placement,
  * mehp24_utils.cpp:166-174, :246-261).  Needs ring dimension >= 2 N^2 for

@@ -836,9 +836,9 @@ class DirectSort : public SortBase<N> {
         if (m_graph) return m_cc->GraphNodes(m_graph->g);
         return m_debugGraphs ? m_cc->GraphNodes(m_debugGraphs->rank) + m_cc->GraphNodes(m_debugGraphs->place) : 0;
     }
-    // the captured sort's NTT kernels replayed alone (bench roofline)
-    bool graphNttTime(int reps, double* ms, uint64_t* launches, double* bytes) {
-        return m_graph && m_cc->GraphNttTime(m_graph->g, reps, ms, launches, bytes);
+    // the captured sort's kernels of one family replayed alone (bench roofline)
+    bool graphFamilyTime(uint32_t family, int reps, double* ms, uint64_t* launches, double* bytes) {
+        return m_graph && m_cc->GraphFamilyTime(m_graph->g, family, reps, ms, launches, bytes);
     }
 
     // Debug sorts (DebugEncryption: PRINT_PT decrypts of the input, the rank

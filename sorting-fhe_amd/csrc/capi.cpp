@@ -103,7 +103,7 @@ struct SorterBase {
     virtual Ct place2N(const Ct& rank, const Ct& in) = 0;
     virtual Ct bitonic(const Ct& in, SignConfig& cfg) = 0;
     virtual size_t graphNodes() const = 0;
-    virtual bool graphNttTime(int reps, double* ms, uint64_t* launches, double* bytes) = 0;
+    virtual bool graphFamilyTime(uint32_t family, int reps, double* ms, uint64_t* launches, double* bytes) = 0;
 };
 
 template <int N>
@@ -135,8 +135,8 @@ struct Sorter : SorterBase {
     }
     Ct place2N(const Ct& r, const Ct& in) override { return ds.rotationIndexCheck2N(r, in); }
     size_t graphNodes() const override { return ds.graphNodes(); }
-    bool graphNttTime(int reps, double* ms, uint64_t* launches, double* bytes) override {
-        return ds.graphNttTime(reps, ms, launches, bytes);
+    bool graphFamilyTime(uint32_t family, int reps, double* ms, uint64_t* launches, double* bytes) override {
+        return ds.graphFamilyTime(family, reps, ms, launches, bytes);
     }
 };
 
@@ -715,12 +715,19 @@ int sfhe_hybrid_params(uint32_t N, int variant, uint32_t* mult_depth, int32_t* r
     return SFHE_OK;
 }
 
-int sfhe_sorter_graph_ntt_time(sfhe_sorter* s, int reps, double* ms, uint64_t* launches, double* bytes) {
+int sfhe_sorter_graph_family_time(sfhe_sorter* s, uint32_t family, int reps, double* ms, uint64_t* launches,
+                                  double* bytes) {
     REQUIRE(s && ms && reps > 0, "null argument");
+    static_assert(SFHE_KFAM_OTHER == SFP_FAM_COUNT && SFHE_KFAM_ALL == SFP_FAM_ALL, "family numbering");
+    REQUIRE(family <= SFHE_KFAM_ALL, "unknown kernel family");
     return guard([&] {
-        if (!s->impl->graphNttTime(reps, ms, launches, bytes))
+        if (!s->impl->graphFamilyTime(family, reps, ms, launches, bytes))
             throw std::runtime_error("no captured sort graph (or no graphs on this backend)");
     });
+}
+
+int sfhe_sorter_graph_ntt_time(sfhe_sorter* s, int reps, double* ms, uint64_t* launches, double* bytes) {
+    return sfhe_sorter_graph_family_time(s, SFHE_KFAM_NTT, reps, ms, launches, bytes);
 }
 
 int sfhe_sorter_graph_nodes(const sfhe_sorter* s, uint64_t* nodes) {

@@ -277,14 +277,23 @@ class PSEvaluator {
                 }
                 progress = true;
             }
-            for (auto& nd : nodes) {
-                if (nd.hasOut || !nd.hasProd || !ready(nd.r)) continue;
-                if (nd.r.isConst)
-                    nd.out = nd.r.c != 0.0 ? cc->EvalAdd(nd.prod, nd.r.c) : nd.prod;
-                else
-                    nd.out = cc->EvalAdd(nd.prod, value(nd.r));
-                nd.hasOut = true;
-                nd.prod = nullptr;
+            // the ready sums, as batches of independent ops
+            std::vector<Node*> sums;
+            for (auto& nd : nodes)
+                if (!nd.hasOut && nd.hasProd && ready(nd.r)) sums.push_back(&nd);
+            for (size_t b0 = 0; b0 < sums.size(); b0 += batchWidth()) {
+                const size_t b1 = std::min(sums.size(), b0 + batchWidth());
+                BatchScope bs(cc, (uint32_t)(b1 - b0));
+                for (size_t t = b0; t < b1; ++t) {
+                    Node& nd = *sums[t];
+                    bs.lane((uint32_t)(t - b0));
+                    if (nd.r.isConst)
+                        nd.out = nd.r.c != 0.0 ? cc->EvalAdd(nd.prod, nd.r.c) : nd.prod;
+                    else
+                        nd.out = cc->EvalAdd(nd.prod, value(nd.r));
+                    nd.hasOut = true;
+                    nd.prod = nullptr;
+                }
                 progress = true;
             }
             if (!progress) SFHE_THROW("internal: Chebyshev wave evaluation stalled");

@@ -155,7 +155,9 @@ DeviceBuffer::~DeviceBuffer() {
             return;
         }
     }
-    if (!st->forkedLanes)
+    if (st->batchDepth)
+        st->batchFree.push_back({words, ptr});  // its batch's launches are not issued yet
+    else if (!st->forkedLanes)
         st->freeList[0][words].push_back(ptr);  // everything is ordered behind lane 0 again
     else if (region == st->region && lane == st->myLane())
         st->freeList[lane][words].push_back(ptr);  // private to this lane in this region
@@ -947,17 +949,16 @@ class SfheInternal {
         if (ell < 2) SFHE_THROW("no levels left to rescale (multiplicative depth exhausted)");
         const uint32_t n = s->n, K = s->K, beta = (ell + s->alpha - 1) / s->alpha;
         const size_t stride = (size_t)(ell + K) * n;
-        std::vector<DeviceBufferPtr> keep;
         auto& convs = modupConv(cc, ell);
         size_t done = 0;
-        if (!s->shardAt(ell) && sfp_batch_begin(s->dev, (uint32_t)cnt)) {
+        BatchScope bs(cc, s->shardAt(ell) ? 0 : (uint32_t)cnt);
+        if (bs) {
             for (; done < cnt; ++done) {
                 out[done] = newCt(cc, level + 1, slots[done]);
                 auto acc = s->alloc(2 * stride);
                 auto ext = s->alloc(stride * beta);
                 auto scratch = s->alloc((size_t)2 * ell * n);
-                keep.insert(keep.end(), {acc, ext, scratch});
-                sfp_batch_lane(s->dev, (uint32_t)done);
+                bs.lane((uint32_t)done);
                 if (sfp_mult_relin_rescale(s->dev, out[done]->c0, out[done]->c1, a[done]->c0, a[done]->c1,
                                            b[done]->c0, b[done]->c1, ell, K, s->Lq, s->alpha, convs.data(),
                                            s->relinKey->ptr, s->moddownConv, s->pInvModQ.data(), s->pModQ.data(),
@@ -968,7 +969,6 @@ class SfheInternal {
                 s->countBytes((3.0 * ell + 2.0 * beta * (ell + K)) * n * 8);
                 s->countBytes(4.0 * ell * n * 8);
             }
-            sfp_batch_end(s->dev);
         }
         for (size_t i = done; i < cnt; ++i)
             out[i] = multRelinRescale(cc, a[i]->c0, a[i]->c1, b[i]->c0, b[i]->c1, level, slots[i]);
@@ -1867,6 +1867,38 @@ void CryptoContextImpl<DCRTPoly>::JoinLanes() {
     s->region = 0;
 }
 
+bool CryptoContextImpl<DCRTPoly>::BeginBatch(uint32_t count) {
+    SfheContextState* s = st.get();
+    s->opMu.lock();  // held until EndBatch: no other host thread issues in between
+    {
+        OpLock g(s);
+        if (!s->batchDepth && sfp_batch_begin(s->dev, count)) {
+            ++s->batchDepth;
+            return true;
+        }
+    }
+    s->opMu.unlock();
+    return false;
+}
+
+void CryptoContextImpl<DCRTPoly>::BatchLane(uint32_t i) {
+    OpLock g(st.get());
+    if (st->batchDepth) sfp_batch_lane(st->dev, i);
+}
+
+void CryptoContextImpl<DCRTPoly>::EndBatch() {
+    OpLock g(st.get());
+    SfheContextState* s = st.get();
+    if (!s->batchDepth) return;
+    sfp_batch_end(s->dev);  // every op of the batch is issued on this lane now
+    --s->batchDepth;
+    std::lock_guard<std::mutex> pg(s->poolMu);
+    const int l = s->forkedLanes ? s->lane : 0;
+    for (auto& e : s->batchFree) s->freeList[l][e.first].push_back(e.second);
+    s->batchFree.clear();
+    s->opMu.unlock();  // (BeginBatch's)
+}
+
 void CryptoContextImpl<DCRTPoly>::SetPlaintextCache(bool on) {
     OpLock g(st.get());
     st->ptCacheOn = on;
@@ -2498,7 +2530,7 @@ std::vector<Ciphertext<DCRTPoly>> CryptoContextImpl<DCRTPoly>::EvalMultMany(
     // runs of up to SFP_BATCH_MAX consecutive pairs at one level
     for (size_t i = 0; i < cnt;) {
         size_t j = i + 1;
-        while (j < cnt && j - i < SFP_BATCH_MAX && A[j]->level == A[i]->level) ++j;
+        while (j < cnt && j - i < batchWidth() && A[j]->level == A[i]->level) ++j;
         std::vector<const CiphertextImpl<DCRTPoly>*> pa, pb;
         std::vector<uint32_t> slots;
         for (size_t k = i; k < j; ++k) {
@@ -3310,11 +3342,11 @@ void CryptoContextImpl<DCRTPoly>::Launch(const std::shared_ptr<CapturedGraph>& g
     if (g->keep) s->wrote(g->keep->buf.get());
 }
 
-bool CryptoContextImpl<DCRTPoly>::GraphNttTime(const std::shared_ptr<CapturedGraph>& g, int reps, double* ms,
-                                               uint64_t* launches, double* bytes) {
+bool CryptoContextImpl<DCRTPoly>::GraphFamilyTime(const std::shared_ptr<CapturedGraph>& g, uint32_t family,
+                                                  int reps, double* ms, uint64_t* launches, double* bytes) {
     if (!g || !g->g) return false;
     OpLock lk(st.get());
-    return sfp_graph_family_time(st->dev, g->g, SFP_FAM_NTT, reps, ms, launches, bytes) == 0;
+    return sfp_graph_family_time(st->dev, g->g, family, reps, ms, launches, bytes) == 0;
 }
 
 size_t CryptoContextImpl<DCRTPoly>::GraphNodes(const std::shared_ptr<CapturedGraph>& g) const {

@@ -550,6 +550,15 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
     // sfp_stack_begin): identical ops of different lanes become one launch;
     // JoinLanes issues them.  For lanes that run the same op sequence.
     void ForkLanes(int count, bool stacked = false);
+    // Batched ops (prims.h sfp_batch_*): between BeginBatch(count) and
+    // EndBatch(), op i is issued after BatchLane(i); the ops must be
+    // independent, their identical launches run merged, everything is issued
+    // on this lane at EndBatch (blocks freed meanwhile are reused after it).
+    // BeginBatch returns false (the ops simply run) where batching is off.
+    // (BeginBatch holds the context's op lock until EndBatch; see BatchScope)
+    bool BeginBatch(uint32_t count);
+    void BatchLane(uint32_t i);
+    void EndBatch();
     void SetLane(int lane);
     void JoinLanes();
     // Plaintext-encoding cache across calls (default on); see DESIGN.md.
@@ -587,8 +596,9 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
     void releaseBootstrapGraphs();
     size_t GraphNodes(const std::shared_ptr<CapturedGraph>& g) const;
     // the graph's NTT kernels replayed alone (sfp_graph_family_time)
-    bool GraphNttTime(const std::shared_ptr<CapturedGraph>& g, int reps, double* ms, uint64_t* launches,
-                      double* bytes);
+    // (family: prims.h SFP_FAM_*, SFP_FAM_COUNT = the other kernels, SFP_FAM_ALL = all)
+    bool GraphFamilyTime(const std::shared_ptr<CapturedGraph>& g, uint32_t family, int reps, double* ms,
+                         uint64_t* launches, double* bytes);
     // dst's rows (same level) overwritten with src's: refills a graph's input
     void CopyCiphertextInto(const Ciphertext<DCRTPoly>& dst, const Ciphertext<DCRTPoly>& src);
 
@@ -597,6 +607,27 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
     uint32_t enabled = 0;
     BootstrapTap bootTap;
     friend class SfheInternal;
+};
+
+// A batch of independent ops (CryptoContextImpl::BeginBatch) for one scope:
+// ends the batch on every exit path.  count < 2: no batch, the ops just run.
+class BatchScope {
+  public:
+    BatchScope(CryptoContextImpl<DCRTPoly>* cc, uint32_t count)
+        : cc_(cc), on_(count > 1 && cc->BeginBatch(count)) {}
+    ~BatchScope() {
+        if (on_) cc_->EndBatch();
+    }
+    BatchScope(const BatchScope&) = delete;
+    BatchScope& operator=(const BatchScope&) = delete;
+    explicit operator bool() const { return on_; }
+    void lane(uint32_t i) {
+        if (on_) cc_->BatchLane(i);
+    }
+
+  private:
+    CryptoContextImpl<DCRTPoly>* cc_;
+    bool on_;
 };
 
 // Registers the context for key deserialization (Deserialize*Key below find

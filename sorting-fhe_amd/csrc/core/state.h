@@ -1,7 +1,9 @@
 // Internal state of a CKKS context (not part of the public API).
 #pragma once
+#include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -89,6 +91,10 @@ struct SfheContextState {
     // ordered after it (same lane, or any lane after a join)
     std::map<size_t, std::vector<uint64_t*>> freeList[SFP_MAX_LANES];
     std::vector<std::pair<size_t, uint64_t*>> deferredFree;  // cross-lane frees inside a region
+    // batched ops (BeginBatch): their launches are issued at EndBatch, so a
+    // block freed while the batch is recorded is reused only after it
+    uint32_t batchDepth = 0;
+    std::vector<std::pair<size_t, uint64_t*>> batchFree;
     // lane 0's free blocks at ForkLanes: every lane of the region is ordered
     // after them, so any lane may reuse them (without this, blocks a lane
     // allocates migrate to lane 0 at every join and the pool grows per region)
@@ -219,6 +225,16 @@ class FullScope {
     int rank_, world_;
     bool sharded_, was_;
 };
+
+// Ops per batch (BeginBatch): SFHE_BATCH_WIDTH, 2..SFP_BATCH_MAX (default).
+inline uint32_t batchWidth() {
+    static const uint32_t w = [] {
+        const char* v = std::getenv("SFHE_BATCH_WIDTH");
+        const long x = v && *v ? std::strtol(v, nullptr, 10) : SFP_BATCH_MAX;
+        return (uint32_t)std::max(2L, std::min<long>(x, SFP_BATCH_MAX));
+    }();
+    return w;
+}
 
 // Serialises host-side use of a context and routes the calling thread's
 // operations to its lane (each host thread of a lane region has its own).

@@ -1254,10 +1254,251 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt_ks(const ArgSet<KsArgs, NG> 
     const bool inv = t >= A.invFrom;
     const u64* iw = fp ? reinterpret_cast<const u64*>(A.itwD) + (size_t)prime * n : A.itw + (size_t)prime * n;
     const u64* ix = A.itwS + (size_t)prime * n;
-    // Register prefetches (the kernel runs at two waves per SIMD, so latency
-    // is hidden by loads in flight, not by other waves): the inverse pass's
-    // twiddles, the previous accumulator, and each digit's key rows below are
-    // issued before the work that precedes their use.
+    // Each digit's key rows are issued before the ROW rounds that precede
+    // their use (loads in flight hide their latency at this occupancy).
+    u64* o0 = A.acc0 + (size_t)t * n + rowOff;
+    u64* o1 = A.acc1 + (size_t)t * n + rowOff;
+    // The digits' products: FP64 rows (every row but q_0 at the metric's
+    // parameters) accumulate exact residues of each product (fpMulMod: an
+    // integer-valued double congruent to v * key, |r| < 2^45, so the few
+    // digits' and the fold's terms sum exactly below 2^52); the integer row
+    // accumulates 128-bit sums.  Either way the stored value is the canonical
+    // residue of the same sum (bit-identical outputs).
+    auto body = [&](auto fpTag) {
+        constexpr bool FP = decltype(fpTag)::value;
+        using AccT = std::conditional_t<FP, double, Acc>;
+        AccT a0[2 * NPAIR], a1[2 * NPAIR];
+#pragma unroll
+        for (int w = 0; w < 2 * NPAIR; ++w) {
+            if constexpr (FP) a0[w] = a1[w] = 0.0;
+            else a0[w] = a1[w] = Acc{0, 0};
+        }
+        // (a * b mod q for canonical u64 operands, as the accumulator's term)
+        auto term = [&](AccT& acc, auto x, u64 w) {
+            if constexpr (FP) {
+                const double wd = u2d(w);
+                double y;
+                if constexpr (std::is_same_v<decltype(x), u64>) y = u2d(x);
+                else y = x;
+                acc += fpMulMod(y, wd, wd * qi, qd);
+            } else {
+                macc(acc, (u64)x, w);
+            }
+        };
+        for (uint32_t j = 0; j < A.beta; ++j) {
+            const bool own = t < A.ell && t >= j * A.alpha && t < min((j + 1) * A.alpha, A.ell);
+            std::conditional_t<FP, double, u64> v[2 * NPAIR];
+            const u64* kb = A.key + (size_t)j * 2 * A.keyRows * n + (size_t)kr * n + rowOff;
+            const u64* ka = kb + (size_t)A.keyRows * n;
+            ulonglong2 kb2[NPAIR], ka2[NPAIR];
+            if (own) {
+                const u64* src = A.in + (size_t)t * n + rowOff;
+                const u64* mul = A.inMul ? A.inMul + (size_t)t * n + rowOff : nullptr;
+#pragma unroll
+                for (int k = 0; k < NPAIR; ++k) {
+                    const uint32_t e = 2 * (threadIdx.x + k * NT);
+                    ulonglong2 x = *reinterpret_cast<const ulonglong2*>(src + e);
+                    if (mul) {
+                        const ulonglong2 m = *reinterpret_cast<const ulonglong2*>(mul + e);
+                        x.x = bmul(x.x, m.x, B);
+                        x.y = bmul(x.y, m.y, B);
+                    }
+                    if constexpr (FP) {
+                        v[2 * k] = u2d(x.x);
+                        v[2 * k + 1] = u2d(x.y);
+                    } else {
+                        v[2 * k] = x.x;
+                        v[2 * k + 1] = x.y;
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < NPAIR; ++k) {
+                    const uint32_t e = 2 * (threadIdx.x + k * NT);
+                    kb2[k] = *reinterpret_cast<const ulonglong2*>(kb + e);
+                    ka2[k] = *reinterpret_cast<const ulonglong2*>(ka + e);
+                }
+            } else {
+                const u64* src = A.ext + j * A.extStride + (size_t)t * n + rowOff;
+                ulonglong2 xs[NPAIR];
+#pragma unroll
+                for (int k = 0; k < NPAIR; ++k)
+                    xs[k] = *reinterpret_cast<const ulonglong2*>(src + 2 * (threadIdx.x + k * NT));
+#pragma unroll
+                for (int k = 0; k < NPAIR; ++k) {  // in flight during the ROW rounds
+                    const uint32_t e = 2 * (threadIdx.x + k * NT);
+                    kb2[k] = *reinterpret_cast<const ulonglong2*>(kb + e);
+                    ka2[k] = *reinterpret_cast<const ulonglong2*>(ka + e);
+                }
+                __syncthreads();  // the previous digit's readers are done with s
+#pragma unroll
+                for (int k = 0; k < NPAIR; ++k) {
+                    const uint32_t e = 2 * (threadIdx.x + k * NT);
+                    const ulonglong2 x = xs[k];
+                    if constexpr (FP) {
+                        s[ldsSw(e)] = __double_as_longlong(u2d(x.x));
+                        s[ldsSw(e + 1)] = __double_as_longlong(u2d(x.y));
+                    } else {
+                        s[ldsSw(e)] = x.x;
+                        s[ldsSw(e + 1)] = x.y;
+                    }
+                }
+                __syncthreads();
+                bool done = false;
+                if constexpr (kPfBuild && FP) {
+#pragma unroll
+                    for (int r = 0; r < kPfRounds; ++r) {
+                        nttRoundFP<false, false, 2, 2, TILE, true, 8>(reinterpret_cast<double*>(s), T, S0, 2 * r,
+                                                                      qd, nullptr, qi, PW + 3 * r);
+                        __syncthreads();
+                    }
+                    done = true;
+                }
+                if (!done) {
+                    const uint32_t nr = (8 + LE - 1) / LE;
+                    for (uint32_t r = 0; r < nr; ++r) {
+                        const uint32_t k0 = LE * r;
+                        const int b = (int)min((uint32_t)LE, 8u - k0);
+                        if constexpr (FP)
+                            nttRoundDynFP<false, false, LE, TILE>(b, reinterpret_cast<double*>(s), T, S0, k0, qd,
+                                                                  reinterpret_cast<const double*>(gw), qi);
+                        else
+                            nttRoundDyn<false, false, LE, TILE>(b, s, T, S0, k0, q, gw, gx);
+                        __syncthreads();
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < NPAIR; ++k) {
+                    const uint32_t e = 2 * (threadIdx.x + k * NT);
+                    u64 x0 = s[ldsSw(e)], x1 = s[ldsSw(e + 1)];
+                    if constexpr (FP) {  // integer-valued doubles in the rounds' range: fpMulMod takes them as they are
+                        v[2 * k] = __longlong_as_double(x0);
+                        v[2 * k + 1] = __longlong_as_double(x1);
+                    } else {  // forward lazy range [0, 4q) -> [0, q)
+                        x0 = x0 >= 2 * q ? x0 - 2 * q : x0;
+                        x1 = x1 >= 2 * q ? x1 - 2 * q : x1;
+                        x0 = x0 >= q ? x0 - q : x0;
+                        x1 = x1 >= q ? x1 - q : x1;
+                        v[2 * k] = x0;
+                        v[2 * k + 1] = x1;
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < NPAIR; ++k) {
+                const ulonglong2 b2 = kb2[k];
+                const ulonglong2 a2 = ka2[k];
+                term(a0[2 * k], v[2 * k], b2.x);
+                term(a0[2 * k + 1], v[2 * k + 1], b2.y);
+                term(a1[2 * k], v[2 * k], a2.x);
+                term(a1[2 * k + 1], v[2 * k + 1], a2.y);
+            }
+        }
+        // the previous accumulator, loaded after the digits (holding it in
+        // registers through them costs a wave per SIMD)
+        ulonglong2 prev[2][NPAIR];
+        if (A.accum) {
+#pragma unroll
+            for (int k = 0; k < NPAIR; ++k) {
+                const uint32_t e = 2 * (threadIdx.x + k * NT);
+                prev[0][k] = *reinterpret_cast<const ulonglong2*>(o0 + e);
+                prev[1][k] = *reinterpret_cast<const ulonglong2*>(o1 + e);
+            }
+        }
+        const bool fold = (A.fold0 || A.fa0) && t == A.ell - 1;
+        if (inv) __syncthreads();  // the last digit's readers are done with s
+#pragma unroll
+        for (int k = 0; k < NPAIR; ++k) {
+            const uint32_t e = 2 * (threadIdx.x + k * NT);
+            if (fold) {  // + P * d_l (sfp_ks_inner_fold)
+                if (A.fa0) {  // d0 = a0 b0, d1 = a0 b1 + a1 b0 at row l (canonical, as k_tensor writes them)
+                    const size_t ro = (size_t)t * n + rowOff + e;
+                    const ulonglong2 x0 = *reinterpret_cast<const ulonglong2*>(A.fa0 + ro);
+                    const ulonglong2 x1 = *reinterpret_cast<const ulonglong2*>(A.fa1 + ro);
+                    const ulonglong2 y0 = *reinterpret_cast<const ulonglong2*>(A.fb0 + ro);
+                    const ulonglong2 y1 = *reinterpret_cast<const ulonglong2*>(A.fb1 + ro);
+                    if constexpr (FP) {
+                        const double fk = u2d(A.foldK), fkq = fk * qi;
+                        const double qx0 = u2d(x0.x), qy0 = u2d(x0.y), qx1 = u2d(x1.x), qy1 = u2d(x1.y);
+                        const double b0x = u2d(y0.x), b0y = u2d(y0.y), b1x = u2d(y1.x), b1y = u2d(y1.y);
+                        const double f0x = fpMulMod(qx0, b0x, b0x * qi, qd), f0y = fpMulMod(qy0, b0y, b0y * qi, qd);
+                        const double f1x = fpMulMod(qx0, b1x, b1x * qi, qd) + fpMulMod(qx1, b0x, b0x * qi, qd);
+                        const double f1y = fpMulMod(qy0, b1y, b1y * qi, qd) + fpMulMod(qy1, b0y, b0y * qi, qd);
+                        a0[2 * k] += fpMulMod(f0x, fk, fkq, qd);
+                        a0[2 * k + 1] += fpMulMod(f0y, fk, fkq, qd);
+                        a1[2 * k] += fpMulMod(f1x, fk, fkq, qd);
+                        a1[2 * k + 1] += fpMulMod(f1y, fk, fkq, qd);
+                    } else {
+                        Acc tt{0, 0}, uu{0, 0};
+                        macc(tt, x0.x, y1.x);
+                        macc(tt, x1.x, y0.x);
+                        macc(uu, x0.y, y1.y);
+                        macc(uu, x1.y, y0.y);
+                        macc(a0[2 * k], bmul(x0.x, y0.x, B), A.foldK);
+                        macc(a0[2 * k + 1], bmul(x0.y, y0.y, B), A.foldK);
+                        macc(a1[2 * k], sf_reduce128_acc(tt.lo, tt.hi, &B), A.foldK);
+                        macc(a1[2 * k + 1], sf_reduce128_acc(uu.lo, uu.hi, &B), A.foldK);
+                    }
+                } else {
+                    const ulonglong2 f0 = *reinterpret_cast<const ulonglong2*>(A.fold0 + (size_t)t * n + rowOff + e);
+                    const ulonglong2 f1 = *reinterpret_cast<const ulonglong2*>(A.fold1 + (size_t)t * n + rowOff + e);
+                    term(a0[2 * k], f0.x, A.foldK);
+                    term(a0[2 * k + 1], f0.y, A.foldK);
+                    term(a1[2 * k], f1.x, A.foldK);
+                    term(a1[2 * k + 1], f1.y, A.foldK);
+                }
+            }
+            if constexpr (FP) {
+                double r[4] = {a0[2 * k], a0[2 * k + 1], a1[2 * k], a1[2 * k + 1]};
+                if (A.accum) {
+                    r[0] += u2d(prev[0][k].x);
+                    r[1] += u2d(prev[0][k].y);
+                    r[2] += u2d(prev[1][k].x);
+                    r[3] += u2d(prev[1][k].y);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) r[u] = fpReduce(r[u], qd, qi);
+                if (!inv) {
+                    *reinterpret_cast<ulonglong2*>(o0 + e) = make_ulonglong2(d2u(r[0]), d2u(r[1]));
+                    *reinterpret_cast<ulonglong2*>(o1 + e) = make_ulonglong2(d2u(r[2]), d2u(r[3]));
+                } else {
+                    s[ldsSw(e)] = __double_as_longlong(r[0]);
+                    s[ldsSw(e + 1)] = __double_as_longlong(r[1]);
+                    s[TILE + ldsSw(e)] = __double_as_longlong(r[2]);
+                    s[TILE + ldsSw(e + 1)] = __double_as_longlong(r[3]);
+                }
+            } else {
+                ulonglong2 r0, r1;
+                r0.x = sf_reduce128_acc(a0[2 * k].lo, a0[2 * k].hi, &B);
+                r0.y = sf_reduce128_acc(a0[2 * k + 1].lo, a0[2 * k + 1].hi, &B);
+                r1.x = sf_reduce128_acc(a1[2 * k].lo, a1[2 * k].hi, &B);
+                r1.y = sf_reduce128_acc(a1[2 * k + 1].lo, a1[2 * k + 1].hi, &B);
+                if (A.accum) {
+                    const ulonglong2 p0 = prev[0][k], p1 = prev[1][k];
+                    r0.x = sf_add(r0.x, p0.x, q);
+                    r0.y = sf_add(r0.y, p0.y, q);
+                    r1.x = sf_add(r1.x, p1.x, q);
+                    r1.y = sf_add(r1.y, p1.y, q);
+                }
+                if (!inv) {
+                    *reinterpret_cast<ulonglong2*>(o0 + e) = r0;
+                    *reinterpret_cast<ulonglong2*>(o1 + e) = r1;
+                } else {
+                    s[ldsSw(e)] = r0.x;
+                    s[ldsSw(e + 1)] = r0.y;
+                    s[TILE + ldsSw(e)] = r1.x;
+                    s[TILE + ldsSw(e + 1)] = r1.y;
+                }
+            }
+        }
+    };
+    if (fp)
+        body(std::true_type{});
+    else
+        body(std::false_type{});
+    if (!inv) return;
+    // ModDown's inverse ROW pass on both accumulators' tiles, round by round
+    // (as k_ntt's first inverse pass: FP64 rows leave canonical, integer rows
+    // in [0, 2q)); its twiddles are loaded here, after the digits
     double PIW[kPfBuild ? kPfRounds * 3 : 1];
     if constexpr (kPfBuild) {
         if (fp && inv) {
@@ -1279,186 +1520,6 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt_ks(const ArgSet<KsArgs, NG> 
             }
         }
     }
-    u64* o0 = A.acc0 + (size_t)t * n + rowOff;
-    u64* o1 = A.acc1 + (size_t)t * n + rowOff;
-    ulonglong2 prev[2][NPAIR];
-    if (A.accum) {
-#pragma unroll
-        for (int k = 0; k < NPAIR; ++k) {
-            const uint32_t e = 2 * (threadIdx.x + k * NT);
-            prev[0][k] = *reinterpret_cast<const ulonglong2*>(o0 + e);
-            prev[1][k] = *reinterpret_cast<const ulonglong2*>(o1 + e);
-        }
-    }
-    Acc a0[2 * NPAIR], a1[2 * NPAIR];
-#pragma unroll
-    for (int w = 0; w < 2 * NPAIR; ++w) a0[w] = a1[w] = Acc{0, 0};
-    for (uint32_t j = 0; j < A.beta; ++j) {
-        const bool own = t < A.ell && t >= j * A.alpha && t < min((j + 1) * A.alpha, A.ell);
-        u64 v[2 * NPAIR];
-        const u64* kb = A.key + (size_t)j * 2 * A.keyRows * n + (size_t)kr * n + rowOff;
-        const u64* ka = kb + (size_t)A.keyRows * n;
-        ulonglong2 kb2[NPAIR], ka2[NPAIR];
-        if (own) {
-            const u64* src = A.in + (size_t)t * n + rowOff;
-            const u64* mul = A.inMul ? A.inMul + (size_t)t * n + rowOff : nullptr;
-#pragma unroll
-            for (int k = 0; k < NPAIR; ++k) {
-                const uint32_t e = 2 * (threadIdx.x + k * NT);
-                ulonglong2 x = *reinterpret_cast<const ulonglong2*>(src + e);
-                if (mul) {
-                    const ulonglong2 m = *reinterpret_cast<const ulonglong2*>(mul + e);
-                    x.x = bmul(x.x, m.x, B);
-                    x.y = bmul(x.y, m.y, B);
-                }
-                v[2 * k] = x.x;
-                v[2 * k + 1] = x.y;
-            }
-#pragma unroll
-            for (int k = 0; k < NPAIR; ++k) {
-                const uint32_t e = 2 * (threadIdx.x + k * NT);
-                kb2[k] = *reinterpret_cast<const ulonglong2*>(kb + e);
-                ka2[k] = *reinterpret_cast<const ulonglong2*>(ka + e);
-            }
-        } else {
-            const u64* src = A.ext + j * A.extStride + (size_t)t * n + rowOff;
-            ulonglong2 xs[NPAIR];
-#pragma unroll
-            for (int k = 0; k < NPAIR; ++k) xs[k] = *reinterpret_cast<const ulonglong2*>(src + 2 * (threadIdx.x + k * NT));
-#pragma unroll
-            for (int k = 0; k < NPAIR; ++k) {  // in flight during the ROW rounds
-                const uint32_t e = 2 * (threadIdx.x + k * NT);
-                kb2[k] = *reinterpret_cast<const ulonglong2*>(kb + e);
-                ka2[k] = *reinterpret_cast<const ulonglong2*>(ka + e);
-            }
-            __syncthreads();  // the previous digit's readers are done with s
-#pragma unroll
-            for (int k = 0; k < NPAIR; ++k) {
-                const uint32_t e = 2 * (threadIdx.x + k * NT);
-                const ulonglong2 x = xs[k];
-                if (fp) {
-                    s[ldsSw(e)] = __double_as_longlong(u2d(x.x));
-                    s[ldsSw(e + 1)] = __double_as_longlong(u2d(x.y));
-                } else {
-                    s[ldsSw(e)] = x.x;
-                    s[ldsSw(e + 1)] = x.y;
-                }
-            }
-            __syncthreads();
-            bool done = false;
-            if constexpr (kPfBuild) {
-                if (fp) {
-#pragma unroll
-                    for (int r = 0; r < kPfRounds; ++r) {
-                        nttRoundFP<false, false, 2, 2, TILE, true, 8>(reinterpret_cast<double*>(s), T, S0, 2 * r,
-                                                                      qd, nullptr, qi, PW + 3 * r);
-                        __syncthreads();
-                    }
-                    done = true;
-                }
-            }
-            if (!done) {
-                const uint32_t nr = (8 + LE - 1) / LE;
-                for (uint32_t r = 0; r < nr; ++r) {
-                    const uint32_t k0 = LE * r;
-                    const int b = (int)min((uint32_t)LE, 8u - k0);
-                    if (fp)
-                        nttRoundDynFP<false, false, LE, TILE>(b, reinterpret_cast<double*>(s), T, S0, k0, qd,
-                                                              reinterpret_cast<const double*>(gw), qi);
-                    else
-                        nttRoundDyn<false, false, LE, TILE>(b, s, T, S0, k0, q, gw, gx);
-                    __syncthreads();
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < NPAIR; ++k) {
-                const uint32_t e = 2 * (threadIdx.x + k * NT);
-                u64 x0 = s[ldsSw(e)], x1 = s[ldsSw(e + 1)];
-                if (fp) {  // canonical [0, q), as the ROW pass stores it
-                    x0 = d2u(fpReduce(__longlong_as_double(x0), qd, qi));
-                    x1 = d2u(fpReduce(__longlong_as_double(x1), qd, qi));
-                } else {  // forward lazy range [0, 4q) -> [0, q)
-                    x0 = x0 >= 2 * q ? x0 - 2 * q : x0;
-                    x1 = x1 >= 2 * q ? x1 - 2 * q : x1;
-                    x0 = x0 >= q ? x0 - q : x0;
-                    x1 = x1 >= q ? x1 - q : x1;
-                }
-                v[2 * k] = x0;
-                v[2 * k + 1] = x1;
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < NPAIR; ++k) {
-            const ulonglong2 b2 = kb2[k];
-            const ulonglong2 a2 = ka2[k];
-            macc(a0[2 * k], v[2 * k], b2.x);
-            macc(a0[2 * k + 1], v[2 * k + 1], b2.y);
-            macc(a1[2 * k], v[2 * k], a2.x);
-            macc(a1[2 * k + 1], v[2 * k + 1], a2.y);
-        }
-    }
-    const bool fold = (A.fold0 || A.fa0) && t == A.ell - 1;
-    if (inv) __syncthreads();  // the last digit's readers are done with s
-#pragma unroll
-    for (int k = 0; k < NPAIR; ++k) {
-        const uint32_t e = 2 * (threadIdx.x + k * NT);
-        if (fold) {  // + P * d_l (sfp_ks_inner_fold)
-            ulonglong2 f0, f1;
-            if (A.fa0) {  // d0 = a0 b0, d1 = a0 b1 + a1 b0 at row l (canonical, as k_tensor writes them)
-                const size_t ro = (size_t)t * n + rowOff + e;
-                const ulonglong2 x0 = *reinterpret_cast<const ulonglong2*>(A.fa0 + ro);
-                const ulonglong2 x1 = *reinterpret_cast<const ulonglong2*>(A.fa1 + ro);
-                const ulonglong2 y0 = *reinterpret_cast<const ulonglong2*>(A.fb0 + ro);
-                const ulonglong2 y1 = *reinterpret_cast<const ulonglong2*>(A.fb1 + ro);
-                Acc tt{0, 0}, uu{0, 0};
-                macc(tt, x0.x, y1.x);
-                macc(tt, x1.x, y0.x);
-                macc(uu, x0.y, y1.y);
-                macc(uu, x1.y, y0.y);
-                f0.x = bmul(x0.x, y0.x, B);
-                f0.y = bmul(x0.y, y0.y, B);
-                f1.x = sf_reduce128_acc(tt.lo, tt.hi, &B);
-                f1.y = sf_reduce128_acc(uu.lo, uu.hi, &B);
-            } else {
-                f0 = *reinterpret_cast<const ulonglong2*>(A.fold0 + (size_t)t * n + rowOff + e);
-                f1 = *reinterpret_cast<const ulonglong2*>(A.fold1 + (size_t)t * n + rowOff + e);
-            }
-            macc(a0[2 * k], f0.x, A.foldK);
-            macc(a0[2 * k + 1], f0.y, A.foldK);
-            macc(a1[2 * k], f1.x, A.foldK);
-            macc(a1[2 * k + 1], f1.y, A.foldK);
-        }
-        ulonglong2 r0, r1;
-        r0.x = sf_reduce128_acc(a0[2 * k].lo, a0[2 * k].hi, &B);
-        r0.y = sf_reduce128_acc(a0[2 * k + 1].lo, a0[2 * k + 1].hi, &B);
-        r1.x = sf_reduce128_acc(a1[2 * k].lo, a1[2 * k].hi, &B);
-        r1.y = sf_reduce128_acc(a1[2 * k + 1].lo, a1[2 * k + 1].hi, &B);
-        if (A.accum) {
-            const ulonglong2 p0 = prev[0][k], p1 = prev[1][k];
-            r0.x = sf_add(r0.x, p0.x, q);
-            r0.y = sf_add(r0.y, p0.y, q);
-            r1.x = sf_add(r1.x, p1.x, q);
-            r1.y = sf_add(r1.y, p1.y, q);
-        }
-        if (!inv) {
-            *reinterpret_cast<ulonglong2*>(o0 + e) = r0;
-            *reinterpret_cast<ulonglong2*>(o1 + e) = r1;
-        } else if (fp) {
-            s[ldsSw(e)] = __double_as_longlong(u2d(r0.x));
-            s[ldsSw(e + 1)] = __double_as_longlong(u2d(r0.y));
-            s[TILE + ldsSw(e)] = __double_as_longlong(u2d(r1.x));
-            s[TILE + ldsSw(e + 1)] = __double_as_longlong(u2d(r1.y));
-        } else {
-            s[ldsSw(e)] = r0.x;
-            s[ldsSw(e + 1)] = r0.y;
-            s[TILE + ldsSw(e)] = r1.x;
-            s[TILE + ldsSw(e + 1)] = r1.y;
-        }
-    }
-    if (!inv) return;
-    // ModDown's inverse ROW pass on both accumulators' tiles, round by round
-    // (as k_ntt's first inverse pass: FP64 rows leave canonical, integer rows
-    // in [0, 2q))
     __syncthreads();
     bool done = false;
     if constexpr (kPfBuild) {
@@ -2206,7 +2267,7 @@ __global__ __launch_bounds__(kThreads) void k_convf(const ConvJobs J, const sf_b
 // P-rows (as k_conv), the dropped row's coefficient r = (a_l - conv_l) P^-1
 // mod q_l, and for every kept target t < l:  y_t = conv_t + P_t [r]_t, with
 // [r]_t the centred lift of r (r > q_l/2 stands for r - q_l).
-constexpr int kMdrsJobs = 8;
+constexpr int kMdrsJobs = 16;
 struct MdrsJob {
     const u64* src;  // K P-rows, coefficient domain
     const u64* al;   // accumulator row l, coefficient domain
@@ -2672,6 +2733,7 @@ using NttKernN = void (*)(RowGroupSet<NG>, const sf_barrett*, const u64*, const 
                           uint32_t, const double*, const double*, const double*, const double*, int);
 using NttKern2 = NttKernN<2>;
 using NttKern4 = NttKernN<4>;
+using NttKern8 = NttKernN<8>;
 struct NttPay {
     RowGroup G;
     uint32_t rows;
@@ -2679,6 +2741,7 @@ struct NttPay {
     int threads, useFp;
     NttKern2 k2;
     NttKern4 k4;
+    NttKern8 k8;
     const u64 *tw, *twS;
     const double* twD;
 };
@@ -2692,6 +2755,7 @@ struct KsPay {
     int threads, useFp;
     KsKernN<2> k2;
     KsKernN<4> k4;
+    KsKernN<8> k8;
 };
 using ConvKern = void (*)(ConvJobs, const sf_barrett*, const double*, uint32_t);
 struct ConvPay {
@@ -2708,7 +2772,7 @@ struct MdrsPay {
 using MdrsKern = void (*)(MdrsArgs, const sf_barrett*, const double*, uint32_t);
 
 // up to this many heads become one launch (the ArgSet<T, 4> kernels)
-constexpr int kMergeMax = 4;
+constexpr int kMergeMax = 8;
 
 // The row-group kernels (k_ntt, k_ntt_ks): the heads' argument sets in one
 // ArgSet<T, NG> (NG = 2 or 4), rows concatenated -- or alternating when every
@@ -2803,23 +2867,29 @@ static bool stackMerge(sfp_dev* d, const StackRec* const* h, int cnt, hipStream_
                 total += rows[i];
                 if (P[i]->g.x != P[0]->g.x || P[i]->useFp != P[0]->useFp) return false;
             }
-            if (total > 65535u || !(cnt == 2 ? (bool)P[0]->k2 : (bool)P[0]->k4)) return false;
+            if (total > 65535u || !(cnt == 2 ? (bool)P[0]->k2 : cnt <= 4 ? (bool)P[0]->k4 : (bool)P[0]->k8))
+                return false;
             if (check) return true;
             const NttPay& A = *P[0];
             auto launch = [&](const auto& S, uint32_t tot) {
                 using SetT = std::decay_t<decltype(S)>;
-                NttKernN<sizeof(SetT::a) / sizeof(RowGroup)> k;
-                if constexpr (sizeof(SetT::a) / sizeof(RowGroup) == 2)
+                constexpr int NG = sizeof(SetT::a) / sizeof(RowGroup);
+                NttKernN<NG> k;
+                if constexpr (NG == 2)
                     k = A.k2;
-                else
+                else if constexpr (NG == 4)
                     k = A.k4;
+                else
+                    k = A.k8;
                 hipLaunchKernelGGL(k, dim3(A.g.x, tot), dim3(A.threads), 0, s, S, d->bar, A.tw, A.twS, d->ninv,
                                    d->ninvS, d->logn, A.twD, d->qinvD, d->ninvD, d->ninvQ, A.useFp);
             };
             if (cnt == 2)
                 launchSets<RowGroup, 2>(G, rows, cnt, launch);
-            else
+            else if (cnt <= 4)
                 launchSets<RowGroup, 4>(G, rows, cnt, launch);
+            else
+                launchSets<RowGroup, 8>(G, rows, cnt, launch);
             return true;
         }
         case STK_KS: {
@@ -2833,23 +2903,29 @@ static bool stackMerge(sfp_dev* d, const StackRec* const* h, int cnt, hipStream_
                 total += rows[i];
                 if (P[i]->g.x != P[0]->g.x || P[i]->useFp != P[0]->useFp) return false;
             }
-            if (total > 65535u || !(cnt == 2 ? (bool)P[0]->k2 : (bool)P[0]->k4)) return false;
+            if (total > 65535u || !(cnt == 2 ? (bool)P[0]->k2 : cnt <= 4 ? (bool)P[0]->k4 : (bool)P[0]->k8))
+                return false;
             if (check) return true;
             const KsPay& B = *P[0];
             auto launch = [&](const auto& S, uint32_t tot) {
                 using SetT = std::decay_t<decltype(S)>;
-                KsKernN<sizeof(SetT::a) / sizeof(KsArgs)> k;
-                if constexpr (sizeof(SetT::a) / sizeof(KsArgs) == 2)
+                constexpr int NG = sizeof(SetT::a) / sizeof(KsArgs);
+                KsKernN<NG> k;
+                if constexpr (NG == 2)
                     k = B.k2;
-                else
+                else if constexpr (NG == 4)
                     k = B.k4;
+                else
+                    k = B.k8;
                 hipLaunchKernelGGL(k, dim3(B.g.x, tot), dim3(B.threads), 0, s, S, d->bar, d->psi, d->psiS, d->logn,
                                    d->psiD, d->qinvD, B.useFp);
             };
             if (cnt == 2)
                 launchSets<KsArgs, 2>(A, rows, cnt, launch);
-            else
+            else if (cnt <= 4)
                 launchSets<KsArgs, 4>(A, rows, cnt, launch);
+            else
+                launchSets<KsArgs, 8>(A, rows, cnt, launch);
             return true;
         }
         case STK_CONV: {
@@ -2895,6 +2971,7 @@ static bool stackMerge(sfp_dev* d, const StackRec* const* h, int cnt, hipStream_
             return true;
         }
         case STK_Y: {
+            if (cnt > 4) return false;  // (four element-wise argument sets fill the 4 KB of kernel arguments)
             if (check) return true;
             const YPayBase* Y[kMergeMax];
             for (int i = 0; i < cnt; ++i) Y[i] = static_cast<const YPayBase*>(pay(i));
@@ -3240,7 +3317,8 @@ sfp_dev* sfp_create(int device, const sfp_tables* t) {
         return nullptr;
     }
     d->nLanes = 4;
-    if (const char* v = std::getenv("SFHE_LANES")) d->nLanes = std::max(1, std::min(SFP_MAX_LANES, std::atoi(v)));
+    if (const char* v = std::getenv("SFHE_LANES"))
+        d->nLanes = std::max(1, std::min(SFP_MAX_LANES - SFP_BATCH_MAX, std::atoi(v)));
     for (int l = 0; l < d->nLanes; ++l)
         if (hipStreamCreateWithFlags(&d->streams[l], hipStreamNonBlocking) != hipSuccess) {
             for (int k = 0; k < l; ++k) hipStreamDestroy(d->streams[k]);
@@ -3394,7 +3472,11 @@ void sfp_set_lane(sfp_dev* d, int lane) {
         record(d, "set_lane", hipErrorInvalidValue);
         return;
     }
-    d->cur = lane;
+    if (d->batchOn) {  // a batched op's lane stays its virtual lane
+        if (lane != d->batchCur) record(d, "set_lane (inside a batch)", hipErrorInvalidValue);
+    } else {
+        d->cur = lane;
+    }
     // HIP's current device is per host thread; a lane may be driven from a
     // thread other than the one that created the device
     thread_local int curDev = -1;
@@ -3477,14 +3559,14 @@ void sfp_stack_end(sfp_dev* d) {
 // Batched ops: `count` (<= SFP_BATCH_MAX) independent ops issued one after the
 // other by the host, each after sfp_batch_lane(i), are recorded on virtual
 // lanes and issued at sfp_batch_end on the caller's stream, identical
-// launches of the ops merged (up to four into one).  Inside a stacked lane
-// region (no nesting) or with serialised lanes the ops run as issued.
+// launches of the ops merged (up to kMergeMax into one).  Inside a stacked
+// lane region (no nesting) the ops run as issued.
 int sfp_batch_begin(sfp_dev* d, uint32_t count) {
     static const bool on = [] {
         const char* v = std::getenv("SFHE_BATCH");
         return !v || *v != '0';
     }();
-    if (!on || d->stackOn || d->serial || count < 2 || count > SFP_BATCH_MAX ||
+    if (!on || d->stackOn || count < 2 || count > SFP_BATCH_MAX ||
         d->nLanes > SFP_MAX_LANES - SFP_BATCH_MAX)
         return 0;
     d->stackStream = d->st();
@@ -3601,7 +3683,7 @@ static void nttRows(sfp_dev* d, const RowGroup& G0, int inverse, int passes = 3)
     const bool small = rows < (uint32_t)kNttSmallRows;
     int npass = 0;
     // kern2 / kern4: the same pass over two / four row groups (merged launches), or null
-    auto pass = [&](auto kern, NttKern2 kern2, NttKern4 kern4, int threads) {
+    auto pass = [&](auto kern, NttKern2 kern2, NttKern4 kern4, NttKern8 kern8, int threads) {
         if (!((passes >> npass++) & 1)) return;
         timedLaunch(d, SFP_FAM_NTT, bytes, [&] {
             RowGroupSet<1> GS;
@@ -3623,6 +3705,7 @@ static void nttRows(sfp_dev* d, const RowGroup& G0, int inverse, int passes = 3)
                 P->useFp = fp;
                 P->k2 = kern2;
                 P->k4 = kern4;
+                P->k8 = kern8;
                 P->tw = tw;
                 P->twS = twS;
                 P->twD = twD;
@@ -3643,18 +3726,18 @@ static void nttRows(sfp_dev* d, const RowGroup& G0, int inverse, int passes = 3)
         constexpr int ST = decltype(tileC)::value;
         if (smallLe == 3) {
             if (!inverse) {
-                pass(k_ntt<false, true, 3, ST>, NttKern2{}, NttKern4{}, ST >> 3);
-                pass(k_ntt<false, false, 3, ST>, NttKern2{}, NttKern4{}, ST >> 3);
+                pass(k_ntt<false, true, 3, ST>, NttKern2{}, NttKern4{}, NttKern8{}, ST >> 3);
+                pass(k_ntt<false, false, 3, ST>, NttKern2{}, NttKern4{}, NttKern8{}, ST >> 3);
             } else {
-                pass(k_ntt<true, false, 3, ST>, NttKern2{}, NttKern4{}, ST >> 3);
-                pass(k_ntt<true, true, 3, ST>, NttKern2{}, NttKern4{}, ST >> 3);
+                pass(k_ntt<true, false, 3, ST>, NttKern2{}, NttKern4{}, NttKern8{}, ST >> 3);
+                pass(k_ntt<true, true, 3, ST>, NttKern2{}, NttKern4{}, NttKern8{}, ST >> 3);
             }
         } else if (!inverse) {
-            pass(k_ntt<false, true, 2, ST>, k_ntt<false, true, 2, ST, 2>, k_ntt<false, true, 2, ST, 4>, ST >> 2);
-            pass(k_ntt<false, false, 2, ST>, k_ntt<false, false, 2, ST, 2>, k_ntt<false, false, 2, ST, 4>, ST >> 2);
+            pass(k_ntt<false, true, 2, ST>, k_ntt<false, true, 2, ST, 2>, k_ntt<false, true, 2, ST, 4>, k_ntt<false, true, 2, ST, 8>, ST >> 2);
+            pass(k_ntt<false, false, 2, ST>, k_ntt<false, false, 2, ST, 2>, k_ntt<false, false, 2, ST, 4>, k_ntt<false, false, 2, ST, 8>, ST >> 2);
         } else {
-            pass(k_ntt<true, false, 2, ST>, k_ntt<true, false, 2, ST, 2>, k_ntt<true, false, 2, ST, 4>, ST >> 2);
-            pass(k_ntt<true, true, 2, ST>, k_ntt<true, true, 2, ST, 2>, k_ntt<true, true, 2, ST, 4>, ST >> 2);
+            pass(k_ntt<true, false, 2, ST>, k_ntt<true, false, 2, ST, 2>, k_ntt<true, false, 2, ST, 4>, k_ntt<true, false, 2, ST, 8>, ST >> 2);
+            pass(k_ntt<true, true, 2, ST>, k_ntt<true, true, 2, ST, 2>, k_ntt<true, true, 2, ST, 4>, k_ntt<true, true, 2, ST, 8>, ST >> 2);
         }
     };
     if (t1k) {
@@ -3664,25 +3747,25 @@ static void nttRows(sfp_dev* d, const RowGroup& G0, int inverse, int passes = 3)
             smallPasses(std::integral_constant<int, 1024>{});
     } else if (!inverse) {
         if (L == 4) {
-            pass(k_ntt<false, true, 4, T>, NttKern2{}, NttKern4{}, T >> 4);
-            pass(k_ntt<false, false, 4, T>, NttKern2{}, NttKern4{}, T >> 4);
+            pass(k_ntt<false, true, 4, T>, NttKern2{}, NttKern4{}, NttKern8{}, T >> 4);
+            pass(k_ntt<false, false, 4, T>, NttKern2{}, NttKern4{}, NttKern8{}, T >> 4);
         } else if (L == 2) {
-            pass(k_ntt<false, true, 2, T>, k_ntt<false, true, 2, T, 2>, k_ntt<false, true, 2, T, 4>, T >> 2);
-            pass(k_ntt<false, false, 2, T>, k_ntt<false, false, 2, T, 2>, k_ntt<false, false, 2, T, 4>, T >> 2);
+            pass(k_ntt<false, true, 2, T>, k_ntt<false, true, 2, T, 2>, k_ntt<false, true, 2, T, 4>, k_ntt<false, true, 2, T, 8>, T >> 2);
+            pass(k_ntt<false, false, 2, T>, k_ntt<false, false, 2, T, 2>, k_ntt<false, false, 2, T, 4>, k_ntt<false, false, 2, T, 8>, T >> 2);
         } else {
-            pass(k_ntt<false, true, 3, T>, NttKern2{}, NttKern4{}, T >> 3);
-            pass(k_ntt<false, false, 3, T>, NttKern2{}, NttKern4{}, T >> 3);
+            pass(k_ntt<false, true, 3, T>, NttKern2{}, NttKern4{}, NttKern8{}, T >> 3);
+            pass(k_ntt<false, false, 3, T>, NttKern2{}, NttKern4{}, NttKern8{}, T >> 3);
         }
     } else {
         if (L == 4) {
-            pass(k_ntt<true, false, 4, T>, NttKern2{}, NttKern4{}, T >> 4);
-            pass(k_ntt<true, true, 4, T>, NttKern2{}, NttKern4{}, T >> 4);
+            pass(k_ntt<true, false, 4, T>, NttKern2{}, NttKern4{}, NttKern8{}, T >> 4);
+            pass(k_ntt<true, true, 4, T>, NttKern2{}, NttKern4{}, NttKern8{}, T >> 4);
         } else if (L == 2) {
-            pass(k_ntt<true, false, 2, T>, k_ntt<true, false, 2, T, 2>, k_ntt<true, false, 2, T, 4>, T >> 2);
-            pass(k_ntt<true, true, 2, T>, k_ntt<true, true, 2, T, 2>, k_ntt<true, true, 2, T, 4>, T >> 2);
+            pass(k_ntt<true, false, 2, T>, k_ntt<true, false, 2, T, 2>, k_ntt<true, false, 2, T, 4>, k_ntt<true, false, 2, T, 8>, T >> 2);
+            pass(k_ntt<true, true, 2, T>, k_ntt<true, true, 2, T, 2>, k_ntt<true, true, 2, T, 4>, k_ntt<true, true, 2, T, 8>, T >> 2);
         } else {
-            pass(k_ntt<true, false, 3, T>, NttKern2{}, NttKern4{}, T >> 3);
-            pass(k_ntt<true, true, 3, T>, NttKern2{}, NttKern4{}, T >> 3);
+            pass(k_ntt<true, false, 3, T>, NttKern2{}, NttKern4{}, NttKern8{}, T >> 3);
+            pass(k_ntt<true, true, 3, T>, NttKern2{}, NttKern4{}, NttKern8{}, T >> 3);
         }
     }
     checkLaunch(d, "ntt");
@@ -3813,30 +3896,55 @@ void sfp_graph_launch(sfp_dev* d, sfp_graph* g) {
 
 size_t sfp_graph_nodes(const sfp_graph* g) { return g ? g->nodes : 0; }
 
+// The family of a kernel (graph timing): every instantiation the launch
+// sites issue; anything else is SFP_FAM_COUNT ("other").
+template <bool I, bool C, int LE, int T>
+static void addNtt(std::unordered_map<const void*, uint32_t>& m, bool merged) {
+    m[(const void*)k_ntt<I, C, LE, T>] = SFP_FAM_NTT;
+    if (merged) {
+        m[(const void*)k_ntt<I, C, LE, T, 2>] = SFP_FAM_NTT;
+        m[(const void*)k_ntt<I, C, LE, T, 4>] = SFP_FAM_NTT;
+        m[(const void*)k_ntt<I, C, LE, T, 8>] = SFP_FAM_NTT;
+    }
+}
+template <int LE, int T>
+static void addNttAll(std::unordered_map<const void*, uint32_t>& m, bool merged) {
+    addNtt<false, true, LE, T>(m, merged);
+    addNtt<false, false, LE, T>(m, merged);
+    addNtt<true, true, LE, T>(m, merged);
+    addNtt<true, false, LE, T>(m, merged);
+}
+static uint32_t kernelFamily(const void* f) {
+    static const std::unordered_map<const void*, uint32_t> fam = [] {
+        std::unordered_map<const void*, uint32_t> m;
+        addNttAll<2, kNttTile>(m, true);
+        addNttAll<2, 1024>(m, true);
+        addNttAll<2, 512>(m, true);
+        addNttAll<3, kNttTile>(m, false);
+        addNttAll<4, kNttTile>(m, false);
+        addNttAll<3, 1024>(m, false);
+        addNttAll<3, 512>(m, false);
+        for (const void* k : {(const void*)k_convf<13>, (const void*)k_convf<16>, (const void*)k_convf<kMaxConvSrc>,
+                              (const void*)k_conv, (const void*)k_mdrsf<13, true>, (const void*)k_mdrsf<16, true>,
+                              (const void*)k_mdrsf<kMaxConvSrc, true>, (const void*)k_mdrsf<13>,
+                              (const void*)k_mdrsf<16>, (const void*)k_mdrsf<kMaxConvSrc>, (const void*)k_conv_mdrs})
+            m[k] = SFP_FAM_CONV;
+        for (const void* k : {(const void*)k_ks_inner<1>, (const void*)k_ks_inner<2>, (const void*)k_ks_inner<4>})
+            m[k] = SFP_FAM_KSINNER;
+        for (const void* k : {(const void*)k_ntt_ks<2, 1024>, (const void*)k_ntt_ks<2, 1024, 2>,
+                              (const void*)k_ntt_ks<2, 1024, 4>, (const void*)k_ntt_ks<2, 1024, 8>,
+                              (const void*)k_ntt_ks<2, kNttTile>, (const void*)k_ntt_ks<2, kNttTile, 2>,
+                              (const void*)k_ntt_ks<2, kNttTile, 4>, (const void*)k_ntt_ks<2, kNttTile, 8>})
+            m[k] = SFP_FAM_NTTKS;
+        return m;
+    }();
+    auto it = fam.find(f);
+    return it == fam.end() ? (uint32_t)SFP_FAM_COUNT : it->second;
+}
+
 int sfp_graph_family_time(sfp_dev* d, sfp_graph* g, uint32_t fam, int reps, double* ms, uint64_t* launches,
                           double* bytes) {
-    if (!g || !g->g || fam != SFP_FAM_NTT || reps < 1 || d->capture) return -1;
-    constexpr int T = kNttTile;
-    const void* fns[] = {(const void*)k_ntt<false, true, 2, T, 2>, (const void*)k_ntt<false, false, 2, T, 2>,
-                         (const void*)k_ntt<true, true, 2, T, 2>,  (const void*)k_ntt<true, false, 2, T, 2>,
-                         (const void*)k_ntt<false, true, 2, 1024, 2>, (const void*)k_ntt<false, false, 2, 1024, 2>,
-                         (const void*)k_ntt<true, true, 2, 1024, 2>,  (const void*)k_ntt<true, false, 2, 1024, 2>,
-                         (const void*)k_ntt<false, true, 2, 512, 2>, (const void*)k_ntt<false, false, 2, 512, 2>,
-                         (const void*)k_ntt<true, true, 2, 512, 2>,  (const void*)k_ntt<true, false, 2, 512, 2>,
-                         (const void*)k_ntt<false, true, 2, T>, (const void*)k_ntt<false, false, 2, T>,
-                         (const void*)k_ntt<true, true, 2, T>,  (const void*)k_ntt<true, false, 2, T>,
-                         (const void*)k_ntt<false, true, 3, T>, (const void*)k_ntt<false, false, 3, T>,
-                         (const void*)k_ntt<true, true, 3, T>,  (const void*)k_ntt<true, false, 3, T>,
-                         (const void*)k_ntt<false, true, 4, T>, (const void*)k_ntt<false, false, 4, T>,
-                         (const void*)k_ntt<true, true, 4, T>,  (const void*)k_ntt<true, false, 4, T>,
-                         (const void*)k_ntt<false, true, 2, 1024>, (const void*)k_ntt<false, false, 2, 1024>,
-                         (const void*)k_ntt<true, true, 2, 1024>,  (const void*)k_ntt<true, false, 2, 1024>,
-                         (const void*)k_ntt<false, true, 3, 1024>, (const void*)k_ntt<false, false, 3, 1024>,
-                         (const void*)k_ntt<true, true, 3, 1024>,  (const void*)k_ntt<true, false, 3, 1024>,
-                         (const void*)k_ntt<false, true, 2, 512>, (const void*)k_ntt<false, false, 2, 512>,
-                         (const void*)k_ntt<true, true, 2, 512>,  (const void*)k_ntt<true, false, 2, 512>,
-                         (const void*)k_ntt<false, true, 3, 512>, (const void*)k_ntt<false, false, 3, 512>,
-                         (const void*)k_ntt<true, true, 3, 512>,  (const void*)k_ntt<true, false, 3, 512>};
+    if (!g || !g->g || fam > SFP_FAM_ALL || reps < 1 || d->capture) return -1;
     size_t nn = 0;
     if (hipGraphGetNodes(g->g, nullptr, &nn) != hipSuccess) return -1;
     std::vector<hipGraphNode_t> nodes(nn);
@@ -3857,9 +3965,8 @@ int sfp_graph_family_time(sfp_dev* d, sfp_graph* g, uint32_t fam, int reps, doub
             hipGraphDestroy(sub);
             return -1;
         }
-        bool ntt = false;
-        for (const void* f : fns) ntt = ntt || kp.func == f;
-        if (!ntt) continue;
+        const uint32_t kf = kernelFamily(kp.func);
+        if (fam != SFP_FAM_ALL && kf != fam) continue;
         hipGraphNode_t nn2 = nullptr;
         if (hipGraphAddKernelNode(&nn2, sub, prev ? &prev : nullptr, prev ? 1 : 0, &kp) != hipSuccess) {
             hipGraphDestroy(sub);
@@ -3867,7 +3974,7 @@ int sfp_graph_family_time(sfp_dev* d, sfp_graph* g, uint32_t fam, int reps, doub
         }
         prev = nn2;
         ++cnt;
-        b += 16.0 * kp.gridDim.y * d->n;  // one pass reads and writes each row once
+        if (kf == SFP_FAM_NTT) b += 16.0 * kp.gridDim.y * d->n;  // one pass reads and writes each row once
     }
     hipGraphExec_t ex = nullptr;
     if (!cnt || hipGraphInstantiate(&ex, sub, nullptr, nullptr, 0) != hipSuccess) {
@@ -4489,6 +4596,7 @@ static void modupInnerCore(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uin
             P->useFp = fp;
             P->k2 = t1k ? k_ntt_ks<2, 1024, 2> : k_ntt_ks<2, kNttTile, 2>;
             P->k4 = t1k ? k_ntt_ks<2, 1024, 4> : k_ntt_ks<2, kNttTile, 4>;
+            P->k8 = t1k ? k_ntt_ks<2, 1024, 8> : k_ntt_ks<2, kNttTile, 8>;
             r.cls = STK_KS;
             r.key = stkKey((const void*)k1, g.x, (uint32_t)threads);
             r.pay = std::move(P);

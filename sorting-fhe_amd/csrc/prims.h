@@ -299,7 +299,7 @@ void sfp_ntt_batch(sfp_dev* d, uint64_t* p, size_t stride, uint32_t count, sfp_l
 // Every prim launches on the current lane.  Work on different lanes may run
 // concurrently; order it with events.  The oracle has one synchronous lane
 // and treats every call below as satisfied.
-#define SFP_MAX_LANES 8
+#define SFP_MAX_LANES 16  // (real lanes <= 8; the rest: a batched op's virtual lanes)
 typedef struct sfp_event sfp_event;
 int sfp_lanes(sfp_dev* d);
 void sfp_set_lane(sfp_dev* d, int lane);
@@ -331,12 +331,12 @@ void sfp_stack_stats(sfp_dev* d, uint64_t* merged, uint64_t* single);
 // Chebyshev PS's products of one tree level, a polynomial's powers of one
 // depth).  sfp_batch_begin(d, count) returns 1 if batching is on; the host
 // then issues op i after sfp_batch_lane(d, i) and calls sfp_batch_end, which
-// issues everything on the caller's lane, up to four identical launches of
-// different ops merged into one.  The ops' buffers must stay allocated until
+// issues everything on the caller's lane, identical launches of different ops
+// merged into one (up to eight; four for the element-wise kernels).  The ops' buffers must stay allocated until
 // sfp_batch_end (their launches are issued there).  Returns 0 (the ops run as
 // issued) for the oracle, with SFHE_BATCH=0, inside a stacked lane region or
 // with serialised lanes.
-#define SFP_BATCH_MAX 4
+#define SFP_BATCH_MAX 8
 int sfp_batch_begin(sfp_dev* d, uint32_t count);
 void sfp_batch_lane(sfp_dev* d, uint32_t i);
 void sfp_batch_end(sfp_dev* d);
@@ -430,12 +430,13 @@ int sfp_capturing(sfp_dev* d);
 // Enqueue the whole graph on the current lane (stream-ordered like a prim).
 void sfp_graph_launch(sfp_dev* d, sfp_graph* g);
 size_t sfp_graph_nodes(const sfp_graph* g);
-// The graph's kernel nodes of family `fam` (SFP_FAM_NTT only), re-instantiated
-// in their captured order as a graph of their own and replayed `reps` times,
+// The graph's kernel nodes of family `fam` (SFP_FAM_*; SFP_FAM_COUNT = every
+// kernel of no family, SFP_FAM_ALL = every kernel node), re-instantiated in
+// their captured order as a graph of their own and replayed `reps` times,
 // timed with HIP events on the current lane: the family's kernels alone,
 // back to back, with exactly the captured launch parameters.  Returns 0 and
-// the milliseconds per replay, the launches and their algorithmic bytes per
-// replay; -1 where the backend has no graphs.
+// the milliseconds per replay, the launches and the algorithmic bytes of
+// their NTT passes per replay; -1 where the backend has no graphs.
 int sfp_graph_family_time(sfp_dev* d, sfp_graph* g, uint32_t fam, int reps, double* ms, uint64_t* launches,
                           double* bytes);
 void sfp_graph_destroy(sfp_dev* d, sfp_graph* g);
@@ -449,7 +450,7 @@ void sfp_graph_destroy(sfp_dev* d, sfp_graph* g);
 //   NTTKS        the same for k_ntt_ks (ModUp's ROW pass fused with the inner product)
 // Inside a stacked region the launches are timed as issued (a merged pair is
 // one launch with the bytes of both).
-enum { SFP_FAM_NTT = 0, SFP_FAM_CONV = 1, SFP_FAM_KSINNER = 2, SFP_FAM_NTTKS = 3, SFP_FAM_COUNT = 4 };
+enum { SFP_FAM_NTT = 0, SFP_FAM_CONV = 1, SFP_FAM_KSINNER = 2, SFP_FAM_NTTKS = 3, SFP_FAM_COUNT = 4, SFP_FAM_ALL = 5 };
 // Time every `period`-th launch of `fam` (0 = off); resets its counters.
 void sfp_prof_set(sfp_dev* d, uint32_t fam, uint32_t period);
 // Since the last sfp_prof_set: launches seen, launches timed, their summed

@@ -37,6 +37,7 @@ ABI_SYMBOLS = [
     "sfhe_comm_uid", "sfhe_shard_rccl", "sfhe_shard_host", "sfhe_pool_bytes", "sfhe_live_contexts",
     "sfhe_serialize_lanes", "sfhe_stack_stats", "sfhe_sorter_graph_nodes", "sfhe_sorter_create_rot",
     "sfhe_sorter_sort_hybrid1", "sfhe_hybrid1_params", "sfhe_sorter_graph_ntt_time",
+    "sfhe_sorter_graph_family_time",
     "sfhe_sorter_sort_hybrid", "sfhe_hybrid_params", "sfhe_sorter_place_2n",
     "sfhe_bootstrap_setup", "sfhe_bootstrap_depth", "sfhe_bootstrap",
     "sfhe_sorter_sort_bitonic", "sfhe_kway_sort", "sfhe_kway_params",
@@ -143,6 +144,7 @@ _SIGS = {
     "sfhe_kway_sort": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _U32, _PVP]),
     "sfhe_kway_params": (C.c_int, [_U32, _PU32, _PU32, _PU32, _PU32, _PI32, _SZ, _PSZ]),
     "sfhe_sorter_graph_ntt_time": (C.c_int, [_VP, C.c_int, _PD, _PU64, _PD]),
+    "sfhe_sorter_graph_family_time": (C.c_int, [_VP, C.c_uint32, C.c_int, _PD, _PU64, _PD]),
     "sfhe_kernel_timing": (C.c_int, [_VP, _U32, _U32]),
     "sfhe_serialize_lanes": (C.c_int, [_VP, C.c_int]),
     "sfhe_stack_stats": (C.c_int, [_VP, _PU64, _PU64]),
@@ -579,6 +581,16 @@ class Sorter:
         NTT kernels replayed alone (sfhe_sorter_graph_ntt_time)."""
         ms, n, b = C.c_double(), C.c_uint64(), C.c_double()
         self.eng._chk(self.eng.lib.sfhe_sorter_graph_ntt_time(self.h, reps, C.byref(ms), C.byref(n), C.byref(b)))
+        return ms.value, n.value, b.value
+
+    def graph_family_time(self, family: str, reps: int = 3):
+        """(ms per sort, launches, NTT algorithmic bytes) of the captured
+        sort's kernels of one family (KFAM names, "other" or "all") replayed
+        alone (sfhe_sorter_graph_family_time)."""
+        f = {**self.eng.KFAM, "other": 4, "all": 5}[family]
+        ms, n, b = C.c_double(), C.c_uint64(), C.c_double()
+        self.eng._chk(self.eng.lib.sfhe_sorter_graph_family_time(self.h, f, reps, C.byref(ms), C.byref(n),
+                                                                 C.byref(b)))
         return ms.value, n.value, b.value
 
     def graph_nodes(self) -> int:

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Batched PS / power waves: bit-exactness tests, then the metric sort A/B
-# (waves on = default, SFHE_PS_WAVES=0), alternated twice on one box.
+# (A: the default; B: $BENV, default SFHE_PS_WAVES=0), alternated twice on one box.
 set -o pipefail
 cd "$(dirname "$0")/.."
 export PYTHONUNBUFFERED=1
@@ -15,6 +15,6 @@ fi
 B="--no-kway --no-hybrid1 --no-c5 --no-cpu-baseline --trials 3 --steps 20 --warmup 3"
 for k in 1 2; do
     timeout -k 10 300 python -u bench.py $B > gpurun_out/${T}_on_$k.json 2> gpurun_out/${T}_on_$k.err || exit $?
-    SFHE_PS_WAVES=0 timeout -k 10 300 python -u bench.py $B > gpurun_out/${T}_off_$k.json 2> gpurun_out/${T}_off_$k.err || exit $?
+    env ${BENV:-SFHE_PS_WAVES=0} timeout -k 10 300 python -u bench.py $B > gpurun_out/${T}_off_$k.json 2> gpurun_out/${T}_off_$k.err || exit $?
 done
 exit 0
