@@ -1227,9 +1227,14 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt_ks(const ArgSet<KsArgs, NG> 
     const u64* gx = twS + (size_t)prime * n;
     constexpr bool kPfBuild = LE == 2;
     constexpr int kPfRounds = 4;
-    double PW[kPfBuild ? kPfRounds * 3 : 1];
-    if constexpr (kPfBuild) {
-        if (fp) {
+#ifndef SFHE_KS_PW_LOOP
+#define SFHE_KS_PW_LOOP 1
+#endif
+    // the ROW rounds' FP64 twiddles, 12 per thread: loaded once per digit
+    // (SFHE_KS_PW_LOOP, keeping them live across the digits costs a wave per
+    // SIMD) or once per block
+    auto loadPW = [&](double* PW) {
+        if constexpr (kPfBuild) {
             const double* gd = reinterpret_cast<const double*>(gw);
 #pragma unroll
             for (int r = 0; r < kPfRounds; ++r) {
@@ -1247,7 +1252,9 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt_ks(const ArgSet<KsArgs, NG> 
                 }
             }
         }
-    }
+    };
+    double PW[kPfBuild ? kPfRounds * 3 : 1];
+    if (!SFHE_KS_PW_LOOP && fp) loadPW(PW);
     const double qd = (double)q, qi = qinvD[prime];
     const uint32_t kr = t < A.ell ? t : A.keyQ + (t - A.ell);
     const size_t rowOff = (size_t)T.r0 * 256;
@@ -1323,6 +1330,7 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt_ks(const ArgSet<KsArgs, NG> 
 #pragma unroll
                 for (int k = 0; k < NPAIR; ++k)
                     xs[k] = *reinterpret_cast<const ulonglong2*>(src + 2 * (threadIdx.x + k * NT));
+                if constexpr (FP && SFHE_KS_PW_LOOP) loadPW(PW);
 #pragma unroll
                 for (int k = 0; k < NPAIR; ++k) {  // in flight during the ROW rounds
                     const uint32_t e = 2 * (threadIdx.x + k * NT);
@@ -1809,47 +1817,65 @@ struct PtrList3 {
 };
 
 // out0 = sum_j a[j] * b[j], out1 = sum_j c[j] * b[j]: two coefficients per
-// thread, 16-byte loads, each plaintext row read once for both polynomials
+// thread, 16-byte loads, each plaintext row read once for both polynomials.
+// FP64 rows sum exact fpMulMod residues (|r| < 1.5 q < 2^43, so the up to
+// SFP_MAX_WSUM terms stay below 2^50) and reduce once; the integer row (q_0)
+// sums 128-bit products.  Same canonical outputs either way.
 __global__ __launch_bounds__(kThreads) void k_mac_plain2(u64* __restrict__ out0, u64* __restrict__ out1,
                                                          const PtrList3 L, uint32_t nin, sfp_limbs m,
-                                                         const sf_barrett* __restrict__ bar, uint32_t logn) {
+                                                         const sf_barrett* __restrict__ bar, uint32_t logn,
+                                                         const double* __restrict__ qinvD) {
     const size_t pairs = ((size_t)m.count << logn) >> 1;
     for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < pairs;
          i += (size_t)gridDim.x * kThreads) {
         const size_t e = 2 * i;
-        const sf_barrett B = loadBar(bar, primeOf(m, (uint32_t)(e >> logn)));
-        Acc x0{0, 0}, y0{0, 0}, x1{0, 0}, y1{0, 0};
-        uint32_t j = 0;
-        for (; j + 2 <= nin; j += 2) {  // two terms' six loads in flight together
-            const ulonglong2 p = *reinterpret_cast<const ulonglong2*>(L.b[j] + e);
-            const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(L.a[j] + e);
-            const ulonglong2 c = *reinterpret_cast<const ulonglong2*>(L.c[j] + e);
-            const ulonglong2 p2 = *reinterpret_cast<const ulonglong2*>(L.b[j + 1] + e);
-            const ulonglong2 a2 = *reinterpret_cast<const ulonglong2*>(L.a[j + 1] + e);
-            const ulonglong2 c2 = *reinterpret_cast<const ulonglong2*>(L.c[j + 1] + e);
-            macc(x0, a.x, p.x);
-            macc(y0, a.y, p.y);
-            macc(x1, c.x, p.x);
-            macc(y1, c.y, p.y);
-            macc(x0, a2.x, p2.x);
-            macc(y0, a2.y, p2.y);
-            macc(x1, c2.x, p2.x);
-            macc(y1, c2.y, p2.y);
-        }
-        if (j < nin) {
-            const ulonglong2 p = *reinterpret_cast<const ulonglong2*>(L.b[j] + e);
-            const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(L.a[j] + e);
-            const ulonglong2 c = *reinterpret_cast<const ulonglong2*>(L.c[j] + e);
-            macc(x0, a.x, p.x);
-            macc(y0, a.y, p.y);
-            macc(x1, c.x, p.x);
-            macc(y1, c.y, p.y);
-        }
+        const uint32_t prime = primeOf(m, (uint32_t)(e >> logn));
+        const sf_barrett B = loadBar(bar, prime);
         ulonglong2 o0, o1;
-        o0.x = sf_reduce128_acc(x0.lo, x0.hi, &B);
-        o0.y = sf_reduce128_acc(y0.lo, y0.hi, &B);
-        o1.x = sf_reduce128_acc(x1.lo, x1.hi, &B);
-        o1.y = sf_reduce128_acc(y1.lo, y1.hi, &B);
+        if (B.q < kFpPrimeBound) {  // (uniform per wave: a wave's 128 words lie in one row)
+            const double qd = (double)B.q, qi = qinvD[prime];
+            double x0 = 0.0, y0 = 0.0, x1 = 0.0, y1 = 0.0;
+            uint32_t j = 0;
+            auto term = [&](const ulonglong2& p, const ulonglong2& a, const ulonglong2& c) {
+                const double px = u2d(p.x), py = u2d(p.y), pxq = px * qi, pyq = py * qi;
+                x0 += fpMulMod(u2d(a.x), px, pxq, qd);
+                y0 += fpMulMod(u2d(a.y), py, pyq, qd);
+                x1 += fpMulMod(u2d(c.x), px, pxq, qd);
+                y1 += fpMulMod(u2d(c.y), py, pyq, qd);
+            };
+            for (; j + 2 <= nin; j += 2) {  // two terms' six loads in flight together
+                const ulonglong2 p = *reinterpret_cast<const ulonglong2*>(L.b[j] + e);
+                const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(L.a[j] + e);
+                const ulonglong2 c = *reinterpret_cast<const ulonglong2*>(L.c[j] + e);
+                const ulonglong2 p2 = *reinterpret_cast<const ulonglong2*>(L.b[j + 1] + e);
+                const ulonglong2 a2 = *reinterpret_cast<const ulonglong2*>(L.a[j + 1] + e);
+                const ulonglong2 c2 = *reinterpret_cast<const ulonglong2*>(L.c[j + 1] + e);
+                term(p, a, c);
+                term(p2, a2, c2);
+            }
+            if (j < nin)
+                term(*reinterpret_cast<const ulonglong2*>(L.b[j] + e), *reinterpret_cast<const ulonglong2*>(L.a[j] + e),
+                     *reinterpret_cast<const ulonglong2*>(L.c[j] + e));
+            o0.x = d2u(fpReduce(x0, qd, qi));
+            o0.y = d2u(fpReduce(y0, qd, qi));
+            o1.x = d2u(fpReduce(x1, qd, qi));
+            o1.y = d2u(fpReduce(y1, qd, qi));
+        } else {
+            Acc x0{0, 0}, y0{0, 0}, x1{0, 0}, y1{0, 0};
+            for (uint32_t j = 0; j < nin; ++j) {
+                const ulonglong2 p = *reinterpret_cast<const ulonglong2*>(L.b[j] + e);
+                const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(L.a[j] + e);
+                const ulonglong2 c = *reinterpret_cast<const ulonglong2*>(L.c[j] + e);
+                macc(x0, a.x, p.x);
+                macc(y0, a.y, p.y);
+                macc(x1, c.x, p.x);
+                macc(y1, c.y, p.y);
+            }
+            o0.x = sf_reduce128_acc(x0.lo, x0.hi, &B);
+            o0.y = sf_reduce128_acc(y0.lo, y0.hi, &B);
+            o1.x = sf_reduce128_acc(x1.lo, x1.hi, &B);
+            o1.y = sf_reduce128_acc(y1.lo, y1.hi, &B);
+        }
         *reinterpret_cast<ulonglong2*>(out0 + e) = o0;
         *reinterpret_cast<ulonglong2*>(out1 + e) = o1;
     }
@@ -4115,7 +4141,7 @@ void sfp_mac_plain2(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint64_t* 
     }
     const size_t total = (size_t)m.count * d->n;
     SFP_GO(k_mac_plain2, dim3(ewGrid(total / 2)), dim3(kThreads), out0, out1, L, nin, m,
-                       d->bar, d->logn);
+                       d->bar, d->logn, d->qinvD);
     checkLaunch(d, "mac_plain2");
 }
 
