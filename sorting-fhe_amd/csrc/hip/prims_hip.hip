@@ -23,6 +23,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <unordered_set>
@@ -154,8 +155,12 @@ struct sfp_dev {
     // FP64 twiddles for primes < 2^42 (exact doubles w and rounded w/q), and
     // per-prime 1/q and n^-1 as doubles
     double *psiD = nullptr, *ipsiD = nullptr;
+    // ROW-pass row factors (rowTwLoad): [prime][k < 8][row < n/256] = psi_rev[row << k] (ipsi for irowD)
+    double *rowD = nullptr, *irowD = nullptr;
     double *qinvD = nullptr, *ninvD = nullptr, *ninvQ = nullptr;
     std::vector<sf_barrett> hbar;
+    std::vector<u64> hninv;  // n^-1 mod q per prime (ModUpPlan)
+    std::map<const sfp_conv*, struct ModUpPlan*> plans;  // keyed by the level's digit-0 table
     // pinned argument ring (host) mirrored on the device
     char* hring = nullptr;
     char* dring = nullptr;
@@ -234,7 +239,25 @@ struct sfp_conv {
     double *vD = nullptr, *vQ = nullptr;      // [ns][hFpT.size()]
     double *hD = nullptr, *hQ = nullptr;      // [kMaxConvBig][hFpT.size()]
     std::vector<uint32_t> hsrc, hdst;
+    std::vector<uint32_t> hrow;  // dst_row
+    std::vector<u64> hinv, hmod; // host copies (ModUpPlan)
 };
+
+struct ModUpPlan {
+    uint32_t ell = 0, rows = 0;
+    std::vector<const sfp_conv*> convs;
+    u64 *postK = nullptr, *postKS = nullptr;
+    double *postD = nullptr, *postQ = nullptr;
+    double *mD = nullptr, *mQ = nullptr, *hD = nullptr, *hQ = nullptr;
+    u64* mI = nullptr;
+    bool big = false;
+};
+static void freePlan(ModUpPlan* P) {
+    for (void* x : {(void*)P->postK, (void*)P->postKS, (void*)P->postD, (void*)P->postQ, (void*)P->mD, (void*)P->mQ,
+                    (void*)P->hD, (void*)P->hQ, (void*)P->mI})
+        hipFree(x);
+    delete P;
+}
 
 static void record(sfp_dev* d, const char* what, hipError_t e) {
     std::lock_guard<std::mutex> g(d->mu);
@@ -686,6 +709,59 @@ __device__ __forceinline__ void nttRoundDynFP(int b, double* s, const NttTile& T
 }
 
 
+// ROW-pass FP64 twiddles of one thread (LE = 2: four rounds x three).  Stage
+// k of the pass at row `row` and in-row offset v uses psi_rev[2^S + row 2^k + v]
+// (S = S0 + k, v < 2^k): across the pass, all n entries of the table, 8 B per
+// coefficient on top of the tile's 16.  The bit-reversed exponent of that
+// index is the sum of those of its disjoint bit fields, so the twiddle is also
+//   psi_rev[2^S + v] * psi_rev[row 2^k]  (mod q):
+// a local factor (2^k entries per stage, shared by every row of the prime:
+// cache-resident) times the row factor rowD[k][row] (wave-uniform: scalar
+// loads).  The last round (stages 6 and 7, three quarters of the table) takes
+// its three twiddles that way, as exact products (fpMulMod, |W| < 1.5 q: W
+// only multiplies, outputs stay canonical and bit-identical); rounds 0-2 read
+// the table (factoring them too cost more VALU time than their bytes).
+struct RowTw {
+    double L[12];
+    double R[2];
+};
+__device__ __forceinline__ void rowTwIssue(RowTw& W, const double* __restrict__ gd, const double* __restrict__ rd,
+                                           const NttTile& T, uint32_t S0) {
+    const uint32_t gid = threadIdx.x;
+    const uint32_t row = __builtin_amdgcn_readfirstlane(T.r0 + (gid >> 6));  // (st = gid >> 6 every round)
+    const uint32_t rowsLog = __builtin_amdgcn_readfirstlane(T.logn - 8);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) W.R[t] = rd[((uint32_t)(6 + t) << rowsLog) + row];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t k0 = 2 * r, logh = 8 - k0 - 2;
+        const uint32_t lo = gid & ((1u << logh) - 1);
+        const uint32_t hi = (gid >> logh) & ((1u << k0) - 1);
+        const uint32_t u = hi * (256u >> k0) + lo;
+        const uint32_t x0 = (T.r0 + (gid >> 6)) * 256u + u;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const uint32_t k = k0 + t;
+            const uint32_t b = r == 3 ? (1u << (S0 + k)) + (u >> (8 - k)) : (1u << (S0 + k)) + (x0 >> (8 - k));
+#pragma unroll
+            for (int qd = 0; qd < (1 << t); ++qd) W.L[3 * r + (1 << t) - 1 + qd] = gd[b + qd];
+        }
+    }
+}
+__device__ __forceinline__ void rowTwFinish(double* PW, const RowTw& W, double q, double qi) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) PW[i] = W.L[i];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const double rf = W.R[t], rfq = rf * qi;
+#pragma unroll
+        for (int qd = 0; qd < (1 << t); ++qd) {
+            const int i = 9 + (1 << t) - 1 + qd;
+            PW[i] = fpMulMod(W.L[i], rf, rfq, q);
+        }
+    }
+}
+
 // A 2-D set of rows for one NTT launch, passed by value: row (p, i) for
 // p < P, i < R lives at base + p*ps + i*is (word offsets).  Prime of row i:
 // primeOf(pm, i).  The first pass reads `src` (optionally the centred lift of
@@ -718,6 +794,20 @@ struct RowGroup {
     // device arrays (constant cache): epilogue constants per i (value, Shoup)
     // and q_liftPrime mod q_i -- pointers keep the kernel arguments small
     const u64 *k, *kS, *k2, *k2S, *liftSub, *preK, *preKS, *emK, *emKS;
+    // ModUp's conversion fused into the forward COL pass (k_ntt<..., CONV>,
+    // ModUpPlan): row (p, i) is Conv_p(y)_i = sum_s y_{p,s} m_p[s][i] mod q_i,
+    // read from the digit's source rows y (cy + (p alpha + s) n: FP64 rows as
+    // doubles, the 60-bit q_0 as u64) instead of its own row.  Multipliers
+    // [p][s][i] (stride cRows): cmD / cmQ (as double, / q_i) for FP64 rows,
+    // cmI for integer rows; chD / chQ [i]: q_0's high-part multiplier (cBig)
+    const u64* cy;
+    const double *cmD, *cmQ, *chD, *chQ;
+    const u64* cmI;
+    uint32_t cRows, cBig;
+    // inverse COL pass: scale row i by post_i (n^-1 times the conversion's
+    // source factor) instead of n^-1; FP64 rows are stored as doubles
+    const u64 *postK, *postKS;
+    const double *postD, *postQ;
 };
 
 // Merged launches (stacked regions, batched ops; sfp_stack_begin /
@@ -774,7 +864,7 @@ __device__ unsigned long long g_nttTrace[kTraceSlots][4][8];
 #define NTT_MARK(i)
 #endif
 
-template <bool INV, bool COL, int LE, int TILE, int NG = 1>
+template <bool INV, bool COL, int LE, int TILE, int NG = 1, bool CONV = false>
 __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroupSet<NG> GS, const sf_barrett* __restrict__ bar,
                                                   const u64* __restrict__ tw, const u64* __restrict__ twS,
                                                   const u64* __restrict__ ninv,
@@ -782,7 +872,8 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroupSet<NG> GS, co
                                                   const double* __restrict__ twD,
                                                   const double* __restrict__ qinvD,
                                                   const double* __restrict__ ninvD,
-                                                  const double* __restrict__ ninvQ, int useFp) {
+                                                  const double* __restrict__ ninvQ, int useFp,
+                                                  const double* __restrict__ rowD) {
     __shared__ u64 s[TILE];
     __shared__ u64 tW[COL ? kNttColTw : 1], tX[COL ? kNttColTw : 1];  // COL twiddles (value; Shoup for integer rows)
 #ifdef SFHE_NTT_TRACE
@@ -824,8 +915,84 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroupSet<NG> GS, co
         return COL ? (size_t)(e >> T.logC) * 256 + T.c0 + (e & (T.C - 1)) : (size_t)T.r0 * 256 + e;
     };
     ulonglong2 xr[NPAIR], mr[NPAIR];
+    if constexpr (CONV) {
+        static_assert(!INV && COL, "the conversion feeds the forward COL pass");
+        // this tile of Conv_pp(y) for target row ii (ModUp): the digit's
+        // source tiles come in groups of four (loads in flight together; the
+        // sources were read by the other target rows' blocks too: L2 hits)
+        const uint32_t ns = min(G.alpha, G.skipEll - pp * G.alpha);
+        const u64* yb = G.cy + (size_t)pp * G.alpha * n;
+        const size_t tb = (size_t)pp * G.alpha * G.cRows + ii;
+        const u64 qc = bar[prime].q;
+        const bool big0 = G.cBig && pp == 0;
+        constexpr int GRP = 4;
+        if (useFp && qc < kFpPrimeBound) {
+            const double qd = (double)qc, qi = qinvD[prime];
+            double acc[2 * NPAIR];
 #pragma unroll
-    for (int k = 0; k < NPAIR; ++k) xr[k] = *reinterpret_cast<const ulonglong2*>(in + tileOff(k));
+            for (int w = 0; w < 2 * NPAIR; ++w) acc[w] = 0.0;
+            for (uint32_t s0 = 0; s0 < ns; s0 += GRP) {
+                ulonglong2 v[GRP][NPAIR];
+#pragma unroll
+                for (int g = 0; g < GRP; ++g)
+                    if (s0 + g < ns)
+#pragma unroll
+                        for (int k = 0; k < NPAIR; ++k)
+                            v[g][k] = *reinterpret_cast<const ulonglong2*>(yb + (size_t)(s0 + g) * n + tileOff(k));
+#pragma unroll
+                for (int g = 0; g < GRP; ++g) {
+                    const uint32_t sI = s0 + g;
+                    if (sI >= ns) break;
+                    const double md = G.cmD[tb + (size_t)sI * G.cRows], mq = G.cmQ[tb + (size_t)sI * G.cRows];
+                    if (big0 && sI == 0) {  // y < 2^60: y_lo + 2^30 y_hi, the second with mod 2^30 mod q
+                        const double hd = G.chD[ii], hq = G.chQ[ii];
+#pragma unroll
+                        for (int k = 0; k < NPAIR; ++k) {
+                            const u64 ya = v[g][k].x, yc = v[g][k].y;
+                            acc[2 * k] += fpMulMod(u2d(ya & 0x3fffffffull), md, mq, qd) +
+                                          fpMulMod(u2d(ya >> 30), hd, hq, qd);
+                            acc[2 * k + 1] += fpMulMod(u2d(yc & 0x3fffffffull), md, mq, qd) +
+                                              fpMulMod(u2d(yc >> 30), hd, hq, qd);
+                        }
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < NPAIR; ++k) {
+                            acc[2 * k] += fpMulMod(__longlong_as_double(v[g][k].x), md, mq, qd);
+                            acc[2 * k + 1] += fpMulMod(__longlong_as_double(v[g][k].y), md, mq, qd);
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < NPAIR; ++k) {  // |acc| < 14 * 1.5 q < 2^46: exact
+                xr[k].x = d2u(fpReduce(acc[2 * k], qd, qi));
+                xr[k].y = d2u(fpReduce(acc[2 * k + 1], qd, qi));
+            }
+        } else {  // an integer target row (q_0 for digits > 0): 128-bit sums of canonical residues
+            const sf_barrett CB = loadBar(bar, prime);
+            Acc acc[2 * NPAIR];
+#pragma unroll
+            for (int w = 0; w < 2 * NPAIR; ++w) acc[w] = Acc{0, 0};
+            for (uint32_t sI = 0; sI < ns; ++sI) {
+                const u64 m = G.cmI[tb + (size_t)sI * G.cRows];
+                const bool raw = big0 && sI == 0;
+#pragma unroll
+                for (int k = 0; k < NPAIR; ++k) {
+                    const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(yb + (size_t)sI * n + tileOff(k));
+                    macc(acc[2 * k], raw ? v.x : d2u(__longlong_as_double(v.x)), m);
+                    macc(acc[2 * k + 1], raw ? v.y : d2u(__longlong_as_double(v.y)), m);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < NPAIR; ++k) {
+                xr[k].x = sf_reduce128_acc(acc[2 * k].lo, acc[2 * k].hi, &CB);
+                xr[k].y = sf_reduce128_acc(acc[2 * k + 1].lo, acc[2 * k + 1].hi, &CB);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < NPAIR; ++k) xr[k] = *reinterpret_cast<const ulonglong2*>(in + tileOff(k));
+    }
     if (pre) {
 #pragma unroll
         for (int k = 0; k < NPAIR; ++k) mr[k] = *reinterpret_cast<const ulonglong2*>(pre + tileOff(k));
@@ -847,31 +1014,15 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroupSet<NG> GS, co
         }
     }
     // ROW pass, FP64 rows, one group per thread per round (LE = 2): every
-    // round's twiddles are data-independent, so all 4 x 3 of them are loaded
-    // here, in flight together with the tile, instead of one HBM latency per
-    // register round (loaded for every row; integer rows ignore them)
+    // round's twiddles are data-independent, so all 4 x 3 of them (as local
+    // and row factors, rowTwIssue) are loaded here, in flight together with
+    // the tile, instead of one latency per register round
     constexpr bool kPfBuild = !COL && LE == 2;
     constexpr int kPfRounds = 8 / 2;
     double PW[kPfBuild ? kPfRounds * 3 : 1];
-    if constexpr (kPfBuild) {
-        const double* gd = reinterpret_cast<const double*>(gwD);
-        const uint32_t gid = threadIdx.x;
-#pragma unroll
-        for (int r = 0; r < kPfRounds; ++r) {
-            const uint32_t k0 = 2 * r, logh = 8 - k0 - 2;
-            const uint32_t lo = gid & ((1u << logh) - 1);
-            const uint32_t rest = gid >> logh;
-            const uint32_t hi = rest & ((1u << k0) - 1);
-            const uint32_t st = rest >> k0;
-            const uint32_t x0 = nttGlobal<false>(T, st, hi * (256u >> k0) + lo);
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                const uint32_t tb = twIndex<false>(T, S0, k0 + t, x0);
-#pragma unroll
-                for (int qd = 0; qd < (1 << t); ++qd) PW[3 * r + (1 << t) - 1 + qd] = gd[tb + qd];
-            }
-        }
-    }
+    RowTw RT;
+    if constexpr (kPfBuild)
+        rowTwIssue(RT, reinterpret_cast<const double*>(gwD), rowD + (size_t)prime * 8 * (n >> 8), T, S0);
     sf_barrett LB{};
     u64 lsub = 0;
     const bool preK = FIRST && G.preK;
@@ -882,6 +1033,8 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroupSet<NG> GS, co
     const u64 q = bar[prime].q;
     const bool fp = useFp && q < kFpPrimeBound;  // uniform per block
     const bool rowPf = kPfBuild && fp;
+    if constexpr (kPfBuild)
+        if (rowPf) rowTwFinish(PW, RT, (double)q, qinvD[prime]);
 
     // the pass's twiddle table for this prime: FP64 values (W/q is formed in
     // registers) or integer values with their Shoup companions
@@ -980,7 +1133,8 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroupSet<NG> GS, co
         NTT_MARK(1 + ri);
     }
     const bool scale = INV && COL;
-    const u64 ni = scale ? ninv[prime] : 0, niS = scale ? ninvS[prime] : 0;
+    const bool post = scale && G.postK;  // (ModUpPlan: n^-1 times the conversion's source factor)
+    const u64 ni = post ? G.postK[ii] : scale ? ninv[prime] : 0, niS = post ? G.postKS[ii] : scale ? ninvS[prime] : 0;
     u64* out = epi ? rowAt(G.eout, pp, ii) : rowAt(G.dst, pp, ii);
     const u64 ek = epi ? G.k[ii] : 0, ekS = epi ? G.kS[ii] : 0;
     const u64* ead = epi && G.eadd.base ? rowAt(G.eadd, pp, ii) : nullptr;
@@ -1001,12 +1155,18 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroupSet<NG> GS, co
         if (fp) {  // every FP pass ends canonical: [0, q) as u64
             const double qd = (double)q, qi = qinvD[prime];
             double a0 = __longlong_as_double(x.x), a1 = __longlong_as_double(x.y);
-            if (scale) {
-                a0 = fpMulMod(a0, ninvD[prime], ninvQ[prime], qd);
-                a1 = fpMulMod(a1, ninvD[prime], ninvQ[prime], qd);
+            if (post) {  // stored as doubles: the fused conversion multiplies them as they are
+                const double pd = G.postD[ii], pq = G.postQ[ii];
+                x.x = __double_as_longlong(fpReduce(fpMulMod(a0, pd, pq, qd), qd, qi));
+                x.y = __double_as_longlong(fpReduce(fpMulMod(a1, pd, pq, qd), qd, qi));
+            } else {
+                if (scale) {
+                    a0 = fpMulMod(a0, ninvD[prime], ninvQ[prime], qd);
+                    a1 = fpMulMod(a1, ninvD[prime], ninvQ[prime], qd);
+                }
+                x.x = d2u(fpReduce(a0, qd, qi));
+                x.y = d2u(fpReduce(a1, qd, qi));
             }
-            x.x = d2u(fpReduce(a0, qd, qi));
-            x.y = d2u(fpReduce(a1, qd, qi));
         } else if (!FIRST) {  // finish the lazy ranges: forward [0,4q), inverse [0,2q) -> [0,q)
             if (scale) {
                 x.x = sf_mul_shoup_lazy(x.x, ni, niS, q);
@@ -1202,7 +1362,8 @@ template <int LE, int TILE, int NG = 1>
 __global__ __launch_bounds__(TILE >> LE) void k_ntt_ks(const ArgSet<KsArgs, NG> AS, const sf_barrett* __restrict__ bar,
                                                      const u64* __restrict__ tw, const u64* __restrict__ twS,
                                                      uint32_t logn, const double* __restrict__ twD,
-                                                     const double* __restrict__ qinvD, int useFp) {
+                                                     const double* __restrict__ qinvD, int useFp,
+                                                     const double* __restrict__ rowD) {
     __shared__ u64 s[2 * TILE];  // the second tile: acc1's inverse ROW pass (same rounds as acc0's)
     constexpr int NT = TILE >> LE;       // threads
     constexpr int NPAIR = (1 << LE) / 2;  // 16-byte pairs per thread
@@ -1233,6 +1394,9 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt_ks(const ArgSet<KsArgs, NG> 
     // the ROW rounds' FP64 twiddles, 12 per thread: loaded once per digit
     // (SFHE_KS_PW_LOOP, keeping them live across the digits costs a wave per
     // SIMD) or once per block
+    // (the full table, not rowTwIssue's factors: the products' registers cost
+    // this kernel a wave per SIMD, and its twiddle bytes are < 10 % of its
+    // key and digit traffic)
     auto loadPW = [&](double* PW) {
         if constexpr (kPfBuild) {
             const double* gd = reinterpret_cast<const double*>(gw);
@@ -2756,7 +2920,7 @@ static uint64_t stkKey(const void* kern, uint32_t a, uint32_t b) {
 
 template <int NG>
 using NttKernN = void (*)(RowGroupSet<NG>, const sf_barrett*, const u64*, const u64*, const u64*, const u64*,
-                          uint32_t, const double*, const double*, const double*, const double*, int);
+                          uint32_t, const double*, const double*, const double*, const double*, int, const double*);
 using NttKern2 = NttKernN<2>;
 using NttKern4 = NttKernN<4>;
 using NttKern8 = NttKernN<8>;
@@ -2769,11 +2933,11 @@ struct NttPay {
     NttKern4 k4;
     NttKern8 k8;
     const u64 *tw, *twS;
-    const double* twD;
+    const double *twD, *rowD;
 };
 template <int NG>
 using KsKernN = void (*)(ArgSet<KsArgs, NG>, const sf_barrett*, const u64*, const u64*, uint32_t, const double*,
-                         const double*, int);
+                         const double*, int, const double*);
 struct KsPay {
     KsArgs a;
     uint32_t rows;
@@ -2908,7 +3072,7 @@ static bool stackMerge(sfp_dev* d, const StackRec* const* h, int cnt, hipStream_
                 else
                     k = A.k8;
                 hipLaunchKernelGGL(k, dim3(A.g.x, tot), dim3(A.threads), 0, s, S, d->bar, A.tw, A.twS, d->ninv,
-                                   d->ninvS, d->logn, A.twD, d->qinvD, d->ninvD, d->ninvQ, A.useFp);
+                                   d->ninvS, d->logn, A.twD, d->qinvD, d->ninvD, d->ninvQ, A.useFp, A.rowD);
             };
             if (cnt == 2)
                 launchSets<RowGroup, 2>(G, rows, cnt, launch);
@@ -2944,7 +3108,7 @@ static bool stackMerge(sfp_dev* d, const StackRec* const* h, int cnt, hipStream_
                 else
                     k = B.k8;
                 hipLaunchKernelGGL(k, dim3(B.g.x, tot), dim3(B.threads), 0, s, S, d->bar, d->psi, d->psiS, d->logn,
-                                   d->psiD, d->qinvD, B.useFp);
+                                   d->psiD, d->qinvD, B.useFp, d->rowD);
             };
             if (cnt == 2)
                 launchSets<KsArgs, 2>(A, rows, cnt, launch);
@@ -3359,7 +3523,9 @@ sfp_dev* sfp_create(int device, const sfp_tables* t) {
               hipMalloc(&d->ipsi, tn) == hipSuccess && hipMalloc(&d->ipsiS, tn) == hipSuccess &&
               hipMalloc(&d->ninv, d->np * 8) == hipSuccess &&
               hipMalloc(&d->ninvS, d->np * 8) == hipSuccess && hipMalloc(&d->psiD, tn) == hipSuccess &&
-              hipMalloc(&d->ipsiD, tn) == hipSuccess && hipMalloc(&d->qinvD, d->np * 8) == hipSuccess &&
+              hipMalloc(&d->ipsiD, tn) == hipSuccess && hipMalloc(&d->rowD, (size_t)d->np * 8 * (d->n >> 8) * 8) == hipSuccess &&
+              hipMalloc(&d->irowD, (size_t)d->np * 8 * (d->n >> 8) * 8) == hipSuccess &&
+              hipMalloc(&d->qinvD, d->np * 8) == hipSuccess &&
               hipMalloc(&d->ninvD, d->np * 8) == hipSuccess && hipMalloc(&d->ninvQ, d->np * 8) == hipSuccess;
     d->ringCap = (size_t)16 << 20;
     if (const char* v = std::getenv("SFHE_ARG_RING_MB"))  // (tests: force chunked uploads)
@@ -3381,6 +3547,7 @@ sfp_dev* sfp_create(int device, const sfp_tables* t) {
     hostToDev(d, d->ipsi, t->ipsi_rev, tn);
     hostToDev(d, d->ipsiS, t->ipsi_rev_shoup, tn);
     hostToDev(d, d->ninv, t->n_inv, d->np * 8);
+    d->hninv.assign(t->n_inv, t->n_inv + d->np);
     hostToDev(d, d->ninvS, t->n_inv_shoup, d->np * 8);
     {
         // FP64 twiddle values (the kernels form W/q in registers)
@@ -3392,6 +3559,18 @@ sfp_dev* sfp_create(int device, const sfp_tables* t) {
         hostToDev(d, d->psiD, a.data(), tn);
         fill(t->ipsi_rev, a.data());
         hostToDev(d, d->ipsiD, a.data(), tn);
+        // ROW-pass row factors (rowTwIssue): psi_rev[row << k] per prime, k < 8, row < n / 256
+        const uint32_t R = d->n >> 8;
+        std::vector<double> rf((size_t)d->np * 8 * R), irf((size_t)d->np * 8 * R);
+        for (uint32_t p = 0; p < d->np; ++p)
+            for (uint32_t k = 0; k < 8; ++k)
+                for (uint32_t row = 0; row < R; ++row) {
+                    const size_t o = ((size_t)p * 8 + k) * R + row, src = (size_t)p * d->n + ((size_t)row << k);
+                    rf[o] = (double)t->psi_rev[src];
+                    irf[o] = (double)t->ipsi_rev[src];
+                }
+        hostToDev(d, d->rowD, rf.data(), rf.size() * 8);
+        hostToDev(d, d->irowD, irf.data(), irf.size() * 8);
         for (uint32_t p = 0; p < d->np; ++p) {
             const double q = (double)d->hbar[p].q;
             qi[p] = 1.0 / q;
@@ -3444,6 +3623,9 @@ static RcclApi& rcclApi() {
 void sfp_destroy(sfp_dev* d) {
     if (!d) return;
     syncAll(d);
+    for (auto& kv : d->plans)
+        if (kv.second) freePlan(kv.second);
+    d->plans.clear();
     if (d->nccl) rcclApi().commDestroy(d->nccl);
     if (d->gnccl) rcclApi().commDestroy(d->gnccl);
     for (sfp_event* e : d->evFree) {
@@ -3460,7 +3642,7 @@ void sfp_destroy(sfp_dev* d) {
     hipFree(d->ipsiS);
     hipFree(d->ninv);
     hipFree(d->ninvS);
-    for (double* x : {d->psiD, d->ipsiD, d->qinvD, d->ninvD, d->ninvQ}) hipFree(x);
+    for (double* x : {d->psiD, d->ipsiD, d->rowD, d->irowD, d->qinvD, d->ninvD, d->ninvQ}) hipFree(x);
     hipFree(d->dring);
     hipHostFree(d->hring);
     hipHostFree(d->bounce);
@@ -3646,6 +3828,31 @@ static int nttFp() {
     return on;
 }
 
+// SFHE_NTT_SMALL_TILE (512 / 1024) and SFHE_NTT_SMALL_LE (2 / 3): the
+// small-launch tile and register-round width (A/B knobs; defaults measured);
+// SFHE_NTT_LE: register-round width experiments for big launches (2, 3, 4)
+static uint32_t nttSmallTile() {
+    static const uint32_t v = [] {
+        const char* e = std::getenv("SFHE_NTT_SMALL_TILE");
+        return e ? (uint32_t)std::atoi(e) : 1024u;
+    }();
+    return v;
+}
+static int nttSmallLe() {
+    static const int v = [] {
+        const char* e = std::getenv("SFHE_NTT_SMALL_LE");
+        return e ? std::atoi(e) : 2;
+    }();
+    return v;
+}
+static int nttLe() {
+    static const int v = [] {
+        const char* e = std::getenv("SFHE_NTT_LE");
+        return e ? std::atoi(e) : 0;
+    }();
+    return v;
+}
+
 static RowGroup rowsOf(uint32_t P, uint32_t R, sfp_limbs pm) {
     RowGroup G;
     std::memset(&G, 0, sizeof G);
@@ -3684,6 +3891,7 @@ static void nttRows(sfp_dev* d, const RowGroup& G0, int inverse, int passes = 3)
     const u64* tw = inverse ? d->ipsi : d->psi;
     const u64* twS = inverse ? d->ipsiS : d->psiS;
     const double* twD = inverse ? d->ipsiD : d->psiD;
+    const double* rowD = inverse ? d->irowD : d->rowD;
     // Launches over few rows are latency-bound (a one-limb pass is one tile
     // round trip per block: ~1.5 us load, ~1 us per register round, tools/
     // microbench with SFHE_NTT_TRACE): up to SFHE_NTT_T1K_ROWS rows (default
@@ -3694,16 +3902,8 @@ static void nttRows(sfp_dev* d, const RowGroup& G0, int inverse, int passes = 3)
         const char* v = std::getenv("SFHE_NTT_T1K_ROWS");
         return v ? (uint32_t)std::atoi(v) : 64u;
     }();
-    // SFHE_NTT_SMALL_TILE (512 / 1024) and SFHE_NTT_SMALL_LE (2 / 3): the
-    // small-launch tile and register-round width (A/B knobs; defaults measured)
-    static const uint32_t smallTile = [] {
-        const char* v = std::getenv("SFHE_NTT_SMALL_TILE");
-        return v ? (uint32_t)std::atoi(v) : 1024u;
-    }();
-    static const int smallLe = [] {
-        const char* v = std::getenv("SFHE_NTT_SMALL_LE");
-        return v ? std::atoi(v) : 2;
-    }();
+    const uint32_t smallTile = nttSmallTile();
+    const int smallLe = nttSmallLe();
     const bool t1k = rows <= t1kRows && d->n <= smallTile * 128u;
     const dim3 g(d->n / (t1k ? smallTile : (uint32_t)kNttTile), rows);
     const bool small = rows < (uint32_t)kNttSmallRows;
@@ -3720,7 +3920,7 @@ static void nttRows(sfp_dev* d, const RowGroup& G0, int inverse, int passes = 3)
             StackRec r;
             r.go = [=](hipStream_t s_) {
                 hipLaunchKernelGGL(kern, g, dim3(threads), 0, s_, GS, d->bar, tw, twS, d->ninv, d->ninvS, d->logn,
-                                   twD, d->qinvD, d->ninvD, d->ninvQ, fp);
+                                   twD, d->qinvD, d->ninvD, d->ninvQ, fp, rowD);
             };
             if (kern2 && d->stackOn) {
                 auto P = std::make_shared<NttPay>();
@@ -3735,6 +3935,7 @@ static void nttRows(sfp_dev* d, const RowGroup& G0, int inverse, int passes = 3)
                 P->tw = tw;
                 P->twS = twS;
                 P->twD = twD;
+                P->rowD = rowD;
                 r.cls = STK_NTT;
                 r.key = stkKey((const void*)kern, g.x, (uint32_t)threads);
                 r.pay = std::move(P);
@@ -3742,10 +3943,7 @@ static void nttRows(sfp_dev* d, const RowGroup& G0, int inverse, int passes = 3)
             issueRec(d, std::move(r));
         });
     };
-    static const int le = [] {  // SFHE_NTT_LE: register-round width experiments (2, 3, 4)
-        const char* v = std::getenv("SFHE_NTT_LE");
-        return v ? std::atoi(v) : 0;
-    }();
+    const int le = nttLe();
     const int L = le ? le : (small ? 2 : 3);
     constexpr int T = kNttTile;
     auto smallPasses = [&](auto tileC) {
@@ -3759,7 +3957,11 @@ static void nttRows(sfp_dev* d, const RowGroup& G0, int inverse, int passes = 3)
                 pass(k_ntt<true, true, 3, ST>, NttKern2{}, NttKern4{}, NttKern8{}, ST >> 3);
             }
         } else if (!inverse) {
-            pass(k_ntt<false, true, 2, ST>, k_ntt<false, true, 2, ST, 2>, k_ntt<false, true, 2, ST, 4>, k_ntt<false, true, 2, ST, 8>, ST >> 2);
+            if (G.cy)  // ModUpPlan: the conversion in the COL pass's prologue (modupConvOk: LE 2, 1024-word tiles)
+                pass(k_ntt<false, true, 2, ST, 1, true>, k_ntt<false, true, 2, ST, 2, true>,
+                     k_ntt<false, true, 2, ST, 4, true>, k_ntt<false, true, 2, ST, 8, true>, ST >> 2);
+            else
+                pass(k_ntt<false, true, 2, ST>, k_ntt<false, true, 2, ST, 2>, k_ntt<false, true, 2, ST, 4>, k_ntt<false, true, 2, ST, 8>, ST >> 2);
             pass(k_ntt<false, false, 2, ST>, k_ntt<false, false, 2, ST, 2>, k_ntt<false, false, 2, ST, 4>, k_ntt<false, false, 2, ST, 8>, ST >> 2);
         } else {
             pass(k_ntt<true, false, 2, ST>, k_ntt<true, false, 2, ST, 2>, k_ntt<true, false, 2, ST, 4>, k_ntt<true, false, 2, ST, 8>, ST >> 2);
@@ -3776,7 +3978,11 @@ static void nttRows(sfp_dev* d, const RowGroup& G0, int inverse, int passes = 3)
             pass(k_ntt<false, true, 4, T>, NttKern2{}, NttKern4{}, NttKern8{}, T >> 4);
             pass(k_ntt<false, false, 4, T>, NttKern2{}, NttKern4{}, NttKern8{}, T >> 4);
         } else if (L == 2) {
-            pass(k_ntt<false, true, 2, T>, k_ntt<false, true, 2, T, 2>, k_ntt<false, true, 2, T, 4>, k_ntt<false, true, 2, T, 8>, T >> 2);
+            if (G.cy)
+                pass(k_ntt<false, true, 2, T, 1, true>, k_ntt<false, true, 2, T, 2, true>,
+                     k_ntt<false, true, 2, T, 4, true>, k_ntt<false, true, 2, T, 8, true>, T >> 2);
+            else
+                pass(k_ntt<false, true, 2, T>, k_ntt<false, true, 2, T, 2>, k_ntt<false, true, 2, T, 4>, k_ntt<false, true, 2, T, 8>, T >> 2);
             pass(k_ntt<false, false, 2, T>, k_ntt<false, false, 2, T, 2>, k_ntt<false, false, 2, T, 4>, k_ntt<false, false, 2, T, 8>, T >> 2);
         } else {
             pass(k_ntt<false, true, 3, T>, NttKern2{}, NttKern4{}, NttKern8{}, T >> 3);
@@ -3944,6 +4150,13 @@ static uint32_t kernelFamily(const void* f) {
     static const std::unordered_map<const void*, uint32_t> fam = [] {
         std::unordered_map<const void*, uint32_t> m;
         addNttAll<2, kNttTile>(m, true);
+        for (const void* k : {(const void*)k_ntt<false, true, 2, kNttTile, 1, true>,
+                              (const void*)k_ntt<false, true, 2, kNttTile, 2, true>,
+                              (const void*)k_ntt<false, true, 2, kNttTile, 4, true>,
+                              (const void*)k_ntt<false, true, 2, kNttTile, 8, true>,
+                              (const void*)k_ntt<false, true, 2, 1024, 1, true>, (const void*)k_ntt<false, true, 2, 1024, 2, true>,
+                              (const void*)k_ntt<false, true, 2, 1024, 4, true>, (const void*)k_ntt<false, true, 2, 1024, 8, true>})
+            m[k] = SFP_FAM_NTT;  // (the ModUp COL pass with its conversion)
         addNttAll<2, 1024>(m, true);
         addNttAll<2, 512>(m, true);
         addNttAll<3, kNttTile>(m, false);
@@ -4295,6 +4508,9 @@ sfp_conv* sfp_upload_conv(sfp_dev* d, uint32_t ns, const uint32_t* src, uint32_t
     c->nt = nt;
     c->hsrc.assign(src, src + ns);
     c->hdst.assign(dst, dst + nt);
+    c->hinv.assign(inv, inv + ns);
+    c->hmod.assign(mod, mod + (size_t)ns * nt);
+    for (uint32_t t = 0; t < nt; ++t) c->hrow.push_back(drow ? drow[t] : t);
     // every device table is checked: a failed allocation must surface as an
     // error here, not as a conversion kernel writing through a null pointer
     bool ok = true;
@@ -4387,6 +4603,15 @@ sfp_conv* sfp_upload_conv(sfp_dev* d, uint32_t ns, const uint32_t* src, uint32_t
 void sfp_free_conv(sfp_dev* d, sfp_conv* c) {
     if (!c) return;
     syncAll(d);
+    for (auto it = d->plans.begin(); it != d->plans.end();) {  // the levels' fused-ModUp plans that use c
+        ModUpPlan* P = it->second;
+        if (it->first == c || (P && std::find(P->convs.begin(), P->convs.end(), c) != P->convs.end())) {
+            if (P) freePlan(P);
+            it = d->plans.erase(it);
+        } else {
+            ++it;
+        }
+    }
     hipFree(c->src);
     hipFree(c->dst);
     hipFree(c->inv);
@@ -4495,6 +4720,127 @@ void sfp_conv_apply_centered(sfp_dev* d, uint64_t* dst, const uint64_t* src, con
     convLaunch(d, J, 1, c->fpOk);
 }
 
+// ModUp with its conversion fused into the forward COL pass (VERDICT r4
+// item 3): the INTT's last pass leaves y_s = [x_s * shat_s^-1]_{q_s} (its n^-1
+// times the conversion's source factor, per row) with FP64 rows stored as
+// doubles, and the COL pass of target row i of digit p computes its tile as
+// sum_s y_s * [shat_s]_{q_i} mod q_i from the digit's source tiles -- the
+// extended limbs are never written before their NTT, and k_convf's launch is
+// gone.  Same integers as k_convf + the plain COL pass (canonical residues).
+// Per level (keyed by its digit-0 table): the INTT's per-row constants and
+// the multipliers indexed by ext row.  Eligible where the FP64 form applies
+// to every source but q_0 (60-bit: split in two 30-bit halves) and the COL
+// pass runs LE = 2 (the defaults); otherwise the unfused launches run.
+static bool modupFuseOn() {  // SFHE_MODUP_FUSE=0: k_convf + the plain COL pass (A/B)
+    static const bool on = [] {
+        const char* v = std::getenv("SFHE_MODUP_FUSE");
+        return !v || *v != '0';
+    }();
+    return on;
+}
+static const ModUpPlan* modupPlan(sfp_dev* d, const sfp_conv* const* convs, uint32_t ell, uint32_t K,
+                                  uint32_t alpha) {
+    if (!modupFuseOn() || !nttFp() || d->n <= (uint32_t)kNttTile || nttSmallLe() != 2 || nttSmallTile() != 1024 ||
+        (nttLe() != 0 && nttLe() != 2))
+        return nullptr;
+    auto it = d->plans.find(convs[0]);
+    if (it != d->plans.end()) return it->second;
+    const uint32_t beta = (ell + alpha - 1) / alpha, rows = ell + K;
+    // eligibility: digit j's sources are rows j alpha + s; only q_0 (digit 0, s = 0) is 60-bit
+    bool ok = true;
+    bool big = false;
+    for (uint32_t j = 0; j < beta && ok; ++j) {
+        const sfp_conv* c = convs[j];
+        ok = c->ns == std::min(alpha, ell - j * alpha);
+        for (uint32_t sI = 0; sI < c->ns && ok; ++sI) {
+            ok = c->hsrc[sI] == j * alpha + sI;
+            if (d->hbar[c->hsrc[sI]].q >= kFpPrimeBound) {
+                ok = ok && j == 0 && sI == 0;
+                big = true;
+            }
+        }
+        for (uint32_t t = 0; t < c->nt && ok; ++t) ok = c->hrow[t] < rows;
+    }
+    if (!ok) {
+        d->plans[convs[0]] = nullptr;
+        return nullptr;
+    }
+    auto* P = new ModUpPlan;
+    P->ell = ell;
+    P->rows = rows;
+    P->big = big;
+    P->convs.assign(convs, convs + beta);
+    std::vector<u64> pk(ell), pks(ell), mI((size_t)beta * alpha * rows, 0);
+    std::vector<double> pd(ell), pq(ell), mD((size_t)beta * alpha * rows, 0.0), mQ((size_t)beta * alpha * rows, 0.0),
+        hD(rows, 0.0), hQ(rows, 0.0);
+    for (uint32_t j = 0; j < beta; ++j) {
+        const sfp_conv* c = convs[j];
+        for (uint32_t sI = 0; sI < c->ns; ++sI) {
+            const uint32_t r = j * alpha + sI, pr = c->hsrc[sI];
+            const sf_barrett& B = d->hbar[pr];
+            const u64 k = sf_mul(c->hinv[sI] % B.q, d->hninv[pr] % B.q, &B);
+            pk[r] = k;
+            pks[r] = sf_shoup_precomp(k, B.q);
+            pd[r] = (double)k;
+            pq[r] = (double)k / (double)B.q;
+            for (uint32_t t = 0; t < c->nt; ++t) {
+                const uint32_t row = c->hrow[t];
+                const u64 p = d->hbar[c->hdst[t]].q, m = c->hmod[(size_t)sI * c->nt + t];
+                const size_t o = ((size_t)j * alpha + sI) * rows + row;
+                mI[o] = m;
+                mD[o] = (double)m;
+                mQ[o] = (double)m / (double)p;
+                if (big && j == 0 && sI == 0) {
+                    const u64 h = (u64)(((unsigned __int128)m << 30) % p);
+                    hD[row] = (double)h;
+                    hQ[row] = (double)h / (double)p;
+                }
+            }
+        }
+    }
+    bool mok = true;
+    auto up = [&](auto*& dp, const auto& v) {
+        if (!mok) return;
+        if (hipMalloc((void**)&dp, v.size() * sizeof(v[0]) + 8) != hipSuccess) {
+            hipGetLastError();
+            dp = nullptr;
+            mok = false;
+            return;
+        }
+        hostToDev(d, dp, v.data(), v.size() * sizeof(v[0]));
+    };
+    up(P->postK, pk);
+    up(P->postKS, pks);
+    up(P->postD, pd);
+    up(P->postQ, pq);
+    up(P->mD, mD);
+    up(P->mQ, mQ);
+    up(P->mI, mI);
+    up(P->hD, hD);
+    up(P->hQ, hQ);
+    if (!mok) {
+        record(d, "modup plan allocation", hipErrorOutOfMemory);
+        freePlan(P);
+        return nullptr;
+    }
+    d->plans[convs[0]] = P;
+    return P;
+}
+static void planInto(const ModUpPlan* P, RowGroup& A, RowGroup& B, const u64* y) {
+    A.postK = P->postK;
+    A.postKS = P->postKS;
+    A.postD = P->postD;
+    A.postQ = P->postQ;
+    B.cy = y;
+    B.cmD = P->mD;
+    B.cmQ = P->mQ;
+    B.cmI = P->mI;
+    B.chD = P->hD;
+    B.chQ = P->hQ;
+    B.cRows = P->rows;
+    B.cBig = P->big ? 1u : 0u;
+}
+
 void sfp_modup(sfp_dev* d, uint64_t* ext, const uint64_t* in, uint32_t ell, uint32_t K,
                uint32_t Lq, uint32_t alpha, const sfp_conv* const* convs, uint64_t* scr) {
     const uint32_t n = d->n;
@@ -4511,20 +4857,23 @@ void sfp_modup(sfp_dev* d, uint64_t* ext, const uint64_t* in, uint32_t ell, uint
     A.copy = RowPtr{ext, stride, (long long)n};
     A.copyByAlpha = 1;
     A.alpha = alpha;
-    nttRows(d, A, 1);
-    // every digit's conversion in one launch
-    ConvJobs J;
-    bool fpOk = true;
-    for (uint32_t j = 0; j < beta; ++j) {
-        J.j[j] = convJob(convs[j], ext + j * stride, scr + (size_t)j * alpha * n, convs[j]->nt, 0);
-        fpOk = fpOk && convs[j]->fpOk;
-    }
-    convLaunch(d, J, beta, fpOk);
-    // NTT of every converted row (digit-own rows skipped)
     RowGroup B = rowsOf(beta, ell + K, sfp_limbs{ell + K, ell, Lq, 0});
     B.src = B.dst = RowPtr{ext, stride, (long long)n};
     B.skipEll = ell;
     B.alpha = alpha;
+    const ModUpPlan* P = modupPlan(d, convs, ell, K, alpha);
+    if (P) planInto(P, A, B, scr);
+    nttRows(d, A, 1);
+    if (!P) {  // every digit's conversion in one launch
+        ConvJobs J;
+        bool fpOk = true;
+        for (uint32_t j = 0; j < beta; ++j) {
+            J.j[j] = convJob(convs[j], ext + j * stride, scr + (size_t)j * alpha * n, convs[j]->nt, 0);
+            fpOk = fpOk && convs[j]->fpOk;
+        }
+        convLaunch(d, J, beta, fpOk);
+    }
+    // NTT of every converted row (digit-own rows skipped)
     nttRows(d, B, 0);
 }
 
@@ -4553,19 +4902,24 @@ static void modupInnerCore(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uin
     A.src = RowPtr{in, 0, (long long)n};
     A.dst = RowPtr{scr, 0, (long long)n};
     if (inMul) A.pre = RowPtr{inMul, 0, (long long)n};
-    nttRows(d, A, 1);
-    ConvJobs J;
-    bool fpOk = true;
-    for (uint32_t j = 0; j < beta; ++j) {
-        J.j[j] = convJob(convs[j], ext + j * stride, scr + (size_t)j * alpha * n, convs[j]->nt, 0);
-        fpOk = fpOk && convs[j]->fpOk;
-    }
-    convLaunch(d, J, beta, fpOk);
-    // the forward COL pass of every converted row; the ROW pass runs fused below
     RowGroup B = rowsOf(beta, ell + K, sfp_limbs{ell + K, ell, Lq, 0});
     B.src = B.dst = RowPtr{ext, stride, (long long)n};
     B.skipEll = ell;
     B.alpha = alpha;
+    const ModUpPlan* P = modupPlan(d, convs, ell, K, alpha);
+    if (P) planInto(P, A, B, scr);
+    nttRows(d, A, 1);
+    if (!P) {
+        ConvJobs J;
+        bool fpOk = true;
+        for (uint32_t j = 0; j < beta; ++j) {
+            J.j[j] = convJob(convs[j], ext + j * stride, scr + (size_t)j * alpha * n, convs[j]->nt, 0);
+            fpOk = fpOk && convs[j]->fpOk;
+        }
+        convLaunch(d, J, beta, fpOk);
+    }
+    // the forward COL pass of every converted row (with the conversion in
+    // its prologue where a plan applies); the ROW pass runs fused below
     nttRows(d, B, 0, 1);
     KsArgs a;
     std::memset(&a, 0, sizeof a);
@@ -4611,7 +4965,7 @@ static void modupInnerCore(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uin
         StackRec r;
         r.go = [=](hipStream_t s_) {
             hipLaunchKernelGGL(k1, g, dim3(threads), 0, s_, AS, d->bar, d->psi, d->psiS, d->logn, d->psiD, d->qinvD,
-                               fp);
+                               fp, d->rowD);
         };
         if (d->stackOn) {
             auto P = std::make_shared<KsPay>();
