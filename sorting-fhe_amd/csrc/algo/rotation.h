@@ -158,13 +158,24 @@ class RotationComposer {
             return out;
         }
         std::shared_ptr<FastRotationPrecomp> pre;
-        for (size_t i = 0; i < amounts.size(); ++i) {
-            if (amounts[i] % (int)in->GetSlots() == 0) {
-                out[i] = in->Clone();
-                continue;
+        for (int a : amounts)
+            if (a % (int)in->GetSlots() != 0) {
+                pre = m_cc->EvalFastRotationPrecompute(in);
+                break;
             }
-            if (!pre) pre = m_cc->EvalFastRotationPrecompute(in);
-            out[i] = m_cc->EvalFastRotation(in, amounts[i], m_cc->GetCyclotomicOrder(), pre);
+        // the rotations are independent: batches of them run as merged
+        // launches (BatchScope; same values, one op per virtual lane)
+        const size_t w = m_cc->BatchWidth();
+        for (size_t b0 = 0; b0 < amounts.size(); b0 += w) {
+            const size_t b1 = std::min(amounts.size(), b0 + w);
+            BatchScope bs(m_cc.get(), (uint32_t)(b1 - b0));
+            for (size_t i = b0; i < b1; ++i) {
+                bs.lane((uint32_t)(i - b0));
+                if (amounts[i] % (int)in->GetSlots() == 0)
+                    out[i] = in->Clone();
+                else
+                    out[i] = m_cc->EvalFastRotation(in, amounts[i], m_cc->GetCyclotomicOrder(), pre);
+            }
         }
         return out;
     }

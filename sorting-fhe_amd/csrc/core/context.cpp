@@ -1881,6 +1881,8 @@ bool CryptoContextImpl<DCRTPoly>::BeginBatch(uint32_t count) {
     return false;
 }
 
+uint32_t CryptoContextImpl<DCRTPoly>::BatchWidth() const { return batchWidth(); }
+
 void CryptoContextImpl<DCRTPoly>::BatchLane(uint32_t i) {
     OpLock g(st.get());
     if (st->batchDepth) sfp_batch_lane(st->dev, i);

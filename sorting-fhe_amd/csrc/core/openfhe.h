@@ -559,6 +559,7 @@ class CryptoContextImpl<DCRTPoly> : public std::enable_shared_from_this<CryptoCo
     bool BeginBatch(uint32_t count);
     void BatchLane(uint32_t i);
     void EndBatch();
+    uint32_t BatchWidth() const;  // ops per batch (SFHE_BATCH_WIDTH)
     void SetLane(int lane);
     void JoinLanes();
     // Plaintext-encoding cache across calls (default on); see DESIGN.md.
