@@ -669,6 +669,14 @@ int sfp_modup_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* 
     (void)key; (void)fold0; (void)fold1; (void)fold_k; (void)accum; (void)inv_from; (void)ext; (void)scratch;
     return -1;
 }
+int sfp_modup_inner_phase(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* in, uint32_t ell, uint32_t K,
+                          uint32_t Lq, uint32_t alpha, const sfp_conv* const* convs, const uint64_t* key,
+                          const uint64_t* fold0, const uint64_t* fold1, uint64_t fold_k, int accum,
+                          uint32_t inv_from, uint64_t* ext, uint64_t* scratch, int phases) {
+    (void)phases; /* no fused form: the caller runs the unfused prims */
+    return sfp_modup_inner(d, acc0, acc1, in, ell, K, Lq, alpha, convs, key, fold0, fold1, fold_k, accum, inv_from,
+                           ext, scratch);
+}
 
 /* no fused tensor + relinearisation + rescale: the host layer runs the prims */
 int sfp_mult_relin_rescale(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint64_t* a0, const uint64_t* a1,

@@ -2761,12 +2761,53 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotateSum(const std::vecto
     const bool shard = s->shardAt(ell);  // local rows; the exchanges inside modupShard / modDownShard
     const size_t stride = (size_t)(shard ? s->extmap(ell).count : ell + K) * n;
     auto out = pend ? SfheInternal::newPendingCt(this, level, slots) : SfheInternal::newCt(this, level, slots);
-    auto t = s->alloc((size_t)s->rows(ell) * n);
-    auto c0 = s->alloc((size_t)s->rows(ell) * n);
-    auto ext = shard ? s->alloc(stride * beta) : nullptr;  // (the unsharded ModUp allocates its own)
     auto acc = s->alloc(2 * stride);
     int rowDone = 0;
-    for (size_t i = 0; i < rot.size(); ++i) {
+    auto& convs = SfheInternal::modupConv(this, ell);
+    if (!shard && sfp_modup_inner_phase(s->dev, nullptr, nullptr, nullptr, ell, K, s->Lq, s->alpha, convs.data(),
+                                        nullptr, nullptr, nullptr, 0, 0, 0, nullptr, nullptr, 0) == 0) {
+        // The terms' rotations and ModUps are independent: each chunk of
+        // them runs as batched ops (merged launches), then its terms' fused
+        // inner products accumulate into acc in turn (never merged: one
+        // accumulator), the last one with the ModDown's first inverse pass.
+        const size_t w = batchWidth();
+        for (size_t b0 = 0; b0 < rot.size(); b0 += w) {
+            const size_t b1 = std::min(rot.size(), b0 + w);
+            std::vector<DeviceBufferPtr> tb, cb, eb, sb;
+            {
+                BatchScope bs(this, (uint32_t)(b1 - b0));
+                for (size_t i = b0; i < b1; ++i) {
+                    bs.lane((uint32_t)(i - b0));
+                    const Ciphertext<DCRTPoly>& x = a[rot[i]];
+                    const uint32_t gal = GaloisForRotation(r[rot[i]]);
+                    tb.push_back(s->alloc((size_t)ell * n));
+                    eb.push_back(s->alloc(stride * beta));
+                    sb.push_back(s->alloc((size_t)ell * n));
+                    cb.push_back(i ? s->alloc((size_t)ell * n) : nullptr);
+                    sfp_automorph(s->dev, i ? cb.back()->ptr : out->c0, x->c0, gal, st->qmap(ell));
+                    sfp_automorph(s->dev, tb.back()->ptr, x->c1, gal, st->qmap(ell));
+                    sfp_modup_inner_phase(s->dev, nullptr, nullptr, tb.back()->ptr, ell, K, s->Lq, s->alpha,
+                                          convs.data(), nullptr, nullptr, nullptr, 0, 0, ~0u, eb.back()->ptr,
+                                          sb.back()->ptr, 1);
+                }
+            }
+            for (size_t i = b0; i < b1; ++i) {
+                const size_t k = i - b0;
+                if (i) sfp_add(s->dev, out->c0, out->c0, cb[k]->ptr, st->qmap(ell));
+                sfp_modup_inner_phase(s->dev, acc->ptr, acc->ptr + stride, tb[k]->ptr, ell, K, s->Lq, s->alpha,
+                                      convs.data(), (*keys[i])->ptr, nullptr, nullptr, 0, i ? 1 : 0,
+                                      i + 1 == rot.size() ? ell : ~0u, eb[k]->ptr, sb[k]->ptr, 2);
+                s->stats.automorph++;
+                s->stats.keyswitch++;
+                s->countBytes((5.0 * ell + 2.0 * beta * (ell + K)) * n * 8);
+            }
+        }
+        rowDone = 1;
+    }
+    auto t = rowDone ? nullptr : s->alloc((size_t)s->rows(ell) * n);
+    auto c0 = rowDone ? nullptr : s->alloc((size_t)s->rows(ell) * n);
+    auto ext = shard ? s->alloc(stride * beta) : nullptr;  // (the unsharded ModUp allocates its own)
+    for (size_t i = 0; i < (rowDone ? 0 : rot.size()); ++i) {
         const Ciphertext<DCRTPoly>& x = a[rot[i]];
         const uint32_t gal = GaloisForRotation(r[rot[i]]);
         // c0' = sum sigma_k(c0_k) (+ the shared ModDown below)

@@ -4893,10 +4893,11 @@ static void modupInnerCore(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uin
                            uint32_t ell, uint32_t K, uint32_t Lq, uint32_t alpha, const sfp_conv* const* convs,
                            const uint64_t* key, const uint64_t* fold0, const uint64_t* fold1,
                            const uint64_t* const* T, uint64_t foldK, int accum, uint32_t invFrom, uint64_t* ext,
-                           uint64_t* scr) {
+                           uint64_t* scr, int phases = 3) {
     const uint32_t n = d->n;
     const uint32_t beta = (ell + alpha - 1) / alpha;
     const long long stride = (long long)(ell + K) * n;
+    if (phases & 1) {
     // INTT of every input row (the digits' own rows are read from `in` by the fused pass)
     RowGroup A = rowsOf(1, ell, sfp_limbs{ell, ell, 0, 0});
     A.src = RowPtr{in, 0, (long long)n};
@@ -4921,6 +4922,8 @@ static void modupInnerCore(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uin
     // the forward COL pass of every converted row (with the conversion in
     // its prologue where a plan applies); the ROW pass runs fused below
     nttRows(d, B, 0, 1);
+    }
+    if (!(phases & 2)) return;
     KsArgs a;
     std::memset(&a, 0, sizeof a);
     a.in = in;
@@ -4986,19 +4989,28 @@ static void modupInnerCore(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uin
     checkLaunch(d, "ntt_ks");
 }
 
-int sfp_modup_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* in, uint32_t ell, uint32_t K,
-                    uint32_t Lq, uint32_t alpha, const sfp_conv* const* convs, const uint64_t* key,
-                    const uint64_t* fold0, const uint64_t* fold1, uint64_t foldK, int accum, uint32_t invFrom,
-                    uint64_t* ext, uint64_t* scr) {
+int sfp_modup_inner_phase(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* in, uint32_t ell, uint32_t K,
+                          uint32_t Lq, uint32_t alpha, const sfp_conv* const* convs, const uint64_t* key,
+                          const uint64_t* fold0, const uint64_t* fold1, uint64_t foldK, int accum, uint32_t invFrom,
+                          uint64_t* ext, uint64_t* scr, int phases) {
     const uint32_t beta = (ell + alpha - 1) / alpha;
     if (!ksFuse() || d->n <= (uint32_t)kNttTile) return -1;  // the caller runs sfp_modup + sfp_ks_inner*
+    if (!phases) return 0;
     if (beta > (uint32_t)kMaxConvJobs || ell + K > SFP_MAX_LIMBS || (fold0 && (!fold1 || ell < 1))) {
         record(d, "modup_inner (too many digits / limbs)", hipErrorInvalidValue);
         return 0;
     }
     modupInnerCore(d, acc0, acc1, in, nullptr, ell, K, Lq, alpha, convs, key, fold0, fold1, nullptr, foldK, accum,
-                   invFrom, ext, scr);
+                   invFrom, ext, scr, phases);
     return 0;
+}
+
+int sfp_modup_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* in, uint32_t ell, uint32_t K,
+                    uint32_t Lq, uint32_t alpha, const sfp_conv* const* convs, const uint64_t* key,
+                    const uint64_t* fold0, const uint64_t* fold1, uint64_t foldK, int accum, uint32_t invFrom,
+                    uint64_t* ext, uint64_t* scr) {
+    return sfp_modup_inner_phase(d, acc0, acc1, in, ell, K, Lq, alpha, convs, key, fold0, fold1, foldK, accum,
+                                 invFrom, ext, scr, 3);
 }
 
 void sfp_ks_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,

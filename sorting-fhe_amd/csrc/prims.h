@@ -192,6 +192,16 @@ int sfp_modup_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* 
                     uint32_t Lq, uint32_t alpha, const sfp_conv* const* convs, const uint64_t* key,
                     const uint64_t* fold0, const uint64_t* fold1, uint64_t fold_k, int accum, uint32_t inv_from,
                     uint64_t* ext, uint64_t* scratch);
+// sfp_modup_inner in two halves (the same launches): phases 1 = the ModUp
+// (INTT of `in` into scratch, the digits' conversions and forward COL pass
+// into ext), 2 = the fused ROW pass + inner product reading ext and `in`
+// (the same ext / scratch / in as its phase 1), 3 = both; 0 = only report
+// whether the fused form exists (0) or not (-1).  Independent key switches
+// run their phase 1 as batched ops, then their accumulating phase 2 in turn.
+int sfp_modup_inner_phase(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* in, uint32_t ell, uint32_t K,
+                          uint32_t Lq, uint32_t alpha, const sfp_conv* const* convs, const uint64_t* key,
+                          const uint64_t* fold0, const uint64_t* fold1, uint64_t fold_k, int accum,
+                          uint32_t inv_from, uint64_t* ext, uint64_t* scratch, int phases);
 
 // Key inner product:  acc0 = sum_j ext_j * kb_j,  acc1 = sum_j ext_j * ka_j
 //   ext  : beta extended polys, each (ell+K) limbs, stride ext_stride.
