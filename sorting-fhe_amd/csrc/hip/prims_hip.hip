@@ -1231,6 +1231,212 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroupSet<NG> GS, co
 #endif
 }
 
+// ModUp's conversion + forward COL pass for TG target rows per block
+// (ModUpPlan, ring 2^16): the digit's source tiles are read once and feed
+// all TG targets' conversion sums (k_ntt<..., CONV> reads them once per
+// target: TG times the L2 traffic), then each target's tile runs the four COL
+// rounds in LDS and is stored, as k_ntt's COL pass stores it (FP64 rows
+// canonical, the integer row q_0 in the lazy forward range).  Grid row
+// (p, g): digit p, targets g TG .. g TG + TG - 1 of its ell + K rows (the
+// digit's own rows and rows past the end skipped).  Same signature as k_ntt
+// (the merged-launch machinery), unused arguments ignored.
+#ifndef SFHE_MODUP_TG
+#define SFHE_MODUP_TG 4
+#endif
+constexpr int kModupTg = SFHE_MODUP_TG;
+template <int TILE, int NG, int TG>
+__global__ __launch_bounds__(TILE >> 2) void k_modup_col(const RowGroupSet<NG> GS, const sf_barrett* __restrict__ bar,
+                                                         const u64* __restrict__ tw, const u64* __restrict__ twS,
+                                                         const u64* __restrict__, const u64* __restrict__,
+                                                         uint32_t logn, const double* __restrict__ twD,
+                                                         const double* __restrict__ qinvD,
+                                                         const double* __restrict__, const double* __restrict__,
+                                                         int useFp, const double* __restrict__) {
+    constexpr int LE = 2, NT = TILE >> LE, NPAIR = (1 << LE) / 2;
+    __shared__ u64 s[TILE];
+    __shared__ u64 tW[kNttColTw], tX[kNttColTw];
+    const uint32_t n = 1u << logn;
+    const uint32_t logR = logn - 8;  // (8: ring 2^16, checked on the host)
+    uint32_t rid;
+    const RowGroup& G = GS.a[argSel(GS, rid)];
+    const uint32_t RG = (G.R + TG - 1) / TG;
+    const uint32_t pp = rid / RG, g0 = (rid % RG) * TG;
+    const uint32_t own0 = pp * G.alpha, own1 = min(own0 + G.alpha, G.skipEll);
+    bool live[TG];  // (compile-time indexed: no scratch)
+    bool any = false;
+#pragma unroll
+    for (int u = 0; u < TG; ++u) {
+        const uint32_t ii = g0 + u;
+        live[u] = ii < G.R && !(ii >= own0 && ii < own1);
+        any = any || live[u];
+    }
+    if (!any) return;
+    NttTile T;
+    T.logn = logn;
+    T.d = logR;
+    T.logC = (uint32_t)__builtin_ctz(TILE) - logR;
+    T.C = 1u << T.logC;
+    const uint32_t tile = (gridDim.x & 7) ? blockIdx.x : (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    T.c0 = tile * T.C;
+    T.r0 = 0;
+    auto tileOff = [&](int k) -> size_t {
+        const uint32_t e = 2 * (threadIdx.x + k * NT);
+        return (size_t)(e >> T.logC) * 256 + T.c0 + (e & (T.C - 1));
+    };
+    const uint32_t ns = own1 - own0;
+    const u64* yb = G.cy + (size_t)own0 * n;
+    const bool big0 = G.cBig && pp == 0;
+    // the targets' arithmetic: FP64 rows take the shared source pass; the
+    // integer row (q_0, digits > 0) takes a pass of its own below
+    uint32_t prime[TG];
+    double qd[TG], qi[TG];
+    bool fpT[TG];
+    int nfp = 0;
+#pragma unroll
+    for (int u = 0; u < TG; ++u) {
+        prime[u] = primeOf(G.pm, min(g0 + u, G.R - 1));
+        const u64 q = bar[prime[u]].q;
+        fpT[u] = useFp && q < kFpPrimeBound;
+        qd[u] = (double)q;
+        qi[u] = qinvD[prime[u]];
+        nfp += live[u] && fpT[u];
+    }
+    double acc[TG][2 * NPAIR];
+#pragma unroll
+    for (int u = 0; u < TG; ++u)
+#pragma unroll
+        for (int w = 0; w < 2 * NPAIR; ++w) acc[u][w] = 0.0;
+    if (nfp) {
+        constexpr int GRP = 4;
+        for (uint32_t s0 = 0; s0 < ns; s0 += GRP) {
+            ulonglong2 v[GRP][NPAIR];
+#pragma unroll
+            for (int g = 0; g < GRP; ++g)
+                if (s0 + g < ns)
+#pragma unroll
+                    for (int k = 0; k < NPAIR; ++k)
+                        v[g][k] = *reinterpret_cast<const ulonglong2*>(yb + (size_t)(s0 + g) * n + tileOff(k));
+#pragma unroll
+            for (int g = 0; g < GRP; ++g) {
+                const uint32_t sI = s0 + g;
+                if (sI >= ns) break;
+                const size_t mrow = (size_t)(own0 + sI) * G.cRows;
+                const bool split = big0 && sI == 0;  // y < 2^60: y_lo + 2^30 y_hi
+                double y[2 * NPAIR], yh[2 * NPAIR];
+#pragma unroll
+                for (int k = 0; k < NPAIR; ++k) {
+                    if (split) {
+                        y[2 * k] = u2d(v[g][k].x & 0x3fffffffull);
+                        y[2 * k + 1] = u2d(v[g][k].y & 0x3fffffffull);
+                        yh[2 * k] = u2d(v[g][k].x >> 30);
+                        yh[2 * k + 1] = u2d(v[g][k].y >> 30);
+                    } else {
+                        y[2 * k] = __longlong_as_double(v[g][k].x);
+                        y[2 * k + 1] = __longlong_as_double(v[g][k].y);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < TG; ++u) {
+                    if (!live[u] || !fpT[u]) continue;
+                    const double md = G.cmD[mrow + g0 + u], mq = G.cmQ[mrow + g0 + u];
+#pragma unroll
+                    for (int w = 0; w < 2 * NPAIR; ++w) acc[u][w] += fpMulMod(y[w], md, mq, qd[u]);
+                    if (split) {
+                        const double hd = G.chD[g0 + u], hq = G.chQ[g0 + u];
+#pragma unroll
+                        for (int w = 0; w < 2 * NPAIR; ++w) acc[u][w] += fpMulMod(yh[w], hd, hq, qd[u]);
+                    }
+                }
+            }
+        }
+    }
+    constexpr int kColPer = (int)((kNttColTw + NT - 1) / NT);
+    const uint32_t colTw = (1u << logR) - 1;
+    bool first = true;
+#pragma unroll
+    for (int u = 0; u < TG; ++u) {
+        if (!live[u]) continue;
+        const uint32_t ii = g0 + u, pr = prime[u];
+        const bool fp = fpT[u];
+        const u64 q = bar[pr].q;
+        ulonglong2 xr[NPAIR];
+        if (fp) {
+#pragma unroll
+            for (int k = 0; k < NPAIR; ++k) {  // |acc| < 14 * 1.5 q < 2^46: exact
+                xr[k].x = __double_as_longlong(fpReduce(acc[u][2 * k], qd[u], qi[u]));
+                xr[k].y = __double_as_longlong(fpReduce(acc[u][2 * k + 1], qd[u], qi[u]));
+            }
+        } else {  // 128-bit sums of canonical residues
+            const sf_barrett CB = loadBar(bar, pr);
+            Acc a2[2 * NPAIR];
+#pragma unroll
+            for (int w = 0; w < 2 * NPAIR; ++w) a2[w] = Acc{0, 0};
+            for (uint32_t sI = 0; sI < ns; ++sI) {
+                const u64 m = G.cmI[(size_t)(own0 + sI) * G.cRows + ii];
+                const bool raw = big0 && sI == 0;
+#pragma unroll
+                for (int k = 0; k < NPAIR; ++k) {
+                    const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(yb + (size_t)sI * n + tileOff(k));
+                    macc(a2[2 * k], raw ? v.x : d2u(__longlong_as_double(v.x)), m);
+                    macc(a2[2 * k + 1], raw ? v.y : d2u(__longlong_as_double(v.y)), m);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < NPAIR; ++k) {
+                xr[k].x = sf_reduce128_acc(a2[2 * k].lo, a2[2 * k].hi, &CB);
+                xr[k].y = sf_reduce128_acc(a2[2 * k + 1].lo, a2[2 * k + 1].hi, &CB);
+            }
+        }
+        // the pass's twiddles for this prime, the tile -> LDS
+        const u64* gwI = tw + (size_t)pr * n;
+        const u64* gwD = reinterpret_cast<const u64*>(twD) + (size_t)pr * n;
+        const u64* gx = twS + (size_t)pr * n;
+        if (!first) __syncthreads();  // the previous target's readers are done with s / tW
+        first = false;
+#pragma unroll
+        for (int c = 0; c < kColPer; ++c) {
+            const uint32_t e = threadIdx.x + c * NT;
+            if (e < colTw) {
+                tW[e] = fp ? gwD[e + 1] : gwI[e + 1];
+                if (!fp) tX[e] = gx[e + 1];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < NPAIR; ++k) {
+            const uint32_t e = 2 * (threadIdx.x + k * NT);
+            s[ldsSw(e)] = xr[k].x;
+            s[ldsSw(e + 1)] = xr[k].y;
+        }
+        __syncthreads();
+        if (fp) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                nttRoundFP<false, true, 2, 2, TILE, false, 8>(reinterpret_cast<double*>(s), T, 0u, 2 * r, qd[u],
+                                                              reinterpret_cast<const double*>(tW), qi[u]);
+                __syncthreads();
+            }
+        } else {
+            for (uint32_t r = 0; r < 4; ++r) {
+                nttRoundDyn<false, true, LE, TILE>(2, s, T, 0u, LE * r, q, tW, tX);
+                __syncthreads();
+            }
+        }
+        u64* out = rowAt(G.dst, pp, ii);
+#pragma unroll
+        for (int k = 0; k < NPAIR; ++k) {
+            const uint32_t e = 2 * (threadIdx.x + k * NT);
+            ulonglong2 x;
+            x.x = s[ldsSw(e)];
+            x.y = s[ldsSw(e + 1)];
+            if (fp) {
+                x.x = d2u(fpReduce(__longlong_as_double(x.x), qd[u], qi[u]));
+                x.y = d2u(fpReduce(__longlong_as_double(x.y), qd[u], qi[u]));
+            }
+            *reinterpret_cast<ulonglong2*>(out + tileOff(k)) = x;
+        }
+    }
+}
+
 // Rings of at most one tile per row (n <= kNttTile = 2^11: the test
 // rings the reference's k-way unit tests use, 2^10): the whole row in LDS, every
 // stage in one block, exact radix-2 butterflies (the oracle's schedule, so
@@ -3905,7 +4111,8 @@ static void nttRows(sfp_dev* d, const RowGroup& G0, int inverse, int passes = 3)
     const uint32_t smallTile = nttSmallTile();
     const int smallLe = nttSmallLe();
     const bool t1k = rows <= t1kRows && d->n <= smallTile * 128u;
-    const dim3 g(d->n / (t1k ? smallTile : (uint32_t)kNttTile), rows);
+    dim3 g(d->n / (t1k ? smallTile : (uint32_t)kNttTile), rows);
+    uint32_t gridRows = rows;  // (k_modup_col: grid rows are groups of target rows)
     const bool small = rows < (uint32_t)kNttSmallRows;
     int npass = 0;
     // kern2 / kern4: the same pass over two / four row groups (merged launches), or null
@@ -3925,7 +4132,7 @@ static void nttRows(sfp_dev* d, const RowGroup& G0, int inverse, int passes = 3)
             if (kern2 && d->stackOn) {
                 auto P = std::make_shared<NttPay>();
                 P->G = G;
-                P->rows = rows;
+                P->rows = gridRows;
                 P->g = g;
                 P->threads = threads;
                 P->useFp = fp;
@@ -3968,7 +4175,29 @@ static void nttRows(sfp_dev* d, const RowGroup& G0, int inverse, int passes = 3)
             pass(k_ntt<true, true, 2, ST>, k_ntt<true, true, 2, ST, 2>, k_ntt<true, true, 2, ST, 4>, k_ntt<true, true, 2, ST, 8>, ST >> 2);
         }
     };
-    if (t1k) {
+    static const bool modupCol = [] {  // SFHE_MODUP_COL=0: k_ntt<..., CONV> (one target per block; A/B)
+        const char* v = std::getenv("SFHE_MODUP_COL");
+        return !v || *v != '0';
+    }();
+    if (G.cy && modupCol && !inverse && d->logn == 16 && smallTile == 1024 && L == 2) {
+        // ModUpPlan at ring 2^16: the conversion + COL pass, kModupTg targets per block
+        constexpr int TG = kModupTg;
+        g.y = G.P * ((G.R + TG - 1) / TG);
+        gridRows = g.y;
+        if (t1k)
+            pass(k_modup_col<1024, 1, TG>, k_modup_col<1024, 2, TG>, k_modup_col<1024, 4, TG>, k_modup_col<1024, 8, TG>,
+                 1024 >> 2);
+        else
+            pass(k_modup_col<T, 1, TG>, k_modup_col<T, 2, TG>, k_modup_col<T, 4, TG>, k_modup_col<T, 8, TG>, T >> 2);
+        g.y = rows;
+        gridRows = rows;
+        if (t1k)
+            pass(k_ntt<false, false, 2, 1024>, k_ntt<false, false, 2, 1024, 2>, k_ntt<false, false, 2, 1024, 4>,
+                 k_ntt<false, false, 2, 1024, 8>, 1024 >> 2);
+        else
+            pass(k_ntt<false, false, 2, T>, k_ntt<false, false, 2, T, 2>, k_ntt<false, false, 2, T, 4>,
+                 k_ntt<false, false, 2, T, 8>, T >> 2);
+    } else if (t1k) {
         if (smallTile == 512)
             smallPasses(std::integral_constant<int, 512>{});
         else
@@ -4157,6 +4386,11 @@ static uint32_t kernelFamily(const void* f) {
                               (const void*)k_ntt<false, true, 2, 1024, 1, true>, (const void*)k_ntt<false, true, 2, 1024, 2, true>,
                               (const void*)k_ntt<false, true, 2, 1024, 4, true>, (const void*)k_ntt<false, true, 2, 1024, 8, true>})
             m[k] = SFP_FAM_NTT;  // (the ModUp COL pass with its conversion)
+        for (const void* k : {(const void*)k_modup_col<kNttTile, 1, kModupTg>, (const void*)k_modup_col<kNttTile, 2, kModupTg>,
+                              (const void*)k_modup_col<kNttTile, 4, kModupTg>, (const void*)k_modup_col<kNttTile, 8, kModupTg>,
+                              (const void*)k_modup_col<1024, 1, kModupTg>, (const void*)k_modup_col<1024, 2, kModupTg>,
+                              (const void*)k_modup_col<1024, 4, kModupTg>, (const void*)k_modup_col<1024, 8, kModupTg>})
+            m[k] = SFP_FAM_NTT;
         addNttAll<2, 1024>(m, true);
         addNttAll<2, 512>(m, true);
         addNttAll<3, kNttTile>(m, false);
@@ -4179,6 +4413,37 @@ static uint32_t kernelFamily(const void* f) {
     }();
     auto it = fam.find(f);
     return it == fam.end() ? (uint32_t)SFP_FAM_COUNT : it->second;
+}
+
+// Rows an NTT-family node transforms: its grid rows, except k_modup_col's
+// (groups of kModupTg target rows, the digits' own rows skipped), read from
+// its argument set.
+template <int NG>
+static double modupColRows(const void* arg) {
+    const auto& S = *static_cast<const RowGroupSet<NG>*>(arg);
+    double r = 0;
+    for (int i = 0; i < NG; ++i) {
+        const RowGroup& G = S.a[i];
+        for (uint32_t p = 0; p < G.P; ++p) {
+            const uint32_t o0 = p * G.alpha, o1 = std::min(o0 + G.alpha, G.skipEll);
+            r += G.R - (o1 > o0 ? o1 - o0 : 0);
+        }
+    }
+    return r;
+}
+static double nttNodeRows(const hipKernelNodeParams& kp) {
+    const void* f = kp.func;
+    if (kp.kernelParams) {
+        if (f == (const void*)k_modup_col<kNttTile, 1, kModupTg> || f == (const void*)k_modup_col<1024, 1, kModupTg>)
+            return modupColRows<1>(kp.kernelParams[0]);
+        if (f == (const void*)k_modup_col<kNttTile, 2, kModupTg> || f == (const void*)k_modup_col<1024, 2, kModupTg>)
+            return modupColRows<2>(kp.kernelParams[0]);
+        if (f == (const void*)k_modup_col<kNttTile, 4, kModupTg> || f == (const void*)k_modup_col<1024, 4, kModupTg>)
+            return modupColRows<4>(kp.kernelParams[0]);
+        if (f == (const void*)k_modup_col<kNttTile, 8, kModupTg> || f == (const void*)k_modup_col<1024, 8, kModupTg>)
+            return modupColRows<8>(kp.kernelParams[0]);
+    }
+    return (double)kp.gridDim.y;
 }
 
 int sfp_graph_family_time(sfp_dev* d, sfp_graph* g, uint32_t fam, int reps, double* ms, uint64_t* launches,
@@ -4213,7 +4478,7 @@ int sfp_graph_family_time(sfp_dev* d, sfp_graph* g, uint32_t fam, int reps, doub
         }
         prev = nn2;
         ++cnt;
-        if (kf == SFP_FAM_NTT) b += 16.0 * kp.gridDim.y * d->n;  // one pass reads and writes each row once
+        if (kf == SFP_FAM_NTT) b += 16.0 * nttNodeRows(kp) * d->n;  // one pass reads and writes each row once
     }
     hipGraphExec_t ex = nullptr;
     if (!cnt || hipGraphInstantiate(&ex, sub, nullptr, nullptr, 0) != hipSuccess) {
