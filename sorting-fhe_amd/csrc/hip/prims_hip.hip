@@ -241,6 +241,10 @@ struct sfp_conv {
     std::vector<uint32_t> hsrc, hdst;
     std::vector<uint32_t> hrow;  // dst_row
     std::vector<u64> hinv, hmod; // host copies (ModUpPlan)
+    // the fused ModDown COL pass's tables (k_moddown_col, built on first use):
+    // mod[i][t] as a double and / q_t over every target, prod(S) mod q_t likewise
+    double *mdD = nullptr, *mdQ = nullptr, *mdSpD = nullptr, *mdSpQ = nullptr;
+    int mdState = 0;  // 0 not built, 1 built, -1 not eligible
 };
 
 struct ModUpPlan {
@@ -808,6 +812,11 @@ struct RowGroup {
     // source factor) instead of n^-1; FP64 rows are stored as doubles
     const u64 *postK, *postKS;
     const double *postD, *postQ;
+    // ModDown's conversion fused into the forward COL pass (k_moddown_col):
+    // the per-level table (device); the call's rows ride in fields the
+    // forward pass's first half otherwise uses: copy = the K source (P) rows
+    // of polynomial p, coefficient form; pre = its dropped row l (with rescale)
+    const struct MdColArgs* md;
 };
 
 // Merged launches (stacked regions, batched ops; sfp_stack_begin /
@@ -2939,6 +2948,280 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
     }
 }
 
+// ModDown's conversion -- and the rescale fused with it -- in the forward
+// COL pass of its output rows (sfp_moddown2 / sfp_moddown_rescale, ring
+// 2^16).  The INTT of the P rows (and the rescale's dropped row) folds the
+// conversion's factors (P/p_i)^-1 into its last pass and stores its FP64 rows
+// as doubles (mdPost), so y_i = x_i (P/p_i)^-1 mod p_i arrives ready to be
+// centred.  A block owns one COL tile of kModdownTg target rows t of one
+// polynomial: it reads that tile of each of the K y rows (L2 hits for every
+// target group after the first), centres them, and accumulates as it goes each
+// FP64 target's conversion sum, the overflow v = rint(sum_i y_i / p_i) and,
+// with the rescale, the dropped row's conversion; then r = (a_l - conv_l)
+// P^-1 mod q_l (centred), and each target's tile
+//   y_t = conv_t - v [P]_t (+ [r]_t pmod_t)
+// runs its COL rounds in LDS and is stored.  The converted rows are never
+// written and read back, and k_mdrsf / k_convf's ModDown launch is gone.
+// The same integers as those kernels (exact FP64 sums of fpMulMod residues;
+// the integer row q_0 in 128-bit sums of canonical y), so the same outputs.
+struct MdColArgs {
+    const uint32_t* sidx;       // source primes [ns]
+    const double *invD, *invQ;  // [ns]: the table's inv_i as a double, / p_i
+    const double *mD, *mQ;      // [ns][nt]: mod[i][t] as a double, / q_t
+    const u64* mI;              // [ns][nt]: mod[i][t] (the integer target)
+    const u64* sprod;           // [nt]: prod(P) mod q_t
+    const double *spD, *spQ;    // [nt]: as a double, / q_t
+    const u64 *pmod, *lsub;     // rescale [l]: pmod_t, q_l mod q_t
+    const double *pmD, *pmQ;    // rescale [l]: pmod_t as a double, / q_t
+    u64 pinvl;                  // rescale: P^-1 mod q_l
+    uint32_t ns, nt, l, rs;     // rs: with the rescale (targets t < l)
+};
+#ifndef SFHE_MODDOWN_TG
+#define SFHE_MODDOWN_TG 4
+#endif
+constexpr int kModdownTg = SFHE_MODDOWN_TG;
+
+// a source word as the INTT left it (the conversion's factor folded into its
+// last pass: a canonical residue stored as a double) -> the centred y_i
+__device__ __forceinline__ double mdCentred(u64 bits, double q, double half) {
+    const double y = __longlong_as_double(bits);
+    return y > half ? y - q : y;
+}
+
+template <int TILE, int NG, int TG>
+__global__ __launch_bounds__(TILE >> 2) void k_moddown_col(const RowGroupSet<NG> GS, const sf_barrett* __restrict__ bar,
+                                                           const u64* __restrict__ tw, const u64* __restrict__ twS,
+                                                           const u64* __restrict__, const u64* __restrict__,
+                                                           uint32_t logn, const double* __restrict__ twD,
+                                                           const double* __restrict__ qinvD,
+                                                           const double* __restrict__, const double* __restrict__, int,
+                                                           const double* __restrict__) {
+    constexpr int LE = 2, NT = TILE >> LE, NPAIR = (1 << LE) / 2, W4 = 2 * NPAIR;
+    __shared__ u64 s[TILE];
+    __shared__ u64 tW[kNttColTw], tX[kNttColTw];
+    const uint32_t n = 1u << logn;
+    const uint32_t logR = logn - 8;  // (8: ring 2^16, checked on the host)
+    uint32_t rid;
+    const RowGroup& G = GS.a[argSel(GS, rid)];
+    const MdColArgs& A = *G.md;
+    const uint32_t RG = (G.R + TG - 1) / TG;
+    const uint32_t pp = rid / RG, g0 = (rid % RG) * TG;
+    NttTile T;
+    T.logn = logn;
+    T.d = logR;
+    T.logC = (uint32_t)__builtin_ctz(TILE) - logR;
+    T.C = 1u << T.logC;
+    const uint32_t tile = (gridDim.x & 7) ? blockIdx.x : (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    T.c0 = tile * T.C;
+    T.r0 = 0;
+    auto tileOff = [&](int k) -> size_t {
+        const uint32_t e = 2 * (threadIdx.x + k * NT);
+        return (size_t)(e >> T.logC) * 256 + T.c0 + (e & (T.C - 1));
+    };
+    const uint32_t ns = A.ns, nt = A.nt, l = A.l;
+    const bool rs = A.rs != 0;
+    bool live[TG];
+    uint32_t prime[TG];
+    double qd[TG], qi[TG];
+    bool fpT[TG];
+#pragma unroll
+    for (int u = 0; u < TG; ++u) {
+        live[u] = g0 + u < G.R;
+        prime[u] = primeOf(G.pm, min(g0 + u, G.R - 1));
+        const u64 q = bar[prime[u]].q;
+        fpT[u] = q < kFpPrimeBound;
+        qd[u] = (double)q;
+        qi[u] = qinvD[prime[u]];
+    }
+    const double qld = rs ? (double)bar[l].q : 1.0;
+    double acc[TG][W4], vacc[W4], cacc[W4];
+#pragma unroll
+    for (int w = 0; w < W4; ++w) {
+        vacc[w] = 0.0;
+        cacc[w] = 0.0;
+#pragma unroll
+        for (int u = 0; u < TG; ++u) acc[u][w] = 0.0;
+    }
+    constexpr int GRP = 4;  // source tiles in flight together
+    for (uint32_t s0 = 0; s0 < ns; s0 += GRP) {
+        ulonglong2 v[GRP][NPAIR];
+#pragma unroll
+        for (int g = 0; g < GRP; ++g)
+            if (s0 + g < ns)
+#pragma unroll
+                for (int k = 0; k < NPAIR; ++k)
+                    v[g][k] = *reinterpret_cast<const ulonglong2*>(rowAt(G.copy, pp, s0 + g) + tileOff(k));
+#pragma unroll
+        for (int g = 0; g < GRP; ++g) {
+            const uint32_t sI = s0 + g;
+            if (sI >= ns) break;
+            const uint32_t pi = A.sidx[sI];
+            const double sq = (double)bar[pi].q, sqi = qinvD[pi], half = 0.5 * (sq - 1.0);
+            double y[W4];
+#pragma unroll
+            for (int k = 0; k < NPAIR; ++k) {
+                y[2 * k] = mdCentred(v[g][k].x, sq, half);
+                y[2 * k + 1] = mdCentred(v[g][k].y, sq, half);
+            }
+            const size_t mrow = (size_t)sI * nt;
+#pragma unroll
+            for (int w = 0; w < W4; ++w) vacc[w] = fma(y[w], sqi, vacc[w]);  // (k_mdrsf's order: i ascending)
+            if (rs) {
+                const double md = A.mD[mrow + l], mq = A.mQ[mrow + l];
+#pragma unroll
+                for (int w = 0; w < W4; ++w) cacc[w] += fpMulMod(y[w], md, mq, qld);
+            }
+#pragma unroll
+            for (int u = 0; u < TG; ++u) {
+                if (!live[u] || !fpT[u]) continue;
+                const double md = A.mD[mrow + g0 + u], mq = A.mQ[mrow + g0 + u];
+#pragma unroll
+                for (int w = 0; w < W4; ++w) acc[u][w] += fpMulMod(y[w], md, mq, qd[u]);
+            }
+        }
+    }
+    double vv[W4], rr[W4];
+#pragma unroll
+    for (int w = 0; w < W4; ++w) {
+        vv[w] = rint(vacc[w]);
+        rr[w] = 0.0;
+    }
+    if (rs) {  // the dropped row: r = (a_l - conv_l) P^-1 mod q_l, centred
+        const u64* al = rowAt(G.pre, pp, 0);
+        const double spl = (double)A.sprod[l], qli = qinvD[l], pl = (double)A.pinvl;
+#pragma unroll
+        for (int k = 0; k < NPAIR; ++k) {
+            const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(al + tileOff(k));
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int w = 2 * k + h;
+                const double cl = fpMulMod(-vv[w], spl, spl / qld, qld) + cacc[w];
+                const double av = __longlong_as_double(h ? a.y : a.x);
+                rr[w] = fpSourceY((u64)fpReduce(av - fpReduce(cl, qld, qli), qld, qli), qld, pl, pl / qld, qli, true);
+            }
+        }
+    }
+    constexpr int kColPer = (int)((kNttColTw + NT - 1) / NT);
+    const uint32_t colTw = (1u << logR) - 1;
+    bool first = true;
+    // FP64 targets first (their sums die there), then the integer row, whose
+    // 128-bit sums then do not share registers with them
+#pragma unroll
+    for (int ph = 0; ph < 2; ++ph)
+#pragma unroll
+    for (int u = 0; u < TG; ++u) {
+        if (!live[u] || fpT[u] != (ph == 0)) continue;
+        const uint32_t t = g0 + u, pr = prime[u];
+        const bool fp = ph == 0;
+        const u64 q = bar[pr].q;
+        ulonglong2 xr[NPAIR];
+        if (fp) {
+            const double spd = A.spD[t], spq = A.spQ[t];
+            const double pmd = rs ? A.pmD[t] : 0.0, pmq = rs ? A.pmQ[t] : 0.0;
+#pragma unroll
+            for (int k = 0; k < NPAIR; ++k) {
+                double a0 = acc[u][2 * k] + fpMulMod(-vv[2 * k], spd, spq, qd[u]);
+                double a1 = acc[u][2 * k + 1] + fpMulMod(-vv[2 * k + 1], spd, spq, qd[u]);
+                if (rs) {
+                    a0 += fpMulMod(rr[2 * k], pmd, pmq, qd[u]);
+                    a1 += fpMulMod(rr[2 * k + 1], pmd, pmq, qd[u]);
+                }
+                xr[k].x = __double_as_longlong(fpReduce(a0, qd[u], qi[u]));
+                xr[k].y = __double_as_longlong(fpReduce(a1, qd[u], qi[u]));
+            }
+        } else {  // the integer row (q_0): 128-bit sums of the canonical y, sources re-read (L2)
+            const sf_barrett CB = loadBar(bar, pr);
+            Acc a2[W4];
+            long long neg[W4];
+#pragma unroll
+            for (int w = 0; w < W4; ++w) {
+                a2[w] = Acc{0, 0};
+                neg[w] = (long long)vv[w];
+            }
+            for (uint32_t sI = 0; sI < ns; ++sI) {
+                const uint32_t pi = A.sidx[sI];
+                const double sq = (double)bar[pi].q, half = 0.5 * (sq - 1.0);
+                const u64 m = A.mI[(size_t)sI * nt + t];
+#pragma unroll
+                for (int k = 0; k < NPAIR; ++k) {
+                    const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(rowAt(G.copy, pp, sI) + tileOff(k));
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const double yc = __longlong_as_double(h ? v.y : v.x);  // canonical
+                        macc(a2[2 * k + h], (u64)yc, m);
+                        neg[2 * k + h] += yc > half;
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < NPAIR; ++k) {
+                u64 o[2];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int w = 2 * k + h;
+                    u64 out = subMultiple(sf_reduce128_acc(a2[w].lo, a2[w].hi, &CB), neg[w], A.sprod[t], CB);
+                    if (rs) {
+                        const double r = rr[w];
+                        u64 lift = sf_reduce128((u64)(r < 0.0 ? r + qld : r), 0, &CB);
+                        if (r < 0.0) lift = sf_sub(lift, A.lsub[t], CB.q);
+                        out = sf_add(out, bmul(lift, A.pmod[t], CB), CB.q);
+                    }
+                    o[h] = out;
+                }
+                xr[k].x = o[0];
+                xr[k].y = o[1];
+            }
+        }
+        // the pass's twiddles for this prime, the tile -> LDS (as k_modup_col)
+        const u64* gwI = tw + (size_t)pr * n;
+        const u64* gwD = reinterpret_cast<const u64*>(twD) + (size_t)pr * n;
+        const u64* gx = twS + (size_t)pr * n;
+        if (!first) __syncthreads();  // the previous target's readers are done with s / tW
+        first = false;
+#pragma unroll
+        for (int c = 0; c < kColPer; ++c) {
+            const uint32_t e = threadIdx.x + c * NT;
+            if (e < colTw) {
+                tW[e] = fp ? gwD[e + 1] : gwI[e + 1];
+                if (!fp) tX[e] = gx[e + 1];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < NPAIR; ++k) {
+            const uint32_t e = 2 * (threadIdx.x + k * NT);
+            s[ldsSw(e)] = xr[k].x;
+            s[ldsSw(e + 1)] = xr[k].y;
+        }
+        __syncthreads();
+        if (fp) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                nttRoundFP<false, true, 2, 2, TILE, false, 8>(reinterpret_cast<double*>(s), T, 0u, 2 * r, qd[u],
+                                                              reinterpret_cast<const double*>(tW), qi[u]);
+                __syncthreads();
+            }
+        } else {
+            for (uint32_t r = 0; r < 4; ++r) {
+                nttRoundDyn<false, true, LE, TILE>(2, s, T, 0u, LE * r, q, tW, tX);
+                __syncthreads();
+            }
+        }
+        u64* out = rowAt(G.dst, pp, t);
+#pragma unroll
+        for (int k = 0; k < NPAIR; ++k) {
+            const uint32_t e = 2 * (threadIdx.x + k * NT);
+            ulonglong2 x;
+            x.x = s[ldsSw(e)];
+            x.y = s[ldsSw(e + 1)];
+            if (fp) {
+                x.x = d2u(fpReduce(__longlong_as_double(x.x), qd[u], qi[u]));
+                x.y = d2u(fpReduce(__longlong_as_double(x.y), qd[u], qi[u]));
+            }
+            *reinterpret_cast<ulonglong2*>(out + tileOff(k)) = x;
+        }
+    }
+}
+
 // prims.h sfp_key_row on the device
 __device__ __forceinline__ uint32_t keyRowOf(const sfp_key_geom& g, uint32_t p) {
     if (!g.rows) return p;
@@ -4179,7 +4462,30 @@ static void nttRows(sfp_dev* d, const RowGroup& G0, int inverse, int passes = 3)
         const char* v = std::getenv("SFHE_MODUP_COL");
         return !v || *v != '0';
     }();
-    if (G.cy && modupCol && !inverse && d->logn == 16 && smallTile == 1024 && L == 2) {
+    if (G.md) {
+        // ModDown (mdColArgs): its conversion + the COL pass, kModdownTg targets per block
+        if (inverse || d->logn != 16 || smallTile != 1024 || L != 2 || passes != 3) {
+            record(d, "ntt: fused ModDown pass outside its shape", hipErrorInvalidValue);
+            return;
+        }
+        constexpr int TG = kModdownTg;
+        g.y = G.P * ((G.R + TG - 1) / TG);
+        gridRows = g.y;
+        if (t1k)
+            pass(k_moddown_col<1024, 1, TG>, k_moddown_col<1024, 2, TG>, k_moddown_col<1024, 4, TG>,
+                 k_moddown_col<1024, 8, TG>, 1024 >> 2);
+        else
+            pass(k_moddown_col<T, 1, TG>, k_moddown_col<T, 2, TG>, k_moddown_col<T, 4, TG>, k_moddown_col<T, 8, TG>,
+                 T >> 2);
+        g.y = rows;
+        gridRows = rows;
+        if (t1k)
+            pass(k_ntt<false, false, 2, 1024>, k_ntt<false, false, 2, 1024, 2>, k_ntt<false, false, 2, 1024, 4>,
+                 k_ntt<false, false, 2, 1024, 8>, 1024 >> 2);
+        else
+            pass(k_ntt<false, false, 2, T>, k_ntt<false, false, 2, T, 2>, k_ntt<false, false, 2, T, 4>,
+                 k_ntt<false, false, 2, T, 8>, T >> 2);
+    } else if (G.cy && modupCol && !inverse && d->logn == 16 && smallTile == 1024 && L == 2) {
         // ModUpPlan at ring 2^16: the conversion + COL pass, kModupTg targets per block
         constexpr int TG = kModupTg;
         g.y = G.P * ((G.R + TG - 1) / TG);
@@ -4391,6 +4697,11 @@ static uint32_t kernelFamily(const void* f) {
                               (const void*)k_modup_col<1024, 1, kModupTg>, (const void*)k_modup_col<1024, 2, kModupTg>,
                               (const void*)k_modup_col<1024, 4, kModupTg>, (const void*)k_modup_col<1024, 8, kModupTg>})
             m[k] = SFP_FAM_NTT;
+        for (const void* k : {(const void*)k_moddown_col<kNttTile, 1, kModdownTg>, (const void*)k_moddown_col<kNttTile, 2, kModdownTg>,
+                              (const void*)k_moddown_col<kNttTile, 4, kModdownTg>, (const void*)k_moddown_col<kNttTile, 8, kModdownTg>,
+                              (const void*)k_moddown_col<1024, 1, kModdownTg>, (const void*)k_moddown_col<1024, 2, kModdownTg>,
+                              (const void*)k_moddown_col<1024, 4, kModdownTg>, (const void*)k_moddown_col<1024, 8, kModdownTg>})
+            m[k] = SFP_FAM_NTT;
         addNttAll<2, 1024>(m, true);
         addNttAll<2, 512>(m, true);
         addNttAll<3, kNttTile>(m, false);
@@ -4415,33 +4726,40 @@ static uint32_t kernelFamily(const void* f) {
     return it == fam.end() ? (uint32_t)SFP_FAM_COUNT : it->second;
 }
 
-// Rows an NTT-family node transforms: its grid rows, except k_modup_col's
-// (groups of kModupTg target rows, the digits' own rows skipped), read from
-// its argument set.
+// An NTT-family node's algorithmic bytes in rows of 16n bytes (one row read
+// and written): its grid rows, except for the fused conversion passes, read
+// from their argument sets, which read their sources once and write their
+// targets once -- k_modup_col: per digit its own rows in, the other R - own
+// rows out (R / 2 rows of 16n); k_moddown_col: per polynomial the cRows
+// source rows (K P rows, + the dropped row with the rescale) in, R rows out.
 template <int NG>
-static double modupColRows(const void* arg) {
+static double fusedColRows(const void* arg, bool moddown) {
     const auto& S = *static_cast<const RowGroupSet<NG>*>(arg);
     double r = 0;
     for (int i = 0; i < NG; ++i) {
         const RowGroup& G = S.a[i];
-        for (uint32_t p = 0; p < G.P; ++p) {
-            const uint32_t o0 = p * G.alpha, o1 = std::min(o0 + G.alpha, G.skipEll);
-            r += G.R - (o1 > o0 ? o1 - o0 : 0);
-        }
+        r += moddown ? 0.5 * G.P * (G.R + G.cRows) : 0.5 * G.P * G.R;
     }
     return r;
 }
 static double nttNodeRows(const hipKernelNodeParams& kp) {
     const void* f = kp.func;
     if (kp.kernelParams) {
-        if (f == (const void*)k_modup_col<kNttTile, 1, kModupTg> || f == (const void*)k_modup_col<1024, 1, kModupTg>)
-            return modupColRows<1>(kp.kernelParams[0]);
-        if (f == (const void*)k_modup_col<kNttTile, 2, kModupTg> || f == (const void*)k_modup_col<1024, 2, kModupTg>)
-            return modupColRows<2>(kp.kernelParams[0]);
-        if (f == (const void*)k_modup_col<kNttTile, 4, kModupTg> || f == (const void*)k_modup_col<1024, 4, kModupTg>)
-            return modupColRows<4>(kp.kernelParams[0]);
-        if (f == (const void*)k_modup_col<kNttTile, 8, kModupTg> || f == (const void*)k_modup_col<1024, 8, kModupTg>)
-            return modupColRows<8>(kp.kernelParams[0]);
+        for (bool md : {false, true}) {
+            auto is = [&](auto k2048, auto k1024) { return f == (const void*)k2048 || f == (const void*)k1024; };
+            if (md ? is(k_moddown_col<kNttTile, 1, kModdownTg>, k_moddown_col<1024, 1, kModdownTg>)
+                   : is(k_modup_col<kNttTile, 1, kModupTg>, k_modup_col<1024, 1, kModupTg>))
+                return fusedColRows<1>(kp.kernelParams[0], md);
+            if (md ? is(k_moddown_col<kNttTile, 2, kModdownTg>, k_moddown_col<1024, 2, kModdownTg>)
+                   : is(k_modup_col<kNttTile, 2, kModupTg>, k_modup_col<1024, 2, kModupTg>))
+                return fusedColRows<2>(kp.kernelParams[0], md);
+            if (md ? is(k_moddown_col<kNttTile, 4, kModdownTg>, k_moddown_col<1024, 4, kModdownTg>)
+                   : is(k_modup_col<kNttTile, 4, kModupTg>, k_modup_col<1024, 4, kModupTg>))
+                return fusedColRows<4>(kp.kernelParams[0], md);
+            if (md ? is(k_moddown_col<kNttTile, 8, kModdownTg>, k_moddown_col<1024, 8, kModdownTg>)
+                   : is(k_modup_col<kNttTile, 8, kModupTg>, k_modup_col<1024, 8, kModupTg>))
+                return fusedColRows<8>(kp.kernelParams[0], md);
+        }
     }
     return (double)kp.gridDim.y;
 }
@@ -4857,6 +5175,29 @@ sfp_conv* sfp_upload_conv(sfp_dev* d, uint32_t ns, const uint32_t* src, uint32_t
     up(c->vQ, vQ);
     up(c->hD, hD);
     up(c->hQ, hQ);
+    // a ModDown table (every source FP64, target t on prime t and row t): the
+    // fused COL pass's multipliers over every target (k_moddown_col)
+    bool mdOk = c->nbig == 0;
+    for (uint32_t t = 0; t < nt && mdOk; ++t) mdOk = dst[t] == t && rows[t] == t;
+    if (mdOk) {
+        std::vector<double> mD((size_t)ns * nt), mQ((size_t)ns * nt), spD(nt), spQ(nt);
+        for (uint32_t t = 0; t < nt; ++t) {
+            const double q = (double)d->hbar[t].q;
+            for (uint32_t i = 0; i < ns; ++i) {
+                mD[(size_t)i * nt + t] = (double)mod[(size_t)i * nt + t];
+                mQ[(size_t)i * nt + t] = mD[(size_t)i * nt + t] / q;
+            }
+            spD[t] = (double)sp[t];
+            spQ[t] = spD[t] / q;
+        }
+        up(c->mdD, mD);
+        up(c->mdQ, mQ);
+        up(c->mdSpD, spD);
+        up(c->mdSpQ, spQ);
+        c->mdState = ok ? 1 : -1;
+    } else {
+        c->mdState = -1;
+    }
     if (!ok) {
         record(d, "upload_conv allocation", hipErrorOutOfMemory);
         sfp_free_conv(d, c);
@@ -4886,7 +5227,7 @@ void sfp_free_conv(sfp_dev* d, sfp_conv* c) {
     hipFree(c->fpT);
     hipFree(c->intT);
     hipFree(c->allT);
-    for (double* x : {c->invD, c->invQ, c->vD, c->vQ, c->hD, c->hQ}) hipFree(x);
+    for (double* x : {c->invD, c->invQ, c->vD, c->vQ, c->hD, c->hQ, c->mdD, c->mdQ, c->mdSpD, c->mdSpQ}) hipFree(x);
     delete c;
 }
 
@@ -5327,6 +5668,84 @@ void sfp_ks_inner_mul(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t
     checkLaunch(d, "ks_inner_mul");
 }
 
+// The fused ModDown COL pass (k_moddown_col): ring 2^16 with the default NTT
+// shape (LE 2, 1024-word small tiles), a ModDown table (every source FP64,
+// target t on prime t; sfp_upload_conv), with the rescale its dropped prime
+// FP64 too.  Returns the call's device table (constant arena), or null: the
+// unfused launches run.  Off by default (SFHE_MODDOWN_COL=1 turns it on): A/B
+// x2 on one box, the metric sort 40.0-40.3 ms fused at every level and
+// 38.7-39.0 up to 16 target rows, against 38.7 unfused.
+static bool moddownColOn() {
+    static const bool on = [] {
+        const char* v = std::getenv("SFHE_MODDOWN_COL");
+        return v && *v == '1';
+    }();
+    return on;
+}
+// A (the INTT of the P rows, after the rescale's dropped row l) gets the
+// conversion's factors in its last pass: row of prime p_i -> n^-1 (P/p_i)^-1,
+// row l -> n^-1; its FP64 rows are stored as doubles.
+static const MdColArgs* mdColArgs(sfp_dev* d, const sfp_conv* c, uint32_t targets, bool rs, uint32_t l, uint32_t Lq,
+                                  const u64* pmod, const u64* lsub, u64 pinvl, RowGroup& A) {
+    if (!moddownColOn() || !nttFp() || d->logn != 16 || nttSmallLe() != 2 || nttSmallTile() != 1024 ||
+        (nttLe() != 0 && nttLe() != 2) || c->mdState != 1 || c->ns > (uint32_t)kMaxConvSrc)
+        return nullptr;
+    static const uint32_t maxT = [] {  // SFHE_MODDOWN_COL_MAXT: fused up to this many target rows (A/B)
+        const char* v = std::getenv("SFHE_MODDOWN_COL_MAXT");
+        return v ? (uint32_t)std::atoi(v) : 1024u;
+    }();
+    if (targets > maxT) return nullptr;
+    if (targets > c->nt || (rs && (l >= c->nt || d->hbar[l].q >= kFpPrimeBound))) return nullptr;
+    for (uint32_t i = 0; i < c->ns; ++i)
+        if (c->hsrc[i] != Lq + i) return nullptr;  // (A's rows: the P primes in order)
+    const uint32_t rows = c->ns + (rs ? 1u : 0u);
+    u64 pk[SFP_MAX_LIMBS], pks[SFP_MAX_LIMBS];
+    double pd[SFP_MAX_LIMBS], pq[SFP_MAX_LIMBS];
+    for (uint32_t r = 0; r < rows; ++r) {
+        const bool dropped = rs && r == 0;
+        const uint32_t pr = dropped ? l : c->hsrc[r - (rs ? 1 : 0)];
+        const sf_barrett& B = d->hbar[pr];
+        const u64 k = dropped ? d->hninv[pr] % B.q : sf_mul(c->hinv[r - (rs ? 1 : 0)] % B.q, d->hninv[pr] % B.q, &B);
+        pk[r] = k;
+        pks[r] = sf_shoup_precomp(k, B.q);
+        pd[r] = (double)k;
+        pq[r] = (double)k / (double)B.q;
+    }
+    A.postK = devConst(d, pk, rows);
+    A.postKS = devConst(d, pks, rows);
+    A.postD = reinterpret_cast<const double*>(devConst(d, reinterpret_cast<const u64*>(pd), rows));
+    A.postQ = reinterpret_cast<const double*>(devConst(d, reinterpret_cast<const u64*>(pq), rows));
+    MdColArgs a;
+    std::memset(&a, 0, sizeof a);
+    a.sidx = c->src;
+    a.invD = c->invD;
+    a.invQ = c->invQ;
+    a.mD = c->mdD;
+    a.mQ = c->mdQ;
+    a.mI = c->mod;
+    a.sprod = c->sprod;
+    a.spD = c->mdSpD;
+    a.spQ = c->mdSpQ;
+    a.ns = c->ns;
+    a.nt = c->nt;
+    a.l = l;
+    a.rs = rs ? 1u : 0u;
+    if (rs) {
+        double pd[SFP_MAX_LIMBS], pq[SFP_MAX_LIMBS];
+        for (uint32_t i = 0; i < l; ++i) {
+            pd[i] = (double)pmod[i];
+            pq[i] = (double)pmod[i] / (double)d->hbar[i].q;
+        }
+        a.pmod = devConst(d, pmod, l);
+        a.lsub = devConst(d, lsub, l);
+        a.pmD = reinterpret_cast<const double*>(devConst(d, reinterpret_cast<const u64*>(pd), l));
+        a.pmQ = reinterpret_cast<const double*>(devConst(d, reinterpret_cast<const u64*>(pq), l));
+        a.pinvl = pinvl;
+    }
+    static_assert(sizeof(MdColArgs) % 8 == 0, "MdColArgs in 8-byte words");
+    return reinterpret_cast<const MdColArgs*>(devConst(d, reinterpret_cast<const u64*>(&a), sizeof a / 8));
+}
+
 void sfp_moddown2(sfp_dev* d, uint64_t* out0, uint64_t* out1, uint64_t* acc, size_t accStride,
                   uint32_t ell, uint32_t K, uint32_t Lq, const sfp_conv* c, const uint64_t* pinv,
                   int add0, int add1, uint64_t* scr, int rowDone) {
@@ -5338,13 +5757,21 @@ void sfp_moddown2(sfp_dev* d, uint64_t* out0, uint64_t* out1, uint64_t* acc, siz
     u64* pRows = acc + (size_t)ell * n;
     RowGroup A = rowsOf(2, K, sfp_limbs{K, 0, Lq, 0});
     A.src = A.dst = RowPtr{pRows, (long long)accStride, (long long)n};
+    const MdColArgs* md = mdColArgs(d, c, ell, false, 0, Lq, nullptr, nullptr, 0, A);
     nttRows(d, A, 1, rowDone ? 2 : 3);
-    ConvJobs J;
-    J.j[0] = convJob(c, scr, pRows, ell, 1);
-    J.j[1] = convJob(c, scr + (size_t)ell * n, pRows + accStride, ell, 1);
-    convLaunch(d, J, 2, c->fpOk);
+    if (!md) {
+        ConvJobs J;
+        J.j[0] = convJob(c, scr, pRows, ell, 1);
+        J.j[1] = convJob(c, scr + (size_t)ell * n, pRows + accStride, ell, 1);
+        convLaunch(d, J, 2, c->fpOk);
+    }
     RowGroup B = rowsOf(2, ell, sfp_limbs{ell, ell, 0, 0});
     B.src = B.dst = RowPtr{scr, (long long)ell * n, (long long)n};
+    if (md) {  // the conversion in the forward COL pass (k_moddown_col)
+        B.md = md;
+        B.copy = RowPtr{pRows, (long long)accStride, (long long)n};
+        B.cRows = c->ns;  // (source rows per polynomial: graph byte accounting)
+    }
     B.epi = 1;
     B.addMask = (add0 ? 1u : 0u) | (add1 ? 2u : 0u);
     B.ein = RowPtr{acc, (long long)accStride, (long long)n};
@@ -5371,7 +5798,6 @@ static void moddownRescaleCore(sfp_dev* d, uint64_t* out0, uint64_t* out1, const
     // INTT of rows [l, ell+K) of both accumulators: the dropped q row and the P rows
     RowGroup A = rowsOf(2, K + 1, sfp_limbs{K + 1, 1, Lq, l});
     A.src = A.dst = RowPtr{acc + (size_t)l * n, (long long)accStride, (long long)n};
-    nttRows(d, A, 1, rowDone ? 2 : 3);
     // conversion + the dropped row's lift
     MdrsArgs M;
     std::memset(&M, 0, sizeof M);  // (stacked launches compare it bytewise)
@@ -5388,81 +5814,91 @@ static void moddownRescaleCore(sfp_dev* d, uint64_t* out0, uint64_t* out1, const
         k1S[i] = sf_shoup_precomp(k1[i], q);
         k2S[i] = sf_shoup_precomp(qlinv[i], q);
     }
-    M.sidx = c->src;
-    M.inv = c->inv;
-    M.mod = c->mod;
-    M.sprod = c->sprod;
-    M.pmod = devConst(d, pmod, l);
-    M.lsub = devConst(d, lsub, l);
-    M.pinvl = pinv[l];
-    M.ns = c->ns;
-    M.nt = c->nt;
-    M.l = l;
-    // FP64 form: every source (P row) and the dropped row's prime FP64
-    const auto lpos = std::lower_bound(c->hFpT.begin(), c->hFpT.end(), l);
-    const bool fp = nttFp() && c->fpOk && c->nbig == 0 && lpos != c->hFpT.end() && *lpos == l;
-    uint32_t zc = (l + kConvChunk - 1) / kConvChunk;
-    if (fp) {
-        M.fpT = c->fpT;
-        M.intT = c->intT;
-        M.invD = c->invD;
-        M.invQ = c->invQ;
-        M.vD = c->vD;
-        M.vQ = c->vQ;
-        M.nFpAll = (uint32_t)c->hFpT.size();
-        M.lD = c->vD + (lpos - c->hFpT.begin());
-        M.lQ = c->vQ + (lpos - c->hFpT.begin());
-        M.nFp = (uint32_t)(lpos - c->hFpT.begin());
-        M.nInt = (uint32_t)(std::lower_bound(c->hIntT.begin(), c->hIntT.end(), l) - c->hIntT.begin());
-        double pd[SFP_MAX_LIMBS], pq[SFP_MAX_LIMBS];
-        for (uint32_t i = 0; i < l; ++i) {
-            pd[i] = (double)pmod[i];
-            pq[i] = (double)pmod[i] / (double)d->hbar[i].q;
+    const MdColArgs* md = mdColArgs(d, c, l, true, l, Lq, pmod, lsub, pinv[l], A);
+    nttRows(d, A, 1, rowDone ? 2 : 3);
+    if (!md) {
+        M.sidx = c->src;
+        M.inv = c->inv;
+        M.mod = c->mod;
+        M.sprod = c->sprod;
+        M.pmod = devConst(d, pmod, l);
+        M.lsub = devConst(d, lsub, l);
+        M.pinvl = pinv[l];
+        M.ns = c->ns;
+        M.nt = c->nt;
+        M.l = l;
+        // FP64 form: every source (P row) and the dropped row's prime FP64
+        const auto lpos = std::lower_bound(c->hFpT.begin(), c->hFpT.end(), l);
+        const bool fp = nttFp() && c->fpOk && c->nbig == 0 && lpos != c->hFpT.end() && *lpos == l;
+        uint32_t zc = (l + kConvChunk - 1) / kConvChunk;
+        if (fp) {
+            M.fpT = c->fpT;
+            M.intT = c->intT;
+            M.invD = c->invD;
+            M.invQ = c->invQ;
+            M.vD = c->vD;
+            M.vQ = c->vQ;
+            M.nFpAll = (uint32_t)c->hFpT.size();
+            M.lD = c->vD + (lpos - c->hFpT.begin());
+            M.lQ = c->vQ + (lpos - c->hFpT.begin());
+            M.nFp = (uint32_t)(lpos - c->hFpT.begin());
+            M.nInt = (uint32_t)(std::lower_bound(c->hIntT.begin(), c->hIntT.end(), l) - c->hIntT.begin());
+            double pd[SFP_MAX_LIMBS], pq[SFP_MAX_LIMBS];
+            for (uint32_t i = 0; i < l; ++i) {
+                pd[i] = (double)pmod[i];
+                pq[i] = (double)pmod[i] / (double)d->hbar[i].q;
+            }
+            M.pmodD = reinterpret_cast<const double*>(devConst(d, reinterpret_cast<const u64*>(pd), l));
+            M.pmodQ = reinterpret_cast<const double*>(devConst(d, reinterpret_cast<const u64*>(pq), l));
+            zc = (M.nFp + kConvChunk - 1) / kConvChunk + (M.nInt + kConvChunk - 1) / kConvChunk;
         }
-        M.pmodD = reinterpret_cast<const double*>(devConst(d, reinterpret_cast<const u64*>(pd), l));
-        M.pmodQ = reinterpret_cast<const double*>(devConst(d, reinterpret_cast<const u64*>(pq), l));
-        zc = (M.nFp + kConvChunk - 1) / kConvChunk + (M.nInt + kConvChunk - 1) / kConvChunk;
-    }
-    // the dropped prime 60-bit, FP64 sources, every target below it an
-    // integer row (scale-59 chains): the integer-l form of k_mdrsf
-    const bool bigl = !fp && nttFp() && c->fpOk && c->nbig == 0 && d->hbar[l].q >= kFpPrimeBound &&
-                      (c->hFpT.empty() || c->hFpT.front() > l);
-    if (bigl) {
-        M.intT = c->intT;
-        M.invD = c->invD;
-        M.invQ = c->invQ;
-        M.nFp = 0;
-        M.nFpAll = (uint32_t)c->hFpT.size();
-        M.nInt = (uint32_t)(std::lower_bound(c->hIntT.begin(), c->hIntT.end(), l) - c->hIntT.begin());
-        zc = (M.nInt + kConvChunk - 1) / kConvChunk;
-    }
-    const dim3 g((fp || bigl) ? n / kConvCoefs : n / (2 * kThreads), 2, zc);
-    timedLaunch(d, SFP_FAM_CONV, 8.0 * n * 2 * (K + 1 + l), [&] {
-        // (fp: LDS for 6 blocks per CU at ns <= 13, as convLaunch)
-        MdrsKern k = (bigl && c->ns <= 13) ? k_mdrsf<13, true>
-                     : (bigl && c->ns <= 16) ? k_mdrsf<16, true>
-                     : bigl                  ? k_mdrsf<kMaxConvSrc, true>
-                     : (fp && c->ns <= 13)   ? k_mdrsf<13>
-                     : (fp && c->ns <= 16)   ? k_mdrsf<16>
-                     : fp                    ? k_mdrsf<kMaxConvSrc>
-                                             : k_conv_mdrs;
-        StackRec r;
-        r.go = [=](hipStream_t s_) { hipLaunchKernelGGL(k, g, dim3(kThreads), 0, s_, M, d->bar, d->qinvD, d->logn); };
-        if (d->stackOn) {
-            auto P = std::make_shared<MdrsPay>();
-            P->M = M;
-            P->g = g;
-            P->k = reinterpret_cast<ConvKern>(k);
-            r.cls = STK_MDRS;
-            r.key = stkKey((const void*)k, g.x, g.z);
-            r.pay = std::move(P);
+        // the dropped prime 60-bit, FP64 sources, every target below it an
+        // integer row (scale-59 chains): the integer-l form of k_mdrsf
+        const bool bigl = !fp && nttFp() && c->fpOk && c->nbig == 0 && d->hbar[l].q >= kFpPrimeBound &&
+                          (c->hFpT.empty() || c->hFpT.front() > l);
+        if (bigl) {
+            M.intT = c->intT;
+            M.invD = c->invD;
+            M.invQ = c->invQ;
+            M.nFp = 0;
+            M.nFpAll = (uint32_t)c->hFpT.size();
+            M.nInt = (uint32_t)(std::lower_bound(c->hIntT.begin(), c->hIntT.end(), l) - c->hIntT.begin());
+            zc = (M.nInt + kConvChunk - 1) / kConvChunk;
         }
-        issueRec(d, std::move(r));
-    });
-    checkLaunch(d, "conv_mdrs");
+        const dim3 g((fp || bigl) ? n / kConvCoefs : n / (2 * kThreads), 2, zc);
+        timedLaunch(d, SFP_FAM_CONV, 8.0 * n * 2 * (K + 1 + l), [&] {
+            // (fp: LDS for 6 blocks per CU at ns <= 13, as convLaunch)
+            MdrsKern k = (bigl && c->ns <= 13) ? k_mdrsf<13, true>
+                         : (bigl && c->ns <= 16) ? k_mdrsf<16, true>
+                         : bigl                  ? k_mdrsf<kMaxConvSrc, true>
+                         : (fp && c->ns <= 13)   ? k_mdrsf<13>
+                         : (fp && c->ns <= 16)   ? k_mdrsf<16>
+                         : fp                    ? k_mdrsf<kMaxConvSrc>
+                                                 : k_conv_mdrs;
+            StackRec r;
+            r.go = [=](hipStream_t s_) { hipLaunchKernelGGL(k, g, dim3(kThreads), 0, s_, M, d->bar, d->qinvD, d->logn); };
+            if (d->stackOn) {
+                auto P = std::make_shared<MdrsPay>();
+                P->M = M;
+                P->g = g;
+                P->k = reinterpret_cast<ConvKern>(k);
+                r.cls = STK_MDRS;
+                r.key = stkKey((const void*)k, g.x, g.z);
+                r.pay = std::move(P);
+            }
+            issueRec(d, std::move(r));
+        });
+        checkLaunch(d, "conv_mdrs");
+    }
     // out_i = (acc_i - NTT(y_i)) (P q_l)^-1 + d_i q_l^-1
     RowGroup B = rowsOf(2, l, sfp_limbs{l, l, 0, 0});
     B.src = B.dst = RowPtr{scr, (long long)l * n, (long long)n};
+    if (md) {  // the conversion and the dropped row's lift in the forward COL pass (k_moddown_col)
+        B.md = md;
+        B.copy = RowPtr{acc + (size_t)ell * n, (long long)accStride, (long long)n};
+        B.pre = RowPtr{acc + (size_t)l * n, (long long)accStride, (long long)n};
+        B.cRows = c->ns + 1;  // (source rows per polynomial: graph byte accounting)
+    }
     B.epi = 1;
     B.ein = RowPtr{acc, (long long)accStride, (long long)n};
     B.eout = RowPtr{out0, (long long)(out1 - out0), (long long)n};

@@ -1,6 +1,7 @@
-"""GPU parity of the NTT kernel's integer path on the rows that normally take
-the FP64 butterflies: SFHE_NTT_FP=0 is read once per process, so
-it runs in a child process that checks encrypt / mult / rotate bit for bit
+"""GPU parity of the NTT kernel variants that are off by default: the integer
+path on the rows that normally take the FP64 butterflies (SFHE_NTT_FP=0) and
+the fused ModDown COL pass (SFHE_MODDOWN_COL=1).  The knobs are
+read once per process, so each runs in a child process that checks encrypt / mult / rotate bit for bit
 against the CPU oracle at ring 2^16 (the measured-and-rejected A/B variants
 of round 2 were removed from k_ntt; their record is DESIGN §4).
 """
@@ -34,7 +35,10 @@ print("variant ok")
 """
 
 
-@pytest.mark.parametrize("env", [{"SFHE_NTT_FP": "0"}], ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
+# SFHE_MODDOWN_COL=1: ModDown's conversion (and the fused rescale's lift) in
+# the forward COL pass, k_moddown_col (measured slower, off by default)
+@pytest.mark.parametrize("env", [{"SFHE_NTT_FP": "0"}, {"SFHE_MODDOWN_COL": "1"}],
+                         ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
 def test_ntt_variant_bitexact(hip_lib, oracle_lib, env):
     child_env = dict(os.environ, **env)
     child_env["PYTHONPATH"] = os.pathsep.join(
