@@ -678,6 +678,11 @@ int sfp_modup_inner_phase(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint
                            ext, scratch);
 }
 
+/* no fused ModUp: nothing to prepare */
+void sfp_modup_prepare(sfp_dev* d, const sfp_conv* const* convs, uint32_t ell, uint32_t K, uint32_t alpha) {
+    (void)d; (void)convs; (void)ell; (void)K; (void)alpha;
+}
+
 /* no fused tensor + relinearisation + rescale: the host layer runs the prims */
 int sfp_mult_relin_rescale(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint64_t* a0, const uint64_t* a1,
                            const uint64_t* b0, const uint64_t* b1, uint32_t ell, uint32_t K, uint32_t Lq,

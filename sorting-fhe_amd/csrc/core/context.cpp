@@ -1988,7 +1988,10 @@ void CryptoContextImpl<DCRTPoly>::EvalMultKeyGen(const PrivateKey<DCRTPoly>& sk)
     // every level's ModUp conversion tables now, as OpenFHE precomputes its
     // CRT tables with the context: built lazily, each upload drained the
     // device inside the first sort
-    for (uint32_t ell = 1; ell <= s->Lq; ++ell) SfheInternal::modupConv(this, ell);
+    // (and the fused ModUp's per-level plans with them: built inside the
+    // first sort they added ~18 ms of drained uploads to the cold sort)
+    for (uint32_t ell = 1; ell <= s->Lq; ++ell)
+        sfp_modup_prepare(s->dev, SfheInternal::modupConv(this, ell).data(), ell, s->K, s->alpha);
 }
 
 void CryptoContextImpl<DCRTPoly>::EvalRotateKeyGen(const PrivateKey<DCRTPoly>& sk,

@@ -5432,6 +5432,11 @@ static const ModUpPlan* modupPlan(sfp_dev* d, const sfp_conv* const* convs, uint
     d->plans[convs[0]] = P;
     return P;
 }
+void sfp_modup_prepare(sfp_dev* d, const sfp_conv* const* convs, uint32_t ell, uint32_t K, uint32_t alpha) {
+    const uint32_t beta = (ell + alpha - 1) / alpha;
+    if (!convs || d->capture || beta > (uint32_t)kMaxConvJobs || ell + K > SFP_MAX_LIMBS) return;
+    modupPlan(d, convs, ell, K, alpha);
+}
 static void planInto(const ModUpPlan* P, RowGroup& A, RowGroup& B, const u64* y) {
     A.postK = P->postK;
     A.postKS = P->postKS;

@@ -203,6 +203,12 @@ int sfp_modup_inner_phase(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint
                           const uint64_t* fold0, const uint64_t* fold1, uint64_t fold_k, int accum,
                           uint32_t inv_from, uint64_t* ext, uint64_t* scratch, int phases);
 
+// Build (and cache) whatever per-level tables the fused ModUp of `ell` limbs
+// needs, outside any sort: the context calls it for every level at key
+// generation (built lazily, each level's upload drained the device inside
+// the first sort).  No-op where no fused form exists (the oracle).
+void sfp_modup_prepare(sfp_dev* d, const sfp_conv* const* convs, uint32_t ell, uint32_t K, uint32_t alpha);
+
 // Key inner product:  acc0 = sum_j ext_j * kb_j,  acc1 = sum_j ext_j * ka_j
 //   ext  : beta extended polys, each (ell+K) limbs, stride ext_stride.
 //   key  : beta digits, each [b rows (Lq+K)][a rows (Lq+K)]; ext limb t maps to
