@@ -2200,6 +2200,10 @@ struct PtrList3 {
 // FP64 rows sum exact fpMulMod residues (|r| < 1.5 q < 2^43, so the up to
 // SFP_MAX_WSUM terms stay below 2^50) and reduce once; the integer row (q_0)
 // sums 128-bit products.  Same canonical outputs either way.
+#ifndef SFHE_MAC_UNROLL
+#define SFHE_MAC_UNROLL 4
+#endif
+constexpr int kMacUnroll = SFHE_MAC_UNROLL;  // terms per step of k_mac_plain2's FP64 loop
 __global__ __launch_bounds__(kThreads) void k_mac_plain2(u64* __restrict__ out0, u64* __restrict__ out1,
                                                          const PtrList3 L, uint32_t nin, sfp_limbs m,
                                                          const sf_barrett* __restrict__ bar, uint32_t logn,
@@ -2222,6 +2226,19 @@ __global__ __launch_bounds__(kThreads) void k_mac_plain2(u64* __restrict__ out0,
                 x1 += fpMulMod(u2d(c.x), px, pxq, qd);
                 y1 += fpMulMod(u2d(c.y), py, pyq, qd);
             };
+            // kMacUnroll terms' 3 kMacUnroll loads in flight together (the
+            // sums are exact integers: any order gives the same residues)
+            for (; j + kMacUnroll <= nin; j += kMacUnroll) {
+                ulonglong2 p[kMacUnroll], a[kMacUnroll], c[kMacUnroll];
+#pragma unroll
+                for (int u = 0; u < kMacUnroll; ++u) {
+                    p[u] = *reinterpret_cast<const ulonglong2*>(L.b[j + u] + e);
+                    a[u] = *reinterpret_cast<const ulonglong2*>(L.a[j + u] + e);
+                    c[u] = *reinterpret_cast<const ulonglong2*>(L.c[j + u] + e);
+                }
+#pragma unroll
+                for (int u = 0; u < kMacUnroll; ++u) term(p[u], a[u], c[u]);
+            }
             for (; j + 2 <= nin; j += 2) {  // two terms' six loads in flight together
                 const ulonglong2 p = *reinterpret_cast<const ulonglong2*>(L.b[j] + e);
                 const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(L.a[j] + e);
@@ -2492,6 +2509,13 @@ template <int NS>
 constexpr int kConvPer = (NS * kConvCoefs + kThreads - 1) / kThreads;
 static_assert(kConvChunk % kConvTpi == 0 && kConvCoefs % 64 == 0 && kConvCoefs <= kThreads, "conversion block shape");
 
+// Integer targets (the 60-bit q_0) folded into the first FP64 chunk's blocks
+// of a job without 60-bit sources: up to kConvIntFold of them (a block of
+// their own repeated phase 1 and added a third of the grid to a ModDown's)
+constexpr uint32_t kConvIntFold = 2;
+__host__ __device__ __forceinline__ bool convIntFolded(uint32_t nbig, uint32_t nFp, uint32_t nInt) {
+    return nbig == 0 && nFp > 0 && nInt <= kConvIntFold;
+}
 template <int NS>
 __global__ __launch_bounds__(kThreads) void k_convf(const ConvJobs J, const sf_barrett* __restrict__ bar,
                                                     const double* __restrict__ qinvD, uint32_t logn) {
@@ -2512,15 +2536,22 @@ __global__ __launch_bounds__(kThreads) void k_convf(const ConvJobs J, const sf_b
     __shared__ double yH[NB * X];  // 60-bit sources' high parts
     __shared__ double vL[X];       // centred: the overflow v of each coefficient
     __shared__ double tSpD[C], tSpQ[C];
+    // the integer targets (q_0) folded into FP64 chunk 0 (convIntFolded)
+    __shared__ u64 iMod[NS * kConvIntFold], iSp[kConvIntFold];
+    __shared__ sf_barrett iB[kConvIntFold];
+    __shared__ uint32_t iRow[kConvIntFold];
     const ConvJob& c = J.j[blockIdx.y];
     const uint32_t fpChunks = (c.nFp + C - 1) / C;
+    const bool fold = convIntFolded(c.nbig, c.nFp, c.nInt);
     const bool fpBlock = blockIdx.z < fpChunks;
+    if (fold && !fpBlock) return;  // (a launch's grid covers its jobs' largest z)
     const uint32_t k0 = (fpBlock ? blockIdx.z : blockIdx.z - fpChunks) * C;
     const uint32_t cnt = fpBlock ? c.nFp : c.nInt;
     if (k0 >= cnt) return;
     const uint32_t tc = min((uint32_t)C, cnt - k0);
     const uint32_t ns = c.ns;
     const uint32_t* tl = fpBlock ? c.fpT : c.intT;
+    const uint32_t ti = (fold && blockIdx.z == 0) ? c.nInt : 0;  // integer targets this block adds
     // the block's source words are issued first (as k_mdrsf)
     const uint32_t x0 = blockIdx.x * X, nsX = ns * X;
     u64 sv[kConvPer<NS>];
@@ -2547,6 +2578,15 @@ __global__ __launch_bounds__(kThreads) void k_convf(const ConvJobs J, const sf_b
         tSpD[k] = (double)c.sprod[t];
         tSpQ[k] = tSpD[k] / (double)tB[k].q;
         tRow[k] = c.drow[t];
+    } else if (threadIdx.x >= 128 && threadIdx.x < 128 + ti) {
+        const uint32_t k = threadIdx.x - 128, t = c.intT[k];
+        iB[k] = loadBar(bar, c.didx[t]);
+        iSp[k] = c.sprod[t];
+        iRow[k] = c.drow[t];
+    }
+    for (uint32_t e = threadIdx.x; e < ns * ti; e += kThreads) {
+        const uint32_t i = e / ti, k = e % ti;
+        iMod[i * kConvIntFold + k] = c.mod[(size_t)i * c.nt + c.intT[k]];
     }
     for (uint32_t e = threadIdx.x; e < ns * tc; e += kThreads) {
         const uint32_t i = e / tc, k = e % tc;
@@ -2643,6 +2683,23 @@ __global__ __launch_bounds__(kThreads) void k_convf(const ConvJobs J, const sf_b
             for (int u = 0; u < kConvTpi; ++u)
                 if (k + u < tc)
                     c.dst[((size_t)tRow[k + u] << logn) + x0 + cx] = (u64)fpReduce(a[u], pd[u], tQi[k + u]);
+        }
+        // the folded integer targets: canonical residues of the FP64 y's
+        // (no 60-bit sources here), as an integer block computes them
+        for (uint32_t kc = w * 64; kc < ti * X; kc += WAVES * 64) {
+            const uint32_t k = kc / X, cx = kc % X + lane;
+            const sf_barrett B = iB[k];
+            Acc s0{0, 0};
+            long long neg = cen ? (long long)vL[cx] : 0;
+#pragma unroll
+            for (int i = 0; i < NS; ++i) {
+                if ((uint32_t)i < ns) {
+                    const double y = __longlong_as_double(yL[i * X + cx]);
+                    macc(s0, (u64)(y < 0.0 ? y + (double)sB[i].q : y), iMod[i * kConvIntFold + k]);
+                    neg += cen && y < 0.0;
+                }
+            }
+            c.dst[((size_t)iRow[k] << logn) + x0 + cx] = subMultiple(sf_reduce128_acc(s0.lo, s0.hi, &B), neg, iSp[k], B);
         }
         return;
     }
@@ -2766,6 +2823,13 @@ __global__ __launch_bounds__(kThreads) void k_conv_mdrs(const MdrsArgs A, const 
 // bootstrapping contexts) and every target below it an integer row: r is
 // formed in integer arithmetic (k_conv_mdrs's), kept as its canonical
 // residue, and only integer blocks run.
+// Integer targets (the 60-bit q_0) of a ModDown+rescale folded into its
+// first FP64 chunk's blocks: up to kMdrsIntFold of them, with at least one
+// FP64 chunk (host and kernel decide it alike)
+constexpr uint32_t kMdrsIntFold = 2;
+__host__ __device__ __forceinline__ bool mdrsIntFolded(bool bigl, uint32_t nFp, uint32_t nInt) {
+    return !bigl && nFp > 0 && nInt <= kMdrsIntFold;
+}
 template <int NS, bool BIGL = false>
 __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_barrett* __restrict__ bar,
                                                     const double* __restrict__ qinvD, uint32_t logn) {
@@ -2783,15 +2847,23 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
     __shared__ uint32_t tRow[C];
     __shared__ double yL[NS * X], rL[X], vL[X];
     __shared__ double tSpD[C], tSpQ[C];
+    // the integer targets (q_0) folded into FP64 chunk 0 (mdrsIntFolded): a
+    // block of their own repeated phase 1 and doubled a small ModDown's grid
+    __shared__ u64 iMod[NS * kMdrsIntFold], iSp[kMdrsIntFold], iPm[kMdrsIntFold], iLs[kMdrsIntFold];
+    __shared__ sf_barrett iB[kMdrsIntFold];
+    __shared__ uint32_t iRow[kMdrsIntFold];
     const MdrsJob& J = A.j[blockIdx.y];
     const uint32_t fpChunks = (A.nFp + C - 1) / C;
+    const bool fold = mdrsIntFolded(BIGL, A.nFp, A.nInt);
     const bool fpBlock = blockIdx.z < fpChunks;
+    if (fold && !fpBlock) return;
     const uint32_t k0 = (fpBlock ? blockIdx.z : blockIdx.z - fpChunks) * C;
     const uint32_t cnt = fpBlock ? A.nFp : A.nInt;
     if (k0 >= cnt) return;
     const uint32_t tc = min((uint32_t)C, cnt - k0);
     const uint32_t ns = A.ns;
     const uint32_t* tl = fpBlock ? A.fpT : A.intT;
+    const uint32_t ti = (fold && blockIdx.z == 0) ? A.nInt : 0;  // integer targets this block adds
     // the block's source words and its dropped-row words are issued first, so
     // their HBM latency overlaps the constant staging below (one round trip
     // for the whole phase 1 instead of one per loop iteration)
@@ -2803,6 +2875,10 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
         sv[k] = J.src[((size_t)(e / X) << logn) + x0 + e % X];
     }
     const u64 alv = J.al[((size_t)A.l << logn) + x0 + threadIdx.x % X];
+    // the dropped row's constants, issued with the loads above (read after
+    // the second barrier, they were a round trip of their own)
+    const u64 qlq = bar[A.l].q, sprl = A.sprod[A.l];
+    const double qliD = qinvD[A.l];
     if (threadIdx.x < ns) {
         const uint32_t i = threadIdx.x, pi = A.sidx[i];
         sB[i] = loadBar(bar, pi);
@@ -2829,6 +2905,17 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
             tPq[k] = A.pmodQ[t];
         }
         tRow[k] = t;
+    } else if (threadIdx.x >= 128 && threadIdx.x < 128 + ti) {
+        const uint32_t k = threadIdx.x - 128, t = A.intT[k];
+        iB[k] = loadBar(bar, t);
+        iSp[k] = A.sprod[t];
+        iPm[k] = A.pmod[t];
+        iLs[k] = A.lsub[t];
+        iRow[k] = t;
+    }
+    for (uint32_t e = threadIdx.x; e < ns * ti; e += kThreads) {
+        const uint32_t i = e / ti, k = e % ti;
+        iMod[i * kMdrsIntFold + k] = A.mod[(size_t)i * A.nt + A.intT[k]];
     }
     for (uint32_t e = threadIdx.x; e < ns * tc; e += kThreads) {
         const uint32_t i = e / tc, k = e % tc;
@@ -2850,7 +2937,7 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
         }
     }
     __syncthreads();
-    const double qld = (double)bar[A.l].q;
+    const double qld = (double)qlq;
     if (threadIdx.x < X) {  // the dropped row: r = (a_l - conv_l) * P^-1 mod q_l, centred
         const uint32_t cx = threadIdx.x;
         // exact centred conversion: the overflow v (convOverflow), removed from every target
@@ -2874,18 +2961,55 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
             const u64 cl = subMultiple(sf_reduce128_acc(sl.lo, sl.hi, &BL), neg, A.sprod[A.l], BL);
             rL[cx] = __longlong_as_double((long long)bmul(sf_sub(alv, cl, BL.q), A.pinvl, BL));
         } else {
-        const double spl = (double)A.sprod[A.l];
+        const double spl = (double)sprl;
         double cl = fpMulMod(-v, spl, spl / qld, qld);
 #pragma unroll
         for (int i = 0; i < NS; ++i)
             if ((uint32_t)i < ns) cl += fpMulMod(yL[i * X + cx], sLD[i], sLQ[i], qld);
-        const double qli = qinvD[A.l];
+        const double qli = qliD;
         const double pl = (double)A.pinvl;
         rL[cx] = fpSourceY((u64)fpReduce((double)alv - fpReduce(cl, qld, qli), qld, qli), qld, pl, pl / qld, qli,
                            true);
         }
     }
     __syncthreads();
+    // integer targets, one at a time: this block's own (an integer chunk), or
+    // the folded ones after the FP64 targets
+    auto intTargets = [&](uint32_t cntT, const sf_barrett* TB, const u64* SM, uint32_t smStride, const u64* TSP,
+                          const u64* TPM, const u64* TLS, const uint32_t* TROW) {
+        for (uint32_t kc = w * 64; kc < cntT * X; kc += WAVES * 64) {
+            const uint32_t k = kc / X, cx = kc % X + lane;
+            const double r = rL[cx];
+            u64 out;
+            {
+                const sf_barrett B = TB[k];
+                Acc s0{0, 0};
+                long long neg = (long long)vL[cx];
+#pragma unroll
+                for (int i = 0; i < NS; ++i) {
+                    if ((uint32_t)i < ns) {
+                        const double y = yL[i * X + cx];
+                        macc(s0, (u64)(y < 0.0 ? y + (double)sB[i].q : y), SM[i * smStride + k]);
+                        neg += y < 0.0;
+                    }
+                }
+                out = subMultiple(sf_reduce128_acc(s0.lo, s0.hi, &B), neg, TSP[k], B);
+                u64 lift;
+                bool rneg;
+                if (BIGL) {  // canonical residue; centred: > q_l / 2 stands for r - q_l
+                    const u64 rc = (u64)__double_as_longlong(r);
+                    rneg = rc > (bar[A.l].q >> 1);
+                    lift = sf_reduce128(rc, 0, &B);
+                } else {
+                    rneg = r < 0.0;
+                    lift = sf_reduce128((u64)(r < 0.0 ? r + qld : r), 0, &B);
+                }
+                if (rneg) lift = sf_sub(lift, TLS[k], B.q);
+                out = sf_add(out, bmul(lift, TPM[k], B), B.q);
+            }
+            J.dst[((size_t)TROW[k] << logn) + x0 + cx] = out;
+        }
+    };
     if (!BIGL && fpBlock) {  // kConvTpi targets at a time, work items as k_convf
         constexpr uint32_t CH = X / 64;
         const uint32_t items = CH * ((tc + kConvTpi - 1) / kConvTpi);
@@ -2912,40 +3036,10 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
                 if (k + u < tc)
                     J.dst[((size_t)tRow[k + u] << logn) + x0 + cx] = (u64)fpReduce(a[u], pd[u], tQi[k + u]);
         }
+        if (ti) intTargets(ti, iB, iMod, kMdrsIntFold, iSp, iPm, iLs, iRow);
         return;
     }
-    for (uint32_t kc = w * 64; kc < tc * X; kc += WAVES * 64) {  // integer targets, one at a time
-        const uint32_t k = kc / X, cx = kc % X + lane;
-        const double r = rL[cx];
-        u64 out;
-        {
-            const sf_barrett B = tB[k];
-            Acc s0{0, 0};
-            long long neg = (long long)vL[cx];
-#pragma unroll
-            for (int i = 0; i < NS; ++i) {
-                if ((uint32_t)i < ns) {
-                    const double y = yL[i * X + cx];
-                    macc(s0, (u64)(y < 0.0 ? y + (double)sB[i].q : y), smod[i * C + k]);
-                    neg += y < 0.0;
-                }
-            }
-            out = subMultiple(sf_reduce128_acc(s0.lo, s0.hi, &B), neg, tSp[k], B);
-            u64 lift;
-            bool rneg;
-            if (BIGL) {  // canonical residue; centred: > q_l / 2 stands for r - q_l
-                const u64 rc = (u64)__double_as_longlong(r);
-                rneg = rc > (bar[A.l].q >> 1);
-                lift = sf_reduce128(rc, 0, &B);
-            } else {
-                rneg = r < 0.0;
-                lift = sf_reduce128((u64)(r < 0.0 ? r + qld : r), 0, &B);
-            }
-            if (rneg) lift = sf_sub(lift, tLs[k], B.q);
-            out = sf_add(out, bmul(lift, tPm[k], B), B.q);
-        }
-        J.dst[((size_t)tRow[k] << logn) + x0 + cx] = out;
-    }
+    intTargets(tc, tB, smod, C, tSp, tPm, tLs, tRow);
 }
 
 // ModDown's conversion -- and the rescale fused with it -- in the forward
@@ -4487,12 +4581,29 @@ static void nttRows(sfp_dev* d, const RowGroup& G0, int inverse, int passes = 3)
                  k_ntt<false, false, 2, T, 8>, T >> 2);
     } else if (G.cy && modupCol && !inverse && d->logn == 16 && smallTile == 1024 && L == 2) {
         // ModUpPlan at ring 2^16: the conversion + COL pass, kModupTg targets per block
+        // small launches (fewer than SFHE_MODUP_TG_SMALL blocks at kModupTg
+        // targets per block, default 512: two per CU) take two targets per
+        // block -- twice the blocks, half of each block's serial target chain
         constexpr int TG = kModupTg;
-        g.y = G.P * ((G.R + TG - 1) / TG);
+        static const uint32_t tgSmall = [] {
+            const char* v = std::getenv("SFHE_MODUP_TG_SMALL");
+            return v ? (uint32_t)std::atoi(v) : 512u;
+        }();
+        const bool tg2 = G.P * ((G.R + TG - 1) / TG) * g.x < tgSmall;
+        const int tg = tg2 ? 2 : TG;
+        g.y = G.P * ((G.R + tg - 1) / tg);
         gridRows = g.y;
-        if (t1k)
+        // (each specialisation named in a call of its own: named only inside a
+        // conditional expression, the device code of some was never emitted --
+        // "Cannot find Symbol" at launch)
+        if (t1k && tg2)
+            pass(k_modup_col<1024, 1, 2>, k_modup_col<1024, 2, 2>, k_modup_col<1024, 4, 2>, k_modup_col<1024, 8, 2>,
+                 1024 >> 2);
+        else if (t1k)
             pass(k_modup_col<1024, 1, TG>, k_modup_col<1024, 2, TG>, k_modup_col<1024, 4, TG>, k_modup_col<1024, 8, TG>,
                  1024 >> 2);
+        else if (tg2)
+            pass(k_modup_col<T, 1, 2>, k_modup_col<T, 2, 2>, k_modup_col<T, 4, 2>, k_modup_col<T, 8, 2>, T >> 2);
         else
             pass(k_modup_col<T, 1, TG>, k_modup_col<T, 2, TG>, k_modup_col<T, 4, TG>, k_modup_col<T, 8, TG>, T >> 2);
         g.y = rows;
@@ -4695,7 +4806,11 @@ static uint32_t kernelFamily(const void* f) {
         for (const void* k : {(const void*)k_modup_col<kNttTile, 1, kModupTg>, (const void*)k_modup_col<kNttTile, 2, kModupTg>,
                               (const void*)k_modup_col<kNttTile, 4, kModupTg>, (const void*)k_modup_col<kNttTile, 8, kModupTg>,
                               (const void*)k_modup_col<1024, 1, kModupTg>, (const void*)k_modup_col<1024, 2, kModupTg>,
-                              (const void*)k_modup_col<1024, 4, kModupTg>, (const void*)k_modup_col<1024, 8, kModupTg>})
+                              (const void*)k_modup_col<1024, 4, kModupTg>, (const void*)k_modup_col<1024, 8, kModupTg>,
+                              (const void*)k_modup_col<kNttTile, 1, 2>, (const void*)k_modup_col<kNttTile, 2, 2>,
+                              (const void*)k_modup_col<kNttTile, 4, 2>, (const void*)k_modup_col<kNttTile, 8, 2>,
+                              (const void*)k_modup_col<1024, 1, 2>, (const void*)k_modup_col<1024, 2, 2>,
+                              (const void*)k_modup_col<1024, 4, 2>, (const void*)k_modup_col<1024, 8, 2>})
             m[k] = SFP_FAM_NTT;
         for (const void* k : {(const void*)k_moddown_col<kNttTile, 1, kModdownTg>, (const void*)k_moddown_col<kNttTile, 2, kModdownTg>,
                               (const void*)k_moddown_col<kNttTile, 4, kModdownTg>, (const void*)k_moddown_col<kNttTile, 8, kModdownTg>,
@@ -4742,23 +4857,21 @@ static double fusedColRows(const void* arg, bool moddown) {
     }
     return r;
 }
+template <int NG>
+static bool isFusedCol(const void* f, bool md) {
+    return md ? (f == (const void*)k_moddown_col<kNttTile, NG, kModdownTg> ||
+                 f == (const void*)k_moddown_col<1024, NG, kModdownTg>)
+              : (f == (const void*)k_modup_col<kNttTile, NG, kModupTg> || f == (const void*)k_modup_col<1024, NG, kModupTg> ||
+                 f == (const void*)k_modup_col<kNttTile, NG, 2> || f == (const void*)k_modup_col<1024, NG, 2>);
+}
 static double nttNodeRows(const hipKernelNodeParams& kp) {
     const void* f = kp.func;
     if (kp.kernelParams) {
         for (bool md : {false, true}) {
-            auto is = [&](auto k2048, auto k1024) { return f == (const void*)k2048 || f == (const void*)k1024; };
-            if (md ? is(k_moddown_col<kNttTile, 1, kModdownTg>, k_moddown_col<1024, 1, kModdownTg>)
-                   : is(k_modup_col<kNttTile, 1, kModupTg>, k_modup_col<1024, 1, kModupTg>))
-                return fusedColRows<1>(kp.kernelParams[0], md);
-            if (md ? is(k_moddown_col<kNttTile, 2, kModdownTg>, k_moddown_col<1024, 2, kModdownTg>)
-                   : is(k_modup_col<kNttTile, 2, kModupTg>, k_modup_col<1024, 2, kModupTg>))
-                return fusedColRows<2>(kp.kernelParams[0], md);
-            if (md ? is(k_moddown_col<kNttTile, 4, kModdownTg>, k_moddown_col<1024, 4, kModdownTg>)
-                   : is(k_modup_col<kNttTile, 4, kModupTg>, k_modup_col<1024, 4, kModupTg>))
-                return fusedColRows<4>(kp.kernelParams[0], md);
-            if (md ? is(k_moddown_col<kNttTile, 8, kModdownTg>, k_moddown_col<1024, 8, kModdownTg>)
-                   : is(k_modup_col<kNttTile, 8, kModupTg>, k_modup_col<1024, 8, kModupTg>))
-                return fusedColRows<8>(kp.kernelParams[0], md);
+            if (isFusedCol<1>(f, md)) return fusedColRows<1>(kp.kernelParams[0], md);
+            if (isFusedCol<2>(f, md)) return fusedColRows<2>(kp.kernelParams[0], md);
+            if (isFusedCol<4>(f, md)) return fusedColRows<4>(kp.kernelParams[0], md);
+            if (isFusedCol<8>(f, md)) return fusedColRows<8>(kp.kernelParams[0], md);
         }
     }
     return (double)kp.gridDim.y;
@@ -5276,7 +5389,8 @@ static void convLaunch(sfp_dev* d, const ConvJobs& J, uint32_t njobs, bool fpOk)
         const ConvJob& j = J.j[k];
         maxT = std::max(maxT, j.ntUse);
         maxS = std::max(maxS, j.ns);
-        maxZ = std::max(maxZ, (j.nFp + kConvChunk - 1) / kConvChunk + (j.nInt + kConvChunk - 1) / kConvChunk);
+        maxZ = std::max(maxZ, (j.nFp + kConvChunk - 1) / kConvChunk +
+                                  (convIntFolded(j.nbig, j.nFp, j.nInt) ? 0 : (j.nInt + kConvChunk - 1) / kConvChunk));
         bytes += 8.0 * d->n * (j.ns + j.ntUse);
     }
     // the block-cooperative kernel (k_convf) runs every job: FP64 targets in
@@ -5855,7 +5969,8 @@ static void moddownRescaleCore(sfp_dev* d, uint64_t* out0, uint64_t* out1, const
             }
             M.pmodD = reinterpret_cast<const double*>(devConst(d, reinterpret_cast<const u64*>(pd), l));
             M.pmodQ = reinterpret_cast<const double*>(devConst(d, reinterpret_cast<const u64*>(pq), l));
-            zc = (M.nFp + kConvChunk - 1) / kConvChunk + (M.nInt + kConvChunk - 1) / kConvChunk;
+            zc = (M.nFp + kConvChunk - 1) / kConvChunk +
+             (mdrsIntFolded(false, M.nFp, M.nInt) ? 0 : (M.nInt + kConvChunk - 1) / kConvChunk);
         }
         // the dropped prime 60-bit, FP64 sources, every target below it an
         // integer row (scale-59 chains): the integer-l form of k_mdrsf
