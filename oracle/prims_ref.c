@@ -300,6 +300,16 @@ void sfp_mac_plain2(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint64_t* 
     sfp_mac_plain(d, out0, a0, b, nin, m);
     sfp_mac_plain(d, out1, a1, b, nin, m);
 }
+
+/* the multi-output form: ng separate sums, exactly as ng sfp_mac_plain2 calls */
+int sfp_mac_plain2_multi(sfp_dev* d, uint64_t* const* out0, uint64_t* const* out1, const uint64_t* const* a0,
+                         const uint64_t* const* a1, const uint64_t* const* b, uint32_t nin, uint32_t ng,
+                         sfp_limbs m) {
+    if (!ng || ng > SFP_MAC_MULTI_G || !nin || nin > SFP_MAC_MULTI_N) return -1;
+    for (uint32_t g = 0; g < ng; ++g) sfp_mac_plain2(d, out0[g], out1[g], a0, a1, b + (size_t)g * nin, nin, m);
+    return 0;
+}
+
 void sfp_mac_plain(sfp_dev* d, uint64_t* out, const uint64_t* const* a, const uint64_t* const* b,
                    uint32_t nin, sfp_limbs m) {
     LOOP_LIMBS({

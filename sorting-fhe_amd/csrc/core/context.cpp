@@ -316,6 +316,12 @@ class SfheInternal {
         return s->ellOf(c.level) + (c.pend ? 1u : 0u);
     }
     static void materialize(CiphertextImpl<DCRTPoly>& c, bool pendingOk) {
+        if (std::shared_ptr<DeferredOp> d = takeDeferred(c, pendingOk)) d->run(c.cc.get(), c, pendingOk);
+        if (c.pend && !pendingOk) settleRows(c);
+    }
+    // c's deferred op, taken out to be run by the caller, with the capture
+    // undo record kept as materialize keeps it
+    static std::shared_ptr<DeferredOp> takeDeferred(CiphertextImpl<DCRTPoly>& c, bool pendingOk) {
         SfheContextState* s = c.cc->state();
         if (c.undo && !(s->capturing && s->captureEpoch == c.undo->epoch)) {
             if (s->abandonedEpochs.count(c.undo->epoch)) {  // the capture's work never ran
@@ -339,12 +345,9 @@ class SfheInternal {
             u->scale = c.scale;
             c.undo = std::move(u);
         }
-        if (c.def) {
-            std::shared_ptr<DeferredOp> d = std::move(c.def);
-            c.def.reset();
-            d->run(c.cc.get(), c, pendingOk);
-        }
-        if (c.pend && !pendingOk) settleRows(c);
+        std::shared_ptr<DeferredOp> d = std::move(c.def);
+        c.def.reset();
+        return d;
     }
     // pending rows -> their rescale (canonical, at c.level)
     static void settleRows(CiphertextImpl<DCRTPoly>& c) {
@@ -1538,6 +1541,68 @@ struct DeferredMacPlain : DeferredOp {
         SfheInternal::adopt(ct, SfheInternal::rescale(cc, t0, t1, level, slots));
     }
 };
+
+// Pending mask sums over the SAME ciphertexts -- the giant steps of one
+// baby-step set (vecRotsOpt), the blind rotations' masks over one set of
+// masked inputs -- consumed together by EvalRotateSum run as multi-output
+// launches of up to SFP_MAC_MULTI_G sums (sfp_mac_plain2_multi): each
+// ciphertext row is read once per group instead of once per sum.  The same
+// residues as each sum's own DeferredMacPlain::run.  SFHE_MAC_MULTI=0: off.
+static void macGroups(CryptoContextImpl<DCRTPoly>* cc, const std::vector<Ciphertext<DCRTPoly>>& a,
+                      const std::vector<size_t>& idx) {
+    static const bool on = [] {
+        const char* v = std::getenv("SFHE_MAC_MULTI");
+        return !v || *v != '0';
+    }();
+    if (!on) return;
+    SfheContextState* s = cc->state();
+    auto macOf = [&](size_t k) -> DeferredMacPlain* {
+        const auto& c = *a[k];
+        if (!c.def || c.undo) return nullptr;
+        auto* m = dynamic_cast<DeferredMacPlain*>(c.def.get());
+        return (m && !m->x0.empty() && m->x0.size() <= SFP_MAC_MULTI_N) ? m : nullptr;
+    };
+    std::vector<bool> used(idx.size(), false);
+    for (size_t u = 0; u < idx.size(); ++u) {
+        DeferredMacPlain* m0 = used[u] ? nullptr : macOf(idx[u]);
+        if (!m0) continue;
+        std::vector<size_t> grp{u};
+        for (size_t v = u + 1; v < idx.size() && grp.size() < SFP_MAC_MULTI_G; ++v) {
+            DeferredMacPlain* m = used[v] ? nullptr : macOf(idx[v]);
+            if (m && m->level == m0->level && m->x0 == m0->x0 && m->x1 == m0->x1) grp.push_back(v);
+        }
+        if (grp.size() < 2) continue;
+        const uint32_t level = m0->level, nin = (uint32_t)m0->x0.size(), ng = (uint32_t)grp.size();
+        std::vector<std::shared_ptr<DeferredOp>> defs;  // (each keeps its pins alive until the launch)
+        std::vector<Plaintext> pts;
+        for (size_t g : grp) {
+            used[g] = true;
+            defs.push_back(SfheInternal::takeDeferred(*a[idx[g]], true));
+            auto* m = static_cast<DeferredMacPlain*>(defs.back().get());
+            for (auto& b : m->pins) s->dep(b.get());
+            pts.insert(pts.end(), m->pts.begin(), m->pts.end());
+        }
+        SfheInternal::encodeBatch(cc, pts, level);
+        std::vector<const uint64_t*> mm;
+        for (auto& p : pts) mm.push_back(SfheInternal::encoded(cc, p, level));
+        const uint32_t ell = s->ellOf(level);
+        const size_t pw = s->polyWords(level);
+        std::vector<DeviceBufferPtr> bufs;
+        std::vector<uint64_t*> o0, o1;
+        for (uint32_t g = 0; g < ng; ++g) {
+            bufs.push_back(s->alloc(2 * pw));
+            o0.push_back(bufs.back()->ptr);
+            o1.push_back(bufs.back()->ptr + pw);
+        }
+        const auto* x = static_cast<DeferredMacPlain*>(defs[0].get());
+        if (sfp_mac_plain2_multi(s->dev, o0.data(), o1.data(), x->x0.data(), x->x1.data(), mm.data(), nin, ng,
+                                 s->qmap(ell)) != 0)
+            for (uint32_t g = 0; g < ng; ++g)
+                sfp_mac_plain2(s->dev, o0[g], o1[g], x->x0.data(), x->x1.data(), mm.data() + (size_t)g * nin, nin,
+                               s->qmap(ell));
+        for (uint32_t g = 0; g < ng; ++g) SfheInternal::adoptPending(*a[idx[grp[g]]], bufs[g], o0[g], o1[g]);
+    }
+}
 
 // EvalMult(ct, ct): the tensor, relinearisation and rescale deferred to the
 // first consumer (the canonical form runs them as one fused chain,
@@ -2750,6 +2815,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotateSum(const std::vecto
     }
     // pending products rotate before their rescale, as in EvalRotate
     uint32_t slots = 0;
+    if (pend) macGroups(this, a, rot);
     for (size_t k : rot) {
         if (pend) {
             SfheInternal::materialize(*a[k], true);

@@ -2277,6 +2277,87 @@ __global__ __launch_bounds__(kThreads) void k_mac_plain2(u64* __restrict__ out0,
     }
 }
 
+// G sums of the same ciphertexts with their own plaintexts (the giant steps
+// of one baby-step set, sfp_mac_plain2_multi): each a_j / c_j word is read
+// once for all G, the plaintexts b[g][j] once each.  The same exact FP64
+// residue sums (FP64 rows) and 128-bit sums (the integer row) as k_mac_plain2.
+struct PtrListM {
+    const u64* a[SFP_MAC_MULTI_N];
+    const u64* c[SFP_MAC_MULTI_N];
+    const u64* b[SFP_MAC_MULTI_G * SFP_MAC_MULTI_N];  // [g * nin + j]
+    u64* o0[SFP_MAC_MULTI_G];
+    u64* o1[SFP_MAC_MULTI_G];
+};
+template <int G>
+__global__ __launch_bounds__(kThreads) void k_mac_plain2_multi(const PtrListM L, uint32_t nin, sfp_limbs m,
+                                                               const sf_barrett* __restrict__ bar, uint32_t logn,
+                                                               const double* __restrict__ qinvD) {
+    const size_t pairs = ((size_t)m.count << logn) >> 1;
+    for (size_t i = blockIdx.x * (size_t)kThreads + threadIdx.x; i < pairs; i += (size_t)gridDim.x * kThreads) {
+        const size_t e = 2 * i;
+        const uint32_t prime = primeOf(m, (uint32_t)(e >> logn));
+        const sf_barrett B = loadBar(bar, prime);
+        if (B.q < kFpPrimeBound) {  // (uniform per wave)
+            const double qd = (double)B.q, qi = qinvD[prime];
+            double x0[G], y0[G], x1[G], y1[G];
+#pragma unroll
+            for (int g = 0; g < G; ++g) x0[g] = y0[g] = x1[g] = y1[g] = 0.0;
+            for (uint32_t j = 0; j < nin; ++j) {
+                const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(L.a[j] + e);
+                const ulonglong2 c = *reinterpret_cast<const ulonglong2*>(L.c[j] + e);
+                ulonglong2 p[G];
+#pragma unroll
+                for (int g = 0; g < G; ++g) p[g] = *reinterpret_cast<const ulonglong2*>(L.b[g * nin + j] + e);
+                const double ax = u2d(a.x), ay = u2d(a.y), cx = u2d(c.x), cy = u2d(c.y);
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    const double px = u2d(p[g].x), py = u2d(p[g].y), pxq = px * qi, pyq = py * qi;
+                    x0[g] += fpMulMod(ax, px, pxq, qd);
+                    y0[g] += fpMulMod(ay, py, pyq, qd);
+                    x1[g] += fpMulMod(cx, px, pxq, qd);
+                    y1[g] += fpMulMod(cy, py, pyq, qd);
+                }
+            }
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                ulonglong2 o0, o1;
+                o0.x = d2u(fpReduce(x0[g], qd, qi));
+                o0.y = d2u(fpReduce(y0[g], qd, qi));
+                o1.x = d2u(fpReduce(x1[g], qd, qi));
+                o1.y = d2u(fpReduce(y1[g], qd, qi));
+                *reinterpret_cast<ulonglong2*>(L.o0[g] + e) = o0;
+                *reinterpret_cast<ulonglong2*>(L.o1[g] + e) = o1;
+            }
+        } else {
+            Acc x0[G], y0[G], x1[G], y1[G];
+#pragma unroll
+            for (int g = 0; g < G; ++g) x0[g] = y0[g] = x1[g] = y1[g] = Acc{0, 0};
+            for (uint32_t j = 0; j < nin; ++j) {
+                const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(L.a[j] + e);
+                const ulonglong2 c = *reinterpret_cast<const ulonglong2*>(L.c[j] + e);
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    const ulonglong2 p = *reinterpret_cast<const ulonglong2*>(L.b[g * nin + j] + e);
+                    macc(x0[g], a.x, p.x);
+                    macc(y0[g], a.y, p.y);
+                    macc(x1[g], c.x, p.x);
+                    macc(y1[g], c.y, p.y);
+                }
+            }
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                ulonglong2 o0, o1;
+                o0.x = sf_reduce128_acc(x0[g].lo, x0[g].hi, &B);
+                o0.y = sf_reduce128_acc(y0[g].lo, y0[g].hi, &B);
+                o1.x = sf_reduce128_acc(x1[g].lo, x1[g].hi, &B);
+                o1.y = sf_reduce128_acc(y1[g].lo, y1[g].hi, &B);
+                *reinterpret_cast<ulonglong2*>(L.o0[g] + e) = o0;
+                *reinterpret_cast<ulonglong2*>(L.o1[g] + e) = o1;
+            }
+        }
+    }
+}
+
 __global__ __launch_bounds__(kThreads) void k_mac_plain(u64* __restrict__ out, PtrList2 ab,
                                                         uint32_t nin, sfp_limbs m,
                                                         const sf_barrett* __restrict__ bar,
@@ -5052,6 +5133,38 @@ void sfp_mac_plain2(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint64_t* 
     SFP_GO(k_mac_plain2, dim3(ewGrid(total / 2)), dim3(kThreads), out0, out1, L, nin, m,
                        d->bar, d->logn, d->qinvD);
     checkLaunch(d, "mac_plain2");
+}
+
+int sfp_mac_plain2_multi(sfp_dev* d, uint64_t* const* out0, uint64_t* const* out1, const uint64_t* const* a0,
+                         const uint64_t* const* a1, const uint64_t* const* b, uint32_t nin, uint32_t ng,
+                         sfp_limbs m) {
+    if (!ng || ng > SFP_MAC_MULTI_G || !nin || nin > SFP_MAC_MULTI_N) return -1;
+    if (!m.count) return 0;
+    if (!limbsOk(d, m, "mac_plain2_multi")) return 0;
+    PtrListM L;
+    std::memset(&L, 0, sizeof L);
+    for (uint32_t j = 0; j < nin; ++j) {
+        L.a[j] = a0[j];
+        L.c[j] = a1[j];
+        for (uint32_t g = 0; g < ng; ++g) L.b[g * nin + j] = b[(size_t)g * nin + j];
+    }
+    for (uint32_t g = 0; g < ng; ++g) {
+        L.o0[g] = out0[g];
+        L.o1[g] = out1[g];
+    }
+    const size_t total = (size_t)m.count * d->n;
+    const dim3 grid(ewGrid(total / 2));
+    // (each specialisation launched by name: see tests/test_kernel_symbols.py)
+    if (ng == 1)
+        SFP_GO(k_mac_plain2_multi<1>, grid, dim3(kThreads), L, nin, m, d->bar, d->logn, d->qinvD);
+    else if (ng == 2)
+        SFP_GO(k_mac_plain2_multi<2>, grid, dim3(kThreads), L, nin, m, d->bar, d->logn, d->qinvD);
+    else if (ng == 3)
+        SFP_GO(k_mac_plain2_multi<3>, grid, dim3(kThreads), L, nin, m, d->bar, d->logn, d->qinvD);
+    else
+        SFP_GO(k_mac_plain2_multi<4>, grid, dim3(kThreads), L, nin, m, d->bar, d->logn, d->qinvD);
+    checkLaunch(d, "mac_plain2_multi");
+    return 0;
 }
 
 void sfp_mac_plain(sfp_dev* d, uint64_t* out, const uint64_t* const* a, const uint64_t* const* b,

@@ -119,6 +119,16 @@ void sfp_mac_plain(sfp_dev* d, uint64_t* out, const uint64_t* const* a, const ui
 // out0 = sum_j a0[j] * b[j], out1 = sum_j a1[j] * b[j]  (nin <= SFP_MAX_WSUM).
 void sfp_mac_plain2(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint64_t* const* a0,
                     const uint64_t* const* a1, const uint64_t* const* b, uint32_t nin, sfp_limbs m);
+// ng such sums over the SAME ciphertexts (a0, a1) with their own plaintexts
+// b[g * nin + j]: out0[g] / out1[g], g < ng <= SFP_MAC_MULTI_G, nin <=
+// SFP_MAC_MULTI_N -- the giant steps of one baby-step set, each ciphertext
+// row read once for all of them.  The same residues as ng sfp_mac_plain2
+// calls.  Returns 0, or -1 (shape unsupported: the caller runs those calls).
+#define SFP_MAC_MULTI_G 4
+#define SFP_MAC_MULTI_N 32
+int sfp_mac_plain2_multi(sfp_dev* d, uint64_t* const* out0, uint64_t* const* out1, const uint64_t* const* a0,
+                         const uint64_t* const* a1, const uint64_t* const* b, uint32_t nin, uint32_t ng,
+                         sfp_limbs m);
 
 // ---- automorphism ----------------------------------------------------------
 // out = sigma_g(in) in the evaluation domain (g odd, < 2n); out != in.
