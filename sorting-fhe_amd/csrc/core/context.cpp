@@ -1554,6 +1554,11 @@ static void macGroups(CryptoContextImpl<DCRTPoly>* cc, const std::vector<Ciphert
         const char* v = std::getenv("SFHE_MAC_MULTI");
         return !v || *v != '0';
     }();
+    static const size_t maxG = [] {  // SFHE_MAC_MULTI_G: sums per launch (A/B; at most SFP_MAC_MULTI_G)
+        const char* v = std::getenv("SFHE_MAC_MULTI_G");
+        const int g = v ? std::atoi(v) : SFP_MAC_MULTI_G;
+        return (size_t)std::max(2, std::min(g, SFP_MAC_MULTI_G));
+    }();
     if (!on) return;
     SfheContextState* s = cc->state();
     auto macOf = [&](size_t k) -> DeferredMacPlain* {
@@ -1567,7 +1572,7 @@ static void macGroups(CryptoContextImpl<DCRTPoly>* cc, const std::vector<Ciphert
         DeferredMacPlain* m0 = used[u] ? nullptr : macOf(idx[u]);
         if (!m0) continue;
         std::vector<size_t> grp{u};
-        for (size_t v = u + 1; v < idx.size() && grp.size() < SFP_MAC_MULTI_G; ++v) {
+        for (size_t v = u + 1; v < idx.size() && grp.size() < maxG; ++v) {
             DeferredMacPlain* m = used[v] ? nullptr : macOf(idx[v]);
             if (m && m->level == m0->level && m->x0 == m0->x0 && m->x1 == m0->x1) grp.push_back(v);
         }

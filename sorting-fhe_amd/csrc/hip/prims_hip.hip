@@ -2328,31 +2328,36 @@ __global__ __launch_bounds__(kThreads) void k_mac_plain2_multi(const PtrListM L,
                 *reinterpret_cast<ulonglong2*>(L.o0[g] + e) = o0;
                 *reinterpret_cast<ulonglong2*>(L.o1[g] + e) = o1;
             }
-        } else {
-            Acc x0[G], y0[G], x1[G], y1[G];
+        } else {  // (128-bit sums in groups of four: the integer row's registers)
 #pragma unroll
-            for (int g = 0; g < G; ++g) x0[g] = y0[g] = x1[g] = y1[g] = Acc{0, 0};
-            for (uint32_t j = 0; j < nin; ++j) {
-                const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(L.a[j] + e);
-                const ulonglong2 c = *reinterpret_cast<const ulonglong2*>(L.c[j] + e);
+            for (int h = 0; h < G; h += 4) {
+                Acc x0[4], y0[4], x1[4], y1[4];
 #pragma unroll
-                for (int g = 0; g < G; ++g) {
-                    const ulonglong2 p = *reinterpret_cast<const ulonglong2*>(L.b[g * nin + j] + e);
-                    macc(x0[g], a.x, p.x);
-                    macc(y0[g], a.y, p.y);
-                    macc(x1[g], c.x, p.x);
-                    macc(y1[g], c.y, p.y);
+                for (int g = 0; g < 4; ++g) x0[g] = y0[g] = x1[g] = y1[g] = Acc{0, 0};
+                for (uint32_t j = 0; j < nin; ++j) {
+                    const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(L.a[j] + e);
+                    const ulonglong2 c = *reinterpret_cast<const ulonglong2*>(L.c[j] + e);
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        if (h + g >= G) break;
+                        const ulonglong2 p = *reinterpret_cast<const ulonglong2*>(L.b[(h + g) * nin + j] + e);
+                        macc(x0[g], a.x, p.x);
+                        macc(y0[g], a.y, p.y);
+                        macc(x1[g], c.x, p.x);
+                        macc(y1[g], c.y, p.y);
+                    }
                 }
-            }
 #pragma unroll
-            for (int g = 0; g < G; ++g) {
-                ulonglong2 o0, o1;
-                o0.x = sf_reduce128_acc(x0[g].lo, x0[g].hi, &B);
-                o0.y = sf_reduce128_acc(y0[g].lo, y0[g].hi, &B);
-                o1.x = sf_reduce128_acc(x1[g].lo, x1[g].hi, &B);
-                o1.y = sf_reduce128_acc(y1[g].lo, y1[g].hi, &B);
-                *reinterpret_cast<ulonglong2*>(L.o0[g] + e) = o0;
-                *reinterpret_cast<ulonglong2*>(L.o1[g] + e) = o1;
+                for (int g = 0; g < 4; ++g) {
+                    if (h + g >= G) break;
+                    ulonglong2 o0, o1;
+                    o0.x = sf_reduce128_acc(x0[g].lo, x0[g].hi, &B);
+                    o0.y = sf_reduce128_acc(y0[g].lo, y0[g].hi, &B);
+                    o1.x = sf_reduce128_acc(x1[g].lo, x1[g].hi, &B);
+                    o1.y = sf_reduce128_acc(y1[g].lo, y1[g].hi, &B);
+                    *reinterpret_cast<ulonglong2*>(L.o0[h + g] + e) = o0;
+                    *reinterpret_cast<ulonglong2*>(L.o1[h + g] + e) = o1;
+                }
             }
         }
     }
@@ -5155,14 +5160,16 @@ int sfp_mac_plain2_multi(sfp_dev* d, uint64_t* const* out0, uint64_t* const* out
     const size_t total = (size_t)m.count * d->n;
     const dim3 grid(ewGrid(total / 2));
     // (each specialisation launched by name: see tests/test_kernel_symbols.py)
-    if (ng == 1)
-        SFP_GO(k_mac_plain2_multi<1>, grid, dim3(kThreads), L, nin, m, d->bar, d->logn, d->qinvD);
-    else if (ng == 2)
-        SFP_GO(k_mac_plain2_multi<2>, grid, dim3(kThreads), L, nin, m, d->bar, d->logn, d->qinvD);
-    else if (ng == 3)
-        SFP_GO(k_mac_plain2_multi<3>, grid, dim3(kThreads), L, nin, m, d->bar, d->logn, d->qinvD);
-    else
-        SFP_GO(k_mac_plain2_multi<4>, grid, dim3(kThreads), L, nin, m, d->bar, d->logn, d->qinvD);
+    switch (ng) {
+        case 1: SFP_GO(k_mac_plain2_multi<1>, grid, dim3(kThreads), L, nin, m, d->bar, d->logn, d->qinvD); break;
+        case 2: SFP_GO(k_mac_plain2_multi<2>, grid, dim3(kThreads), L, nin, m, d->bar, d->logn, d->qinvD); break;
+        case 3: SFP_GO(k_mac_plain2_multi<3>, grid, dim3(kThreads), L, nin, m, d->bar, d->logn, d->qinvD); break;
+        case 4: SFP_GO(k_mac_plain2_multi<4>, grid, dim3(kThreads), L, nin, m, d->bar, d->logn, d->qinvD); break;
+        case 5: SFP_GO(k_mac_plain2_multi<5>, grid, dim3(kThreads), L, nin, m, d->bar, d->logn, d->qinvD); break;
+        case 6: SFP_GO(k_mac_plain2_multi<6>, grid, dim3(kThreads), L, nin, m, d->bar, d->logn, d->qinvD); break;
+        case 7: SFP_GO(k_mac_plain2_multi<7>, grid, dim3(kThreads), L, nin, m, d->bar, d->logn, d->qinvD); break;
+        default: SFP_GO(k_mac_plain2_multi<8>, grid, dim3(kThreads), L, nin, m, d->bar, d->logn, d->qinvD); break;
+    }
     checkLaunch(d, "mac_plain2_multi");
     return 0;
 }

@@ -124,7 +124,7 @@ void sfp_mac_plain2(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint64_t* 
 // SFP_MAC_MULTI_N -- the giant steps of one baby-step set, each ciphertext
 // row read once for all of them.  The same residues as ng sfp_mac_plain2
 // calls.  Returns 0, or -1 (shape unsupported: the caller runs those calls).
-#define SFP_MAC_MULTI_G 4
+#define SFP_MAC_MULTI_G 8
 #define SFP_MAC_MULTI_N 32
 int sfp_mac_plain2_multi(sfp_dev* d, uint64_t* const* out0, uint64_t* const* out1, const uint64_t* const* a0,
                          const uint64_t* const* a1, const uint64_t* const* b, uint32_t nin, uint32_t ng,
