@@ -2845,6 +2845,14 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotateSum(const std::vecto
         // inner products accumulate into acc in turn (never merged: one
         // accumulator), the last one with the ModDown's first inverse pass.
         const size_t w = batchWidth();
+        // sigma_k(c0_k) of every term but the first, summed into out->c0 by one
+        // weighted sum (weights 1) after the loop instead of one add per term
+        std::vector<DeviceBufferPtr> c0s;
+        static const bool oneSumOn = [] {  // SFHE_ROTSUM_C0=0: one add per term (A/B)
+            const char* v = std::getenv("SFHE_ROTSUM_C0");
+            return !v || *v != '0';
+        }();
+        const bool oneSum = oneSumOn && rot.size() <= SFP_MAX_WSUM;
         for (size_t b0 = 0; b0 < rot.size(); b0 += w) {
             const size_t b1 = std::min(rot.size(), b0 + w);
             std::vector<DeviceBufferPtr> tb, cb, eb, sb;
@@ -2867,7 +2875,8 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotateSum(const std::vecto
             }
             for (size_t i = b0; i < b1; ++i) {
                 const size_t k = i - b0;
-                if (i) sfp_add(s->dev, out->c0, out->c0, cb[k]->ptr, st->qmap(ell));
+                if (i && oneSum) c0s.push_back(cb[k]);
+                else if (i) sfp_add(s->dev, out->c0, out->c0, cb[k]->ptr, st->qmap(ell));
                 sfp_modup_inner_phase(s->dev, acc->ptr, acc->ptr + stride, tb[k]->ptr, ell, K, s->Lq, s->alpha,
                                       convs.data(), (*keys[i])->ptr, nullptr, nullptr, 0, i ? 1 : 0,
                                       i + 1 == rot.size() ? ell : ~0u, eb[k]->ptr, sb[k]->ptr, 2);
@@ -2875,6 +2884,12 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotateSum(const std::vecto
                 s->stats.keyswitch++;
                 s->countBytes((5.0 * ell + 2.0 * beta * (ell + K)) * n * 8);
             }
+        }
+        if (!c0s.empty()) {
+            std::vector<const uint64_t*> ins{out->c0};
+            for (auto& b : c0s) ins.push_back(b->ptr);
+            const std::vector<uint64_t> ones(ins.size() * ell, 1);
+            sfp_lin_wsum(s->dev, out->c0, ins.data(), ones.data(), (uint32_t)ins.size(), st->qmap(ell));
         }
         rowDone = 1;
     }
