@@ -258,14 +258,21 @@ def test_direct_sort_h2test_large_fails_as_attributed(hip_lib):
     of [-1, 1] (its hits sit at x = 0, where every giant step T_{2^i} is at an
     extremum), so no affine re-expansion moves them (that is what rescues the
     doubled sinc in DirectSort); the reference's sort_hybrid
-    switches to the composite-sign indicator at N >= 256 for this reason."""
+    switches to the composite-sign indicator at N >= 256 for this reason.
+
+    The test draws a fresh input every run (tests/utils.h shuffles with
+    std::random_device), and at N = 256 the error straddles the gate
+    (0.0097 ... 0.026 over runs): N = 256 may pass or fail, N = 512 and 1024
+    always fail."""
     rc, out = run(exe("DirectSortH2Test"), "--gtest_filter=*/6.*:*/7.*:*/8.*", timeout=600)
     errs = [float(x) for x in re.findall(r"Maximum error: ([0-9.e+-]+)", out)]
     levels = [int(x) for x in re.findall(r"Result Level: (\d+)", out)]
     print("max errors:", errs, "levels:", levels)
     assert rc != 0
-    assert "3 tests ran, 3 failed" in out, out[-3000:]
-    assert len(errs) == 3 and all(0.01 < e < 0.6 for e in errs), errs
+    assert "3 tests ran, 3 failed" in out or "3 tests ran, 2 failed" in out, out[-3000:]
+    assert len(errs) == 3, errs
+    assert 0.005 < errs[0] < 0.6, errs  # N = 256: either side of the gate
+    assert all(0.01 < e < 0.6 for e in errs[1:]), errs
     assert "unexpected exception" not in out, out[-3000:]
     assert "Use the level returned" not in out, out[-3000:]  # the level gate holds
 
