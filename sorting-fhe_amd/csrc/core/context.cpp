@@ -2332,8 +2332,14 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalAdd(const Ciphertext<DCRTP
         const uint32_t ell = st->ellOf(a->level) + 1;
         auto out = SfheInternal::newPendingCt(this, a->level, a->slots);
         auto k = SfheInternal::constResidues(st.get(), c * a->scale, ell);
-        sfp_add_const(st->dev, out->c0, a->c0, k.data(), st->qmap(ell));
-        sfp_d2d(st->dev, out->c1, a->c1, (size_t)st->rows(ell) * st->n * 8);
+        if (2 * k.size() <= SFP_MAX_LIMBS &&
+            SfheInternal::packed(st.get(), {out->c0, a->c0}, {out->c1, a->c1}, a->level - 1)) {
+            k.resize(2 * k.size(), 0);  // c1 rows: + 0, i.e. the copy, in the same launch
+            sfp_add_const(st->dev, out->c0, a->c0, k.data(), SfheInternal::both(st.get(), ell));
+        } else {
+            sfp_add_const(st->dev, out->c0, a->c0, k.data(), st->qmap(ell));
+            sfp_d2d(st->dev, out->c1, a->c1, (size_t)st->rows(ell) * st->n * 8);
+        }
         st->stats.add++;
         st->countBytes(4.0 * ell * st->n * 8);
         return SfheInternal::traced(this, out, "EvalAdd");
