@@ -462,11 +462,13 @@ def main(argv=None):
     dt = timed_steps(step, eng.sync, world, args.steps, args.warmup)
     tail = eng.shard_tail()
 
-    # profiling leg (after the timed region): one sort with the lanes
-    # serialised on one stream and every launch of each family bracketed by
-    # HIP events on that stream -- per-launch durations as rocprofv3 measures
-    # them (no other lane's kernels inside a timed interval; the batches'
-    # stacked launches are timed as issued, a merged pair as one launch)
+    # profiling leg (after the timed region): one EAGER sort (SFHE_GRAPH=0)
+    # with the lanes serialised on one stream and every launch of each family
+    # bracketed by HIP events on that stream -- per-launch durations as
+    # rocprofv3 measures them (no other lane's kernels inside a timed
+    # interval).  Batched ops merge here as in the captured sort (prims.h
+    # sfp_batch_*), a merged launch timed as one launch with the bytes of all
+    # of its ops; stacked lane regions (SFHE_STACK_BATCHES) are off in both.
     graph_nodes = sorter.graph_nodes()
     stk0 = eng.stack_stats()
     eng.sync()
@@ -475,11 +477,27 @@ def main(argv=None):
     for fam in families:
         eng.kernel_timing(fam, 1)
     eng.op_stats(reset=True)
+    if mode:
+        eng.comm_stats_reset(timed=True)
     t0 = time.perf_counter()
     step()
     eng.sync()
     serial_ms = (time.perf_counter() - t0) * 1e3
     stats = eng.op_stats()  # the SURVEY §8(d) byte model over one (eager) sort
+    collectives = None
+    if mode:  # each rank's exchange share of a sort, so the 1 -> 8 curve decomposes
+        mine = dict(eng.comm_stats(), rank=rank, serial_sort_ms=serial_ms)
+        import torch.distributed as dist
+        every = [None] * world
+        dist.all_gather_object(every, mine)
+        collectives = {
+            "per_rank": every,
+            "source": "the profiling sort after the timed region (eager, lanes serialised on one stream)",
+            "note": "calls = all-gathers / broadcasts this rank issued in one sort (ModUp / ModDown "
+                    "all-gathers and rescale broadcasts at dealt levels, one batch-group all-gather per "
+                    "phase); bytes = what it received; ms = their summed duration (HIP events on the "
+                    "engine stream around each RCCL call); serial_sort_ms - ms = that sort's compute. "
+                    "The timed graph issues the same collectives"}
     stk1 = eng.stack_stats()
     kt = {fam: eng.kernel_timing_read(fam) for fam in families}
     for fam in families:
@@ -609,15 +627,27 @@ def main(argv=None):
         "graph": {"replayed": graph_nodes > 0, "nodes": graph_nodes,
                   "note": "timed steps replay the sort as one hipGraph (captured during warmup; "
                           "SFHE_GRAPH=0 runs them eagerly)"},
-        "stacked": {"merged_pairs_per_sort": stk1[0] - stk0[0], "alone_per_sort": stk1[1] - stk0[1],
-                    "note": "the batches' identical ops issued as one launch (prims.h sfp_stack_*); "
-                            "counted over the profiling sort's stacked regions (SFHE_STACK_BATCHES=0: off)"},
+        # the sort's algorithmic bytes over the timed sort's wall time, against HBM peak
+        "whole_sort_frac": stats["algo_bytes"] / sort_s / (HBM_PEAK_GBS * 1e9),
+        "batched_ops": {"merged_launches_per_sort": stk1[0] - stk0[0],
+                        "alone_launches_per_sort": stk1[1] - stk0[1],
+                        "source": "the serialised eager profiling sort after the timed region",
+                        "note": "launches of batched ops (prims.h sfp_batch_*: independent ops of one lane, "
+                                "e.g. one Chebyshev PS level's products) issued as ONE merged launch of 2-8 "
+                                "ops, and those issued alone; the captured sort records the same merged "
+                                "launches.  Stacked lane regions (SFHE_STACK_BATCHES=1) are off"},
         "roofline": roofline,
         "kernels": kernels,
+        "kernels_source": ("the serialised eager profiling sort after the timed region (SFHE_GRAPH=0, lanes on "
+                           f"one stream, {serial_ms:.1f} ms): HIP events around every launch of each family; "
+                           "batched ops merged as in the timed graph, a merged launch counted as one.  The "
+                           "timed graph's own kernels: roofline (NTT) and graph_breakdown (every family)"),
         "graph_breakdown": graph_breakdown,
         "trials": trials,
         "cpu_baseline": None,
     }
+    if collectives:
+        result["collectives"] = collectives
     if replicas:
         result["replicas"] = replicas
     if dog:

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define SFHE_ABI_VERSION 2  /* bumped when a declaration or struct below changes */
+#define SFHE_ABI_VERSION 3  /* bumped when a declaration or struct below changes */
 
 #define SFHE_OK 0
 #define SFHE_EINVAL (-1)   /* bad argument */
@@ -123,6 +123,13 @@ int sfhe_serialize_lanes(sfhe_ctx* c, int on);
  * the sort's two batches issue their identical ops as one launch each --
  * `merged` such pairs, `single` launches issued alone inside stacked regions. */
 int sfhe_stack_stats(sfhe_ctx* c, uint64_t* merged, uint64_t* single);
+/* Collective statistics of a sharded context (no reference counterpart; the
+ * reference has no distributed code): sfhe_comm_stats_reset zeroes them
+ * (timed != 0: every eager collective is also timed with events on its
+ * stream); sfhe_comm_stats returns the collectives this rank issued since,
+ * the bytes it received through them and their summed duration in ms. */
+int sfhe_comm_stats_reset(sfhe_ctx* c, int timed);
+int sfhe_comm_stats(sfhe_ctx* c, uint64_t* calls, double* bytes, double* ms);
 
 /* ---- encryption ------------------------------------------------------------
  * Replaces Encryption::encryptInput (encryption.cpp:5-12, MakeCKKSPacked-

@@ -29,6 +29,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "../sorting-fhe_amd/csrc/prims.h"
 
@@ -54,6 +55,10 @@ struct sfp_dev {
     double* enc_ksi;
     /* switching-key geometry (sfp_set_key_geom; rows == 0: whole keys) */
     sfp_key_geom kg;
+    /* collective statistics (sfp_comm_stats) */
+    uint64_t comm_calls;
+    double comm_bytes, comm_ms;
+    int comm_timed;
 };
 
 void sfp_set_key_geom(sfp_dev* d, const sfp_key_geom* g) {
@@ -787,15 +792,40 @@ void sfp_comm_set_host(sfp_dev* d, int rank, int world, sfp_host_allgather_fn ag
     d->user = user;
 }
 int sfp_comm_capturable(sfp_dev* d) { (void)d; return 0; /* no graphs in the oracle */ }
+static double comm_now_ms(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec * 1e3 + t.tv_nsec * 1e-6;
+}
+void sfp_comm_stats_reset(sfp_dev* d, int timed) {
+    d->comm_calls = 0;
+    d->comm_bytes = 0;
+    d->comm_ms = 0;
+    d->comm_timed = timed;
+}
+void sfp_comm_stats(sfp_dev* d, uint64_t* calls, double* bytes, double* ms) {
+    if (calls) *calls = d->comm_calls;
+    if (bytes) *bytes = d->comm_bytes;
+    if (ms) *ms = d->comm_ms;
+}
+/* one host collective: counted, and timed by the wall clock (the oracle is synchronous) */
+static double comm_begin(sfp_dev* d) { return d->comm_timed ? comm_now_ms() : 0.0; }
+static void comm_end(sfp_dev* d, double t0, double received) {
+    d->comm_calls++;
+    d->comm_bytes += received;
+    if (d->comm_timed) d->comm_ms += comm_now_ms() - t0;
+}
 void sfp_allgather(sfp_dev* d, const void* send, void* recv, size_t bytes) {
     if (d->world <= 1 || !d->ag) {
         if (send != recv) memmove(recv, send, bytes);
         return;
     }
+    const double t0 = comm_begin(d);
     void* tmp = malloc(bytes ? bytes : 1); /* send may alias recv */
     memcpy(tmp, send, bytes);
     d->ag(d->user, tmp, recv, bytes);
     free(tmp);
+    comm_end(d, t0, (double)bytes * (d->world - 1));
 }
 int sfp_group_init_rccl(sfp_dev* d, int group, int groups, const void* uid128) {
     (void)d; (void)group; (void)groups; (void)uid128;
@@ -812,14 +842,18 @@ void sfp_group_allgather(sfp_dev* d, const void* send, void* recv, size_t bytes)
         if (send != recv) memmove(recv, send, bytes);
         return;
     }
+    const double t0 = comm_begin(d);
     void* tmp = malloc(bytes ? bytes : 1);
     memcpy(tmp, send, bytes);
     d->gag(d->guser, tmp, recv, bytes);
     free(tmp);
+    comm_end(d, t0, (double)bytes * (d->gworld - 1));
 }
 void sfp_bcast(sfp_dev* d, void* buf, size_t bytes, int root) {
     if (d->world <= 1 || !d->bc) return;
+    const double t0 = comm_begin(d);
     d->bc(d->user, buf, bytes, root);
+    comm_end(d, t0, d->rank == root ? 0.0 : (double)bytes);
 }
 
 void sfp_gather_rows(sfp_dev* d, uint64_t* dst, const uint64_t* src, const uint32_t* rows, uint32_t count) {

@@ -795,6 +795,22 @@ int sfhe_stack_stats(sfhe_ctx* c, uint64_t* merged, uint64_t* single) {
     });
 }
 
+int sfhe_comm_stats_reset(sfhe_ctx* c, int timed) {
+    REQUIRE(c, "null context");
+    return guard([&] {
+        OpLock g(c->cc->state());
+        sfp_comm_stats_reset(c->cc->state()->dev, timed);
+    });
+}
+
+int sfhe_comm_stats(sfhe_ctx* c, uint64_t* calls, double* bytes, double* ms) {
+    REQUIRE(c, "null context");
+    return guard([&] {
+        OpLock g(c->cc->state());
+        sfp_comm_stats(c->cc->state()->dev, calls, bytes, ms);
+    });
+}
+
 int sfhe_kernel_timing_read(sfhe_ctx* c, uint32_t family, uint64_t* launches, uint64_t* timed,
                             double* ms, double* bytes) {
     REQUIRE(c, "null context");

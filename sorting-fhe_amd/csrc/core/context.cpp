@@ -155,14 +155,19 @@ DeviceBuffer::~DeviceBuffer() {
             return;
         }
     }
-    if (st->batchDepth)
-        st->batchFree.push_back({words, ptr});  // its batch's launches are not issued yet
-    else if (!st->forkedLanes)
-        st->freeList[0][words].push_back(ptr);  // everything is ordered behind lane 0 again
-    else if (region == st->region && lane == st->myLane())
-        st->freeList[lane][words].push_back(ptr);  // private to this lane in this region
+    if (st->batchDepth && std::this_thread::get_id() == st->batchThread)
+        st->batchFree.push_back({words, ptr, lane, region});  // its batch's launches are not issued yet
     else
-        st->deferredFree.push_back({words, ptr});  // another lane may still use it: after the join
+        st->poolReturn(words, ptr, lane, region, st->myLane());
+}
+
+void SfheContextState::poolReturn(size_t words, uint64_t* p, int lane, uint64_t region, int freer) {
+    if (!forkedLanes)
+        freeList[0][words].push_back(p);  // everything is ordered behind lane 0 again
+    else if (region == this->region && lane == freer)
+        freeList[lane][words].push_back(p);  // private to this lane in this region
+    else
+        deferredFree.push_back({words, p});  // another lane may still use it: after the join
 }
 
 DeviceBufferPtr SfheContextState::alloc(size_t words) {
@@ -954,6 +959,7 @@ class SfheInternal {
         const size_t stride = (size_t)(ell + K) * n;
         auto& convs = modupConv(cc, ell);
         size_t done = 0;
+        {  // (the batch ends here: unfused pairs below run as ordinary ops on the caller's lane)
         BatchScope bs(cc, s->shardAt(ell) ? 0 : (uint32_t)cnt);
         if (bs) {
             for (; done < cnt; ++done) {
@@ -972,6 +978,7 @@ class SfheInternal {
                 s->countBytes((3.0 * ell + 2.0 * beta * (ell + K)) * n * 8);
                 s->countBytes(4.0 * ell * n * 8);
             }
+        }
         }
         for (size_t i = done; i < cnt; ++i)
             out[i] = multRelinRescale(cc, a[i]->c0, a[i]->c1, b[i]->c0, b[i]->c1, level, slots[i]);
@@ -1943,7 +1950,9 @@ bool CryptoContextImpl<DCRTPoly>::BeginBatch(uint32_t count) {
     {
         OpLock g(s);
         if (!s->batchDepth && sfp_batch_begin(s->dev, count)) {
+            std::lock_guard<std::mutex> pg(s->poolMu);
             ++s->batchDepth;
+            s->batchThread = std::this_thread::get_id();
             return true;
         }
     }
@@ -1963,10 +1972,10 @@ void CryptoContextImpl<DCRTPoly>::EndBatch() {
     SfheContextState* s = st.get();
     if (!s->batchDepth) return;
     sfp_batch_end(s->dev);  // every op of the batch is issued on this lane now
-    --s->batchDepth;
     std::lock_guard<std::mutex> pg(s->poolMu);
-    const int l = s->forkedLanes ? s->lane : 0;
-    for (auto& e : s->batchFree) s->freeList[l][e.first].push_back(e.second);
+    --s->batchDepth;
+    // (this thread freed them: the same lane test ~DeviceBuffer applies)
+    for (auto& e : s->batchFree) s->poolReturn(e.words, e.ptr, e.lane, e.region, s->myLane());
     s->batchFree.clear();
     s->opMu.unlock();  // (BeginBatch's)
 }

@@ -7,6 +7,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <unordered_map>
 #include <unordered_set>
 #include <vector>
@@ -92,9 +93,24 @@ struct SfheContextState {
     std::map<size_t, std::vector<uint64_t*>> freeList[SFP_MAX_LANES];
     std::vector<std::pair<size_t, uint64_t*>> deferredFree;  // cross-lane frees inside a region
     // batched ops (BeginBatch): their launches are issued at EndBatch, so a
-    // block freed while the batch is recorded is reused only after it
+    // block the batching thread frees while the batch is recorded is reused
+    // only after it -- then by the ordinary rule (its lane and region, see
+    // ~DeviceBuffer).  Blocks other threads free meanwhile take that rule at
+    // once.  batchDepth / batchThread change under poolMu (buffers are freed
+    // from any host thread).
+    struct BatchFreed {
+        size_t words;
+        uint64_t* ptr;
+        int lane;
+        uint64_t region;
+    };
     uint32_t batchDepth = 0;
-    std::vector<std::pair<size_t, uint64_t*>> batchFree;
+    std::thread::id batchThread;
+    std::vector<BatchFreed> batchFree;
+    // a freed block back to the pool (poolMu held; `freer` = the freeing
+    // thread's lane): private to its lane inside its region, deferred to the
+    // join when another lane may still read it, lane 0's outside regions
+    void poolReturn(size_t words, uint64_t* p, int lane, uint64_t region, int freer);
     // lane 0's free blocks at ForkLanes: every lane of the region is ordered
     // after them, so any lane may reuse them (without this, blocks a lane
     // allocates migrate to lane 0 at every join and the pool grows per region)

@@ -214,6 +214,12 @@ struct sfp_dev {
     // device CKKS encoder (sfp_encode): the host encoder's tables
     u64* encRot = nullptr;         // [n/2] 5^j mod 2n
     double2* encKsi = nullptr;     // [2n+1] exp(2 pi i k / 2n)
+    // collective statistics (sfp_comm_stats): counts, bytes received, and
+    // the event pairs of the timed (eager) collectives
+    uint64_t commCalls = 0;
+    double commBytes = 0;
+    bool commTimed = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> commEv;
 };
 
 struct sfp_conv {
@@ -817,6 +823,14 @@ struct RowGroup {
     // forward pass's first half otherwise uses: copy = the K source (P) rows
     // of polynomial p, coefficient form; pre = its dropped row l (with rescale)
     const struct MdColArgs* md;
+    // icol (k_ntt<false, true, ..., ICOL>, with lift): src is the dropped row
+    // after only the FIRST pass of its inverse NTT (the ROW pass); the forward
+    // COL pass runs the inverse COL pass of that tile (prime liftPrime,
+    // inverse twiddles iTw / iTwS / iTwD, n^-1) in its prologue, then lifts:
+    // a rescale's dropped row never makes the inverse COL round trip
+    uint32_t icol;
+    const u64 *iTw, *iTwS;
+    const double* iTwD;
 };
 
 // Merged launches (stacked regions, batched ops; sfp_stack_begin /
@@ -873,7 +887,7 @@ __device__ unsigned long long g_nttTrace[kTraceSlots][4][8];
 #define NTT_MARK(i)
 #endif
 
-template <bool INV, bool COL, int LE, int TILE, int NG = 1, bool CONV = false>
+template <bool INV, bool COL, int LE, int TILE, int NG = 1, bool CONV = false, bool ICOL = false>
 __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroupSet<NG> GS, const sf_barrett* __restrict__ bar,
                                                   const u64* __restrict__ tw, const u64* __restrict__ twS,
                                                   const u64* __restrict__ ninv,
@@ -885,6 +899,8 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroupSet<NG> GS, co
                                                   const double* __restrict__ rowD) {
     __shared__ u64 s[TILE];
     __shared__ u64 tW[COL ? kNttColTw : 1], tX[COL ? kNttColTw : 1];  // COL twiddles (value; Shoup for integer rows)
+    __shared__ u64 tWi[ICOL ? kNttColTw : 1], tXi[ICOL ? kNttColTw : 1];  // ICOL: the source row's inverse ones
+    static_assert(!ICOL || (!INV && COL && !CONV), "the inverse COL prologue feeds the forward COL pass");
 #ifdef SFHE_NTT_TRACE
     unsigned long long tprev = clock64();
 #endif
@@ -1022,6 +1038,22 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroupSet<NG> GS, co
             cwD[c] = gwD[e];
         }
     }
+    // ICOL: the source row's prime and its inverse COL-pass twiddles, in
+    // flight with the tile and the forward ones
+    const uint32_t lp = ICOL ? G.liftPrime : 0u;
+    u64 icI[ICOL ? kColPer : 1], icX[ICOL ? kColPer : 1], icD[ICOL ? kColPer : 1];
+    if constexpr (ICOL) {
+        const u64* iI = G.iTw + (size_t)lp * n;
+        const u64* iX = G.iTwS + (size_t)lp * n;
+        const u64* iD = reinterpret_cast<const u64*>(G.iTwD) + (size_t)lp * n;
+#pragma unroll
+        for (int c = 0; c < kColPer; ++c) {
+            const uint32_t e = min(threadIdx.x + c * NT, colTw - 1) + 1;
+            icI[c] = iI[e];
+            icX[c] = iX[e];
+            icD[c] = iD[e];
+        }
+    }
     // ROW pass, FP64 rows, one group per thread per round (LE = 2): every
     // round's twiddles are data-independent, so all 4 x 3 of them (as local
     // and row factors, rowTwIssue) are loaded here, in flight together with
@@ -1058,6 +1090,18 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroupSet<NG> GS, co
             }
         }
     }
+    const u64 qL = ICOL ? bar[lp].q : 0;
+    const bool fpL = ICOL && useFp && qL < kFpPrimeBound;  // the source row's arithmetic
+    if constexpr (ICOL) {
+#pragma unroll
+        for (int c = 0; c < kColPer; ++c) {
+            const uint32_t e = threadIdx.x + c * NT;
+            if (e < colTw) {
+                tWi[e] = fpL ? icD[c] : icI[c];
+                if (!fpL) tXi[e] = icX[c];
+            }
+        }
+    }
     const u64* rw = COL ? tW : gw;
     const u64* rx = COL ? tX : gx;
     u64* cp = nullptr;
@@ -1071,6 +1115,11 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroupSet<NG> GS, co
         const uint32_t e = 2 * (threadIdx.x + k * NT);
         const size_t g = tileOff(k);
         ulonglong2 x = xr[k];
+        if constexpr (ICOL) {  // the source row as its own prime's pass stages it (lifted after its COL rounds)
+            s[ldsSw(e)] = fpL ? __double_as_longlong(u2d(x.x)) : x.x;
+            s[ldsSw(e + 1)] = fpL ? __double_as_longlong(u2d(x.y)) : x.y;
+            continue;
+        }
         if (FIRST) {
             if (cp) *reinterpret_cast<ulonglong2*>(cp + g) = x;
             if (pre) {
@@ -1101,6 +1150,44 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroupSet<NG> GS, co
     __syncthreads();
     NTT_MARK(0);
     const uint32_t nr = (T.d + LE - 1) / LE;
+    if constexpr (ICOL) {
+        // the source tile's inverse COL pass (k_ntt<true, true>'s rounds and
+        // its n^-1 store, canonical mod q_l) ...
+        const double qLd = (double)qL, qLi = qinvD[lp];
+        for (uint32_t ri = 0; ri < nr; ++ri) {
+            const uint32_t r = nr - 1 - ri;
+            const uint32_t k0 = LE * r;
+            const int b = (int)min((uint32_t)LE, T.d - k0);
+            if (fpL)
+                nttRoundDynFP<true, true, LE, TILE>(b, reinterpret_cast<double*>(s), T, 0u, k0, qLd,
+                                                    reinterpret_cast<const double*>(tWi), qLi);
+            else
+                nttRoundDyn<true, true, LE, TILE>(b, s, T, 0u, k0, qL, tWi, tXi);
+            __syncthreads();
+        }
+        // ... then, word by word (each thread its own slots), the centred lift
+        // to this row's prime that the unfused forward pass applies at its load
+        const u64 niL = ninv[lp], niLS = ninvS[lp];
+        const double niLD = ninvD[lp], niLQ = ninvQ[lp];
+#pragma unroll
+        for (int k = 0; k < NPAIR; ++k) {
+            const uint32_t e = 2 * (threadIdx.x + k * NT);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                u64 v = s[ldsSw(e + h)];
+                if (fpL) {
+                    v = d2u(fpReduce(fpMulMod(__longlong_as_double(v), niLD, niLQ, qLd), qLd, qLi));
+                } else {
+                    v = sf_mul_shoup_lazy(v, niL, niLS, qL);
+                    v = v >= qL ? v - qL : v;
+                }
+                u64 rr = sf_reduce128(v, 0, &LB);
+                if (v > lhalf) rr = sf_sub(rr, lsub, q);
+                s[ldsSw(e + h)] = fp ? __double_as_longlong(u2d(rr)) : rr;
+            }
+        }
+        __syncthreads();
+    }
     if constexpr (kPfBuild) {
         if (rowPf) {
 #pragma unroll
@@ -4531,9 +4618,36 @@ static RowGroup rowsOf(uint32_t P, uint32_t R, sfp_limbs pm) {
     return G;
 }
 
+// Would a forward NTT over `rows` rows take a two-stage (LE = 2) COL pass --
+// the passes that have the inverse-COL prologue (RowGroup::icol)?  Mirrors
+// nttRows' choice of path.  SFHE_ICOL=0 turns the prologue off (A/B).
+static int nttLe();
+static uint32_t nttSmallTile();
+static int nttSmallLe();
+static uint32_t nttT1kRows();
+static bool icolPath(sfp_dev* d, uint32_t rows) {
+    static const bool on = [] {
+        const char* v = std::getenv("SFHE_ICOL");
+        return !v || *v != '0';
+    }();
+    if (!on || d->n <= (uint32_t)kNttTile) return false;
+    const uint32_t st = nttSmallTile();
+    const bool t1k = rows <= nttT1kRows() && d->n <= st * 128u;
+    if (t1k) return nttSmallLe() == 2 && (st == 1024 || st == 512);
+    const int le = nttLe();
+    return (le ? le : (rows < (uint32_t)kNttSmallRows ? 2 : 3)) == 2;
+}
+
 // Both passes of a (batched) NTT over the rows of G -- or only the first
 // (passes == 1: its output feeds a fused second pass, k_ntt_ks) or only the
 // second (passes == 2: a fused kernel ran the first).
+static uint32_t nttT1kRows() {
+    static const uint32_t v = [] {
+        const char* e = std::getenv("SFHE_NTT_T1K_ROWS");
+        return e ? (uint32_t)std::atoi(e) : 64u;
+    }();
+    return v;
+}
 static int nttFp();
 static void nttRows(sfp_dev* d, const RowGroup& G0, int inverse, int passes = 3) {
     const RowGroup& G = G0;
@@ -4567,10 +4681,7 @@ static void nttRows(sfp_dev* d, const RowGroup& G0, int inverse, int passes = 3)
     // 64) they run 1024-word tiles -- twice the blocks, half the work each;
     // needs >= 2 columns per COL tile, i.e. n <= 2^17.  Measured on the metric
     // sort: NTT 47.9 -> 46.0 ms, wall 58.1 -> 57.5 ms.
-    static const uint32_t t1kRows = [] {
-        const char* v = std::getenv("SFHE_NTT_T1K_ROWS");
-        return v ? (uint32_t)std::atoi(v) : 64u;
-    }();
+    const uint32_t t1kRows = nttT1kRows();
     const uint32_t smallTile = nttSmallTile();
     const int smallLe = nttSmallLe();
     const bool t1k = rows <= t1kRows && d->n <= smallTile * 128u;
@@ -4630,6 +4741,9 @@ static void nttRows(sfp_dev* d, const RowGroup& G0, int inverse, int passes = 3)
             if (G.cy)  // ModUpPlan: the conversion in the COL pass's prologue (modupConvOk: LE 2, 1024-word tiles)
                 pass(k_ntt<false, true, 2, ST, 1, true>, k_ntt<false, true, 2, ST, 2, true>,
                      k_ntt<false, true, 2, ST, 4, true>, k_ntt<false, true, 2, ST, 8, true>, ST >> 2);
+            else if (G.icol)  // a rescale's lift with its source's inverse COL pass in the prologue
+                pass(k_ntt<false, true, 2, ST, 1, false, true>, k_ntt<false, true, 2, ST, 2, false, true>,
+                     k_ntt<false, true, 2, ST, 4, false, true>, k_ntt<false, true, 2, ST, 8, false, true>, ST >> 2);
             else
                 pass(k_ntt<false, true, 2, ST>, k_ntt<false, true, 2, ST, 2>, k_ntt<false, true, 2, ST, 4>, k_ntt<false, true, 2, ST, 8>, ST >> 2);
             pass(k_ntt<false, false, 2, ST>, k_ntt<false, false, 2, ST, 2>, k_ntt<false, false, 2, ST, 4>, k_ntt<false, false, 2, ST, 8>, ST >> 2);
@@ -4638,6 +4752,10 @@ static void nttRows(sfp_dev* d, const RowGroup& G0, int inverse, int passes = 3)
             pass(k_ntt<true, true, 2, ST>, k_ntt<true, true, 2, ST, 2>, k_ntt<true, true, 2, ST, 4>, k_ntt<true, true, 2, ST, 8>, ST >> 2);
         }
     };
+    if (G.icol && (inverse || !icolPath(d, rows))) {
+        record(d, "ntt: inverse-COL prologue outside its shape", hipErrorInvalidValue);
+        return;
+    }
     static const bool modupCol = [] {  // SFHE_MODUP_COL=0: k_ntt<..., CONV> (one target per block; A/B)
         const char* v = std::getenv("SFHE_MODUP_COL");
         return !v || *v != '0';
@@ -4713,6 +4831,9 @@ static void nttRows(sfp_dev* d, const RowGroup& G0, int inverse, int passes = 3)
             if (G.cy)
                 pass(k_ntt<false, true, 2, T, 1, true>, k_ntt<false, true, 2, T, 2, true>,
                      k_ntt<false, true, 2, T, 4, true>, k_ntt<false, true, 2, T, 8, true>, T >> 2);
+            else if (G.icol)
+                pass(k_ntt<false, true, 2, T, 1, false, true>, k_ntt<false, true, 2, T, 2, false, true>,
+                     k_ntt<false, true, 2, T, 4, false, true>, k_ntt<false, true, 2, T, 8, false, true>, T >> 2);
             else
                 pass(k_ntt<false, true, 2, T>, k_ntt<false, true, 2, T, 2>, k_ntt<false, true, 2, T, 4>, k_ntt<false, true, 2, T, 8>, T >> 2);
             pass(k_ntt<false, false, 2, T>, k_ntt<false, false, 2, T, 2>, k_ntt<false, false, 2, T, 4>, k_ntt<false, false, 2, T, 8>, T >> 2);
@@ -4889,6 +5010,19 @@ static uint32_t kernelFamily(const void* f) {
                               (const void*)k_ntt<false, true, 2, 1024, 1, true>, (const void*)k_ntt<false, true, 2, 1024, 2, true>,
                               (const void*)k_ntt<false, true, 2, 1024, 4, true>, (const void*)k_ntt<false, true, 2, 1024, 8, true>})
             m[k] = SFP_FAM_NTT;  // (the ModUp COL pass with its conversion)
+        for (const void* k : {(const void*)k_ntt<false, true, 2, kNttTile, 1, false, true>,
+                              (const void*)k_ntt<false, true, 2, kNttTile, 2, false, true>,
+                              (const void*)k_ntt<false, true, 2, kNttTile, 4, false, true>,
+                              (const void*)k_ntt<false, true, 2, kNttTile, 8, false, true>,
+                              (const void*)k_ntt<false, true, 2, 1024, 1, false, true>,
+                              (const void*)k_ntt<false, true, 2, 1024, 2, false, true>,
+                              (const void*)k_ntt<false, true, 2, 1024, 4, false, true>,
+                              (const void*)k_ntt<false, true, 2, 1024, 8, false, true>,
+                              (const void*)k_ntt<false, true, 2, 512, 1, false, true>,
+                              (const void*)k_ntt<false, true, 2, 512, 2, false, true>,
+                              (const void*)k_ntt<false, true, 2, 512, 4, false, true>,
+                              (const void*)k_ntt<false, true, 2, 512, 8, false, true>})
+            m[k] = SFP_FAM_NTT;  // (a rescale's lift pass with its source's inverse COL pass: a row's read + write)
         for (const void* k : {(const void*)k_modup_col<kNttTile, 1, kModupTg>, (const void*)k_modup_col<kNttTile, 2, kModupTg>,
                               (const void*)k_modup_col<kNttTile, 4, kModupTg>, (const void*)k_modup_col<kNttTile, 8, kModupTg>,
                               (const void*)k_modup_col<1024, 1, kModupTg>, (const void*)k_modup_col<1024, 2, kModupTg>,
@@ -5269,11 +5403,20 @@ static void rescaleCore(sfp_dev* d, uint64_t* out, const uint64_t* in, uint32_t 
         A.preK = dmk + 2 * cnt;
         A.preKS = dmk + 2 * cnt + 1;
     }
-    nttRows(d, A, 1);
+    // the dropped row's inverse COL pass runs in the lift pass's prologue
+    // (icol) where that pass has one: one dependent launch fewer per rescale
+    const bool icol = icolPath(d, npoly * cnt);
+    nttRows(d, A, 1, icol ? 1 : 3);
     RowGroup B = rowsOf(npoly, cnt, sfp_limbs{cnt, cnt, 0, 0});
     B.src = RowPtr{last, (long long)n, 0};
     B.lift = 1;
     B.liftPrime = dropPrime;
+    if (icol) {
+        B.icol = 1;
+        B.iTw = d->ipsi;
+        B.iTwS = d->ipsiS;
+        B.iTwD = d->ipsiD;
+    }
     B.dst = RowPtr{tmp, (long long)cnt * n, (long long)n};
     B.epi = 1;
     B.ein = RowPtr{in, (long long)inStride, (long long)n};
@@ -6488,11 +6631,51 @@ void sfp_group_set_host(sfp_dev* d, int group, int groups, sfp_host_allgather_fn
     d->gHostUser = user;
 }
 
+// One collective of sfp_comm_stats: counted, and bracketed by events on its
+// stream when timing is on and nothing is being captured.
+template <class F>
+static void commIssue(sfp_dev* d, double received, F&& go) {
+    d->commCalls++;
+    d->commBytes += received;
+    if (!d->commTimed || d->capture) return go();
+    hipEvent_t a = takeEvent(d), b = takeEvent(d);
+    SFP_CHECK(hipEventRecord(a, d->st()));
+    go();
+    SFP_CHECK(hipEventRecord(b, d->st()));
+    d->commEv.push_back({a, b});
+}
+
+void sfp_comm_stats_reset(sfp_dev* d, int timed) {
+    syncAll(d);
+    for (auto& e : d->commEv) {
+        d->evPool.push_back(e.first);
+        d->evPool.push_back(e.second);
+    }
+    d->commEv.clear();
+    d->commCalls = 0;
+    d->commBytes = 0;
+    d->commTimed = timed != 0;
+}
+
+void sfp_comm_stats(sfp_dev* d, uint64_t* calls, double* bytes, double* ms) {
+    syncAll(d);
+    double t = 0;
+    for (auto& e : d->commEv) {
+        float x = 0;
+        if (hipEventElapsedTime(&x, e.first, e.second) == hipSuccess) t += x;
+    }
+    if (calls) *calls = d->commCalls;
+    if (bytes) *bytes = d->commBytes;
+    if (ms) *ms = t;
+}
+
 void sfp_group_allgather(sfp_dev* d, const void* send, void* recv, size_t bytes) {
     if (d->gnccl) {
         stackFlush(d);  // (collectives are issued in program order)
-        ncclCheck(d, "ncclAllGather (groups)",
-                  rcclApi().allGather(send, recv, bytes, ncclUint8, d->gnccl, d->st()));
+        commIssue(d, (double)bytes * (d->gworld - 1), [&] {
+            ncclCheck(d, "ncclAllGather (groups)",
+                      rcclApi().allGather(send, recv, bytes, ncclUint8, d->gnccl, d->st()));
+        });
         return;
     }
     if (d->gworld == 1) {
@@ -6503,10 +6686,12 @@ void sfp_group_allgather(sfp_dev* d, const void* send, void* recv, size_t bytes)
         record(d, "group allgather (no communicator)", hipErrorInvalidValue);
         return;
     }
-    std::vector<char> hs(bytes), hr(bytes * d->gworld);
-    devToHost(d, hs.data(), send, bytes);
-    d->gHostAg(d->gHostUser, hs.data(), hr.data(), bytes);
-    hostToDev(d, recv, hr.data(), hr.size());
+    commIssue(d, (double)bytes * (d->gworld - 1), [&] {
+        std::vector<char> hs(bytes), hr(bytes * d->gworld);
+        devToHost(d, hs.data(), send, bytes);
+        d->gHostAg(d->gHostUser, hs.data(), hr.data(), bytes);
+        hostToDev(d, recv, hr.data(), hr.size());
+    });
 }
 
 void sfp_comm_set_host(sfp_dev* d, int rank, int world, sfp_host_allgather_fn ag, sfp_host_bcast_fn bc,
@@ -6533,32 +6718,41 @@ void sfp_allgather(sfp_dev* d, const void* send, void* recv, size_t bytes) {
     }
     if (d->nccl) {
         stackFlush(d);  // (collectives are issued in program order)
-        ncclCheck(d, "ncclAllGather", rcclApi().allGather(send, recv, bytes, ncclUint8, d->nccl, d->st()));
+        commIssue(d, (double)bytes * (d->world - 1), [&] {
+            ncclCheck(d, "ncclAllGather", rcclApi().allGather(send, recv, bytes, ncclUint8, d->nccl, d->st()));
+        });
         return;
     }
     if (!d->hostAg) {
         record(d, "allgather (no communicator)", hipErrorInvalidValue);
         return;
     }
-    std::vector<char> hs(bytes), hr(bytes * d->world);
-    devToHost(d, hs.data(), send, bytes);
-    d->hostAg(d->hostUser, hs.data(), hr.data(), bytes);
-    hostToDev(d, recv, hr.data(), hr.size());
+    commIssue(d, (double)bytes * (d->world - 1), [&] {
+        std::vector<char> hs(bytes), hr(bytes * d->world);
+        devToHost(d, hs.data(), send, bytes);
+        d->hostAg(d->hostUser, hs.data(), hr.data(), bytes);
+        hostToDev(d, recv, hr.data(), hr.size());
+    });
 }
 
 void sfp_bcast(sfp_dev* d, void* buf, size_t bytes, int root) {
     if (d->world == 1 && !d->nccl) return;
+    const double got = d->rank == root ? 0.0 : (double)bytes;
     if (d->nccl) {
         stackFlush(d);  // (collectives are issued in program order)
-        ncclCheck(d, "ncclBroadcast", rcclApi().broadcast(buf, buf, bytes, ncclUint8, root, d->nccl, d->st()));
+        commIssue(d, got, [&] {
+            ncclCheck(d, "ncclBroadcast", rcclApi().broadcast(buf, buf, bytes, ncclUint8, root, d->nccl, d->st()));
+        });
         return;
     }
     if (!d->hostBc) {
         record(d, "bcast (no communicator)", hipErrorInvalidValue);
         return;
     }
-    std::vector<char> h(bytes);
-    devToHost(d, h.data(), buf, bytes);
-    d->hostBc(d->hostUser, h.data(), bytes, root);
-    hostToDev(d, buf, h.data(), bytes);
+    commIssue(d, got, [&] {
+        std::vector<char> h(bytes);
+        devToHost(d, h.data(), buf, bytes);
+        d->hostBc(d->hostUser, h.data(), bytes, root);
+        hostToDev(d, buf, h.data(), bytes);
+    });
 }

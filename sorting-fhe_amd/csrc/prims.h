@@ -360,8 +360,10 @@ void sfp_stack_stats(sfp_dev* d, uint64_t* merged, uint64_t* single);
 // issues everything on the caller's lane, identical launches of different ops
 // merged into one (up to eight; four for the element-wise kernels).  The ops' buffers must stay allocated until
 // sfp_batch_end (their launches are issued there).  Returns 0 (the ops run as
-// issued) for the oracle, with SFHE_BATCH=0, inside a stacked lane region or
-// with serialised lanes.
+// issued) for the oracle, with SFHE_BATCH=0 or inside a stacked lane region.
+// Serialised lanes (sfp_serialize) still batch: a profiling sort then issues
+// the same merged launches as the captured sort, each timed as ONE launch
+// carrying the bytes of every op merged into it.
 #define SFP_BATCH_MAX 8
 int sfp_batch_begin(sfp_dev* d, uint32_t count);
 void sfp_batch_lane(sfp_dev* d, uint32_t i);
@@ -396,6 +398,17 @@ int sfp_group_init_rccl(sfp_dev* d, int group, int groups, const void* uid128);
 void sfp_group_set_host(sfp_dev* d, int group, int groups, sfp_host_allgather_fn ag, void* user);
 // recv = groups blocks of `bytes`, group-major (recv may contain send in place)
 void sfp_group_allgather(sfp_dev* d, const void* send, void* recv, size_t bytes);
+
+// Collective statistics (multi-GPU attribution: the bench splits a sharded
+// sort's time into compute and exchange).  sfp_comm_stats_reset zeroes the
+// counters; timed != 0 also brackets every collective with events on the
+// stream it runs on (eager work only: a captured collective is counted, not
+// timed).  sfp_comm_stats: collectives this rank issued since the reset (the
+// all-gathers and broadcasts of both communicators that moved data), the
+// bytes this rank received through them, and their summed duration in ms
+// (0 unless timed).  Synchronises the lanes.
+void sfp_comm_stats_reset(sfp_dev* d, int timed);
+void sfp_comm_stats(sfp_dev* d, uint64_t* calls, double* bytes, double* ms);
 
 // dst row i = src row rows[i] (count rows of n words; rows: host array)
 void sfp_gather_rows(sfp_dev* d, uint64_t* dst, const uint64_t* src, const uint32_t* rows, uint32_t count);

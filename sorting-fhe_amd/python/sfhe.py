@@ -35,7 +35,7 @@ ABI_SYMBOLS = [
     "sfhe_sorter_destroy", "sfhe_sorter_sort", "sfhe_sorter_rank", "sfhe_sorter_place",
     "sfhe_decompose", "sfhe_kernel_timing", "sfhe_kernel_timing_read",
     "sfhe_comm_uid", "sfhe_shard_rccl", "sfhe_shard_host", "sfhe_pool_bytes", "sfhe_live_contexts",
-    "sfhe_serialize_lanes", "sfhe_stack_stats", "sfhe_sorter_graph_nodes", "sfhe_sorter_create_rot",
+    "sfhe_serialize_lanes", "sfhe_stack_stats", "sfhe_comm_stats_reset", "sfhe_comm_stats", "sfhe_sorter_graph_nodes", "sfhe_sorter_create_rot",
     "sfhe_sorter_sort_hybrid1", "sfhe_hybrid1_params", "sfhe_sorter_graph_ntt_time",
     "sfhe_sorter_graph_family_time",
     "sfhe_sorter_sort_hybrid", "sfhe_hybrid_params", "sfhe_sorter_place_2n",
@@ -148,6 +148,8 @@ _SIGS = {
     "sfhe_kernel_timing": (C.c_int, [_VP, _U32, _U32]),
     "sfhe_serialize_lanes": (C.c_int, [_VP, C.c_int]),
     "sfhe_stack_stats": (C.c_int, [_VP, _PU64, _PU64]),
+    "sfhe_comm_stats_reset": (C.c_int, [_VP, C.c_int]),
+    "sfhe_comm_stats": (C.c_int, [_VP, _PU64, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "sfhe_kernel_timing_read": (C.c_int, [_VP, _U32, _PU64, _PU64, _PD, _PD]),
     "sfhe_decompose": (C.c_int, [_U32, _PI32, _SZ, C.c_int32, C.c_int32, C.c_int, _PI32, _PI32, _SZ, _PSZ]),
     "sfhe_comm_uid": (C.c_int, [_VP]),
@@ -172,7 +174,7 @@ def lib_path(backend: str = "hip") -> str:
     return os.environ.get("SFHE_PRODUCT_LIB", PRODUCT_LIB) if backend == "hip" else ORACLE_LIB
 
 
-ABI_VERSION = 2  # include/sfhe.h SFHE_ABI_VERSION
+ABI_VERSION = 3  # include/sfhe.h SFHE_ABI_VERSION
 
 
 def load(backend: str = "hip"):
@@ -397,6 +399,16 @@ class Engine:
         m, s1 = C.c_uint64(), C.c_uint64()
         self._chk(self.lib.sfhe_stack_stats(self.ctx, C.byref(m), C.byref(s1)))
         return m.value, s1.value
+
+    def comm_stats_reset(self, timed: bool = True):
+        """Zero the collective counters (timed: also time each eager collective)."""
+        self._chk(self.lib.sfhe_comm_stats_reset(self.ctx, 1 if timed else 0))
+
+    def comm_stats(self) -> dict:
+        """Collectives this rank issued since comm_stats_reset: calls, bytes received, ms."""
+        n, by, ms = C.c_uint64(), C.c_double(), C.c_double()
+        self._chk(self.lib.sfhe_comm_stats(self.ctx, C.byref(n), C.byref(by), C.byref(ms)))
+        return {"calls": n.value, "bytes": by.value, "ms": ms.value}
 
     def kernel_timing_read(self, family: str) -> dict:
         la, ti = C.c_uint64(), C.c_uint64()

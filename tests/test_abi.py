@@ -35,7 +35,7 @@ def test_abi_version_and_backends(oracle_lib):
     lib = ctypes.CDLL(sfhe.PRODUCT_LIB)
     lib.sfhe_abi_version.restype = ctypes.c_int
     lib.sfhe_backend.restype = ctypes.c_char_p
-    assert lib.sfhe_abi_version() == sfhe.ABI_VERSION == 2
+    assert lib.sfhe_abi_version() == sfhe.ABI_VERSION == 3
     assert lib.sfhe_backend() == b"hip-gfx950"
     assert oracle_lib.sfhe_backend() == b"oracle-c"
 

@@ -81,9 +81,13 @@ def _sharded_worker(rank, world, port, q, groups=1, N=8):
         out["ct"] = sorter.sort(ct, *spec["cfg"])
 
     dt = bench.timed_steps(step, eng.sync, w, steps=1, warmup=0)
+    # the bench's collective attribution (its profiling sort): one more sort with the counters on
+    eng.comm_stats_reset(timed=True)
+    step()
+    comm = eng.comm_stats()
     line = bench.fallback_line(rep, spec, w, type("A", (), {"steps": 1, "warmup": 0, "workload": "t"})(), "test")
     q.put((r, dt, rep["value"], out["ct"].download(), eng.shard_tail(), line["scaling"],
-           bench.parallelism(w, groups, "gloo", eng.shard_tail())))
+           bench.parallelism(w, groups, "gloo", eng.shard_tail()), comm))
     import torch.distributed as dist
     dist.destroy_process_group()
 
@@ -115,6 +119,12 @@ def test_sharded_bench_flow(oracle_lib, world, groups, N, label):
     ct0 = res[0][3]
     for t in res[1:]:
         assert np.array_equal(ct0, t[3])              # every rank holds the whole result
+    for t in res:  # every rank exchanged data in its sort, and timed it
+        c = t[7]
+        assert c["calls"] > 0 and c["bytes"] > 0 and c["ms"] > 0, c
+    per = world // groups                             # (rank = group * per + in-group rank)
+    for g in range(groups):                           # one batch group's ranks issue the same collectives
+        assert len({t[7]["calls"] for t in res[g * per:(g + 1) * per]}) == 1, [t[7] for t in res]
     depth, rots = sfhe.direct_sort_params(N, "oracle")
     ref = sfhe.Engine("oracle", mult_depth=depth, ring_dim=1 << 12, batch_size=N, rotations=rots,
                       seed=20251205 + N)

@@ -263,7 +263,17 @@ def test_direct_sort_h2test_large_fails_as_attributed(hip_lib):
     The test draws a fresh input every run (tests/utils.h shuffles with
     std::random_device), and at N = 256 the error straddles the gate
     (0.0097 ... 0.026 over runs): N = 256 may pass or fail, N = 512 and 1024
-    always fail."""
+    always fail.
+
+    Gates per N, from the runs on record (each the maximum over the N hits of
+    the series' rounding noise, so it spreads from run to run): N = 256
+    0.0097 / 0.026 (rounds 3, 5), N = 512 0.072 / 0.073, N = 1024 0.25 /
+    0.381 (round 3; round 5, gpurun_out/r05m_gpu_tests.log).  Each window is
+    the observed range widened x2 to x3 on either side; and the attributed
+    mechanism (noise x4 per giant-step doubling, one more doubling per
+    doubling of N) makes the error grow with N, which is asserted too --
+    a regression of a different kind (a wrong level, a wrong polynomial)
+    breaks either the windows or the order."""
     rc, out = run(exe("DirectSortH2Test"), "--gtest_filter=*/6.*:*/7.*:*/8.*", timeout=600)
     errs = [float(x) for x in re.findall(r"Maximum error: ([0-9.e+-]+)", out)]
     levels = [int(x) for x in re.findall(r"Result Level: (\d+)", out)]
@@ -271,8 +281,10 @@ def test_direct_sort_h2test_large_fails_as_attributed(hip_lib):
     assert rc != 0
     assert "3 tests ran, 3 failed" in out or "3 tests ran, 2 failed" in out, out[-3000:]
     assert len(errs) == 3, errs
-    assert 0.005 < errs[0] < 0.6, errs  # N = 256: either side of the gate
-    assert all(0.01 < e < 0.6 for e in errs[1:]), errs
+    windows = ((0.004, 0.08), (0.025, 0.22), (0.08, 0.9))  # N = 256 (either side of 0.01), 512, 1024
+    assert all(lo < e < hi for e, (lo, hi) in zip(errs, windows)), errs
+    assert errs[1] > 0.01 and errs[2] > 0.01, errs  # 512 and 1024 fail the reference's gate
+    assert errs[0] < errs[1] < errs[2], errs  # grows with N, as the attribution predicts
     assert "unexpected exception" not in out, out[-3000:]
     assert "Use the level returned" not in out, out[-3000:]  # the level gate holds
 

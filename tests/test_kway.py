@@ -125,14 +125,18 @@ def test_kway_handle_oracle(oracle_lib):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("N,k,M,logn", [(8, 2, 3, 12), (27, 3, 3, 13)])
-def test_kway_graph_replay_hip(hip_lib, oracle_lib, N, k, M, logn):
+@pytest.mark.parametrize("N,k,M,logn,chunk", [(8, 2, 3, 12, None), (27, 3, 3, 13, None), (8, 2, 3, 12, "2")])
+def test_kway_graph_replay_hip(hip_lib, oracle_lib, N, k, M, logn, chunk, monkeypatch):
     """The k-way network as a hipGraph (BASELINE config 4): a persistent
     adapter sorts eagerly, then captures the whole sort -- every stage's
     comparisons, masked rotations and sub-sorters with the bootstraps between
     them -- and replays it.  Eager, captured and replayed sorts are the
     oracle's residues bit for bit; a new input through the replayed graph
-    sorts correctly."""
+    sorts correctly.  chunk = "2": SFHE_KWAY_CHUNK=2 (read at every sort), so
+    the six stages of M = 3 are captured as a CHAIN of three graphs, each
+    reading the previous one's output (config 4's N = 1024 runs four)."""
+    if chunk is not None:
+        monkeypatch.setenv("SFHE_KWAY_CHUNK", chunk)
     batch, depth, budget, rots = sfhe.kway_params(N, "hip")
     kw = dict(mult_depth=depth, ring_dim=1 << logn, batch_size=batch, scaling_mod_size=59, rotations=rots,
               seed=11)
@@ -148,7 +152,7 @@ def test_kway_graph_replay_hip(hip_lib, oracle_lib, N, k, M, logn):
     ct = e.encrypt(x.tolist())
     outs = [s.sort(ct, 3, 2, 2, depth) for _ in range(3)]  # eager, captured, replayed
     nodes = s.graph_nodes()
-    print(f"k-way N={N} (k={k}, M={M}) @ 2^{logn}: graph of {nodes} nodes")
+    print(f"k-way N={N} (k={k}, M={M}) @ 2^{logn}, chunk {chunk or 14}: graph of {nodes} nodes")
     assert nodes > 100
     for i, o in enumerate(outs):
         assert np.array_equal(o.download(), want), f"sort {i} differs from the oracle"
