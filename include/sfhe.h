@@ -221,8 +221,9 @@ int sfhe_sorter_graph_nodes(const sfhe_sorter* s, uint64_t* nodes);
  * coefficient per pass).  SFHE_EINVAL-class error when no graph exists. */
 int sfhe_sorter_graph_ntt_time(sfhe_sorter* s, int reps, double* ms, uint64_t* launches, double* bytes);
 /* The same for any family SFHE_KFAM_* (OTHER: the kernels of no family, ALL:
- * every kernel node -- the sort's kernel time without lane overlap); *bytes
- * counts the NTT passes only. */
+ * every kernel node -- the sort's kernel time without lane overlap); *bytes:
+ * the algorithmic bytes of the family's kernels for NTT, CONV and NTTKS
+ * (sources read and targets written once), 0 for the others. */
 int sfhe_sorter_graph_family_time(sfhe_sorter* s, uint32_t family, int reps, double* ms, uint64_t* launches,
                                   double* bytes);
 /* DirectSort<N>::sort_hybrid1 (sort_algo.h:1213-1229): constructRank, then
@@ -286,6 +287,12 @@ void sfhe_kway_destroy(sfhe_kway* s);
  * a shape runs eagerly, the second is captured whole -- stages and the
  * bootstraps between them -- and later sorts replay it (SFHE_GRAPH=0: eager). */
 int sfhe_kway_graph_nodes(const sfhe_kway* s, uint64_t* nodes);
+/* The captured k-way sort's kernels of one family (SFHE_KFAM_*) replayed
+ * alone, summed over its chain of graphs: ms per sort, launches, and their
+ * algorithmic bytes (NTT, conversion and k_ntt_ks families; 0 for others).
+ * No reference counterpart (bench attribution of BASELINE config 4). */
+int sfhe_kway_graph_family_time(sfhe_kway* s, uint32_t family, int reps, double* ms, uint64_t* launches,
+                                double* bytes);
 /* KWayAdapter<N>::getSizeParameters (kway_adapter.h:41-64): batch (next power
  * of two >= N), depth 40, first modulus 60 / scale 59 bits, level budget
  * {4,4} (N <= 128) or {5,5}, the +-2^i rotation keys below N. */

@@ -122,6 +122,25 @@ class KWayAdapter : public SortBase<N> {
             for (const auto& cg : m_graph->chain) n += m_cc->GraphNodes(cg);
         return n;
     }
+    // the chain's kernels of one family replayed alone, graph by graph
+    // (sfp_graph_family_time), summed over the chain: per sort
+    bool graphFamilyTime(uint32_t family, int reps, double* ms, uint64_t* launches, double* bytes) {
+        if (!m_graph || m_graph->chain.empty()) return false;
+        double tms = 0, tb = 0;
+        uint64_t tn = 0;
+        for (const auto& cg : m_graph->chain) {
+            double m = 0, b = 0;
+            uint64_t n = 0;
+            if (!m_cc->GraphFamilyTime(cg, family, reps, &m, &n, &b)) continue;  // (no kernel of it there)
+            tms += m;
+            tn += n;
+            tb += b;
+        }
+        if (ms) *ms = tms;
+        if (launches) *launches = tn;
+        if (bytes) *bytes = tb;
+        return tn > 0;
+    }
     ~KWayAdapter() override { m_graph.reset(); }
 
   private:

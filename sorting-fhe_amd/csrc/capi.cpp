@@ -615,6 +615,7 @@ struct KWayBase {
     virtual ~KWayBase() = default;
     virtual Ct run(const Ct& in, SignConfig& cfg) = 0;
     virtual size_t graphNodes() const = 0;
+    virtual bool graphFamilyTime(uint32_t family, int reps, double* ms, uint64_t* launches, double* bytes) = 0;
 };
 template <int N>
 struct KWayImpl : KWayBase {
@@ -624,6 +625,9 @@ struct KWayImpl : KWayBase {
             std::make_shared<Encryption>(c->cc, c->keys.publicKey), k, M) {}
     Ct run(const Ct& in, SignConfig& cfg) override { return a.sort(in, SignFunc::CompositeSign, cfg); }
     size_t graphNodes() const override { return a.graphNodes(); }
+    bool graphFamilyTime(uint32_t family, int reps, double* ms, uint64_t* launches, double* bytes) override {
+        return a.graphFamilyTime(family, reps, ms, launches, bytes);
+    }
 };
 std::unique_ptr<KWayBase> makeKWay(sfhe_ctx* c, uint32_t N, int k, int M) {
     switch (N) {
@@ -669,6 +673,16 @@ int sfhe_kway_run(sfhe_kway* s, const sfhe_ct* in, int n, int dg, int df, uint32
 }
 
 void sfhe_kway_destroy(sfhe_kway* s) { delete s; }
+
+int sfhe_kway_graph_family_time(sfhe_kway* s, uint32_t family, int reps, double* ms, uint64_t* launches,
+                                double* bytes) {
+    REQUIRE(s && ms && reps > 0, "null argument");
+    REQUIRE(family <= SFHE_KFAM_ALL, "unknown kernel family");
+    return guard([&] {
+        if (!s->impl->graphFamilyTime(family, reps, ms, launches, bytes))
+            throw std::runtime_error("no captured k-way graph with kernels of that family");
+    });
+}
 
 int sfhe_kway_graph_nodes(const sfhe_kway* s, uint64_t* nodes) {
     REQUIRE(s && nodes, "null argument");

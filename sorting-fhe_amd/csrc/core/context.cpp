@@ -658,26 +658,118 @@ class SfheInternal {
     // and part, the tail Q rows, the rank's dealt Q rows above the tail and
     // the P rows -- every row a replicated level or this rank's dealt rows
     // read.
-    static DeviceBufferPtr sliceKey(SfheContextState* s, const DeviceBufferPtr& whole) {
+    // A tier's key (one digit over Lq + K' rows) takes the same layout: its
+    // K' P rows at pstart.., the slots of the P primes it lacks zero.
+    static DeviceBufferPtr sliceKey(SfheContextState* s, const DeviceBufferPtr& whole, int tier = -1) {
         const sfp_key_geom& g = s->kgeom;
-        const uint32_t n = s->n, NP = s->Lq + s->K;
+        const uint32_t n = s->n, NP = s->Lq + s->Kof(tier), digits = tier < 0 ? s->dnum : 1;
         std::vector<uint32_t> rows;
-        for (uint32_t p = 0; p < NP; ++p) {
+        for (uint32_t p = 0; p < s->Lq + s->K; ++p) {
             const bool keep = p < g.tail || p >= s->Lq || p % g.world == (uint32_t)s->rank;
             if (!keep) continue;
             if (sfp_key_row(&g, p) != rows.size()) SFHE_THROW("internal: key slice row map");
             rows.push_back(p);
         }
         if (rows.size() != g.rows) SFHE_THROW("internal: key slice size");
-        auto out = s->alloc((size_t)s->dnum * 2 * g.rows * n);
-        for (uint32_t part = 0; part < 2 * s->dnum; ++part)
-            sfp_gather_rows(s->dev, out->ptr + (size_t)part * g.rows * n, whole->ptr + (size_t)part * NP * n,
-                            rows.data(), g.rows);
+        auto out = s->alloc((size_t)digits * 2 * g.rows * n);
+        out->ksTier = tier;
+        const uint32_t have = NP < s->Lq + s->K ? g.pstart + (NP - s->Lq) : g.rows;  // rows a tier key fills
+        for (uint32_t part = 0; part < 2 * digits; ++part) {
+            uint64_t* o = out->ptr + (size_t)part * g.rows * n;
+            sfp_gather_rows(s->dev, o, whole->ptr + (size_t)part * NP * n, rows.data(), have);
+            if (have < g.rows) sfp_zero(s->dev, o + (size_t)have * n, (size_t)(g.rows - have) * n * 8);
+        }
         return out;
+    }
+
+    // modupConvShard split for the overlapped ModUp: per digit (own rows'
+    // part, the rest's part); the own rows of digit j are local rows
+    // ceil((j alpha - rank) / W) .. in this rank's coefficient buffer
+    static std::vector<std::pair<sfp_conv*, sfp_conv*>>& modupConvSplit(SfheContextState* s, uint32_t ell) {
+        auto it = s->modupConvSplit.find(ell);
+        if (it != s->modupConvSplit.end()) return it->second;
+        std::vector<std::pair<sfp_conv*, sfp_conv*>> v;
+        const uint32_t beta = (ell + s->alpha - 1) / s->alpha;
+        std::vector<uint32_t> dst;
+        for (uint32_t i = 0; i < s->owned(ell); ++i) dst.push_back(s->qprimeShard(i));
+        for (uint32_t k = 0; k < s->owned(s->K); ++k) dst.push_back(s->Lq + s->rank + k * s->world);
+        for (uint32_t j = 0; j < beta; ++j) {
+            std::vector<uint32_t> src;
+            std::vector<char> own, rest;
+            for (uint32_t i = j * s->alpha; i < std::min((j + 1) * s->alpha, ell); ++i) {
+                src.push_back(i);
+                own.push_back(i % s->world == (uint32_t)s->rank);
+                rest.push_back(!own.back());
+            }
+            const bool any = std::find(own.begin(), own.end(), 1) != own.end();
+            v.push_back({any ? makeConv(s, src, dst, nullptr, &own, false) : nullptr,
+                         makeConv(s, src, dst, nullptr, &rest, true)});
+        }
+        return s->modupConvSplit[ell] = v;
+    }
+
+    // The overlapped ModUp (SFHE_SHARD_OVERLAP, on by default): the all-gather
+    // of the coefficient rows runs on a lane of its own while this lane
+    // converts the rank's OWN rows of every digit (they need no exchange);
+    // then the rest's part is added (the parts sum mod each target prime to
+    // the whole conversion: the same residues) and the NTT runs.  Without a
+    // spare lane (the oracle's single synchronous lane, a region using every
+    // lane) the same split runs in order on this lane.  Returns false with
+    // SFHE_SHARD_OVERLAP=0 (the caller runs the unsplit form).
+    static bool modupShardOverlap(SfheContextState* s, uint64_t* ext, const uint64_t* d, uint32_t ell) {
+        static const bool on = [] {
+            const char* v = std::getenv("SFHE_SHARD_OVERLAP");
+            return !v || *v != '0';
+        }();
+        if (!on) return false;
+        const int L = sfp_get_lane(s->dev), C0 = sfp_lanes(s->dev) - 1;
+        const int C = (C0 > L && C0 >= std::max(1, s->forkedLanes)) ? C0 : L;
+        const uint32_t n = s->n, beta = (ell + s->alpha - 1) / s->alpha, W = (uint32_t)s->world;
+        const uint32_t per = (ell + W - 1) / W, lr = s->owned(ell);
+        const sfp_limbs em = s->extmap(ell);
+        const size_t stride = (size_t)em.count * n;
+        auto& parts = modupConvSplit(s, ell);
+        auto send = s->alloc((size_t)per * n);
+        auto all = s->alloc((size_t)per * W * n);
+        auto nat = s->alloc((size_t)ell * n);
+        auto tmp = s->alloc(stride);
+        if (lr) {
+            sfp_d2d(s->dev, send->ptr, d, (size_t)lr * n * 8);
+            sfp_ntt(s->dev, send->ptr, s->shardMap(ell), 1);
+        }
+        // the exchange on lane C, after this lane's INTT
+        if (C != L) {
+            sfp_lane_wait(s->dev, C, L);
+            sfp_set_lane(s->dev, C);
+        }
+        sfp_allgather(s->dev, send->ptr, all->ptr, (size_t)per * n * 8);
+        auto idx = naturalOrder(s, ell, per);
+        sfp_gather_rows(s->dev, nat->ptr, all->ptr, idx.data(), ell);
+        sfp_set_lane(s->dev, L);
+        // meanwhile: every digit's conversion of this rank's own rows
+        for (uint32_t j = 0; j < beta; ++j) {
+            uint64_t* e = ext + j * stride;
+            const uint32_t lo = j * s->alpha;
+            const uint32_t first = (lo + W - 1 - (uint32_t)s->rank) / W;  // local index of its first own row
+            if (parts[j].first)
+                sfp_conv_apply(s->dev, e, send->ptr + (size_t)first * n, parts[j].first);
+            else
+                sfp_zero(s->dev, e, stride * 8);
+        }
+        // the rest's part once the rows arrived, then the NTT
+        if (C != L) sfp_lane_wait(s->dev, L, C);
+        for (uint32_t j = 0; j < beta; ++j) {
+            uint64_t* e = ext + j * stride;
+            sfp_conv_apply(s->dev, tmp->ptr, nat->ptr + (size_t)j * s->alpha * n, parts[j].second);
+            sfp_add(s->dev, e, e, tmp->ptr, em);
+            sfp_ntt(s->dev, e, em, 0);
+        }
+        return true;
     }
 
     // ModUp of the local rows of d (ell limbs, dealt): beta blocks of extmap(ell) rows
     static void modupShard(SfheContextState* s, uint64_t* ext, const uint64_t* d, uint32_t ell) {
+        if (modupShardOverlap(s, ext, d, ell)) return;
         const uint32_t n = s->n, beta = (ell + s->alpha - 1) / s->alpha;
         const sfp_limbs em = s->extmap(ell);
         const size_t stride = (size_t)em.count * n;
@@ -838,12 +930,12 @@ class SfheInternal {
                           const uint64_t* fold0, const uint64_t* fold1, u64 foldK, int accum,
                           uint32_t invFrom = ~0u) {
         SfheContextState* s = cc->st.get();
-        const uint32_t n = s->n, K = s->K;
+        const uint32_t n = s->n, K = s->Kof(key->ksTier);  // (the key's special-prime tier)
         const uint32_t beta = (ell + s->alpha - 1) / s->alpha;
         const size_t stride = (size_t)(ell + K) * n;
         auto ext = s->alloc(stride * beta);
         auto scratch = s->alloc((size_t)ell * n);
-        auto& convs = modupConv(cc, ell);
+        auto& convs = modupConv(cc, ell, key->ksTier);
         if (sfp_modup_inner(s->dev, acc, acc + stride, d, ell, K, s->Lq, s->alpha, convs.data(), key->ptr, fold0,
                             fold1, foldK, accum, invFrom, ext->ptr, scratch->ptr) == 0)
             return invFrom != ~0u;
@@ -863,14 +955,15 @@ class SfheInternal {
                           uint64_t* out0, uint64_t* out1, int add0, int add1) {
         SfheContextState* s = cc->st.get();
         if (s->shardAt(ell)) return keySwitchShard(cc, d, ell, key, out0, out1, add0, add1);
-        const uint32_t n = s->n, K = s->K;
+        const int tier = key->ksTier;
+        const uint32_t n = s->n, K = s->Kof(tier);
         const uint32_t beta = (ell + s->alpha - 1) / s->alpha;
         const size_t stride = (size_t)(ell + K) * n;
         auto acc = s->alloc(2 * stride);
         const int rowDone = modupInner(cc, acc->ptr, d, ell, key, nullptr, nullptr, 0, 0, ell);
         auto md = s->alloc((size_t)2 * ell * n);
-        sfp_moddown2(s->dev, out0, out1, acc->ptr, stride, ell, K, s->Lq, s->moddownConv, s->pInvModQ.data(), add0,
-                     add1, md->ptr, rowDone);
+        sfp_moddown2(s->dev, out0, out1, acc->ptr, stride, ell, K, s->Lq, s->moddownConvOf(tier), s->pInvModQof(tier),
+                     add0, add1, md->ptr, rowDone);
         s->stats.keyswitch++;
         // (3 l + 2 beta (l+K)) B
         s->countBytes((3.0 * ell + 2.0 * beta * (ell + K)) * n * 8);
@@ -888,15 +981,17 @@ class SfheInternal {
             keySwitchShard(cc, d2, ell, s->relinKey, d0, d1, 1, 1);
             return rescale(cc, d0, d1, level, slots);
         }
-        const uint32_t n = s->n, K = s->K;
+        const DeviceBufferPtr& key = s->relinFor(ell);
+        const int tier = key->ksTier;
+        const uint32_t n = s->n, K = s->Kof(tier);
         const uint32_t beta = (ell + s->alpha - 1) / s->alpha;
         const size_t stride = (size_t)(ell + K) * n;
         auto acc = s->alloc(2 * stride);
-        const int rowDone = modupInner(cc, acc->ptr, d2, ell, s->relinKey, d0, d1, s->pModQ[ell - 1], 0, ell - 1);
+        const int rowDone = modupInner(cc, acc->ptr, d2, ell, key, d0, d1, s->pModQof(tier)[ell - 1], 0, ell - 1);
         Ct out = newCt(cc, level + 1, slots);
         auto scratch = s->alloc((size_t)2 * (ell - 1) * n);
         sfp_moddown_rescale(s->dev, out->c0, out->c1, d0, d1, acc->ptr, stride, ell, K, s->Lq,
-                            s->moddownConv, s->pInvModQ.data(), s->pModQ.data(),
+                            s->moddownConvOf(tier), s->pInvModQof(tier), s->pModQof(tier),
                             s->qInvTable[ell].data(), scratch->ptr, rowDone);
         s->stats.keyswitch++;
         s->stats.rescale++;
@@ -916,16 +1011,18 @@ class SfheInternal {
         if (ell < 2) SFHE_THROW("no levels left to rescale (multiplicative depth exhausted)");
         const size_t pw = s->polyWords(level);
         if (!s->shardAt(ell)) {
-            const uint32_t n = s->n, K = s->K, beta = (ell + s->alpha - 1) / s->alpha;
+            const DeviceBufferPtr& key = s->relinFor(ell);
+            const int tier = key->ksTier;
+            const uint32_t n = s->n, K = s->Kof(tier), beta = (ell + s->alpha - 1) / s->alpha;
             const size_t stride = (size_t)(ell + K) * n;
             Ct out = newCt(cc, level + 1, slots);
             auto acc = s->alloc(2 * stride);
             auto ext = s->alloc(stride * beta);
             auto scratch = s->alloc((size_t)2 * ell * n);
-            auto& convs = modupConv(cc, ell);
+            auto& convs = modupConv(cc, ell, tier);
             if (sfp_mult_relin_rescale(s->dev, out->c0, out->c1, a0, a1, b0, b1, ell, K, s->Lq, s->alpha,
-                                       convs.data(), s->relinKey->ptr, s->moddownConv, s->pInvModQ.data(),
-                                       s->pModQ.data(), s->qInvTable[ell].data(), acc->ptr, ext->ptr,
+                                       convs.data(), key->ptr, s->moddownConvOf(tier), s->pInvModQof(tier),
+                                       s->pModQof(tier), s->qInvTable[ell].data(), acc->ptr, ext->ptr,
                                        scratch->ptr) == 0) {
                 s->stats.keyswitch++;
                 s->stats.rescale++;
@@ -955,9 +1052,11 @@ class SfheInternal {
         const uint32_t ell = s->ellOf(level);
         std::vector<Ct> out(cnt);
         if (ell < 2) SFHE_THROW("no levels left to rescale (multiplicative depth exhausted)");
-        const uint32_t n = s->n, K = s->K, beta = (ell + s->alpha - 1) / s->alpha;
+        const DeviceBufferPtr& key = s->relinFor(ell);
+        const int tier = key->ksTier;
+        const uint32_t n = s->n, K = s->Kof(tier), beta = (ell + s->alpha - 1) / s->alpha;
         const size_t stride = (size_t)(ell + K) * n;
-        auto& convs = modupConv(cc, ell);
+        auto& convs = modupConv(cc, ell, tier);
         size_t done = 0;
         {  // (the batch ends here: unfused pairs below run as ordinary ops on the caller's lane)
         BatchScope bs(cc, s->shardAt(ell) ? 0 : (uint32_t)cnt);
@@ -970,7 +1069,7 @@ class SfheInternal {
                 bs.lane((uint32_t)done);
                 if (sfp_mult_relin_rescale(s->dev, out[done]->c0, out[done]->c1, a[done]->c0, a[done]->c1,
                                            b[done]->c0, b[done]->c1, ell, K, s->Lq, s->alpha, convs.data(),
-                                           s->relinKey->ptr, s->moddownConv, s->pInvModQ.data(), s->pModQ.data(),
+                                           key->ptr, s->moddownConvOf(tier), s->pInvModQof(tier), s->pModQof(tier),
                                            s->qInvTable[ell].data(), acc->ptr, ext->ptr, scratch->ptr) != 0)
                     break;  // (no fused form: nothing issued for this pair)
                 s->stats.keyswitch++;
@@ -990,21 +1089,27 @@ class SfheInternal {
                                 uint64_t* out1, int add0, int add1) {
         SfheContextState* s = cc->st.get();
         if (s->shardAt(ell)) return innerModDownShard(s, ext, stride, beta, ell, key, out0, out1, add0, add1);
-        const uint32_t n = s->n, K = s->K;
+        const int tier = key->ksTier;
+        const uint32_t n = s->n, K = s->Kof(tier);
         const size_t accStride = (size_t)(ell + K) * n;
+        if (stride != accStride) SFHE_THROW("internal: extended digits of another special-prime tier");
         auto acc = s->alloc(2 * accStride);
         sfp_ks_inner(s->dev, acc->ptr, acc->ptr + accStride, ext, stride, key->ptr, beta, ell, K,
                      s->Lq);
         auto scratch = s->alloc((size_t)2 * ell * n);
-        sfp_moddown2(s->dev, out0, out1, acc->ptr, accStride, ell, K, s->Lq, s->moddownConv,
-                     s->pInvModQ.data(), add0, add1, scratch->ptr, 0);
+        sfp_moddown2(s->dev, out0, out1, acc->ptr, accStride, ell, K, s->Lq, s->moddownConvOf(tier),
+                     s->pInvModQof(tier), add0, add1, scratch->ptr, 0);
     }
 
-    static std::vector<sfp_conv*>& modupConv(CC* cc, uint32_t ell) {
+    // ModUp conversion tables of ell limbs: digit j -> the other q rows and
+    // the special primes of tier `tier` (-1: all K)
+    static std::vector<sfp_conv*>& modupConv(CC* cc, uint32_t ell, int tier = -1) {
         SfheContextState* s = cc->st.get();
-        auto it = s->modupConv.find(ell);
-        if (it != s->modupConv.end()) return it->second;
+        auto& cache = tier < 0 ? s->modupConv : s->tiers[(size_t)tier].modupConv;
+        auto it = cache.find(ell);
+        if (it != cache.end()) return it->second;
         std::vector<sfp_conv*> v;
+        const uint32_t K = s->Kof(tier);
         uint32_t beta = (ell + s->alpha - 1) / s->alpha;
         for (uint32_t j = 0; j < beta; ++j) {
             uint32_t lo = j * s->alpha, hi = std::min(lo + s->alpha, ell);
@@ -1012,33 +1117,100 @@ class SfheInternal {
             for (uint32_t i = lo; i < hi; ++i) src.push_back(i);
             for (uint32_t i = 0; i < ell; ++i)
                 if (i < lo || i >= hi) dst.push_back(i);
-            for (uint32_t k = 0; k < s->K; ++k) dst.push_back(s->Lq + k);
+            for (uint32_t k = 0; k < K; ++k) dst.push_back(s->Lq + k);
             // extended layout: q rows at their index, P row k at ell + k
             for (uint32_t p : dst) row.push_back(p < s->Lq ? p : ell + (p - s->Lq));
             v.push_back(makeConv(s, src, dst, row.data()));
         }
-        return s->modupConv[ell] = v;
+        return cache[ell] = v;
     }
 
+    // Special-prime tiers: for each limb bound b of
+    // SFHE_KS_TIERS (default "2,4,6,8,10"; "0": none) up to one digit (b <= alpha),
+    // the first K' special primes with P' >= Q_b * 2^20 -- the margin the
+    // context's P has over its largest digit -- when K' < K.  Unsharded
+    // contexts only (a sharded rank keeps one key slice).
+    static void buildTiers(SfheContextState* s) {
+        const char* v = std::getenv("SFHE_KS_TIERS");
+        const std::string spec = v ? v : "2,4,6,8,10";
+        std::vector<uint32_t> bounds;
+        for (size_t i = 0; i < spec.size();) {
+            size_t j = spec.find(',', i);
+            if (j == std::string::npos) j = spec.size();
+            const long b = std::strtol(spec.substr(i, j - i).c_str(), nullptr, 10);
+            if (b > 0) bounds.push_back((uint32_t)b);
+            i = j + 1;
+        }
+        std::sort(bounds.begin(), bounds.end());
+        for (uint32_t b : bounds) {
+            if (b > s->alpha || b > s->Lq) break;
+            double bits = 0;
+            for (uint32_t i = 0; i < b; ++i) bits += std::log2((double)s->primes[i]);
+            uint32_t K = 0;
+            for (double bp = 0; bp < bits + 20.0 && K < s->K; ++K) bp += std::log2((double)s->primes[s->Lq + K]);
+            if (K + 1 >= s->K || (!s->tiers.empty() && K <= s->tiers.back().K)) continue;
+            KsTier t;
+            t.maxEll = b;
+            t.K = K;
+            t.pModQ.resize(s->Lq);
+            t.pInvModQ.resize(s->Lq);
+            for (uint32_t i = 0; i < s->Lq; ++i) {
+                const u64 qi = s->primes[i];
+                u64 pr = 1;
+                for (uint32_t k = 0; k < K; ++k) pr = mulmod(pr, s->primes[s->Lq + k] % qi, qi);
+                t.pModQ[i] = pr;
+                t.pInvModQ[i] = invmod(pr, qi);
+            }
+            std::vector<uint32_t> src, dst;
+            for (uint32_t k = 0; k < K; ++k) src.push_back(s->Lq + k);
+            for (uint32_t i = 0; i < s->Lq; ++i) dst.push_back(i);
+            t.moddownConv = makeConv(s, src, dst);
+            s->tiers.push_back(std::move(t));
+        }
+    }
+    // the tiers' switching keys for the key of s' (after the context's own;
+    // a sharded rank keeps its slice, as of every key)
+    static void genTierKeys(CC* cc, const uint64_t* sPrime, const uint64_t* sk, uint32_t gal) {
+        SfheContextState* s = cc->st.get();
+        for (size_t t = 0; t < s->tiers.size(); ++t) {
+            auto key = genSwitchKey(cc, sPrime, sk, (int)t);
+            if (gal)
+                s->tiers[t].rotKeys[gal] = key;
+            else
+                s->tiers[t].relinKey = key;
+        }
+    }
+
+    // keep (optional, one flag per source): a PART of the conversion from
+    // src -- its constants those of the whole set (y_i = x_i (S/s_i)^-1 mod
+    // s_i, multipliers S/s_i mod t) -- over the kept sources only, or, with
+    // zeroRest, over every source with the multipliers of the others zeroed.
+    // Parts over complementary sources sum (mod t) to the whole conversion.
     static sfp_conv* makeConv(SfheContextState* s, const std::vector<uint32_t>& src,
-                              const std::vector<uint32_t>& dst, const uint32_t* dstRow = nullptr) {
-        const uint32_t ns = (uint32_t)src.size(), nt = (uint32_t)dst.size();
-        std::vector<u64> inv(ns), mod((size_t)ns * nt);
-        for (uint32_t i = 0; i < ns; ++i) {
+                              const std::vector<uint32_t>& dst, const uint32_t* dstRow = nullptr,
+                              const std::vector<char>* keep = nullptr, bool zeroRest = false) {
+        const uint32_t nsAll = (uint32_t)src.size(), nt = (uint32_t)dst.size();
+        std::vector<u64> inv, mod;
+        std::vector<uint32_t> used;
+        for (uint32_t i = 0; i < nsAll; ++i) {
+            const bool kept = !keep || (*keep)[i];
+            if (!kept && !zeroRest) continue;
+            used.push_back(src[i]);
             u64 qi = s->primes[src[i]];
             u64 prod = 1;
-            for (uint32_t k = 0; k < ns; ++k)
+            for (uint32_t k = 0; k < nsAll; ++k)
                 if (k != i) prod = mulmod(prod, s->primes[src[k]] % qi, qi);
-            inv[i] = invmod(prod, qi);
+            inv.push_back(invmod(prod, qi));
             for (uint32_t t = 0; t < nt; ++t) {
                 u64 pt = s->primes[dst[t]];
                 u64 pr = 1;
-                for (uint32_t k = 0; k < ns; ++k)
+                for (uint32_t k = 0; k < nsAll; ++k)
                     if (k != i) pr = mulmod(pr, s->primes[src[k]] % pt, pt);
-                mod[(size_t)i * nt + t] = pr;
+                mod.push_back(kept ? pr : 0);
             }
         }
-        sfp_conv* c = sfp_upload_conv(s->dev, ns, src.data(), nt, dst.data(), dstRow, inv.data(), mod.data());
+        const uint32_t ns = (uint32_t)used.size();
+        sfp_conv* c = sfp_upload_conv(s->dev, ns, used.data(), nt, dst.data(), dstRow, inv.data(), mod.data());
         if (!c) {
             const char* e = sfp_last_error(s->dev);
             SFHE_THROW(std::string("base-conversion table upload failed: ") + (e ? e : "unknown"));
@@ -1046,23 +1218,27 @@ class SfheInternal {
         return c;
     }
 
-    // switching key from s' (device, Lq+K limbs, eval domain) to s
-    static DeviceBufferPtr genSwitchKey(CC* cc, const uint64_t* sPrime, const uint64_t* sk) {
+    // switching key from s' (device, Lq+K limbs, eval domain) to s; tier >= 0:
+    // that special-prime tier's key (one digit over the Q primes and P')
+    static DeviceBufferPtr genSwitchKey(CC* cc, const uint64_t* sPrime, const uint64_t* sk, int tier = -1) {
         SfheContextState* s = cc->st.get();
         if (s->sharded) {  // every rank builds the whole key (same seed, same words) ...
             DeviceBufferPtr whole;
             {
                 FullScope fs(s);
-                whole = genSwitchKey(cc, sPrime, sk);
+                whole = genSwitchKey(cc, sPrime, sk, tier);
             }
-            return s->kgeom.rows ? sliceKey(s, whole) : whole;  // ... and keeps its slice
+            return s->kgeom.rows ? sliceKey(s, whole, tier) : whole;  // ... and keeps its slice
         }
-        const uint32_t n = s->n, NP = s->Lq + s->K;
+        const uint32_t n = s->n, NP = s->Lq + s->Kof(tier);
+        const uint32_t digits = tier < 0 ? s->dnum : 1;
+        const u64* pModQ = s->pModQof(tier);
         const sfp_limbs all{NP, NP, 0};
-        auto key = s->alloc((size_t)s->dnum * 2 * NP * n);
+        auto key = s->alloc((size_t)digits * 2 * NP * n);
+        key->ksTier = tier;
         auto tmp = s->alloc((size_t)NP * n);
         std::vector<int64_t> e(n);
-        for (uint32_t j = 0; j < s->dnum; ++j) {
+        for (uint32_t j = 0; j < digits; ++j) {
             uint64_t* b = key->ptr + (size_t)j * 2 * NP * n;
             uint64_t* a = b + (size_t)NP * n;
             sfp_sample_uniform(s->dev, a, all, s->nextSeed());
@@ -1075,7 +1251,7 @@ class SfheInternal {
             // + P * s' on the digit's q-limbs
             uint32_t lo = j * s->alpha, hi = std::min(lo + s->alpha, s->Lq);
             if (lo >= hi) continue;
-            std::vector<u64> pk(s->pModQ.begin() + lo, s->pModQ.begin() + hi);
+            std::vector<u64> pk(pModQ + lo, pModQ + hi);
             sfp_mul_const(s->dev, tmp->ptr, sPrime + (size_t)lo * n, pk.data(),
                           Range(lo, hi - lo));
             sfp_add(s->dev, b + (size_t)lo * n, b + (size_t)lo * n, tmp->ptr, Range(lo, hi - lo));
@@ -1637,7 +1813,7 @@ struct DeferredRelin : DeferredOp {
         uint64_t* d1 = d0 + pw;
         uint64_t* d2 = d1 + pw;
         sfp_tensor(s->dev, d0, d1, d2, a0, a1, b0, b1, s->qmap(s->ellOf(level)));
-        SfheInternal::keySwitch(cc, d2, s->ellOf(level), s->relinKey, d0, d1, 1, 1);
+        SfheInternal::keySwitch(cc, d2, s->ellOf(level), s->relinFor(s->ellOf(level)), d0, d1, 1, 1);
         SfheInternal::adoptPending(ct, t, d0, d1);
     }
 };
@@ -1831,6 +2007,7 @@ CryptoContextImpl<DCRTPoly>::CryptoContextImpl(const CCParams<CryptoContextCKKSR
         for (uint32_t i = 0; i < s.Lq; ++i) dst.push_back(i);
         s.moddownConv = SfheInternal::makeConv(&s, src, dst);
     }
+    SfheInternal::buildTiers(&s);
     s.qInvTable.resize(s.Lq + 1);
     for (uint32_t ell = 2; ell <= s.Lq; ++ell) {
         u64 ql = s.primes[ell - 1];
@@ -1845,6 +2022,13 @@ CryptoContextImpl<DCRTPoly>::~CryptoContextImpl() {
     g_liveContexts.fetch_sub(1);
     st->relinKey.reset();
     st->rotKeys.clear();
+    for (auto& t : st->tiers) {
+        t.relinKey.reset();
+        t.rotKeys.clear();
+        for (auto& kv : t.modupConv)
+            for (auto* c : kv.second) sfp_free_conv(st->dev, c);
+        if (t.moddownConv) sfp_free_conv(st->dev, t.moddownConv);
+    }
     st->ptCache.clear();
     releaseBootstrapGraphs();  // the replay graphs' blocks back to the pool first
     st->boot.clear();  // its diagonal encodings return blocks to the pool below
@@ -1853,6 +2037,11 @@ CryptoContextImpl<DCRTPoly>::~CryptoContextImpl() {
     if (st->moddownConv) sfp_free_conv(st->dev, st->moddownConv);
     for (auto& kv : st->modupConvShard)
         for (auto* c : kv.second) sfp_free_conv(st->dev, c);
+    for (auto& kv : st->modupConvSplit)
+        for (auto& pr : kv.second) {
+            sfp_free_conv(st->dev, pr.first);
+            sfp_free_conv(st->dev, pr.second);
+        }
     if (st->moddownConvShard) sfp_free_conv(st->dev, st->moddownConvShard);
     st->releaseAll();
     sfp_destroy(st->dev);
@@ -2063,6 +2252,7 @@ void CryptoContextImpl<DCRTPoly>::EvalMultKeyGen(const PrivateKey<DCRTPoly>& sk)
     auto s2 = s->alloc((size_t)NP * s->n);
     sfp_mul(s->dev, s2->ptr, sk->s->ptr, sk->s->ptr, sfp_limbs{NP, NP, 0});
     s->relinKey = SfheInternal::genSwitchKey(this, s2->ptr, sk->s->ptr);
+    SfheInternal::genTierKeys(this, s2->ptr, sk->s->ptr, 0);
     s->keyTag = sk->tag;
     // every level's ModUp conversion tables now, as OpenFHE precomputes its
     // CRT tables with the context: built lazily, each upload drained the
@@ -2071,6 +2261,11 @@ void CryptoContextImpl<DCRTPoly>::EvalMultKeyGen(const PrivateKey<DCRTPoly>& sk)
     // first sort they added ~18 ms of drained uploads to the cold sort)
     for (uint32_t ell = 1; ell <= s->Lq; ++ell)
         sfp_modup_prepare(s->dev, SfheInternal::modupConv(this, ell).data(), ell, s->K, s->alpha);
+    if (!s->sharded)
+        for (size_t t = 0; t < s->tiers.size(); ++t)
+            for (uint32_t ell = 1; ell <= s->tiers[t].maxEll; ++ell)
+                sfp_modup_prepare(s->dev, SfheInternal::modupConv(this, ell, (int)t).data(), ell, s->tiers[t].K,
+                                  s->alpha);
 }
 
 void CryptoContextImpl<DCRTPoly>::EvalRotateKeyGen(const PrivateKey<DCRTPoly>& sk,
@@ -2087,16 +2282,19 @@ void CryptoContextImpl<DCRTPoly>::EvalRotateKeyGen(const PrivateKey<DCRTPoly>& s
         if (gal == 1 || s->rotKeys.count(gal)) continue;
         sfp_automorph(s->dev, sg->ptr, sk->s->ptr, gal, sfp_limbs{NP, NP, 0});
         s->rotKeys[gal] = SfheInternal::genSwitchKey(this, sg->ptr, sk->s->ptr);
+        SfheInternal::genTierKeys(this, sg->ptr, sk->s->ptr, gal);
     }
 }
 
 void CryptoContextImpl<DCRTPoly>::ClearEvalMultKeys() {
     OpLock g(st.get());
     st->relinKey.reset();
+    for (auto& t : st->tiers) t.relinKey.reset();
 }
 void CryptoContextImpl<DCRTPoly>::ClearEvalAutomorphismKeys() {
     OpLock g(st.get());
     st->rotKeys.clear();
+    for (auto& t : st->tiers) t.rotKeys.clear();
     st->rotIndices.clear();
 }
 
@@ -2586,7 +2784,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalMult(const Ciphertext<DCRT
     uint64_t* d1 = d0 + pw;
     uint64_t* d2 = d1 + pw;
     sfp_tensor(s->dev, d0, d1, d2, a->c0, a->c1, b->c0, b->c1, st->qmap(ell));
-    SfheInternal::keySwitch(this, d2, ell, s->relinKey, d0, d1, 1, 1);
+    SfheInternal::keySwitch(this, d2, ell, s->relinFor(ell), d0, d1, 1, 1);
     return SfheInternal::traced(this, SfheInternal::rescale(this, d0, d1, a->level, slots), "EvalMult");
 }
 
@@ -2699,8 +2897,7 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotate(const Ciphertext<DC
     if (!(SfheInternal::lazy(s) && SfheInternal::isLazy(a))) SfheInternal::deps(s, {&a});
     uint32_t gal = GaloisForRotation(r);
     if (gal == 1) return a->Clone();
-    auto it = s->rotKeys.find(gal);
-    if (it == s->rotKeys.end())
+    if (!s->rotKeys.count(gal))
         SFHE_THROW("EvalKey for index [" + std::to_string(gal) + "] (rotation " +
                    std::to_string(r) + ") is not found");
     // a lazy product rotates before its rescale: the key switch's rounding is
@@ -2717,8 +2914,8 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotate(const Ciphertext<DC
     sfp_automorph(s->dev, t->ptr, a->c1, gal, st->qmap(ell));
     s->stats.automorph++;
     s->countBytes(3.0 * ell * s->n * 8);
-    // c0' = sigma(c0) + ks0, c1' = ks1
-    SfheInternal::keySwitch(this, t->ptr, ell, it->second, out->c0, out->c1, 1, 0);
+    // c0' = sigma(c0) + ks0, c1' = ks1 (with the key of ell's special-prime tier)
+    SfheInternal::keySwitch(this, t->ptr, ell, *s->rotFor(gal, ell), out->c0, out->c1, 1, 0);
     return SfheInternal::traced(this, out, "EvalRotate");
 }
 
@@ -2752,12 +2949,15 @@ std::shared_ptr<FastRotationPrecomp> CryptoContextImpl<DCRTPoly>::EvalFastRotati
         SfheInternal::modupShard(s, pre->ext->ptr, a->c1, ell);
         return pre;
     }
-    pre->stride = (size_t)(ell + s->K) * s->n;
+    // the extended digits over ell's special-prime tier (its rotation keys
+    // exist for every rotation key: they are generated together)
+    const int tier = s->tierAt(ell);
+    const uint32_t K = s->Kof(tier);
+    pre->stride = (size_t)(ell + K) * s->n;
     pre->ext = s->alloc(pre->stride * pre->beta);
     auto scratch = s->alloc((size_t)ell * s->n);
-    auto& convs = SfheInternal::modupConv(this, ell);
-    sfp_modup(s->dev, pre->ext->ptr, a->c1, ell, s->K, s->Lq, s->alpha, convs.data(),
-              scratch->ptr);
+    auto& convs = SfheInternal::modupConv(this, ell, tier);
+    sfp_modup(s->dev, pre->ext->ptr, a->c1, ell, K, s->Lq, s->alpha, convs.data(), scratch->ptr);
     return pre;
 }
 
@@ -2777,10 +2977,12 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalFastRotation(
     if (gal == 1) return a->Clone();
     if (!pre || pre->level != a->level)
         SFHE_THROW("fast-rotation precomputation does not match");
-    auto it = s->rotKeys.find(gal);
-    if (it == s->rotKeys.end())
-        SFHE_THROW("EvalKey for rotation " + std::to_string(r) + " is not found");
+    if (!s->rotKeys.count(gal)) SFHE_THROW("EvalKey for rotation " + std::to_string(r) + " is not found");
     const uint32_t ell = pinned ? s->ellOf(pre->level) + 1 : SfheInternal::ctEll(s, *a);
+    // the key of the precomputation's tier (its extended rows: ell + K' per digit)
+    const DeviceBufferPtr* key = s->rotFor(gal, ell);
+    if (!s->shardAt(ell) && (size_t)(ell + s->Kof((*key)->ksTier)) * s->n != pre->stride)
+        key = &s->rotKeys.at(gal);
     const uint64_t* c0in = pinned ? pre->pinC0 : a->c0;
     // sigma commutes with the (coefficient-wise) base extension, so rotating
     // the extended digits equals extending the rotated c1.
@@ -2791,11 +2993,10 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalFastRotation(
     auto out = pre->pend ? SfheInternal::newPendingCt(this, a->level, a->slots)
                          : SfheInternal::newCt(this, a->level, a->slots);
     sfp_automorph(s->dev, out->c0, c0in, gal, st->qmap(ell));
-    SfheInternal::innerAndModDown(this, ext->ptr, pre->stride, pre->beta, ell, it->second,
-                                  out->c0, out->c1, 1, 0);
+    SfheInternal::innerAndModDown(this, ext->ptr, pre->stride, pre->beta, ell, *key, out->c0, out->c1, 1, 0);
     s->stats.keyswitch++;
     s->stats.automorph++;
-    s->countBytes((3.0 * ell + 2.0 * pre->beta * (ell + s->K)) * s->n * 8);
+    s->countBytes((3.0 * ell + 2.0 * pre->beta * (pre->stride / s->n)) * s->n * 8);
     return SfheInternal::traced(this, out, "EvalFastRotation");
 }
 
@@ -2826,13 +3027,9 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotateSum(const std::vecto
         for (size_t k = 0; k < a.size(); ++k) terms.push_back(EvalRotate(a[k], r[k]));
         return EvalAddMany(terms);
     }
-    std::vector<const DeviceBufferPtr*> keys;
-    for (size_t k : rot) {
-        auto it = s->rotKeys.find(GaloisForRotation(r[k]));
-        if (it == s->rotKeys.end())
+    for (size_t k : rot)
+        if (!s->rotKeys.count(GaloisForRotation(r[k])))
             SFHE_THROW("EvalKey for rotation " + std::to_string(r[k]) + " is not found");
-        keys.push_back(&it->second);
-    }
     // pending products rotate before their rescale, as in EvalRotate
     uint32_t slots = 0;
     if (pend) macGroups(this, a, rot);
@@ -2846,13 +3043,19 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotateSum(const std::vecto
         slots = std::max(slots, a[k]->slots);
     }
     const uint32_t level = a[rot[0]]->level, ell = SfheInternal::ctEll(s, *a[rot[0]]);
-    const uint32_t n = s->n, K = s->K, beta = (ell + s->alpha - 1) / s->alpha;
+    // the terms' keys of their (shared) limb count's special-prime tier
+    std::vector<const DeviceBufferPtr*> keys;
+    for (size_t k : rot) keys.push_back(s->rotFor(GaloisForRotation(r[k]), ell));
+    const int tier = (*keys[0])->ksTier;
+    for (auto* k : keys)
+        if ((*k)->ksTier != tier) SFHE_THROW("internal: rotation keys of different special-prime tiers");
+    const uint32_t n = s->n, K = s->Kof(tier), beta = (ell + s->alpha - 1) / s->alpha;
     const bool shard = s->shardAt(ell);  // local rows; the exchanges inside modupShard / modDownShard
     const size_t stride = (size_t)(shard ? s->extmap(ell).count : ell + K) * n;
     auto out = pend ? SfheInternal::newPendingCt(this, level, slots) : SfheInternal::newCt(this, level, slots);
     auto acc = s->alloc(2 * stride);
     int rowDone = 0;
-    auto& convs = SfheInternal::modupConv(this, ell);
+    auto& convs = SfheInternal::modupConv(this, ell, tier);
     if (!shard && sfp_modup_inner_phase(s->dev, nullptr, nullptr, nullptr, ell, K, s->Lq, s->alpha, convs.data(),
                                         nullptr, nullptr, nullptr, 0, 0, 0, nullptr, nullptr, 0) == 0) {
         // The terms' rotations and ModUps are independent: each chunk of
@@ -2934,8 +3137,8 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotateSum(const std::vecto
         SfheInternal::modDownShard(s, acc->ptr, ell, out->c0, out->c1, 1, 0);
     } else {
         auto md = s->alloc((size_t)2 * ell * n);
-        sfp_moddown2(s->dev, out->c0, out->c1, acc->ptr, stride, ell, K, s->Lq, s->moddownConv,
-                     s->pInvModQ.data(), 1, 0, md->ptr, rowDone);
+        sfp_moddown2(s->dev, out->c0, out->c1, acc->ptr, stride, ell, K, s->Lq, s->moddownConvOf(tier),
+                     s->pInvModQof(tier), 1, 0, md->ptr, rowDone);
     }
     Ciphertext<DCRTPoly> res = SfheInternal::traced(this, out, "EvalRotateSum");
     for (size_t k : ident) res = EvalAdd(res, a[k]);
@@ -3246,6 +3449,7 @@ void CryptoContextImpl<DCRTPoly>::EvalConjugateKeyGen(const PrivateKey<DCRTPoly>
     auto sg = s->alloc((size_t)NP * s->n);
     sfp_automorph(s->dev, sg->ptr, sk->s->ptr, gal, sfp_limbs{NP, NP, 0});
     s->rotKeys[gal] = SfheInternal::genSwitchKey(this, sg->ptr, sk->s->ptr);
+    SfheInternal::genTierKeys(this, sg->ptr, sk->s->ptr, gal);
 }
 
 // ============================================================================

@@ -390,6 +390,7 @@ bool CryptoContextImpl<DCRTPoly>::DeserializeEvalMultKey(std::istream& is, SerTy
         auto key = getWords(is, s, switchKeyWords(s));
         if (!key) return false;
         s->relinKey = key;
+        s->tiersReady = false;  // (the records carry the context's keys only: switches use the whole P)
     }
     return true;
 }
@@ -440,6 +441,7 @@ bool CryptoContextImpl<DCRTPoly>::DeserializeEvalAutomorphismKey(std::istream& i
             auto key = getWords(is, s, switchKeyWords(s));
             if (!key) return false;
             s->rotKeys[gal] = key;
+            s->tiersReady = false;
         }
         if (!get(is, ni)) return false;
         for (uint32_t j = 0; j < ni; ++j) {

@@ -28,6 +28,7 @@ class DeviceBuffer {
     int lane;                      // lane of the last writer (allocating lane until an in-place write)
     uint64_t region;               // fork/join region it was allocated in (0: none)
     uint64_t seq = 0;              // position of its last write in lane's sequence
+    int ksTier = -1;               // a switching key: its special-prime tier (-1: the whole P)
     sfp_event* ready = nullptr;    // shared encodings: end of the producing work
     uint64_t readyEpoch = 0;       // capture epoch `ready` was recorded in (0: none)
     uint64_t capEpoch = 0;         // capture epoch it was allocated in (0: none)
@@ -48,6 +49,22 @@ struct PtCacheEntry {
     std::vector<std::complex<double>> values;
     uint32_t slots;
     DeviceBufferPtr buf;
+};
+
+// A special-prime tier: key switches at ell <= maxEll limbs
+// (a single digit, beta = 1) run over the first K special primes P' only,
+// P' >= Q_maxEll * 2^20 as the context's P >= its largest digit * 2^20 --
+// the same noise margin with fewer extended rows (the metric context, K = 13:
+// K' = 3 / 5 / 7 / 9 / 11 up to 2 / 4 / 6 / 8 / 10 limbs).  Its keys are
+// another set (one digit, b rows then a rows over the Q primes and P'),
+// generated with the context's keys.
+struct KsTier {
+    uint32_t maxEll = 0, K = 0;
+    std::vector<uint64_t> pModQ, pInvModQ;  // P' mod q_i, P'^-1 mod q_i
+    sfp_conv* moddownConv = nullptr;        // P' -> Q
+    std::map<uint32_t, std::vector<sfp_conv*>> modupConv;  // ell -> Q_ell -> P'
+    DeviceBufferPtr relinKey;
+    std::map<uint32_t, DeviceBufferPtr> rotKeys;
 };
 
 struct SfheContextState {
@@ -83,6 +100,34 @@ struct SfheContextState {
     DeviceBufferPtr relinKey;
     std::map<uint32_t, DeviceBufferPtr> rotKeys;  // galois -> key
     std::set<int32_t> rotIndices;
+    // special-prime tiers, ascending maxEll (SFHE_KS_TIERS; replicated levels only when sharded)
+    std::vector<KsTier> tiers;
+    bool tiersReady = true;  // false once keys arrive without their tier keys (deserialized)
+    // the tier of a key switch at ell limbs (-1: the whole P)
+    int tierAt(uint32_t ell) const {
+        if (!tiersReady || shardAt(ell)) return -1;  // (dealt levels: the exchanges use the whole P)
+        for (size_t t = 0; t < tiers.size(); ++t)
+            if (ell <= tiers[t].maxEll) return (int)t;
+        return -1;
+    }
+    uint32_t Kof(int t) const { return t < 0 ? K : tiers[(size_t)t].K; }
+    const uint64_t* pModQof(int t) const { return t < 0 ? pModQ.data() : tiers[(size_t)t].pModQ.data(); }
+    const uint64_t* pInvModQof(int t) const { return t < 0 ? pInvModQ.data() : tiers[(size_t)t].pInvModQ.data(); }
+    sfp_conv* moddownConvOf(int t) const { return t < 0 ? moddownConv : tiers[(size_t)t].moddownConv; }
+    // the relinearisation / rotation key a switch at ell limbs uses (its tier's when it has one)
+    const DeviceBufferPtr& relinFor(uint32_t ell) const {
+        const int t = tierAt(ell);
+        return t >= 0 && tiers[(size_t)t].relinKey ? tiers[(size_t)t].relinKey : relinKey;
+    }
+    const DeviceBufferPtr* rotFor(uint32_t gal, uint32_t ell) const {
+        const int t = tierAt(ell);
+        if (t >= 0) {
+            auto it = tiers[(size_t)t].rotKeys.find(gal);
+            if (it != tiers[(size_t)t].rotKeys.end()) return &it->second;
+        }
+        auto it = rotKeys.find(gal);
+        return it == rotKeys.end() ? nullptr : &it->second;
+    }
     // bootstrapping precomputations per slot count (EvalBootstrapSetup)
     std::map<uint32_t, std::shared_ptr<BootstrapPrecomp>> boot;
 
@@ -180,6 +225,10 @@ struct SfheContextState {
     sfp_key_geom kgeom{};
     uint32_t keyRows() const { return kgeom.rows ? kgeom.rows : Lq + K; }
     std::map<uint32_t, std::vector<sfp_conv*>> modupConvShard;  // ell -> per digit (owned targets)
+    // the same, split for the overlapped ModUp: per digit the
+    // table of this rank's own source rows, then the whole digit with the
+    // multipliers of those rows zeroed (the rows the all-gather brings)
+    std::map<uint32_t, std::vector<std::pair<sfp_conv*, sfp_conv*>>> modupConvSplit;
     sfp_conv* moddownConvShard = nullptr;                        // P -> owned Q rows
 
     // ---- helpers ----

@@ -4620,15 +4620,15 @@ static RowGroup rowsOf(uint32_t P, uint32_t R, sfp_limbs pm) {
 
 // Would a forward NTT over `rows` rows take a two-stage (LE = 2) COL pass --
 // the passes that have the inverse-COL prologue (RowGroup::icol)?  Mirrors
-// nttRows' choice of path.  SFHE_ICOL=0 turns the prologue off (A/B).
+// nttRows' choice of path.  Off by default (SFHE_ICOL=1 turns it on).
 static int nttLe();
 static uint32_t nttSmallTile();
 static int nttSmallLe();
 static uint32_t nttT1kRows();
 static bool icolPath(sfp_dev* d, uint32_t rows) {
-    static const bool on = [] {
+    static const bool on = [] {  // (measured: sort 36.22 -> 36.63 ms with it on)
         const char* v = std::getenv("SFHE_ICOL");
-        return !v || *v != '0';
+        return v && *v == '1';
     }();
     if (!on || d->n <= (uint32_t)kNttTile) return false;
     const uint32_t st = nttSmallTile();
@@ -5097,6 +5097,51 @@ static double nttNodeRows(const hipKernelNodeParams& kp) {
     return (double)kp.gridDim.y;
 }
 
+// A conversion-family node's algorithmic bytes (8n per source row read and
+// per target row written): k_mdrsf / k_conv_mdrs per polynomial (grid row)
+// the K source rows and the dropped row in, l target rows out; k_convf /
+// k_conv per job its ns sources in, its ntUse targets out.
+static double convNodeBytes(const hipKernelNodeParams& kp, uint32_t n) {
+    const void* f = kp.func;
+    if (!kp.kernelParams) return 0;
+    const bool mdrs = f == (const void*)k_mdrsf<13> || f == (const void*)k_mdrsf<16> ||
+                      f == (const void*)k_mdrsf<kMaxConvSrc> || f == (const void*)k_mdrsf<13, true> ||
+                      f == (const void*)k_mdrsf<16, true> || f == (const void*)k_mdrsf<kMaxConvSrc, true> ||
+                      f == (const void*)k_conv_mdrs;
+    if (mdrs) {
+        const MdrsArgs& A = *static_cast<const MdrsArgs*>(kp.kernelParams[0]);
+        return 8.0 * n * kp.gridDim.y * (A.ns + 1.0 + A.l);
+    }
+    const ConvJobs& J = *static_cast<const ConvJobs*>(kp.kernelParams[0]);
+    double r = 0;
+    for (uint32_t j = 0; j < kp.gridDim.y && j < (uint32_t)kMaxConvJobs; ++j) r += J.j[j].ns + (double)J.j[j].ntUse;
+    return 8.0 * n * r;
+}
+// k_ntt_ks: per extended row, beta ext rows + 2 beta key rows in, two
+// accumulator rows out (+ two in when accumulating)
+template <int NG>
+static double ksNodeBytesNG(const void* arg, uint32_t gridY, uint32_t n) {
+    const auto& S = *static_cast<const ArgSet<KsArgs, NG>*>(arg);
+    double b = 0;
+    for (int i = 0; i < NG; ++i) {
+        const uint32_t r0 = S.start[i], r1 = i + 1 < NG ? S.start[i + 1] : gridY;
+        const uint32_t rows = S.inter ? gridY / NG : (r1 > r0 ? r1 - r0 : 0);  // (unused sets: none)
+        b += 8.0 * n * rows * (3.0 * S.a[i].beta + (S.a[i].accum ? 4.0 : 2.0));
+    }
+    return b;
+}
+static double ksNodeBytes(const hipKernelNodeParams& kp, uint32_t n) {
+    const void* f = kp.func;
+    if (!kp.kernelParams) return 0;
+    if (f == (const void*)k_ntt_ks<2, 1024> || f == (const void*)k_ntt_ks<2, kNttTile>)
+        return ksNodeBytesNG<1>(kp.kernelParams[0], kp.gridDim.y, n);
+    if (f == (const void*)k_ntt_ks<2, 1024, 2> || f == (const void*)k_ntt_ks<2, kNttTile, 2>)
+        return ksNodeBytesNG<2>(kp.kernelParams[0], kp.gridDim.y, n);
+    if (f == (const void*)k_ntt_ks<2, 1024, 4> || f == (const void*)k_ntt_ks<2, kNttTile, 4>)
+        return ksNodeBytesNG<4>(kp.kernelParams[0], kp.gridDim.y, n);
+    return ksNodeBytesNG<8>(kp.kernelParams[0], kp.gridDim.y, n);
+}
+
 int sfp_graph_family_time(sfp_dev* d, sfp_graph* g, uint32_t fam, int reps, double* ms, uint64_t* launches,
                           double* bytes) {
     if (!g || !g->g || fam > SFP_FAM_ALL || reps < 1 || d->capture) return -1;
@@ -5130,6 +5175,8 @@ int sfp_graph_family_time(sfp_dev* d, sfp_graph* g, uint32_t fam, int reps, doub
         prev = nn2;
         ++cnt;
         if (kf == SFP_FAM_NTT) b += 16.0 * nttNodeRows(kp) * d->n;  // one pass reads and writes each row once
+        if (kf == SFP_FAM_CONV && fam == SFP_FAM_CONV) b += convNodeBytes(kp, d->n);
+        if (kf == SFP_FAM_NTTKS && fam == SFP_FAM_NTTKS) b += ksNodeBytes(kp, d->n);
     }
     hipGraphExec_t ex = nullptr;
     if (!cnt || hipGraphInstantiate(&ex, sub, nullptr, nullptr, 0) != hipSuccess) {

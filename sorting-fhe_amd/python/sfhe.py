@@ -42,7 +42,7 @@ ABI_SYMBOLS = [
     "sfhe_bootstrap_setup", "sfhe_bootstrap_depth", "sfhe_bootstrap",
     "sfhe_sorter_sort_bitonic", "sfhe_kway_sort", "sfhe_kway_params",
     "sfhe_save", "sfhe_load", "sfhe_ct_save", "sfhe_ct_load",
-    "sfhe_kway_create", "sfhe_kway_run", "sfhe_kway_destroy", "sfhe_kway_graph_nodes", "sfhe_shard_tail",
+    "sfhe_kway_create", "sfhe_kway_run", "sfhe_kway_destroy", "sfhe_kway_graph_nodes", "sfhe_kway_graph_family_time", "sfhe_shard_tail",
     "sfhe_key_rows",
     "sfhe_groups_rccl", "sfhe_groups_host", "sfhe_groups",
     "sfhe_encode_counts", "sfhe_bootstrap_graphs",
@@ -138,6 +138,7 @@ _SIGS = {
     "sfhe_kway_run": (C.c_int, [_VP, _VP, C.c_int, C.c_int, C.c_int, _U32, _PVP]),
     "sfhe_kway_destroy": (None, [_VP]),
     "sfhe_kway_graph_nodes": (C.c_int, [_VP, _PU64]),
+    "sfhe_kway_graph_family_time": (C.c_int, [_VP, _U32, C.c_int, _PD, _PU64, _PD]),
     "sfhe_load": (C.c_int, [C.c_char_p, _PVP]),
     "sfhe_ct_save": (C.c_int, [_VP, _VP, C.c_char_p]),
     "sfhe_ct_load": (C.c_int, [_VP, C.c_char_p, _PVP]),
@@ -643,6 +644,15 @@ class KWay:
         v = C.c_uint64()
         self.eng._chk(self.eng.lib.sfhe_kway_graph_nodes(self.h, C.byref(v)))
         return v.value
+
+    def graph_family_time(self, family: str, reps: int = 1):
+        """(ms per sort, launches, algorithmic bytes) of the captured sort's
+        kernels of one family replayed alone, over its chain of graphs."""
+        f = {**self.eng.KFAM, "other": 4, "all": 5}[family]
+        ms, n, b = C.c_double(), C.c_uint64(), C.c_double()
+        self.eng._chk(self.eng.lib.sfhe_kway_graph_family_time(self.h, f, reps, C.byref(ms), C.byref(n),
+                                                               C.byref(b)))
+        return ms.value, n.value, b.value
 
 
 def kway_params(N: int, backend: str = "hip"):

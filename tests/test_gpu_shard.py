@@ -91,6 +91,11 @@ print("RCCL communicator OK", flush=True)
 # path: every ModUp / ModDown all-gather and rescale broadcast is an RCCL
 # call), captured into the sort's hipGraph with its collectives and replayed
 os.environ["SFHE_SHARD_TAIL"] = {tail!r}
+# special-prime tiers (DESIGN.md §4b) run at replicated levels only: below the
+# largest tier bound (10 limbs) a small tail would have the sharded sort take
+# them at fewer levels than the unsharded one, so both run without them there
+if int({tail!r}) < 10:
+    os.environ["SFHE_KS_TIERS"] = "0"
 N, logn = {N}, {logn}
 depth, rots = sfhe.direct_sort_params(N, "hip")
 kw = dict(mult_depth=depth, ring_dim=1 << logn, batch_size=N, rotations=rots, seed=4099)

@@ -157,9 +157,9 @@ import torch.distributed as dist
 import sfhe
 from test_shard import sort_program
 rank = int(sys.argv[1])
-dist.init_process_group("gloo", init_method="tcp://127.0.0.1:{port}", rank=rank, world_size=2)
+dist.init_process_group("gloo", init_method="tcp://127.0.0.1:{port}", rank=rank, world_size={W})
 kw = {kw!r}
-e = sfhe.Engine("oracle", shard=("host", rank, 2, sfhe.GlooComm()), **kw)
+e = sfhe.Engine("oracle", shard=("host", rank, {W}, sfhe.GlooComm()), **kw)
 out = sort_program(e, {N})
 np.savez({path!r} + str(rank) + ".npz", **out)
 dist.barrier()
@@ -167,12 +167,15 @@ dist.destroy_process_group()
 """
 
 
-@pytest.mark.parametrize("N,logn", [(8, 12), (64, 13)])
-def test_sharded_sort_gloo_two_processes(oracle_lib, tmp_path, N, logn):
-    """A whole DirectSort<N> limb-sharded over two PROCESSES (one per
-    'GPU', gloo host transport): every exchange of a real sharded sort
-    (ModUp / ModDown all-gathers, rescale broadcasts) crosses a process
-    boundary; both ranks' results are bit-identical to the unsharded sort."""
+@pytest.mark.parametrize("N,logn,W,overlap", [(8, 12, 2, None), (64, 13, 2, None), (64, 13, 4, None), (64, 13, 4, "0")])
+def test_sharded_sort_gloo_two_processes(oracle_lib, tmp_path, N, logn, W, overlap):
+    """A whole DirectSort<N> limb-sharded over W PROCESSES (one per 'GPU',
+    gloo host transport): every exchange of a real sharded sort (ModUp /
+    ModDown all-gathers, rescale broadcasts) crosses a process boundary;
+    every rank's result is bit-identical to the unsharded sort.  The ModUp
+    is the overlapped form by default (each rank converts its own rows while
+    the all-gather brings the rest, then adds the rest's part: DESIGN.md §7);
+    overlap "0" runs the unsplit form (SFHE_SHARD_OVERLAP=0) at W = 4."""
     import socket
     depth, rots = sfhe.direct_sort_params(N, "oracle")
     kw = dict(mult_depth=depth, ring_dim=1 << logn, batch_size=N, rotations=rots, seed=777)
@@ -181,9 +184,11 @@ def test_sharded_sort_gloo_two_processes(oracle_lib, tmp_path, N, logn):
         port = s.getsockname()[1]
     path = str(tmp_path / "rank")
     code = GLOO_SORT_SCRIPT.format(py=os.path.join(ROOT, "sorting-fhe_amd", "python"), root=ROOT,
-                                   tests=os.path.join(ROOT, "tests"), port=port, path=path, kw=kw, N=N)
-    env = dict(os.environ, OMP_NUM_THREADS="4")
-    procs = [subprocess.Popen([sys.executable, "-c", code, str(r)], env=env) for r in range(2)]
+                                   tests=os.path.join(ROOT, "tests"), port=port, path=path, kw=kw, N=N, W=W)
+    env = dict(os.environ, OMP_NUM_THREADS=str(max(1, 8 // W)))
+    if overlap is not None:
+        env["SFHE_SHARD_OVERLAP"] = overlap
+    procs = [subprocess.Popen([sys.executable, "-c", code, str(r)], env=env) for r in range(W)]
     try:
         for p in procs:
             assert p.wait(timeout=900) == 0
@@ -192,7 +197,7 @@ def test_sharded_sort_gloo_two_processes(oracle_lib, tmp_path, N, logn):
             if p.poll() is None:
                 p.kill()
     ref = sort_program(sfhe.Engine("oracle", **kw), N)
-    for r in range(2):
+    for r in range(W):
         z = np.load(f"{path}{r}.npz")
         compare(ref, {k: z[k] for k in z.files})
 

@@ -12,6 +12,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "openfhe.h"
@@ -54,6 +55,9 @@ static double chain(const Ct& in, int reps, F&& body, size_t* nodes) {
 
 int main(int argc, char** argv) {
     const int reps = argc > 1 ? std::atoi(argv[1]) : 20;
+    // argv[2]: which chains ("all", or a comma list of mult,mult2,lanes,rot,rsc)
+    const std::string only = argc > 2 ? argv[2] : "all";
+    auto want = [&](const char* c) { return only == "all" || ("," + only + ",").find("," + std::string(c) + ",") != std::string::npos; };
     const int R = 8;
     CCParams<CryptoContextCKKSRNS> p;
     p.SetMultiplicativeDepth(34);
@@ -76,15 +80,19 @@ int main(int argc, char** argv) {
     auto report = [&](const char* name, uint32_t ell, int ops, double us, size_t nodes) {
         std::printf("%-6s %5u %4d %8zu %10.1f %10.2f\n", name, ell, ops, nodes, us, us / ops);
     };
-    for (uint32_t ell0 : {13u, 20u, 35u}) {
+    for (uint32_t ell0 : {10u, 13u, 20u, 35u}) {
         Ct x = atEll(x0, ell0);
         size_t nodes = 0;
-        double us = chain(x, reps, [&](const Ct& in) {
-            Ct y = in;
-            for (int k = 0; k < R; ++k) y = cc->EvalMultMany({y}, {y})[0];
-            return y;
-        }, &nodes);
-        report("mult", ell0, R, us, nodes);
+        double us = 0;
+        if (want("mult")) {
+            us = chain(x, reps, [&](const Ct& in) {
+                Ct y = in;
+                for (int k = 0; k < R; ++k) y = cc->EvalMultMany({y}, {y})[0];
+                return y;
+            }, &nodes);
+            report("mult", ell0, R, us, nodes);
+        }
+        if (want("mult2")) {
         us = chain(x, reps, [&](const Ct& in) {
             Ct y = in, z = cc->EvalAdd(in, 0.25);
             cc->Settle(z);
@@ -96,6 +104,8 @@ int main(int argc, char** argv) {
             return cc->EvalAdd(y, z);
         }, &nodes);
         report("mult2", ell0, R, us, nodes);
+        }
+        if (want("lanes")) {
         us = chain(x, reps, [&](const Ct& in) {
             Ct z = cc->EvalAdd(in, 0.25);
             cc->Settle(z);
@@ -110,11 +120,14 @@ int main(int argc, char** argv) {
             return cc->EvalAdd(a, b);
         }, &nodes);
         report("lanes", ell0, R, us, nodes);
+        }
     }
     for (uint32_t ell : {4u, 9u, 13u, 20u, 35u}) {
         Ct x = atEll(x0, ell);
         size_t nodes = 0;
-        double us = chain(x, reps, [&](const Ct& in) {
+        double us = 0;
+        if (want("rot")) {
+        us = chain(x, reps, [&](const Ct& in) {
             Ct y = in;
             for (int k = 0; k < R; ++k) {
                 y = cc->EvalRotate(y, 1);
@@ -123,6 +136,8 @@ int main(int argc, char** argv) {
             return y;
         }, &nodes);
         report("rot", ell, R, us, nodes);
+        }
+        if (!want("rsc") || ell + R > cc->state()->Lq) continue;
         Ct xs = atEll(x0, ell + R);
         us = chain(xs, reps, [&](const Ct& in) {
             Ct y = in;

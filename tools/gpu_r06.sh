@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-6 GPU call (developer script), from the repo root on the box:
-#   TAG=r06b TESTS="tests/test_x.py" CHAIN=1 BENCH=1 AB="SFHE_ICOL=0" bash tools/gpu_r06.sh
+#   TAG=r06b TESTS="tests/test_x.py" CHAIN=1 BENCH=1 AB="SFHE_ICOL=0" CHAINPROF=mult bash tools/gpu_r06.sh
 # TESTS: pytest selection run with -m gpu (TESTS=all: the whole suite);
 # CHAIN: tools/build/chainbench (and again under each AB setting);
 # BENCH: the short metric bench (BENCHARGS replaces its arguments), again
@@ -31,5 +31,10 @@ if [ -n "$BENCH" ]; then
             env $ab timeout -k 10 400 python -u bench.py $B > $O/bench${r}_$ab.json 2> $O/bench${r}_$ab.err || exit $?
         done
     done
+fi
+if [ -n "$CHAINPROF" ]; then  # kernel trace of one chain (CHAINPROF = chainbench's chain list)
+    export TMPDIR=/tmp
+    timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/cprof -o run -- \
+        tools/build/chainbench 3 $CHAINPROF > $O/chainprof.log 2>&1 || exit $?
 fi
 exit 0
