@@ -1853,6 +1853,7 @@ CryptoContextImpl<DCRTPoly>::CryptoContextImpl(const CCParams<CryptoContextCKKSR
     if (sbits < 20 || sbits > 60) SFHE_THROW("scaling mod size must be in [20, 60]");
     if (fbits < sbits || fbits > 60) SFHE_THROW("first mod size must be in [scale bits, 60]");
     s.dnum = p.GetNumLargeDigits();
+    if (s.dnum == 0 && std::getenv("SFHE_DNUM")) s.dnum = (uint32_t)std::atoi(std::getenv("SFHE_DNUM"));  // (A/B)
     if (s.dnum == 0) s.dnum = s.Lq > 3 ? 3 : std::max<uint32_t>(1, s.Lq);
     s.dnum = std::min(s.dnum, s.Lq);
     s.alpha = (s.Lq + s.dnum - 1) / s.dnum;
