@@ -534,6 +534,11 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalChebyshevSeriesPS(
             bestL = l;
         }
     }
+    static const uint32_t forceL = [] {  // SFHE_PS_L=l: the baby-step exponent for series of degree >= 64 (A/B)
+        const char* v = std::getenv("SFHE_PS_L");
+        return v ? (uint32_t)std::atoi(v) : 0u;
+    }();
+    if (forceL && d >= 64 && (1ull << D) - (1ull << forceL) >= d && forceL + 1 <= D) bestL = forceL;
     const uint32_t l = std::min(bestL, (uint32_t)(31 - __builtin_clz(std::max<uint32_t>(d, 2))));
     Ciphertext<DCRTPoly> out;
     {

@@ -101,6 +101,21 @@ def main():
             algo = sum(16.0 * ntt_rows(nm, g, a.n) * a.n for nm, g, _ in F[:k])
             entry["algorithmic_bytes_per_launch"] = algo / k
             entry["traffic_over_algorithmic"] = (fetch + write) / algo
+            # the excess located by pass (forward / inverse x COL / ROW)
+            by = collections.defaultdict(lambda: [0, 0.0, 0.0, 0.0])
+            for (nm, g, vf), (_, _, vw) in zip(F[:k], W[:k]):
+                m = re.search(r"k_ntt<\s*(\w+),\s*(\w+)", nm)
+                key = ("inverse" if m and m.group(1) == "true" else "forward") + " " + \
+                      ("COL" if m and m.group(2) == "true" else "ROW")
+                b = by[key]
+                b[0] += 1
+                b[1] += vf * 1024 * 2
+                b[2] += vw * 1024
+                b[3] += 16.0 * ntt_rows(nm, g, a.n) * a.n
+            entry["by_pass"] = {key: {"launches": b[0], "fetch_over_read": b[1] / (b[3] / 2),
+                                      "write_over_written": b[2] / (b[3] / 2),
+                                      "traffic_over_algorithmic": (b[1] + b[2]) / b[3]}
+                                for key, b in sorted(by.items())}
         if fam == "conv" and conv_algo and k == conv_algo[0]:
             entry["algorithmic_bytes_per_launch"] = conv_algo[1] / k
             entry["traffic_over_algorithmic"] = (fetch + write) / conv_algo[1]
