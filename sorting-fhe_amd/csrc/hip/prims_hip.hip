@@ -2986,6 +2986,108 @@ __global__ __launch_bounds__(kThreads) void k_conv_mdrs(const MdrsArgs A, const 
     }
 }
 
+// Integer form, block-cooperative as k_mdrsf (round 6: k_conv_mdrs, one
+// thread per coefficient pair with every source in registers, took 424 VGPRs
+// and 18.7 % of the k-way sort at one wave per SIMD, profiles/r06/): for
+// tables whose sources the FP64 forms cannot take (the scale-59 chains' 60-bit
+// P primes).  A block owns kConvCoefs coefficients of one polynomial and one
+// chunk of kConvChunk targets.  Phase 1: the canonical y_i of every (source,
+// coefficient) pair into LDS.  Then one thread per coefficient: the overflow
+// v (convOverflow's operations in its order), the count of centred y_i, and
+// the dropped row's r = (a_l - conv_l) P^-1 mod q_l.  Phase 2: one lane per
+// coefficient and target, the 128-bit sum over the sources from LDS.  The
+// same integers as k_conv_mdrs, so the same outputs.
+template <int NS>
+__global__ __launch_bounds__(kThreads) void k_mdrsi(const MdrsArgs A, const sf_barrett* __restrict__ bar,
+                                                    const double* __restrict__ qinvD, uint32_t logn) {
+    constexpr int C = kConvChunk, X = kConvCoefs, WAVES = kThreads / 64;
+    __shared__ u64 smod[NS * C];  // mod[i][t] of this chunk's targets
+    __shared__ u64 sLm[NS];       // mod[i][l]
+    __shared__ sf_barrett sB[NS], tB[C];
+    __shared__ u64 sInv[NS], tSp[C], tPm[C], tLs[C];
+    __shared__ double sQi[NS];
+    __shared__ u64 yL[NS * X];     // canonical y_i
+    __shared__ u64 rL[X];          // the dropped row's r, canonical mod q_l
+    __shared__ long long nL[X];    // v + #{y_i > s_i / 2}: the multiple of prod(S) the centred sum drops
+    const MdrsJob& J = A.j[blockIdx.y];
+    const uint32_t k0 = blockIdx.z * C;
+    if (k0 >= A.l) return;
+    const uint32_t tc = min((uint32_t)C, A.l - k0);
+    const uint32_t ns = A.ns, x0 = blockIdx.x * X, nsX = ns * X;
+    // the block's source words and its dropped-row words first (one round trip)
+    u64 sv[kConvPer<NS>];
+#pragma unroll
+    for (int k = 0; k < kConvPer<NS>; ++k) {
+        const uint32_t e = min(threadIdx.x + k * kThreads, nsX - 1);  // (unconditional: no branch between loads)
+        sv[k] = J.src[((size_t)(e / X) << logn) + x0 + e % X];
+    }
+    const u64 alv = J.al[((size_t)A.l << logn) + x0 + threadIdx.x % X];
+    const sf_barrett BL = loadBar(bar, A.l);
+    const u64 sprl = A.sprod[A.l];
+    if (threadIdx.x < ns) {
+        const uint32_t i = threadIdx.x, pi = A.sidx[i];
+        sB[i] = loadBar(bar, pi);
+        sInv[i] = A.inv[i];
+        sQi[i] = qinvD[pi];
+        sLm[i] = A.mod[(size_t)i * A.nt + A.l];
+    } else if (threadIdx.x >= 64 && threadIdx.x < 64 + tc) {
+        const uint32_t k = threadIdx.x - 64, t = k0 + k;
+        tB[k] = loadBar(bar, t);
+        tSp[k] = A.sprod[t];
+        tPm[k] = A.pmod[t];
+        tLs[k] = A.lsub[t];
+    }
+    for (uint32_t e = threadIdx.x; e < ns * tc; e += kThreads) {
+        const uint32_t i = e / tc, k = e % tc;
+        smod[i * C + k] = A.mod[(size_t)i * A.nt + k0 + k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kConvPer<NS>; ++k) {
+        const uint32_t e = threadIdx.x + k * kThreads;
+        if (e < nsX) {
+            const uint32_t i = e / X;
+            yL[e] = bmul(sv[k], sInv[i], sB[i]);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < X) {
+        const uint32_t cx = threadIdx.x;
+        double aa = 0.0;
+        long long cnt = 0;
+        Acc sl{0, 0};
+#pragma unroll
+        for (int i = 0; i < NS; ++i)
+            if ((uint32_t)i < ns) {
+                const u64 y = yL[i * X + cx];
+                aa = fma(centredY(y, sB[i].q), sQi[i], aa);
+                cnt += y > (sB[i].q >> 1);
+                macc(sl, y, sLm[i]);
+            }
+        const long long na = (long long)rint(aa) + cnt;
+        nL[cx] = na;
+        const u64 cl = subMultiple(sf_reduce128_acc(sl.lo, sl.hi, &BL), na, sprl, BL);
+        rL[cx] = bmul(sf_sub(alv, cl, BL.q), A.pinvl, BL);
+    }
+    __syncthreads();
+    const uint32_t lane = threadIdx.x % 64, w = threadIdx.x / 64;
+    const u64 lhalf = BL.q >> 1;
+    for (uint32_t kc = w * 64; kc < tc * X; kc += WAVES * 64) {
+        const uint32_t k = kc / X, cx = kc % X + lane;
+        const sf_barrett B = tB[k];
+        Acc s0{0, 0};
+#pragma unroll
+        for (int i = 0; i < NS; ++i)
+            if ((uint32_t)i < ns) macc(s0, yL[i * X + cx], smod[i * C + k]);
+        u64 out = subMultiple(sf_reduce128_acc(s0.lo, s0.hi, &B), nL[cx], tSp[k], B);
+        const u64 r = rL[cx];
+        u64 lift = sf_reduce128(r, 0, &B);
+        if (r > lhalf) lift = sf_sub(lift, tLs[k], B.q);
+        out = sf_add(out, bmul(lift, tPm[k], B), B.q);
+        J.dst[((size_t)(k0 + k) << logn) + x0 + cx] = out;
+    }
+}
+
 // FP64 form of k_conv_mdrs, block-cooperative as k_convf: every source (P
 // row) and the dropped row's prime below kFpPrimeBound.  Phase 1: the
 // centred y_i of every (source, coefficient) pair into LDS; then wave 0 forms
@@ -5046,7 +5148,8 @@ static uint32_t kernelFamily(const void* f) {
         for (const void* k : {(const void*)k_convf<13>, (const void*)k_convf<16>, (const void*)k_convf<kMaxConvSrc>,
                               (const void*)k_conv, (const void*)k_mdrsf<13, true>, (const void*)k_mdrsf<16, true>,
                               (const void*)k_mdrsf<kMaxConvSrc, true>, (const void*)k_mdrsf<13>,
-                              (const void*)k_mdrsf<16>, (const void*)k_mdrsf<kMaxConvSrc>, (const void*)k_conv_mdrs})
+                              (const void*)k_mdrsf<16>, (const void*)k_mdrsf<kMaxConvSrc>, (const void*)k_conv_mdrs,
+                              (const void*)k_mdrsi<16>, (const void*)k_mdrsi<kMaxConvSrc>})
             m[k] = SFP_FAM_CONV;
         for (const void* k : {(const void*)k_ks_inner<1>, (const void*)k_ks_inner<2>, (const void*)k_ks_inner<4>})
             m[k] = SFP_FAM_KSINNER;
@@ -5107,7 +5210,8 @@ static double convNodeBytes(const hipKernelNodeParams& kp, uint32_t n) {
     const bool mdrs = f == (const void*)k_mdrsf<13> || f == (const void*)k_mdrsf<16> ||
                       f == (const void*)k_mdrsf<kMaxConvSrc> || f == (const void*)k_mdrsf<13, true> ||
                       f == (const void*)k_mdrsf<16, true> || f == (const void*)k_mdrsf<kMaxConvSrc, true> ||
-                      f == (const void*)k_conv_mdrs;
+                      f == (const void*)k_conv_mdrs || f == (const void*)k_mdrsi<16> ||
+                      f == (const void*)k_mdrsi<kMaxConvSrc>;
     if (mdrs) {
         const MdrsArgs& A = *static_cast<const MdrsArgs*>(kp.kernelParams[0]);
         return 8.0 * n * kp.gridDim.y * (A.ns + 1.0 + A.l);
@@ -6212,6 +6316,16 @@ void sfp_moddown2(sfp_dev* d, uint64_t* out0, uint64_t* out1, uint64_t* acc, siz
     nttRows(d, B, 0);
 }
 
+// The integer ModDown + rescale (tables with 60-bit sources) on the block-
+// cooperative k_mdrsi; SFHE_MDRSI=0: the one-thread-per-pair k_conv_mdrs (A/B)
+static bool mdrsiOn() {
+    static const bool on = [] {
+        const char* v = std::getenv("SFHE_MDRSI");
+        return !v || *v != '0';
+    }();
+    return on;
+}
+
 // sfp_moddown_rescale; T[4] (a0, a1, b0, b1) non-null: d0 / d1 are the
 // tensor of (a0, a1) and (b0, b1), formed in the final pass's epilogue
 static void moddownRescaleCore(sfp_dev* d, uint64_t* out0, uint64_t* out1, const uint64_t* d0, const uint64_t* d1,
@@ -6295,7 +6409,7 @@ static void moddownRescaleCore(sfp_dev* d, uint64_t* out0, uint64_t* out1, const
             M.nInt = (uint32_t)(std::lower_bound(c->hIntT.begin(), c->hIntT.end(), l) - c->hIntT.begin());
             zc = (M.nInt + kConvChunk - 1) / kConvChunk;
         }
-        const dim3 g((fp || bigl) ? n / kConvCoefs : n / (2 * kThreads), 2, zc);
+        const dim3 g((fp || bigl || mdrsiOn()) ? n / kConvCoefs : n / (2 * kThreads), 2, zc);
         timedLaunch(d, SFP_FAM_CONV, 8.0 * n * 2 * (K + 1 + l), [&] {
             // (fp: LDS for 6 blocks per CU at ns <= 13, as convLaunch)
             MdrsKern k = (bigl && c->ns <= 13) ? k_mdrsf<13, true>
@@ -6304,7 +6418,9 @@ static void moddownRescaleCore(sfp_dev* d, uint64_t* out0, uint64_t* out1, const
                          : (fp && c->ns <= 13)   ? k_mdrsf<13>
                          : (fp && c->ns <= 16)   ? k_mdrsf<16>
                          : fp                    ? k_mdrsf<kMaxConvSrc>
-                                                 : k_conv_mdrs;
+                         : !mdrsiOn()            ? k_conv_mdrs
+                         : c->ns <= 16           ? k_mdrsi<16>
+                                                 : k_mdrsi<kMaxConvSrc>;
             StackRec r;
             r.go = [=](hipStream_t s_) { hipLaunchKernelGGL(k, g, dim3(kThreads), 0, s_, M, d->bar, d->qinvD, d->logn); };
             if (d->stackOn) {
