@@ -872,15 +872,16 @@ __device__ __forceinline__ u64* rowAt(const RowPtr& r, uint32_t p, uint32_t i) {
 }
 
 // Developer build knob: SFHE_NTT_TRACE accumulates per-phase shader clocks
-// of every block (thread 0, after each barrier) for tools/microbench.
+// of every block (thread 0, after each barrier) for tools/microbench.  The
+// deltas stay in registers until the block's end (an atomic per mark would be
+// waited for by the next barrier and inflate the phase it ends).
 #ifdef SFHE_NTT_TRACE
 constexpr int kTraceSlots = 256;  // spread the atomics: no contention artefacts
 __device__ unsigned long long g_nttTrace[kTraceSlots][4][8];
 #define NTT_MARK(i)                                                          \
-    if (threadIdx.x == 0) {                                                  \
+    {                                                                        \
         const unsigned long long t_ = clock64();                             \
-        atomicAdd(&g_nttTrace[(blockIdx.x + blockIdx.y * gridDim.x) % kTraceSlots][INV * 2 + COL][(i)], \
-                  t_ - tprev);                                               \
+        tacc[(i)] += t_ - tprev;                                             \
         tprev = t_;                                                          \
     }
 #else
@@ -902,7 +903,7 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroupSet<NG> GS, co
     __shared__ u64 tWi[ICOL ? kNttColTw : 1], tXi[ICOL ? kNttColTw : 1];  // ICOL: the source row's inverse ones
     static_assert(!ICOL || (!INV && COL && !CONV), "the inverse COL prologue feeds the forward COL pass");
 #ifdef SFHE_NTT_TRACE
-    unsigned long long tprev = clock64();
+    unsigned long long tprev = clock64(), tacc[6] = {0, 0, 0, 0, 0, 0};
 #endif
     constexpr bool FIRST = (COL != INV);  // forward: COL first; inverse: ROW first
     const uint32_t n = 1u << logn;
@@ -1322,8 +1323,11 @@ __global__ __launch_bounds__(TILE >> LE) void k_ntt(const RowGroupSet<NG> GS, co
     }
     NTT_MARK(5);
 #ifdef SFHE_NTT_TRACE
-    if (threadIdx.x == 0)
-        atomicAdd(&g_nttTrace[(blockIdx.x + blockIdx.y * gridDim.x) % kTraceSlots][INV * 2 + COL][7], 1ull);
+    if (threadIdx.x == 0) {
+        auto& slot = g_nttTrace[(blockIdx.x + blockIdx.y * gridDim.x) % kTraceSlots][INV * 2 + COL];
+        for (int i = 0; i < 6; ++i) atomicAdd(&slot[i], tacc[i]);
+        atomicAdd(&slot[7], 1ull);
+    }
 #endif
 }
 
