@@ -878,6 +878,7 @@ __device__ __forceinline__ u64* rowAt(const RowPtr& r, uint32_t p, uint32_t i) {
 #ifdef SFHE_NTT_TRACE
 constexpr int kTraceSlots = 256;  // spread the atomics: no contention artefacts
 __device__ unsigned long long g_nttTrace[kTraceSlots][4][8];
+__device__ unsigned long long g_mdrsTrace[kTraceSlots][8];  // k_mdrsf (FP64 blocks): phases 0..3, [7] blocks
 #define NTT_MARK(i)                                                          \
     {                                                                        \
         const unsigned long long t_ = clock64();                             \
@@ -3147,6 +3148,24 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
     // their HBM latency overlaps the constant staging below (one round trip
     // for the whole phase 1 instead of one per loop iteration)
     const uint32_t x0 = blockIdx.x * X, nsX = ns * X;
+#ifdef SFHE_NTT_TRACE
+    unsigned long long tprev = clock64(), tacc[4] = {0, 0, 0, 0};
+#define MDRS_MARK(i)                                 \
+    {                                                \
+        const unsigned long long t_ = clock64();     \
+        tacc[(i)] += t_ - tprev;                     \
+        tprev = t_;                                  \
+    }
+#define MDRS_FLUSH()                                                                       \
+    if (threadIdx.x == 0) {                                                                \
+        auto& slot = g_mdrsTrace[(blockIdx.x + blockIdx.y * gridDim.x) % kTraceSlots];     \
+        for (int i_ = 0; i_ < 4; ++i_) atomicAdd(&slot[i_], tacc[i_]);                     \
+        atomicAdd(&slot[7], 1ull);                                                         \
+    }
+#else
+#define MDRS_MARK(i)
+#define MDRS_FLUSH()
+#endif
     u64 sv[kConvPer<NS>];
 #pragma unroll
     for (int k = 0; k < kConvPer<NS>; ++k) {
@@ -3206,6 +3225,7 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
         }
     }
     __syncthreads();
+    MDRS_MARK(0);
     const uint32_t lane = threadIdx.x % 64, w = threadIdx.x / 64;
 #pragma unroll
     for (int k = 0; k < kConvPer<NS>; ++k) {
@@ -3216,6 +3236,7 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
         }
     }
     __syncthreads();
+    MDRS_MARK(1);
     const double qld = (double)qlq;
     if (threadIdx.x < X) {  // the dropped row: r = (a_l - conv_l) * P^-1 mod q_l, centred
         const uint32_t cx = threadIdx.x;
@@ -3252,6 +3273,7 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
         }
     }
     __syncthreads();
+    MDRS_MARK(2);
     // integer targets, one at a time: this block's own (an integer chunk), or
     // the folded ones after the FP64 targets
     auto intTargets = [&](uint32_t cntT, const sf_barrett* TB, const u64* SM, uint32_t smStride, const u64* TSP,
@@ -3316,10 +3338,14 @@ __global__ __launch_bounds__(kThreads) void k_mdrsf(const MdrsArgs A, const sf_b
                     J.dst[((size_t)tRow[k + u] << logn) + x0 + cx] = (u64)fpReduce(a[u], pd[u], tQi[k + u]);
         }
         if (ti) intTargets(ti, iB, iMod, kMdrsIntFold, iSp, iPm, iLs, iRow);
+        MDRS_MARK(3);
+        MDRS_FLUSH();
         return;
     }
     intTargets(tc, tB, smod, C, tSp, tPm, tLs, tRow);
 }
+#undef MDRS_MARK
+#undef MDRS_FLUSH
 
 // ModDown's conversion -- and the rescale fused with it -- in the forward
 // COL pass of its output rows (sfp_moddown2 / sfp_moddown_rescale, ring
@@ -4973,6 +4999,29 @@ void sfp_ntt_batch(sfp_dev* d, uint64_t* p, size_t stride, uint32_t count, sfp_l
     RowGroup G = rowsOf(count, m.count, m);
     G.src = G.dst = RowPtr{p, (long long)stride, (long long)d->n};
     nttRows(d, G, inverse);
+}
+
+// Developer hook (SFHE_NTT_TRACE builds): k_mdrsf's FP64 blocks' phase clocks
+// since the last call -- [0] loads + constants, [1] phase 1 (y), [2] the
+// overflow and the dropped row, [3] phase 2 and the stores, [7] blocks; -1
+// otherwise.
+extern "C" int sfp_mdrs_trace(sfp_dev* d, unsigned long long* out8) {
+#ifdef SFHE_NTT_TRACE
+    syncAll(d);
+    static unsigned long long all[kTraceSlots * 8];
+    SFP_CHECK(hipMemcpyFromSymbol(all, HIP_SYMBOL(g_mdrsTrace), sizeof all));
+    for (int i = 0; i < 8; ++i) {
+        out8[i] = 0;
+        for (int k = 0; k < kTraceSlots; ++k) out8[i] += all[k * 8 + i];
+    }
+    static const unsigned long long zero[kTraceSlots * 8] = {};
+    SFP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_mdrsTrace), zero, sizeof zero));
+    return 0;
+#else
+    (void)d;
+    (void)out8;
+    return -1;
+#endif
 }
 
 // Developer hook (SFHE_NTT_TRACE builds): per-kernel phase clocks since the

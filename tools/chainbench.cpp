@@ -20,9 +20,19 @@
 #include "state.h"
 
 using namespace lbcrypto;
+
 using Ct = Ciphertext<DCRTPoly>;
 
 static CryptoContext<DCRTPoly> cc;
+
+// (SFHE_NTT_TRACE builds of the library: k_mdrsf's per-phase clocks)
+extern "C" int sfp_mdrs_trace(sfp_dev* d, unsigned long long* out8);
+static void mdrsTrace(bool print) {
+    unsigned long long t[8];
+    if (sfp_mdrs_trace(cc->state()->dev, t) != 0 || !print || !t[7]) return;
+    std::printf("       k_mdrsf blocks=%llu clk/block: load+constants %6.0f  y %6.0f  overflow+r %6.0f  phase2+store %6.0f\n",
+                t[7], (double)t[0] / t[7], (double)t[1] / t[7], (double)t[2] / t[7], (double)t[3] / t[7]);
+}
 
 static Ct atEll(const Ct& x, uint32_t ell) {
     Ct y = x->Clone();
@@ -85,12 +95,14 @@ int main(int argc, char** argv) {
         size_t nodes = 0;
         double us = 0;
         if (want("mult")) {
+            mdrsTrace(false);
             us = chain(x, reps, [&](const Ct& in) {
                 Ct y = in;
                 for (int k = 0; k < R; ++k) y = cc->EvalMultMany({y}, {y})[0];
                 return y;
             }, &nodes);
             report("mult", ell0, R, us, nodes);
+            mdrsTrace(true);
         }
         if (want("mult2")) {
         us = chain(x, reps, [&](const Ct& in) {
