@@ -20,15 +20,15 @@ fi
 if [ -n "$CHAIN" ]; then
     timeout -k 10 240 tools/build/chainbench ${CHAIN_REPS:-20} > $O/chain.log 2>&1 || exit $?
     for ab in $AB; do
-        env $ab timeout -k 10 240 tools/build/chainbench ${CHAIN_REPS:-20} > $O/chain_$ab.log 2>&1 || exit $?
+        env ${ab//+/ } timeout -k 10 240 tools/build/chainbench ${CHAIN_REPS:-20} > $O/chain_$ab.log 2>&1 || exit $?
     done
 fi
 if [ -n "$BENCH" ]; then
     B=${BENCHARGS:-"--steps 10 --warmup 3 --no-kway --no-cpu-baseline --no-hybrid1 --no-c5 --trials 3"}
     for r in $(seq 1 ${REPS:-1}); do
         timeout -k 10 400 python -u bench.py $B > $O/bench$r.json 2> $O/bench$r.err || exit $?
-        for ab in $AB; do
-            env $ab timeout -k 10 400 python -u bench.py $B > $O/bench${r}_$ab.json 2> $O/bench${r}_$ab.err || exit $?
+        for ab in $AB; do  # (one setting per word; '+' joins several)
+            env ${ab//+/ } timeout -k 10 400 python -u bench.py $B > $O/bench${r}_$ab.json 2> $O/bench${r}_$ab.err || exit $?
         done
     done
 fi
