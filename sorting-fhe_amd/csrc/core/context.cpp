@@ -1084,18 +1084,25 @@ class SfheInternal {
         return out;
     }
 
+    // gal != 0 (hoisted rotations, unsharded levels): ext is the unpermuted
+    // ModUp and the inner product reads it through X -> X^gal
     static void innerAndModDown(CC* cc, const uint64_t* ext, size_t stride, uint32_t beta,
                                 uint32_t ell, const DeviceBufferPtr& key, uint64_t* out0,
-                                uint64_t* out1, int add0, int add1) {
+                                uint64_t* out1, int add0, int add1, uint32_t gal = 0) {
         SfheContextState* s = cc->st.get();
-        if (s->shardAt(ell)) return innerModDownShard(s, ext, stride, beta, ell, key, out0, out1, add0, add1);
+        if (s->shardAt(ell)) {
+            if (gal) SFHE_THROW("internal: a permuted inner product at a sharded level");
+            return innerModDownShard(s, ext, stride, beta, ell, key, out0, out1, add0, add1);
+        }
         const int tier = key->ksTier;
         const uint32_t n = s->n, K = s->Kof(tier);
         const size_t accStride = (size_t)(ell + K) * n;
         if (stride != accStride) SFHE_THROW("internal: extended digits of another special-prime tier");
         auto acc = s->alloc(2 * accStride);
-        sfp_ks_inner(s->dev, acc->ptr, acc->ptr + accStride, ext, stride, key->ptr, beta, ell, K,
-                     s->Lq);
+        if (gal)
+            sfp_ks_inner_aut(s->dev, acc->ptr, acc->ptr + accStride, ext, stride, key->ptr, beta, ell, K, s->Lq, gal);
+        else
+            sfp_ks_inner(s->dev, acc->ptr, acc->ptr + accStride, ext, stride, key->ptr, beta, ell, K, s->Lq);
         auto scratch = s->alloc((size_t)2 * ell * n);
         sfp_moddown2(s->dev, out0, out1, acc->ptr, accStride, ell, K, s->Lq, s->moddownConvOf(tier),
                      s->pInvModQof(tier), add0, add1, scratch->ptr, 0);
@@ -2986,15 +2993,28 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalFastRotation(
         key = &s->rotKeys.at(gal);
     const uint64_t* c0in = pinned ? pre->pinC0 : a->c0;
     // sigma commutes with the (coefficient-wise) base extension, so rotating
-    // the extended digits equals extending the rotated c1.
-    auto ext = s->alloc(pre->stride * pre->beta);
-    // one permutation launch over every digit's rows (the map is prime-independent)
-    const uint32_t rows = pre->beta * (uint32_t)(pre->stride / s->n);
-    sfp_automorph(s->dev, ext->ptr, pre->ext->ptr, gal, sfp_limbs{rows, rows, 0, 0});
+    // the extended digits equals extending the rotated c1.  Unsharded, the
+    // inner product reads the shared digits through sigma (sfp_ks_inner_aut:
+    // the permuted copy is never written); SFHE_KS_AUT=0 permutes them first.
+    static const bool autFused = [] {
+        const char* v = std::getenv("SFHE_KS_AUT");
+        return !v || *v != '0';
+    }();
+    const bool fuse = autFused && !s->shardAt(ell);
+    DeviceBufferPtr ext;
+    if (!fuse) {
+        ext = s->alloc(pre->stride * pre->beta);
+        // one permutation launch over every digit's rows (the map is prime-independent)
+        const uint32_t rows = pre->beta * (uint32_t)(pre->stride / s->n);
+        sfp_automorph(s->dev, ext->ptr, pre->ext->ptr, gal, sfp_limbs{rows, rows, 0, 0});
+    } else {
+        s->dep(pre->ext.get());
+    }
     auto out = pre->pend ? SfheInternal::newPendingCt(this, a->level, a->slots)
                          : SfheInternal::newCt(this, a->level, a->slots);
     sfp_automorph(s->dev, out->c0, c0in, gal, st->qmap(ell));
-    SfheInternal::innerAndModDown(this, ext->ptr, pre->stride, pre->beta, ell, *key, out->c0, out->c1, 1, 0);
+    SfheInternal::innerAndModDown(this, fuse ? pre->ext->ptr : ext->ptr, pre->stride, pre->beta, ell, *key, out->c0,
+                                  out->c1, 1, 0, fuse ? gal : 0u);
     s->stats.keyswitch++;
     s->stats.automorph++;
     s->countBytes((3.0 * ell + 2.0 * pre->beta * (pre->stride / s->n)) * s->n * 8);

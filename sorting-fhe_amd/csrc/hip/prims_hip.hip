@@ -3645,6 +3645,7 @@ struct KsInnerArgs {
     int accum;
     const u64* pmul;
     sfp_key_geom kg;
+    uint32_t gal;  // != 0: ext read through the automorphism X -> X^gal (sfp_ks_inner_aut)
 };
 template <int NG = 1>
 __global__ __launch_bounds__(kThreads) void k_ks_inner(const ArgSet<KsInnerArgs, NG> S,
@@ -3676,8 +3677,22 @@ __global__ __launch_bounds__(kThreads) void k_ks_inner(const ArgSet<KsInnerArgs,
         const uint32_t kr = keyQ == SFP_KEY_ROW_BY_PRIME ? keyRowOf(kg, pr) : (t < ell ? t : keyQ + (t - ell));
         const sf_barrett B = loadBar(bar, pr);
         Acc s0{0, 0}, s0b{0, 0}, s1{0, 0}, s1b{0, 0};
+        // (gal: the two coefficients' sources, as k_automorph maps them)
+        size_t src0 = e, src1 = e + 1;
+        if (A.gal) {
+            const u64 mask = 2ull * n - 1;
+            const size_t row = e - x;
+            src0 = row + sf_brev((uint32_t)((((2ull * sf_brev(x, logn) + 1) * A.gal & mask) - 1) >> 1), logn);
+            src1 = row + sf_brev((uint32_t)((((2ull * sf_brev(x + 1, logn) + 1) * A.gal & mask) - 1) >> 1), logn);
+        }
         for (uint32_t j = 0; j < beta; ++j) {
-            const ulonglong2 ev = *reinterpret_cast<const ulonglong2*>(ext + j * extStride + e);
+            ulonglong2 ev;
+            if (A.gal) {
+                ev.x = ext[j * extStride + src0];
+                ev.y = ext[j * extStride + src1];
+            } else {
+                ev = *reinterpret_cast<const ulonglong2*>(ext + j * extStride + e);
+            }
             const u64* kb = key + (size_t)j * 2 * NP * n + ((size_t)kr << logn) + x;
             const ulonglong2 b2 = *reinterpret_cast<const ulonglong2*>(kb);
             const ulonglong2 a2 = *reinterpret_cast<const ulonglong2*>(kb + (size_t)NP * n);
@@ -6224,9 +6239,20 @@ void sfp_ks_inner_fold(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_
     // reads beta ext rows + 2*beta key rows, writes 2 accumulator rows, per limb
     timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + 2.0), [&] {
         issueY<KsInnerArgs>(d, k_ks_inner<1>, k_ks_inner<2>, k_ks_inner<4>, dim3(ewGrid(total / 2)),
-                                KsInnerArgs{acc0, acc1, ext, extStride, key, beta, sfp_limbs{ell + K, ell, Lq, 0, 1}, keyQ0, keyRows0, fold0, fold1, foldK, 0, (const u64*)nullptr, d->kg});
+                                KsInnerArgs{acc0, acc1, ext, extStride, key, beta, sfp_limbs{ell + K, ell, Lq, 0, 1}, keyQ0, keyRows0, fold0, fold1, foldK, 0, (const u64*)nullptr, d->kg, 0u});
     });
     checkLaunch(d, "ks_inner");
+}
+
+void sfp_ks_inner_aut(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext, size_t extStride,
+                      const uint64_t* key, uint32_t beta, uint32_t ell, uint32_t K, uint32_t Lq, uint32_t gal) {
+    const uint32_t keyQ0 = d->kg.rows ? d->kg.pstart : Lq, keyRows0 = d->kg.rows ? d->kg.rows : Lq + K;
+    const size_t total = (size_t)(ell + K) * d->n;
+    timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + 2.0), [&] {
+        issueY<KsInnerArgs>(d, k_ks_inner<1>, k_ks_inner<2>, k_ks_inner<4>, dim3(ewGrid(total / 2)),
+                                KsInnerArgs{acc0, acc1, ext, extStride, key, beta, sfp_limbs{ell + K, ell, Lq, 0, 1}, keyQ0, keyRows0, (const u64*)nullptr, (const u64*)nullptr, (u64)0, 0, (const u64*)nullptr, d->kg, gal});
+    });
+    checkLaunch(d, "ks_inner_aut");
 }
 
 void sfp_ks_inner_acc(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext, size_t extStride,
@@ -6236,7 +6262,7 @@ void sfp_ks_inner_acc(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t
     // reads beta ext rows + 2*beta key rows + 2 accumulator rows, writes 2, per limb
     timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + 4.0), [&] {
         issueY<KsInnerArgs>(d, k_ks_inner<1>, k_ks_inner<2>, k_ks_inner<4>, dim3(ewGrid(total / 2)),
-                                KsInnerArgs{acc0, acc1, ext, extStride, key, beta, sfp_limbs{ell + K, ell, Lq, 0, 1}, keyQ0, keyRows0, (const u64*)nullptr, (const u64*)nullptr, (u64)0, 1, (const u64*)nullptr, d->kg});
+                                KsInnerArgs{acc0, acc1, ext, extStride, key, beta, sfp_limbs{ell + K, ell, Lq, 0, 1}, keyQ0, keyRows0, (const u64*)nullptr, (const u64*)nullptr, (u64)0, 1, (const u64*)nullptr, d->kg, 0u});
     });
     checkLaunch(d, "ks_inner_acc");
 }
@@ -6249,7 +6275,7 @@ void sfp_ks_inner_mul(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t
     // reads beta ext rows + 2*beta key rows + the plaintext row (+ 2 accumulator rows), writes 2, per limb
     timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + (accum ? 5.0 : 3.0)), [&] {
         issueY<KsInnerArgs>(d, k_ks_inner<1>, k_ks_inner<2>, k_ks_inner<4>, dim3(ewGrid(total / 2)),
-                                KsInnerArgs{acc0, acc1, ext, extStride, key, beta, sfp_limbs{ell + K, ell, Lq, 0, 1}, keyQ0, keyRows0, (const u64*)nullptr, (const u64*)nullptr, (u64)0, accum, pm, d->kg});
+                                KsInnerArgs{acc0, acc1, ext, extStride, key, beta, sfp_limbs{ell + K, ell, Lq, 0, 1}, keyQ0, keyRows0, (const u64*)nullptr, (const u64*)nullptr, (u64)0, accum, pm, d->kg, 0u});
     });
     checkLaunch(d, "ks_inner_mul");
 }
@@ -6785,7 +6811,7 @@ void sfp_ks_inner_map(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t
     const size_t total = (size_t)pm.count * d->n;
     timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + (accum ? 4.0 : 2.0)), [&] {
         issueY<KsInnerArgs>(d, k_ks_inner<1>, k_ks_inner<2>, k_ks_inner<4>, dim3(ewGrid(total / 2)),
-                                KsInnerArgs{acc0, acc1, ext, extStride, key, beta, pm, keyQ, keyRows, (const u64*)nullptr, (const u64*)nullptr, (u64)0, accum, (const u64*)nullptr, d->kg});
+                                KsInnerArgs{acc0, acc1, ext, extStride, key, beta, pm, keyQ, keyRows, (const u64*)nullptr, (const u64*)nullptr, (u64)0, accum, (const u64*)nullptr, d->kg, 0u});
     });
     checkLaunch(d, "ks_inner_map");
 }

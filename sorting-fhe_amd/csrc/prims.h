@@ -226,6 +226,13 @@ void sfp_modup_prepare(sfp_dev* d, const sfp_conv* const* convs, uint32_t ell, u
 void sfp_ks_inner(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
                   size_t ext_stride, const uint64_t* key, uint32_t beta, uint32_t ell, uint32_t K,
                   uint32_t Lq);
+// sfp_ks_inner of the extended digits under the automorphism X -> X^gal: ext
+// is read at the source index sfp_automorph maps each coefficient from, as if
+// the digits had been permuted first (a hoisted rotation: the permuted copy
+// of its digits is never written).
+void sfp_ks_inner_aut(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
+                      size_t ext_stride, const uint64_t* key, uint32_t beta, uint32_t ell, uint32_t K,
+                      uint32_t Lq, uint32_t gal);
 // Key inner product times a plaintext in the extended basis, accumulated
 // (double hoisting: a hoisted rotation's product with a diagonal before its
 // ModDown, EvalRotMultAddHoisted):

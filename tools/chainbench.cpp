@@ -18,6 +18,7 @@
 #include "openfhe.h"
 #include "prims.h"
 #include "state.h"
+#include "rotation.h"
 
 using namespace lbcrypto;
 
@@ -81,7 +82,9 @@ int main(int argc, char** argv) {
     cc->Enable(LEVELEDSHE);
     auto kp = cc->KeyGen();
     cc->EvalMultKeyGen(kp.secretKey);
-    cc->EvalRotateKeyGen(kp.secretKey, {1});
+    std::vector<int> baby;
+    for (int k = 1; k < 16; ++k) baby.push_back(k);
+    cc->EvalRotateKeyGen(kp.secretKey, baby);
     std::vector<double> v(256);
     for (int i = 0; i < 256; ++i) v[i] = 0.5 + 0.001 * i;
     Ct x0 = cc->Encrypt(kp.publicKey, cc->MakeCKKSPackedPlaintext(v));
@@ -132,6 +135,25 @@ int main(int argc, char** argv) {
             return cc->EvalAdd(a, b);
         }, &nodes);
         report("lanes", ell0, R, us, nodes);
+        }
+    }
+    // hoist: the rank phase's baby rotations -- 16 rotations of one ciphertext
+    // sharing one ModUp (RotationComposer::rotateMany), summed
+    if (want("hoist")) {
+        RotationComposer<256> rot(cc, nullptr, baby);
+        std::vector<int> amounts;
+        for (int k = 0; k < 16; ++k) amounts.push_back(k);
+        for (uint32_t ell : {35u, 20u, 13u}) {
+            Ct x = atEll(x0, ell);
+            size_t nodes = 0;
+            const double us = chain(x, reps, [&](const Ct& in) {
+                auto r = rot.rotateMany(in, amounts);
+                Ct sum = r[0];
+                for (size_t k = 1; k < r.size(); ++k) sum = cc->EvalAdd(sum, r[k]);
+                cc->Settle(sum);
+                return sum;
+            }, &nodes);
+            report("hoist", ell, 16, us, nodes);
         }
     }
     for (uint32_t ell : {4u, 9u, 13u, 20u, 35u}) {
