@@ -554,6 +554,21 @@ void sfp_ks_inner_acc(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t
     ks_inner_rows(d, acc0, acc1, ext, ext_stride, key, beta, ell, K, Lq, NULL, NULL, 0, 1, NULL);
 }
 
+/* the digits permuted by X -> X^gal (sfp_automorph), then sfp_ks_inner_mul */
+void sfp_ks_inner_mul_aut(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
+                          size_t ext_stride, const uint64_t* key, uint32_t beta, uint32_t ell, uint32_t K,
+                          uint32_t Lq, const uint64_t* pm, int accum, uint32_t gal) {
+    const uint32_t rows = (uint32_t)(ext_stride / d->n);
+    uint64_t* t = (uint64_t*)malloc(ext_stride * beta * 8);
+    sfp_limbs m;
+    memset(&m, 0, sizeof m);
+    m.count = rows;
+    m.split = rows;
+    for (uint32_t j = 0; j < beta; ++j) sfp_automorph(d, t + j * ext_stride, ext + j * ext_stride, gal, m);
+    sfp_ks_inner_mul(d, acc0, acc1, t, ext_stride, key, beta, ell, K, Lq, pm, accum);
+    free(t);
+}
+
 /* the digits permuted by X -> X^gal (sfp_automorph), then sfp_ks_inner */
 void sfp_ks_inner_aut(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
                       size_t ext_stride, const uint64_t* key, uint32_t beta, uint32_t ell, uint32_t K,

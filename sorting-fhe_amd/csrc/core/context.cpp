@@ -3225,11 +3225,22 @@ Ciphertext<DCRTPoly> CryptoContextImpl<DCRTPoly>::EvalRotMultAddHoisted(
             x0.push_back(rc0->ptr);
             m0.push_back(m);
             keep.push_back(rc0);
-            auto rext = s->alloc(stride * beta);
-            const uint32_t rows = beta * (ell + K);
-            sfp_automorph(s->dev, rext->ptr, ext->ptr, gal, sfp_limbs{rows, rows, 0, 0});
-            sfp_ks_inner_mul(s->dev, acc->ptr, acc->ptr + stride, rext->ptr, stride, it->second->ptr, beta, ell, K,
-                             s->Lq, SfheInternal::encodedExt(this, pt, level), accOn ? 1 : 0);
+            // the shared digits read through sigma by the inner product (as
+            // EvalFastRotation; SFHE_KS_AUT=0: a permuted copy per rotation)
+            static const bool autFused = [] {
+                const char* v = std::getenv("SFHE_KS_AUT");
+                return !v || *v != '0';
+            }();
+            if (autFused) {
+                sfp_ks_inner_mul_aut(s->dev, acc->ptr, acc->ptr + stride, ext->ptr, stride, it->second->ptr, beta, ell,
+                                     K, s->Lq, SfheInternal::encodedExt(this, pt, level), accOn ? 1 : 0, gal);
+            } else {
+                auto rext = s->alloc(stride * beta);
+                const uint32_t rows = beta * (ell + K);
+                sfp_automorph(s->dev, rext->ptr, ext->ptr, gal, sfp_limbs{rows, rows, 0, 0});
+                sfp_ks_inner_mul(s->dev, acc->ptr, acc->ptr + stride, rext->ptr, stride, it->second->ptr, beta, ell,
+                                 K, s->Lq, SfheInternal::encodedExt(this, pt, level), accOn ? 1 : 0);
+            }
             accOn = true;
             s->stats.keyswitch++;
             s->stats.automorph++;

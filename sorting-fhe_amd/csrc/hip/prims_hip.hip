@@ -6270,12 +6270,18 @@ void sfp_ks_inner_acc(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t
 void sfp_ks_inner_mul(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext, size_t extStride,
                       const uint64_t* key, uint32_t beta, uint32_t ell, uint32_t K, uint32_t Lq, const uint64_t* pm,
                       int accum) {
+    sfp_ks_inner_mul_aut(d, acc0, acc1, ext, extStride, key, beta, ell, K, Lq, pm, accum, 0);
+}
+
+void sfp_ks_inner_mul_aut(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext, size_t extStride,
+                          const uint64_t* key, uint32_t beta, uint32_t ell, uint32_t K, uint32_t Lq,
+                          const uint64_t* pm, int accum, uint32_t gal) {
     const uint32_t keyQ0 = d->kg.rows ? d->kg.pstart : Lq, keyRows0 = d->kg.rows ? d->kg.rows : Lq + K;
     const size_t total = (size_t)(ell + K) * d->n;
     // reads beta ext rows + 2*beta key rows + the plaintext row (+ 2 accumulator rows), writes 2, per limb
     timedLaunch(d, SFP_FAM_KSINNER, 8.0 * total * (3.0 * beta + (accum ? 5.0 : 3.0)), [&] {
         issueY<KsInnerArgs>(d, k_ks_inner<1>, k_ks_inner<2>, k_ks_inner<4>, dim3(ewGrid(total / 2)),
-                                KsInnerArgs{acc0, acc1, ext, extStride, key, beta, sfp_limbs{ell + K, ell, Lq, 0, 1}, keyQ0, keyRows0, (const u64*)nullptr, (const u64*)nullptr, (u64)0, accum, pm, d->kg, 0u});
+                                KsInnerArgs{acc0, acc1, ext, extStride, key, beta, sfp_limbs{ell + K, ell, Lq, 0, 1}, keyQ0, keyRows0, (const u64*)nullptr, (const u64*)nullptr, (u64)0, accum, pm, d->kg, gal});
     });
     checkLaunch(d, "ks_inner_mul");
 }

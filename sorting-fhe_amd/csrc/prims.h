@@ -241,6 +241,10 @@ void sfp_ks_inner_aut(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t
 void sfp_ks_inner_mul(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
                       size_t ext_stride, const uint64_t* key, uint32_t beta, uint32_t ell, uint32_t K,
                       uint32_t Lq, const uint64_t* pm, int accum);
+// sfp_ks_inner_mul of the digits under X -> X^gal (as sfp_ks_inner_aut)
+void sfp_ks_inner_mul_aut(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
+                          size_t ext_stride, const uint64_t* key, uint32_t beta, uint32_t ell, uint32_t K,
+                          uint32_t Lq, const uint64_t* pm, int accum, uint32_t gal);
 // sfp_ks_inner accumulating: acc0 += sum_j ext_j * kb_j, acc1 += sum_j ext_j * ka_j
 // (the key switches of a rotation sum share one ModDown, EvalRotateSum).
 void sfp_ks_inner_acc(sfp_dev* d, uint64_t* acc0, uint64_t* acc1, const uint64_t* ext,
